@@ -1,0 +1,131 @@
+"""ctypes binding of libautovc_hip.so (the C-ABI declared in include/autovc_hip.h).
+
+The library is loaded lazily, *after* ``import torch``, so the process has exactly one
+HIP runtime (torch's libamdhip64.so.7 satisfies the .so's NEEDED entry).  There is no
+fallback: if the library is missing or fails to load, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+import torch  # noqa: F401  (must precede the HIP library)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libautovc_hip.so")
+CSRC = os.path.join(HERE, "csrc")
+SOURCES = ["gemm.hip", "bn.hip", "lstm.hip", "elem.hip"]
+ABI_VERSION = 1
+
+F32, BF16 = 0, 1
+ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU = 0, 1, 2, 3, 4
+
+c_void_p, c_int, c_ll, c_float, c_size = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_size_t
+
+
+class Operand(ctypes.Structure):
+    _fields_ = [("ptr", c_void_p), ("dtype", c_int), ("kstrided", c_int), ("ld", c_ll), ("batch_stride", c_ll),
+                ("taps", c_int), ("pad", c_int), ("t_out", c_int), ("t_in", c_int), ("chans", c_int)]
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [("M", c_int), ("N", c_int), ("K", c_int), ("batch", c_int), ("a", Operand), ("b", Operand),
+                ("c", c_void_p), ("ldc", c_ll), ("c_batch_stride", c_ll), ("bias", c_void_p),
+                ("accumulate", c_int), ("split_k", c_int), ("bn_partial", c_void_p), ("compute", c_int)]
+
+
+_SIGS = {
+    "avc_abi_version": (c_int, []),
+    "avc_last_error": (ctypes.c_char_p, []),
+    "avc_gemm": (c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
+    "avc_bn_finalize": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
+                                c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "avc_bn_eval": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_void_p,
+                            c_void_p, c_void_p]),
+    "avc_bn_stats": (c_int, [c_void_p, c_ll, c_int, c_int, c_void_p, c_void_p]),
+    "avc_bn_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "avc_bn_bwd_ws": (c_size, [c_int, c_int]),
+    "avc_bn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "avc_colsum_ws": (c_size, [c_int, c_int]),
+    "avc_colsum": (c_int, [c_void_p, c_ll, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "avc_lstm_fwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                             c_void_p, c_int, c_void_p]),
+    "avc_lstm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                             c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "avc_enc_concat": (c_int, [c_void_p, c_ll, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "avc_codes_gather": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "avc_codes_scatter": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "avc_dec_concat": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "avc_dec_concat_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "avc_conv_pack": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "avc_conv_grad_unpack": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "avc_convert": (c_int, [c_void_p, c_void_p, c_int, c_ll, c_void_p]),
+    "avc_transpose": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "avc_add": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_void_p]),
+    "avc_mse_loss": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_void_p]),
+    "avc_l1_loss": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_void_p]),
+    "avc_loss_grad": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_int, c_void_p, c_float, c_void_p]),
+    "avc_adam": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_float, c_float, c_float, c_float, c_void_p,
+                         c_void_p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    """Compile csrc/*.hip for gfx950 into libautovc_hip.so (in-tree)."""
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    if not force and os.path.exists(LIB_PATH):
+        newest = max(os.path.getmtime(p) for p in srcs + [os.path.join(CSRC, "common.h"),
+                                                          os.path.join(HERE, "..", "include", "autovc_hip.h")])
+        if os.path.getmtime(LIB_PATH) >= newest:
+            return LIB_PATH
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    tmp = LIB_PATH + ".tmp"
+    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-pass-failed",
+           "-o", tmp] + srcs
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libautovc_hip.so not found at {LIB_PATH}; run autoformer_amd._lib.build() "
+                               "(or __graft_entry__.build()). There is no CPU fallback.")
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = L.avc_abi_version()
+        if v != ABI_VERSION:
+            raise RuntimeError(f"libautovc_hip ABI {v} != expected {ABI_VERSION}; rebuild")
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().avc_last_error().decode(errors="replace")
+        raise RuntimeError(f"libautovc_hip {what} failed ({rc}): {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)
+
+
+def exported_symbols():
+    return list(_SIGS.keys())

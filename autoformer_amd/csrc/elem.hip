@@ -1,0 +1,314 @@
+// elem.hip — layout glue, weight repacks, losses and the fused Adam step.
+//
+// Glue replaces the tensor reshuffles of factory/AutoVC.py: input concat with the
+// broadcast speaker embedding (:46-48), code extraction (:56-66) and expansion + concat
+// (:197-204).  Losses replace F.mse_loss / F.l1_loss of train.py:85-86,94 and Adam
+// replaces torch.optim.Adam (train.py:49,99).
+#include <cstdarg>
+#include <cstdio>
+
+#include "common.h"
+
+static thread_local char g_err[512] = "";
+
+void avc_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int avc_check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    avc_set_error("%s: %s", what, hipGetErrorString(e));
+    return -2;
+  }
+  return 0;
+}
+
+extern "C" int avc_abi_version(void) { return AVC_ABI_VERSION; }
+extern "C" const char* avc_last_error(void) { return g_err; }
+
+namespace {
+
+__global__ void enc_concat_kernel(const float* mel, long long mel_ld, const float* emb, float* out, int B, int T,
+                                  int nm, int de) {
+  const int C = nm + de;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = (long long)B * T * C;
+  if (i >= total) return;
+  int c = (int)(i % C);
+  long long f = i / C;
+  int b = (int)(f / T);
+  out[i] = c < nm ? mel[f * mel_ld + c] : emb[(long long)b * de + (c - nm)];
+}
+
+__global__ void codes_gather_kernel(const float* lo, float* codes, int B, int T, int D, int freq) {
+  const int nc = T / freq, W = 2 * D;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * nc * W) return;
+  int c = (int)(i % W);
+  int k = (int)((i / W) % nc);
+  int b = (int)(i / ((long long)W * nc));
+  int t = c < D ? k * freq + freq - 1 : k * freq;
+  codes[i] = lo[((long long)b * T + t) * W + c];
+}
+
+__global__ void codes_scatter_kernel(const float* dcodes, float* dlo, int B, int T, int D, int freq) {
+  const int nc = T / freq, W = 2 * D;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * T * W) return;
+  int c = (int)(i % W);
+  int t = (int)((i / W) % T);
+  int b = (int)(i / ((long long)W * T));
+  int k = t / freq, r = t - k * freq;
+  bool hit = c < D ? (r == freq - 1) : (r == 0);
+  dlo[i] = hit ? dcodes[((long long)b * nc + k) * W + c] : 0.f;
+}
+
+__global__ void dec_concat_kernel(const float* codes, const float* emb, float* out, int B, int T, int nc, int cd,
+                                  int de) {
+  const int C = cd + de;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * T * C) return;
+  int c = (int)(i % C);
+  int t = (int)((i / C) % T);
+  int b = (int)(i / ((long long)C * T));
+  const int rep = T / nc;
+  out[i] = c < cd ? codes[((long long)b * nc + t / rep) * cd + c] : emb[(long long)b * de + (c - cd)];
+}
+
+__global__ void dec_concat_bwd_kernel(const float* dout, float* dcodes, int B, int T, int nc, int cd, int de) {
+  const int C = cd + de;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * nc * cd) return;
+  int c = (int)(i % cd);
+  int k = (int)((i / cd) % nc);
+  int b = (int)(i / ((long long)cd * nc));
+  const int rep = T / nc;
+  float s = 0.f;
+  for (int t = k * rep; t < (k + 1) * rep; ++t) s += dout[((long long)b * T + t) * C + c];
+  dcodes[i] = s;
+}
+
+template <typename T>
+__device__ __forceinline__ void put(void* dst, long long i, float v);
+template <>
+__device__ __forceinline__ void put<float>(void* dst, long long i, float v) {
+  reinterpret_cast<float*>(dst)[i] = v;
+}
+template <>
+__device__ __forceinline__ void put<bf16>(void* dst, long long i, float v) {
+  reinterpret_cast<bf16*>(dst)[i] = (bf16)v;
+}
+
+__device__ __forceinline__ void putd(void* dst, long long i, float v, int dtype) {
+  if (dtype == AVC_F32) put<float>(dst, i, v);
+  else put<bf16>(dst, i, v);
+}
+
+__global__ void conv_pack_kernel(const float* w, void* out, int dtype, int Co, int Ci, int K, int mode) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = (long long)Co * Ci * K;
+  if (i >= total) return;
+  // i indexes the SOURCE W[co][ci][k]
+  int k = (int)(i % K);
+  int ci = (int)((i / K) % Ci);
+  int co = (int)(i / ((long long)K * Ci));
+  long long o = mode == 0 ? ((long long)co * K + k) * Ci + ci : ((long long)ci * K + (K - 1 - k)) * Co + co;
+  putd(out, o, w[i], dtype);
+}
+
+__global__ void conv_grad_unpack_kernel(const float* dwf, float* dw, int Co, int Ci, int K, int acc) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = (long long)Co * Ci * K;
+  if (i >= total) return;
+  int k = (int)(i % K);
+  int ci = (int)((i / K) % Ci);
+  int co = (int)(i / ((long long)K * Ci));
+  float v = dwf[((long long)co * K + k) * Ci + ci];
+  dw[i] = acc ? dw[i] + v : v;
+}
+
+__global__ void convert_kernel(const float* src, void* dst, int dtype, long long n) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) putd(dst, i, src[i], dtype);
+}
+
+__global__ void transpose_kernel(const float* src, void* dst, int dtype, int R, int C) {
+  __shared__ float tile[32][33];
+  int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  for (int y = ty; y < 32; y += 8) {
+    int r = r0 + y, c = c0 + tx;
+    tile[y][tx] = (r < R && c < C) ? src[(long long)r * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) {
+    int c = c0 + y, r = r0 + tx;  // dst[c][r]
+    if (c < C && r < R) putd(dst, (long long)c * R + r, tile[tx][y], dtype);
+  }
+}
+
+__global__ void add_kernel(const float* a, const float* b, float* o, long long n) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) o[i] = a[i] + b[i];
+}
+
+__global__ void loss_kernel(const float* a, const float* b, long long n, float* out, int mode) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float d = a[i] - b[i];
+    s += mode == 0 ? d * d : fabsf(d);
+  }
+  s = warp_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, (red[0] + red[1] + red[2] + red[3]) / (float)n);
+}
+
+__global__ void loss_grad_kernel(const float* a, const float* b, long long n, const float* dloss, int mode, float* g,
+                                 float sign) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float d = a[i] - b[i];
+  float f = mode == 0 ? 2.f * d : (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f));
+  g[i] = sign * dloss[0] * f / (float)n;
+}
+
+__global__ void adam_prep_kernel(float* state, float lr, float beta1, float beta2) {
+  float step = state[0] + 1.f;
+  state[0] = step;
+  double bc1 = 1.0 - pow((double)beta1, (double)step);
+  double bc2 = 1.0 - pow((double)beta2, (double)step);
+  state[1] = (float)(lr / bc1);
+  state[2] = (float)sqrt(bc2);
+}
+
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, long long n, float beta1, float beta2, float eps,
+                            const float* __restrict__ state) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const float step_size = state[1], bc2s = state[2];
+  for (; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float gi = g[i];
+    float mi = m[i];
+    mi = mi + (1.f - beta1) * (gi - mi);
+    float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    p[i] = p[i] - step_size * (mi / denom);
+  }
+}
+
+}  // namespace
+
+#define GRID1(n) dim3(cdiv((n), 256)), dim3(256), 0, as_stream(stream)
+
+extern "C" int avc_enc_concat(const float* mel, long long mel_ld, const float* emb, float* out, int B, int T, int nm,
+                              int de, void* stream) {
+  AVC_CHECK_ARG(mel && emb && out, "avc_enc_concat: null");
+  long long n = (long long)B * T * (nm + de);
+  enc_concat_kernel<<<GRID1(n)>>>(mel, mel_ld, emb, out, B, T, nm, de);
+  return avc_check_launch("avc_enc_concat");
+}
+
+extern "C" int avc_codes_gather(const float* lo, float* codes, int B, int T, int D, int freq, void* stream) {
+  AVC_CHECK_ARG(lo && codes && freq > 0 && T % freq == 0, "avc_codes_gather: T %% freq must be 0");
+  long long n = (long long)B * (T / freq) * 2 * D;
+  codes_gather_kernel<<<GRID1(n)>>>(lo, codes, B, T, D, freq);
+  return avc_check_launch("avc_codes_gather");
+}
+
+extern "C" int avc_codes_scatter(const float* dcodes, float* dlo, int B, int T, int D, int freq, void* stream) {
+  AVC_CHECK_ARG(dcodes && dlo && freq > 0 && T % freq == 0, "avc_codes_scatter: T %% freq must be 0");
+  long long n = (long long)B * T * 2 * D;
+  codes_scatter_kernel<<<GRID1(n)>>>(dcodes, dlo, B, T, D, freq);
+  return avc_check_launch("avc_codes_scatter");
+}
+
+extern "C" int avc_dec_concat(const float* codes, const float* emb, float* out, int B, int T, int nc, int cd, int de,
+                              void* stream) {
+  AVC_CHECK_ARG(codes && emb && out && nc > 0 && T % nc == 0, "avc_dec_concat: bad args");
+  long long n = (long long)B * T * (cd + de);
+  dec_concat_kernel<<<GRID1(n)>>>(codes, emb, out, B, T, nc, cd, de);
+  return avc_check_launch("avc_dec_concat");
+}
+
+extern "C" int avc_dec_concat_bwd(const float* dout, float* dcodes, int B, int T, int nc, int cd, int de,
+                                  void* stream) {
+  AVC_CHECK_ARG(dout && dcodes && nc > 0 && T % nc == 0, "avc_dec_concat_bwd: bad args");
+  long long n = (long long)B * nc * cd;
+  dec_concat_bwd_kernel<<<GRID1(n)>>>(dout, dcodes, B, T, nc, cd, de);
+  return avc_check_launch("avc_dec_concat_bwd");
+}
+
+extern "C" int avc_conv_pack(const float* w, void* out, int dtype, int Co, int Ci, int K, int mode, void* stream) {
+  AVC_CHECK_ARG(w && out && (mode == 0 || mode == 1), "avc_conv_pack: bad args");
+  long long n = (long long)Co * Ci * K;
+  conv_pack_kernel<<<GRID1(n)>>>(w, out, dtype, Co, Ci, K, mode);
+  return avc_check_launch("avc_conv_pack");
+}
+
+extern "C" int avc_conv_grad_unpack(const float* dwf, float* dw, int Co, int Ci, int K, int acc, void* stream) {
+  AVC_CHECK_ARG(dwf && dw, "avc_conv_grad_unpack: null");
+  long long n = (long long)Co * Ci * K;
+  conv_grad_unpack_kernel<<<GRID1(n)>>>(dwf, dw, Co, Ci, K, acc);
+  return avc_check_launch("avc_conv_grad_unpack");
+}
+
+extern "C" int avc_convert(const float* src, void* dst, int dtype, long long n, void* stream) {
+  AVC_CHECK_ARG(src && dst, "avc_convert: null");
+  if (n == 0) return 0;
+  convert_kernel<<<GRID1(n)>>>(src, dst, dtype, n);
+  return avc_check_launch("avc_convert");
+}
+
+extern "C" int avc_transpose(const float* src, void* dst, int dtype, int R, int C, void* stream) {
+  AVC_CHECK_ARG(src && dst, "avc_transpose: null");
+  dim3 g(cdiv(C, 32), cdiv(R, 32));
+  transpose_kernel<<<g, 256, 0, as_stream(stream)>>>(src, dst, dtype, R, C);
+  return avc_check_launch("avc_transpose");
+}
+
+extern "C" int avc_add(const float* a, const float* b, float* o, long long n, void* stream) {
+  AVC_CHECK_ARG(a && b && o, "avc_add: null");
+  if (n == 0) return 0;
+  add_kernel<<<GRID1(n)>>>(a, b, o, n);
+  return avc_check_launch("avc_add");
+}
+
+static int loss_launch(const float* a, const float* b, long long n, float* out, int mode, void* stream) {
+  AVC_CHECK_ARG(a && b && out && n > 0, "avc loss: bad args");
+  (void)hipMemsetAsync(out, 0, sizeof(float), as_stream(stream));
+  int grid = (int)std::min<long long>(1024, cdiv(n, 256));
+  loss_kernel<<<grid, 256, 0, as_stream(stream)>>>(a, b, n, out, mode);
+  return avc_check_launch("avc loss");
+}
+
+extern "C" int avc_mse_loss(const float* a, const float* b, long long n, float* out, void* stream) {
+  return loss_launch(a, b, n, out, 0, stream);
+}
+extern "C" int avc_l1_loss(const float* a, const float* b, long long n, float* out, void* stream) {
+  return loss_launch(a, b, n, out, 1, stream);
+}
+
+extern "C" int avc_loss_grad(const float* a, const float* b, long long n, const float* dloss, int mode, float* g,
+                             float sign, void* stream) {
+  AVC_CHECK_ARG(a && b && dloss && g, "avc_loss_grad: null");
+  loss_grad_kernel<<<GRID1(n)>>>(a, b, n, dloss, mode, g, sign);
+  return avc_check_launch("avc_loss_grad");
+}
+
+extern "C" int avc_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
+                        float eps, float* state, void* stream) {
+  AVC_CHECK_ARG(p && g && m && v && state, "avc_adam: null");
+  hipStream_t s = as_stream(stream);
+  adam_prep_kernel<<<1, 1, 0, s>>>(state, lr, beta1, beta2);
+  int grid = (int)std::min<long long>(4096, cdiv(n, 256));
+  adam_kernel<<<grid, 256, 0, s>>>(p, g, m, v, n, beta1, beta2, eps, state);
+  return avc_check_launch("avc_adam");
+}

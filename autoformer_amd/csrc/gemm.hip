@@ -1,0 +1,481 @@
+// gemm.hip — LDS-tiled MFMA GEMM with frame-window (im2col / time-shift) operand
+// addressing and fused epilogues (bias, accumulate, split-K atomics, BatchNorm batch
+// statistics).  gfx950 only.
+//
+// Replaces the implicit cuDNN/cuBLAS calls behind nn.Conv1d (factory/Norm.py:21-28),
+// nn.Linear (Norm.py:40-50) and nn.LSTM's input projections (AutoVC.py:43,77,96), plus
+// every weight/data-gradient GEMM of their backward.
+//
+// Tile 128x128x32, 256 threads = 4 waves in a 2x2 grid, each wave 64x64 = 4x4 MFMA
+// 16x16 tiles.  Operands are staged global -> registers -> LDS (register staging lets
+// the loader apply the conv window / zero padding and the fp32->bf16 conversion), LDS is
+// double-buffered with one barrier per K-tile.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
+
+struct OpDev {
+  const void* ptr;
+  long long ld, bstride;
+  int dtype, win, vec, taps, pad, t_out, t_in, chans, rows;
+  FastDiv tdiv;
+};
+
+struct GemmArgs {
+  int M, N, K, batch, split_k, klen;
+  OpDev a, b;
+  float* c;
+  long long ldc, cbs;
+  const float* bias;
+  int accumulate, atomic;
+  float* bn_partial;
+};
+
+template <bool BF>
+struct Traits;
+template <>
+struct Traits<true> {
+  typedef bf16 T;
+  static constexpr int LDK = BK + 8;  // 80-byte rows
+};
+template <>
+struct Traits<false> {
+  typedef float T;
+  static constexpr int LDK = BK + 4;  // 144-byte rows
+};
+
+__device__ __forceinline__ float ld1(const void* p, long long idx, int dtype) {
+  return dtype == AVC_F32 ? reinterpret_cast<const float*>(p)[idx] : (float)reinterpret_cast<const bf16*>(p)[idx];
+}
+
+// window split of a (tap, c) index
+__device__ __forceinline__ void split_tap(int x, const OpDev& o, int& tap, int& c) {
+  tap = 0;
+  for (int j = 1; j < o.taps; ++j) tap += (x >= j * o.chans);
+  c = x - tap * o.chans;
+}
+
+// K-major operand: thread owns rows (tid>>3)+32i, k offset (tid&7)*4.
+struct KMajorState {
+  int rowok[4];
+  long long rowbase[4];  // plain: r*ld ; window: (b*t_in + t) frame index
+  int tt[4];             // window: t
+};
+
+__device__ __forceinline__ void kmajor_init(const OpDev& o, int row0, int tid, KMajorState& s) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int r = row0 + (tid >> 3) + 32 * i;
+    s.rowok[i] = r < o.rows;
+    if (o.win) {
+      uint32_t b = fdiv((uint32_t)r, o.tdiv);
+      int t = r - (int)b * o.t_out;
+      s.tt[i] = t;
+      s.rowbase[i] = (long long)b * o.t_in + t;
+    } else {
+      s.tt[i] = 0;
+      s.rowbase[i] = (long long)r * o.ld;
+    }
+  }
+}
+
+__device__ __forceinline__ f32x4 kmajor_elem_load(const OpDev& o, const KMajorState& s, int i, int k, int K,
+                                                  long long boff) {
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (o.vec) {
+    if (!s.rowok[i] || k >= K) return v;
+    long long idx;
+    if (o.win) {
+      int tap, c;
+      split_tap(k, o, tap, c);
+      int t2 = s.tt[i] + tap - o.pad;
+      if (t2 < 0 || t2 >= o.t_in) return v;
+      idx = (s.rowbase[i] + tap - o.pad) * o.ld + c;
+    } else {
+      idx = s.rowbase[i] + k;
+    }
+    return load4(o.ptr, idx + boff, o.dtype);
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    int kk = k + e;
+    if (!s.rowok[i] || kk >= K) continue;
+    long long idx;
+    if (o.win) {
+      int tap, c;
+      split_tap(kk, o, tap, c);
+      int t2 = s.tt[i] + tap - o.pad;
+      if (t2 < 0 || t2 >= o.t_in) continue;
+      idx = (s.rowbase[i] + tap - o.pad) * o.ld + c;
+    } else {
+      idx = s.rowbase[i] + kk;
+    }
+    v[e] = ld1(o.ptr, idx + boff, o.dtype);
+  }
+  return v;
+}
+
+// K-strided operand: thread owns rows row0+(tid&31)*4 .. +3 and k (tid>>5)*4+j.
+struct KStridedState {
+  int r;  // first of 4 rows
+  int tap, c;
+};
+
+__device__ __forceinline__ void kstrided_init(const OpDev& o, int row0, int tid, KStridedState& s) {
+  s.r = row0 + (tid & 31) * 4;
+  if (o.win) {
+    split_tap(s.r, o, s.tap, s.c);
+  } else {
+    s.tap = 0;
+    s.c = s.r;
+  }
+}
+
+__device__ __forceinline__ f32x4 kstrided_load(const OpDev& o, const KStridedState& s, int k, int K, long long boff) {
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (k >= K) return v;
+  long long fr = k;
+  if (o.vec && o.win) {
+    uint32_t b = fdiv((uint32_t)k, o.tdiv);
+    int t = k - (int)b * o.t_out;
+    int t2 = t + s.tap - o.pad;
+    if (t2 < 0 || t2 >= o.t_in) return v;
+    fr = (long long)b * o.t_in + t2;
+  } else {
+    fr = k;
+  }
+  if (o.vec) {
+    if (s.r >= o.rows) return v;
+    return load4(o.ptr, fr * o.ld + s.c + boff, o.dtype);
+  }
+  // scalar path (odd sizes): every element resolves its own (tap, c) and frame.
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    int rr = s.r + e;
+    if (rr >= o.rows) continue;
+    long long idx;
+    if (o.win) {
+      int tap2, c2;
+      split_tap(rr, o, tap2, c2);
+      uint32_t b = fdiv((uint32_t)k, o.tdiv);
+      int t3 = k - (int)b * o.t_out + tap2 - o.pad;
+      if (t3 < 0 || t3 >= o.t_in) continue;
+      idx = ((long long)b * o.t_in + t3) * o.ld + c2;
+    } else {
+      idx = (long long)k * o.ld + rr;
+    }
+    v[e] = ld1(o.ptr, idx + boff, o.dtype);
+  }
+  return v;
+}
+
+template <bool BF>
+__device__ __forceinline__ void store4(typename Traits<BF>::T* dst, f32x4 v) {
+  if constexpr (BF) {
+    bf16x4 h = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    *reinterpret_cast<bf16x4*>(dst) = h;
+  } else {
+    *reinterpret_cast<f32x4*>(dst) = v;
+  }
+}
+
+template <bool KS>
+struct Loader {
+  KMajorState km;
+  KStridedState ks;
+  f32x4 v[4];
+
+  __device__ __forceinline__ void init(const OpDev& o, int row0, int tid) {
+    if constexpr (KS) kstrided_init(o, row0, tid, ks);
+    else kmajor_init(o, row0, tid, km);
+  }
+  __device__ __forceinline__ void load(const OpDev& o, int k0, int kend, int tid, long long boff) {
+    if constexpr (KS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = kstrided_load(o, ks, k0 + (tid >> 5) * 4 + j, kend, boff);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = kmajor_elem_load(o, km, i, k0 + (tid & 7) * 4, kend, boff);
+    }
+  }
+  template <bool BF>
+  __device__ __forceinline__ void write(typename Traits<BF>::T* lds, int tid) {
+    constexpr int LDK = Traits<BF>::LDK;
+    if constexpr (KS) {
+      const int r = (tid & 31) * 4, kq = (tid >> 5) * 4;
+#pragma unroll
+      for (int ri = 0; ri < 4; ++ri) {
+        f32x4 w = {v[0][ri], v[1][ri], v[2][ri], v[3][ri]};
+        store4<BF>(lds + (r + ri) * LDK + kq, w);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) store4<BF>(lds + ((tid >> 3) + 32 * i) * LDK + (tid & 7) * 4, v[i]);
+    }
+  }
+};
+
+template <bool BF, bool AKS, bool BKS>
+__global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
+  typedef typename Traits<BF>::T T;
+  constexpr int LDK = Traits<BF>::LDK;
+  constexpr int TILE = (BM + BN) * LDK;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* smem = reinterpret_cast<T*>(smem_raw);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int bz = blockIdx.z / g.split_k, ks = blockIdx.z % g.split_k;
+  const int kbeg = ks * g.klen;
+  const int kend = min(g.K, kbeg + g.klen);
+  const long long aoff = (long long)bz * g.a.bstride, boff = (long long)bz * g.b.bstride;
+
+  Loader<AKS> la;
+  Loader<BKS> lb;
+  la.init(g.a, m0, tid);
+  lb.init(g.b, n0, tid);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nkt > 0) {
+    la.load(g.a, kbeg, kend, tid, aoff);
+    lb.load(g.b, kbeg, kend, tid, boff);
+    la.template write<BF>(smem, tid);
+    lb.template write<BF>(smem + BM * LDK, tid);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    T* As = smem + (kt & 1) * TILE;
+    T* Bs = As + BM * LDK;
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      la.load(g.a, kbeg + (kt + 1) * BK, kend, tid, aoff);
+      lb.load(g.b, kbeg + (kt + 1) * BK, kend, tid, boff);
+    }
+    if constexpr (BF) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + (lane & 15)) * LDK + 8 * (lane >> 4));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + j * 16 + (lane & 15)) * LDK + 8 * (lane >> 4));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 4) {
+        float af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = As[(wm * 64 + i * 16 + (lane & 15)) * LDK + kk + (lane >> 4)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = Bs[(wn * 64 + j * 16 + (lane & 15)) * LDK + kk + (lane >> 4)];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (more) {
+      T* An = smem + ((kt + 1) & 1) * TILE;
+      la.template write<BF>(An, tid);
+      lb.template write<BF>(An + BM * LDK, tid);
+    }
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  const int rbase = m0 + wm * 64 + 4 * (lane >> 4);
+  const int cbase = n0 + wn * 64 + (lane & 15);
+  float* C = g.c + (long long)bz * g.cbs;
+  if (g.bias && ks == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int col = cbase + j * 16;
+      float bv = col < g.N ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] += bv;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      int row = rbase + i * 16 + e;
+      if (row >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int col = cbase + j * 16;
+        if (col >= g.N) continue;
+        float* p = C + (long long)row * g.ldc + col;
+        float v = acc[i][j][e];
+        if (g.atomic) atomicAdd(p, v);
+        else if (g.accumulate) *p += v;
+        else *p = v;
+      }
+    }
+
+  if (g.bn_partial) {
+    // Per-column (sum, M2 about the tile mean) over this tile's valid rows.
+    float* red = reinterpret_cast<float*>(smem_raw);  // [2][BN]
+    const int cnt = min(BM, g.M - m0);
+    float s[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t += (rbase + i * 16 + e < g.M) ? acc[i][j][e] : 0.f;
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      s[j] = t;
+    }
+    __syncthreads();
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[wm * BN + wn * 64 + j * 16 + lane] = s[j];
+    }
+    __syncthreads();
+    float mean[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int cl = wn * 64 + j * 16 + (lane & 15);
+      mean[j] = (red[cl] + red[BN + cl]) / (float)cnt;
+    }
+    float q[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float d = acc[i][j][e] - mean[j];
+          t += (rbase + i * 16 + e < g.M) ? d * d : 0.f;
+        }
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      q[j] = t;
+    }
+    __syncthreads();
+    float* red2 = red + 2 * BN;
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red2[wm * BN + wn * 64 + j * 16 + lane] = q[j];
+    }
+    __syncthreads();
+    if (tid < BN) {
+      int col = n0 + tid;
+      if (col < g.N) {
+        float* p = g.bn_partial + ((long long)blockIdx.y * g.N + col) * 2;
+        p[0] = red[tid] + red[BN + tid];
+        p[1] = red2[tid] + red2[BN + tid];
+      }
+    }
+  }
+}
+
+__global__ void zero2d_kernel(float* c, long long ldc, long long cbs, int M, int N) {
+  long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = (long long)M * N;
+  if (idx >= total) return;
+  int r = (int)(idx / N), col = (int)(idx % N);
+  c[(long long)blockIdx.y * cbs + (long long)r * ldc + col] = 0.f;
+}
+
+bool aligned4(const void* p, int dtype) {
+  uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  return dtype == AVC_F32 ? (a % 16 == 0) : (a % 8 == 0);
+}
+
+int make_op(const avc_operand& o, int rows, int K, OpDev& d, const char* name) {
+  AVC_CHECK_ARG(o.ptr != nullptr, "avc_gemm: operand %s is null", name);
+  AVC_CHECK_ARG(o.dtype == AVC_F32 || o.dtype == AVC_BF16, "avc_gemm: operand %s bad dtype", name);
+  d.ptr = o.ptr;
+  d.ld = o.ld;
+  d.bstride = o.batch_stride;
+  d.dtype = o.dtype;
+  d.win = o.taps > 0;
+  d.taps = o.taps > 0 ? o.taps : 1;
+  d.pad = o.pad;
+  d.t_out = o.t_out > 0 ? o.t_out : 1;
+  d.t_in = o.t_in > 0 ? o.t_in : 1;
+  d.chans = o.chans > 0 ? o.chans : 1;
+  d.rows = rows;
+  d.tdiv = make_fastdiv((uint32_t)d.t_out);
+  if (d.win) {
+    AVC_CHECK_ARG(o.t_out > 0 && o.t_in > 0 && o.chans > 0, "avc_gemm: operand %s window needs t_out/t_in/chans", name);
+    int span = d.taps * d.chans;
+    AVC_CHECK_ARG(span == (o.kstrided ? rows : K), "avc_gemm: operand %s taps*chans=%d != split dim %d", name, span,
+                  o.kstrided ? rows : K);
+  }
+  int contig = o.kstrided ? rows : K;
+  d.vec = (o.ld % 4 == 0) && (contig % 4 == 0) && (o.batch_stride % 4 == 0) && aligned4(o.ptr, o.dtype) &&
+          (!d.win || d.chans % 4 == 0);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
+  AVC_CHECK_ARG(d != nullptr, "avc_gemm: null desc");
+  AVC_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0, "avc_gemm: negative dims");
+  if (d->M == 0 || d->N == 0) return 0;
+  AVC_CHECK_ARG(d->c != nullptr, "avc_gemm: null C");
+  GemmArgs g;
+  g.M = d->M;
+  g.N = d->N;
+  g.K = d->K;
+  g.batch = d->batch > 0 ? d->batch : 1;
+  g.split_k = d->split_k > 1 ? d->split_k : 1;
+  if (make_op(d->a, d->M, d->K, g.a, "A")) return -1;
+  if (make_op(d->b, d->N, d->K, g.b, "B")) return -1;
+  int kl = (d->K + g.split_k - 1) / g.split_k;
+  kl = ((kl + BK - 1) / BK) * BK;
+  g.klen = kl > 0 ? kl : BK;
+  g.c = d->c;
+  g.ldc = d->ldc;
+  g.cbs = d->c_batch_stride;
+  g.bias = d->bias;
+  g.accumulate = d->accumulate;
+  g.atomic = g.split_k > 1;
+  g.bn_partial = d->bn_partial;
+  AVC_CHECK_ARG(!(g.bn_partial && (g.split_k > 1 || g.batch > 1 || d->accumulate)),
+                "avc_gemm: bn_partial needs split_k == 1, batch == 1, accumulate == 0");
+  hipStream_t s = as_stream(stream);
+  if (g.atomic && !d->accumulate) {
+    long long tot = (long long)g.M * g.N;
+    dim3 zg(cdiv(tot, 256), g.batch);
+    zero2d_kernel<<<zg, 256, 0, s>>>(g.c, g.ldc, g.cbs, g.M, g.N);
+  }
+  dim3 grid(cdiv(g.N, BN), cdiv(g.M, BM), g.batch * g.split_k);
+  const bool bf = d->compute == AVC_BF16;
+  const bool aks = d->a.kstrided != 0, bks = d->b.kstrided != 0;
+  size_t lds = bf ? 2 * (BM + BN) * Traits<true>::LDK * sizeof(bf16) : 2 * (BM + BN) * Traits<false>::LDK * sizeof(float);
+#define AVC_GEMM_LAUNCH(BFV, A, B) gemm_kernel<BFV, A, B><<<grid, NT, lds, s>>>(g)
+  if (bf) {
+    if (!aks && !bks) AVC_GEMM_LAUNCH(true, false, false);
+    else if (!aks && bks) AVC_GEMM_LAUNCH(true, false, true);
+    else if (aks && !bks) AVC_GEMM_LAUNCH(true, true, false);
+    else AVC_GEMM_LAUNCH(true, true, true);
+  } else {
+    if (!aks && !bks) AVC_GEMM_LAUNCH(false, false, false);
+    else if (!aks && bks) AVC_GEMM_LAUNCH(false, false, true);
+    else if (aks && !bks) AVC_GEMM_LAUNCH(false, true, false);
+    else AVC_GEMM_LAUNCH(false, true, true);
+  }
+#undef AVC_GEMM_LAUNCH
+  return avc_check_launch("avc_gemm");
+}

@@ -1,0 +1,491 @@
+// lstm.hip — LSTM recurrences (forward and backward) for the AutoVC path.
+//
+// Replaces the time loops inside nn.LSTM: encoder BiLSTM(512->44, 2 layers)
+// (factory/AutoVC.py:43,54-55), decoder lstm1(344->512) (:77,103) and lstm2(512->1024,
+// 2 layers) (:96,110).  Gate order i, f, g, o; h0 = c0 = 0; the input projection
+// x W_ih^T + b_ih + b_hh is a separate GEMM over all frames (gemm.hip) and arrives here
+// as `xproj`.
+//
+// Two designs, chosen by H:
+//  * small H (<= 64, the encoder): batch rows are independent in the recurrence, so one
+//    workgroup owns one (utterance, direction) for all T steps.  W_hh lives in registers
+//    (one gate row per thread), h/gates in LDS; no inter-workgroup sync at all.
+//  * large H (multiple of 128, the decoder): one fused kernel per time step.  Each
+//    workgroup owns (16*MT utterances) x (8 hidden units, all 4 gates) [forward] or
+//    (16*MT utterances) x (16 hidden units) [backward]; the recurrent product runs on
+//    MFMA with K split over the 4 waves and operands loaded straight into registers;
+//    the cell update is fused into the same kernel's epilogue.  Kernel boundaries are the
+//    grid-wide sync (cheaper on gfx950 than a software grid barrier at 256 workgroups,
+//    MI355X_MICROARCH.md rows "boundary" vs "barrier-xcd"); the host loop is
+//    graph-capturable.
+#include "common.h"
+
+namespace {
+
+// =============================================================== small H: persistent
+template <int HM>
+__global__ void __launch_bounds__(256) lstm_small_fwd(const float* __restrict__ xproj, const float* __restrict__ whh,
+                                                      int T, int H, int dirs, float* __restrict__ hout,
+                                                      float* __restrict__ cout, float* __restrict__ gout) {
+  const int b = blockIdx.x, d = blockIdx.y, tid = threadIdx.x;
+  const int G = 4 * H;
+  __shared__ __attribute__((aligned(16))) float hs[HM];
+  __shared__ float gs[4 * HM];
+  float w[HM];
+  const float* W = whh + (long long)d * G * H;
+#pragma unroll
+  for (int k = 0; k < HM; ++k) w[k] = (tid < G && k < H) ? W[(long long)tid * H + k] : 0.f;
+  if (tid < HM) hs[tid] = 0.f;
+  float c = 0.f;
+  const long long ldx = (long long)dirs * G, ldh = (long long)dirs * H;
+  const int q = tid < G ? tid / H : 0;
+  const int t0 = d ? T - 1 : 0, dt = d ? -1 : 1;
+  float xn = tid < G ? xproj[((long long)b * T + t0) * ldx + d * G + tid] : 0.f;
+  __syncthreads();
+  for (int s = 0; s < T; ++s) {
+    const int t = t0 + dt * s;
+    const float x = xn;
+    if (s + 1 < T && tid < G) xn = xproj[((long long)b * T + t + dt) * ldx + d * G + tid];
+    if (tid < G) {
+      float acc = x;
+      const f32x4* h4 = reinterpret_cast<const f32x4*>(hs);
+#pragma unroll
+      for (int k = 0; k < HM / 4; ++k) {
+        f32x4 hv = h4[k];
+        acc += hv[0] * w[4 * k] + hv[1] * w[4 * k + 1] + hv[2] * w[4 * k + 2] + hv[3] * w[4 * k + 3];
+      }
+      const float gv = q == 2 ? tanhf(acc) : sigmoidf_(acc);
+      gs[tid] = gv;
+      gout[((long long)b * T + t) * ldx + d * G + tid] = gv;
+    }
+    __syncthreads();
+    if (tid < H) {
+      const float ig = gs[tid], fg = gs[H + tid], gg = gs[2 * H + tid], og = gs[3 * H + tid];
+      c = fg * c + ig * gg;
+      const float h = og * tanhf(c);
+      hs[tid] = h;
+      const long long o = ((long long)b * T + t) * ldh + d * H + tid;
+      hout[o] = h;
+      cout[o] = c;
+    }
+    __syncthreads();
+  }
+}
+
+template <int HM>
+__global__ void __launch_bounds__(256) lstm_small_bwd(const float* __restrict__ dhout, const float* __restrict__ call,
+                                                      const float* __restrict__ gall, const float* __restrict__ whh,
+                                                      int T, int H, int dirs, float* __restrict__ dg) {
+  const int b = blockIdx.x, d = blockIdx.y, tid = threadIdx.x;
+  const int G = 4 * H;
+  __shared__ float dhs[HM];
+  __shared__ float dgs[4 * HM];
+  // k-role: thread (k = tid>>2, q = tid&3) holds W[q*H + g'][k], g' < H
+  const int kk = tid >> 2, qq = tid & 3;
+  float wc[HM];
+  const float* W = whh + (long long)d * G * H;
+#pragma unroll
+  for (int g = 0; g < HM; ++g) wc[g] = (kk < H && g < H) ? W[(long long)(qq * H + g) * H + kk] : 0.f;
+  if (tid < HM) dhs[tid] = 0.f;
+  for (int i = tid; i < 4 * HM; i += 256) dgs[i] = 0.f;
+  float dc = 0.f;
+  const long long ldg = (long long)dirs * G, ldh = (long long)dirs * H;
+  // backward walks opposite to the forward recurrence
+  const int t0 = d ? 0 : T - 1, dt = d ? 1 : -1;
+  const int fwd_prev = d ? 1 : -1;  // offset of the forward's previous time step
+  float pdh = 0, pc = 0, pcp = 0, pi = 0, pf = 0, pg = 0, po = 0;
+  auto fetch = [&](int t) {
+    if (tid < H) {
+      const long long o = ((long long)b * T + t) * ldh + d * H + tid;
+      const long long og = ((long long)b * T + t) * ldg + d * G + tid;
+      pdh = dhout[o];
+      pc = call[o];
+      const int tp = t + fwd_prev;
+      pcp = (tp >= 0 && tp < T) ? call[((long long)b * T + tp) * ldh + d * H + tid] : 0.f;
+      pi = gall[og];
+      pf = gall[og + H];
+      pg = gall[og + 2 * H];
+      po = gall[og + 3 * H];
+    }
+  };
+  fetch(t0);
+  __syncthreads();
+  for (int s = 0; s < T; ++s) {
+    const int t = t0 + dt * s;
+    if (tid < H) {
+      const float dh = pdh + dhs[tid];
+      const float c = pc, cp = pcp, ig = pi, fg = pf, gg = pg, og = po;
+      const float tc = tanhf(c);
+      const float do_ = dh * tc;
+      float dcs = dc + dh * og * (1.f - tc * tc);
+      const float di = dcs * gg, dgg = dcs * ig, df = dcs * cp;
+      dc = dcs * fg;
+      const float a0 = di * ig * (1.f - ig), a1 = df * fg * (1.f - fg), a2 = dgg * (1.f - gg * gg),
+                  a3 = do_ * og * (1.f - og);
+      const long long og_ = ((long long)b * T + t) * ldg + d * G + tid;
+      dg[og_] = a0;
+      dg[og_ + H] = a1;
+      dg[og_ + 2 * H] = a2;
+      dg[og_ + 3 * H] = a3;
+      dgs[tid] = a0;
+      dgs[H + tid] = a1;
+      dgs[2 * H + tid] = a2;
+      dgs[3 * H + tid] = a3;
+    }
+    if (s + 1 < T) fetch(t + dt);
+    __syncthreads();
+    if (tid < 4 * H) {
+      float p = 0.f;
+      const float* src = dgs + qq * H;
+#pragma unroll
+      for (int g = 0; g < HM; ++g) p += (g < H ? src[g] : 0.f) * wc[g];
+      p += __shfl_xor(p, 1, 64);
+      p += __shfl_xor(p, 2, 64);
+      if (qq == 0 && kk < H) dhs[kk] = p;
+    }
+    __syncthreads();
+  }
+}
+
+// =============================================================== large H: per-step kernels
+struct StepArgs {
+  const float* xproj;  // (B,T,dirs*4H)
+  const void* w;       // fwd: dirs x [4H][H]; bwd: dirs x [H][4H]
+  float* hout;         // (B,T,dirs*H)
+  float* call;         // (B,T,dirs*H)
+  float* gall;         // (B,T,dirs*4H) activated gates
+  void* hb;            // bf16 ping-pong [2][dirs][B][H] (fwd) / [2][dirs][B][4H] (bwd)
+  const float* dhout;  // bwd
+  float* dg;           // bwd (B,T,dirs*4H)
+  float* dcb;          // bwd [dirs][B][H]
+  int B, T, H, dirs, s;
+};
+
+template <bool BF, int MT>
+__global__ void __launch_bounds__(256) lstm_step_fwd(StepArgs a) {
+  const int H = a.H, G = 4 * H, T = a.T, B = a.B;
+  const int d = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j0 = blockIdx.x * 8, b0 = blockIdx.y * 16 * MT;
+  const int t = d ? T - 1 - a.s : a.s;
+  const int tp = d ? t + 1 : t - 1;
+  const long long ldx = (long long)a.dirs * G, ldh = (long long)a.dirs * H;
+  __shared__ float red[4][16 * MT][33];
+
+  // prefetch the epilogue's inputs (independent of the GEMM)
+  const int pr = tid >> 3, pj = tid & 7;
+  const int pb = b0 + pr;
+  const bool pv = pr < 16 * MT && pb < B;
+  float px[4] = {0.f, 0.f, 0.f, 0.f}, pcp = 0.f;
+  if (pv) {
+    const long long ox = ((long long)pb * T + t) * ldx + d * G + j0 + pj;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) px[q] = a.xproj[ox + q * H];
+    if (a.s > 0) pcp = a.call[((long long)pb * T + tp) * ldh + d * H + j0 + pj];
+  }
+
+  f32x4 acc[MT][2];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m][0] = acc[m][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (a.s > 0) {
+    const int kw = H / 4, kbeg = w * kw;
+    const int r16 = lane & 15, kh = lane >> 4;
+    if constexpr (BF) {
+      const bf16* hp = reinterpret_cast<const bf16*>(a.hb) + ((long long)((a.s - 1) & 1) * a.dirs + d) * B * H;
+      const bf16* W = reinterpret_cast<const bf16*>(a.w) + (long long)d * G * H;
+      const bf16* arow[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        int b = b0 + m * 16 + r16;
+        arow[m] = b < B ? hp + (long long)b * H : nullptr;
+      }
+      const bf16* brow[2];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        int col = n * 16 + r16;
+        brow[n] = W + (long long)((col >> 3) * H + j0 + (col & 7)) * H;
+      }
+      const bf16x8 z = {};
+#pragma unroll 4
+      for (int k0 = kbeg; k0 < kbeg + kw; k0 += 32) {
+        const int ko = k0 + 8 * kh;
+        bf16x8 af[MT], bfr[2];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) af[m] = arow[m] ? *reinterpret_cast<const bf16x8*>(arow[m] + ko) : z;
+#pragma unroll
+        for (int n = 0; n < 2; ++n) bfr[n] = *reinterpret_cast<const bf16x8*>(brow[n] + ko);
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+      }
+    } else {
+      const float* W = reinterpret_cast<const float*>(a.w) + (long long)d * G * H;
+      const float* arow[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        int b = b0 + m * 16 + r16;
+        arow[m] = b < B ? a.hout + ((long long)b * T + tp) * ldh + d * H : nullptr;
+      }
+      const float* brow[2];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        int col = n * 16 + r16;
+        brow[n] = W + (long long)((col >> 3) * H + j0 + (col & 7)) * H;
+      }
+#pragma unroll 8
+      for (int k0 = kbeg; k0 < kbeg + kw; k0 += 4) {
+        float af[MT], bfr[2];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) af[m] = arow[m] ? arow[m][k0 + kh] : 0.f;
+#pragma unroll
+        for (int n = 0; n < 2; ++n) bfr[n] = brow[n][k0 + kh];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[m], bfr[n], acc[m][n], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[w][m * 16 + 4 * (lane >> 4) + e][n * 16 + (lane & 15)] = acc[m][n][e];
+  __syncthreads();
+  if (pv) {
+    float pre[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      pre[q] = px[q] + red[0][pr][q * 8 + pj] + red[1][pr][q * 8 + pj] + red[2][pr][q * 8 + pj] + red[3][pr][q * 8 + pj];
+    const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), gg = tanhf(pre[2]), og = sigmoidf_(pre[3]);
+    const float c = fg * pcp + ig * gg;
+    const float h = og * tanhf(c);
+    const int j = j0 + pj;
+    const long long oh = ((long long)pb * T + t) * ldh + d * H + j;
+    a.hout[oh] = h;
+    a.call[oh] = c;
+    const long long og_ = ((long long)pb * T + t) * ldx + d * G + j;
+    a.gall[og_] = ig;
+    a.gall[og_ + H] = fg;
+    a.gall[og_ + 2 * H] = gg;
+    a.gall[og_ + 3 * H] = og;
+    if constexpr (BF) {
+      bf16* hn = reinterpret_cast<bf16*>(a.hb) + ((long long)(a.s & 1) * a.dirs + d) * B * H;
+      hn[(long long)pb * H + j] = (bf16)h;
+    }
+  }
+}
+
+template <bool BF, int MT>
+__global__ void __launch_bounds__(256) lstm_step_bwd(StepArgs a) {
+  const int H = a.H, G = 4 * H, T = a.T, B = a.B;
+  const int d = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j0 = blockIdx.x * 16, b0 = blockIdx.y * 16 * MT;
+  const int t = d ? a.s : T - 1 - a.s;
+  const int tn = d ? t - 1 : t + 1;  // time handled by the previous backward step
+  const int tp = d ? t + 1 : t - 1;  // forward's previous time step
+  const long long ldg = (long long)a.dirs * G, ldh = (long long)a.dirs * H;
+  __shared__ float red[4][16 * MT][17];
+  constexpr int PPT = MT;  // (row, unit) pairs per thread: 16*MT*16 / 256
+
+  float pdh[PPT], pc[PPT], pcp[PPT], pg[PPT][4], pdc[PPT];
+  int prow[PPT], pjj[PPT];
+  bool pv[PPT];
+#pragma unroll
+  for (int u = 0; u < PPT; ++u) {
+    const int p = tid + 256 * u;
+    prow[u] = p >> 4;
+    pjj[u] = p & 15;
+    const int b = b0 + prow[u];
+    pv[u] = b < B;
+    pdh[u] = pc[u] = pcp[u] = pdc[u] = 0.f;
+    pg[u][0] = pg[u][1] = pg[u][2] = pg[u][3] = 0.f;
+    if (pv[u]) {
+      const int j = j0 + pjj[u];
+      const long long oh = ((long long)b * T + t) * ldh + d * H + j;
+      pdh[u] = a.dhout[oh];
+      pc[u] = a.call[oh];
+      if (tp >= 0 && tp < T) pcp[u] = a.call[((long long)b * T + tp) * ldh + d * H + j];
+      const long long og_ = ((long long)b * T + t) * ldg + d * G + j;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pg[u][q] = a.gall[og_ + q * H];
+      if (a.s > 0) pdc[u] = a.dcb[((long long)d * B + b) * H + j];
+    }
+  }
+
+  f32x4 acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (a.s > 0) {
+    const int kw = G / 4, kbeg = w * kw;
+    const int r16 = lane & 15, kh = lane >> 4;
+    if constexpr (BF) {
+      const bf16* gp = reinterpret_cast<const bf16*>(a.hb) + ((long long)((a.s - 1) & 1) * a.dirs + d) * B * G;
+      const bf16* WT = reinterpret_cast<const bf16*>(a.w) + (long long)d * H * G;
+      const bf16* arow[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        int b = b0 + m * 16 + r16;
+        arow[m] = b < B ? gp + (long long)b * G : nullptr;
+      }
+      const bf16* brow = WT + (long long)(j0 + r16) * G;
+      const bf16x8 z = {};
+#pragma unroll 4
+      for (int k0 = kbeg; k0 < kbeg + kw; k0 += 32) {
+        const int ko = k0 + 8 * kh;
+        bf16x8 bfr = *reinterpret_cast<const bf16x8*>(brow + ko);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          bf16x8 af = arow[m] ? *reinterpret_cast<const bf16x8*>(arow[m] + ko) : z;
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[m], 0, 0, 0);
+        }
+      }
+    } else {
+      const float* WT = reinterpret_cast<const float*>(a.w) + (long long)d * H * G;
+      const float* arow[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        int b = b0 + m * 16 + r16;
+        arow[m] = b < B ? a.dg + ((long long)b * T + tn) * ldg + d * G : nullptr;
+      }
+      const float* brow = WT + (long long)(j0 + r16) * G;
+#pragma unroll 8
+      for (int k0 = kbeg; k0 < kbeg + kw; k0 += 4) {
+        float bfr = brow[k0 + kh];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          float af = arow[m] ? arow[m][k0 + kh] : 0.f;
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(af, bfr, acc[m], 0, 0, 0);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[w][m * 16 + 4 * (lane >> 4) + e][lane & 15] = acc[m][e];
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < PPT; ++u) {
+    if (!pv[u]) continue;
+    const int r = prow[u], jl = pjj[u], b = b0 + r, j = j0 + jl;
+    const float dh = pdh[u] + red[0][r][jl] + red[1][r][jl] + red[2][r][jl] + red[3][r][jl];
+    const float ig = pg[u][0], fg = pg[u][1], gg = pg[u][2], og = pg[u][3];
+    const float tc = tanhf(pc[u]);
+    const float do_ = dh * tc;
+    const float dcs = pdc[u] + dh * og * (1.f - tc * tc);
+    const float di = dcs * gg, dgg = dcs * ig, df = dcs * pcp[u];
+    a.dcb[((long long)d * B + b) * H + j] = dcs * fg;
+    const float v[4] = {di * ig * (1.f - ig), df * fg * (1.f - fg), dgg * (1.f - gg * gg), do_ * og * (1.f - og)};
+    const long long og_ = ((long long)b * T + t) * ldg + d * G + j;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a.dg[og_ + q * H] = v[q];
+    if constexpr (BF) {
+      bf16* gn = reinterpret_cast<bf16*>(a.hb) + ((long long)(a.s & 1) * a.dirs + d) * B * G + (long long)b * G;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gn[q * H + j] = (bf16)v[q];
+    }
+  }
+}
+
+template <int HM>
+void launch_small_fwd(dim3 g, hipStream_t s, const float* x, const float* w, int T, int H, int dirs, float* h, float* c,
+                      float* gt) {
+  lstm_small_fwd<HM><<<g, 256, 0, s>>>(x, w, T, H, dirs, h, c, gt);
+}
+template <int HM>
+void launch_small_bwd(dim3 g, hipStream_t s, const float* dh, const float* c, const float* gt, const float* w, int T,
+                      int H, int dirs, float* dg) {
+  lstm_small_bwd<HM><<<g, 256, 0, s>>>(dh, c, gt, w, T, H, dirs, dg);
+}
+
+}  // namespace
+
+extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T, int H, int dirs, float* h,
+                            float* c, float* gates, void* hbuf, int compute, void* stream) {
+  AVC_CHECK_ARG(xproj && w_hh && h && c && gates && B > 0 && T > 0 && H > 0 && (dirs == 1 || dirs == 2),
+                "avc_lstm_fwd: bad args");
+  hipStream_t s = as_stream(stream);
+  if (H <= 64) {
+    AVC_CHECK_ARG(wdtype == AVC_F32, "avc_lstm_fwd: small-H path takes fp32 W_hh");
+    dim3 g(B, dirs);
+    if (H <= 16) launch_small_fwd<16>(g, s, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
+    else if (H <= 32) launch_small_fwd<32>(g, s, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
+    else if (H <= 48) launch_small_fwd<48>(g, s, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
+    else launch_small_fwd<64>(g, s, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
+    return avc_check_launch("avc_lstm_fwd(small)");
+  }
+  AVC_CHECK_ARG(H % 128 == 0, "avc_lstm_fwd: H must be <= 64 or a multiple of 128 (got %d)", H);
+  const bool bf = compute == AVC_BF16;
+  AVC_CHECK_ARG(!bf || (wdtype == AVC_BF16 && hbuf), "avc_lstm_fwd: bf16 compute needs bf16 W_hh and hbuf");
+  AVC_CHECK_ARG(bf || wdtype == AVC_F32, "avc_lstm_fwd: fp32 compute needs fp32 W_hh");
+  StepArgs a = {};
+  a.xproj = xproj;
+  a.w = w_hh;
+  a.hout = h;
+  a.call = c;
+  a.gall = gates;
+  a.hb = hbuf;
+  a.B = B;
+  a.T = T;
+  a.H = H;
+  a.dirs = dirs;
+  const int mt = (H >= 1024 && B > 16) ? 2 : 1;
+  dim3 g(H / 8, cdiv(B, 16 * mt), dirs);
+  for (int st = 0; st < T; ++st) {
+    a.s = st;
+    if (bf) {
+      if (mt == 2) lstm_step_fwd<true, 2><<<g, 256, 0, s>>>(a);
+      else lstm_step_fwd<true, 1><<<g, 256, 0, s>>>(a);
+    } else {
+      if (mt == 2) lstm_step_fwd<false, 2><<<g, 256, 0, s>>>(a);
+      else lstm_step_fwd<false, 1><<<g, 256, 0, s>>>(a);
+    }
+  }
+  return avc_check_launch("avc_lstm_fwd");
+}
+
+extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c, const float* gates, const void* w_hh,
+                            const void* w_hh_t, int wdtype, int B, int T, int H, int dirs, float* dgates, float* dcbuf,
+                            void* gbuf, int compute, void* stream) {
+  (void)h;
+  AVC_CHECK_ARG(dh_out && c && gates && dgates && B > 0 && T > 0 && H > 0 && (dirs == 1 || dirs == 2),
+                "avc_lstm_bwd: bad args");
+  hipStream_t s = as_stream(stream);
+  if (H <= 64) {
+    AVC_CHECK_ARG(w_hh && wdtype == AVC_F32, "avc_lstm_bwd: small-H path takes fp32 W_hh");
+    dim3 g(B, dirs);
+    if (H <= 16) launch_small_bwd<16>(g, s, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
+    else if (H <= 32) launch_small_bwd<32>(g, s, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
+    else if (H <= 48) launch_small_bwd<48>(g, s, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
+    else launch_small_bwd<64>(g, s, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
+    return avc_check_launch("avc_lstm_bwd(small)");
+  }
+  AVC_CHECK_ARG(H % 128 == 0, "avc_lstm_bwd: H must be <= 64 or a multiple of 128 (got %d)", H);
+  AVC_CHECK_ARG(w_hh_t && dcbuf, "avc_lstm_bwd: large-H path needs W_hh^T and dcbuf");
+  const bool bf = compute == AVC_BF16;
+  AVC_CHECK_ARG(!bf || (wdtype == AVC_BF16 && gbuf), "avc_lstm_bwd: bf16 compute needs bf16 W_hh^T and gbuf");
+  StepArgs a = {};
+  a.w = w_hh_t;
+  a.call = const_cast<float*>(c);
+  a.gall = const_cast<float*>(gates);
+  a.hb = gbuf;
+  a.dhout = dh_out;
+  a.dg = dgates;
+  a.dcb = dcbuf;
+  a.B = B;
+  a.T = T;
+  a.H = H;
+  a.dirs = dirs;
+  dim3 g(H / 16, cdiv(B, 16), dirs);
+  for (int st = 0; st < T; ++st) {
+    a.s = st;
+    if (bf) lstm_step_bwd<true, 1><<<g, 256, 0, s>>>(a);
+    else lstm_step_bwd<false, 1><<<g, 256, 0, s>>>(a);
+  }
+  return avc_check_launch("avc_lstm_bwd");
+}

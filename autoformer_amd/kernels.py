@@ -1,0 +1,271 @@
+"""Thin, validated Python wrappers over the C-ABI (include/autovc_hip.h).
+
+Every function takes torch tensors that already live on the HIP device, checks shapes /
+dtypes / contiguity on the host, and launches on torch's current stream.  No function
+here has a CPU fallback.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import torch
+
+from . import _lib as L
+from ._lib import ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_TANH, BF16, F32  # noqa: F401
+
+_COMPUTE = {"bf16": BF16, "fp32": F32}[os.environ.get("AUTOVC_COMPUTE", "bf16")]
+
+
+def set_compute(name: str) -> None:
+    """'bf16' (bf16 MFMA, fp32 accumulate/state) or 'fp32' (exact fp32 MFMA, parity mode)."""
+    global _COMPUTE
+    _COMPUTE = {"bf16": BF16, "fp32": F32}[name]
+
+
+def compute() -> int:
+    return _COMPUTE
+
+
+def compute_torch_dtype():
+    return torch.bfloat16 if _COMPUTE == BF16 else torch.float32
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+def _dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"unsupported dtype {t.dtype}")
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("autoformer_amd kernels need HIP device tensors (no CPU fallback)")
+
+
+# ------------------------------------------------------------------------- GEMM
+def operand(t: torch.Tensor, ld: int, kstrided: bool = False, window=None, batch_stride: int = 0) -> L.Operand:
+    """window = (taps, pad, t_out, t_in, chans) or None."""
+    _dev(t)
+    o = L.Operand()
+    o.ptr = t.data_ptr()
+    o.dtype = _dt(t)
+    o.kstrided = int(kstrided)
+    o.ld = int(ld)
+    o.batch_stride = int(batch_stride)
+    if window is not None:
+        o.taps, o.pad, o.t_out, o.t_in, o.chans = (int(v) for v in window)
+    return o
+
+
+def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=None, accumulate=False, split_k=1,
+         bn_partial=None, batch=1, c_batch_stride=0, comp=None):
+    _dev(c, bias, bn_partial)
+    assert c.dtype == torch.float32
+    d = L.GemmDesc()
+    d.M, d.N, d.K, d.batch = int(M), int(N), int(K), int(batch)
+    d.a, d.b = a, b
+    d.c = c.data_ptr()
+    d.ldc = int(N if ldc is None else ldc)
+    d.c_batch_stride = int(c_batch_stride)
+    d.bias = _ptr(bias)
+    d.accumulate = int(accumulate)
+    d.split_k = int(split_k)
+    d.bn_partial = _ptr(bn_partial)
+    d.compute = _COMPUTE if comp is None else comp
+    L.check(L.lib().avc_gemm(d, stream()), "avc_gemm")
+
+
+def auto_split_k(M, N, K, target=256, min_k=1024):
+    tiles = math.ceil(M / 128) * math.ceil(N / 128)
+    if tiles >= target // 2:
+        return 1
+    s = max(1, min(target // max(tiles, 1), K // min_k))
+    return s
+
+
+# ------------------------------------------------------------------------- BN
+def bn_partial_buffer(M, C, device):
+    return torch.empty(math.ceil(M / 128), C, 2, device=device, dtype=torch.float32)
+
+
+def bn_finalize(partial, M, C, gamma, beta, rmean, rvar, nbt, momentum, eps):
+    dev = partial.device
+    mean, rstd, scale, shift = (torch.empty(C, device=dev) for _ in range(4))
+    L.call("avc_bn_finalize", partial.data_ptr(), M, C, _ptr(gamma), _ptr(beta), _ptr(rmean), _ptr(rvar), _ptr(nbt),
+           float(momentum), float(eps), mean.data_ptr(), rstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), stream())
+    return mean, rstd, scale, shift
+
+
+def bn_eval(rmean, rvar, gamma, beta, eps):
+    C = rmean.numel()
+    dev = rmean.device
+    mean, rstd, scale, shift = (torch.empty(C, device=dev) for _ in range(4))
+    L.call("avc_bn_eval", rmean.data_ptr(), rvar.data_ptr(), _ptr(gamma), _ptr(beta), C, float(eps), mean.data_ptr(),
+           rstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), stream())
+    return mean, rstd, scale, shift
+
+
+def bn_stats(y, M, C, ld=None):
+    partial = bn_partial_buffer(M, C, y.device)
+    L.call("avc_bn_stats", y.data_ptr(), int(C if ld is None else ld), M, C, partial.data_ptr(), stream())
+    return partial
+
+
+def bn_apply(y, scale, shift, act, residual=None, out=None):
+    M, C = y.shape
+    out = torch.empty_like(y) if out is None else out
+    L.call("avc_bn_apply", y.data_ptr(), scale.data_ptr(), shift.data_ptr(), _ptr(residual), out.data_ptr(), M, C,
+           int(act), stream())
+    return out
+
+
+def bn_bwd(dA, a, y, mean, rstd, gamma, act, need_dbias=True):
+    M, C = y.shape
+    dev = y.device
+    dy = torch.empty_like(y)
+    dgamma = torch.empty(C, device=dev)
+    dbeta = torch.empty(C, device=dev)
+    dbias = torch.empty(C, device=dev) if need_dbias else None
+    ws = torch.empty(int(L.lib().avc_bn_bwd_ws(M, C)), device=dev)
+    L.call("avc_bn_bwd", dA.data_ptr(), a.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), _ptr(gamma), M,
+           C, int(act), dy.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), _ptr(dbias), ws.data_ptr(), stream())
+    return dy, dgamma, dbeta, dbias
+
+
+def colsum(x, M, N, ld=None, out=None, accumulate=False):
+    dev = x.device
+    out = torch.empty(N, device=dev) if out is None else out
+    ws = torch.empty(int(L.lib().avc_colsum_ws(M, N)), device=dev)
+    L.call("avc_colsum", x.data_ptr(), int(N if ld is None else ld), M, N, out.data_ptr(), int(accumulate),
+           ws.data_ptr(), stream())
+    return out
+
+
+# ------------------------------------------------------------------------- LSTM
+def lstm_fwd(xproj, w_hh, B, T, H, dirs, hbuf=None):
+    dev = xproj.device
+    h = torch.empty(B * T, dirs * H, device=dev)
+    c = torch.empty(B * T, dirs * H, device=dev)
+    g = torch.empty(B * T, dirs * 4 * H, device=dev)
+    L.call("avc_lstm_fwd", xproj.data_ptr(), w_hh.data_ptr(), _dt(w_hh), B, T, H, dirs, h.data_ptr(), c.data_ptr(),
+           g.data_ptr(), _ptr(hbuf), _COMPUTE if H > 64 else F32, stream())
+    return h, c, g
+
+
+def lstm_bwd(dh, h, c, g, w_hh, w_hh_t, B, T, H, dirs):
+    dev = dh.device
+    dg = torch.empty(B * T, dirs * 4 * H, device=dev)
+    dcbuf = gbuf = None
+    wdt = _dt(w_hh if w_hh_t is None else w_hh_t)
+    if H > 64:
+        dcbuf = torch.empty(dirs * B * H, device=dev)
+        if _COMPUTE == BF16:
+            gbuf = torch.empty(2 * dirs * B * 4 * H, device=dev, dtype=torch.bfloat16)
+    L.call("avc_lstm_bwd", dh.data_ptr(), h.data_ptr(), c.data_ptr(), g.data_ptr(), _ptr(w_hh), _ptr(w_hh_t), wdt, B,
+           T, H, dirs, dg.data_ptr(), _ptr(dcbuf), _ptr(gbuf), _COMPUTE if H > 64 else F32, stream())
+    return dg
+
+
+# ------------------------------------------------------------------------- glue
+def enc_concat(mel2d, emb, B, T):
+    nm, de = mel2d.shape[1], emb.shape[1]
+    out = torch.empty(B * T, nm + de, device=mel2d.device)
+    L.call("avc_enc_concat", mel2d.data_ptr(), nm, emb.data_ptr(), out.data_ptr(), B, T, nm, de, stream())
+    return out
+
+
+def codes_gather(lo, B, T, D, freq):
+    codes = torch.empty(B, (T // freq) * 2 * D, device=lo.device)
+    L.call("avc_codes_gather", lo.data_ptr(), codes.data_ptr(), B, T, D, freq, stream())
+    return codes
+
+
+def codes_scatter(dcodes, B, T, D, freq):
+    dlo = torch.empty(B * T, 2 * D, device=dcodes.device)
+    L.call("avc_codes_scatter", dcodes.data_ptr(), dlo.data_ptr(), B, T, D, freq, stream())
+    return dlo
+
+
+def dec_concat(codes, emb, B, T, nc, cd):
+    de = emb.shape[1]
+    out = torch.empty(B * T, cd + de, device=codes.device)
+    L.call("avc_dec_concat", codes.data_ptr(), emb.data_ptr(), out.data_ptr(), B, T, nc, cd, de, stream())
+    return out
+
+
+def dec_concat_bwd(dout, B, T, nc, cd, de):
+    dcodes = torch.empty(B, nc * cd, device=dout.device)
+    L.call("avc_dec_concat_bwd", dout.data_ptr(), dcodes.data_ptr(), B, T, nc, cd, de, stream())
+    return dcodes
+
+
+# ------------------------------------------------------------------------- weights
+def conv_pack(w, mode, dtype):
+    Co, Ci, K = w.shape
+    tdt = torch.bfloat16 if dtype == BF16 else torch.float32
+    out = torch.empty(Co * Ci * K, device=w.device, dtype=tdt)
+    L.call("avc_conv_pack", w.data_ptr(), out.data_ptr(), dtype, Co, Ci, K, int(mode), stream())
+    return out.view(Co, K * Ci) if mode == 0 else out.view(Ci, K * Co)
+
+
+def conv_grad_unpack(dwf, Co, Ci, K):
+    dw = torch.empty(Co, Ci, K, device=dwf.device)
+    L.call("avc_conv_grad_unpack", dwf.data_ptr(), dw.data_ptr(), Co, Ci, K, 0, stream())
+    return dw
+
+
+def convert(src, dtype, out=None):
+    tdt = torch.bfloat16 if dtype == BF16 else torch.float32
+    out = torch.empty(src.shape, device=src.device, dtype=tdt) if out is None else out
+    L.call("avc_convert", src.data_ptr(), out.data_ptr(), dtype, src.numel(), stream())
+    return out
+
+
+def transpose(src, dtype, out=None):
+    R, C = src.shape
+    tdt = torch.bfloat16 if dtype == BF16 else torch.float32
+    out = torch.empty(C, R, device=src.device, dtype=tdt) if out is None else out
+    L.call("avc_transpose", src.data_ptr(), out.data_ptr(), dtype, R, C, stream())
+    return out
+
+
+def add(a, b, out=None):
+    out = torch.empty_like(a) if out is None else out
+    L.call("avc_add", a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), stream())
+    return out
+
+
+# ------------------------------------------------------------------------- losses / optimizer
+def mse_loss(a, b):
+    out = torch.empty((), device=a.device)
+    L.call("avc_mse_loss", a.data_ptr(), b.data_ptr(), a.numel(), out.data_ptr(), stream())
+    return out
+
+
+def l1_loss(a, b):
+    out = torch.empty((), device=a.device)
+    L.call("avc_l1_loss", a.data_ptr(), b.data_ptr(), a.numel(), out.data_ptr(), stream())
+    return out
+
+
+def loss_grad(a, b, dloss, mode, sign):
+    g = torch.empty_like(a)
+    L.call("avc_loss_grad", a.data_ptr(), b.data_ptr(), a.numel(), dloss.data_ptr(), int(mode), g.data_ptr(),
+           float(sign), stream())
+    return g
+
+
+def adam(p, g, m, v, lr, beta1, beta2, eps, state):
+    L.call("avc_adam", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), float(lr), float(beta1),
+           float(beta2), float(eps), state.data_ptr(), stream())

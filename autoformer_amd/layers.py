@@ -1,0 +1,380 @@
+"""Autograd functions of the AutoVC training path, each a sequence of HIP kernels.
+
+Activations are frame-major 2-D tensors (B*T, C) — the reference's (B, C, T) conv tensors
+transposed once at the model boundary, which for AutoVC is free because its inputs and
+outputs are already (B, T, 80) (factory/AutoVC.py:46, 208-209).
+
+Weights stay fp32 ``nn.Parameter``s in the reference layout (state_dict parity); the
+kernel-side copies (im2col-ordered conv weights, bf16 casts, transposed W_hh, stacked
+bidirectional W_ih, b_ih + b_hh) are rebuilt by HIP kernels whenever a parameter changes
+(``param._version``) or the optimizer signals an update (``weights_changed()``), i.e. once
+per training step.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import kernels as K
+from .kernels import operand
+
+_EPOCH = [0]
+
+
+def weights_changed() -> None:
+    """Call after updating parameters through raw pointers (fused Adam, DDP broadcast)."""
+    _EPOCH[0] += 1
+
+
+class PackCache:
+    __slots__ = ("key", "val")
+
+    def __init__(self):
+        self.key = None
+        self.val = None
+
+    def get(self, params, build):
+        key = (_EPOCH[0], K.compute(), tuple((p.data_ptr(), p._version) for p in params))
+        if key != self.key:
+            with torch.no_grad():
+                self.val = build()
+            self.key = key
+        return self.val
+
+
+def _need(t):
+    return t is not None and t.requires_grad
+
+
+# =============================================================================== conv + BN
+class ConvBNCore:
+    """ConvNorm (Norm.py:4-37) + BatchNorm1d + activation, frame-major.
+
+    act: K.ACT_* applied after BN (AutoVC order: conv -> BN -> act, AutoVC.py:50-51)."""
+
+    def __init__(self, conv: torch.nn.Conv1d, bn: torch.nn.BatchNorm1d, act: int):
+        self.conv, self.bn, self.act = conv, bn, act
+        self.pad = conv.padding[0]
+        self.cache = PackCache()
+
+    def packs(self):
+        w = self.conv.weight
+
+        def build():
+            dt = K.compute()
+            return K.conv_pack(w, 0, dt), K.conv_pack(w, 1, dt)
+        return self.cache.get([w], build)
+
+    def forward(self, x, B, T_in, residual=None):
+        conv, bn = self.conv, self.bn
+        Co, Ci, Kw = conv.weight.shape
+        T_out = T_in + 2 * self.pad - Kw + 1
+        M = B * T_out
+        Wf, _ = self.packs()
+        y = torch.empty(M, Co, device=x.device)
+        partial = K.bn_partial_buffer(M, Co, x.device) if bn.training else None
+        K.gemm(M, Co, Kw * Ci, operand(x, Ci, window=(Kw, self.pad, T_out, T_in, Ci)), operand(Wf, Kw * Ci), y,
+               bias=conv.bias, bn_partial=partial)
+        if bn.training:
+            nbt = bn.num_batches_tracked if bn.track_running_stats else None
+            mom = bn.momentum if bn.momentum is not None else 0.1
+            stats = K.bn_finalize(partial, M, Co, bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, mom,
+                                  bn.eps)
+        else:
+            stats = K.bn_eval(bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.eps)
+        mean, rstd, scale, shift = stats
+        a = K.bn_apply(y, scale, shift, self.act, residual)
+        return a, (y, mean, rstd, T_out)
+
+    def backward(self, dA, x, a, saved, B, T_in, n_dx):
+        y, mean, rstd, T_out = saved
+        if not self.bn.training:
+            raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
+        conv = self.conv
+        Co, Ci, Kw = conv.weight.shape
+        M = B * T_out
+        dy, dgamma, dbeta, dbias = K.bn_bwd(dA, a, y, mean, rstd, self.bn.weight, self.act)
+        dWf = torch.empty(Co, Kw * Ci, device=x.device)
+        sk = K.auto_split_k(Co, Kw * Ci, M)
+        K.gemm(Co, Kw * Ci, M, operand(dy, Co, kstrided=True),
+               operand(x, Ci, kstrided=True, window=(Kw, self.pad, T_out, T_in, Ci)), dWf, split_k=sk)
+        dW = K.conv_grad_unpack(dWf, Co, Ci, Kw)
+        dx = None
+        if n_dx:
+            _, Wd = self.packs()
+            dx = torch.empty(B * T_in, n_dx, device=x.device)
+            K.gemm(B * T_in, n_dx, Kw * Co, operand(dy, Co, window=(Kw, Kw - 1 - self.pad, T_in, T_out, Co)),
+                   operand(Wd, Kw * Co), dx)
+        return dx, dW, dbias, dgamma, dbeta
+
+
+class _ConvBNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, core, B, T_in, residual, w, b, gamma, beta):
+        a, saved = core.forward(x, B, T_in, residual)
+        ctx.core, ctx.B, ctx.T_in, ctx.saved = core, B, T_in, saved
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, a)
+        return a
+
+    @staticmethod
+    def backward(ctx, dA):
+        x, a = ctx.saved_tensors
+        dA = dA.contiguous()
+        n_dx = x.shape[1] if ctx.needs_input_grad[0] else 0
+        dx, dW, db, dg, dbe = ctx.core.backward(dA, x, a, ctx.saved, ctx.B, ctx.T_in, n_dx)
+        dres = dA if ctx.has_res and ctx.needs_input_grad[4] else None
+        return dx, None, None, None, dres, dW, db, dg, dbe
+
+
+def conv_bn(core: ConvBNCore, x, B, T_in, residual=None):
+    c, bn = core.conv, core.bn
+    return _ConvBNFn.apply(x, core, B, T_in, residual, c.weight, c.bias, bn.weight, bn.bias)
+
+
+class _EncConv0Fn(torch.autograd.Function):
+    """cat(mel, c_org broadcast) -> conv0 + BN + ReLU (AutoVC.py:46-51); dL/dmel via a
+    data-gradient GEMM restricted to the 80 mel channels."""
+
+    @staticmethod
+    def forward(ctx, mel2d, emb, core, B, T, w, b, gamma, beta):
+        if emb.requires_grad:
+            raise NotImplementedError("gradients w.r.t. the speaker embedding are not supported")
+        x = K.enc_concat(mel2d, emb, B, T)
+        a, saved = core.forward(x, B, T)
+        ctx.core, ctx.B, ctx.T, ctx.saved, ctx.n_mel = core, B, T, saved, mel2d.shape[1]
+        ctx.save_for_backward(x, a)
+        return a
+
+    @staticmethod
+    def backward(ctx, dA):
+        x, a = ctx.saved_tensors
+        n_dx = ctx.n_mel if ctx.needs_input_grad[0] else 0
+        dx, dW, db, dg, dbe = ctx.core.backward(dA.contiguous(), x, a, ctx.saved, ctx.B, ctx.T, n_dx)
+        return dx, None, None, None, None, dW, db, dg, dbe
+
+
+def enc_conv0(core, mel2d, emb, B, T):
+    c, bn = core.conv, core.bn
+    return _EncConv0Fn.apply(mel2d, emb, core, B, T, c.weight, c.bias, bn.weight, bn.bias)
+
+
+# =============================================================================== LSTM
+class LSTMLayerCore:
+    """One layer (both directions) of nn.LSTM(batch_first=True), h0 = c0 = 0."""
+
+    def __init__(self, mod, layer: int):
+        self.mod, self.layer = mod, layer
+        self.dirs = 2 if mod.bidirectional else 1
+        self.H = mod.hidden_size
+        self.cache = PackCache()
+
+    def params(self):
+        out = []
+        for sfx in (["", "_reverse"] if self.dirs == 2 else [""]):
+            for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh"):
+                out.append(getattr(self.mod, f"{n}_l{self.layer}{sfx}"))
+        return out
+
+    def packs(self):
+        ps = self.params()
+
+        def build():
+            dt = K.compute()
+            H, dirs = self.H, self.dirs
+            In = ps[0].shape[1]
+            dev = ps[0].device
+            tdt = K.compute_torch_dtype()
+            wih = torch.empty(dirs * 4 * H, In, device=dev, dtype=tdt)
+            bsum = torch.empty(dirs * 4 * H, device=dev)
+            large = H > 64
+            whh = torch.empty(dirs * 4 * H, H, device=dev, dtype=tdt if large else torch.float32)
+            whh_t = torch.empty(dirs * H, 4 * H, device=dev, dtype=tdt) if large else None
+            for d in range(dirs):
+                w_ih, w_hh, b_ih, b_hh = ps[4 * d: 4 * d + 4]
+                K.convert(w_ih, dt, out=wih[d * 4 * H:(d + 1) * 4 * H])
+                K.add(b_ih, b_hh, out=bsum[d * 4 * H:(d + 1) * 4 * H])
+                K.convert(w_hh, dt if large else K.F32, out=whh[d * 4 * H:(d + 1) * 4 * H])
+                if large:
+                    K.transpose(w_hh, dt, out=whh_t[d * H:(d + 1) * H])
+            return wih, bsum, whh, whh_t
+        return self.cache.get(ps, build)
+
+    def forward(self, x, B, T):
+        H, dirs = self.H, self.dirs
+        In = x.shape[1]
+        wih, bsum, whh, _ = self.packs()
+        xproj = torch.empty(B * T, dirs * 4 * H, device=x.device)
+        K.gemm(B * T, dirs * 4 * H, In, operand(x, In), operand(wih, In), xproj, bias=bsum)
+        hbuf = None
+        if H > 64 and K.compute() == K.BF16:
+            hbuf = torch.empty(2 * dirs * B * H, device=x.device, dtype=torch.bfloat16)
+        h, c, g = K.lstm_fwd(xproj, whh, B, T, H, dirs, hbuf)
+        return h, (c, g)
+
+    def backward(self, dh, x, h, saved, B, T, need_dx):
+        c, g = saved
+        H, dirs = self.H, self.dirs
+        In = x.shape[1]
+        wih, _, whh, whh_t = self.packs()
+        dg = K.lstm_bwd(dh, h, c, g, whh if H <= 64 else None, whh_t, B, T, H, dirs)
+        G = dirs * 4 * H
+        M = B * T
+        dwih = torch.empty(G, In, device=x.device)
+        K.gemm(G, In, M, operand(dg, G, kstrided=True), operand(x, In, kstrided=True), dwih,
+               split_k=K.auto_split_k(G, In, M))
+        db = K.colsum(dg, M, G)
+        grads = []
+        for d in range(dirs):
+            dwhh = torch.empty(4 * H, H, device=x.device)
+            shift = 1 if d == 0 else -1
+            K.gemm(4 * H, H, M, operand(dg[:, d * 4 * H:], G, kstrided=True),
+                   operand(h[:, d * H:], dirs * H, kstrided=True, window=(1, shift, T, T, H)), dwhh,
+                   split_k=K.auto_split_k(4 * H, H, M))
+            dbd = db[d * 4 * H:(d + 1) * 4 * H]
+            # b_ih and b_hh receive the same gradient but must not share storage
+            grads += [dwih[d * 4 * H:(d + 1) * 4 * H], dwhh, dbd, K.convert(dbd, K.F32)]
+        dx = None
+        if need_dx:
+            dx = torch.empty(M, In, device=x.device)
+            K.gemm(M, In, G, operand(dg, G), operand(wih, In, kstrided=True), dx)
+        return dx, grads
+
+
+class _LSTMLayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, core, B, T, *params):
+        h, saved = core.forward(x, B, T)
+        ctx.core, ctx.B, ctx.T, ctx.saved = core, B, T, saved
+        ctx.save_for_backward(x, h)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, h = ctx.saved_tensors
+        dx, grads = ctx.core.backward(dh.contiguous(), x, h, ctx.saved, ctx.B, ctx.T, ctx.needs_input_grad[0])
+        return (dx, None, None, None, *grads)
+
+
+def lstm(mod, cores, x, B, T):
+    for core in cores:
+        x = _LSTMLayerFn.apply(x, core, B, T, *core.params())
+    return x
+
+
+# =============================================================================== linear
+class _LinearFn(torch.autograd.Function):
+    """LinearNorm (Norm.py:40-50) on frame-major rows."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, cache):
+        M, In = x.shape
+        Out = w.shape[0]
+        wc = cache.get([w], lambda: K.convert(w, K.compute()))
+        y = torch.empty(M, Out, device=x.device)
+        K.gemm(M, Out, In, operand(x, In), operand(wc, In), y, bias=b)
+        ctx.cache = cache
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        M, In = x.shape
+        Out = w.shape[0]
+        dw = torch.empty(Out, In, device=x.device)
+        K.gemm(Out, In, M, operand(dy, Out, kstrided=True), operand(x, In, kstrided=True), dw,
+               split_k=K.auto_split_k(Out, In, M))
+        db = K.colsum(dy, M, Out)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wc = ctx.cache.get([w], lambda: K.convert(w, K.compute()))
+            dx = torch.empty(M, In, device=x.device)
+            K.gemm(M, In, Out, operand(dy, Out), operand(wc, In, kstrided=True), dx)
+        return dx, dw, db, None
+
+
+def linear(x, w, b, cache):
+    return _LinearFn.apply(x, w, b, cache)
+
+
+# =============================================================================== glue
+class _CodesFn(torch.autograd.Function):
+    """AutoVC.py:56-66 + torch.cat(codes, -1) (:195, :211)."""
+
+    @staticmethod
+    def forward(ctx, lo, B, T, D, freq):
+        ctx.args = (B, T, D, freq)
+        return K.codes_gather(lo, B, T, D, freq)
+
+    @staticmethod
+    def backward(ctx, dcodes):
+        B, T, D, freq = ctx.args
+        return K.codes_scatter(dcodes.contiguous(), B, T, D, freq), None, None, None, None
+
+
+def codes(lo, B, T, D, freq):
+    return _CodesFn.apply(lo, B, T, D, freq)
+
+
+class _DecConcatFn(torch.autograd.Function):
+    """Code expansion + c_trg broadcast concat (AutoVC.py:197-204)."""
+
+    @staticmethod
+    def forward(ctx, codes, emb, B, T, nc, cd):
+        if emb.requires_grad:
+            raise NotImplementedError("gradients w.r.t. the speaker embedding are not supported")
+        ctx.args = (B, T, nc, cd, emb.shape[1])
+        return K.dec_concat(codes, emb, B, T, nc, cd)
+
+    @staticmethod
+    def backward(ctx, dout):
+        B, T, nc, cd, de = ctx.args
+        return K.dec_concat_bwd(dout.contiguous(), B, T, nc, cd, de), None, None, None, None, None
+
+
+def dec_concat(codes, emb, B, T, nc, cd):
+    return _DecConcatFn.apply(codes, emb, B, T, nc, cd)
+
+
+# =============================================================================== layout
+def _transpose_batched(x, B, R, C):
+    """x viewed as B x [R][C] -> B x [C][R] (fp32)."""
+    out = torch.empty(B * C * R, device=x.device)
+    for b in range(B):
+        K.transpose(x.reshape(B, R, C)[b], K.F32, out=out[b * C * R:(b + 1) * C * R].view(C, R))
+    return out
+
+
+class _BCTToFramesFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        B, C, T = x.shape
+        ctx.shape = (B, C, T)
+        return _transpose_batched(x.contiguous(), B, C, T).view(B * T, C)
+
+    @staticmethod
+    def backward(ctx, g):
+        B, C, T = ctx.shape
+        return _transpose_batched(g.contiguous(), B, T, C).view(B, C, T)
+
+
+class _FramesToBCTFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, B, T):
+        C = x.shape[1]
+        ctx.shape = (B, C, T)
+        return _transpose_batched(x.contiguous(), B, T, C).view(B, C, T)
+
+    @staticmethod
+    def backward(ctx, g):
+        B, C, T = ctx.shape
+        return _transpose_batched(g.contiguous(), B, C, T).view(B * T, C), None, None
+
+
+def bct_to_frames(x):
+    return _BCTToFramesFn.apply(x)
+
+
+def frames_to_bct(x, B, T):
+    return _FramesToBCTFn.apply(x, B, T)

@@ -1,0 +1,168 @@
+/*
+ * autovc_hip.h — C-ABI of libautovc_hip.so, the MI355X (gfx950) kernels behind the
+ * AutoVC / MetaConv / MetaPool / Discriminator training path.
+ *
+ * The reference (achyun/Autoformer) has no native code: every op on its hot path is an
+ * implicit PyTorch -> cuDNN/cuBLAS call made by nn.Module forwards.  Each entry point
+ * below replaces one such family of implicit calls; the reference call site is cited.
+ * The Python host layer (autoformer_amd/) binds these with ctypes behind the reference's
+ * own plugin API: factory.<Model>(dim_neck, dim_emb, dim_pre, freq), forward(x, c_org,
+ * c_trg) (reference train.py:45-47, factory/AutoVC.py:185-211).
+ *
+ * Conventions
+ *   - Activations are frame-major ("channels-last"): row r = b*T + t, C contiguous.
+ *   - All device buffers are owned by the caller (PyTorch's caching allocator); the
+ *     library never allocates or frees device memory.
+ *   - Every launch goes on the hipStream_t passed as `stream`; no implicit syncs, so the
+ *     calls are hipGraph-capturable.
+ *   - Return 0 on success, a negative code on failure; avc_last_error() gives the
+ *     (thread-local) message.
+ */
+#ifndef AUTOVC_HIP_H
+#define AUTOVC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AVC_ABI_VERSION 1
+
+enum { AVC_F32 = 0, AVC_BF16 = 1 };
+enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4 };
+
+/* One GEMM operand, logically an R x K matrix (R = M for A, N for B).
+ *   kstrided = 0 : element (r, k) at ptr[r*ld + k]   (K contiguous)
+ *   kstrided = 1 : element (r, k) at ptr[k*ld + r]   (R contiguous)
+ * Frame window (taps > 0): the frame-indexed dimension (r when kstrided = 0, k when
+ * kstrided = 1) is a frame f = b*t_out + t; the other dimension is split as
+ * tap*chans + c, and the element is src[(b*t_in + t + tap - pad)*ld + c], zero when
+ * t + tap - pad is outside [0, t_in).  This expresses Conv1d im2col (taps = kernel size)
+ * and the LSTM's h_{t-1} time shift (taps = 1, pad = +-1) without materialising either.
+ * batch_stride: element offset between consecutive blockIdx.z batches (0 = shared). */
+typedef struct {
+  const void* ptr;
+  int dtype;
+  int kstrided;
+  long long ld;
+  long long batch_stride;
+  int taps, pad, t_out, t_in, chans;
+} avc_operand;
+
+/* C[z][m][n] (+)= sum_k A(m,k) B(n,k) (+ bias[n]) ; fp32 C.
+ * compute: AVC_BF16 -> bf16 MFMA 16x16x32 with fp32 accumulate; AVC_F32 -> exact fp32 MFMA.
+ * split_k > 1 accumulates with fp32 atomics (C is zeroed first unless accumulate).
+ * bn_partial (nullable, split_k == 1, batch == 1): per 128-row tile and column the
+ *   pair (sum, M2 about the tile mean) of the stored values, layout [ceil(M/128)][N][2],
+ *   the BatchNorm batch-statistics epilogue.  */
+typedef struct {
+  int M, N, K, batch;
+  avc_operand a, b;
+  float* c;
+  long long ldc, c_batch_stride;
+  const float* bias;
+  int accumulate;
+  int split_k;
+  float* bn_partial;
+  int compute;
+} avc_gemm_desc;
+
+int avc_abi_version(void);
+const char* avc_last_error(void);
+
+/* Conv1d / Linear / LSTM-projection / weight-gradient GEMMs.
+ * Replaces: nn.Conv1d (factory/Norm.py:21-28 via AutoVC.py:26-41, 79-94, 125-171,
+ * Discriminator.py:7-9, MLPMixer.py:53,82), nn.Linear (Norm.py:40-50, MLPMixer.py:70-76),
+ * the W_ih products inside nn.LSTM (AutoVC.py:43,77,96) and all their backward GEMMs. */
+int avc_gemm(const avc_gemm_desc* d, void* stream);
+
+/* BatchNorm1d training-mode statistics from avc_gemm's bn_partial: mean/rstd per
+ * channel, scale = gamma*rstd, shift = beta - mean*scale, running-stat update with
+ * momentum and UNBIASED variance, num_batches_tracked += 1.
+ * Replaces nn.BatchNorm1d.forward (train mode) at AutoVC.py:38,91,138,154,169. */
+int avc_bn_finalize(const float* partial, int M, int C, const float* gamma, const float* beta,
+                    float* running_mean, float* running_var, long long* num_batches_tracked,
+                    float momentum, float eps, float* mean, float* rstd, float* scale, float* shift,
+                    void* stream);
+
+/* Eval-mode coefficients from the running statistics (nn.BatchNorm1d in .eval()). */
+int avc_bn_eval(const float* running_mean, const float* running_var, const float* gamma, const float* beta, int C,
+                float eps, float* mean, float* rstd, float* scale, float* shift, void* stream);
+
+/* Per-channel statistics pass for inputs that did not come out of avc_gemm (ld >= C). */
+int avc_bn_stats(const float* y, long long ld, int M, int C, float* partial, void* stream);
+
+/* out[r][c] = act(y[r][c]*scale[c] + shift[c]) (+ residual[r][c]); rows of length C. */
+int avc_bn_apply(const float* y, const float* scale, const float* shift, const float* residual,
+                 float* out, int M, int C, int act, void* stream);
+
+/* BatchNorm1d + activation backward.  dz = dA * act'(a); yhat = (y-mean)*rstd.
+ * Writes dy = gamma*rstd*(dz - sum(dz)/N - yhat*sum(dz*yhat)/N), and dgamma, dbeta and
+ * the (analytically ~0) bias gradient of the producing conv.  `ws` >= avc_bn_bwd_ws floats. */
+size_t avc_bn_bwd_ws(int M, int C);
+int avc_bn_bwd(const float* dA, const float* a, const float* y, const float* mean, const float* rstd,
+               const float* gamma, int M, int C, int act, float* dy, float* dgamma, float* dbeta,
+               float* dbias, float* ws, void* stream);
+
+/* out[n] (+)= sum_m x[m*ld + n] (bias gradients). ws >= avc_colsum_ws floats. */
+size_t avc_colsum_ws(int M, int N);
+int avc_colsum(const float* x, long long ld, int M, int N, float* out, int accumulate, float* ws,
+               void* stream);
+
+/* LSTM layer recurrence (both directions of a bidirectional layer in one call).
+ * Replaces the time loop of nn.LSTM (AutoVC.py:43,55 encoder BiLSTM; :77,103 lstm1;
+ * :96,110 lstm2).  xproj (B,T,dirs*4H) already holds x W_ih^T + b_ih + b_hh.
+ * w_hh: dirs x [4H][H] in `wdtype`; outputs h (B,T,dirs*H) fp32, c (B,T,dirs*H),
+ * gates (B,T,dirs*4H) activated.  hbuf: 2*B*H elements of wdtype scratch (large H). */
+int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T, int H, int dirs,
+                 float* h, float* c, float* gates, void* hbuf, int compute, void* stream);
+
+/* Backward recurrence.  dh_out (B,T,dirs*H) = dL/dh; writes dgates (B,T,dirs*4H)
+ * (pre-activation).  w_hh_t: dirs x [H][4H] transposed copy (large H) or w_hh itself
+ * (small H, pass the same layout as avc_lstm_fwd). dcbuf: B*H*dirs fp32, gbuf: 2*B*4H*dirs wdtype. */
+int avc_lstm_bwd(const float* dh_out, const float* h, const float* c, const float* gates,
+                 const void* w_hh, const void* w_hh_t, int wdtype, int B, int T, int H, int dirs,
+                 float* dgates, float* dcbuf, void* gbuf, int compute, void* stream);
+
+/* Elementwise / layout kernels of the model glue (AutoVC.py:46-48, 56-66, 197-207). */
+int avc_enc_concat(const float* mel, long long mel_ld, const float* emb, float* out, int B, int T,
+                   int n_mel, int d_emb, void* stream);
+int avc_codes_gather(const float* lstm_out, float* codes, int B, int T, int dim_neck, int freq,
+                     void* stream);
+int avc_codes_scatter(const float* dcodes, float* dlstm_out, int B, int T, int dim_neck, int freq,
+                      void* stream);
+int avc_dec_concat(const float* codes, const float* emb, float* out, int B, int T, int n_codes,
+                   int code_dim, int d_emb, void* stream);
+int avc_dec_concat_bwd(const float* dout, float* dcodes, int B, int T, int n_codes, int code_dim,
+                       int d_emb, void* stream);
+
+/* Weight repacks (and fp32 -> compute dtype).  conv: W[co][ci][k] ->
+ *   mode 0: Wf[co][k][ci] (forward im2col order)
+ *   mode 1: Wd[ci][k'][co] with k' = K-1-k (data-gradient order)
+ * grad_unpack: dWf[co][k][ci] -> dW[co][ci][k] (accumulate optional). */
+int avc_conv_pack(const float* w, void* out, int dtype, int Cout, int Cin, int Kw, int mode, void* stream);
+int avc_conv_grad_unpack(const float* dwf, float* dw, int Cout, int Cin, int Kw, int accumulate, void* stream);
+/* dst = convert(src) (n elements), and optional transpose of a [R][C] matrix. */
+int avc_convert(const float* src, void* dst, int dtype, long long n, void* stream);
+int avc_transpose(const float* src, void* dst, int dtype, int R, int C, void* stream);
+/* out = a + b elementwise (n), e.g. b_ih + b_hh. */
+int avc_add(const float* a, const float* b, float* out, long long n, void* stream);
+
+/* Losses of Solver.train (train.py:85-86, 94) and their gradients. */
+int avc_mse_loss(const float* a, const float* b, long long n, float* out, void* stream);
+int avc_l1_loss(const float* a, const float* b, long long n, float* out, void* stream);
+/* g = scale * dL * (mode 0: 2(a-b)/n ; mode 1: sign(a-b)/n) ; dL = *dloss (device) */
+int avc_loss_grad(const float* a, const float* b, long long n, const float* dloss, int mode, float* g,
+                  float sign, void* stream);
+
+/* Fused Adam (torch.optim.Adam defaults, train.py:49,99) over one flat fp32 buffer.
+ * state[0] = step count (float), updated on device (graph-replayable). */
+int avc_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
+             float beta2, float eps, float* state, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,95 @@
+"""CPU-side checks of the C-ABI library: it loads and exports every symbol the header declares
+(no compute calls — there is no GPU here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from .conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "autovc_hip.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(avc_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from autoformer_amd import _lib
+
+    if not os.path.exists(_lib.LIB_PATH):
+        _lib.build()
+    return _lib.lib()
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    assert "avc_gemm" in syms and "avc_lstm_fwd" in syms and len(syms) >= 25
+
+
+def test_library_exports_every_declared_symbol(lib):
+    so = ctypes.CDLL(os.path.join(ROOT, "autoformer_amd", "libautovc_hip.so"))
+    missing = [s for s in declared_symbols() if not hasattr(so, s)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_header(lib):
+    from autoformer_amd import _lib
+
+    assert set(_lib.exported_symbols()) == set(declared_symbols())
+
+
+def test_abi_version_and_error_channel(lib):
+    assert lib.avc_abi_version() == 1
+    assert isinstance(lib.avc_last_error(), bytes)
+
+
+def test_argument_validation_without_gpu(lib):
+    from autoformer_amd import _lib
+
+    # null descriptor is rejected on the host before any launch
+    rc = lib.avc_gemm(None, None)
+    assert rc != 0
+    assert b"null" in lib.avc_last_error()
+    with pytest.raises(RuntimeError):
+        _lib.check(rc, "avc_gemm")
+
+
+def test_struct_layout_matches_header():
+    from autoformer_amd import _lib
+
+    # avc_operand: ptr(8) int int ll ll int*5 (+pad) -> 56 bytes on x86-64
+    assert ctypes.sizeof(_lib.Operand) == 56
+    assert ctypes.sizeof(_lib.GemmDesc) == 4 * 4 + 2 * 56 + 8 + 8 + 8 + 8 + 4 + 4 + 8 + 4 + 4
+
+
+def test_product_path_does_not_import_oracle():
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "autoformer_amd")):
+        for f in files:
+            if f.endswith(".py"):
+                txt = open(os.path.join(dirpath, f)).read()
+                assert "import oracle" not in txt and "from oracle" not in txt, f
+
+
+def test_factory_state_dict_layout_matches_reference():
+    import json
+
+    import factory.AutoVC as A
+
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "state_dict_layout.json")))
+    m = A.AutoVC(44, 256, 512, 22)
+    assert [[k, list(v.shape)] for k, v in m.state_dict().items()] == ref["AutoVC"]
+
+
+def test_ops_refuse_cpu_tensors(lib):
+    import torch
+
+    import factory.AutoVC as A
+
+    m = A.AutoVC(44, 256, 512, 22)
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(2, 176, 80), torch.zeros(2, 256), torch.zeros(2, 256))

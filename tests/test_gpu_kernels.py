@@ -1,0 +1,278 @@
+"""Per-kernel numerics on the MI355X, through the C-ABI, against plain PyTorch fp32
+references of the same op (computed on the CPU).
+
+Tolerances: fp32 compute (exact fp32 MFMA) -> rel <= 1e-5 (GEMM) / 1e-4 (recurrences);
+bf16 compute -> rel-Frobenius <= 1.5e-2.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(autouse=True)
+def _fp32():
+    import autoformer_amd as A
+
+    A.set_compute("fp32")
+    torch.manual_seed(0)
+    yield
+    A.set_compute("fp32")
+
+
+def relf(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return float((a - b).norm() / max(b.norm().item(), 1e-30))
+
+
+def rinf(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return float((a - b).abs().max() / max(b.abs().max().item(), 1e-30))
+
+
+def _gemm_ref(A_, B_):  # A (M,K) B (N,K)
+    return A_.double() @ B_.double().t()
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 200, 96), (128, 128, 32), (7, 9, 20), (1000, 80, 400)])
+@pytest.mark.parametrize("comp", ["fp32", "bf16"])
+def test_gemm_plain_all_layouts(M, N, K, comp):
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute(comp)
+    a = torch.randn(M, K)
+    b = torch.randn(N, K)
+    ref = _gemm_ref(a, b)
+    tol = 1e-5 if comp == "fp32" else 1.5e-2
+    for aks in (False, True):
+        for bks in (False, True):
+            ad = (a.t().contiguous() if aks else a).to(DEV)
+            bd = (b.t().contiguous() if bks else b).to(DEV)
+            c = torch.empty(M, N, device=DEV)
+            Kr.gemm(M, N, K, Kr.operand(ad, M if aks else K, kstrided=aks), Kr.operand(bd, N if bks else K, kstrided=bks), c)
+            assert relf(c, ref) < tol, (aks, bks, relf(c, ref))
+
+
+def test_gemm_bias_accumulate_splitk_batch():
+    from autoformer_amd import kernels as Kr
+
+    M, N, K = 256, 192, 4096
+    a, b, bias = torch.randn(M, K), torch.randn(N, K), torch.randn(N)
+    ref = _gemm_ref(a, b) + bias.double()
+    ad, bd = a.to(DEV), b.to(DEV)
+    for sk in (1, 4):
+        c = torch.empty(M, N, device=DEV)
+        Kr.gemm(M, N, K, Kr.operand(ad, K), Kr.operand(bd, K), c, bias=bias.to(DEV), split_k=sk)
+        assert relf(c, ref) < 1e-5
+    c0 = torch.randn(M, N)
+    c = c0.to(DEV)
+    Kr.gemm(M, N, K, Kr.operand(ad, K), Kr.operand(bd, K), c, accumulate=True, split_k=3)
+    assert relf(c, ref - bias.double() + c0.double()) < 1e-5
+    # batched: 3 independent products with per-batch A and C strides, shared B
+    Bn = 3
+    a3 = torch.randn(Bn, 64, 48)
+    c3 = torch.empty(Bn, 64, 40, device=DEV)
+    b3 = torch.randn(40, 48)
+    Kr.gemm(64, 40, 48, Kr.operand(a3.to(DEV), 48, batch_stride=64 * 48), Kr.operand(b3.to(DEV), 48), c3, batch=Bn,
+            c_batch_stride=64 * 40)
+    assert relf(c3, torch.einsum("bmk,nk->bmn", a3.double(), b3.double())) < 1e-5
+
+
+@pytest.mark.parametrize("B,T,Cin,Cout,Kw,pad", [(2, 176, 336, 512, 5, 2), (3, 37, 80, 96, 5, 2), (2, 80, 176, 88, 3, 0),
+                                                  (2, 30, 44, 22, 3, 0)])
+@pytest.mark.parametrize("comp", ["fp32", "bf16"])
+def test_conv_gemm_fwd_dgrad_wgrad(B, T, Cin, Cout, Kw, pad, comp):
+    """Conv1d as a windowed GEMM: forward, data- and weight-gradient vs F.conv1d autograd."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute(comp)
+    tol = 1e-5 if comp == "fp32" else 1.5e-2
+    x = torch.randn(B, Cin, T, requires_grad=True)
+    w = torch.randn(Cout, Cin, Kw, requires_grad=True) * 0.1
+    w.retain_grad()
+    y = F.conv1d(x, w, padding=pad)
+    To = y.shape[-1]
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    dt = Kr.BF16 if comp == "bf16" else Kr.F32
+    xf = x.detach().transpose(1, 2).reshape(B * T, Cin).contiguous().to(DEV)
+    wd = w.detach().to(DEV)
+    Wf = Kr.conv_pack(wd, 0, dt)
+    Wd = Kr.conv_pack(wd, 1, dt)
+    out = torch.empty(B * To, Cout, device=DEV)
+    Kr.gemm(B * To, Cout, Kw * Cin, Kr.operand(xf, Cin, window=(Kw, pad, To, T, Cin)), Kr.operand(Wf, Kw * Cin), out)
+    assert relf(out, y.detach().transpose(1, 2).reshape(B * To, Cout)) < tol
+    gyf = gy.transpose(1, 2).reshape(B * To, Cout).contiguous().to(DEV)
+    dx = torch.empty(B * T, Cin, device=DEV)
+    Kr.gemm(B * T, Cin, Kw * Cout, Kr.operand(gyf, Cout, window=(Kw, Kw - 1 - pad, T, To, Cout)),
+            Kr.operand(Wd, Kw * Cout), dx)
+    assert relf(dx, x.grad.transpose(1, 2).reshape(B * T, Cin)) < tol
+    dwf = torch.empty(Cout, Kw * Cin, device=DEV)
+    Kr.gemm(Cout, Kw * Cin, B * To, Kr.operand(gyf, Cout, kstrided=True),
+            Kr.operand(xf, Cin, kstrided=True, window=(Kw, pad, To, T, Cin)), dwf, split_k=2)
+    dw = Kr.conv_grad_unpack(dwf, Cout, Cin, Kw)
+    assert relf(dw, w.grad) < tol
+
+
+def test_gemm_time_shift_window():
+    """k-strided frame window with taps=1 (the LSTM h_{t-1} / h_{t+1} shift)."""
+    from autoformer_amd import kernels as Kr
+
+    B, T, H, G = 3, 20, 44, 176
+    dg = torch.randn(B * T, G)
+    h = torch.randn(B, T, H)
+    for shift, ref_h in ((1, torch.cat([torch.zeros(B, 1, H), h[:, :-1]], 1)),
+                         (-1, torch.cat([h[:, 1:], torch.zeros(B, 1, H)], 1))):
+        out = torch.empty(G, H, device=DEV)
+        Kr.gemm(G, H, B * T, Kr.operand(dg.to(DEV), G, kstrided=True),
+                Kr.operand(h.reshape(B * T, H).to(DEV), H, kstrided=True, window=(1, shift, T, T, H)), out)
+        ref = dg.double().t() @ ref_h.reshape(B * T, H).double()
+        assert relf(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("M,C", [(8192, 512), (352, 80), (300, 176)])
+def test_bn_stats_epilogue_and_finalize(M, C):
+    from autoformer_amd import kernels as Kr
+
+    x = torch.randn(M, 64) * 3
+    w = torch.randn(C, 64)
+    y = x.double() @ w.double().t() + 5.0  # large mean: checks the centred (Chan) merge
+    bias = torch.full((C,), 5.0)
+    yd = torch.empty(M, C, device=DEV)
+    part = Kr.bn_partial_buffer(M, C, DEV)
+    Kr.gemm(M, C, 64, Kr.operand(x.to(DEV), 64), Kr.operand(w.to(DEV), 64), yd, bias=bias.to(DEV), bn_partial=part)
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C)
+    rm, rv, nbt = torch.randn(C).to(DEV), (torch.rand(C) + 0.5).to(DEV), torch.zeros((), dtype=torch.long, device=DEV)
+    rm0, rv0 = rm.cpu().double(), rv.cpu().double()
+    mean, rstd, scale, shift = Kr.bn_finalize(part, M, C, gamma.to(DEV), beta.to(DEV), rm, rv, nbt, 0.1, 1e-5)
+    m_ref = y.mean(0)
+    v_ref = y.var(0, unbiased=False)
+    assert rinf(mean, m_ref) < 1e-5
+    assert rinf(rstd, 1 / torch.sqrt(v_ref + 1e-5)) < 1e-4
+    assert rinf(rm, 0.9 * rm0 + 0.1 * m_ref) < 1e-5
+    assert rinf(rv, 0.9 * rv0 + 0.1 * y.var(0, unbiased=True)) < 1e-4
+    assert int(nbt.item()) == 1
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_bn_act_forward_backward(act):
+    from autoformer_amd import kernels as Kr
+
+    M, C = 1000, 96
+    y = torch.randn(M, C) * 2 + 1
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C)
+    yt = y.clone().requires_grad_(True)
+    g_t = gamma.clone().requires_grad_(True)
+    b_t = beta.clone().requires_grad_(True)
+    z = F.batch_norm(yt.t().unsqueeze(0), None, None, g_t, b_t, True, 0.1, 1e-5).squeeze(0).t()
+    a_ref = [z, torch.relu(z), torch.tanh(z)][act]
+    dA = torch.randn(M, C)
+    a_ref.backward(dA)
+    yd = y.to(DEV)
+    part = Kr.bn_stats(yd, M, C)
+    mean, rstd, scale, shift = Kr.bn_finalize(part, M, C, gamma.to(DEV), beta.to(DEV), None, None, None, 0.1, 1e-5)
+    a = Kr.bn_apply(yd, scale, shift, act)
+    assert rinf(a, a_ref.detach()) < 1e-5
+    dy, dgam, dbet, dbias = Kr.bn_bwd(dA.to(DEV), a, yd, mean, rstd, gamma.to(DEV), act)
+    assert relf(dy, yt.grad) < 1e-4
+    assert relf(dgam, g_t.grad) < 1e-5
+    assert relf(dbet, b_t.grad) < 1e-5
+    assert float(dbias.abs().max()) < 1e-3
+
+
+def _lstm_case(B, T, In, H, dirs, comp):
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+    from autoformer_amd.factory.Norm import LSTMParams
+    from autoformer_amd.layers import LSTMLayerCore, lstm
+
+    A.set_compute(comp)
+    mod = LSTMParams(In, H, 1, bidirectional=dirs == 2)
+    x = torch.randn(B, T, In)
+    ref_mod = torch.nn.LSTM(In, H, 1, batch_first=True, bidirectional=dirs == 2)
+    ref_mod.load_state_dict(mod.state_dict())
+    xr = x.clone().requires_grad_(True)
+    out_ref, _ = ref_mod(xr)
+    gy = torch.randn_like(out_ref)
+    out_ref.backward(gy)
+    mod = mod.to(DEV)
+    xd = x.reshape(B * T, In).to(DEV).requires_grad_(True)
+    core = LSTMLayerCore(mod, 0)
+    out = lstm(mod, [core], xd, B, T)
+    out.backward(gy.reshape(B * T, -1).to(DEV))
+    torch.cuda.synchronize()
+    res = {"out": relf(out.detach(), out_ref.detach().reshape(B * T, -1)),
+           "dx": relf(xd.grad, xr.grad.reshape(B * T, In))}
+    for (n, p), (n2, p2) in zip(mod.named_parameters(), ref_mod.named_parameters()):
+        assert n == n2
+        res[n] = relf(p.grad, p2.grad)
+    return res
+
+
+@pytest.mark.parametrize("B,T,In,H,dirs", [(4, 33, 512, 44, 2), (3, 20, 88, 44, 2), (5, 17, 344, 512, 1),
+                                           (20, 9, 512, 1024, 1), (2, 12, 96, 128, 2)])
+def test_lstm_layer_fp32(B, T, In, H, dirs):
+    res = _lstm_case(B, T, In, H, dirs, "fp32")
+    bad = {k: v for k, v in res.items() if v > 1e-4}
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("B,T,In,H,dirs", [(4, 33, 512, 44, 2), (20, 16, 512, 1024, 1), (64, 8, 344, 512, 1)])
+def test_lstm_layer_bf16(B, T, In, H, dirs):
+    res = _lstm_case(B, T, In, H, dirs, "bf16")
+    bad = {k: v for k, v in res.items() if v > 3e-2}
+    assert not bad, bad
+
+
+def test_glue_kernels():
+    from autoformer_amd import kernels as Kr
+
+    B, T, D, freq = 3, 32, 44, 8
+    lo = torch.randn(B, T, 2 * D)
+    codes = Kr.codes_gather(lo.reshape(B * T, 2 * D).to(DEV), B, T, D, freq)
+    ref = torch.cat([torch.cat((lo[:, i + freq - 1, :D], lo[:, i, D:]), -1) for i in range(0, T, freq)], -1)
+    assert rinf(codes, ref) == 0.0
+    dc = torch.randn(B, (T // freq) * 2 * D)
+    lo_r = lo.clone().requires_grad_(True)
+    ref2 = torch.cat([torch.cat((lo_r[:, i + freq - 1, :D], lo_r[:, i, D:]), -1) for i in range(0, T, freq)], -1)
+    ref2.backward(dc)
+    dlo = Kr.codes_scatter(dc.to(DEV), B, T, D, freq)
+    assert rinf(dlo, lo_r.grad.reshape(B * T, 2 * D)) == 0.0
+    emb = torch.randn(B, 256)
+    out = Kr.dec_concat(codes, emb.to(DEV), B, T, T // freq, 2 * D)
+    cl = list(ref.split(2 * D, -1))
+    ref3 = torch.cat((torch.cat([c.unsqueeze(1).expand(-1, freq, -1) for c in cl], 1),
+                      emb.unsqueeze(1).expand(-1, T, -1)), -1)
+    assert rinf(out, ref3.reshape(B * T, -1)) == 0.0
+    mel = torch.randn(B, T, 80)
+    xc = Kr.enc_concat(mel.reshape(B * T, 80).to(DEV), emb.to(DEV), B, T)
+    assert rinf(xc, torch.cat((mel, emb.unsqueeze(1).expand(-1, T, -1)), -1).reshape(B * T, -1)) == 0.0
+
+
+def test_losses_and_adam():
+    from autoformer_amd import kernels as Kr
+
+    a, b = torch.randn(5000), torch.randn(5000)
+    ad, bd = a.to(DEV), b.to(DEV)
+    assert abs(Kr.mse_loss(ad, bd).item() - F.mse_loss(a, b).item()) < 1e-5
+    assert abs(Kr.l1_loss(ad, bd).item() - F.l1_loss(a, b).item()) < 1e-5
+    # Adam vs torch.optim.Adam for 3 steps
+    p = torch.randn(1000)
+    pt = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pt], 1e-3)
+    pd, m, v = p.to(DEV), torch.zeros(1000, device=DEV), torch.zeros(1000, device=DEV)
+    st = torch.zeros(4, device=DEV)
+    for i in range(3):
+        g = torch.randn(1000)
+        pt.grad = g.clone()
+        opt.step()
+        Kr.adam(pd, g.to(DEV), m, v, 1e-3, 0.9, 0.999, 1e-8, st)
+    assert rinf(pd, pt.detach()) < 1e-6

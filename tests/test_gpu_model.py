@@ -1,0 +1,131 @@
+"""Whole-model parity on the MI355X: the HIP AutoVC against the reference goldens
+(tests/golden, generated from /root/reference) and the CPU oracle.
+
+Bars: fp32 mel_postnet rel-inf <= 1e-3 (north star); losses rel <= 1e-4;
+grads rel-Frobenius <= 1e-2 per tensor with an absolute floor of 1e-6 for the conv biases
+that feed a BatchNorm (analytically zero gradient); bf16 mode loose (rel-inf <= 5e-2).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def rel_inf(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+def _model(freq, comp="fp32"):
+    import autoformer_amd as A
+    from autoformer_amd.detinit import det_init_
+    from factory.AutoVC import AutoVC
+
+    A.set_compute(comp)
+    m = AutoVC(44, 256, 512, freq)
+    det_init_(m)
+    return m.to(DEV).train()
+
+
+def _step(m, x, e):
+    x_id, x_psnt, code = m(x, e, e)
+    l1 = F.mse_loss(x, x_id.squeeze())
+    l2 = F.mse_loss(x, x_psnt.squeeze())
+    code_re = m(x_psnt, e, None)
+    l3 = F.l1_loss(code, code_re)
+    return (x_id, x_psnt, code, code_re), (l1, l2, l3), l1 + l2 + l3
+
+
+@pytest.mark.parametrize("fname", ["autovc_T176.npz", "autovc_T128.npz"])
+def test_autovc_fp32_matches_reference_goldens(golden, fname):
+    g = golden(fname)
+    m = _model(int(g["freq"]))
+    x, e = torch.from_numpy(g["x"]).to(DEV), torch.from_numpy(g["emb"]).to(DEV)
+    outs, losses, total = _step(m, x, e)
+    m.zero_grad()
+    total.backward()
+    torch.cuda.synchronize()
+    assert rel_inf(outs[1].detach().cpu(), g["mel_psnt"]) < 1e-3
+    assert rel_inf(outs[0].detach().cpu(), g["mel"]) < 1e-3
+    assert rel_inf(outs[2].detach().cpu(), g["codes"]) < 1e-3
+    assert rel_inf(outs[3].detach().cpu(), g["codes_re"]) < 1e-3
+    np.testing.assert_allclose([l.item() for l in losses], g["losses"], rtol=1e-4)
+    bad = {}
+    for name, p in m.named_parameters():
+        ref_n = float(g["gnorm/" + name])
+        got = p.grad.detach().cpu().double()
+        head = g["ghead/" + name].astype(np.float64)
+        err = np.abs(got.reshape(-1)[:64].numpy() - head).max()
+        if "conv.bias" in name and "postnet.convolutions.4" not in name:
+            ok = err < 1e-6 + 1e-2 * np.abs(head).max()
+        else:
+            ok = abs(got.norm().item() - ref_n) <= 1e-2 * ref_n + 1e-6 and err <= 1e-2 * max(np.abs(head).max(), 1e-6)
+        if not ok:
+            bad[name] = (got.norm().item(), ref_n, err)
+    assert not bad, bad
+    for k, v in m.state_dict().items():
+        if "running_" in k or "num_batches" in k:
+            np.testing.assert_allclose(v.detach().cpu().numpy(), g["bn/" + k], rtol=1e-4, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("fname", ["autovc_T176.npz", "autovc_T128.npz"])
+def test_autovc_three_adam_steps_match_reference_solver(golden, fname):
+    """train.py Solver semantics (train.py:82-99) with torch.optim.Adam over the HIP model."""
+    g = golden(fname)
+    m = _model(int(g["freq"]))
+    opt = torch.optim.Adam(m.parameters(), 1e-4)
+    got = []
+    for i in range(3):
+        x = torch.from_numpy(g[f"adam_x{i}"]).to(DEV)
+        e = torch.from_numpy(g[f"adam_e{i}"]).to(DEV)
+        _, losses, total = _step(m, x, e)
+        opt.zero_grad()
+        total.backward()
+        opt.step()
+        got.append([l.item() for l in losses])
+    np.testing.assert_allclose(np.array(got), g["adam_losses"], rtol=2e-3)
+
+
+def test_autovc_bf16_loose(golden):
+    g = golden("autovc_T128.npz")
+    m = _model(int(g["freq"]), "bf16")
+    x, e = torch.from_numpy(g["x"]).to(DEV), torch.from_numpy(g["emb"]).to(DEV)
+    outs, losses, total = _step(m, x, e)
+    total.backward()
+    torch.cuda.synchronize()
+    assert rel_inf(outs[1].detach().cpu(), g["mel_psnt"]) < 5e-2
+    np.testing.assert_allclose([l.item() for l in losses], g["losses"], rtol=5e-2)
+    for p in m.parameters():
+        assert torch.isfinite(p.grad).all()
+
+
+def test_autovc_vs_oracle_batch8():
+    """Larger batch than the goldens, against the CPU oracle on identical weights/inputs."""
+    from autoformer_amd.detinit import det_inputs
+    from oracle import autovc_cpu as O
+
+    B, T, freq = 8, 64, 16
+    x, e = det_inputs(B, T, seed=9)
+    xt, et = torch.from_numpy(x), torch.from_numpy(e)
+    sd = O.make_state(O.autovc_spec())
+    losses_ref, total_ref, outs_ref = O.step_losses(lambda a, b, c: O.autovc_forward(sd, a, b, c, freq=freq), xt, et)
+    m = _model(freq)
+    outs, losses, total = _step(m, xt.to(DEV), et.to(DEV))
+    assert rel_inf(outs[1].detach().cpu(), outs_ref[1].detach()) < 1e-3
+    np.testing.assert_allclose([l.item() for l in losses], [l.item() for l in losses_ref], rtol=1e-4)
+
+
+def test_encoder_list_api_and_eval_mode(golden):
+    g = golden("autovc_T176.npz")
+    m = _model(22)
+    x, e = torch.from_numpy(g["x"]).to(DEV), torch.from_numpy(g["emb"]).to(DEV)
+    codes = m.encoder(x, e)
+    assert isinstance(codes, list) and len(codes) == 8 and codes[0].shape == (2, 88)
+    m.eval()
+    with torch.no_grad():
+        mel, psnt, c = m(x, e, e)
+    assert torch.isfinite(psnt).all()
