@@ -58,6 +58,7 @@ def operand(t: torch.Tensor, ld: int, kstrided: bool = False, window=None, batch
     """window = (taps, pad, t_out, t_in, chans) or None."""
     _dev(t)
     o = L.Operand()
+    o._keep = t  # the descriptor holds a raw pointer: keep the tensor alive until launch
     o.ptr = t.data_ptr()
     o.dtype = _dt(t)
     o.kstrided = int(kstrided)
