@@ -33,7 +33,8 @@ class Operand(ctypes.Structure):
 class GemmDesc(ctypes.Structure):
     _fields_ = [("M", c_int), ("N", c_int), ("K", c_int), ("batch", c_int), ("a", Operand), ("b", Operand),
                 ("c", c_void_p), ("ldc", c_ll), ("c_batch_stride", c_ll), ("bias", c_void_p),
-                ("accumulate", c_int), ("split_k", c_int), ("bn_partial", c_void_p), ("compute", c_int)]
+                ("accumulate", c_int), ("split_k", c_int), ("bn_partial", c_void_p), ("compute", c_int),
+                ("c_bf16", c_void_p)]
 
 
 _SIGS = {

@@ -27,6 +27,7 @@ struct GemmArgs {
   int M, N, K, batch, split_k, klen;
   OpDev a, b;
   float* c;
+  bf16* c16;
   long long ldc, cbs;
   const float* bias;
   int accumulate, atomic;
@@ -218,7 +219,7 @@ struct Loader {
 };
 
 template <bool BF, bool AKS, bool BKS>
-__global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
+__global__ void __launch_bounds__(NT) gemm_generic_kernel(GemmArgs g) {
   typedef typename Traits<BF>::T T;
   constexpr int LDK = Traits<BF>::LDK;
   constexpr int TILE = (BM + BN) * LDK;
@@ -427,6 +428,365 @@ int make_op(const avc_operand& o, int rows, int K, OpDev& d, const char* name) {
   return 0;
 }
 
+
+// ============================================================================ fast path
+// bf16 MFMA, operands whose contiguous dimension is a multiple of 4 elements.  Loads are
+// raw buffer loads: a padding / out-of-range element gets an offset past num_records and
+// the hardware returns zeros, so the loader has no branches and all loads of a K-tile are
+// in flight together (the generic kernel above serialises them behind exec-masked
+// branches).  BK = 64, 2 LDS stages, 2 workgroups per CU, XCD-aware tile order.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+constexpr int FBK = 64, FLDK = FBK + 8;  // 144-byte LDS rows
+constexpr unsigned FINVALID = 0x7FFFFFF0u;
+
+__device__ __forceinline__ unsigned pk2(float a, float b) {
+  bf16x2 h = {(bf16)a, (bf16)b};
+  return __builtin_bit_cast(unsigned, h);
+}
+__device__ __forceinline__ unsigned short lo16(unsigned x) { return (unsigned short)(x & 0xFFFFu); }
+__device__ __forceinline__ unsigned short hi16(unsigned x) { return (unsigned short)(x >> 16); }
+__device__ __forceinline__ unsigned join16(unsigned short a, unsigned short b) { return (unsigned)a | ((unsigned)b << 16); }
+
+template <int DT>
+struct RawT;
+template <>
+struct RawT<AVC_BF16> {
+  typedef u32x2 T;
+  static constexpr int ES = 2;
+  static __device__ __forceinline__ T load(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+  }
+  // 4 elements as two packed bf16 pairs
+  static __device__ __forceinline__ u32x2 pack(T v) { return v; }
+};
+template <>
+struct RawT<AVC_F32> {
+  typedef u32x4 T;
+  static constexpr int ES = 4;
+  static __device__ __forceinline__ T load(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  }
+  static __device__ __forceinline__ u32x2 pack(T v) {
+    return u32x2{pk2(__uint_as_float(v[0]), __uint_as_float(v[1])), pk2(__uint_as_float(v[2]), __uint_as_float(v[3]))};
+  }
+};
+
+template <int R, bool KS, int DT>
+struct FLoader {
+  static constexpr int NV = R * FBK / 1024;  // 4-element vectors per thread per K-tile
+  static constexpr int NB = NV / 4;          // k-strided: 4x4 blocks per thread
+  typedef typename RawT<DT>::T Raw;
+  Raw raw[NV];
+  __amdgpu_buffer_rsrc_t rsrc;
+  // k-major state
+  int frame[NV], tt[NV], rok[NV], kq;
+  // k-strided state
+  int rq[NB > 0 ? NB : 1], kb[NB > 0 ? NB : 1], tap, c, rowok;
+
+  __device__ __forceinline__ void init(const OpDev& o, int row0, int tid, long long boff) {
+    const char* base = reinterpret_cast<const char*>(o.ptr) + boff * RawT<DT>::ES;
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, (int)FINVALID, 0x00020000);
+    if constexpr (!KS) {
+      kq = (tid & 15) * 4;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int r = row0 + (tid >> 4) + 16 * i;
+        rok[i] = r < o.rows;
+        if (o.win) {
+          const int b = (int)fdiv((uint32_t)r, o.tdiv);
+          tt[i] = r - b * o.t_out;
+          frame[i] = b * o.t_in + tt[i];
+        } else {
+          tt[i] = 0;
+          frame[i] = r;
+        }
+      }
+    } else {
+      constexpr int RQ = R / 4;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int bi = tid + 256 * j;
+        rq[j] = bi % RQ;
+        kb[j] = (bi / RQ) * 4;
+      }
+      const int r = row0 + rq[0] * 4;  // NB > 1 only when RQ divides 256: same rq for every j
+      rowok = r < o.rows;
+      if (o.win) {
+        tap = 0;
+        for (int j = 1; j < o.taps; ++j) tap += (r >= j * o.chans);
+        c = r - tap * o.chans;
+      } else {
+        tap = 0;
+        c = r;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void load(const OpDev& o, int kbase, int kend) {
+    if constexpr (!KS) {
+      const int k = kbase + kq;
+      int tp = 0, cc = k;
+      if (o.win) {
+        for (int j = 1; j < o.taps; ++j) tp += (k >= j * o.chans);
+        cc = k - tp * o.chans;
+      }
+      const bool kok = k < kend;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int t2 = tt[i] + tp - o.pad;
+        const bool ok = kok && rok[i] && (!o.win || (t2 >= 0 && t2 < o.t_in));
+        const unsigned elem = (unsigned)(frame[i] + tp - o.pad) * (unsigned)o.ld + (unsigned)cc;
+        raw[i] = RawT<DT>::load(rsrc, ok ? elem * RawT<DT>::ES : FINVALID);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int k = kbase + kb[j] + jj;
+          unsigned elem;
+          bool ok = rowok && k < kend;
+          if (o.win) {
+            const int b = (int)fdiv((uint32_t)k, o.tdiv);
+            const int t2 = k - b * o.t_out + tap - o.pad;
+            ok = ok && t2 >= 0 && t2 < o.t_in;
+            elem = (unsigned)(b * o.t_in + t2) * (unsigned)o.ld + (unsigned)c;
+          } else {
+            elem = (unsigned)k * (unsigned)o.ld + (unsigned)c;
+          }
+          raw[4 * j + jj] = RawT<DT>::load(rsrc, ok ? elem * RawT<DT>::ES : FINVALID);
+        }
+      }
+    }
+  }
+
+  __device__ __forceinline__ void write(bf16* lds, int tid) {
+    if constexpr (!KS) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+        *reinterpret_cast<u32x2*>(lds + ((tid >> 4) + 16 * i) * FLDK + kq) = RawT<DT>::pack(raw[i]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        u32x2 p[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) p[jj] = RawT<DT>::pack(raw[4 * j + jj]);
+        // p[jj] = rows (r0 r1 | r2 r3) at k = kb+jj  ->  row ri: k0..k3
+        const u32x2 r0 = {join16(lo16(p[0][0]), lo16(p[1][0])), join16(lo16(p[2][0]), lo16(p[3][0]))};
+        const u32x2 r1 = {join16(hi16(p[0][0]), hi16(p[1][0])), join16(hi16(p[2][0]), hi16(p[3][0]))};
+        const u32x2 r2 = {join16(lo16(p[0][1]), lo16(p[1][1])), join16(lo16(p[2][1]), lo16(p[3][1]))};
+        const u32x2 r3 = {join16(hi16(p[0][1]), hi16(p[1][1])), join16(hi16(p[2][1]), hi16(p[3][1]))};
+        bf16* d = lds + (rq[j] * 4) * FLDK + kb[j];
+        *reinterpret_cast<u32x2*>(d) = r0;
+        *reinterpret_cast<u32x2*>(d + FLDK) = r1;
+        *reinterpret_cast<u32x2*>(d + 2 * FLDK) = r2;
+        *reinterpret_cast<u32x2*>(d + 3 * FLDK) = r3;
+      }
+    }
+  }
+};
+
+template <int BN_, bool AKS, bool BKS, int ADT, int BDT>
+__global__ void __launch_bounds__(256, 2) gemm_fast_kernel(GemmArgs g) {
+  constexpr int NJ = BN_ / 32;  // 16-wide MFMA column tiles per wave
+  constexpr int WN = BN_ / 2;   // wave tile columns
+  constexpr int TILE = (BM + BN_) * FLDK;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16* smem = reinterpret_cast<bf16*>(smem_raw);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  // XCD-aware bijective remap: blocks that share an A row-panel run on one XCD's L2.
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int nN = (g.N + BN_ - 1) / BN_, nM = (g.M + BM - 1) / BM;
+  const int z = lid / (nN * nM);
+  const int rem = lid - z * nN * nM;
+  const int mt = rem / nN, nt = rem - mt * nN;
+  const int m0 = mt * BM, n0 = nt * BN_;
+  const int bz = z / g.split_k, ks = z - bz * g.split_k;
+  const int kbeg = ks * g.klen;
+  const int kend = min(g.K, kbeg + g.klen);
+
+  FLoader<BM, AKS, ADT> la;
+  FLoader<BN_, BKS, BDT> lb;
+  la.init(g.a, m0, tid, (long long)bz * g.a.bstride);
+  lb.init(g.b, n0, tid, (long long)bz * g.b.bstride);
+
+  f32x4 acc[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = kend > kbeg ? (kend - kbeg + FBK - 1) / FBK : 0;
+  if (nkt > 0) {
+    la.load(g.a, kbeg, kend);
+    lb.load(g.b, kbeg, kend);
+    la.write(smem, tid);
+    lb.write(smem + BM * FLDK, tid);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bf16* As = smem + (kt & 1) * TILE;
+    const bf16* Bs = As + BM * FLDK;
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      la.load(g.a, kbeg + (kt + 1) * FBK, kend);
+      lb.load(g.b, kbeg + (kt + 1) * FBK, kend);
+    }
+#pragma unroll
+    for (int kk = 0; kk < FBK; kk += 32) {
+      bf16x8 af[4], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + (lane & 15)) * FLDK + kk + 8 * (lane >> 4));
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WN + j * 16 + (lane & 15)) * FLDK + kk + 8 * (lane >> 4));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      bf16* An = smem + ((kt + 1) & 1) * TILE;
+      la.write(An, tid);
+      lb.write(An + BM * FLDK, tid);
+    }
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  const int rbase = m0 + wm * 64 + 4 * (lane >> 4);
+  const int cbase = n0 + wn * WN + (lane & 15);
+  float* C = g.c + (long long)bz * g.cbs;
+  bf16* C16 = g.c16 ? g.c16 + (long long)bz * g.cbs : nullptr;
+  if (g.bias && ks == 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = cbase + j * 16;
+      const float bv = col < g.N ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] += bv;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = rbase + i * 16 + e;
+      if (row >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int col = cbase + j * 16;
+        if (col >= g.N) continue;
+        const long long o = (long long)row * g.ldc + col;
+        float v = acc[i][j][e];
+        if (g.atomic) {
+          atomicAdd(C + o, v);
+        } else {
+          if (g.accumulate) v += C[o];
+          C[o] = v;
+          if (C16) C16[o] = (bf16)v;
+        }
+      }
+    }
+  if (g.bn_partial) {
+    float* red = reinterpret_cast<float*>(smem_raw);  // [2][BN_] sums, then [2][BN_] M2
+    const int cnt = min(BM, g.M - m0);
+    float s[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t += (rbase + i * 16 + e < g.M) ? acc[i][j][e] : 0.f;
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      s[j] = t;
+    }
+    __syncthreads();
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) red[wm * BN_ + wn * WN + j * 16 + lane] = s[j];
+    }
+    __syncthreads();
+    float qv[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int cl = wn * WN + j * 16 + (lane & 15);
+      const float mean = (red[cl] + red[BN_ + cl]) / (float)cnt;
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = acc[i][j][e] - mean;
+          t += (rbase + i * 16 + e < g.M) ? d * d : 0.f;
+        }
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      qv[j] = t;
+    }
+    float* red2 = red + 2 * BN_;
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) red2[wm * BN_ + wn * WN + j * 16 + lane] = qv[j];
+    }
+    __syncthreads();
+    if (tid < BN_) {
+      const int col = n0 + tid;
+      if (col < g.N) {
+        float* p = g.bn_partial + ((long long)mt * g.N + col) * 2;
+        p[0] = red[tid] + red[BN_ + tid];
+        p[1] = red2[tid] + red2[BN_ + tid];
+      }
+    }
+  }
+}
+
+template <int BN_, bool AKS, bool BKS, int ADT, int BDT>
+void launch_fast(const GemmArgs& g, int nblocks, hipStream_t s) {
+  const size_t lds = 2 * (BM + BN_) * FLDK * sizeof(bf16);
+  static bool attr = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_fast_kernel<BN_, AKS, BKS, ADT, BDT>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  gemm_fast_kernel<BN_, AKS, BKS, ADT, BDT><<<nblocks, 256, lds, s>>>(g);
+}
+
+template <int BN_, bool AKS, bool BKS>
+void launch_fast_dt(const GemmArgs& g, int nblocks, hipStream_t s) {
+  const bool af = g.a.dtype == AVC_F32, bfl = g.b.dtype == AVC_F32;
+  if (af && bfl) launch_fast<BN_, AKS, BKS, AVC_F32, AVC_F32>(g, nblocks, s);
+  else if (af) launch_fast<BN_, AKS, BKS, AVC_F32, AVC_BF16>(g, nblocks, s);
+  else if (bfl) launch_fast<BN_, AKS, BKS, AVC_BF16, AVC_F32>(g, nblocks, s);
+  else launch_fast<BN_, AKS, BKS, AVC_BF16, AVC_BF16>(g, nblocks, s);
+}
+
+template <int BN_>
+void launch_fast_layout(const GemmArgs& g, bool aks, bool bks, int nblocks, hipStream_t s) {
+  if (!aks && !bks) launch_fast_dt<BN_, false, false>(g, nblocks, s);
+  else if (!aks && bks) launch_fast_dt<BN_, false, true>(g, nblocks, s);
+  else if (aks && !bks) launch_fast_dt<BN_, true, false>(g, nblocks, s);
+  else launch_fast_dt<BN_, true, true>(g, nblocks, s);
+}
+
+bool fits32(const OpDev& o, int rows, int K, bool ks) {
+  // largest element offset the 32-bit buffer addressing can see
+  long long frames = o.win ? (long long)((ks ? K : rows) / (o.t_out > 0 ? o.t_out : 1) + 1) * o.t_in : (ks ? K : rows);
+  long long span = frames * o.ld + (ks ? rows : K) + o.ld;
+  return span * (o.dtype == AVC_F32 ? 4 : 2) < (long long)FINVALID - 64;
+}
+
 }  // namespace
 
 extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
@@ -446,6 +806,7 @@ extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
   kl = ((kl + BK - 1) / BK) * BK;
   g.klen = kl > 0 ? kl : BK;
   g.c = d->c;
+  g.c16 = reinterpret_cast<bf16*>(d->c_bf16);
   g.ldc = d->ldc;
   g.cbs = d->c_batch_stride;
   g.bias = d->bias;
@@ -460,11 +821,24 @@ extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
     dim3 zg(cdiv(tot, 256), g.batch);
     zero2d_kernel<<<zg, 256, 0, s>>>(g.c, g.ldc, g.cbs, g.M, g.N);
   }
-  dim3 grid(cdiv(g.N, BN), cdiv(g.M, BM), g.batch * g.split_k);
   const bool bf = d->compute == AVC_BF16;
   const bool aks = d->a.kstrided != 0, bks = d->b.kstrided != 0;
+  if (bf && g.a.vec && g.b.vec && fits32(g.a, g.M, g.K, aks) && fits32(g.b, g.N, g.K, bks)) {
+    // re-split K in units of the fast kernel's BK
+    int klf = (d->K + g.split_k - 1) / g.split_k;
+    g.klen = ((klf + FBK - 1) / FBK) * FBK;
+    if (g.klen <= 0) g.klen = FBK;
+    const long long t128 = (long long)cdiv(g.M, BM) * cdiv(g.N, 128) * g.batch * g.split_k;
+    const bool narrow = g.N <= 64 || t128 < 384;
+    const int nb = narrow ? cdiv(g.M, BM) * cdiv(g.N, 64) * g.batch * g.split_k : (int)t128;
+    if (narrow) launch_fast_layout<64>(g, aks, bks, nb, s);
+    else launch_fast_layout<128>(g, aks, bks, nb, s);
+    return avc_check_launch("avc_gemm(fast)");
+  }
+  AVC_CHECK_ARG(!g.c16, "avc_gemm: c_bf16 output needs the fast path (bf16 compute, vectorisable operands)");
+  dim3 grid(cdiv(g.N, BN), cdiv(g.M, BM), g.batch * g.split_k);
   size_t lds = bf ? 2 * (BM + BN) * Traits<true>::LDK * sizeof(bf16) : 2 * (BM + BN) * Traits<false>::LDK * sizeof(float);
-#define AVC_GEMM_LAUNCH(BFV, A, B) gemm_kernel<BFV, A, B><<<grid, NT, lds, s>>>(g)
+#define AVC_GEMM_LAUNCH(BFV, A, B) gemm_generic_kernel<BFV, A, B><<<grid, NT, lds, s>>>(g)
   if (bf) {
     if (!aks && !bks) AVC_GEMM_LAUNCH(true, false, false);
     else if (!aks && bks) AVC_GEMM_LAUNCH(true, false, true);

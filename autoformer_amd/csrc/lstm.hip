@@ -18,6 +18,8 @@
 //    grid-wide sync (cheaper on gfx950 than a software grid barrier at 256 workgroups,
 //    MI355X_MICROARCH.md rows "boundary" vs "barrier-xcd"); the host loop is
 //    graph-capturable.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -159,6 +161,7 @@ struct StepArgs {
   float* dg;           // bwd (B,T,dirs*4H)
   float* dcb;          // bwd [dirs][B][H]
   int B, T, H, dirs, s;
+  int dbg;  // diagnostic ablation bits (AVC_LSTM_DEBUG): 1 skip product, 2 skip stores
 };
 
 template <bool BF, int MT>
@@ -392,6 +395,156 @@ __global__ void __launch_bounds__(256) lstm_step_bwd(StepArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------- bf16 step kernels, H known
+// Every operand fragment of a wave's K-slice is loaded before the first MFMA, so a step
+// pays ONE L2/MALL round trip instead of one per k-step.
+template <int H, int MT>
+__global__ void __launch_bounds__(256) lstm_step_fwd_bf(StepArgs a) {
+  constexpr int G = 4 * H, KW = H / 4, NK = KW / 32;
+  const int T = a.T, B = a.B, d = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j0 = blockIdx.x * 8, b0 = blockIdx.y * 16 * MT;
+  const int t = d ? T - 1 - a.s : a.s;
+  const int tp = d ? t + 1 : t - 1;
+  const long long ldx = (long long)a.dirs * G, ldh = (long long)a.dirs * H;
+  __shared__ float red[4][16 * MT][33];
+  const int pr = tid >> 3, pj = tid & 7, pb = b0 + pr;
+  const bool pv = pr < 16 * MT && pb < B;
+  float px[4] = {0.f, 0.f, 0.f, 0.f}, pcp = 0.f;
+  if (pv) {
+    const long long ox = ((long long)pb * T + t) * ldx + d * G + j0 + pj;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) px[q] = a.xproj[ox + q * H];
+    if (a.s > 0) pcp = a.call[((long long)pb * T + tp) * ldh + d * H + j0 + pj];
+  }
+  f32x4 acc[MT][2];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m][0] = acc[m][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (a.s > 0 && !(a.dbg & 1)) {
+    const int r16 = lane & 15, ko = w * KW + 8 * (lane >> 4);
+    const bf16* hp = reinterpret_cast<const bf16*>(a.hb) + ((long long)((a.s - 1) & 1) * a.dirs + d) * B * H;
+    const bf16* W = reinterpret_cast<const bf16*>(a.w) + (long long)d * G * H;
+    bf16x8 af[NK][MT], bw[NK][2];
+    const bf16x8 z = {};
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int b = b0 + m * 16 + r16;
+      const bf16* row = hp + (long long)(b < B ? b : 0) * H + ko;
+#pragma unroll
+      for (int k = 0; k < NK; ++k) af[k][m] = b < B ? *reinterpret_cast<const bf16x8*>(row + 32 * k) : z;
+    }
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int col = n * 16 + r16;
+      const bf16* row = W + (long long)((col >> 3) * H + j0 + (col & 7)) * H + ko;
+#pragma unroll
+      for (int k = 0; k < NK; ++k) bw[k][n] = *reinterpret_cast<const bf16x8*>(row + 32 * k);
+    }
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k][m], bw[k][n], acc[m][n], 0, 0, 0);
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[w][m * 16 + 4 * (lane >> 4) + e][n * 16 + (lane & 15)] = acc[m][n][e];
+  __syncthreads();
+  if (pv && !(a.dbg & 2)) {
+    float pre[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      pre[q] = px[q] + red[0][pr][q * 8 + pj] + red[1][pr][q * 8 + pj] + red[2][pr][q * 8 + pj] + red[3][pr][q * 8 + pj];
+    const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), gg = tanhf(pre[2]), og = sigmoidf_(pre[3]);
+    const float c = fg * pcp + ig * gg;
+    const float h = og * tanhf(c);
+    const int j = j0 + pj;
+    const long long oh = ((long long)pb * T + t) * ldh + d * H + j;
+    a.hout[oh] = h;
+    a.call[oh] = c;
+    const long long og_ = ((long long)pb * T + t) * ldx + d * G + j;
+    a.gall[og_] = ig;
+    a.gall[og_ + H] = fg;
+    a.gall[og_ + 2 * H] = gg;
+    a.gall[og_ + 3 * H] = og;
+    bf16* hn = reinterpret_cast<bf16*>(a.hb) + ((long long)(a.s & 1) * a.dirs + d) * B * H;
+    hn[(long long)pb * H + j] = (bf16)h;
+  }
+}
+
+// backward: 8 waves split K = 4H; tile 16 utterances x 16 hidden units.
+template <int H>
+__global__ void __launch_bounds__(512) lstm_step_bwd_bf(StepArgs a) {
+  constexpr int G = 4 * H, KW = G / 8, NK = KW / 32;
+  const int T = a.T, B = a.B, d = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j0 = blockIdx.x * 16, b0 = blockIdx.y * 16;
+  const int t = d ? a.s : T - 1 - a.s;
+  const int tp = d ? t + 1 : t - 1;
+  const long long ldg = (long long)a.dirs * G, ldh = (long long)a.dirs * H;
+  __shared__ float red[8][16][17];
+  const int prow = tid >> 4, pjj = tid & 15, pb = b0 + prow;
+  const bool pv = tid < 256 && pb < B;
+  float pdh = 0.f, pc = 0.f, pcp = 0.f, pdc = 0.f, pg[4] = {0.f, 0.f, 0.f, 0.f};
+  if (pv) {
+    const int j = j0 + pjj;
+    const long long oh = ((long long)pb * T + t) * ldh + d * H + j;
+    pdh = a.dhout[oh];
+    pc = a.call[oh];
+    if (tp >= 0 && tp < T) pcp = a.call[((long long)pb * T + tp) * ldh + d * H + j];
+    const long long og_ = ((long long)pb * T + t) * ldg + d * G + j;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pg[q] = a.gall[og_ + q * H];
+    if (a.s > 0) pdc = a.dcb[((long long)d * B + pb) * H + j];
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (a.s > 0) {
+    const int r16 = lane & 15, ko = w * KW + 8 * (lane >> 4);
+    const bf16* gp = reinterpret_cast<const bf16*>(a.hb) + ((long long)((a.s - 1) & 1) * a.dirs + d) * B * G;
+    const bf16* WT = reinterpret_cast<const bf16*>(a.w) + (long long)d * H * G;
+    const int b = b0 + r16;
+    const bf16* arow = gp + (long long)(b < B ? b : 0) * G + ko;
+    const bf16* brow = WT + (long long)(j0 + r16) * G + ko;
+    bf16x8 af[NK], bw[NK];
+    const bf16x8 z = {};
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      af[k] = b < B ? *reinterpret_cast<const bf16x8*>(arow + 32 * k) : z;
+      bw[k] = *reinterpret_cast<const bf16x8*>(brow + 32 * k);
+    }
+#pragma unroll
+    for (int k = 0; k < NK; ++k) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k], bw[k], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[w][4 * (lane >> 4) + e][lane & 15] = acc[e];
+  __syncthreads();
+  if (pv) {
+    const int j = j0 + pjj;
+    float dh = pdh;
+#pragma unroll
+    for (int ww = 0; ww < 8; ++ww) dh += red[ww][prow][pjj];
+    const float ig = pg[0], fg = pg[1], gg = pg[2], og = pg[3];
+    const float tc = tanhf(pc);
+    const float do_ = dh * tc;
+    const float dcs = pdc + dh * og * (1.f - tc * tc);
+    const float di = dcs * gg, dgg = dcs * ig, df = dcs * pcp;
+    a.dcb[((long long)d * B + pb) * H + j] = dcs * fg;
+    const float v[4] = {di * ig * (1.f - ig), df * fg * (1.f - fg), dgg * (1.f - gg * gg), do_ * og * (1.f - og)};
+    const long long og_ = ((long long)pb * T + t) * ldg + d * G + j;
+    bf16* gn = reinterpret_cast<bf16*>(a.hb) + ((long long)(a.s & 1) * a.dirs + d) * B * G + (long long)pb * G;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      a.dg[og_ + q * H] = v[q];
+      gn[q * H + j] = (bf16)v[q];
+    }
+  }
+}
+
 template <int HM>
 void launch_small_fwd(dim3 g, hipStream_t s, const float* x, const float* w, int T, int H, int dirs, float* h, float* c,
                       float* gt) {
@@ -424,6 +577,8 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
   AVC_CHECK_ARG(!bf || (wdtype == AVC_BF16 && hbuf), "avc_lstm_fwd: bf16 compute needs bf16 W_hh and hbuf");
   AVC_CHECK_ARG(bf || wdtype == AVC_F32, "avc_lstm_fwd: fp32 compute needs fp32 W_hh");
   StepArgs a = {};
+  static const int dbg = getenv("AVC_LSTM_DEBUG") ? atoi(getenv("AVC_LSTM_DEBUG")) : 0;
+  a.dbg = dbg;
   a.xproj = xproj;
   a.w = w_hh;
   a.hout = h;
@@ -434,11 +589,17 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
   a.T = T;
   a.H = H;
   a.dirs = dirs;
-  const int mt = (H >= 1024 && B > 16) ? 2 : 1;
+  const int mt = (H >= 1024 && B > 16) ? 2 : 1;  // 256 workgroups at B = 64
   dim3 g(H / 8, cdiv(B, 16 * mt), dirs);
   for (int st = 0; st < T; ++st) {
     a.s = st;
-    if (bf) {
+    if (bf && H == 1024) {
+      if (mt == 2) lstm_step_fwd_bf<1024, 2><<<g, 256, 0, s>>>(a);
+      else lstm_step_fwd_bf<1024, 1><<<g, 256, 0, s>>>(a);
+    } else if (bf && H == 512) {
+      if (mt == 2) lstm_step_fwd_bf<512, 2><<<g, 256, 0, s>>>(a);
+      else lstm_step_fwd_bf<512, 1><<<g, 256, 0, s>>>(a);
+    } else if (bf) {
       if (mt == 2) lstm_step_fwd<true, 2><<<g, 256, 0, s>>>(a);
       else lstm_step_fwd<true, 1><<<g, 256, 0, s>>>(a);
     } else {
@@ -484,7 +645,9 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
   dim3 g(H / 16, cdiv(B, 16), dirs);
   for (int st = 0; st < T; ++st) {
     a.s = st;
-    if (bf) lstm_step_bwd<true, 1><<<g, 256, 0, s>>>(a);
+    if (bf && H == 1024) lstm_step_bwd_bf<1024><<<g, 512, 0, s>>>(a);
+    else if (bf && H == 512) lstm_step_bwd_bf<512><<<g, 512, 0, s>>>(a);
+    else if (bf) lstm_step_bwd<true, 1><<<g, 256, 0, s>>>(a);
     else lstm_step_bwd<false, 1><<<g, 256, 0, s>>>(a);
   }
   return avc_check_launch("avc_lstm_bwd");

@@ -1,0 +1,71 @@
+"""Data parallelism for the training step: one process per GPU, utterance batches sharded
+across ranks, per-replica BatchNorm (no SyncBN — the reference is single-device and
+its BN statistics are per batch of 64), gradients averaged with one
+bucketed all-reduce over the flat gradient buffer (RCCL over xGMI when the backend is
+"nccl"; gloo on CPU for tests).
+
+The reference has no distributed code at all; this is the only exchange
+step of the path.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+BUCKET_BYTES = 32 << 20
+
+
+def init_from_env(backend: str = "nccl"):
+    """Initialise the default process group from torchrun's env; returns (rank, world, local_rank)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return 0, 1, 0
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if not dist.is_initialized():
+        dist.init_process_group(backend=backend)
+    return dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def flatten_params_(module, device=None):
+    """Move every parameter into one contiguous fp32 buffer (and its .grad into another)
+    so the optimizer and the all-reduce are single kernels over 28.5M values.  Returns
+    (params, flat, gflat)."""
+    params = [p for p in module.parameters() if p.requires_grad]
+    device = device or params[0].device
+    n = sum(p.numel() for p in params)
+    flat = torch.empty(n, device=device, dtype=torch.float32)
+    gflat = torch.zeros(n, device=device, dtype=torch.float32)
+    off = 0
+    with torch.no_grad():
+        for p in params:
+            k = p.numel()
+            flat[off:off + k].copy_(p.detach().reshape(-1))
+            p.data = flat[off:off + k].view_as(p)
+            p.grad = gflat[off:off + k].view_as(p)
+            off += k
+    return params, flat, gflat
+
+
+def broadcast_(flat: torch.Tensor, src: int = 0):
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.broadcast(flat, src)
+
+
+def allreduce_mean_(gflat: torch.Tensor, bucket_bytes: int = BUCKET_BYTES):
+    """Average gradients over ranks in ~32 MB buckets (xGMI ring: per-link bound, so a few
+    large collectives beat many small ones)."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return
+    world = dist.get_world_size()
+    use_avg = dist.get_backend() == "nccl"
+    step = max(1, bucket_bytes // gflat.element_size())
+    works = []
+    for off in range(0, gflat.numel(), step):
+        chunk = gflat[off:off + step]
+        works.append(dist.all_reduce(chunk, op=dist.ReduceOp.AVG if use_avg else dist.ReduceOp.SUM, async_op=True))
+    for w in works:
+        w.wait()
+    if not use_avg:
+        gflat.mul_(1.0 / world)

@@ -70,8 +70,8 @@ def operand(t: torch.Tensor, ld: int, kstrided: bool = False, window=None, batch
 
 
 def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=None, accumulate=False, split_k=1,
-         bn_partial=None, batch=1, c_batch_stride=0, comp=None):
-    _dev(c, bias, bn_partial)
+         bn_partial=None, batch=1, c_batch_stride=0, comp=None, c_bf16=None):
+    _dev(c, bias, bn_partial, c_bf16)
     assert c.dtype == torch.float32
     d = L.GemmDesc()
     d.M, d.N, d.K, d.batch = int(M), int(N), int(K), int(batch)
@@ -84,6 +84,7 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     d.split_k = int(split_k)
     d.bn_partial = _ptr(bn_partial)
     d.compute = _COMPUTE if comp is None else comp
+    d.c_bf16 = _ptr(c_bf16)
     L.check(L.lib().avc_gemm(d, stream()), "avc_gemm")
 
 

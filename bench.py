@@ -1,0 +1,176 @@
+#!/usr/bin/env python
+"""Benchmark: mel-frames/s of the AutoVC train.py step (fwd + encoder re-pass + MSE/L1 +
+bwd + Adam) on synthetic (B, T, 80) batches resident in HBM, 1..N GPUs (one process per
+GPU, data parallel, RCCL gradient all-reduce).
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "mel-frames/sec fwd+bwd, AutoVC 80×128 mel, batch=64, at 1/2/4/8 GPUs"
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3     # f32 MFMA
+# algorithmic work of one train.py step per mel frame (torch flop counter on the reference)
+FLOP_PER_FRAME = {(128, 16): 191.55e6, (176, 22): 191.59e6}
+
+
+def synthetic_batch(B, T, rank, device):
+    """log10-mel-like clamp(N(-2.5, 1.5^2), -5, 2), unit-norm embeddings."""
+    g = torch.Generator().manual_seed(1234 + rank)
+    x = torch.clamp(torch.randn(B, T, 80, generator=g) * 1.5 - 2.5, -5.0, 2.0)
+    g2 = torch.Generator().manual_seed(5678 + rank)
+    e = torch.nn.functional.normalize(torch.randn(B, 256, generator=g2), dim=-1)
+    return x.to(device), e.to(device)
+
+
+def kernel_timing(model, B, T, reps=3):
+    """Average duration of the dominant kernel family, measured with HIP events on the
+    stream the kernels are launched on (torch's current stream: the C-ABI launches there).
+
+    The dominant kernels of the step are the per-time-step LSTM recurrence kernels of the
+    decoder's lstm2 (H=1024): 2 layers x T launches forward, twice that counting the
+    backward.  Here the forward recurrence of lstm2 layer 1 is replayed standalone."""
+    from autoformer_amd import kernels as K
+
+    core = model.decoder._lstm2[1]
+    wih, bsum, whh, whh_t = core.packs()
+    H = core.H
+    dev = whh.device
+    xproj = torch.randn(B * T, 4 * H, device=dev) * 0.1
+    hbuf = torch.empty(2 * B * H, device=dev, dtype=torch.bfloat16) if K.compute() == K.BF16 else None
+    s = torch.cuda.current_stream()
+    K.lstm_fwd(xproj, whh, B, T, H, 1, hbuf)  # warm
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        K.lstm_fwd(xproj, whh, B, T, H, 1, hbuf)
+    e1.record(s)
+    torch.cuda.synchronize()
+    avg_ms = e0.elapsed_time(e1) / (reps * T)  # per launch (one launch per time step)
+    flops = 2.0 * B * H * 4 * H  # recurrent product h_{t-1} W_hh^T per launch
+    w_bytes = 2.0 * (4 * H) * H * math.ceil(B / 32)   # bf16 W_hh slices read per launch
+    h_bytes = 2.0 * B * H * (H // 8)                  # h_{t-1} re-read by every unit block
+    return {"kernel": "lstm_step_fwd<bf16,MT=2> (decoder lstm2, H=1024, B=%d)" % B, "avg_us": avg_ms * 1e3,
+            "flops": flops, "l2_bytes": w_bytes + h_bytes}
+
+
+def cpu_baseline(B, T, freq, steps=2):
+    """The CPU oracle (oracle/autovc_cpu.py, the pinned restatement of the reference) timed on
+    this box's host cores: same step, fp32, bounded sample of 1 warm-up + `steps` steps."""
+    from oracle import autovc_cpu as O
+
+    x, e = synthetic_batch(B, T, 0, "cpu")
+    s = O.OracleSolver(freq=freq)
+    s.step(x, e)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        s.step(x, e)
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": round(B * T / dt, 1), "unit": "mel-frames/s", "cores": torch.get_num_threads(),
+            "kind": "port", "sample": f"oracle train step B={B} T={T} freq={freq} fp32, 1 warm-up + {steps} timed "
+                                      f"steps ({dt * 1e3:.0f} ms/step)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--len-crop", type=int, default=128)
+    ap.add_argument("--freq", type=int, default=16)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    from autoformer_amd import dist as D
+    from autoformer_amd import set_compute
+    from autoformer_amd.detinit import det_init_
+    from autoformer_amd.factory.AutoVC import AutoVC
+    from autoformer_amd.train import TrainStep
+
+    rank, world, local = D.init_from_env("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    set_compute(args.dtype)
+    B, T, freq = args.batch, args.len_crop, args.freq
+
+    model = AutoVC(44, 256, 512, freq)
+    det_init_(model)
+    model = model.to(dev).train()
+    x, e = synthetic_batch(B, T, rank, dev)
+    trainer = TrainStep(model, lr=1e-4)
+
+    for _ in range(args.warmup):
+        trainer.step(x, e)
+    if not args.no_graph:
+        trainer.capture(x, e)
+        trainer.step(x, e)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = trainer.step(x, e)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    loss_v = float(loss.item())
+    ms = elapsed / args.steps * 1e3
+    frames = world * B * T
+    value = frames / (elapsed / args.steps)
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    fpf = FLOP_PER_FRAME.get((T, freq), 191.55e6)
+    peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+    out = {"metric": METRIC, "value": round(value, 1), "unit": "mel-frames/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
+           "config": {"workload": f"AutoVC train.py step (fwd + encoder re-pass + 2xMSE + L1 + bwd + Adam), "
+                                  f"B={B}/GPU, T={T}, freq={freq}, dim_neck=44, dim_emb=256, dim_pre=512",
+                      "global_batch": B * world, "seq_len": T, "freq": freq, "parallelism": f"dp{world}",
+                      "graph": not args.no_graph},
+           "step_mfma_frac": round(value * fpf / (world * peak * 1e12), 5),
+           "final_loss": loss_v}
+    if not args.no_kernel_timing:
+        kt = kernel_timing(model, B, T)
+        ach = kt["flops"] / (kt["avg_us"] * 1e-6) / 1e12
+        out["roofline"] = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
+                           "frac": round(ach / peak, 5), "traffic": None, "kernel": kt["kernel"],
+                           "avg_us": round(kt["avg_us"], 3)}
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(B, T, freq)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -67,6 +67,7 @@ typedef struct {
   int split_k;
   float* bn_partial;
   int compute;
+  void* c_bf16; /* nullable: also store C rounded to bf16 (same ldc), for the next GEMM */
 } avc_gemm_desc;
 
 int avc_abi_version(void);

@@ -276,3 +276,22 @@ def test_losses_and_adam():
         opt.step()
         Kr.adam(pd, g.to(DEV), m, v, 1e-3, 0.9, 0.999, 1e-8, st)
     assert rinf(pd, pt.detach()) < 1e-6
+
+
+def test_gemm_fast_bf16_copy_and_mixed_dtypes():
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute("bf16")
+    M, N, K_ = 512, 320, 256
+    a = torch.randn(M, K_)
+    b = torch.randn(N, K_)
+    ref = _gemm_ref(a.bfloat16().float(), b.bfloat16().float())
+    for adt in (torch.float32, torch.bfloat16):
+        for bdt in (torch.float32, torch.bfloat16):
+            ad, bd = a.to(DEV).to(adt), b.to(DEV).to(bdt)
+            c = torch.empty(M, N, device=DEV)
+            c16 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            Kr.gemm(M, N, K_, Kr.operand(ad, K_), Kr.operand(bd, K_), c, c_bf16=c16)
+            assert relf(c, ref) < 1e-5
+            assert relf(c16.float(), ref) < 5e-3
