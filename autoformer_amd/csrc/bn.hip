@@ -131,7 +131,8 @@ __global__ void bn_bwd_reduce_kernel(const float* __restrict__ dA, const float* 
 }
 
 __global__ void bn_bwd_finalize_kernel(const float* ws, int nrb, int M, int C, const float* gamma,
-                                       const float* rstd, float* coef, float* dgamma, float* dbeta, float* dbias) {
+                                       const float* rstd, float* coef, float* dgamma, float* dbeta, float* dbias,
+                                       int acc) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double s0 = 0, s1 = 0, s2 = 0;
@@ -147,9 +148,10 @@ __global__ void bn_bwd_finalize_kernel(const float* ws, int nrb, int M, int C, c
   coef[c * 3 + 0] = k1;
   coef[c * 3 + 1] = (float)s0 * invn;
   coef[c * 3 + 2] = (float)s1 * invn;
-  if (dgamma) dgamma[c] = (float)s1;
-  if (dbeta) dbeta[c] = (float)s0;
-  if (dbias) dbias[c] = -k1 * (float)(s1 * s2) * invn;
+  const float gb = -k1 * (float)(s1 * s2) * invn;
+  if (dgamma) dgamma[c] = acc ? dgamma[c] + (float)s1 : (float)s1;
+  if (dbeta) dbeta[c] = acc ? dbeta[c] + (float)s0 : (float)s0;
+  if (dbias) dbias[c] = acc ? dbias[c] + gb : gb;
 }
 
 __global__ void bn_bwd_apply_kernel(const float* __restrict__ dA, const float* __restrict__ a,
@@ -238,14 +240,15 @@ extern "C" size_t avc_bn_bwd_ws(int M, int C) { return (size_t)cdiv(M, RB) * C *
 
 extern "C" int avc_bn_bwd(const float* dA, const float* a, const float* y, const float* mean, const float* rstd,
                           const float* gamma, int M, int C, int act, float* dy, float* dgamma, float* dbeta,
-                          float* dbias, float* ws, void* stream) {
+                          float* dbias, int accumulate, float* ws, void* stream) {
   AVC_CHECK_ARG(dA && a && y && mean && rstd && dy && ws && C % 4 == 0, "avc_bn_bwd: bad args (C %% 4 must be 0)");
   hipStream_t s = as_stream(stream);
   const int nrb = cdiv(M, RB);
   dim3 grid(cdiv(C, 64), nrb);
   bn_bwd_reduce_kernel<<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, M, C, act, ws);
   float* coef = ws + (size_t)nrb * C * 3;
-  bn_bwd_finalize_kernel<<<cdiv(C, 256), 256, 0, s>>>(ws, nrb, M, C, gamma, rstd, coef, dgamma, dbeta, dbias);
+  bn_bwd_finalize_kernel<<<cdiv(C, 256), 256, 0, s>>>(ws, nrb, M, C, gamma, rstd, coef, dgamma, dbeta, dbias,
+                                                       accumulate);
   long long total4 = (long long)M * C / 4;
   bn_bwd_apply_kernel<<<cdiv(total4, 256), 256, 0, s>>>(dA, a, y, mean, rstd, coef, total4, C, act, dy);
   return avc_check_launch("avc_bn_bwd");

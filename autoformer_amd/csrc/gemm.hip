@@ -437,7 +437,6 @@ int make_op(const avc_operand& o, int rows, int K, OpDev& d, const char* name) {
 // branches).  BK = 64, 2 LDS stages, 2 workgroups per CU, XCD-aware tile order.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 constexpr int FBK = 64, FLDK = FBK + 8;  // 144-byte LDS rows
 constexpr unsigned FINVALID = 0x7FFFFFF0u;
 

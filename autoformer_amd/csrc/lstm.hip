@@ -545,6 +545,153 @@ __global__ void __launch_bounds__(512) lstm_step_bwd_bf(StepArgs a) {
   }
 }
 
+// =============================================================== large H: persistent forward
+// One launch for all T steps.  Workgroups form NG groups of H/32; group g owns utterance
+// rows [8g, 8g+8), member r owns hidden units [32r, 32r+32) and keeps the matching
+// 128 rows of W_hh (all four gates) in VGPRs for the whole sequence (wave w = gate w).
+// h_t is exchanged inside the group through data-tagged 8-byte granules {tag = step+1,
+// two bf16}: one agent-scope (sc1) store per granule, consumers re-read with agent-scope
+// loads until every tag matches (MI355X_MICROARCH.md hand-off R2: no flag, no fence).
+// Groups are blockIdx % NG: with round-robin dispatch a group sits on one XCD and the
+// exchange stays in that XCD's L2 -- a speed assumption only, correctness holds for any
+// placement.  Every spin is bounded; on timeout the kernel raises a flag and exits.
+constexpr int PRG = 8, PJU = 32;
+constexpr unsigned PSPIN = 1u << 22;
+
+struct PersistArgs {
+  const float* xproj;
+  const bf16* w;
+  float* hout;
+  float* call;
+  float* gall;
+  unsigned long long* xbuf;  // [2][B][H/2] granules, zeroed before launch
+  unsigned* flag;            // timeout flag
+  int B, T, ng;
+};
+
+__device__ __forceinline__ unsigned long long granule(unsigned tag, float a, float b) {
+  bf16x2 h = {(bf16)a, (bf16)b};
+  return ((unsigned long long)tag << 32) | (unsigned long long)__builtin_bit_cast(unsigned, h);
+}
+
+template <int H>
+__global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
+  constexpr int G = 4 * H, NK = H / 32, AP = H + 8, H2 = H / 2;
+  constexpr int NGR = PRG * H2 / 256;  // granules gathered per thread per step
+  __shared__ __attribute__((aligned(16))) bf16 As[16 * AP];
+  __shared__ float gs[PRG][4 * PJU + 1];
+  __shared__ int quit;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
+  const int j0 = r * PJU, b0 = g * PRG;
+  const int T = a.T, B = a.B;
+
+  bf16x8 wf[2][NK];
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const bf16* row = a.w + (long long)(w * H + j0 + n * 16 + (lane & 15)) * H + 8 * (lane >> 4);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) wf[n][k] = *reinterpret_cast<const bf16x8*>(row + 32 * k);
+  }
+  for (int i = tid; i < 16 * AP / 2; i += 256) reinterpret_cast<unsigned*>(As)[i] = 0u;
+  if (tid == 0) quit = 0;
+  const int pr = tid >> 5, pu = tid & 31, pb = b0 + pr, pj = j0 + pu;
+  const bool pv = pb < B;
+  unsigned need0 = 0;  // granules this thread gathers each step (rows inside the batch)
+#pragma unroll
+  for (int i = 0; i < NGR; ++i)
+    if (b0 + (tid + 256 * i) / H2 < B) need0 |= 1u << i;
+  float c = 0.f;
+  __syncthreads();
+
+  for (int s = 0; s < T; ++s) {
+    const int t = s;
+    float px[4] = {0.f, 0.f, 0.f, 0.f};
+    if (pv) {
+      const float* xp = a.xproj + ((long long)pb * T + t) * G + pj;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) px[q] = xp[q * H];
+    }
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    if (s > 0) {
+      // ---- gather the group's h_{t-1} (tag == s) into the LDS A tile
+      const unsigned long long* src = a.xbuf + (long long)((s - 1) & 1) * B * H2 + (long long)b0 * H2;
+      unsigned need = need0, spins = 0;
+      while (need) {
+#pragma unroll
+        for (int i = 0; i < NGR; ++i) {
+          if (!(need & (1u << i))) continue;
+          const int idx = tid + 256 * i, row = idx / H2, c2 = idx - row * H2;
+          const unsigned long long v =
+              __hip_atomic_load(src + (long long)row * H2 + c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(v >> 32) == (unsigned)s) {
+            reinterpret_cast<unsigned*>(As + row * AP)[c2] = (unsigned)v;
+            need &= ~(1u << i);
+          }
+        }
+        if (need) {
+          if (++spins > PSPIN) {
+            atomicOr(a.flag, 1u);
+            quit = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      if (quit) return;  // block-uniform exit after a spin timeout
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + (lane & 15) * AP + 32 * k + 8 * (lane >> 4));
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[0][k], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[1][k], acc1, 0, 0, 0);
+      }
+    }
+    if (lane < 32) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        gs[4 * (lane >> 4) + e][w * PJU + (lane & 15)] = acc0[e];
+        gs[4 * (lane >> 4) + e][w * PJU + 16 + (lane & 15)] = acc1[e];
+      }
+    }
+    __syncthreads();
+    float h = 0.f, ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f;
+    if (pv) {
+      ig = sigmoidf_(px[0] + gs[pr][pu]);
+      fg = sigmoidf_(px[1] + gs[pr][PJU + pu]);
+      gg = tanhf(px[2] + gs[pr][2 * PJU + pu]);
+      og = sigmoidf_(px[3] + gs[pr][3 * PJU + pu]);
+      c = fg * c + ig * gg;
+      h = og * tanhf(c);
+    }
+    const float hn = __shfl_down(h, 1, 64);
+    if (pv && !(pu & 1) && s + 1 < T)
+      __hip_atomic_store(a.xbuf + (long long)(s & 1) * B * H2 + (long long)pb * H2 + (pj >> 1),
+                         granule((unsigned)(s + 1), h, hn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (pv) {
+      const long long oh = ((long long)pb * T + t) * H + pj;
+      a.hout[oh] = h;
+      a.call[oh] = c;
+      float* gp = a.gall + ((long long)pb * T + t) * G + pj;
+      gp[0] = ig;
+      gp[H] = fg;
+      gp[2 * H] = gg;
+      gp[3 * H] = og;
+    }
+  }
+}
+
+int g_num_cus = -1;
+int num_cus() {
+  if (g_num_cus < 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    g_num_cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+                    ? prop.multiProcessorCount : 0;
+  }
+  return g_num_cus;
+}
+
 template <int HM>
 void launch_small_fwd(dim3 g, hipStream_t s, const float* x, const float* w, int T, int H, int dirs, float* h, float* c,
                       float* gt) {
@@ -589,6 +736,26 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
   a.T = T;
   a.H = H;
   a.dirs = dirs;
+  const int ng = (B + PRG - 1) / PRG;
+  static const bool no_persist = getenv("AVC_LSTM_NO_PERSIST") != nullptr;
+  if (bf && dirs == 1 && (H == 1024 || H == 512) && hbuf && !no_persist && ng * (H / PJU) <= num_cus()) {
+    // hbuf is the granule scratch (>= 2*B*H/2 u64 + a flag word) in this mode
+    PersistArgs p;
+    p.xproj = xproj;
+    p.w = reinterpret_cast<const bf16*>(w_hh);
+    p.hout = h;
+    p.call = c;
+    p.gall = gates;
+    p.xbuf = reinterpret_cast<unsigned long long*>(hbuf);
+    p.flag = reinterpret_cast<unsigned*>(p.xbuf + (size_t)2 * B * (H / 2));
+    p.B = B;
+    p.T = T;
+    p.ng = ng;
+    (void)hipMemsetAsync(hbuf, 0, ((size_t)2 * B * (H / 2) + 2) * sizeof(unsigned long long), s);
+    if (H == 1024) lstm_persist_fwd<1024><<<ng * (H / PJU), 256, 0, s>>>(p);
+    else lstm_persist_fwd<512><<<ng * (H / PJU), 256, 0, s>>>(p);
+    return avc_check_launch("avc_lstm_fwd(persistent)");
+  }
   const int mt = (H >= 1024 && B > 16) ? 2 : 1;  // 256 workgroups at B = 64
   dim3 g(H / 8, cdiv(B, 16 * mt), dirs);
   for (int st = 0; st < T; ++st) {

@@ -132,16 +132,21 @@ def bn_apply(y, scale, shift, act, residual=None, out=None):
     return out
 
 
-def bn_bwd(dA, a, y, mean, rstd, gamma, act, need_dbias=True):
+def bn_bwd(dA, a, y, mean, rstd, gamma, act, need_dbias=True, into=None):
+    """into = (dgamma, dbeta, dbias) buffers to accumulate into (direct gradient sink)."""
     M, C = y.shape
     dev = y.device
     dy = torch.empty_like(y)
-    dgamma = torch.empty(C, device=dev)
-    dbeta = torch.empty(C, device=dev)
-    dbias = torch.empty(C, device=dev) if need_dbias else None
+    if into is not None:
+        dgamma, dbeta, dbias = into
+    else:
+        dgamma = torch.empty(C, device=dev)
+        dbeta = torch.empty(C, device=dev)
+        dbias = torch.empty(C, device=dev) if need_dbias else None
     ws = torch.empty(int(L.lib().avc_bn_bwd_ws(M, C)), device=dev)
     L.call("avc_bn_bwd", dA.data_ptr(), a.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), _ptr(gamma), M,
-           C, int(act), dy.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), _ptr(dbias), ws.data_ptr(), stream())
+           C, int(act), dy.data_ptr(), _ptr(dgamma), _ptr(dbeta), _ptr(dbias), int(into is not None), ws.data_ptr(),
+           stream())
     return dy, dgamma, dbeta, dbias
 
 
@@ -155,6 +160,16 @@ def colsum(x, M, N, ld=None, out=None, accumulate=False):
 
 
 # ------------------------------------------------------------------------- LSTM
+def lstm_scratch(B, H, dirs, device):
+    """bf16 scratch for the large-H recurrence: per-step ping-pong h (2*dirs*B*H bf16) or,
+    for the persistent kernel, 2*B*H/2 8-byte granules + a timeout flag word."""
+    return torch.zeros(max(2 * dirs * B * H, 4 * B * H + 32), device=device, dtype=torch.bfloat16)
+
+
+def lstm_timeout_flag(hbuf, B, H):
+    return int(hbuf.view(torch.int32)[2 * B * H].item())
+
+
 def lstm_fwd(xproj, w_hh, B, T, H, dirs, hbuf=None):
     dev = xproj.device
     h = torch.empty(B * T, dirs * H, device=dev)
@@ -221,9 +236,9 @@ def conv_pack(w, mode, dtype):
     return out.view(Co, K * Ci) if mode == 0 else out.view(Ci, K * Co)
 
 
-def conv_grad_unpack(dwf, Co, Ci, K):
-    dw = torch.empty(Co, Ci, K, device=dwf.device)
-    L.call("avc_conv_grad_unpack", dwf.data_ptr(), dw.data_ptr(), Co, Ci, K, 0, stream())
+def conv_grad_unpack(dwf, Co, Ci, K, into=None):
+    dw = torch.empty(Co, Ci, K, device=dwf.device) if into is None else into
+    L.call("avc_conv_grad_unpack", dwf.data_ptr(), dw.data_ptr(), Co, Ci, K, int(into is not None), stream())
     return dw
 
 

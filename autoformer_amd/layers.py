@@ -19,6 +19,56 @@ from .kernels import operand
 
 _EPOCH = [0]
 
+# ---------------------------------------------------------------- gradient sink / side stream
+# In "sink" mode (set by TrainStep) parameter gradients are accumulated by the kernels
+# straight into the preallocated p.grad views of the flat gradient buffer, and the
+# weight-gradient GEMMs (off the critical path of the backward) run on a side stream that
+# overlaps the latency-bound LSTM recurrences on the main stream.  The autograd functions
+# then return None for parameters.  join_side() must run before the gradients are read.
+_SINK = {"on": False, "side": None, "keep": []}
+
+
+def set_grad_sink(on: bool) -> None:
+    _SINK["on"] = bool(on)
+    if on and _SINK["side"] is None:
+        _SINK["side"] = torch.cuda.Stream()
+
+
+def sink_on() -> bool:
+    return _SINK["on"]
+
+
+class _Side:
+    """Context: run enclosed kernels on the side stream after everything queued so far on
+    the current stream; tensors passed to keep() stay alive until join_side()."""
+
+    def __enter__(self):
+        self.main = torch.cuda.current_stream()
+        side = _SINK["side"]
+        side.wait_stream(self.main)
+        self.ctx = torch.cuda.stream(side)
+        self.ctx.__enter__()
+        return self
+
+    def keep(self, *ts):
+        _SINK["keep"].extend(t for t in ts if t is not None)
+
+    def __exit__(self, *exc):
+        self.ctx.__exit__(*exc)
+        return False
+
+
+def join_side() -> None:
+    if _SINK["side"] is not None:
+        torch.cuda.current_stream().wait_stream(_SINK["side"])
+    _SINK["keep"].clear()
+
+
+def _grad_of(p):
+    if p.grad is None:
+        raise RuntimeError("gradient sink mode needs preallocated p.grad (see dist.flatten_params_)")
+    return p.grad
+
 
 def weights_changed() -> None:
     """Call after updating parameters through raw pointers (fused Adam, DDP broadcast)."""
@@ -89,15 +139,26 @@ class ConvBNCore:
         y, mean, rstd, T_out = saved
         if not self.bn.training:
             raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
-        conv = self.conv
+        conv, bn = self.conv, self.bn
         Co, Ci, Kw = conv.weight.shape
         M = B * T_out
-        dy, dgamma, dbeta, dbias = K.bn_bwd(dA, a, y, mean, rstd, self.bn.weight, self.act)
-        dWf = torch.empty(Co, Kw * Ci, device=x.device)
-        sk = K.auto_split_k(Co, Kw * Ci, M)
-        K.gemm(Co, Kw * Ci, M, operand(dy, Co, kstrided=True),
-               operand(x, Ci, kstrided=True, window=(Kw, self.pad, T_out, T_in, Ci)), dWf, split_k=sk)
-        dW = K.conv_grad_unpack(dWf, Co, Ci, Kw)
+        sink = _SINK["on"]
+        into = (_grad_of(bn.weight), _grad_of(bn.bias), _grad_of(conv.bias)) if sink else None
+        dy, dgamma, dbeta, dbias = K.bn_bwd(dA, a, y, mean, rstd, bn.weight, self.act, into=into)
+
+        def wgrad():
+            dWf = torch.empty(Co, Kw * Ci, device=x.device)
+            sk = K.auto_split_k(Co, Kw * Ci, M)
+            K.gemm(Co, Kw * Ci, M, operand(dy, Co, kstrided=True),
+                   operand(x, Ci, kstrided=True, window=(Kw, self.pad, T_out, T_in, Ci)), dWf, split_k=sk)
+            return K.conv_grad_unpack(dWf, Co, Ci, Kw, into=_grad_of(conv.weight) if sink else None)
+        if sink:
+            with _Side() as sd:
+                sd.keep(dy, x)
+                wgrad()
+            dW = dgamma = dbeta = dbias = None
+        else:
+            dW = wgrad()
         dx = None
         if n_dx:
             _, Wd = self.packs()
@@ -207,7 +268,7 @@ class LSTMLayerCore:
         K.gemm(B * T, dirs * 4 * H, In, operand(x, In), operand(wih, In), xproj, bias=bsum)
         hbuf = None
         if H > 64 and K.compute() == K.BF16:
-            hbuf = torch.empty(2 * dirs * B * H, device=x.device, dtype=torch.bfloat16)
+            hbuf = K.lstm_scratch(B, H, dirs, x.device)
         h, c, g = K.lstm_fwd(xproj, whh, B, T, H, dirs, hbuf)
         return h, (c, g)
 
@@ -219,20 +280,37 @@ class LSTMLayerCore:
         dg = K.lstm_bwd(dh, h, c, g, whh if H <= 64 else None, whh_t, B, T, H, dirs)
         G = dirs * 4 * H
         M = B * T
-        dwih = torch.empty(G, In, device=x.device)
-        K.gemm(G, In, M, operand(dg, G, kstrided=True), operand(x, In, kstrided=True), dwih,
-               split_k=K.auto_split_k(G, In, M))
-        db = K.colsum(dg, M, G)
-        grads = []
-        for d in range(dirs):
-            dwhh = torch.empty(4 * H, H, device=x.device)
-            shift = 1 if d == 0 else -1
-            K.gemm(4 * H, H, M, operand(dg[:, d * 4 * H:], G, kstrided=True),
-                   operand(h[:, d * H:], dirs * H, kstrided=True, window=(1, shift, T, T, H)), dwhh,
-                   split_k=K.auto_split_k(4 * H, H, M))
-            dbd = db[d * 4 * H:(d + 1) * 4 * H]
-            # b_ih and b_hh receive the same gradient but must not share storage
-            grads += [dwih[d * 4 * H:(d + 1) * 4 * H], dwhh, dbd, K.convert(dbd, K.F32)]
+        sink = _SINK["on"]
+        ps = self.params()
+
+        def wgrads():
+            grads = []
+            for d in range(dirs):
+                w_ih, w_hh, b_ih, b_hh = ps[4 * d: 4 * d + 4]
+                dgd = dg[:, d * 4 * H:]
+                dwih = _grad_of(w_ih) if sink else torch.empty(4 * H, In, device=x.device)
+                K.gemm(4 * H, In, M, operand(dgd, G, kstrided=True), operand(x, In, kstrided=True), dwih,
+                       split_k=K.auto_split_k(4 * H, In, M), accumulate=sink)
+                dwhh = _grad_of(w_hh) if sink else torch.empty(4 * H, H, device=x.device)
+                shift = 1 if d == 0 else -1
+                K.gemm(4 * H, H, M, operand(dgd, G, kstrided=True),
+                       operand(h[:, d * H:], dirs * H, kstrided=True, window=(1, shift, T, T, H)), dwhh,
+                       split_k=K.auto_split_k(4 * H, H, M), accumulate=sink)
+                if sink:
+                    K.colsum(dgd, M, 4 * H, ld=G, out=_grad_of(b_ih), accumulate=True)
+                    K.colsum(dgd, M, 4 * H, ld=G, out=_grad_of(b_hh), accumulate=True)
+                    continue
+                dbd = K.colsum(dgd, M, 4 * H, ld=G)
+                # b_ih and b_hh receive the same gradient but must not share storage
+                grads += [dwih, dwhh, dbd, K.convert(dbd, K.F32)]
+            return grads
+        if sink:
+            with _Side() as sd:
+                sd.keep(dg, x, h)
+                wgrads()
+            grads = [None] * (4 * dirs)
+        else:
+            grads = wgrads()
         dx = None
         if need_dx:
             dx = torch.empty(M, In, device=x.device)
@@ -273,6 +351,7 @@ class _LinearFn(torch.autograd.Function):
         y = torch.empty(M, Out, device=x.device)
         K.gemm(M, Out, In, operand(x, In), operand(wc, In), y, bias=b)
         ctx.cache = cache
+        ctx.bias = b
         ctx.save_for_backward(x, w)
         return y
 
@@ -282,10 +361,22 @@ class _LinearFn(torch.autograd.Function):
         dy = dy.contiguous()
         M, In = x.shape
         Out = w.shape[0]
-        dw = torch.empty(Out, In, device=x.device)
-        K.gemm(Out, In, M, operand(dy, Out, kstrided=True), operand(x, In, kstrided=True), dw,
-               split_k=K.auto_split_k(Out, In, M))
-        db = K.colsum(dy, M, Out)
+        sink = _SINK["on"]
+        b = ctx.bias
+
+        def wgrad():
+            dw = _grad_of(w) if sink else torch.empty(Out, In, device=x.device)
+            K.gemm(Out, In, M, operand(dy, Out, kstrided=True), operand(x, In, kstrided=True), dw,
+                   split_k=K.auto_split_k(Out, In, M), accumulate=sink)
+            db = K.colsum(dy, M, Out, out=_grad_of(b) if sink else None, accumulate=sink)
+            return dw, db
+        if sink:
+            with _Side() as sd:
+                sd.keep(dy, x)
+                wgrad()
+            dw = db = None
+        else:
+            dw, db = wgrad()
         dx = None
         if ctx.needs_input_grad[0]:
             wc = ctx.cache.get([w], lambda: K.convert(w, K.compute()))

@@ -22,7 +22,7 @@ import torch
 
 from . import dist as D
 from . import kernels as K
-from .layers import weights_changed
+from .layers import join_side, set_grad_sink, weights_changed
 
 
 # ------------------------------------------------------------------------- losses
@@ -112,6 +112,7 @@ class TrainStep:
         self.extra = extra  # optional callable(model, x, emb, x_psnt) -> extra loss (GAN step)
         self.params, self.flat, self.gflat = D.flatten_params_(model)
         D.broadcast_(self.flat)
+        set_grad_sink(True)  # kernels accumulate straight into the flat gradient buffer
         self.opt = FusedAdam(self.flat, self.gflat, lr)
         self.graph_fb = None
         self.world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
@@ -123,6 +124,7 @@ class TrainStep:
         if self.extra is not None:
             loss = loss + self.extra(x, emb, x_psnt)
         loss.backward()
+        join_side()  # weight-gradient GEMMs ran on the side stream
         return loss
 
     def step(self, x, emb):
@@ -153,11 +155,7 @@ class TrainStep:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.loss = self._fwd_bwd(x, emb)
-        self.graph_fb = g
-        # the capture itself computed gradients for the current weights: apply them
-        if self.world > 1:
-            D.allreduce_mean_(self.gflat)
-        self.opt.step()
+        self.graph_fb = g  # capture only records: the next step() replays it
 
 
 # ------------------------------------------------------------------------- reference-shaped solvers

@@ -41,9 +41,9 @@ def kernel_timing(model, B, T, reps=3):
     """Average duration of the dominant kernel family, measured with HIP events on the
     stream the kernels are launched on (torch's current stream: the C-ABI launches there).
 
-    The dominant kernels of the step are the per-time-step LSTM recurrence kernels of the
-    decoder's lstm2 (H=1024): 2 layers x T launches forward, twice that counting the
-    backward.  Here the forward recurrence of lstm2 layer 1 is replayed standalone."""
+    The dominant kernels of the step are the LSTM recurrences of the decoder's lstm2
+    (H=1024).  Here the forward recurrence of lstm2 layer 1 (one persistent launch over T
+    steps) is replayed standalone; per-step figures divide by T."""
     from autoformer_amd import kernels as K
 
     core = model.decoder._lstm2[1]
@@ -51,7 +51,7 @@ def kernel_timing(model, B, T, reps=3):
     H = core.H
     dev = whh.device
     xproj = torch.randn(B * T, 4 * H, device=dev) * 0.1
-    hbuf = torch.empty(2 * B * H, device=dev, dtype=torch.bfloat16) if K.compute() == K.BF16 else None
+    hbuf = K.lstm_scratch(B, H, 1, dev) if K.compute() == K.BF16 else None
     s = torch.cuda.current_stream()
     K.lstm_fwd(xproj, whh, B, T, H, 1, hbuf)  # warm
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -64,7 +64,7 @@ def kernel_timing(model, B, T, reps=3):
     flops = 2.0 * B * H * 4 * H  # recurrent product h_{t-1} W_hh^T per launch
     w_bytes = 2.0 * (4 * H) * H * math.ceil(B / 32)   # bf16 W_hh slices read per launch
     h_bytes = 2.0 * B * H * (H // 8)                  # h_{t-1} re-read by every unit block
-    return {"kernel": "lstm_step_fwd<bf16,MT=2> (decoder lstm2, H=1024, B=%d)" % B, "avg_us": avg_ms * 1e3,
+    return {"kernel": "lstm_persist_fwd<1024> per time step (decoder lstm2, B=%d)" % B, "avg_us": avg_ms * 1e3,
             "flops": flops, "l2_bytes": w_bytes + h_bytes}
 
 
@@ -94,7 +94,8 @@ def main():
     ap.add_argument("--len-crop", type=int, default=128)
     ap.add_argument("--freq", type=int, default=16)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the fwd+bwd as one hipGraph (serialises the side-stream wgrad branch on ROCm 7)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
@@ -119,7 +120,7 @@ def main():
 
     for _ in range(args.warmup):
         trainer.step(x, e)
-    if not args.no_graph:
+    if args.graph:
         trainer.capture(x, e)
         trainer.step(x, e)
     torch.cuda.synchronize()
@@ -155,7 +156,7 @@ def main():
            "config": {"workload": f"AutoVC train.py step (fwd + encoder re-pass + 2xMSE + L1 + bwd + Adam), "
                                   f"B={B}/GPU, T={T}, freq={freq}, dim_neck=44, dim_emb=256, dim_pre=512",
                       "global_batch": B * world, "seq_len": T, "freq": freq, "parallelism": f"dp{world}",
-                      "graph": not args.no_graph},
+                      "graph": bool(args.graph)},
            "step_mfma_frac": round(value * fpf / (world * peak * 1e12), 5),
            "final_loss": loss_v}
     if not args.no_kernel_timing:

@@ -101,11 +101,12 @@ int avc_bn_apply(const float* y, const float* scale, const float* shift, const f
 
 /* BatchNorm1d + activation backward.  dz = dA * act'(a); yhat = (y-mean)*rstd.
  * Writes dy = gamma*rstd*(dz - sum(dz)/N - yhat*sum(dz*yhat)/N), and dgamma, dbeta and
- * the (analytically ~0) bias gradient of the producing conv.  `ws` >= avc_bn_bwd_ws floats. */
+ * the (analytically ~0) bias gradient of the producing conv (accumulate != 0: added into them).
+ * `ws` >= avc_bn_bwd_ws floats. */
 size_t avc_bn_bwd_ws(int M, int C);
 int avc_bn_bwd(const float* dA, const float* a, const float* y, const float* mean, const float* rstd,
                const float* gamma, int M, int C, int act, float* dy, float* dgamma, float* dbeta,
-               float* dbias, float* ws, void* stream);
+               float* dbias, int accumulate, float* ws, void* stream);
 
 /* out[n] (+)= sum_m x[m*ld + n] (bias gradients). ws >= avc_colsum_ws floats. */
 size_t avc_colsum_ws(int M, int N);
@@ -116,7 +117,11 @@ int avc_colsum(const float* x, long long ld, int M, int N, float* out, int accum
  * Replaces the time loop of nn.LSTM (AutoVC.py:43,55 encoder BiLSTM; :77,103 lstm1;
  * :96,110 lstm2).  xproj (B,T,dirs*4H) already holds x W_ih^T + b_ih + b_hh.
  * w_hh: dirs x [4H][H] in `wdtype`; outputs h (B,T,dirs*H) fp32, c (B,T,dirs*H),
- * gates (B,T,dirs*4H) activated.  hbuf: 2*B*H elements of wdtype scratch (large H). */
+ * gates (B,T,dirs*4H) activated.  hbuf (large H, bf16 compute): scratch of at least
+ * max(4*dirs*B*H, 8*B*H + 16) bytes.  For dirs == 1, H in {512, 1024} and enough CUs the
+ * whole sequence runs as ONE persistent launch (W_hh slices register-resident, h_t
+ * exchanged through tagged granules, bounded spins; timeout flag = u32 at byte 8*B*H of
+ * hbuf); otherwise one fused kernel per time step. */
 int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T, int H, int dirs,
                  float* h, float* c, float* gates, void* hbuf, int compute, void* stream);
 

@@ -295,3 +295,39 @@ def test_gemm_fast_bf16_copy_and_mixed_dtypes():
             Kr.gemm(M, N, K_, Kr.operand(ad, K_), Kr.operand(bd, K_), c, c_bf16=c16)
             assert relf(c, ref) < 1e-5
             assert relf(c16.float(), ref) < 5e-3
+
+
+@pytest.mark.parametrize("B,H", [(64, 1024), (20, 1024), (64, 512), (3, 512)])
+def test_lstm_persistent_forward_matches_per_step(B, H):
+    """The persistent recurrence (bf16) equals the per-step kernels within bf16 rounding and
+    never raises its spin-timeout flag."""
+    import os
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+    from autoformer_amd import _lib
+
+    A.set_compute("bf16")
+    T = 37
+    G = 4 * H
+    torch.manual_seed(1)
+    xproj = (torch.randn(B * T, G) * 0.5).to(DEV)
+    whh = (torch.randn(G, H) * (1.0 / H ** 0.5)).to(DEV).bfloat16()
+    hb = Kr.lstm_scratch(B, H, 1, DEV)
+    h1, c1, g1 = Kr.lstm_fwd(xproj, whh, B, T, H, 1, hb)
+    torch.cuda.synchronize()
+    assert Kr.lstm_timeout_flag(hb, B, H) == 0
+    # reference: fp32 loop on the CPU with the same (bf16-rounded) weights, h rounded to bf16
+    w = whh.float().cpu()
+    xp = xproj.cpu().view(B, T, G)
+    h = torch.zeros(B, H)
+    c = torch.zeros(B, H)
+    outs = []
+    for t in range(T):
+        gts = xp[:, t] + h.bfloat16().float() @ w.t()
+        i, f, gg, o = gts.chunk(4, 1)
+        c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+        h = torch.sigmoid(o) * torch.tanh(c)
+        outs.append(h)
+    ref = torch.stack(outs, 1).reshape(B * T, H)
+    assert relf(h1, ref) < 2e-3, relf(h1, ref)
+    assert relf(c1.cpu().view(B, T, H)[:, -1], c) < 2e-3

@@ -129,3 +129,63 @@ def test_encoder_list_api_and_eval_mode(golden):
     with torch.no_grad():
         mel, psnt, c = m(x, e, e)
     assert torch.isfinite(psnt).all()
+
+
+def test_trainstep_sink_graph_matches_plain_autograd(golden):
+    """TrainStep (flat buffers, gradient sink + side stream, fused Adam, hipGraph replay)
+    reproduces the reference Solver's 3-step losses in fp32 compute."""
+    from autoformer_amd.train import TrainStep
+    from autoformer_amd.layers import set_grad_sink
+
+    g = golden("autovc_T176.npz")
+    m = _model(int(g["freq"]))
+    ts = TrainStep(m, lr=1e-4)
+    try:
+        got = []
+        for i in range(3):
+            x = torch.from_numpy(g[f"adam_x{i}"]).to(DEV)
+            e = torch.from_numpy(g[f"adam_e{i}"]).to(DEV)
+            ts.step(x, e)
+            torch.cuda.synchronize()
+        # losses of the reference Solver are recorded before each step's update; recompute ours
+        # by re-running the three steps on a fresh model and reading the fused losses
+    finally:
+        set_grad_sink(False)
+    m2 = _model(int(g["freq"]))
+    ts2 = TrainStep(m2, lr=1e-4)
+    try:
+        from autoformer_amd.train import vc_losses
+        for i in range(3):
+            x = torch.from_numpy(g[f"adam_x{i}"]).to(DEV)
+            e = torch.from_numpy(g[f"adam_e{i}"]).to(DEV)
+            _, parts, _ = vc_losses(m2, x, e)
+            got.append([p.item() for p in parts])
+            ts2.step(x, e)
+    finally:
+        set_grad_sink(False)
+    np.testing.assert_allclose(np.array(got), g["adam_losses"], rtol=2e-3)
+    for (n, p), (_, p2) in zip(m.named_parameters(), m2.named_parameters()):
+        assert torch.allclose(p, p2, rtol=1e-4, atol=1e-6), n
+
+
+def test_trainstep_graph_replay_equals_eager():
+    from autoformer_amd.detinit import det_inputs
+    from autoformer_amd.layers import set_grad_sink
+    from autoformer_amd.train import TrainStep
+
+    x, e = det_inputs(4, 64, seed=3)
+    x, e = torch.from_numpy(x).to(DEV), torch.from_numpy(e).to(DEV)
+    ma, mb = _model(16, "bf16"), _model(16, "bf16")
+    ta, tb = TrainStep(ma), TrainStep(mb)
+    try:
+        for _ in range(3):
+            la = ta.step(x, e)
+        tb.step(x, e)
+        tb.capture(x, e, warmup=0)  # records only
+        tb.step(x, e)               # replay = step 2
+        lb = tb.step(x, e)          # replay = step 3
+        torch.cuda.synchronize()
+        assert abs(la.item() - lb.item()) <= 1e-3 * abs(la.item())
+        assert torch.allclose(ta.flat, tb.flat, rtol=1e-3, atol=1e-5)
+    finally:
+        set_grad_sink(False)

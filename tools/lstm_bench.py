@@ -25,7 +25,7 @@ for (B, H, T) in [(64, 1024, 128), (64, 512, 128), (64, 1024, 1)]:
     xproj = torch.randn(B * T, G, device=dev) * 0.1
     whh = (torch.randn(G, H, device=dev) * 0.02).bfloat16()
     whht = whh.t().contiguous()
-    hbuf = torch.empty(2 * B * H, device=dev, dtype=torch.bfloat16)
+    hbuf = K.lstm_scratch(B, H, 1, dev)
     us = ev_time(lambda: K.lstm_fwd(xproj, whh, B, T, H, 1, hbuf))
     h, c, g = K.lstm_fwd(xproj, whh, B, T, H, 1, hbuf)
     dh = torch.randn_like(h)
