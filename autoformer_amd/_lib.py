@@ -20,7 +20,7 @@ SOURCES = ["gemm.hip", "bn.hip", "lstm.hip", "elem.hip"]
 ABI_VERSION = 1
 
 F32, BF16 = 0, 1
-ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU = 0, 1, 2, 3, 4
+ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
 
 c_void_p, c_int, c_ll, c_float, c_size = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_size_t
 
@@ -71,6 +71,10 @@ _SIGS = {
     "avc_loss_grad": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_int, c_void_p, c_float, c_void_p]),
     "avc_adam": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_float, c_float, c_float, c_float, c_void_p,
                          c_void_p]),
+    "avc_act_fwd": (c_int, [c_void_p, c_void_p, c_ll, c_int, c_void_p]),
+    "avc_act_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p]),
+    "avc_bce_loss": (c_int, [c_void_p, c_ll, c_float, c_void_p, c_void_p]),
+    "avc_bce_grad": (c_int, [c_void_p, c_ll, c_float, c_void_p, c_void_p, c_int, c_void_p]),
 }
 
 _lib = None

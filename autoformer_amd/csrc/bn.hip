@@ -96,6 +96,16 @@ __global__ void bn_apply_kernel(const float* __restrict__ y, const float* __rest
   *reinterpret_cast<f32x4*>(out + e) = o;
 }
 
+__global__ void bn_apply1_kernel(const float* __restrict__ y, const float* __restrict__ scale,
+                                 const float* __restrict__ shift, const float* __restrict__ res, float* __restrict__ out,
+                                 long long total, int C, int act) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = (int)(i % C);
+  float o = act_fwd(y[i] * scale[c] + shift[c], act);
+  out[i] = res ? o + res[i] : o;
+}
+
 // backward reduce: per (row block of RB rows, 64 channels) partial sums of dz, dz*yhat, yhat.
 constexpr int RB = 128;
 __global__ void bn_bwd_reduce_kernel(const float* __restrict__ dA, const float* __restrict__ a,
@@ -176,6 +186,19 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ dA, const float* _
   *reinterpret_cast<f32x4*>(dy + e) = o;
 }
 
+__global__ void bn_bwd_apply1_kernel(const float* __restrict__ dA, const float* __restrict__ a,
+                                     const float* __restrict__ y, const float* __restrict__ mean,
+                                     const float* __restrict__ rstd, const float* __restrict__ coef, long long total,
+                                     int C, int act, float* __restrict__ dy) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = (int)(i % C);
+  const float* cf = coef + c * 3;
+  const float dz = act_bwd_from_out(dA[i], a[i], act);
+  const float yh = (y[i] - mean[c]) * rstd[c];
+  dy[i] = cf[0] * (dz - cf[1] - yh * cf[2]);
+}
+
 // column sums: partial per 128-row block, then finalize
 __global__ void colsum_partial_kernel(const float* x, long long ld, int M, int N, float* ws) {
   __shared__ float red[4][64];
@@ -229,10 +252,14 @@ extern "C" int avc_bn_stats(const float* y, long long ld, int M, int C, float* p
 
 extern "C" int avc_bn_apply(const float* y, const float* scale, const float* shift, const float* residual, float* out,
                             int M, int C, int act, void* stream) {
-  AVC_CHECK_ARG(y && scale && shift && out && C % 4 == 0, "avc_bn_apply: bad args (C %% 4 must be 0)");
-  long long total4 = (long long)M * C / 4;
-  if (total4 == 0) return 0;
-  bn_apply_kernel<<<cdiv(total4, 256), 256, 0, as_stream(stream)>>>(y, scale, shift, residual, out, total4, C, act);
+  AVC_CHECK_ARG(y && scale && shift && out && C > 0, "avc_bn_apply: bad args");
+  const long long total = (long long)M * C;
+  if (total == 0) return 0;
+  if (C % 4 == 0)
+    bn_apply_kernel<<<cdiv(total / 4, 256), 256, 0, as_stream(stream)>>>(y, scale, shift, residual, out, total / 4, C,
+                                                                        act);
+  else
+    bn_apply1_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(y, scale, shift, residual, out, total, C, act);
   return avc_check_launch("avc_bn_apply");
 }
 
@@ -241,7 +268,7 @@ extern "C" size_t avc_bn_bwd_ws(int M, int C) { return (size_t)cdiv(M, RB) * C *
 extern "C" int avc_bn_bwd(const float* dA, const float* a, const float* y, const float* mean, const float* rstd,
                           const float* gamma, int M, int C, int act, float* dy, float* dgamma, float* dbeta,
                           float* dbias, int accumulate, float* ws, void* stream) {
-  AVC_CHECK_ARG(dA && a && y && mean && rstd && dy && ws && C % 4 == 0, "avc_bn_bwd: bad args (C %% 4 must be 0)");
+  AVC_CHECK_ARG(dA && a && y && mean && rstd && dy && ws && C > 0, "avc_bn_bwd: bad args");
   hipStream_t s = as_stream(stream);
   const int nrb = cdiv(M, RB);
   dim3 grid(cdiv(C, 64), nrb);
@@ -249,8 +276,11 @@ extern "C" int avc_bn_bwd(const float* dA, const float* a, const float* y, const
   float* coef = ws + (size_t)nrb * C * 3;
   bn_bwd_finalize_kernel<<<cdiv(C, 256), 256, 0, s>>>(ws, nrb, M, C, gamma, rstd, coef, dgamma, dbeta, dbias,
                                                        accumulate);
-  long long total4 = (long long)M * C / 4;
-  bn_bwd_apply_kernel<<<cdiv(total4, 256), 256, 0, s>>>(dA, a, y, mean, rstd, coef, total4, C, act, dy);
+  const long long total = (long long)M * C;
+  if (C % 4 == 0)
+    bn_bwd_apply_kernel<<<cdiv(total / 4, 256), 256, 0, s>>>(dA, a, y, mean, rstd, coef, total / 4, C, act, dy);
+  else
+    bn_bwd_apply1_kernel<<<cdiv(total, 256), 256, 0, s>>>(dA, a, y, mean, rstd, coef, total, C, act, dy);
   return avc_check_launch("avc_bn_bwd");
 }
 

@@ -62,6 +62,7 @@ __device__ __forceinline__ float act_fwd(float x, int act) {
     case AVC_ACT_TANH: return tanhf(x);
     case AVC_ACT_LEAKY: return x > 0.f ? x : 0.01f * x;
     case AVC_ACT_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    case AVC_ACT_SIGMOID: return 1.f / (1.f + expf(-x));
     default: return x;
   }
 }
@@ -72,6 +73,7 @@ __device__ __forceinline__ float act_bwd_from_out(float g, float a, int act) {
     case AVC_ACT_RELU: return a > 0.f ? g : 0.f;
     case AVC_ACT_TANH: return g * (1.f - a * a);
     case AVC_ACT_LEAKY: return a > 0.f ? g : 0.01f * g;
+    case AVC_ACT_SIGMOID: return g * a * (1.f - a);
     default: return g;
   }
 }

@@ -204,6 +204,42 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   }
 }
 
+__global__ void act_fwd_kernel(const float* x, float* y, long long n, int act) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = act_fwd(x[i], act);
+}
+
+__global__ void act_bwd_kernel(const float* g, const float* yout, float* dx, long long n, int act) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dx[i] = act_bwd_from_out(g[i], yout[i], act);
+}
+
+// nn.BCELoss(mean) on probabilities p against a constant target; log clamped at -100
+__global__ void bce_kernel(const float* p, long long n, float target, float* out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float lp = fmaxf(logf(p[i]), -100.f), l1p = fmaxf(logf(1.f - p[i]), -100.f);
+    s += -(target * lp + (1.f - target) * l1p);
+  }
+  s = warp_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, (red[0] + red[1] + red[2] + red[3]) / (float)n);
+}
+
+// d BCE / d p (PyTorch: grad * (p - t) / max(p (1 - p), 1e-12) / n), chained through the
+// sigmoid that produced p when `through_sigmoid` (dlogit = dp * p (1 - p)).
+__global__ void bce_grad_kernel(const float* p, long long n, float target, const float* dloss, float* g,
+                                int through_sigmoid) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float pi = p[i];
+  float d = dloss[0] * (pi - target) / fmaxf((1.f - pi) * pi, 1e-12f) / (float)n;
+  if (through_sigmoid) d *= pi * (1.f - pi);
+  g[i] = d;
+}
+
 }  // namespace
 
 #define GRID1(n) dim3(cdiv((n), 256)), dim3(256), 0, as_stream(stream)
@@ -311,4 +347,32 @@ extern "C" int avc_adam(float* p, const float* g, float* m, float* v, long long 
   int grid = (int)std::min<long long>(4096, cdiv(n, 256));
   adam_kernel<<<grid, 256, 0, s>>>(p, g, m, v, n, beta1, beta2, eps, state);
   return avc_check_launch("avc_adam");
+}
+
+extern "C" int avc_act_fwd(const float* x, float* y, long long n, int act, void* stream) {
+  AVC_CHECK_ARG(x && y, "avc_act_fwd: null");
+  if (n == 0) return 0;
+  act_fwd_kernel<<<GRID1(n)>>>(x, y, n, act);
+  return avc_check_launch("avc_act_fwd");
+}
+
+extern "C" int avc_act_bwd(const float* g, const float* yout, float* dx, long long n, int act, void* stream) {
+  AVC_CHECK_ARG(g && yout && dx, "avc_act_bwd: null");
+  if (n == 0) return 0;
+  act_bwd_kernel<<<GRID1(n)>>>(g, yout, dx, n, act);
+  return avc_check_launch("avc_act_bwd");
+}
+
+extern "C" int avc_bce_loss(const float* p, long long n, float target, float* out, void* stream) {
+  AVC_CHECK_ARG(p && out && n > 0, "avc_bce_loss: bad args");
+  (void)hipMemsetAsync(out, 0, sizeof(float), as_stream(stream));
+  bce_kernel<<<(int)std::min<long long>(1024, cdiv(n, 256)), 256, 0, as_stream(stream)>>>(p, n, target, out);
+  return avc_check_launch("avc_bce_loss");
+}
+
+extern "C" int avc_bce_grad(const float* p, long long n, float target, const float* dloss, float* g,
+                            int through_sigmoid, void* stream) {
+  AVC_CHECK_ARG(p && dloss && g, "avc_bce_grad: null");
+  bce_grad_kernel<<<GRID1(n)>>>(p, n, target, dloss, g, through_sigmoid);
+  return avc_check_launch("avc_bce_grad");
 }

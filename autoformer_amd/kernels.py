@@ -12,7 +12,7 @@ import os
 import torch
 
 from . import _lib as L
-from ._lib import ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_TANH, BF16, F32  # noqa: F401
+from ._lib import ACT_GELU, ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, BF16, F32  # noqa: F401
 
 _COMPUTE = {"bf16": BF16, "fp32": F32}[os.environ.get("AUTOVC_COMPUTE", "bf16")]
 
@@ -286,3 +286,28 @@ def loss_grad(a, b, dloss, mode, sign):
 def adam(p, g, m, v, lr, beta1, beta2, eps, state):
     L.call("avc_adam", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), float(lr), float(beta1),
            float(beta2), float(eps), state.data_ptr(), stream())
+
+
+def act_fwd(x, act, out=None):
+    out = torch.empty_like(x) if out is None else out
+    L.call("avc_act_fwd", x.data_ptr(), out.data_ptr(), x.numel(), int(act), stream())
+    return out
+
+
+def act_bwd(g, yout, act):
+    dx = torch.empty_like(g)
+    L.call("avc_act_bwd", g.data_ptr(), yout.data_ptr(), dx.data_ptr(), g.numel(), int(act), stream())
+    return dx
+
+
+def bce_loss(p, target):
+    out = torch.empty((), device=p.device)
+    L.call("avc_bce_loss", p.data_ptr(), p.numel(), float(target), out.data_ptr(), stream())
+    return out
+
+
+def bce_grad(p, target, dloss, through_sigmoid=False):
+    g = torch.empty_like(p)
+    L.call("avc_bce_grad", p.data_ptr(), p.numel(), float(target), dloss.data_ptr(), g.data_ptr(),
+           int(through_sigmoid), stream())
+    return g

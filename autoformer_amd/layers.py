@@ -95,6 +95,42 @@ def _need(t):
     return t is not None and t.requires_grad
 
 
+# =============================================================================== plain conv helpers
+def conv_packs(cache, w):
+    """(Wf [Co][Kw*Ci], Wd [Ci][Kw*Co]) in the compute dtype, rebuilt when w changes."""
+    def build():
+        dt = K.compute()
+        return K.conv_pack(w, 0, dt), K.conv_pack(w, 1, dt)
+    return cache.get([w], build)
+
+
+def conv_fwd(x, B, T_in, w, bias, pad, Wf, out=None):
+    """Conv1d(stride 1) on frame-major x (B*T_in, Ci) -> (B*T_out, Co), T_out."""
+    Co, Ci, Kw = w.shape
+    T_out = T_in + 2 * pad - Kw + 1
+    y = torch.empty(B * T_out, Co, device=x.device) if out is None else out
+    K.gemm(B * T_out, Co, Kw * Ci, operand(x, Ci, window=(Kw, pad, T_out, T_in, Ci)), operand(Wf, Kw * Ci), y,
+           bias=bias)
+    return y, T_out
+
+
+def conv_wgrad(dy, x, B, T_in, T_out, w, pad, into=None):
+    Co, Ci, Kw = w.shape
+    M = B * T_out
+    dWf = torch.empty(Co, Kw * Ci, device=x.device)
+    K.gemm(Co, Kw * Ci, M, operand(dy, Co, kstrided=True),
+           operand(x, Ci, kstrided=True, window=(Kw, pad, T_out, T_in, Ci)), dWf, split_k=K.auto_split_k(Co, Kw * Ci, M))
+    return K.conv_grad_unpack(dWf, Co, Ci, Kw, into=into)
+
+
+def conv_dgrad(dy, B, T_in, T_out, w, pad, Wd, n_dx=None):
+    Co, Ci, Kw = w.shape
+    n_dx = Ci if n_dx is None else n_dx
+    dx = torch.empty(B * T_in, n_dx, device=dy.device)
+    K.gemm(B * T_in, n_dx, Kw * Co, operand(dy, Co, window=(Kw, Kw - 1 - pad, T_in, T_out, Co)), operand(Wd, Kw * Co), dx)
+    return dx
+
+
 # =============================================================================== conv + BN
 class ConvBNCore:
     """ConvNorm (Norm.py:4-37) + BatchNorm1d + activation, frame-major.

@@ -62,6 +62,39 @@ class _L1Fn(torch.autograd.Function):
         return ga, gb
 
 
+class _BCEFn(torch.autograd.Function):
+    """nn.BCELoss(mean) against a constant target (train_with_discriminator.py:58-61)."""
+
+    @staticmethod
+    def forward(ctx, p, target):
+        p = p.contiguous()
+        ctx.save_for_backward(p)
+        ctx.target = float(target)
+        return K.bce_loss(p, target)
+
+    @staticmethod
+    def backward(ctx, g):
+        (p,) = ctx.saved_tensors
+        return K.bce_grad(p, ctx.target, g.contiguous()), None
+
+
+def bce_loss(p, target):
+    return _BCEFn.apply(p, target)
+
+
+def discriminator_loss(real, fake):
+    """train_with_discriminator.py:58-61."""
+    return bce_loss(real, 1.0) + bce_loss(fake, 0.0)
+
+
+def gan_extra(D):
+    """Extra loss term of the two-model step (train_with_discriminator.py:102-107):
+    d_loss = BCE(D(x_real), 1) + BCE(D(x_identic_psnt.squeeze()), 0), added to the G loss."""
+    def extra(x_real, emb, x_psnt):
+        return discriminator_loss(D(x_real), D(x_psnt.squeeze()))
+    return extra
+
+
 def mse_loss(a, b):
     return _MSEFn.apply(a, b.reshape(a.shape))
 
@@ -106,11 +139,14 @@ class TrainStep:
     With world > 1 the gradients are averaged by RCCL between backward and Adam; the
     whole step minus the collective is captured in hipGraphs once `capture()` is called."""
 
-    def __init__(self, model, lr=1e-4, lambda_cd=1.0, extra=None):
+    def __init__(self, model, lr=1e-4, lambda_cd=1.0, extra=None, extra_modules=()):
         self.model = model
         self.lambda_cd = lambda_cd
-        self.extra = extra  # optional callable(model, x, emb, x_psnt) -> extra loss (GAN step)
-        self.params, self.flat, self.gflat = D.flatten_params_(model)
+        self.extra = extra  # optional callable(x, emb, x_psnt) -> extra loss (GAN step)
+        # one flat buffer (and one fused Adam) over every module: Adam is elementwise, so this
+        # equals the reference's separate g_optimizer / d_optimizer with the same settings
+        owner = torch.nn.ModuleList([model, *extra_modules]) if extra_modules else model
+        self.params, self.flat, self.gflat = D.flatten_params_(owner)
         D.broadcast_(self.flat)
         set_grad_sink(True)  # kernels accumulate straight into the flat gradient buffer
         self.opt = FusedAdam(self.flat, self.gflat, lr)

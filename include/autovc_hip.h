@@ -31,7 +31,7 @@ extern "C" {
 #define AVC_ABI_VERSION 1
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
-enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4 };
+enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
 
 /* One GEMM operand, logically an R x K matrix (R = M for A, N for B).
  *   kstrided = 0 : element (r, k) at ptr[r*ld + k]   (K contiguous)
@@ -162,6 +162,17 @@ int avc_l1_loss(const float* a, const float* b, long long n, float* out, void* s
 /* g = scale * dL * (mode 0: 2(a-b)/n ; mode 1: sign(a-b)/n) ; dL = *dloss (device) */
 int avc_loss_grad(const float* a, const float* b, long long n, const float* dloss, int mode, float* g,
                   float sign, void* stream);
+
+/* Activation-only passes (Discriminator's conv -> LeakyReLU -> BN order,
+ * factory/Discriminator.py:18-29); the backward takes the activation OUTPUT. */
+int avc_act_fwd(const float* x, float* y, long long n, int act, void* stream);
+int avc_act_bwd(const float* g, const float* yout, float* dx, long long n, int act, void* stream);
+
+/* nn.BCELoss (mean) against a constant target (train_with_discriminator.py:58-61); the
+ * gradient optionally chained through the Sigmoid that produced p. */
+int avc_bce_loss(const float* p, long long n, float target, float* out, void* stream);
+int avc_bce_grad(const float* p, long long n, float target, const float* dloss, float* g,
+                 int through_sigmoid, void* stream);
 
 /* Fused Adam (torch.optim.Adam defaults, train.py:49,99) over one flat fp32 buffer.
  * state[0] = step count (float), updated on device (graph-replayable). */

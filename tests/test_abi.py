@@ -59,12 +59,29 @@ def test_argument_validation_without_gpu(lib):
         _lib.check(rc, "avc_gemm")
 
 
-def test_struct_layout_matches_header():
+def test_struct_layout_matches_header(tmp_path):
+    """Field offsets of the ctypes structs == what a C compiler makes of include/autovc_hip.h."""
+    import subprocess
+
     from autoformer_amd import _lib
 
-    # avc_operand: ptr(8) int int ll ll int*5 (+pad) -> 56 bytes on x86-64
-    assert ctypes.sizeof(_lib.Operand) == 56
-    assert ctypes.sizeof(_lib.GemmDesc) == 4 * 4 + 2 * 56 + 8 + 8 + 8 + 8 + 4 + 4 + 8 + 4 + 4
+    fields = {"avc_operand": [f[0] for f in _lib.Operand._fields_], "avc_gemm_desc": [f[0] for f in _lib.GemmDesc._fields_]}
+    src = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
+    for st, fs in fields.items():
+        src.append(f'printf("{st} %zu\\n", sizeof({st}));')
+        for f in fs:
+            src.append(f'printf("{st}.{f} %zu\\n", offsetof({st}, {f}));')
+    src.append("return 0;}")
+    c = tmp_path / "probe.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", str(c), "-o", str(exe)], check=True)
+    out = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                               check=True).stdout.split("\n") if line)
+    for st, cls in (("avc_operand", _lib.Operand), ("avc_gemm_desc", _lib.GemmDesc)):
+        assert int(out[st]) == ctypes.sizeof(cls), st
+        for f in fields[st]:
+            assert int(out[f"{st}.{f}"]) == getattr(cls, f).offset, (st, f)
 
 
 def test_product_path_does_not_import_oracle():
