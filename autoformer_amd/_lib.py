@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must precede the HIP library)
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["gemm.hip", "bn.hip", "lstm.hip", "elem.hip"]
+SOURCES = ["gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip"]
 ABI_VERSION = 1
 
 F32, BF16 = 0, 1
@@ -34,7 +34,7 @@ class GemmDesc(ctypes.Structure):
     _fields_ = [("M", c_int), ("N", c_int), ("K", c_int), ("batch", c_int), ("a", Operand), ("b", Operand),
                 ("c", c_void_p), ("ldc", c_ll), ("c_batch_stride", c_ll), ("bias", c_void_p),
                 ("accumulate", c_int), ("split_k", c_int), ("bn_partial", c_void_p), ("compute", c_int),
-                ("c_bf16", c_void_p)]
+                ("c_bf16", c_void_p), ("residual", c_void_p)]
 
 
 _SIGS = {
@@ -75,6 +75,19 @@ _SIGS = {
     "avc_act_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p]),
     "avc_bce_loss": (c_int, [c_void_p, c_ll, c_float, c_void_p, c_void_p]),
     "avc_bce_grad": (c_int, [c_void_p, c_ll, c_float, c_void_p, c_void_p, c_int, c_void_p]),
+    "avc_norm_ws": (c_size, [c_int, c_int]),
+    "avc_group_norm_fwd": (c_int, [c_void_p, c_int, c_ll, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
+                                   c_void_p, c_void_p]),
+    "avc_group_norm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_ll, c_int, c_void_p,
+                                   c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "avc_layer_norm_fwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
+                                   c_void_p, c_void_p]),
+    "avc_layer_norm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                   c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "avc_gelu_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_void_p]),
+    "avc_pool3_mixer": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "avc_patchify": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "avc_transpose_batched": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
 }
 
 _lib = None

@@ -28,6 +28,7 @@ struct GemmArgs {
   OpDev a, b;
   float* c;
   bf16* c16;
+  const float* res;
   long long ldc, cbs;
   const float* bias;
   int accumulate, atomic;
@@ -321,6 +322,7 @@ __global__ void __launch_bounds__(NT) gemm_generic_kernel(GemmArgs g) {
         if (col >= g.N) continue;
         float* p = C + (long long)row * g.ldc + col;
         float v = acc[i][j][e];
+        if (g.res && ks == 0) v += g.res[(long long)bz * g.cbs + (long long)row * g.ldc + col];
         if (g.atomic) atomicAdd(p, v);
         else if (g.accumulate) *p += v;
         else *p = v;
@@ -686,6 +688,7 @@ __global__ void __launch_bounds__(256, 2) gemm_fast_kernel(GemmArgs g) {
         if (col >= g.N) continue;
         const long long o = (long long)row * g.ldc + col;
         float v = acc[i][j][e];
+        if (g.res && ks == 0) v += g.res[(long long)bz * g.cbs + o];
         if (g.atomic) {
           atomicAdd(C + o, v);
         } else {
@@ -806,18 +809,23 @@ extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
   g.klen = kl > 0 ? kl : BK;
   g.c = d->c;
   g.c16 = reinterpret_cast<bf16*>(d->c_bf16);
+  g.res = d->residual;
   g.ldc = d->ldc;
   g.cbs = d->c_batch_stride;
   g.bias = d->bias;
   g.accumulate = d->accumulate;
-  g.atomic = g.split_k > 1;
+  // split-K partials, or a batch whose outputs all land in one C (c_batch_stride == 0: a sum
+  // over the batch, e.g. a weight gradient of a per-utterance product), accumulate atomically
+  g.atomic = g.split_k > 1 || (g.batch > 1 && d->c_batch_stride == 0);
   g.bn_partial = d->bn_partial;
   AVC_CHECK_ARG(!(g.bn_partial && (g.split_k > 1 || g.batch > 1 || d->accumulate)),
                 "avc_gemm: bn_partial needs split_k == 1, batch == 1, accumulate == 0");
   hipStream_t s = as_stream(stream);
+  AVC_CHECK_ARG(!(g.res && g.atomic && g.batch > 1 && d->c_batch_stride == 0),
+                "avc_gemm: residual with a batch-summed output is not supported");
   if (g.atomic && !d->accumulate) {
     long long tot = (long long)g.M * g.N;
-    dim3 zg(cdiv(tot, 256), g.batch);
+    dim3 zg(cdiv(tot, 256), d->c_batch_stride == 0 ? 1 : g.batch);
     zero2d_kernel<<<zg, 256, 0, s>>>(g.c, g.ldc, g.cbs, g.M, g.N);
   }
   const bool bf = d->compute == AVC_BF16;

@@ -70,8 +70,8 @@ def operand(t: torch.Tensor, ld: int, kstrided: bool = False, window=None, batch
 
 
 def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=None, accumulate=False, split_k=1,
-         bn_partial=None, batch=1, c_batch_stride=0, comp=None, c_bf16=None):
-    _dev(c, bias, bn_partial, c_bf16)
+         bn_partial=None, batch=1, c_batch_stride=0, comp=None, c_bf16=None, residual=None):
+    _dev(c, bias, bn_partial, c_bf16, residual)
     assert c.dtype == torch.float32
     d = L.GemmDesc()
     d.M, d.N, d.K, d.batch = int(M), int(N), int(K), int(batch)
@@ -85,6 +85,7 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     d.bn_partial = _ptr(bn_partial)
     d.compute = _COMPUTE if comp is None else comp
     d.c_bf16 = _ptr(c_bf16)
+    d.residual = _ptr(residual)
     L.check(L.lib().avc_gemm(d, stream()), "avc_gemm")
 
 
@@ -311,3 +312,70 @@ def bce_grad(p, target, dloss, through_sigmoid=False):
     L.call("avc_bce_grad", p.data_ptr(), p.numel(), float(target), dloss.data_ptr(), g.data_ptr(),
            int(through_sigmoid), stream())
     return g
+
+
+# ------------------------------------------------------------------------- MetaFormer blocks
+def _ws(rows, C, dev):
+    return torch.empty(int(L.lib().avc_norm_ws(rows, C)), device=dev)
+
+
+def group_norm_fwd(x, B, C, gamma, beta, eps):
+    S = x.numel() // B
+    y = torch.empty_like(x)
+    mean, rstd = torch.empty(B, device=x.device), torch.empty(B, device=x.device)
+    L.call("avc_group_norm_fwd", x.data_ptr(), B, S, C, _ptr(gamma), _ptr(beta), float(eps), y.data_ptr(),
+           mean.data_ptr(), rstd.data_ptr(), stream())
+    return y, mean, rstd
+
+
+def group_norm_bwd(dy, x, gamma, mean, rstd, B, C, dgamma=None, dbeta=None, accumulate=False):
+    S = x.numel() // B
+    dx = torch.empty_like(x)
+    L.call("avc_group_norm_bwd", dy.data_ptr(), x.data_ptr(), _ptr(gamma), mean.data_ptr(), rstd.data_ptr(), B, S, C,
+           dx.data_ptr(), _ptr(dgamma), _ptr(dbeta), int(accumulate), _ws(x.numel() // C, C, x.device).data_ptr(),
+           stream())
+    return dx
+
+
+def layer_norm_fwd(x, gamma, beta, eps):
+    R, D = x.shape
+    y = torch.empty_like(x)
+    mean, rstd = torch.empty(R, device=x.device), torch.empty(R, device=x.device)
+    L.call("avc_layer_norm_fwd", x.data_ptr(), R, D, _ptr(gamma), _ptr(beta), float(eps), y.data_ptr(),
+           mean.data_ptr(), rstd.data_ptr(), stream())
+    return y, mean, rstd
+
+
+def layer_norm_bwd(dy, x, gamma, mean, rstd, dgamma=None, dbeta=None, accumulate=False):
+    R, D = x.shape
+    dx = torch.empty_like(x)
+    L.call("avc_layer_norm_bwd", dy.data_ptr(), x.data_ptr(), _ptr(gamma), mean.data_ptr(), rstd.data_ptr(), R, D,
+           dx.data_ptr(), _ptr(dgamma), _ptr(dbeta), int(accumulate), _ws(R, D, x.device).data_ptr(), stream())
+    return dx
+
+
+def gelu_bwd(g, x):
+    dx = torch.empty_like(x)
+    L.call("avc_gelu_bwd", g.data_ptr(), x.data_ptr(), dx.data_ptr(), x.numel(), stream())
+    return dx
+
+
+def pool3_mixer(x, B, Lf, C, backward=False):
+    y = torch.empty_like(x)
+    L.call("avc_pool3_mixer", x.data_ptr(), y.data_ptr(), B, Lf, C, int(backward), stream())
+    return y
+
+
+def patchify(src, B, Lf, C, ps, backward=False):
+    if backward:
+        dst = torch.empty(B * Lf, C, device=src.device)
+    else:
+        dst = torch.empty(B * (C // ps) * (Lf // ps), ps * ps, device=src.device)
+    L.call("avc_patchify", src.data_ptr(), dst.data_ptr(), B, Lf, C, int(ps), int(backward), stream())
+    return dst
+
+
+def transpose_batched(src, B, R, C, out=None, accumulate=False):
+    dst = torch.empty(B * C * R, device=src.device) if out is None else out
+    L.call("avc_transpose_batched", src.data_ptr(), dst.data_ptr(), B, R, C, int(accumulate), stream())
+    return dst

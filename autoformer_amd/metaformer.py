@@ -1,0 +1,279 @@
+"""MetaFormer (MetaConv / MetaPool) autograd functions on HIP kernels.
+
+Frame-major convention as in layers.py: a reference (B, C, L) tensor is held as (B*L, C).
+The MetaFormer models switch which axis is "time" several times (the decoder runs convs
+with time as channels, MetaConv.py:162-179), so explicit batched transposes appear where
+the reference's conv axis changes.
+
+References:
+  MetaBlock      factory/MetaConv.py:8-76 (conv mixer), factory/MetaPool.py:18-77 (pool mixer)
+  GroupNorm(1)   factory/Norm.py:53-60
+  PatchEmbed     factory/Norm.py:63-82
+  MLPMixer       factory/MLPMixer.py:58-92 (depth 1, expansion 4, dropout 0)
+"""
+from __future__ import annotations
+
+import torch
+
+from . import kernels as K
+from . import layers as Lyr
+from .kernels import operand
+
+
+# ------------------------------------------------------------------------------ elementwise
+class _AddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        return K.add(a, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
+def add(a, b):
+    return _AddFn.apply(a, b)
+
+
+class _TransposeFn(torch.autograd.Function):
+    """(B, R, C) -> (B, C, R), both stored as 2-D row blocks."""
+
+    @staticmethod
+    def forward(ctx, x, B, R, C):
+        ctx.dims = (B, R, C)
+        return K.transpose_batched(x.contiguous(), B, R, C).view(B * C, R)
+
+    @staticmethod
+    def backward(ctx, g):
+        B, R, C = ctx.dims
+        return K.transpose_batched(g.contiguous(), B, C, R).view(B * R, C), None, None, None
+
+
+def transpose(x, B, R, C):
+    return _TransposeFn.apply(x, B, R, C)
+
+
+class _GroupNormFn(torch.autograd.Function):
+    """GroupNorm(1, C) on frame-major (B*L, C): per-sample statistics over all L*C values."""
+
+    @staticmethod
+    def forward(ctx, x, B, gamma, beta, eps):
+        C = x.shape[1]
+        y, mean, rstd = K.group_norm_fwd(x, B, C, gamma, beta, eps)
+        ctx.save_for_backward(x, gamma, mean, rstd)
+        ctx.B = B
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, gamma, mean, rstd = ctx.saved_tensors
+        C = x.shape[1]
+        dgamma = torch.empty(C, device=x.device)
+        dbeta = torch.empty(C, device=x.device)
+        dx = K.group_norm_bwd(g.contiguous(), x, gamma, mean, rstd, ctx.B, C, dgamma, dbeta)
+        return dx, None, dgamma, dbeta, None
+
+
+def group_norm(x, B, gn):
+    return _GroupNormFn.apply(x, B, gn.weight, gn.bias, gn.eps)
+
+
+class _PoolMixerFn(torch.autograd.Function):
+    """Pooling token mixer: AvgPool1d(3, 1, 1, count_include_pad=False)(x) - x (MetaPool.py:7-15)."""
+
+    @staticmethod
+    def forward(ctx, x, B, Lf):
+        ctx.dims = (B, Lf, x.shape[1])
+        return K.pool3_mixer(x, B, Lf, x.shape[1])
+
+    @staticmethod
+    def backward(ctx, g):
+        B, Lf, C = ctx.dims
+        return K.pool3_mixer(g.contiguous(), B, Lf, C, backward=True), None, None
+
+
+def pool_mixer(x, B, Lf):
+    return _PoolMixerFn.apply(x, B, Lf)
+
+
+# ------------------------------------------------------------------------------ plain conv
+class _ConvFn(torch.autograd.Function):
+    """Conv1d + bias (stride 1) on frame-major input (PatchEmbed, MLP-Mixer output conv)."""
+
+    @staticmethod
+    def forward(ctx, x, cache, B, T_in, pad, w, b):
+        Wf, _ = Lyr.conv_packs(cache, w)
+        y, T_out = Lyr.conv_fwd(x, B, T_in, w, b, pad, Wf)
+        ctx.cache, ctx.args = cache, (B, T_in, T_out, pad)
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        B, T_in, T_out, pad = ctx.args
+        dy = dy.contiguous()
+        dW = Lyr.conv_wgrad(dy, x, B, T_in, T_out, w, pad)
+        db = K.colsum(dy, B * T_out, w.shape[0])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            _, Wd = Lyr.conv_packs(ctx.cache, w)
+            dx = Lyr.conv_dgrad(dy, B, T_in, T_out, w, pad, Wd)
+        return dx, None, None, None, None, dW, db
+
+
+def conv(x, conv_mod, cache, B, T_in):
+    return _ConvFn.apply(x, cache, B, T_in, conv_mod.padding[0], conv_mod.weight, conv_mod.bias)
+
+
+class _EncEmbedFn(torch.autograd.Function):
+    """cat(mel, c_org broadcast) -> PatchEmbed conv (MetaConv.py:108-112); dL/dmel only."""
+
+    @staticmethod
+    def forward(ctx, mel2d, emb, cache, B, T, w, b):
+        if emb.requires_grad:
+            raise NotImplementedError("gradients w.r.t. the speaker embedding are not supported")
+        x = K.enc_concat(mel2d, emb, B, T)
+        Wf, _ = Lyr.conv_packs(cache, w)
+        y, _ = Lyr.conv_fwd(x, B, T, w, b, w.shape[-1] // 2, Wf)
+        ctx.cache, ctx.args, ctx.n_mel = cache, (B, T), mel2d.shape[1]
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        B, T = ctx.args
+        pad = w.shape[-1] // 2
+        dy = dy.contiguous()
+        dW = Lyr.conv_wgrad(dy, x, B, T, T, w, pad)
+        db = K.colsum(dy, B * T, w.shape[0])
+        dmel = None
+        if ctx.needs_input_grad[0]:
+            _, Wd = Lyr.conv_packs(ctx.cache, w)
+            dmel = Lyr.conv_dgrad(dy, B, T, T, w, pad, Wd, n_dx=ctx.n_mel)
+        return dmel, None, None, None, None, dW, db
+
+
+def enc_embed(mel2d, emb, proj, cache, B, T):
+    return _EncEmbedFn.apply(mel2d, emb, cache, B, T, proj.weight, proj.bias)
+
+
+# ------------------------------------------------------------------------------ MLP-Mixer
+def _lin(x, M, N, Kd, w, b=None, residual=None, out=None):
+    """y = x (M x Kd, row-major) . w^T (w: N x Kd) + b (+ residual)."""
+    y = torch.empty(M, N, device=x.device) if out is None else out
+    K.gemm(M, N, Kd, operand(x, Kd), operand(w, Kd), y, bias=b, residual=residual)
+    return y
+
+
+class _MLPMixerFn(torch.autograd.Function):
+    """MLPMixer(image C x L (rows = channels of the frame-major input), patch ps, dim D,
+    depth 1, out_dim O) -> frame-major (B*D, O)  [reference: (B, O, D)]."""
+
+    @staticmethod
+    def forward(ctx, nf, mix, B, Lf, *params):
+        (we, be, g1, b1n, w1, bb1, w2, bb2, g2, b2n, w3, bb3, w4, bb4, wc, bc) = params
+        C = nf.shape[1]
+        ps = mix.ps
+        NP = (C // ps) * (Lf // ps)
+        D = we.shape[0]
+        dev = nf.device
+        P = K.patchify(nf, B, Lf, C, ps)                       # (B*NP, ps^2)
+        Z = _lin(P, B * NP, D, ps * ps, we, be)                 # (B*NP, D)
+        Y1, m1, r1 = K.layer_norm_fwd(Z, g1, b1n, mix.ln_eps[0])
+        # token mixing: UT_b (D x 4NP) = Y1_b^T . W1^T + b1   (Conv1d(NP -> 4NP, k1) on (B, NP, D))
+        W1 = w1.view(4 * NP, NP)
+        W2 = w2.view(NP, 4 * NP)
+        UT = torch.empty(B * D, 4 * NP, device=dev)
+        K.gemm(D, 4 * NP, NP, operand(Y1, D, kstrided=True, batch_stride=NP * D), operand(W1, NP), UT, bias=bb1,
+               batch=B, c_batch_stride=D * 4 * NP)
+        V = K.act_fwd(UT, K.ACT_GELU)
+        RT = torch.empty(B * D, NP, device=dev)
+        K.gemm(D, NP, 4 * NP, operand(V, 4 * NP, batch_stride=D * 4 * NP), operand(W2, 4 * NP), RT, bias=bb2,
+               batch=B, c_batch_stride=D * NP)
+        Z1 = K.transpose_batched(RT, B, D, NP, out=K.convert(Z, K.F32), accumulate=True).view(B * NP, D)
+        Y2, m2, r2 = K.layer_norm_fwd(Z1, g2, b2n, mix.ln_eps[1])
+        U2 = _lin(Y2, B * NP, 4 * D, D, w3, bb3)
+        V2 = K.act_fwd(U2, K.ACT_GELU)
+        Z2 = _lin(V2, B * NP, D, 4 * D, w4, bb4, residual=Z1)
+        Z2T = K.transpose_batched(Z2, B, NP, D).view(B * D, NP)
+        Wf, _ = Lyr.conv_packs(mix.cache, wc)
+        out, _ = Lyr.conv_fwd(Z2T, B, D, wc, bc, wc.shape[-1] // 2, Wf)
+        ctx.mix, ctx.dims = mix, (B, Lf, C, ps, NP, D)
+        ctx.stats = (m1, r1, m2, r2)
+        ctx.save_for_backward(P, Z, Y1, UT, V, Z1, Y2, U2, V2, Z2T, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (P, Z, Y1, UT, V, Z1, Y2, U2, V2, Z2T, we, be, g1, b1n, w1, bb1, w2, bb2, g2, b2n, w3, bb3, w4, bb4, wc,
+         bc) = ctx.saved_tensors
+        mix = ctx.mix
+        B, Lf, C, ps, NP, D = ctx.dims
+        m1, r1, m2, r2 = ctx.stats
+        dev = dout.device
+        dout = dout.contiguous()
+        pad = wc.shape[-1] // 2
+        # output conv (NP -> O, k5) over the D frames
+        dwc = Lyr.conv_wgrad(dout, Z2T, B, D, D, wc, pad)
+        dbc = K.colsum(dout, B * D, wc.shape[0])
+        _, Wd = Lyr.conv_packs(mix.cache, wc)
+        dZ2T = Lyr.conv_dgrad(dout, B, D, D, wc, pad, Wd)
+        dZ2 = K.transpose_batched(dZ2T, B, D, NP).view(B * NP, D)
+        M = B * NP
+        # channel FF: Z2 = GELU(LN2(Z1) W3^T + b3) W4^T + b4 + Z1
+        dw4 = torch.empty_like(w4)
+        K.gemm(D, 4 * D, M, operand(dZ2, D, kstrided=True), operand(V2, 4 * D, kstrided=True), dw4,
+               split_k=K.auto_split_k(D, 4 * D, M))
+        db4 = K.colsum(dZ2, M, D)
+        dV2 = torch.empty(M, 4 * D, device=dev)
+        K.gemm(M, 4 * D, D, operand(dZ2, D), operand(w4, 4 * D, kstrided=True), dV2)
+        dU2 = K.gelu_bwd(dV2, U2)
+        dw3 = torch.empty_like(w3)
+        K.gemm(4 * D, D, M, operand(dU2, 4 * D, kstrided=True), operand(Y2, D, kstrided=True), dw3,
+               split_k=K.auto_split_k(4 * D, D, M))
+        db3 = K.colsum(dU2, M, 4 * D)
+        dY2 = torch.empty(M, D, device=dev)
+        K.gemm(M, D, 4 * D, operand(dU2, 4 * D), operand(w3, D, kstrided=True), dY2)
+        dg2 = torch.empty(D, device=dev)
+        db2n = torch.empty(D, device=dev)
+        dZ1 = K.add(dZ2, K.layer_norm_bwd(dY2, Z1, g2, m2, r2, dg2, db2n))
+        # token FF: Z1 = Z + (GELU(Y1^T W1^T + b1) W2^T + b2)^T   per utterance
+        W1 = w1.view(4 * NP, NP)
+        W2 = w2.view(NP, 4 * NP)
+        dRT = K.transpose_batched(dZ1, B, NP, D).view(B * D, NP)
+        dW2 = torch.empty(NP, 4 * NP, device=dev)
+        K.gemm(NP, 4 * NP, D, operand(dRT, NP, kstrided=True, batch_stride=D * NP),
+               operand(V, 4 * NP, kstrided=True, batch_stride=D * 4 * NP), dW2, batch=B, c_batch_stride=0)
+        dbb2 = K.colsum(dRT, B * D, NP)
+        dV = torch.empty(B * D, 4 * NP, device=dev)
+        K.gemm(B * D, 4 * NP, NP, operand(dRT, NP), operand(W2, 4 * NP, kstrided=True), dV)
+        dUT = K.gelu_bwd(dV, UT)
+        dW1 = torch.empty(4 * NP, NP, device=dev)
+        K.gemm(4 * NP, NP, D, operand(dUT, 4 * NP, kstrided=True, batch_stride=D * 4 * NP),
+               operand(Y1, D, batch_stride=NP * D), dW1, batch=B, c_batch_stride=0)
+        dbb1 = K.colsum(dUT, B * D, 4 * NP)
+        dY1T = torch.empty(B * D, NP, device=dev)
+        K.gemm(B * D, NP, 4 * NP, operand(dUT, 4 * NP), operand(W1, NP, kstrided=True), dY1T)
+        dY1 = K.transpose_batched(dY1T, B, D, NP).view(M, D)
+        dg1 = torch.empty(D, device=dev)
+        db1n = torch.empty(D, device=dev)
+        dZ = K.add(dZ1, K.layer_norm_bwd(dY1, Z, g1, m1, r1, dg1, db1n))
+        # patch embedding
+        pp = ps * ps
+        dwe = torch.empty_like(we)
+        K.gemm(D, pp, M, operand(dZ, D, kstrided=True), operand(P, pp, kstrided=True), dwe,
+               split_k=K.auto_split_k(D, pp, M))
+        dbe = K.colsum(dZ, M, D)
+        dnf = None
+        if ctx.needs_input_grad[0]:
+            dP = torch.empty(M, pp, device=dev)
+            K.gemm(M, pp, D, operand(dZ, D), operand(we, pp, kstrided=True), dP)
+            dnf = K.patchify(dP, B, Lf, C, ps, backward=True)
+        return (dnf, None, None, None, dwe, dbe, dg1, db1n, dW1.view_as(w1), dbb1, dW2.view_as(w2), dbb2, dg2, db2n,
+                dw3, dbb3, dw4, dbb4, dwc, dbc)
+
+
+def mlp_mixer(nf, mixer, B, Lf):
+    return _MLPMixerFn.apply(nf, mixer, B, Lf, *mixer.flat_params())

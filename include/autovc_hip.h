@@ -53,7 +53,8 @@ typedef struct {
 
 /* C[z][m][n] (+)= sum_k A(m,k) B(n,k) (+ bias[n]) ; fp32 C.
  * compute: AVC_BF16 -> bf16 MFMA 16x16x32 with fp32 accumulate; AVC_F32 -> exact fp32 MFMA.
- * split_k > 1 accumulates with fp32 atomics (C is zeroed first unless accumulate).
+ * split_k > 1 accumulates with fp32 atomics (C is zeroed first unless accumulate); so does a
+ * batch > 1 with c_batch_stride == 0 (the output is the SUM over the batch).
  * bn_partial (nullable, split_k == 1, batch == 1): per 128-row tile and column the
  *   pair (sum, M2 about the tile mean) of the stored values, layout [ceil(M/128)][N][2],
  *   the BatchNorm batch-statistics epilogue.  */
@@ -67,7 +68,8 @@ typedef struct {
   int split_k;
   float* bn_partial;
   int compute;
-  void* c_bf16; /* nullable: also store C rounded to bf16 (same ldc), for the next GEMM */
+  void* c_bf16;         /* nullable: also store C rounded to bf16 (same ldc), for the next GEMM */
+  const float* residual; /* nullable: C = A.B + bias + residual (same ldc / batch stride) */
 } avc_gemm_desc;
 
 int avc_abi_version(void);
@@ -173,6 +175,31 @@ int avc_act_bwd(const float* g, const float* yout, float* dx, long long n, int a
 int avc_bce_loss(const float* p, long long n, float target, float* out, void* stream);
 int avc_bce_grad(const float* p, long long n, float target, const float* dloss, float* g,
                  int through_sigmoid, void* stream);
+
+/* MetaFormer blocks (MetaConv.py:8-76, MetaPool.py:7-77, MLPMixer.py:16-92, Norm.py:53-60).
+ * GroupNorm(1, C) over each sample's S = L*C contiguous frame-major elements; LayerNorm
+ * over rows of D; backward passes write dx and (accumulate != 0: add into) dgamma/dbeta.
+ * ws >= avc_norm_ws(rows, C) floats. */
+size_t avc_norm_ws(int rows, int C);
+int avc_group_norm_fwd(const float* x, int B, long long S, int C, const float* gamma, const float* beta, float eps,
+                       float* y, float* mean, float* rstd, void* stream);
+int avc_group_norm_bwd(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
+                       int B, long long S, int C, float* dx, float* dgamma, float* dbeta, int accumulate, float* ws,
+                       void* stream);
+int avc_layer_norm_fwd(const float* x, int R, int D, const float* gamma, const float* beta, float eps, float* y,
+                       float* mean, float* rstd, void* stream);
+int avc_layer_norm_bwd(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
+                       int R, int D, float* dx, float* dgamma, float* dbeta, int accumulate, float* ws, void* stream);
+/* exact (erf) GELU backward from the GELU input x; the forward is avc_act_fwd(AVC_ACT_GELU). */
+int avc_gelu_bwd(const float* g, const float* x, float* dx, long long n, void* stream);
+/* y = AvgPool1d(3,1,1,count_include_pad=False)(x) - x along the frames of (B, L, C);
+ * backward != 0 maps dy -> dx instead. */
+int avc_pool3_mixer(const float* x, float* y, int B, int L, int C, int backward, void* stream);
+/* Rearrange('b c (h p1) (w p2) -> b (h w) (p1 p2 c)') of the (C x L) image held frame-major
+ * as (B, L, C) (image rows = channels); backward != 0 scatters a patch gradient back. */
+int avc_patchify(const float* src, float* dst, int B, int L, int C, int ps, int backward, void* stream);
+/* dst[b] (+)= src[b]^T for B row-major R x C matrices. */
+int avc_transpose_batched(const float* src, float* dst, int B, int R, int C, int accumulate, void* stream);
 
 /* Fused Adam (torch.optim.Adam defaults, train.py:49,99) over one flat fp32 buffer.
  * state[0] = step count (float), updated on device (graph-replayable). */

@@ -110,3 +110,13 @@ def test_ops_refuse_cpu_tensors(lib):
     m = A.AutoVC(44, 256, 512, 22)
     with pytest.raises(RuntimeError):
         m(torch.zeros(2, 176, 80), torch.zeros(2, 256), torch.zeros(2, 256))
+
+
+@pytest.mark.parametrize("mod,cls", [("factory.MetaConv", "MetaConv"), ("factory.MetaPool", "MetaPool")])
+def test_metaformer_state_dict_layout_matches_reference(mod, cls):
+    import importlib
+    import json
+
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "state_dict_layout.json")))
+    m = getattr(importlib.import_module(mod), cls)(44, 256, 512, 22)
+    assert [[k, list(v.shape)] for k, v in m.state_dict().items()] == ref[cls]
