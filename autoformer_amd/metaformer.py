@@ -226,14 +226,14 @@ class _MLPMixerFn(torch.autograd.Function):
         dw4 = torch.empty_like(w4)
         K.gemm(D, 4 * D, M, operand(dZ2, D, kstrided=True), operand(V2, 4 * D, kstrided=True), dw4,
                split_k=K.auto_split_k(D, 4 * D, M))
-        db4 = K.colsum(dZ2, M, D)
+        dbb4 = K.colsum(dZ2, M, D)
         dV2 = torch.empty(M, 4 * D, device=dev)
         K.gemm(M, 4 * D, D, operand(dZ2, D), operand(w4, 4 * D, kstrided=True), dV2)
         dU2 = K.gelu_bwd(dV2, U2)
         dw3 = torch.empty_like(w3)
         K.gemm(4 * D, D, M, operand(dU2, 4 * D, kstrided=True), operand(Y2, D, kstrided=True), dw3,
                split_k=K.auto_split_k(4 * D, D, M))
-        db3 = K.colsum(dU2, M, 4 * D)
+        dbb3 = K.colsum(dU2, M, 4 * D)
         dY2 = torch.empty(M, D, device=dev)
         K.gemm(M, D, 4 * D, operand(dU2, 4 * D), operand(w3, D, kstrided=True), dY2)
         dg2 = torch.empty(D, device=dev)

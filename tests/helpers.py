@@ -9,10 +9,12 @@ def rel_inf(a, b):
     return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
 
 
-def grad_mismatches(model, g, tol=1e-2, bn_fed_bias=lambda n: "conv.bias" in n and "postnet.convolutions.4" not in n):
-    """Per-parameter check against the golden gradient norm and first-64-element head.
-    Conv biases feeding a training-mode BatchNorm have an analytically zero gradient: only an
-    absolute floor applies to them."""
+def grad_mismatches(model, g, tol=1e-2, head_tol=1e-2,
+                    bn_fed_bias=lambda n: "conv.bias" in n and "postnet.convolutions.4" not in n):
+    """Per-parameter check against the golden gradient norm (rel <= tol) and first-64-element
+    head (max abs error <= head_tol * max|head|).  Parameters whose true gradient is
+    analytically zero (conv biases feeding a training-mode BatchNorm; `bn_fed_bias`) get an
+    absolute floor only: their golden values are fp32 rounding noise."""
     bad = {}
     for name, p in model.named_parameters():
         ref_n = float(g["gnorm/" + name])
@@ -20,9 +22,9 @@ def grad_mismatches(model, g, tol=1e-2, bn_fed_bias=lambda n: "conv.bias" in n a
         head = g["ghead/" + name].astype(np.float64)
         err = np.abs(got.reshape(-1)[:64].numpy() - head).max()
         if bn_fed_bias(name):
-            ok = err < 1e-6 + tol * np.abs(head).max()
+            ok = err < 1e-6 + head_tol * np.abs(head).max()
         else:
-            ok = abs(got.norm().item() - ref_n) <= tol * ref_n + 1e-6 and err <= tol * max(np.abs(head).max(), 1e-6)
+            ok = abs(got.norm().item() - ref_n) <= tol * ref_n + 1e-6 and err <= head_tol * max(np.abs(head).max(), 1e-6)
         if not ok:
             bad[name] = (got.norm().item(), ref_n, err)
     return bad

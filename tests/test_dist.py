@@ -1,0 +1,78 @@
+"""Data-parallel plumbing (dist.py) with world_size 2 on gloo, CPU only: rendezvous from the
+torchrun-style environment, parameter flattening, rank-0 broadcast, bucketed gradient mean."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from autoformer_amd import dist as D
+
+    try:
+        r, w, local = D.init_from_env("gloo")
+        assert (r, w, local) == (rank, world, rank)
+        torch.manual_seed(100 + rank)  # ranks start from different weights
+        m = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.Conv1d(5, 3, 3))
+        params, flat, gflat = D.flatten_params_(m, device=torch.device("cpu"))
+        assert flat.numel() == sum(p.numel() for p in m.parameters())
+        assert all(p.data_ptr() >= flat.data_ptr() for p in params)
+        D.broadcast_(flat)
+        # gradients: rank-dependent, averaged in 3 small buckets (bucket_bytes=64 -> 16 floats)
+        gflat.copy_(torch.arange(gflat.numel(), dtype=torch.float32) * (rank + 1))
+        D.allreduce_mean_(gflat, bucket_bytes=64)
+        q.put((rank, flat.clone(), gflat.clone(), m[0].weight.grad.clone()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # surface worker failures to the parent
+        q.put((rank, repr(e), None, None))
+        raise
+
+
+@pytest.mark.timeout(120)
+def test_dp_broadcast_and_allreduce_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        rank, flat, gflat, g0 = q.get(timeout=100)
+        assert not isinstance(flat, str), flat
+        res[rank] = (flat, gflat, g0)
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=0, atol=0)  # weights identical after broadcast
+    n = res[0][1].numel()
+    expect = torch.arange(n, dtype=torch.float32) * 1.5  # mean of (1x, 2x)
+    for r in (0, 1):
+        torch.testing.assert_close(res[r][1], expect)
+        torch.testing.assert_close(res[r][2].reshape(-1), expect[:35])  # .grad views the flat buffer
+
+
+def test_single_process_is_a_noop(monkeypatch):
+    from autoformer_amd import dist as D
+
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    assert D.init_from_env("gloo") == (0, 1, 0)
+    g = torch.ones(10)
+    D.allreduce_mean_(g)
+    D.broadcast_(g)
+    assert torch.equal(g, torch.ones(10))

@@ -96,12 +96,13 @@ def test_pool_mixer_fwd_bwd(B, L, C):
     dy = _t(B * L, C, seed=8)
     y = MF.pool_mixer(x, B, L)
     y.backward(dy)
-    xr = x.detach().clone().requires_grad_()
-    xb = _frames_to_bcl(xr, B, L)
+    # reference on the CPU in fp64 (contiguous (B, C, L) input)
+    xr = x.detach().cpu().double().requires_grad_()
+    xb = xr.view(B, L, C).transpose(1, 2).contiguous()
     yr = (F.avg_pool1d(xb, 3, 1, 1, count_include_pad=False) - xb).transpose(1, 2).reshape(B * L, C)
-    yr.backward(dy)
-    torch.testing.assert_close(y, yr, rtol=1e-6, atol=1e-6)
-    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-6, atol=1e-6)
+    yr.backward(dy.cpu().double())
+    torch.testing.assert_close(y.cpu().double(), yr, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(x.grad.cpu().double(), xr.grad, rtol=1e-6, atol=1e-6)
 
 
 @pytest.mark.parametrize("B,L,C,ps", [(2, 176, 176, 16), (2, 344, 344, 8), (1, 16, 8, 4)])
@@ -202,8 +203,16 @@ def test_metaformer_fp32_matches_reference_goldens(golden, kind):
     for o, k in zip(outs, ("mel", "mel_psnt", "codes", "codes_re")):
         assert rel_inf(o.detach().cpu(), g[k]) < 1e-3, k
     np.testing.assert_allclose([l.item() for l in losses], g["losses"], rtol=1e-4)
-    bad = grad_mismatches(m, g)
-    assert not bad, bad
+    # The reference's own fp32 gradients sit up to 1.4e-2 (head, relative to max|head|) and
+    # 4e-4 (norm) away from an fp64 evaluation of the same step (measured with the oracle in
+    # fp64), so heads are held to 5e-2 and norms to 1e-2.  Analytically-zero gradients: conv
+    # biases feeding a training-mode BN (incl. postnet.convolutions.4), and for MetaPool the
+    # GroupNorm bias norm1.bias (a per-channel constant is annihilated by pool(x) - x).
+    def zero_grad(n):
+        return "conv.bias" in n or (kind == "metapool" and n.endswith("norm1.bias"))
+
+    bad = grad_mismatches(m, g, tol=1e-2, head_tol=5e-2, bn_fed_bias=zero_grad)
+    assert not bad, sorted(bad.items())
     assert not bn_state_mismatches(m, g)
 
 
