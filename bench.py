@@ -37,35 +37,61 @@ def synthetic_batch(B, T, rank, device):
     return x.to(device), e.to(device)
 
 
-def kernel_timing(model, B, T, reps=3):
-    """Average duration of the dominant kernel family, measured with HIP events on the
-    stream the kernels are launched on (torch's current stream: the C-ABI launches there).
+DOMINANT = "lstm_step_bwd_bf<1024>"
+PEAK_HBM_GBS = 8000.0       # MI355X HBM3E (MI355X_MICROARCH.md)
 
-    The dominant kernels of the step are the LSTM recurrences of the decoder's lstm2
-    (H=1024).  Here the forward recurrence of lstm2 layer 1 (one persistent launch over T
-    steps) is replayed standalone; per-step figures divide by T."""
+
+def kernel_timing(model, B, T, reps=3):
+    """Average launch duration of the dominant fixed-shape kernel, timed with HIP events on
+    the stream it is launched on (the C-ABI launches on torch's current stream).
+
+    The kernel is lstm_step_bwd_bf<1024>: one backward time step of the decoder's lstm2
+    (H=1024, B=64), 256 launches per train step, the largest single-kernel share of the step
+    (profiles/r1_bench_kernel_stats.csv).  K.lstm_bwd launches it T times; per launch =
+    elapsed / T.  Algorithmic bytes per launch:
+      W_hh^T bf16 (4H*H*2) + dgates_{t+1} bf16 (B*4H*2) + gates fp32 (B*4H*4)
+      + dh, c_t, c_{t-1} fp32 (3*B*H*4) + dc read+write (2*B*H*4)
+      + dgates_t fp32 + bf16 writes (B*4H*6)."""
     from autoformer_amd import kernels as K
 
     core = model.decoder._lstm2[1]
-    wih, bsum, whh, whh_t = core.packs()
+    _, _, whh, whh_t = core.packs()
     H = core.H
     dev = whh.device
-    xproj = torch.randn(B * T, 4 * H, device=dev) * 0.1
-    hbuf = K.lstm_scratch(B, H, 1, dev) if K.compute() == K.BF16 else None
+    g = torch.Generator(device=dev).manual_seed(7)
+    dh = torch.randn(B * T, H, device=dev, generator=g) * 0.1
+    h = torch.randn(B * T, H, device=dev, generator=g) * 0.5
+    c = torch.randn(B * T, H, device=dev, generator=g) * 0.5
+    gates = torch.rand(B * T, 4 * H, device=dev, generator=g)
+    K.lstm_bwd(dh, h, c, gates, whh, whh_t, B, T, H, 1)  # warm
     s = torch.cuda.current_stream()
-    K.lstm_fwd(xproj, whh, B, T, H, 1, hbuf)  # warm
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(reps):
-        K.lstm_fwd(xproj, whh, B, T, H, 1, hbuf)
+        K.lstm_bwd(dh, h, c, gates, whh, whh_t, B, T, H, 1)
     e1.record(s)
     torch.cuda.synchronize()
-    avg_ms = e0.elapsed_time(e1) / (reps * T)  # per launch (one launch per time step)
-    flops = 2.0 * B * H * 4 * H  # recurrent product h_{t-1} W_hh^T per launch
-    w_bytes = 2.0 * (4 * H) * H * math.ceil(B / 32)   # bf16 W_hh slices read per launch
-    h_bytes = 2.0 * B * H * (H // 8)                  # h_{t-1} re-read by every unit block
-    return {"kernel": "lstm_persist_fwd<1024> per time step (decoder lstm2, B=%d)" % B, "avg_us": avg_ms * 1e3,
-            "flops": flops, "l2_bytes": w_bytes + h_bytes}
+    avg_us = e0.elapsed_time(e1) * 1e3 / (reps * T)
+    G = 4 * H
+    alg_bytes = G * H * 2 + B * G * 2 + B * G * 4 + 3 * B * H * 4 + 2 * B * H * 4 + B * G * 6
+    return {"kernel": DOMINANT + " (decoder lstm2 backward step, B=%d, H=%d)" % (B, H), "avg_us": avg_us,
+            "bytes": float(alg_bytes), "flops": 2.0 * B * G * H}
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/r*_pmc_traffic.json, written by tools/rocpd_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes, FETCH_SIZE doubled per MI355X_MICROARCH.md)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    data = json.load(open(files[-1]))["kernels"]
+    for name, e in data.items():
+        if kernel in name and "hbm_bytes_per_launch" in e:
+            return e["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    return None, None
 
 
 def cpu_baseline(B, T, freq, steps=2):
@@ -161,10 +187,12 @@ def main():
            "final_loss": loss_v}
     if not args.no_kernel_timing:
         kt = kernel_timing(model, B, T)
-        ach = kt["flops"] / (kt["avg_us"] * 1e-6) / 1e12
-        out["roofline"] = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
-                           "frac": round(ach / peak, 5), "traffic": None, "kernel": kt["kernel"],
-                           "avg_us": round(kt["avg_us"], 3)}
+        ach = kt["bytes"] / (kt["avg_us"] * 1e-6) / 1e9
+        traffic, src = pmc_traffic(DOMINANT)
+        out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                           "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": traffic, "kernel": kt["kernel"],
+                           "avg_us": round(kt["avg_us"], 3), "alg_bytes_per_launch": kt["bytes"],
+                           "flop_per_launch": kt["flops"], "traffic_source": src}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(B, T, freq)
     print(json.dumps(out), flush=True)
