@@ -104,11 +104,21 @@ def build(verbose: bool = False, force: bool = False) -> str:
             return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = LIB_PATH + ".tmp"
-    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-pass-failed",
-           "-o", tmp] + srcs
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True, cwd=CSRC)
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-pass-failed"]
+    objdir = os.path.join(HERE, "_build")
+    os.makedirs(objdir, exist_ok=True)
+    objs = [os.path.join(objdir, os.path.basename(p) + ".o") for p in srcs]
+    # one hipcc per translation unit, concurrently (the gfx950 device compile dominates)
+    procs = []
+    for src, obj in zip(srcs, objs):
+        cmd = [hipcc] + flags + ["-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((cmd, subprocess.Popen(cmd, cwd=CSRC)))
+    failed = [cmd for cmd, pr in procs if pr.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs, check=True, cwd=CSRC)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
 

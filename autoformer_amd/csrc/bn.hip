@@ -12,37 +12,53 @@ namespace {
 
 constexpr int PTILE = 128;  // rows per partial (must match gemm.hip BM)
 
-__global__ void bn_finalize_kernel(const float* partial, int M, int C, const float* gamma, const float* beta,
-                                   float* rmean, float* rvar, long long* nbt, float momentum, float eps,
-                                   float* mean_out, float* rstd_out, float* scale, float* shift) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// One block per 64 channels; 4 row-groups of 64 threads stride over the per-tile partials
+// (independent loads, no serial chain).  Merge = two passes over the partials:
+//   mean = sum_t s_t / n;   M2 = sum_t [ q_t + n_t (s_t / n_t - mean)^2 ]   (Chan, parallel form)
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ partial, int M, int C,
+                                                          const float* gamma, const float* beta, float* rmean,
+                                                          float* rvar, long long* nbt, float momentum, float eps,
+                                                          float* mean_out, float* rstd_out, float* scale,
+                                                          float* shift) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
-  if (c >= C) return;
   const int nt = (M + PTILE - 1) / PTILE;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int t = 0; t < nt; ++t) {
-    double nb = (double)min(PTILE, M - t * PTILE);
-    double sb = partial[((long long)t * C + c) * 2 + 0];
-    double qb = partial[((long long)t * C + c) * 2 + 1];
-    double mb = sb / nb;
-    double tot = n + nb;
-    double d = mb - mean;
-    mean += d * nb / tot;
-    m2 += qb + d * d * n * nb / tot;
-    n = tot;
-  }
-  double var = m2 / n;
-  float rstd = (float)(1.0 / sqrt(var + (double)eps));
-  float g = gamma ? gamma[c] : 1.f;
-  float b = beta ? beta[c] : 0.f;
-  mean_out[c] = (float)mean;
+  const bool cv = c < C;
+  float s = 0.f;
+  if (cv)
+    for (int t = grp; t < nt; t += 4) s += partial[((long long)t * C + c) * 2];
+  red[grp][cl] = s;
+  __syncthreads();
+  const float n = (float)M;
+  const float mean = (red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]) / n;
+  __syncthreads();
+  float q = 0.f;
+  if (cv)
+    for (int t = grp; t < nt; t += 4) {
+      const float nb = (float)min(PTILE, M - t * PTILE);
+      const float d = partial[((long long)t * C + c) * 2] / nb - mean;
+      q += partial[((long long)t * C + c) * 2 + 1] + nb * d * d;
+    }
+  red[grp][cl] = q;
+  __syncthreads();
+  if (grp != 0 || !cv) return;
+  const float m2 = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+  const float var = m2 / n;
+  const float rstd = 1.f / sqrtf(var + eps);
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  mean_out[c] = mean;
   rstd_out[c] = rstd;
   scale[c] = g * rstd;
-  shift[c] = b - (float)mean * g * rstd;
+  shift[c] = b - mean * g * rstd;
   if (rmean) {
-    double unb = n > 1.0 ? m2 / (n - 1.0) : var;
-    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
-    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+    const float unb = n > 1.f ? m2 / (n - 1.f) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
   }
 }
 
@@ -106,11 +122,70 @@ __global__ void bn_apply1_kernel(const float* __restrict__ y, const float* __res
   out[i] = res ? o + res[i] : o;
 }
 
-// backward reduce: per (row block of RB rows, 64 channels) partial sums of dz, dz*yhat, yhat.
-constexpr int RB = 128;
-__global__ void bn_bwd_reduce_kernel(const float* __restrict__ dA, const float* __restrict__ a,
-                                     const float* __restrict__ y, const float* __restrict__ mean,
-                                     const float* __restrict__ rstd, int M, int C, int act, float* ws) {
+// backward reduce: per (64-row block, 64 channels) partial sums of dz, dz*yhat, yhat.
+// 256 threads = 16 channel quads (float4, one 256-B row segment) x 16 row lanes; the 4 rows
+// of a lane are loaded together (12 independent 16-B loads in flight per thread).
+constexpr int RB = 64;
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const float* __restrict__ dA, const float* __restrict__ a,
+                                                            const float* __restrict__ y,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd, int M, int C, int act,
+                                                            float* ws) {
+  __shared__ float red[3][16][65];
+  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + cq * 4;
+  const int r0 = blockIdx.y * RB;
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0;
+  if (c < C) {
+    const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + c);
+    const f32x4 rs = *reinterpret_cast<const f32x4*>(rstd + c);
+    f32x4 g[4], av[4], yv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = r0 + rl + 16 * i;
+      const long long idx = (long long)(r < M ? r : 0) * C + c;
+      g[i] = *reinterpret_cast<const f32x4*>(dA + idx);
+      av[i] = *reinterpret_cast<const f32x4*>(a + idx);
+      yv[i] = *reinterpret_cast<const f32x4*>(y + idx);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (r0 + rl + 16 * i >= M) continue;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float dz = act_bwd_from_out(g[i][k], av[i][k], act);
+        const float yh = (yv[i][k] - mu[k]) * rs[k];
+        s0[k] += dz;
+        s1[k] += dz * yh;
+        s2[k] += yh;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    red[0][rl][cq * 4 + k] = s0[k];
+    red[1][rl][cq * 4 + k] = s1[k];
+    red[2][rl][cq * 4 + k] = s2[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 192) {
+    const int q = threadIdx.x >> 6, cl = threadIdx.x & 63;
+    const int cc = blockIdx.x * 64 + cl;
+    if (cc < C) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) t += red[q][i][cl];
+      ws[((long long)blockIdx.y * C + cc) * 3 + q] = t;
+    }
+  }
+}
+
+// scalar variant (C % 4 != 0): 64 channels x 4 row lanes
+__global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const float* __restrict__ dA, const float* __restrict__ a,
+                                                             const float* __restrict__ y,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd, int M, int C, int act,
+                                                             float* ws) {
   __shared__ float red[3][4][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -120,9 +195,9 @@ __global__ void bn_bwd_reduce_kernel(const float* __restrict__ dA, const float* 
     const float mu = mean[c], rs = rstd[c];
     const int r1 = min(M, r0 + RB);
     for (int r = r0 + rl; r < r1; r += 4) {
-      long long idx = (long long)r * C + c;
-      float dz = act_bwd_from_out(dA[idx], a[idx], act);
-      float yh = (y[idx] - mu) * rs;
+      const long long idx = (long long)r * C + c;
+      const float dz = act_bwd_from_out(dA[idx], a[idx], act);
+      const float yh = (y[idx] - mu) * rs;
       s0 += dz;
       s1 += dz * yh;
       s2 += yh;
@@ -140,27 +215,38 @@ __global__ void bn_bwd_reduce_kernel(const float* __restrict__ dA, const float* 
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(const float* ws, int nrb, int M, int C, const float* gamma,
-                                       const float* rstd, float* coef, float* dgamma, float* dbeta, float* dbias,
-                                       int acc) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s0 = 0, s1 = 0, s2 = 0;
-  for (int b = 0; b < nrb; ++b) {
-    const float* p = ws + ((long long)b * C + c) * 3;
-    s0 += p[0];
-    s1 += p[1];
-    s2 += p[2];
-  }
+// one block per 64 channels, 4 row groups reduce the per-block partials in parallel
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ ws, int nrb, int M, int C,
+                                                              const float* gamma, const float* rstd, float* coef,
+                                                              float* dgamma, float* dbeta, float* dbias, int acc) {
+  __shared__ float red[3][4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+  if (c < C)
+    for (int b = grp; b < nrb; b += 4) {
+      const float* p = ws + ((long long)b * C + c) * 3;
+      s0 += p[0];
+      s1 += p[1];
+      s2 += p[2];
+    }
+  red[0][grp][cl] = s0;
+  red[1][grp][cl] = s1;
+  red[2][grp][cl] = s2;
+  __syncthreads();
+  if (grp != 0 || c >= C) return;
+  s0 = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+  s1 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+  s2 = red[2][0][cl] + red[2][1][cl] + red[2][2][cl] + red[2][3][cl];
   const float g = gamma ? gamma[c] : 1.f;
   const float k1 = g * rstd[c];
   const float invn = 1.f / (float)M;
   coef[c * 3 + 0] = k1;
-  coef[c * 3 + 1] = (float)s0 * invn;
-  coef[c * 3 + 2] = (float)s1 * invn;
-  const float gb = -k1 * (float)(s1 * s2) * invn;
-  if (dgamma) dgamma[c] = acc ? dgamma[c] + (float)s1 : (float)s1;
-  if (dbeta) dbeta[c] = acc ? dbeta[c] + (float)s0 : (float)s0;
+  coef[c * 3 + 1] = s0 * invn;
+  coef[c * 3 + 2] = s1 * invn;
+  const float gb = -k1 * s1 * s2 * invn;
+  if (dgamma) dgamma[c] = acc ? dgamma[c] + s1 : s1;
+  if (dbeta) dbeta[c] = acc ? dbeta[c] + s0 : s0;
   if (dbias) dbias[c] = acc ? dbias[c] + gb : gb;
 }
 
@@ -199,27 +285,68 @@ __global__ void bn_bwd_apply1_kernel(const float* __restrict__ dA, const float* 
   dy[i] = cf[0] * (dz - cf[1] - yh * cf[2]);
 }
 
-// column sums: partial per 128-row block, then finalize
-__global__ void colsum_partial_kernel(const float* x, long long ld, int M, int N, float* ws) {
-  __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+// column sums: partial per 64-row block (vectorised like bn_bwd_reduce when N % 4 == 0 and
+// ld % 4 == 0, scalar otherwise), then a parallel finalize.
+template <bool V4>
+__global__ void __launch_bounds__(256) colsum_partial_kernel(const float* __restrict__ x, long long ld, int M, int N,
+                                                             float* ws) {
+  __shared__ float red[16][65];
+  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
   const int r0 = blockIdx.y * RB;
-  float s = 0.f;
-  if (c < N) {
-    const int r1 = min(M, r0 + RB);
-    for (int r = r0 + rl; r < r1; r += 4) s += x[(long long)r * ld + c];
+  if constexpr (V4) {
+    const int c = blockIdx.x * 64 + cq * 4;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    if (c < N) {
+      f32x4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = r0 + rl + 16 * i;
+        v[i] = *reinterpret_cast<const f32x4*>(x + (long long)(r < M ? r : 0) * ld + c);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (r0 + rl + 16 * i < M) s += v[i];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[rl][cq * 4 + k] = s[k];
+  } else {
+    // 16 channels x 16 row lanes, each thread 4 channels strided by 16
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = blockIdx.x * 64 + cq + 16 * k;
+      float s = 0.f;
+      if (c < N)
+        for (int i = 0; i < 4; ++i) {
+          const int r = r0 + rl + 16 * i;
+          if (r < M) s += x[(long long)r * ld + c];
+        }
+      red[rl][cq + 16 * k] = s;
+    }
   }
-  red[rl][cl] = s;
   __syncthreads();
-  if (rl == 0 && c < N) ws[(long long)blockIdx.y * N + c] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+  if (threadIdx.x < 64) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c < N) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) t += red[i][threadIdx.x];
+      ws[(long long)blockIdx.y * N + c] = t;
+    }
+  }
 }
 
-__global__ void colsum_final_kernel(const float* ws, int nrb, int N, float* out, int accumulate) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
+__global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restrict__ ws, int nrb, int N, float* out,
+                                                           int accumulate) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (int b = 0; b < nrb; ++b) s += ws[(long long)b * N + c];
+  if (c < N)
+    for (int b = grp; b < nrb; b += 4) s += ws[(long long)b * N + c];
+  red[grp][cl] = s;
+  __syncthreads();
+  if (grp != 0 || c >= N) return;
+  s = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
   out[c] = accumulate ? out[c] + s : s;
 }
 
@@ -229,7 +356,7 @@ extern "C" int avc_bn_finalize(const float* partial, int M, int C, const float* 
                                float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
                                float* mean, float* rstd, float* scale, float* shift, void* stream) {
   AVC_CHECK_ARG(partial && mean && rstd && scale && shift && M > 0 && C > 0, "avc_bn_finalize: bad args");
-  bn_finalize_kernel<<<cdiv(C, 256), 256, 0, as_stream(stream)>>>(partial, M, C, gamma, beta, running_mean,
+  bn_finalize_kernel<<<cdiv(C, 64), 256, 0, as_stream(stream)>>>(partial, M, C, gamma, beta, running_mean,
                                                                    running_var, nbt, momentum, eps, mean, rstd,
                                                                    scale, shift);
   return avc_check_launch("avc_bn_finalize");
@@ -272,9 +399,13 @@ extern "C" int avc_bn_bwd(const float* dA, const float* a, const float* y, const
   hipStream_t s = as_stream(stream);
   const int nrb = cdiv(M, RB);
   dim3 grid(cdiv(C, 64), nrb);
-  bn_bwd_reduce_kernel<<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, M, C, act, ws);
+  if (C % 4 == 0 && aligned16(dA) && aligned16(a) && aligned16(y)) {
+    bn_bwd_reduce_kernel<<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, M, C, act, ws);
+  } else {
+    bn_bwd_reduce1_kernel<<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, M, C, act, ws);
+  }
   float* coef = ws + (size_t)nrb * C * 3;
-  bn_bwd_finalize_kernel<<<cdiv(C, 256), 256, 0, s>>>(ws, nrb, M, C, gamma, rstd, coef, dgamma, dbeta, dbias,
+  bn_bwd_finalize_kernel<<<cdiv(C, 64), 256, 0, s>>>(ws, nrb, M, C, gamma, rstd, coef, dgamma, dbeta, dbias,
                                                        accumulate);
   const long long total = (long long)M * C;
   if (C % 4 == 0)
@@ -291,7 +422,10 @@ extern "C" int avc_colsum(const float* x, long long ld, int M, int N, float* out
   AVC_CHECK_ARG(x && out && ws && ld >= N, "avc_colsum: bad args");
   hipStream_t s = as_stream(stream);
   const int nrb = cdiv(M, RB);
-  colsum_partial_kernel<<<dim3(cdiv(N, 64), nrb), 256, 0, s>>>(x, ld, M, N, ws);
-  colsum_final_kernel<<<cdiv(N, 256), 256, 0, s>>>(ws, nrb, N, out, accumulate);
+  if (N % 4 == 0 && ld % 4 == 0 && aligned16(x))
+    colsum_partial_kernel<true><<<dim3(cdiv(N, 64), nrb), 256, 0, s>>>(x, ld, M, N, ws);
+  else
+    colsum_partial_kernel<false><<<dim3(cdiv(N, 64), nrb), 256, 0, s>>>(x, ld, M, N, ws);
+  colsum_final_kernel<<<cdiv(N, 64), 256, 0, s>>>(ws, nrb, N, out, accumulate);
   return avc_check_launch("avc_colsum");
 }

@@ -49,3 +49,17 @@ case("wgrad TT bf16", 512, 2560, 8192, bf, bf, aks=True, bks=True, split=3)
 case("wgrad TT f32 nosplit", 512, 2560, 8192, f32, f32, aks=True, bks=True)
 case("dx NT(kstrided B) f32", 8192, 1024, 4096, f32, bf, bks=True)
 case("big square bf16", 4096, 4096, 4096, bf, bf)
+
+
+def torch_case(name, M, N, K_):
+    a = torch.randn(M, K_, device=dev).to(bf)
+    b = torch.randn(N, K_, device=dev).to(bf)
+    us = timeit(lambda: torch.matmul(a, b.t()))
+    print(f"{'hipBLASLt ' + name:40s} M={M:5d} N={N:5d} K={K_:5d}  {us:8.1f} us  {2*M*N*K_/us/1e6:7.1f} TFLOP/s", flush=True)
+
+
+torch_case("conv-shaped", 8192, 512, 2560)
+torch_case("xproj lstm2", 8192, 4096, 1024)
+torch_case("wgrad-shaped", 512, 2560, 8192)
+torch_case("big square", 4096, 4096, 4096)
+torch_case("lstm2 W_ih wgrad", 4096, 1024, 8192)
