@@ -16,8 +16,8 @@ import torch  # noqa: F401  (must precede the HIP library)
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip"]
-ABI_VERSION = 1
+SOURCES = ["gemm_nt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip"]
+ABI_VERSION = 2
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -46,16 +46,17 @@ _SIGS = {
     "avc_bn_eval": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p]),
     "avc_bn_stats": (c_int, [c_void_p, c_ll, c_int, c_int, c_void_p, c_void_p]),
-    "avc_bn_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "avc_bn_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                              c_void_p]),
     "avc_bn_bwd_ws": (c_size, [c_int, c_int]),
     "avc_bn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
-                           c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+                           c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "avc_colsum_ws": (c_size, [c_int, c_int]),
     "avc_colsum": (c_int, [c_void_p, c_ll, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "avc_lstm_fwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_int, c_void_p]),
     "avc_lstm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                             c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+                             c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "avc_enc_concat": (c_int, [c_void_p, c_ll, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_codes_gather": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_codes_scatter": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),

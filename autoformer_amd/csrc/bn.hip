@@ -94,7 +94,7 @@ __global__ void bn_stats_kernel(const float* y, long long ld, int M, int C, floa
 
 __global__ void bn_apply_kernel(const float* __restrict__ y, const float* __restrict__ scale,
                                 const float* __restrict__ shift, const float* __restrict__ res, float* __restrict__ out,
-                                long long total4, int C, int act) {
+                                bf16* __restrict__ out16, long long total4, int C, int act) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total4) return;
   long long e = i * 4;
@@ -110,16 +110,19 @@ __global__ void bn_apply_kernel(const float* __restrict__ y, const float* __rest
     o += r;
   }
   *reinterpret_cast<f32x4*>(out + e) = o;
+  if (out16) *reinterpret_cast<bf16x4*>(out16 + e) = bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
 }
 
 __global__ void bn_apply1_kernel(const float* __restrict__ y, const float* __restrict__ scale,
                                  const float* __restrict__ shift, const float* __restrict__ res, float* __restrict__ out,
-                                 long long total, int C, int act) {
+                                 bf16* __restrict__ out16, long long total, int C, int act) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int c = (int)(i % C);
   float o = act_fwd(y[i] * scale[c] + shift[c], act);
-  out[i] = res ? o + res[i] : o;
+  o = res ? o + res[i] : o;
+  out[i] = o;
+  if (out16) out16[i] = (bf16)o;
 }
 
 // backward reduce: per (64-row block, 64 channels) partial sums of dz, dz*yhat, yhat.
@@ -253,7 +256,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
 __global__ void bn_bwd_apply_kernel(const float* __restrict__ dA, const float* __restrict__ a,
                                     const float* __restrict__ y, const float* __restrict__ mean,
                                     const float* __restrict__ rstd, const float* __restrict__ coef, long long total4,
-                                    int C, int act, float* __restrict__ dy) {
+                                    int C, int act, float* __restrict__ dy, bf16* __restrict__ dy16) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total4) return;
   long long e = i * 4;
@@ -270,19 +273,22 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ dA, const float* _
     o[k] = cf[0] * (dz - cf[1] - yh * cf[2]);
   }
   *reinterpret_cast<f32x4*>(dy + e) = o;
+  if (dy16) *reinterpret_cast<bf16x4*>(dy16 + e) = bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
 }
 
 __global__ void bn_bwd_apply1_kernel(const float* __restrict__ dA, const float* __restrict__ a,
                                      const float* __restrict__ y, const float* __restrict__ mean,
                                      const float* __restrict__ rstd, const float* __restrict__ coef, long long total,
-                                     int C, int act, float* __restrict__ dy) {
+                                     int C, int act, float* __restrict__ dy, bf16* __restrict__ dy16) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int c = (int)(i % C);
   const float* cf = coef + c * 3;
   const float dz = act_bwd_from_out(dA[i], a[i], act);
   const float yh = (y[i] - mean[c]) * rstd[c];
-  dy[i] = cf[0] * (dz - cf[1] - yh * cf[2]);
+  const float o = cf[0] * (dz - cf[1] - yh * cf[2]);
+  dy[i] = o;
+  if (dy16) dy16[i] = (bf16)o;
 }
 
 // column sums: partial per 64-row block (vectorised like bn_bwd_reduce when N % 4 == 0 and
@@ -378,23 +384,26 @@ extern "C" int avc_bn_stats(const float* y, long long ld, int M, int C, float* p
 }
 
 extern "C" int avc_bn_apply(const float* y, const float* scale, const float* shift, const float* residual, float* out,
-                            int M, int C, int act, void* stream) {
+                            void* out_bf16, int M, int C, int act, void* stream) {
+  bf16* o16 = reinterpret_cast<bf16*>(out_bf16);
   AVC_CHECK_ARG(y && scale && shift && out && C > 0, "avc_bn_apply: bad args");
   const long long total = (long long)M * C;
   if (total == 0) return 0;
   if (C % 4 == 0)
-    bn_apply_kernel<<<cdiv(total / 4, 256), 256, 0, as_stream(stream)>>>(y, scale, shift, residual, out, total / 4, C,
-                                                                        act);
+    bn_apply_kernel<<<cdiv(total / 4, 256), 256, 0, as_stream(stream)>>>(y, scale, shift, residual, out, o16, total / 4,
+                                                                        C, act);
   else
-    bn_apply1_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(y, scale, shift, residual, out, total, C, act);
+    bn_apply1_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(y, scale, shift, residual, out, o16, total, C,
+                                                                      act);
   return avc_check_launch("avc_bn_apply");
 }
 
 extern "C" size_t avc_bn_bwd_ws(int M, int C) { return (size_t)cdiv(M, RB) * C * 3 + (size_t)C * 3; }
 
 extern "C" int avc_bn_bwd(const float* dA, const float* a, const float* y, const float* mean, const float* rstd,
-                          const float* gamma, int M, int C, int act, float* dy, float* dgamma, float* dbeta,
-                          float* dbias, int accumulate, float* ws, void* stream) {
+                          const float* gamma, int M, int C, int act, float* dy, void* dy_bf16, float* dgamma,
+                          float* dbeta, float* dbias, int accumulate, float* ws, void* stream) {
+  bf16* d16 = reinterpret_cast<bf16*>(dy_bf16);
   AVC_CHECK_ARG(dA && a && y && mean && rstd && dy && ws && C > 0, "avc_bn_bwd: bad args");
   hipStream_t s = as_stream(stream);
   const int nrb = cdiv(M, RB);
@@ -409,9 +418,9 @@ extern "C" int avc_bn_bwd(const float* dA, const float* a, const float* y, const
                                                        accumulate);
   const long long total = (long long)M * C;
   if (C % 4 == 0)
-    bn_bwd_apply_kernel<<<cdiv(total / 4, 256), 256, 0, s>>>(dA, a, y, mean, rstd, coef, total / 4, C, act, dy);
+    bn_bwd_apply_kernel<<<cdiv(total / 4, 256), 256, 0, s>>>(dA, a, y, mean, rstd, coef, total / 4, C, act, dy, d16);
   else
-    bn_bwd_apply1_kernel<<<cdiv(total, 256), 256, 0, s>>>(dA, a, y, mean, rstd, coef, total, C, act, dy);
+    bn_bwd_apply1_kernel<<<cdiv(total, 256), 256, 0, s>>>(dA, a, y, mean, rstd, coef, total, C, act, dy, d16);
   return avc_check_launch("avc_bn_bwd");
 }
 

@@ -10,30 +10,12 @@
 // 16x16 tiles.  Operands are staged global -> registers -> LDS (register staging lets
 // the loader apply the conv window / zero padding and the fp32->bf16 conversion), LDS is
 // double-buffered with one barrier per K-tile.
-#include "common.h"
+#include "gemm_internal.h"
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
-
-struct OpDev {
-  const void* ptr;
-  long long ld, bstride;
-  int dtype, win, vec, taps, pad, t_out, t_in, chans, rows;
-  FastDiv tdiv;
-};
-
-struct GemmArgs {
-  int M, N, K, batch, split_k, klen;
-  OpDev a, b;
-  float* c;
-  bf16* c16;
-  const float* res;
-  long long ldc, cbs;
-  const float* bias;
-  int accumulate, atomic;
-  float* bn_partial;
-};
+using namespace avcg;
+constexpr int BN = 128, BK = 32, NT = 256;
 
 template <bool BF>
 struct Traits;
@@ -418,6 +400,7 @@ int make_op(const avc_operand& o, int rows, int K, OpDev& d, const char* name) {
   d.chans = o.chans > 0 ? o.chans : 1;
   d.rows = rows;
   d.tdiv = make_fastdiv((uint32_t)d.t_out);
+  d.cdv = make_fastdiv((uint32_t)d.chans);
   if (d.win) {
     AVC_CHECK_ARG(o.t_out > 0 && o.t_in > 0 && o.chans > 0, "avc_gemm: operand %s window needs t_out/t_in/chans", name);
     int span = d.taps * d.chans;
@@ -439,7 +422,7 @@ int make_op(const avc_operand& o, int rows, int K, OpDev& d, const char* name) {
 // branches).  BK = 64, 2 LDS stages, 2 workgroups per CU, XCD-aware tile order.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-constexpr int FBK = 64, FLDK = FBK + 8;  // 144-byte LDS rows
+constexpr int FLDK = FBK + 8;  // 144-byte LDS rows
 constexpr unsigned FINVALID = 0x7FFFFFF0u;
 
 __device__ __forceinline__ unsigned pk2(float a, float b) {
@@ -662,95 +645,7 @@ __global__ void __launch_bounds__(256, 2) gemm_fast_kernel(GemmArgs g) {
     __syncthreads();
   }
 
-  // ---------------------------------------------------------------- epilogue
-  const int rbase = m0 + wm * 64 + 4 * (lane >> 4);
-  const int cbase = n0 + wn * WN + (lane & 15);
-  float* C = g.c + (long long)bz * g.cbs;
-  bf16* C16 = g.c16 ? g.c16 + (long long)bz * g.cbs : nullptr;
-  if (g.bias && ks == 0) {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int col = cbase + j * 16;
-      const float bv = col < g.N ? g.bias[col] : 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i][j] += bv;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = rbase + i * 16 + e;
-      if (row >= g.M) continue;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int col = cbase + j * 16;
-        if (col >= g.N) continue;
-        const long long o = (long long)row * g.ldc + col;
-        float v = acc[i][j][e];
-        if (g.res && ks == 0) v += g.res[(long long)bz * g.cbs + o];
-        if (g.atomic) {
-          atomicAdd(C + o, v);
-        } else {
-          if (g.accumulate) v += C[o];
-          C[o] = v;
-          if (C16) C16[o] = (bf16)v;
-        }
-      }
-    }
-  if (g.bn_partial) {
-    float* red = reinterpret_cast<float*>(smem_raw);  // [2][BN_] sums, then [2][BN_] M2
-    const int cnt = min(BM, g.M - m0);
-    float s[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) t += (rbase + i * 16 + e < g.M) ? acc[i][j][e] : 0.f;
-      t += __shfl_xor(t, 16, 64);
-      t += __shfl_xor(t, 32, 64);
-      s[j] = t;
-    }
-    __syncthreads();
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) red[wm * BN_ + wn * WN + j * 16 + lane] = s[j];
-    }
-    __syncthreads();
-    float qv[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int cl = wn * WN + j * 16 + (lane & 15);
-      const float mean = (red[cl] + red[BN_ + cl]) / (float)cnt;
-      float t = 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float d = acc[i][j][e] - mean;
-          t += (rbase + i * 16 + e < g.M) ? d * d : 0.f;
-        }
-      t += __shfl_xor(t, 16, 64);
-      t += __shfl_xor(t, 32, 64);
-      qv[j] = t;
-    }
-    float* red2 = red + 2 * BN_;
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) red2[wm * BN_ + wn * WN + j * 16 + lane] = qv[j];
-    }
-    __syncthreads();
-    if (tid < BN_) {
-      const int col = n0 + tid;
-      if (col < g.N) {
-        float* p = g.bn_partial + ((long long)mt * g.N + col) * 2;
-        p[0] = red[tid] + red[BN_ + tid];
-        p[1] = red2[tid] + red2[BN_ + tid];
-      }
-    }
-  }
+  fast_epilogue<BN_>(g, acc, m0, n0, mt, bz, ks, smem_raw);
 }
 
 template <int BN_, bool AKS, bool BKS, int ADT, int BDT>
@@ -835,6 +730,7 @@ extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
     int klf = (d->K + g.split_k - 1) / g.split_k;
     g.klen = ((klf + FBK - 1) / FBK) * FBK;
     if (g.klen <= 0) g.klen = FBK;
+    if (!aks && !bks && gemm_nt_launch(g, s)) return avc_check_launch("avc_gemm(nt)");
     const long long t128 = (long long)cdiv(g.M, BM) * cdiv(g.N, 128) * g.batch * g.split_k;
     const bool narrow = g.N <= 64 || t128 < 384;
     const int nb = narrow ? cdiv(g.M, BM) * cdiv(g.N, 64) * g.batch * g.split_k : (int)t128;

@@ -1,0 +1,137 @@
+// gemm_internal.h — device-side GEMM argument structs and the shared MFMA epilogue used by
+// the LDS-tiled kernels in gemm.hip and gemm_nt.hip (internal to libautovc_hip.so).
+#pragma once
+#include "common.h"
+
+namespace avcg {
+
+constexpr int BM = 128;                    // rows per workgroup tile (BN partial-stat tiles follow it)
+constexpr int FBK = 64;                    // K per LDS stage of the fast kernels
+
+struct OpDev {
+  const void* ptr;
+  long long ld, bstride;
+  int dtype, win, vec, taps, pad, t_out, t_in, chans, rows;
+  FastDiv tdiv;
+  FastDiv cdv;  // window: divide a K index by chans
+};
+
+struct GemmArgs {
+  int M, N, K, batch, split_k, klen;
+  OpDev a, b;
+  float* c;
+  bf16* c16;
+  const float* res;
+  long long ldc, cbs;
+  const float* bias;
+  int accumulate, atomic;
+  float* bn_partial;
+};
+
+
+// Accumulator layout shared by the fast kernels: 4 waves as 2 (M) x 2 (N); wave (wm, wn) owns
+// rows wm*64 + i*16 + 4*(lane>>4) + e and columns wn*BN_/2 + j*16 + (lane&15) of the tile.
+// Fused epilogue: bias, residual, accumulate / atomics (split-K, batch-sum), bf16 copy, and
+// BatchNorm partial statistics (per 128-row tile: column sum and M2 about the tile mean).
+template <int BN_>
+__device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4][BN_ / 32], int m0, int n0, int mt,
+                                              int bz, int ks, char* smem_raw) {
+  constexpr int NJ = BN_ / 32;
+  constexpr int WN = BN_ / 2;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int rbase = m0 + wm * 64 + 4 * (lane >> 4);
+  const int cbase = n0 + wn * WN + (lane & 15);
+  float* C = g.c + (long long)bz * g.cbs;
+  bf16* C16 = g.c16 ? g.c16 + (long long)bz * g.cbs : nullptr;
+  if (g.bias && ks == 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = cbase + j * 16;
+      const float bv = col < g.N ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] += bv;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = rbase + i * 16 + e;
+      if (row >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int col = cbase + j * 16;
+        if (col >= g.N) continue;
+        const long long o = (long long)row * g.ldc + col;
+        float v = acc[i][j][e];
+        if (g.res && ks == 0) v += g.res[(long long)bz * g.cbs + o];
+        if (g.atomic) {
+          atomicAdd(C + o, v);
+        } else {
+          if (g.accumulate) v += C[o];
+          C[o] = v;
+          if (C16) C16[o] = (bf16)v;
+        }
+      }
+    }
+  if (g.bn_partial) {
+    float* red = reinterpret_cast<float*>(smem_raw);  // [2][BN_] sums, then [2][BN_] M2
+    const int cnt = min(BM, g.M - m0);
+    float s[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t += (rbase + i * 16 + e < g.M) ? acc[i][j][e] : 0.f;
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      s[j] = t;
+    }
+    __syncthreads();
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) red[wm * BN_ + wn * WN + j * 16 + lane] = s[j];
+    }
+    __syncthreads();
+    float qv[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int cl = wn * WN + j * 16 + (lane & 15);
+      const float mean = (red[cl] + red[BN_ + cl]) / (float)cnt;
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = acc[i][j][e] - mean;
+          t += (rbase + i * 16 + e < g.M) ? d * d : 0.f;
+        }
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      qv[j] = t;
+    }
+    float* red2 = red + 2 * BN_;
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) red2[wm * BN_ + wn * WN + j * 16 + lane] = qv[j];
+    }
+    __syncthreads();
+    if (tid < BN_) {
+      const int col = n0 + tid;
+      if (col < g.N) {
+        float* p = g.bn_partial + ((long long)mt * g.N + col) * 2;
+        p[0] = red[tid] + red[BN_ + tid];
+        p[1] = red2[tid] + red2[BN_ + tid];
+      }
+    }
+  }
+}
+
+// Entry of the NT (both operands K-contiguous, bf16) LDS-DMA pipelined kernel (gemm_nt.hip).
+// Returns false when the shape/operands do not qualify (caller falls back).
+bool gemm_nt_launch(const GemmArgs& g, hipStream_t s);
+
+}  // namespace avcg

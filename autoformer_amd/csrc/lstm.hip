@@ -574,6 +574,47 @@ __device__ __forceinline__ unsigned long long granule(unsigned tag, float a, flo
   return ((unsigned long long)tag << 32) | (unsigned long long)__builtin_bit_cast(unsigned, h);
 }
 
+// Gather the group's tagged granules of one step into LDS rows of `ap` bf16 pairs
+// (row = idx / PER, pair = idx % PER for idx = tid + 256 i).  Loads are issued CH at a time
+// unconditionally (all in flight together: a per-granule branch around each load made the
+// compiler wait for every load in turn), then matched against the tag; late granules are
+// re-read with the whole chunk.  Returns false after a spin timeout (flag raised).
+template <int NGR, int PER, int CH>
+__device__ __forceinline__ bool gather_granules(const unsigned long long* src, bf16* lds, int ap,
+                                                unsigned long long need, unsigned tag, unsigned* flag) {
+  const int tid = threadIdx.x;
+  unsigned spins = 0;
+#pragma unroll
+  for (int c0 = 0; c0 < NGR; c0 += CH) {
+    while (true) {
+      unsigned long long v[CH];
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int idx = tid + 256 * (c0 + i), row = idx / PER, c2 = idx - row * PER;
+        // rows outside the batch are never needed: read row 0's slot instead (valid memory)
+        const int rr = ((need >> (c0 + i)) & 1ull) ? row : 0;
+        v[i] = __hip_atomic_load(src + (long long)rr * PER + c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int idx = tid + 256 * (c0 + i), row = idx / PER, c2 = idx - row * PER;
+        if (((need >> (c0 + i)) & 1ull) && (unsigned)(v[i] >> 32) == tag) {
+          reinterpret_cast<unsigned*>(lds + row * ap)[c2] = (unsigned)v[i];
+          need &= ~(1ull << (c0 + i));
+        }
+      }
+      const unsigned long long cm = (CH >= 64 ? ~0ull : ((1ull << CH) - 1ull)) << c0;
+      if (!(need & cm)) break;
+      if (++spins > PSPIN) {
+        atomicOr(flag, 1u);
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return true;
+}
+
 template <int H>
 __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
   constexpr int G = 4 * H, NK = H / 32, AP = H + 8, H2 = H / 2;
@@ -616,28 +657,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
     if (s > 0) {
       // ---- gather the group's h_{t-1} (tag == s) into the LDS A tile
       const unsigned long long* src = a.xbuf + (long long)((s - 1) & 1) * B * H2 + (long long)b0 * H2;
-      unsigned need = need0, spins = 0;
-      while (need) {
-#pragma unroll
-        for (int i = 0; i < NGR; ++i) {
-          if (!(need & (1u << i))) continue;
-          const int idx = tid + 256 * i, row = idx / H2, c2 = idx - row * H2;
-          const unsigned long long v =
-              __hip_atomic_load(src + (long long)row * H2 + c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((unsigned)(v >> 32) == (unsigned)s) {
-            reinterpret_cast<unsigned*>(As + row * AP)[c2] = (unsigned)v;
-            need &= ~(1u << i);
-          }
-        }
-        if (need) {
-          if (++spins > PSPIN) {
-            atomicOr(a.flag, 1u);
-            quit = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
+      if (!gather_granules<NGR, H2, 16>(src, As, AP, need0, (unsigned)s, a.flag)) quit = 1;
       __syncthreads();
       if (quit) return;  // block-uniform exit after a spin timeout
 #pragma unroll
@@ -679,6 +699,144 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
       gp[3 * H] = og;
     }
   }
+}
+
+// =============================================================== large H: persistent backward
+// One launch for all T steps of dirs == 1 (the decoder LSTMs).  Same decomposition as the
+// forward: group g = utterances [8g, 8g+8), member r = hidden units [32r, 32r+32).  The
+// recurrent product dh_rec[b][j] = sum_q dG_{t+1}[b][q] W_hh[q][j] runs over all 4H gate
+// rows q, so each member keeps W_hh^T[j0..j0+32][0..4H) in VGPRs (wave w = the K-block of
+// gate w, 2 x H/32 bf16x8 fragments) and gathers the group's whole dG_{t+1} (8 x 4H bf16)
+// into LDS each step from tagged granules {tag = step + 1, two bf16}.  The four waves'
+// partial products are summed through LDS; the cell-gradient carry dc stays in a register
+// of the thread that owns (b, j) for the whole sequence.  Outputs: dG (fp32) and its bf16
+// twin for the input-gradient / weight-gradient GEMMs.  Bounded spins as in the forward.
+struct PersistBwdArgs {
+  const float* dhout;  // (B,T,H)
+  const float* call;   // (B,T,H) cell states
+  const float* gall;   // (B,T,4H) activated gates i,f,g,o
+  const bf16* wt;      // W_hh^T [H][4H]
+  float* dg;           // (B,T,4H)
+  bf16* dg16;          // (B,T,4H) or null
+  unsigned long long* xbuf;  // [2][B][2H] granules, zeroed before launch
+  unsigned* flag;
+  int B, T, ng;
+};
+
+template <int H>
+__global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
+  constexpr int G = 4 * H, NK = H / 32, AP = G + 8, G2 = G / 2;
+  constexpr int NGR = PRG * G2 / 256;  // granules gathered per thread per step
+  static_assert(NGR <= 64, "gather mask is 64 bits");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16* As = reinterpret_cast<bf16*>(smem_raw);                          // [PRG + 1][AP], row PRG = zeros
+  float* red = reinterpret_cast<float*>(smem_raw + (PRG + 1) * AP * 2);  // [4][PRG][PJU + 1]
+  int* quit = reinterpret_cast<int*>(red + 4 * PRG * (PJU + 1));
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
+  const int j0 = r * PJU, b0 = g * PRG;
+  const int T = a.T, B = a.B;
+
+  // W_hh^T fragments: B operand of the product, n = unit j0 + 16n + (lane&15), k = gate row
+  bf16x8 wf[2][NK];
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const bf16* row = a.wt + (long long)(j0 + n * 16 + (lane & 15)) * G + w * H + 8 * (lane >> 4);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) wf[n][k] = *reinterpret_cast<const bf16x8*>(row + 32 * k);
+  }
+  for (int i = tid; i < (PRG + 1) * AP / 2; i += 256) reinterpret_cast<unsigned*>(As)[i] = 0u;
+  if (tid == 0) *quit = 0;
+  const int pr = tid >> 5, pu = tid & 31, pb = b0 + pr, pj = j0 + pu;
+  const bool pv = pb < B;
+  unsigned long long need0 = 0;
+#pragma unroll
+  for (int i = 0; i < NGR; ++i)
+    if (b0 + (tid + 256 * i) / G2 < B) need0 |= 1ull << i;
+  // MFMA A rows: 0..7 gathered utterances, 8..15 read the zero row
+  const int arow = (lane & 15) < PRG ? (lane & 15) : PRG;
+  float dc = 0.f;
+  __syncthreads();
+
+  for (int s = 0; s < T; ++s) {
+    const int t = T - 1 - s;
+    // per-element inputs of this step (independent of the exchange: issued first)
+    float dh = 0.f, ct = 0.f, cp = 0.f, gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f;
+    if (pv) {
+      const long long oh = ((long long)pb * T + t) * H + pj;
+      dh = a.dhout[oh];
+      ct = a.call[oh];
+      cp = t > 0 ? a.call[oh - H] : 0.f;
+      const float* gp = a.gall + ((long long)pb * T + t) * G + pj;
+      gi = gp[0];
+      gf = gp[H];
+      gg = gp[2 * H];
+      go = gp[3 * H];
+    }
+    if (s > 0) {
+      const unsigned long long* src = a.xbuf + (long long)((s - 1) & 1) * B * G2 + (long long)b0 * G2;
+      if (!gather_granules<NGR, G2, 16>(src, As, AP, need0, (unsigned)s, a.flag)) *quit = 1;
+      __syncthreads();
+      if (*quit) return;  // block-uniform exit after a spin timeout
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      const bf16* ap = As + arow * AP + w * H + 8 * (lane >> 4);
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(ap + 32 * k);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[0][k], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[1][k], acc1, 0, 0, 0);
+      }
+      // rows 4*(lane>>4)+e < 8 only for lanes 0..31
+      if (lane < 32) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          red[(w * PRG + 4 * (lane >> 4) + e) * (PJU + 1) + (lane & 15)] = acc0[e];
+          red[(w * PRG + 4 * (lane >> 4) + e) * (PJU + 1) + 16 + (lane & 15)] = acc1[e];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) dh += red[(ww * PRG + pr) * (PJU + 1) + pu];
+    }
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+    if (pv) {
+      const float tc = tanhf(ct);
+      const float dcs = dc + dh * go * (1.f - tc * tc);
+      v0 = dcs * gg * gi * (1.f - gi);        // d(pre i)
+      v1 = dcs * cp * gf * (1.f - gf);        // d(pre f)
+      v2 = dcs * gi * (1.f - gg * gg);        // d(pre g)
+      v3 = dh * tc * go * (1.f - go);         // d(pre o)
+      dc = dcs * gf;
+    }
+    const float n0 = __shfl_down(v0, 1, 64), n1 = __shfl_down(v1, 1, 64);
+    const float n2 = __shfl_down(v2, 1, 64), n3 = __shfl_down(v3, 1, 64);
+    if (pv && !(pu & 1) && s + 1 < T) {
+      unsigned long long* dst = a.xbuf + (long long)(s & 1) * B * G2 + (long long)pb * G2 + (pj >> 1);
+      const unsigned tag = (unsigned)(s + 1);
+      __hip_atomic_store(dst, granule(tag, v0, n0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(dst + H / 2, granule(tag, v1, n1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(dst + H, granule(tag, v2, n2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(dst + 3 * H / 2, granule(tag, v3, n3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (pv) {
+      const long long og = ((long long)pb * T + t) * G + pj;
+      a.dg[og] = v0;
+      a.dg[og + H] = v1;
+      a.dg[og + 2 * H] = v2;
+      a.dg[og + 3 * H] = v3;
+      if (a.dg16) {
+        a.dg16[og] = (bf16)v0;
+        a.dg16[og + H] = (bf16)v1;
+        a.dg16[og + 2 * H] = (bf16)v2;
+        a.dg16[og + 3 * H] = (bf16)v3;
+      }
+    }
+  }
+}
+
+template <int H>
+constexpr size_t persist_bwd_lds() {
+  return (size_t)(PRG + 1) * (4 * H + 8) * 2 + (size_t)4 * PRG * (PJU + 1) * 4 + 16;
 }
 
 int g_num_cus = -1;
@@ -778,8 +936,8 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
 }
 
 extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c, const float* gates, const void* w_hh,
-                            const void* w_hh_t, int wdtype, int B, int T, int H, int dirs, float* dgates, float* dcbuf,
-                            void* gbuf, int compute, void* stream) {
+                            const void* w_hh_t, int wdtype, int B, int T, int H, int dirs, float* dgates,
+                            void* dgates_bf16, float* dcbuf, void* gbuf, int compute, void* stream) {
   (void)h;
   AVC_CHECK_ARG(dh_out && c && gates && dgates && B > 0 && T > 0 && H > 0 && (dirs == 1 || dirs == 2),
                 "avc_lstm_bwd: bad args");
@@ -797,6 +955,37 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
   AVC_CHECK_ARG(w_hh_t && dcbuf, "avc_lstm_bwd: large-H path needs W_hh^T and dcbuf");
   const bool bf = compute == AVC_BF16;
   AVC_CHECK_ARG(!bf || (wdtype == AVC_BF16 && gbuf), "avc_lstm_bwd: bf16 compute needs bf16 W_hh^T and gbuf");
+  const int ng = (B + PRG - 1) / PRG;
+  static const bool no_persist = getenv("AVC_LSTM_NO_PERSIST") != nullptr;
+  if (bf && dirs == 1 && (H == 1024 || H == 512) && !no_persist && ng * (H / PJU) <= num_cus()) {
+    // gbuf is the granule scratch (>= 2*B*2H u64 + a flag word) in this mode
+    PersistBwdArgs p;
+    p.dhout = dh_out;
+    p.call = c;
+    p.gall = gates;
+    p.wt = reinterpret_cast<const bf16*>(w_hh_t);
+    p.dg = dgates;
+    p.dg16 = reinterpret_cast<bf16*>(dgates_bf16);
+    p.xbuf = reinterpret_cast<unsigned long long*>(gbuf);
+    p.flag = reinterpret_cast<unsigned*>(p.xbuf + (size_t)2 * B * (2 * H));
+    p.B = B;
+    p.T = T;
+    p.ng = ng;
+    (void)hipMemsetAsync(gbuf, 0, ((size_t)2 * B * (2 * H) + 2) * sizeof(unsigned long long), s);
+    if (H == 1024) {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_persist_bwd<1024>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_bwd_lds<1024>());
+        attr = true;
+      }
+      lstm_persist_bwd<1024><<<ng * (H / PJU), 256, persist_bwd_lds<1024>(), s>>>(p);
+    } else {
+      lstm_persist_bwd<512><<<ng * (H / PJU), 256, persist_bwd_lds<512>(), s>>>(p);
+    }
+    return avc_check_launch("avc_lstm_bwd(persistent)");
+  }
+  AVC_CHECK_ARG(dgates_bf16 == nullptr, "avc_lstm_bwd: the bf16 dG twin is produced by the persistent path only");
   StepArgs a = {};
   a.w = w_hh_t;
   a.call = const_cast<float*>(c);

@@ -57,6 +57,10 @@ def _dev(*ts):
 def operand(t: torch.Tensor, ld: int, kstrided: bool = False, window=None, batch_stride: int = 0) -> L.Operand:
     """window = (taps, pad, t_out, t_in, chans) or None."""
     _dev(t)
+    if _COMPUTE == BF16 and t.dtype == torch.float32:
+        tw = getattr(t, "_bf16", None)
+        if tw is not None:
+            t = tw
     o = L.Operand()
     o._keep = t  # the descriptor holds a raw pointer: keep the tensor alive until launch
     o.ptr = t.data_ptr()
@@ -125,19 +129,47 @@ def bn_stats(y, M, C, ld=None):
     return partial
 
 
-def bn_apply(y, scale, shift, act, residual=None, out=None):
+def _twin_buf(t, want):
+    """bf16 twin buffer for an fp32 activation in bf16 compute mode (GEMM operand copy)."""
+    if want is None:
+        want = _COMPUTE == BF16
+    return torch.empty(t.shape, device=t.device, dtype=torch.bfloat16) if want else None
+
+
+def attach_twin(t, t16):
+    """Record t16 (bf16, same layout) as the GEMM-operand twin of fp32 t: operand() uses it
+    in bf16 compute mode (the bf16 products are identical; the loads are half as wide)."""
+    if t16 is not None:
+        t._bf16 = t16
+    return t
+
+
+def twin(t):
+    """The bf16 twin of t, made by one conversion pass if t has none (bf16 mode only)."""
+    if _COMPUTE != BF16 or t.dtype != torch.float32:
+        return t
+    tw = getattr(t, "_bf16", None)
+    if tw is None:
+        tw = convert(t.contiguous(), BF16)
+        t._bf16 = tw
+    return t
+
+
+def bn_apply(y, scale, shift, act, residual=None, out=None, twin16=None):
     M, C = y.shape
     out = torch.empty_like(y) if out is None else out
-    L.call("avc_bn_apply", y.data_ptr(), scale.data_ptr(), shift.data_ptr(), _ptr(residual), out.data_ptr(), M, C,
-           int(act), stream())
-    return out
+    o16 = _twin_buf(out, twin16)
+    L.call("avc_bn_apply", y.data_ptr(), scale.data_ptr(), shift.data_ptr(), _ptr(residual), out.data_ptr(), _ptr(o16),
+           M, C, int(act), stream())
+    return attach_twin(out, o16)
 
 
-def bn_bwd(dA, a, y, mean, rstd, gamma, act, need_dbias=True, into=None):
+def bn_bwd(dA, a, y, mean, rstd, gamma, act, need_dbias=True, into=None, twin16=None):
     """into = (dgamma, dbeta, dbias) buffers to accumulate into (direct gradient sink)."""
     M, C = y.shape
     dev = y.device
     dy = torch.empty_like(y)
+    d16 = _twin_buf(dy, twin16)
     if into is not None:
         dgamma, dbeta, dbias = into
     else:
@@ -146,9 +178,9 @@ def bn_bwd(dA, a, y, mean, rstd, gamma, act, need_dbias=True, into=None):
         dbias = torch.empty(C, device=dev) if need_dbias else None
     ws = torch.empty(int(L.lib().avc_bn_bwd_ws(M, C)), device=dev)
     L.call("avc_bn_bwd", dA.data_ptr(), a.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), _ptr(gamma), M,
-           C, int(act), dy.data_ptr(), _ptr(dgamma), _ptr(dbeta), _ptr(dbias), int(into is not None), ws.data_ptr(),
-           stream())
-    return dy, dgamma, dbeta, dbias
+           C, int(act), dy.data_ptr(), _ptr(d16), _ptr(dgamma), _ptr(dbeta), _ptr(dbias), int(into is not None),
+           ws.data_ptr(), stream())
+    return attach_twin(dy, d16), dgamma, dbeta, dbias
 
 
 def colsum(x, M, N, ld=None, out=None, accumulate=False):
@@ -181,18 +213,46 @@ def lstm_fwd(xproj, w_hh, B, T, H, dirs, hbuf=None):
     return h, c, g
 
 
-def lstm_bwd(dh, h, c, g, w_hh, w_hh_t, B, T, H, dirs):
+def lstm_persistent_bwd(B, H, dirs):
+    """Whether avc_lstm_bwd takes the one-launch persistent path (mirrors lstm.hip)."""
+    return _COMPUTE == BF16 and dirs == 1 and H in (512, 1024) and os.environ.get("AVC_LSTM_NO_PERSIST") is None \
+        and ((B + 7) // 8) * (H // 32) <= num_cus()
+
+
+def num_cus():
+    if "cus" not in _CACHE:
+        _CACHE["cus"] = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    return _CACHE["cus"]
+
+
+_CACHE = {}
+
+
+def lstm_bwd_scratch(B, H, dirs, device):
+    nbytes = max(16 * dirs * B * H, 32 * B * H + 16)
+    return torch.empty((nbytes + 1) // 2, device=device, dtype=torch.bfloat16)
+
+
+def lstm_bwd_timeout_flag(gbuf, B, H):
+    return int(gbuf.view(torch.int32)[8 * B * H].item())
+
+
+def lstm_bwd(dh, h, c, g, w_hh, w_hh_t, B, T, H, dirs, gbuf=None):
+    """dL/d(pre-activation gates); in the persistent bf16 mode also its bf16 twin."""
     dev = dh.device
     dg = torch.empty(B * T, dirs * 4 * H, device=dev)
-    dcbuf = gbuf = None
+    dcbuf = dg16 = None
     wdt = _dt(w_hh if w_hh_t is None else w_hh_t)
     if H > 64:
         dcbuf = torch.empty(dirs * B * H, device=dev)
         if _COMPUTE == BF16:
-            gbuf = torch.empty(2 * dirs * B * 4 * H, device=dev, dtype=torch.bfloat16)
+            if gbuf is None:
+                gbuf = lstm_bwd_scratch(B, H, dirs, dev)
+            if lstm_persistent_bwd(B, H, dirs):
+                dg16 = torch.empty(B * T, 4 * H, device=dev, dtype=torch.bfloat16)
     L.call("avc_lstm_bwd", dh.data_ptr(), h.data_ptr(), c.data_ptr(), g.data_ptr(), _ptr(w_hh), _ptr(w_hh_t), wdt, B,
-           T, H, dirs, dg.data_ptr(), _ptr(dcbuf), _ptr(gbuf), _COMPUTE if H > 64 else F32, stream())
-    return dg
+           T, H, dirs, dg.data_ptr(), _ptr(dg16), _ptr(dcbuf), _ptr(gbuf), _COMPUTE if H > 64 else F32, stream())
+    return attach_twin(dg, dg16)
 
 
 # ------------------------------------------------------------------------- glue

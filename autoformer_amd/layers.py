@@ -156,6 +156,7 @@ class ConvBNCore:
         T_out = T_in + 2 * self.pad - Kw + 1
         M = B * T_out
         Wf, _ = self.packs()
+        x = K.twin(x)
         y = torch.empty(M, Co, device=x.device)
         partial = K.bn_partial_buffer(M, Co, x.device) if bn.training else None
         K.gemm(M, Co, Kw * Ci, operand(x, Ci, window=(Kw, self.pad, T_out, T_in, Ci)), operand(Wf, Kw * Ci), y,
@@ -286,6 +287,8 @@ class LSTMLayerCore:
             large = H > 64
             whh = torch.empty(dirs * 4 * H, H, device=dev, dtype=tdt if large else torch.float32)
             whh_t = torch.empty(dirs * H, 4 * H, device=dev, dtype=tdt) if large else None
+            # W_ih^T (In x 4H) makes the input-gradient GEMM K-contiguous in both operands
+            wih_t = torch.empty(In, 4 * H, device=dev, dtype=tdt) if dirs == 1 else None
             for d in range(dirs):
                 w_ih, w_hh, b_ih, b_hh = ps[4 * d: 4 * d + 4]
                 K.convert(w_ih, dt, out=wih[d * 4 * H:(d + 1) * 4 * H])
@@ -293,13 +296,16 @@ class LSTMLayerCore:
                 K.convert(w_hh, dt if large else K.F32, out=whh[d * 4 * H:(d + 1) * 4 * H])
                 if large:
                     K.transpose(w_hh, dt, out=whh_t[d * H:(d + 1) * H])
-            return wih, bsum, whh, whh_t
+            if wih_t is not None:
+                K.transpose(ps[0], dt, out=wih_t)
+            return wih, bsum, whh, whh_t, wih_t
         return self.cache.get(ps, build)
 
     def forward(self, x, B, T):
         H, dirs = self.H, self.dirs
         In = x.shape[1]
-        wih, bsum, whh, _ = self.packs()
+        wih, bsum, whh, _, _ = self.packs()
+        x = K.twin(x)
         xproj = torch.empty(B * T, dirs * 4 * H, device=x.device)
         K.gemm(B * T, dirs * 4 * H, In, operand(x, In), operand(wih, In), xproj, bias=bsum)
         hbuf = None
@@ -312,7 +318,7 @@ class LSTMLayerCore:
         c, g = saved
         H, dirs = self.H, self.dirs
         In = x.shape[1]
-        wih, _, whh, whh_t = self.packs()
+        wih, _, whh, whh_t, wih_t = self.packs()
         dg = K.lstm_bwd(dh, h, c, g, whh if H <= 64 else None, whh_t, B, T, H, dirs)
         G = dirs * 4 * H
         M = B * T
@@ -323,7 +329,7 @@ class LSTMLayerCore:
             grads = []
             for d in range(dirs):
                 w_ih, w_hh, b_ih, b_hh = ps[4 * d: 4 * d + 4]
-                dgd = dg[:, d * 4 * H:]
+                dgd = dg if dirs == 1 else dg[:, d * 4 * H:]  # the full tensor keeps its bf16 twin
                 dwih = _grad_of(w_ih) if sink else torch.empty(4 * H, In, device=x.device)
                 K.gemm(4 * H, In, M, operand(dgd, G, kstrided=True), operand(x, In, kstrided=True), dwih,
                        split_k=K.auto_split_k(4 * H, In, M), accumulate=sink)
@@ -350,7 +356,10 @@ class LSTMLayerCore:
         dx = None
         if need_dx:
             dx = torch.empty(M, In, device=x.device)
-            K.gemm(M, In, G, operand(dg, G), operand(wih, In, kstrided=True), dx)
+            if wih_t is not None:
+                K.gemm(M, In, G, operand(K.twin(dg), G), operand(wih_t, G), dx)
+            else:
+                K.gemm(M, In, G, operand(dg, G), operand(wih, In, kstrided=True), dx)
         return dx, grads
 
 

@@ -55,7 +55,7 @@ def kernel_timing(model, B, T, reps=3):
     from autoformer_amd import kernels as K
 
     core = model.decoder._lstm2[1]
-    _, _, whh, whh_t = core.packs()
+    whh, whh_t = core.packs()[2:4]
     H = core.H
     dev = whh.device
     g = torch.Generator(device=dev).manual_seed(7)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 1
+#define AVC_ABI_VERSION 2
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -99,7 +99,7 @@ int avc_bn_stats(const float* y, long long ld, int M, int C, float* partial, voi
 
 /* out[r][c] = act(y[r][c]*scale[c] + shift[c]) (+ residual[r][c]); rows of length C. */
 int avc_bn_apply(const float* y, const float* scale, const float* shift, const float* residual,
-                 float* out, int M, int C, int act, void* stream);
+                 float* out, void* out_bf16, int M, int C, int act, void* stream);
 
 /* BatchNorm1d + activation backward.  dz = dA * act'(a); yhat = (y-mean)*rstd.
  * Writes dy = gamma*rstd*(dz - sum(dz)/N - yhat*sum(dz*yhat)/N), and dgamma, dbeta and
@@ -107,8 +107,8 @@ int avc_bn_apply(const float* y, const float* scale, const float* shift, const f
  * `ws` >= avc_bn_bwd_ws floats. */
 size_t avc_bn_bwd_ws(int M, int C);
 int avc_bn_bwd(const float* dA, const float* a, const float* y, const float* mean, const float* rstd,
-               const float* gamma, int M, int C, int act, float* dy, float* dgamma, float* dbeta,
-               float* dbias, int accumulate, float* ws, void* stream);
+               const float* gamma, int M, int C, int act, float* dy, void* dy_bf16, float* dgamma,
+               float* dbeta, float* dbias, int accumulate, float* ws, void* stream);
 
 /* out[n] (+)= sum_m x[m*ld + n] (bias gradients). ws >= avc_colsum_ws floats. */
 size_t avc_colsum_ws(int M, int N);
@@ -129,10 +129,16 @@ int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T,
 
 /* Backward recurrence.  dh_out (B,T,dirs*H) = dL/dh; writes dgates (B,T,dirs*4H)
  * (pre-activation).  w_hh_t: dirs x [H][4H] transposed copy (large H) or w_hh itself
- * (small H, pass the same layout as avc_lstm_fwd). dcbuf: B*H*dirs fp32, gbuf: 2*B*4H*dirs wdtype. */
+ * (small H, pass the same layout as avc_lstm_fwd). dcbuf: B*H*dirs fp32.  gbuf (large H,
+ * bf16 compute): at least max(16*dirs*B*H, 32*B*H + 16) bytes.  For dirs == 1, H in
+ * {512, 1024} and enough CUs the whole sequence is ONE persistent launch (W_hh^T slices
+ * register-resident, dG_{t+1} exchanged through tagged granules, bounded spins; timeout
+ * flag = u32 at byte 32*B*H of gbuf), which can also write a bf16 copy of dgates
+ * (dgates_bf16, else null); otherwise one fused kernel per time step and dgates_bf16 must
+ * be null. */
 int avc_lstm_bwd(const float* dh_out, const float* h, const float* c, const float* gates,
                  const void* w_hh, const void* w_hh_t, int wdtype, int B, int T, int H, int dirs,
-                 float* dgates, float* dcbuf, void* gbuf, int compute, void* stream);
+                 float* dgates, void* dgates_bf16, float* dcbuf, void* gbuf, int compute, void* stream);
 
 /* Elementwise / layout kernels of the model glue (AutoVC.py:46-48, 56-66, 197-207). */
 int avc_enc_concat(const float* mel, long long mel_ld, const float* emb, float* out, int B, int T,

@@ -331,3 +331,91 @@ def test_lstm_persistent_forward_matches_per_step(B, H):
     ref = torch.stack(outs, 1).reshape(B * T, H)
     assert relf(h1, ref) < 2e-3, relf(h1, ref)
     assert relf(c1.cpu().view(B, T, H)[:, -1], c) < 2e-3
+
+
+@pytest.mark.parametrize("M,N,K,split", [(300, 200, 96, 1), (1000, 80, 400, 1), (1024, 512, 2560, 1),
+                                         (513, 640, 1024, 3), (64, 136, 8, 1)])
+def test_gemm_nt_lds_pipeline_bf16_operands(M, N, K, split):
+    """bf16 K-contiguous operands take the LDS-DMA NT kernel (gemm_nt.hip): products of bf16
+    values accumulate in fp32, so the result matches an fp64 product of the same bf16 values
+    to fp32 accumulation error (M/N tails, K tails of 8, split-K, bias)."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute("bf16")
+    a = torch.randn(M, K).to(torch.bfloat16)
+    b = torch.randn(N, K).to(torch.bfloat16)
+    bias = torch.randn(N)
+    ref = _gemm_ref(a.float(), b.float()) + bias.double()
+    c = torch.empty(M, N, device=DEV)
+    ad, bd = a.to(DEV), b.to(DEV)
+    Kr.gemm(M, N, K, Kr.operand(ad, K), Kr.operand(bd, K), c, bias=bias.to(DEV), split_k=split)
+    assert relf(c, ref) < 1e-5, relf(c, ref)
+
+
+@pytest.mark.parametrize("B,T,Cin,Cout,Kw,pad", [(3, 37, 64, 96, 5, 2), (64, 128, 512, 512, 5, 2), (2, 9, 8, 24, 3, 1)])
+def test_gemm_nt_conv_window_and_bn_stats(B, T, Cin, Cout, Kw, pad):
+    """Windowed (im2col) A operand through the NT kernel + the BN partial-statistics epilogue."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute("bf16")
+    x = torch.randn(B, T, Cin).to(torch.bfloat16)
+    w = (torch.randn(Cout, Cin, Kw) * 0.1).to(torch.bfloat16)
+    ref = F.conv1d(x.float().transpose(1, 2).double(), w.float().double(), padding=pad).transpose(1, 2)
+    ref = ref.reshape(B * T, Cout)
+    Wf = w.permute(0, 2, 1).reshape(Cout, Kw * Cin).contiguous().to(DEV)  # [co][k][ci]
+    M = B * T
+    y = torch.empty(M, Cout, device=DEV)
+    part = Kr.bn_partial_buffer(M, Cout, DEV)
+    Kr.gemm(M, Cout, Kw * Cin, Kr.operand(x.reshape(M, Cin).to(DEV), Cin, window=(Kw, pad, T, T, Cin)),
+            Kr.operand(Wf, Kw * Cin), y, bn_partial=part)
+    assert relf(y, ref) < 1e-5, relf(y, ref)
+    mean, rstd, _, _ = Kr.bn_finalize(part, M, Cout, None, None, None, None, None, 0.1, 1e-5)
+    refm = ref.mean(0)
+    refv = ref.var(0, unbiased=False)
+    assert rinf(mean, refm) < 1e-4
+    assert rinf(1.0 / rstd.double() ** 2 - 1e-5, refv) < 1e-3
+
+
+@pytest.mark.parametrize("B,H", [(64, 1024), (20, 1024), (64, 512), (3, 512)])
+def test_lstm_persistent_backward(B, H):
+    """The one-launch backward recurrence (bf16 products, fp32 cell math) against an fp32
+    CPU loop that rounds dG_{t+1} to bf16 for the recurrent product, as the kernel does;
+    its bf16 dG twin equals the fp32 output rounded; the spin-timeout flag stays clear."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute("bf16")
+    assert Kr.lstm_persistent_bwd(B, H, 1)
+    T = 29
+    G = 4 * H
+    torch.manual_seed(2)
+    dh = (torch.randn(B * T, H) * 0.1)
+    c = torch.randn(B * T, H) * 0.7
+    gates = torch.rand(B * T, G) * 0.9 + 0.05
+    gates[:, 2 * H:3 * H] = gates[:, 2 * H:3 * H] * 2 - 1  # g gate in (-1, 1)
+    whh = (torch.randn(G, H) * (1.0 / H ** 0.5)).bfloat16()
+    wt = whh.t().contiguous()
+    gbuf = Kr.lstm_bwd_scratch(B, H, 1, DEV)
+    dg = Kr.lstm_bwd(dh.to(DEV), dh.to(DEV), c.to(DEV), gates.to(DEV), None, wt.to(DEV), B, T, H, 1, gbuf=gbuf)
+    torch.cuda.synchronize()
+    assert Kr.lstm_bwd_timeout_flag(gbuf, B, H) == 0
+    assert getattr(dg, "_bf16", None) is not None
+    torch.testing.assert_close(dg._bf16.float(), dg.to(torch.bfloat16).float(), rtol=0, atol=0)
+    w = whh.float()
+    dhv, cv, gv = dh.view(B, T, H), c.view(B, T, H), gates.view(B, T, G)
+    ref = torch.zeros(B, T, G)
+    dc = torch.zeros(B, H)
+    nxt = None
+    for t in range(T - 1, -1, -1):
+        d = dhv[:, t] + (nxt.bfloat16().float() @ w if nxt is not None else 0)
+        i, f, gg, o = gv[:, t].chunk(4, 1)
+        tc = torch.tanh(cv[:, t])
+        cp = cv[:, t - 1] if t > 0 else torch.zeros(B, H)
+        dcs = dc + d * o * (1 - tc * tc)
+        out = torch.cat([dcs * gg * i * (1 - i), dcs * cp * f * (1 - f), dcs * i * (1 - gg * gg), d * tc * o * (1 - o)], 1)
+        ref[:, t] = out
+        dc = dcs * f
+        nxt = out
+    assert relf(dg, ref.reshape(B * T, G)) < 2e-3, relf(dg, ref.reshape(B * T, G))

@@ -49,6 +49,10 @@ case("wgrad TT bf16", 512, 2560, 8192, bf, bf, aks=True, bks=True, split=3)
 case("wgrad TT f32 nosplit", 512, 2560, 8192, f32, f32, aks=True, bks=True)
 case("dx NT(kstrided B) f32", 8192, 1024, 4096, f32, bf, bks=True)
 case("big square bf16", 4096, 4096, 4096, bf, bf)
+case("xproj lstm1 bf16 A", 8192, 2048, 344, bf, bf)
+case("dgrad conv bf16", 8192, 512, 2560, bf, bf, win=(64, 128, 512, 5, 2))
+case("postnet last conv bf16", 8192, 80, 2560, bf, bf, win=(64, 128, 512, 5, 2))
+case("postnet first conv bf16", 8192, 512, 400, bf, bf, win=(64, 128, 80, 5, 2))
 
 
 def torch_case(name, M, N, K_):
