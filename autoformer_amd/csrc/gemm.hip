@@ -731,6 +731,7 @@ extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
     g.klen = ((klf + FBK - 1) / FBK) * FBK;
     if (g.klen <= 0) g.klen = FBK;
     if (!aks && !bks && gemm_nt_launch(g, s)) return avc_check_launch("avc_gemm(nt)");
+    if (aks && bks && gemm_tt_launch(g, s)) return avc_check_launch("avc_gemm(tt)");
     const long long t128 = (long long)cdiv(g.M, BM) * cdiv(g.N, 128) * g.batch * g.split_k;
     const bool narrow = g.N <= 64 || t128 < 384;
     const int nb = narrow ? cdiv(g.M, BM) * cdiv(g.N, 64) * g.batch * g.split_k : (int)t128;

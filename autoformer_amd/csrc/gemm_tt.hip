@@ -1,0 +1,213 @@
+// gemm_tt.hip — bf16 "TT" GEMM (both operands K-strided) fed by LDS DMA: the weight-gradient
+// shape C[M][N] = sum_k A[k][M] B[k][N], k = frames.
+//
+// Serves every weight gradient of the path: dW of each Conv1d (dy^T . im2col(x), with the
+// frame window on B: factory/Norm.py:21-28), dW_ih / dW_hh of the LSTMs (dG^T . x and
+// dG^T . h_{t-1}, the latter a one-frame shift window: AutoVC.py:43,77,96) and the linear
+// projection (Norm.py:40-50).
+//
+// Both operands are stored frame-major, so a K-tile is 64 frame rows x 128 columns: it is
+// copied global -> LDS row by row with global_load_lds_dwordx4 (256-B rows, 16-B chunks
+// XOR-swizzled as chunk ^ (((row&3)<<2) | ((row>>2)&3)) via the source address) and the
+// MFMA fragments, which need 8 consecutive frames per lane, are read with the gfx950
+// transposing LDS read ds_read_b64_tr_b16 (cdna_hip_programming.md §5.5 T10, layout (b):
+// conflict-free for the 16x16x32 operands).  128 x 128 tile, BK = 64, 4 waves as 2 x 2,
+// 2 LDS stages, counted vmcnt + raw barrier, shared fused epilogue (gemm_internal.h).
+#include "gemm_internal.h"
+
+namespace avcg {
+namespace {
+
+__device__ __attribute__((aligned(16))) unsigned int g_zero16_tt[4] = {0u, 0u, 0u, 0u};
+
+constexpr int TROW = 256;          // LDS bytes per frame row of a 128-column tile
+constexpr int TSTAGE_OP = FBK * TROW;  // one operand's K-tile: 16 KiB
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4* lds_s4_ptr;
+
+__device__ __forceinline__ void glds16(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)lds, 16, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+__device__ __forceinline__ int tswz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+// One K-strided operand: tile of 64 frame rows x 128 columns [col0, col0 + 128).  Wave w,
+// instruction i covers rows 4*(4i + w) .. +4; lane L writes row +(L>>4), slot L&15, holding
+// global chunk (L&15) ^ tswz(row) = (L&15) ^ (((L>>4)<<2) | w): one fixed column per lane.
+template <bool WIN>
+struct TtLoader {
+  const bf16* base;
+  int col_ok;          // this lane's 8 columns lie inside the operand
+  int coff;            // element offset of the lane's column inside a frame row
+  int tap;             // window: tap of the lane's column
+  long long ld;
+  int pad, t_in, t_out;
+  FastDiv tdiv;
+
+  __device__ __forceinline__ void init(const OpDev& o, int col0, int bz) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    base = reinterpret_cast<const bf16*>(o.ptr) + (long long)bz * o.bstride;
+    const int ch = (lane & 15) ^ (((lane >> 4) << 2) | (w & 3));
+    const int col = col0 + 8 * ch;
+    col_ok = col < o.rows;
+    ld = o.ld;
+    pad = o.pad;
+    t_in = o.t_in;
+    t_out = o.t_out;
+    tdiv = o.tdiv;
+    if (WIN) {
+      tap = col_ok ? (int)fdiv((uint32_t)col, o.cdv) : 0;
+      coff = col - tap * o.chans;
+    } else {
+      tap = 0;
+      coff = col;
+    }
+  }
+
+  __device__ __forceinline__ void issue(char* lds_tile, int kbase, int kend) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * (4 * i + w) + (lane >> 4);
+      const int k = kbase + r;
+      bool ok = col_ok && k < kend;
+      long long frame = k;
+      if (WIN) {
+        const int b = (int)fdiv((uint32_t)(ok ? k : 0), tdiv);
+        const int t2 = k - b * t_out + tap - pad;
+        ok = ok && t2 >= 0 && t2 < t_in;
+        frame = (long long)b * t_in + t2;
+      }
+      const void* src = ok ? (const void*)(base + frame * ld + coff) : (const void*)g_zero16_tt;
+      glds16(src, lds_tile + 4 * (4 * i + w) * TROW);
+    }
+  }
+};
+
+// Per-lane byte offsets of the two transposed reads (frames +0..3 and +4..7 of the lane's
+// 8-frame group) of 16-column block `blk` (= first chunk / 2) inside a 64-frame tile, k-sub 0.
+__device__ __forceinline__ void tr_offsets(int chunk0, int& o0, int& o1) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, ql = lane & 15, q = ql >> 2, p = ql & 3;
+  const int r0 = 8 * g + q, r1 = 8 * g + 4 + q;
+  o0 = r0 * TROW + 16 * ((chunk0 + (p >> 1)) ^ tswz(r0)) + 8 * (p & 1);
+  o1 = r1 * TROW + 16 * ((chunk0 + (p >> 1)) ^ tswz(r1)) + 8 * (p & 1);
+}
+
+__device__ __forceinline__ bf16x8 tr_frag(const char* tile, int o0, int o1) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(tile + o0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(tile + o1));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <bool WINB>
+__global__ void __launch_bounds__(256, 2) gemm_tt_kernel(GemmArgs g) {
+  constexpr int BN_ = 128, NJ = 4;
+  constexpr int STAGE = 2 * TSTAGE_OP;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int tid = threadIdx.x, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int nN = (g.N + BN_ - 1) / BN_, nM = (g.M + BM - 1) / BM;
+  const int z = lid / (nN * nM);
+  const int rem = lid - z * nN * nM;
+  const int mt = rem / nN, nt = rem - mt * nN;
+  const int m0 = mt * BM, n0 = nt * BN_;
+  const int bz = z / g.split_k, ks = z - bz * g.split_k;
+  const int kbeg = ks * g.klen;
+  const int kend = min(g.K, kbeg + g.klen);
+  const int nkt = kend > kbeg ? (kend - kbeg + FBK - 1) / FBK : 0;
+
+  TtLoader<false> la;
+  TtLoader<WINB> lb;
+  la.init(g.a, m0, bz);
+  lb.init(g.b, n0, bz);
+
+  f32x4 acc[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int ao0[4], ao1[4], bo0[NJ], bo1[NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) tr_offsets(wm * 8 + 2 * i, ao0[i], ao1[i]);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) tr_offsets(wn * 8 + 2 * j, bo0[j], bo1[j]);
+
+  if (nkt > 0) {
+    la.issue(smem_raw, kbeg, kend);
+    lb.issue(smem_raw + TSTAGE_OP, kbeg, kend);
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    wait_vm<0>();
+    raw_barrier();
+    if (kt + 1 < nkt) {
+      char* st = smem_raw + ((kt + 1) & 1) * STAGE;
+      la.issue(st, kbeg + (kt + 1) * FBK, kend);
+      lb.issue(st + TSTAGE_OP, kbeg + (kt + 1) * FBK, kend);
+    }
+    const char* As = smem_raw + (kt & 1) * STAGE;
+    const char* Bs = As + TSTAGE_OP;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ko = h * 32 * TROW;
+      bf16x8 af[4], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = tr_frag(As + ko, ao0[i], ao1[i]);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bfr[j] = tr_frag(Bs + ko, bo0[j], bo1[j]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  fast_epilogue<BN_>(g, acc, m0, n0, mt, bz, ks, smem_raw);
+}
+
+template <bool WINB>
+void launch(const GemmArgs& g, int nblocks, hipStream_t s) {
+  const size_t lds = 2 * 2 * (size_t)TSTAGE_OP;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tt_kernel<WINB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  gemm_tt_kernel<WINB><<<nblocks, 256, lds, s>>>(g);
+}
+
+bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+bool gemm_tt_launch(const GemmArgs& g, hipStream_t s) {
+  static const bool off = getenv("AVC_TT_DISABLE") != nullptr;
+  if (off || g.klen % FBK || g.M % 8 || g.N % 8) return false;
+  for (const OpDev* o : {&g.a, &g.b})
+    if (o->dtype != AVC_BF16 || !ok16(o->ptr) || o->ld % 8 || o->bstride % 8) return false;
+  if (g.a.win) return false;
+  if (g.b.win && g.b.chans % 8) return false;
+  const int nb = ((g.M + BM - 1) / BM) * ((g.N + 127) / 128) * g.batch * g.split_k;
+  if (g.b.win) launch<true>(g, nb, s);
+  else launch<false>(g, nb, s);
+  return true;
+}
+
+}  // namespace avcg

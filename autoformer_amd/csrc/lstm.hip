@@ -10,7 +10,9 @@
 //  * small H (<= 64, the encoder): batch rows are independent in the recurrence, so one
 //    workgroup owns one (utterance, direction) for all T steps.  W_hh lives in registers
 //    (one gate row per thread), h/gates in LDS; no inter-workgroup sync at all.
-//  * large H (multiple of 128, the decoder): one fused kernel per time step.  Each
+//  * large H (multiple of 128, the decoder): one persistent launch per layer when it fits
+//    (bf16, one direction, H in {512, 1024}: lstm_persist_fwd / lstm_persist_bwd below),
+//    otherwise one fused kernel per time step.  Each
 //    workgroup owns (16*MT utterances) x (8 hidden units, all 4 gates) [forward] or
 //    (16*MT utterances) x (16 hidden units) [backward]; the recurrent product runs on
 //    MFMA with K split over the 4 waves and operands loaded straight into registers;

@@ -38,14 +38,32 @@ def sink_on() -> bool:
     return _SINK["on"]
 
 
+def mark():
+    """Event on the current stream (sink mode): a later _Side(after=...) starts from here, so
+    the critical-path kernels launched in between (data gradients) are not delayed behind
+    the host work of queueing the weight-gradient branch."""
+    if not _SINK["on"]:
+        return None
+    ev = torch.cuda.Event()
+    ev.record()
+    return ev
+
+
 class _Side:
     """Context: run enclosed kernels on the side stream after everything queued so far on
-    the current stream; tensors passed to keep() stay alive until join_side()."""
+    the current stream (or after the event `after`); tensors passed to keep() stay alive
+    until join_side()."""
+
+    def __init__(self, after=None):
+        self.after = after
 
     def __enter__(self):
         self.main = torch.cuda.current_stream()
         side = _SINK["side"]
-        side.wait_stream(self.main)
+        if self.after is not None:
+            side.wait_event(self.after)
+        else:
+            side.wait_stream(self.main)
         self.ctx = torch.cuda.stream(side)
         self.ctx.__enter__()
         return self
@@ -189,19 +207,20 @@ class ConvBNCore:
             K.gemm(Co, Kw * Ci, M, operand(dy, Co, kstrided=True),
                    operand(x, Ci, kstrided=True, window=(Kw, self.pad, T_out, T_in, Ci)), dWf, split_k=sk)
             return K.conv_grad_unpack(dWf, Co, Ci, Kw, into=_grad_of(conv.weight) if sink else None)
-        if sink:
-            with _Side() as sd:
-                sd.keep(dy, x)
-                wgrad()
-            dW = dgamma = dbeta = dbias = None
-        else:
-            dW = wgrad()
+        ev = mark()
         dx = None
         if n_dx:
             _, Wd = self.packs()
             dx = torch.empty(B * T_in, n_dx, device=x.device)
             K.gemm(B * T_in, n_dx, Kw * Co, operand(dy, Co, window=(Kw, Kw - 1 - self.pad, T_in, T_out, Co)),
                    operand(Wd, Kw * Co), dx)
+        if sink:
+            with _Side(ev) as sd:
+                sd.keep(dy, x)
+                wgrad()
+            dW = dgamma = dbeta = dbias = None
+        else:
+            dW = wgrad()
         return dx, dW, dbias, dgamma, dbeta
 
 
@@ -346,13 +365,7 @@ class LSTMLayerCore:
                 # b_ih and b_hh receive the same gradient but must not share storage
                 grads += [dwih, dwhh, dbd, K.convert(dbd, K.F32)]
             return grads
-        if sink:
-            with _Side() as sd:
-                sd.keep(dg, x, h)
-                wgrads()
-            grads = [None] * (4 * dirs)
-        else:
-            grads = wgrads()
+        ev = mark()
         dx = None
         if need_dx:
             dx = torch.empty(M, In, device=x.device)
@@ -360,6 +373,13 @@ class LSTMLayerCore:
                 K.gemm(M, In, G, operand(K.twin(dg), G), operand(wih_t, G), dx)
             else:
                 K.gemm(M, In, G, operand(dg, G), operand(wih, In, kstrided=True), dx)
+        if sink:
+            with _Side(ev) as sd:
+                sd.keep(dg, x, h)
+                wgrads()
+            grads = [None] * (4 * dirs)
+        else:
+            grads = wgrads()
         return dx, grads
 
 
@@ -415,18 +435,19 @@ class _LinearFn(torch.autograd.Function):
                    split_k=K.auto_split_k(Out, In, M), accumulate=sink)
             db = K.colsum(dy, M, Out, out=_grad_of(b) if sink else None, accumulate=sink)
             return dw, db
-        if sink:
-            with _Side() as sd:
-                sd.keep(dy, x)
-                wgrad()
-            dw = db = None
-        else:
-            dw, db = wgrad()
+        ev = mark()
         dx = None
         if ctx.needs_input_grad[0]:
             wc = ctx.cache.get([w], lambda: K.convert(w, K.compute()))
             dx = torch.empty(M, In, device=x.device)
             K.gemm(M, In, Out, operand(dy, Out), operand(wc, In, kstrided=True), dx)
+        if sink:
+            with _Side(ev) as sd:
+                sd.keep(dy, x)
+                wgrad()
+            dw = db = None
+        else:
+            dw, db = wgrad()
         return dx, dw, db, None
 
 

@@ -37,21 +37,18 @@ def synthetic_batch(B, T, rank, device):
     return x.to(device), e.to(device)
 
 
-DOMINANT = "lstm_step_bwd_bf<1024>"
+DOMINANT = "lstm_persist_bwd<1024>"
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
 def kernel_timing(model, B, T, reps=3):
-    """Average launch duration of the dominant fixed-shape kernel, timed with HIP events on
-    the stream it is launched on (the C-ABI launches on torch's current stream).
+    """Average launch duration of the dominant kernel, timed with HIP events on the stream it
+    is launched on (the C-ABI launches on torch's current stream).
 
-    The kernel is lstm_step_bwd_bf<1024>: one backward time step of the decoder's lstm2
-    (H=1024, B=64), 256 launches per train step, the largest single-kernel share of the step
-    (profiles/r1_bench_kernel_stats.csv).  K.lstm_bwd launches it T times; per launch =
-    elapsed / T.  Algorithmic bytes per launch:
-      W_hh^T bf16 (4H*H*2) + dgates_{t+1} bf16 (B*4H*2) + gates fp32 (B*4H*4)
-      + dh, c_t, c_{t-1} fp32 (3*B*H*4) + dc read+write (2*B*H*4)
-      + dgates_t fp32 + bf16 writes (B*4H*6)."""
+    The kernel is lstm_persist_bwd<1024>: the whole backward recurrence of one decoder lstm2
+    layer (H=1024, B=64, T steps) in one launch, the largest single-kernel share of the step
+    (profiles/).  Algorithmic bytes per launch: W_hh^T once (4H*H bf16) + per
+    step dh, c fp32 (2*B*H*4) + activated gates fp32 (B*4H*4) + dG fp32 and bf16 out (B*4H*6)."""
     from autoformer_amd import kernels as K
 
     core = model.decoder._lstm2[1]
@@ -63,19 +60,24 @@ def kernel_timing(model, B, T, reps=3):
     h = torch.randn(B * T, H, device=dev, generator=g) * 0.5
     c = torch.randn(B * T, H, device=dev, generator=g) * 0.5
     gates = torch.rand(B * T, 4 * H, device=dev, generator=g)
-    K.lstm_bwd(dh, h, c, gates, whh, whh_t, B, T, H, 1)  # warm
+    if not K.lstm_persistent_bwd(B, H, 1):
+        raise RuntimeError("bench: the persistent backward recurrence does not apply to this shape/device")
+    gbuf = K.lstm_bwd_scratch(B, H, 1, dev)
+    K.lstm_bwd(dh, h, c, gates, whh, whh_t, B, T, H, 1, gbuf=gbuf)  # warm
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(reps):
-        K.lstm_bwd(dh, h, c, gates, whh, whh_t, B, T, H, 1)
+        K.lstm_bwd(dh, h, c, gates, whh, whh_t, B, T, H, 1, gbuf=gbuf)
     e1.record(s)
     torch.cuda.synchronize()
-    avg_us = e0.elapsed_time(e1) * 1e3 / (reps * T)
+    if K.lstm_bwd_timeout_flag(gbuf, B, H):
+        raise RuntimeError("bench: persistent LSTM backward hit its spin timeout")
+    avg_us = e0.elapsed_time(e1) * 1e3 / reps
     G = 4 * H
-    alg_bytes = G * H * 2 + B * G * 2 + B * G * 4 + 3 * B * H * 4 + 2 * B * H * 4 + B * G * 6
-    return {"kernel": DOMINANT + " (decoder lstm2 backward step, B=%d, H=%d)" % (B, H), "avg_us": avg_us,
-            "bytes": float(alg_bytes), "flops": 2.0 * B * G * H}
+    alg_bytes = G * H * 2 + T * (2 * B * H * 4 + B * G * 4 + B * G * 6)
+    return {"kernel": DOMINANT + " (decoder lstm2 backward recurrence, one launch = T=%d steps, B=%d, H=%d)"
+            % (T, B, H), "avg_us": avg_us, "bytes": float(alg_bytes), "flops": 2.0 * B * G * H * T}
 
 
 def pmc_traffic(kernel):

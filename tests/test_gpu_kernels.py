@@ -419,3 +419,67 @@ def test_lstm_persistent_backward(B, H):
         dc = dcs * f
         nxt = out
     assert relf(dg, ref.reshape(B * T, G)) < 2e-3, relf(dg, ref.reshape(B * T, G))
+
+
+def _im2col(x, B, T, Cin, Kw, pad):
+    """(B*T, Cin) frames -> (B*T, Kw*Cin) window rows [tap][ci], zero outside each utterance."""
+    xb = x.view(B, T, Cin)
+    cols = torch.zeros(B, T, Kw, Cin, dtype=x.dtype)
+    for k in range(Kw):
+        src = torch.arange(T) + k - pad
+        ok = (src >= 0) & (src < T)
+        cols[:, ok, k] = xb[:, src[ok]]
+    return cols.reshape(B * T, Kw * Cin)
+
+
+@pytest.mark.parametrize("M,N,K,split", [(256, 640, 1000, 1), (80, 1024, 513, 3), (512, 2560, 2048, 2)])
+def test_gemm_tt_lds_transposed_reads(M, N, K, split):
+    """K-strided bf16 operands take the LDS-DMA TT kernel (gemm_tt.hip, ds_read_b64_tr_b16
+    fragments); exact products of bf16 values, fp32 accumulation."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute("bf16")
+    a = torch.randn(K, M).to(torch.bfloat16)   # A[k][m]
+    b = torch.randn(K, N).to(torch.bfloat16)   # B[k][n]
+    ref = a.double().t() @ b.double()
+    c = torch.empty(M, N, device=DEV)
+    Kr.gemm(M, N, K, Kr.operand(a.to(DEV), M, kstrided=True), Kr.operand(b.to(DEV), N, kstrided=True), c,
+            split_k=split)
+    assert relf(c, ref) < 1e-5, relf(c, ref)
+
+
+@pytest.mark.parametrize("B,T,Cin,Cout,Kw,pad", [(4, 37, 64, 96, 5, 2), (64, 128, 512, 512, 5, 2), (3, 20, 88, 176, 3, 1)])
+def test_gemm_tt_conv_weight_gradient_window(B, T, Cin, Cout, Kw, pad):
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute("bf16")
+    x = torch.randn(B * T, Cin).to(torch.bfloat16)
+    dy = torch.randn(B * T, Cout).to(torch.bfloat16)
+    ref = dy.double().t() @ _im2col(x.double(), B, T, Cin, Kw, pad)
+    M, N = Cout, Kw * Cin
+    c = torch.empty(M, N, device=DEV)
+    Kr.gemm(M, N, B * T, Kr.operand(dy.to(DEV), Cout, kstrided=True),
+            Kr.operand(x.to(DEV), Cin, kstrided=True, window=(Kw, pad, T, T, Cin)), c,
+            split_k=Kr.auto_split_k(M, N, B * T))
+    assert relf(c, ref) < 1e-5, relf(c, ref)
+
+
+def test_gemm_tt_time_shift_window():
+    """dW_hh = dG^T . h_{t-1}: B operand is h shifted one frame inside each utterance."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute("bf16")
+    B, T, H = 6, 23, 128
+    G = 4 * H
+    dg = torch.randn(B * T, G).to(torch.bfloat16)
+    h = torch.randn(B * T, H).to(torch.bfloat16)
+    hp = torch.zeros(B, T, H, dtype=torch.float64)
+    hp[:, 1:] = h.double().view(B, T, H)[:, :-1]
+    ref = dg.double().t() @ hp.reshape(B * T, H)
+    c = torch.empty(G, H, device=DEV)
+    Kr.gemm(G, H, B * T, Kr.operand(dg.to(DEV), G, kstrided=True),
+            Kr.operand(h.to(DEV), H, kstrided=True, window=(1, 1, T, T, H)), c)
+    assert relf(c, ref) < 1e-5, relf(c, ref)
