@@ -54,7 +54,7 @@ _SIGS = {
     "avc_colsum_ws": (c_size, [c_int, c_int]),
     "avc_colsum": (c_int, [c_void_p, c_ll, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "avc_lstm_fwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
-                             c_void_p, c_int, c_void_p]),
+                             c_void_p, c_void_p, c_int, c_void_p]),
     "avc_lstm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                              c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "avc_enc_concat": (c_int, [c_void_p, c_ll, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
@@ -65,7 +65,7 @@ _SIGS = {
     "avc_conv_pack": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_conv_grad_unpack": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_convert": (c_int, [c_void_p, c_void_p, c_int, c_ll, c_void_p]),
-    "avc_transpose": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "avc_transpose": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_ll, c_void_p]),
     "avc_add": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_void_p]),
     "avc_mse_loss": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_void_p]),
     "avc_l1_loss": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_void_p]),

@@ -17,12 +17,14 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 // One block per 64 channels; 4 row-groups of 64 threads stride over the per-tile partials
 // (independent loads, no serial chain).  Merge = two passes over the partials:
 //   mean = sum_t s_t / n;   M2 = sum_t [ q_t + n_t (s_t / n_t - mean)^2 ]   (Chan, parallel form)
-__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ partial, int M, int C,
+constexpr int FG = 16;  // row groups of the finalize reductions (1024 threads = 64 channels x 16)
+
+__global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restrict__ partial, int M, int C,
                                                           const float* gamma, const float* beta, float* rmean,
                                                           float* rvar, long long* nbt, float momentum, float eps,
                                                           float* mean_out, float* rstd_out, float* scale,
                                                           float* shift) {
-  __shared__ float red[4][64];
+  __shared__ float red[FG][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
@@ -30,15 +32,18 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   const bool cv = c < C;
   float s = 0.f;
   if (cv)
-    for (int t = grp; t < nt; t += 4) s += partial[((long long)t * C + c) * 2];
+    for (int t = grp; t < nt; t += FG) s += partial[((long long)t * C + c) * 2];
   red[grp][cl] = s;
   __syncthreads();
   const float n = (float)M;
-  const float mean = (red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]) / n;
+  float tot = 0.f;
+#pragma unroll
+  for (int i = 0; i < FG; ++i) tot += red[i][cl];
+  const float mean = tot / n;
   __syncthreads();
   float q = 0.f;
   if (cv)
-    for (int t = grp; t < nt; t += 4) {
+    for (int t = grp; t < nt; t += FG) {
       const float nb = (float)min(PTILE, M - t * PTILE);
       const float d = partial[((long long)t * C + c) * 2] / nb - mean;
       q += partial[((long long)t * C + c) * 2 + 1] + nb * d * d;
@@ -46,7 +51,9 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   red[grp][cl] = q;
   __syncthreads();
   if (grp != 0 || !cv) return;
-  const float m2 = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+  float m2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < FG; ++i) m2 += red[i][cl];
   const float var = m2 / n;
   const float rstd = 1.f / sqrtf(var + eps);
   const float g = gamma ? gamma[c] : 1.f;
@@ -219,15 +226,15 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const float* __rest
 }
 
 // one block per 64 channels, 4 row groups reduce the per-block partials in parallel
-__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ ws, int nrb, int M, int C,
-                                                              const float* gamma, const float* rstd, float* coef,
-                                                              float* dgamma, float* dbeta, float* dbias, int acc) {
-  __shared__ float red[3][4][64];
+__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __restrict__ ws, int nrb, int M, int C,
+                                                               const float* gamma, const float* rstd, float* coef,
+                                                               float* dgamma, float* dbeta, float* dbias, int acc) {
+  __shared__ float red[3][FG][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f;
   if (c < C)
-    for (int b = grp; b < nrb; b += 4) {
+    for (int b = grp; b < nrb; b += FG) {
       const float* p = ws + ((long long)b * C + c) * 3;
       s0 += p[0];
       s1 += p[1];
@@ -238,9 +245,13 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
   red[2][grp][cl] = s2;
   __syncthreads();
   if (grp != 0 || c >= C) return;
-  s0 = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
-  s1 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
-  s2 = red[2][0][cl] + red[2][1][cl] + red[2][2][cl] + red[2][3][cl];
+  s0 = s1 = s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < FG; ++i) {
+    s0 += red[0][i][cl];
+    s1 += red[1][i][cl];
+    s2 += red[2][i][cl];
+  }
   const float g = gamma ? gamma[c] : 1.f;
   const float k1 = g * rstd[c];
   const float invn = 1.f / (float)M;
@@ -341,18 +352,20 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const float* __rest
   }
 }
 
-__global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restrict__ ws, int nrb, int N, float* out,
-                                                           int accumulate) {
-  __shared__ float red[4][64];
+__global__ void __launch_bounds__(1024) colsum_final_kernel(const float* __restrict__ ws, int nrb, int N, float* out,
+                                                            int accumulate) {
+  __shared__ float red[FG][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
   if (c < N)
-    for (int b = grp; b < nrb; b += 4) s += ws[(long long)b * N + c];
+    for (int b = grp; b < nrb; b += FG) s += ws[(long long)b * N + c];
   red[grp][cl] = s;
   __syncthreads();
   if (grp != 0 || c >= N) return;
-  s = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+  s = 0.f;
+#pragma unroll
+  for (int i = 0; i < FG; ++i) s += red[i][cl];
   out[c] = accumulate ? out[c] + s : s;
 }
 
@@ -362,7 +375,7 @@ extern "C" int avc_bn_finalize(const float* partial, int M, int C, const float* 
                                float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
                                float* mean, float* rstd, float* scale, float* shift, void* stream) {
   AVC_CHECK_ARG(partial && mean && rstd && scale && shift && M > 0 && C > 0, "avc_bn_finalize: bad args");
-  bn_finalize_kernel<<<cdiv(C, 64), 256, 0, as_stream(stream)>>>(partial, M, C, gamma, beta, running_mean,
+  bn_finalize_kernel<<<cdiv(C, 64), 1024, 0, as_stream(stream)>>>(partial, M, C, gamma, beta, running_mean,
                                                                    running_var, nbt, momentum, eps, mean, rstd,
                                                                    scale, shift);
   return avc_check_launch("avc_bn_finalize");
@@ -414,7 +427,7 @@ extern "C" int avc_bn_bwd(const float* dA, const float* a, const float* y, const
     bn_bwd_reduce1_kernel<<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, M, C, act, ws);
   }
   float* coef = ws + (size_t)nrb * C * 3;
-  bn_bwd_finalize_kernel<<<cdiv(C, 64), 256, 0, s>>>(ws, nrb, M, C, gamma, rstd, coef, dgamma, dbeta, dbias,
+  bn_bwd_finalize_kernel<<<cdiv(C, 64), 1024, 0, s>>>(ws, nrb, M, C, gamma, rstd, coef, dgamma, dbeta, dbias,
                                                        accumulate);
   const long long total = (long long)M * C;
   if (C % 4 == 0)
@@ -435,6 +448,6 @@ extern "C" int avc_colsum(const float* x, long long ld, int M, int N, float* out
     colsum_partial_kernel<true><<<dim3(cdiv(N, 64), nrb), 256, 0, s>>>(x, ld, M, N, ws);
   else
     colsum_partial_kernel<false><<<dim3(cdiv(N, 64), nrb), 256, 0, s>>>(x, ld, M, N, ws);
-  colsum_final_kernel<<<cdiv(N, 64), 256, 0, s>>>(ws, nrb, N, out, accumulate);
+  colsum_final_kernel<<<cdiv(N, 64), 1024, 0, s>>>(ws, nrb, N, out, accumulate);
   return avc_check_launch("avc_colsum");
 }

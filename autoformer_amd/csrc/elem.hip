@@ -136,7 +136,7 @@ __global__ void convert_kernel(const float* src, void* dst, int dtype, long long
   if (i < n) putd(dst, i, src[i], dtype);
 }
 
-__global__ void transpose_kernel(const float* src, void* dst, int dtype, int R, int C) {
+__global__ void transpose_kernel(const float* src, void* dst, int dtype, int R, int C, long long ldo) {
   __shared__ float tile[32][33];
   int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
   int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
@@ -147,7 +147,7 @@ __global__ void transpose_kernel(const float* src, void* dst, int dtype, int R, 
   __syncthreads();
   for (int y = ty; y < 32; y += 8) {
     int c = c0 + y, r = r0 + tx;  // dst[c][r]
-    if (c < C && r < R) putd(dst, (long long)c * R + r, tile[tx][y], dtype);
+    if (c < C && r < R) putd(dst, (long long)c * ldo + r, tile[tx][y], dtype);
   }
 }
 
@@ -303,10 +303,11 @@ extern "C" int avc_convert(const float* src, void* dst, int dtype, long long n, 
   return avc_check_launch("avc_convert");
 }
 
-extern "C" int avc_transpose(const float* src, void* dst, int dtype, int R, int C, void* stream) {
-  AVC_CHECK_ARG(src && dst, "avc_transpose: null");
+extern "C" int avc_transpose(const float* src, void* dst, int dtype, int R, int C, long long ld_dst, void* stream) {
+  AVC_CHECK_ARG(src && dst && (ld_dst == 0 || ld_dst >= R), "avc_transpose: bad args");
+  if (ld_dst == 0) ld_dst = R;
   dim3 g(cdiv(C, 32), cdiv(R, 32));
-  transpose_kernel<<<g, 256, 0, as_stream(stream)>>>(src, dst, dtype, R, C);
+  transpose_kernel<<<g, 256, 0, as_stream(stream)>>>(src, dst, dtype, R, C, ld_dst);
   return avc_check_launch("avc_transpose");
 }
 

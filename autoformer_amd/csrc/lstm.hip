@@ -564,6 +564,7 @@ struct PersistArgs {
   const float* xproj;
   const bf16* w;
   float* hout;
+  bf16* hout16;  // optional bf16 copy of h
   float* call;
   float* gall;
   unsigned long long* xbuf;  // [2][B][H/2] granules, zeroed before launch
@@ -693,6 +694,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
     if (pv) {
       const long long oh = ((long long)pb * T + t) * H + pj;
       a.hout[oh] = h;
+      if (a.hout16) a.hout16[oh] = (bf16)h;
       a.call[oh] = c;
       float* gp = a.gall + ((long long)pb * T + t) * G + pj;
       gp[0] = ig;
@@ -866,7 +868,7 @@ void launch_small_bwd(dim3 g, hipStream_t s, const float* dh, const float* c, co
 }  // namespace
 
 extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T, int H, int dirs, float* h,
-                            float* c, float* gates, void* hbuf, int compute, void* stream) {
+                            void* h_bf16, float* c, float* gates, void* hbuf, int compute, void* stream) {
   AVC_CHECK_ARG(xproj && w_hh && h && c && gates && B > 0 && T > 0 && H > 0 && (dirs == 1 || dirs == 2),
                 "avc_lstm_fwd: bad args");
   hipStream_t s = as_stream(stream);
@@ -904,6 +906,7 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
     p.xproj = xproj;
     p.w = reinterpret_cast<const bf16*>(w_hh);
     p.hout = h;
+    p.hout16 = reinterpret_cast<bf16*>(h_bf16);
     p.call = c;
     p.gall = gates;
     p.xbuf = reinterpret_cast<unsigned long long*>(hbuf);
@@ -916,6 +919,7 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
     else lstm_persist_fwd<512><<<ng * (H / PJU), 256, 0, s>>>(p);
     return avc_check_launch("avc_lstm_fwd(persistent)");
   }
+  AVC_CHECK_ARG(h_bf16 == nullptr, "avc_lstm_fwd: the bf16 h copy is produced by the persistent path only");
   const int mt = (H >= 1024 && B > 16) ? 2 : 1;  // 256 workgroups at B = 64
   dim3 g(H / 8, cdiv(B, 16 * mt), dirs);
   for (int st = 0; st < T; ++st) {

@@ -203,14 +203,23 @@ def lstm_timeout_flag(hbuf, B, H):
     return int(hbuf.view(torch.int32)[2 * B * H].item())
 
 
+def lstm_persistent_fwd(B, H, dirs):
+    """Whether avc_lstm_fwd takes the one-launch persistent path (mirrors lstm.hip)."""
+    return _COMPUTE == BF16 and dirs == 1 and H in (512, 1024) and os.environ.get("AVC_LSTM_NO_PERSIST") is None \
+        and ((B + 7) // 8) * (H // 32) <= num_cus()
+
+
 def lstm_fwd(xproj, w_hh, B, T, H, dirs, hbuf=None):
     dev = xproj.device
     h = torch.empty(B * T, dirs * H, device=dev)
     c = torch.empty(B * T, dirs * H, device=dev)
     g = torch.empty(B * T, dirs * 4 * H, device=dev)
-    L.call("avc_lstm_fwd", xproj.data_ptr(), w_hh.data_ptr(), _dt(w_hh), B, T, H, dirs, h.data_ptr(), c.data_ptr(),
-           g.data_ptr(), _ptr(hbuf), _COMPUTE if H > 64 else F32, stream())
-    return h, c, g
+    h16 = None
+    if hbuf is not None and H > 64 and lstm_persistent_fwd(B, H, dirs):
+        h16 = torch.empty(B * T, H, device=dev, dtype=torch.bfloat16)
+    L.call("avc_lstm_fwd", xproj.data_ptr(), w_hh.data_ptr(), _dt(w_hh), B, T, H, dirs, h.data_ptr(), _ptr(h16),
+           c.data_ptr(), g.data_ptr(), _ptr(hbuf), _COMPUTE if H > 64 else F32, stream())
+    return attach_twin(h, h16), c, g
 
 
 def lstm_persistent_bwd(B, H, dirs):
@@ -310,11 +319,12 @@ def convert(src, dtype, out=None):
     return out
 
 
-def transpose(src, dtype, out=None):
+def transpose(src, dtype, out=None, ld_out=0):
+    """out[c][r] = src[r][c] (out rows ld_out apart: a column block of a wider matrix)."""
     R, C = src.shape
     tdt = torch.bfloat16 if dtype == BF16 else torch.float32
     out = torch.empty(C, R, device=src.device, dtype=tdt) if out is None else out
-    L.call("avc_transpose", src.data_ptr(), out.data_ptr(), dtype, R, C, stream())
+    L.call("avc_transpose", src.data_ptr(), out.data_ptr(), dtype, R, C, int(ld_out), stream())
     return out
 
 

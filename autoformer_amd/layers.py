@@ -231,11 +231,13 @@ class _ConvBNFn(torch.autograd.Function):
         ctx.core, ctx.B, ctx.T_in, ctx.saved = core, B, T_in, saved
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, a)
+        ctx.x16 = getattr(x, "_bf16", None)
         return a
 
     @staticmethod
     def backward(ctx, dA):
         x, a = ctx.saved_tensors
+        K.attach_twin(x, ctx.x16)
         dA = dA.contiguous()
         n_dx = x.shape[1] if ctx.needs_input_grad[0] else 0
         dx, dW, db, dg, dbe = ctx.core.backward(dA, x, a, ctx.saved, ctx.B, ctx.T_in, n_dx)
@@ -260,11 +262,13 @@ class _EncConv0Fn(torch.autograd.Function):
         a, saved = core.forward(x, B, T)
         ctx.core, ctx.B, ctx.T, ctx.saved, ctx.n_mel = core, B, T, saved, mel2d.shape[1]
         ctx.save_for_backward(x, a)
+        ctx.x16 = getattr(x, "_bf16", None)
         return a
 
     @staticmethod
     def backward(ctx, dA):
         x, a = ctx.saved_tensors
+        K.attach_twin(x, ctx.x16)
         n_dx = ctx.n_mel if ctx.needs_input_grad[0] else 0
         dx, dW, db, dg, dbe = ctx.core.backward(dA.contiguous(), x, a, ctx.saved, ctx.B, ctx.T, n_dx)
         return dx, None, None, None, None, dW, db, dg, dbe
@@ -306,8 +310,8 @@ class LSTMLayerCore:
             large = H > 64
             whh = torch.empty(dirs * 4 * H, H, device=dev, dtype=tdt if large else torch.float32)
             whh_t = torch.empty(dirs * H, 4 * H, device=dev, dtype=tdt) if large else None
-            # W_ih^T (In x 4H) makes the input-gradient GEMM K-contiguous in both operands
-            wih_t = torch.empty(In, 4 * H, device=dev, dtype=tdt) if dirs == 1 else None
+            # W_ih^T (In x dirs*4H) makes the input-gradient GEMM K-contiguous in both operands
+            wih_t = torch.empty(In, dirs * 4 * H, device=dev, dtype=tdt)
             for d in range(dirs):
                 w_ih, w_hh, b_ih, b_hh = ps[4 * d: 4 * d + 4]
                 K.convert(w_ih, dt, out=wih[d * 4 * H:(d + 1) * 4 * H])
@@ -315,8 +319,8 @@ class LSTMLayerCore:
                 K.convert(w_hh, dt if large else K.F32, out=whh[d * 4 * H:(d + 1) * 4 * H])
                 if large:
                     K.transpose(w_hh, dt, out=whh_t[d * H:(d + 1) * H])
-            if wih_t is not None:
-                K.transpose(ps[0], dt, out=wih_t)
+            for d in range(dirs):
+                K.transpose(ps[4 * d], dt, out=wih_t[:, d * 4 * H:], ld_out=dirs * 4 * H)
             return wih, bsum, whh, whh_t, wih_t
         return self.cache.get(ps, build)
 
@@ -344,24 +348,33 @@ class LSTMLayerCore:
         sink = _SINK["on"]
         ps = self.params()
 
+        K.twin(dg)  # bf16 operand copy for the GEMMs (already there on the persistent path)
+        # GEMM operand sources: the bf16 twins when present (column views of them keep bf16)
+        dg_op = getattr(dg, "_bf16", None) if K.compute() == K.BF16 else None
+        dg_op = dg if dg_op is None else dg_op
+        h_op = getattr(h, "_bf16", None) if K.compute() == K.BF16 else None
+        h_op = h if h_op is None else h_op
+
         def wgrads():
             grads = []
             for d in range(dirs):
                 w_ih, w_hh, b_ih, b_hh = ps[4 * d: 4 * d + 4]
-                dgd = dg if dirs == 1 else dg[:, d * 4 * H:]  # the full tensor keeps its bf16 twin
+                dgd = dg_op if dirs == 1 else dg_op[:, d * 4 * H:]
                 dwih = _grad_of(w_ih) if sink else torch.empty(4 * H, In, device=x.device)
                 K.gemm(4 * H, In, M, operand(dgd, G, kstrided=True), operand(x, In, kstrided=True), dwih,
                        split_k=K.auto_split_k(4 * H, In, M), accumulate=sink)
                 dwhh = _grad_of(w_hh) if sink else torch.empty(4 * H, H, device=x.device)
                 shift = 1 if d == 0 else -1
+                hd = h_op if dirs == 1 else h_op[:, d * H:]
                 K.gemm(4 * H, H, M, operand(dgd, G, kstrided=True),
-                       operand(h[:, d * H:], dirs * H, kstrided=True, window=(1, shift, T, T, H)), dwhh,
+                       operand(hd, dirs * H, kstrided=True, window=(1, shift, T, T, H)), dwhh,
                        split_k=K.auto_split_k(4 * H, H, M), accumulate=sink)
+                dg32 = dg if dirs == 1 else dg[:, d * 4 * H:]
                 if sink:
-                    K.colsum(dgd, M, 4 * H, ld=G, out=_grad_of(b_ih), accumulate=True)
-                    K.colsum(dgd, M, 4 * H, ld=G, out=_grad_of(b_hh), accumulate=True)
+                    K.colsum(dg32, M, 4 * H, ld=G, out=_grad_of(b_ih), accumulate=True)
+                    K.colsum(dg32, M, 4 * H, ld=G, out=_grad_of(b_hh), accumulate=True)
                     continue
-                dbd = K.colsum(dgd, M, 4 * H, ld=G)
+                dbd = K.colsum(dg32, M, 4 * H, ld=G)
                 # b_ih and b_hh receive the same gradient but must not share storage
                 grads += [dwih, dwhh, dbd, K.convert(dbd, K.F32)]
             return grads
@@ -369,13 +382,10 @@ class LSTMLayerCore:
         dx = None
         if need_dx:
             dx = torch.empty(M, In, device=x.device)
-            if wih_t is not None:
-                K.gemm(M, In, G, operand(K.twin(dg), G), operand(wih_t, G), dx)
-            else:
-                K.gemm(M, In, G, operand(dg, G), operand(wih, In, kstrided=True), dx)
+            K.gemm(M, In, G, operand(dg, G), operand(wih_t, G), dx)
         if sink:
             with _Side(ev) as sd:
-                sd.keep(dg, x, h)
+                sd.keep(dg, x, h, dg_op, h_op)
                 wgrads()
             grads = [None] * (4 * dirs)
         else:
@@ -389,11 +399,15 @@ class _LSTMLayerFn(torch.autograd.Function):
         h, saved = core.forward(x, B, T)
         ctx.core, ctx.B, ctx.T, ctx.saved = core, B, T, saved
         ctx.save_for_backward(x, h)
+        # saved tensors come back as new Python objects: carry the bf16 twins explicitly
+        ctx.twins = (getattr(x, "_bf16", None), getattr(h, "_bf16", None))
         return h
 
     @staticmethod
     def backward(ctx, dh):
         x, h = ctx.saved_tensors
+        K.attach_twin(x, ctx.twins[0])
+        K.attach_twin(h, ctx.twins[1])
         dx, grads = ctx.core.backward(dh.contiguous(), x, h, ctx.saved, ctx.B, ctx.T, ctx.needs_input_grad[0])
         return (dx, None, None, None, *grads)
 

@@ -123,9 +123,10 @@ int avc_colsum(const float* x, long long ld, int M, int N, float* out, int accum
  * max(4*dirs*B*H, 8*B*H + 16) bytes.  For dirs == 1, H in {512, 1024} and enough CUs the
  * whole sequence runs as ONE persistent launch (W_hh slices register-resident, h_t
  * exchanged through tagged granules, bounded spins; timeout flag = u32 at byte 8*B*H of
- * hbuf); otherwise one fused kernel per time step. */
+ * hbuf); otherwise one fused kernel per time step.  The persistent launch can also write a
+ * bf16 copy of h (h_bf16, the next GEMMs' operand; else null — other paths need null). */
 int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T, int H, int dirs,
-                 float* h, float* c, float* gates, void* hbuf, int compute, void* stream);
+                 float* h, void* h_bf16, float* c, float* gates, void* hbuf, int compute, void* stream);
 
 /* Backward recurrence.  dh_out (B,T,dirs*H) = dL/dh; writes dgates (B,T,dirs*4H)
  * (pre-activation).  w_hh_t: dirs x [H][4H] transposed copy (large H) or w_hh itself
@@ -158,9 +159,12 @@ int avc_dec_concat_bwd(const float* dout, float* dcodes, int B, int T, int n_cod
  * grad_unpack: dWf[co][k][ci] -> dW[co][ci][k] (accumulate optional). */
 int avc_conv_pack(const float* w, void* out, int dtype, int Cout, int Cin, int Kw, int mode, void* stream);
 int avc_conv_grad_unpack(const float* dwf, float* dw, int Cout, int Cin, int Kw, int accumulate, void* stream);
-/* dst = convert(src) (n elements), and optional transpose of a [R][C] matrix. */
+/* dst = convert(src) (n elements). */
 int avc_convert(const float* src, void* dst, int dtype, long long n, void* stream);
-int avc_transpose(const float* src, void* dst, int dtype, int R, int C, void* stream);
+/* dst[c * ld_dst + r] = convert(src[r][c]) for a row-major [R][C] fp32 matrix (ld_dst = 0:
+ * R, a plain transpose; ld_dst > R: a column block of a wider matrix, e.g. the stacked
+ * W_ih^T of a bidirectional LSTM). */
+int avc_transpose(const float* src, void* dst, int dtype, int R, int C, long long ld_dst, void* stream);
 /* out = a + b elementwise (n), e.g. b_ih + b_hh. */
 int avc_add(const float* a, const float* b, float* out, long long n, void* stream);
 
