@@ -57,6 +57,7 @@ _SIGS = {
                              c_void_p, c_void_p, c_int, c_void_p]),
     "avc_lstm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                              c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "avc_lstm_trace": (c_int, [c_void_p]),
     "avc_enc_concat": (c_int, [c_void_p, c_ll, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_codes_gather": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_codes_scatter": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),

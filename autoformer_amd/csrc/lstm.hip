@@ -27,14 +27,23 @@
 namespace {
 
 // =============================================================== small H: persistent
+// The per-step inputs (xproj rows forward; dh, c, c_prev, gates backward) are staged in LDS
+// one chunk of SC steps ahead: each thread issues plain loads for chunk k+1 when chunk k
+// starts and writes them to the other LDS buffer when it ends, so the T-step dependency chain
+// only touches LDS and registers (a one-step prefetch left a global-memory round trip on
+// every step of the chain).
+constexpr int SC = 16;
+
 template <int HM>
 __global__ void __launch_bounds__(256) lstm_small_fwd(const float* __restrict__ xproj, const float* __restrict__ whh,
                                                       int T, int H, int dirs, float* __restrict__ hout,
                                                       float* __restrict__ cout, float* __restrict__ gout) {
+  constexpr int GM = 4 * HM, NPF = (SC * GM + 255) / 256;
   const int b = blockIdx.x, d = blockIdx.y, tid = threadIdx.x;
   const int G = 4 * H;
   __shared__ __attribute__((aligned(16))) float hs[HM];
-  __shared__ float gs[4 * HM];
+  __shared__ float gs[GM];
+  __shared__ float xs[2][SC * GM];
   float w[HM];
   const float* W = whh + (long long)d * G * H;
 #pragma unroll
@@ -44,19 +53,40 @@ __global__ void __launch_bounds__(256) lstm_small_fwd(const float* __restrict__ 
   const long long ldx = (long long)dirs * G, ldh = (long long)dirs * H;
   const int q = tid < G ? tid / H : 0;
   const int t0 = d ? T - 1 : 0, dt = d ? -1 : 1;
-  float xn = tid < G ? xproj[((long long)b * T + t0) * ldx + d * G + tid] : 0.f;
+  const float* xb = xproj + (long long)b * T * ldx + d * G;
+  // chunk element e: step s = k*SC + e/G, gate row e%G
+  float pf[NPF];
+  auto issue = [&](int k) {
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int e = tid + 256 * i, si = e / G, s = k * SC + si;
+      pf[i] = (si < SC && s < T) ? xb[(long long)(t0 + dt * s) * ldx + (e - si * G)] : 0.f;
+    }
+  };
+  auto commit = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int e = tid + 256 * i;
+      if (e < SC * G) xs[buf][e] = pf[i];
+    }
+  };
+  const int nch = (T + SC - 1) / SC;
+  issue(0);
+  commit(0);
   __syncthreads();
-  for (int s = 0; s < T; ++s) {
-    const int t = t0 + dt * s;
-    const float x = xn;
-    if (s + 1 < T && tid < G) xn = xproj[((long long)b * T + t + dt) * ldx + d * G + tid];
+  for (int k = 0; k < nch; ++k) {
+    if (k + 1 < nch) issue(k + 1);
+    const float* xk = xs[k & 1];
+    const int ns = min(SC, T - k * SC);
+  for (int i = 0; i < ns; ++i) {
+    const int t = t0 + dt * (k * SC + i);
     if (tid < G) {
-      float acc = x;
+      float acc = xk[i * G + tid];
       const f32x4* h4 = reinterpret_cast<const f32x4*>(hs);
 #pragma unroll
-      for (int k = 0; k < HM / 4; ++k) {
-        f32x4 hv = h4[k];
-        acc += hv[0] * w[4 * k] + hv[1] * w[4 * k + 1] + hv[2] * w[4 * k + 2] + hv[3] * w[4 * k + 3];
+      for (int kq = 0; kq < HM / 4; ++kq) {
+        f32x4 hv = h4[kq];
+        acc += hv[0] * w[4 * kq] + hv[1] * w[4 * kq + 1] + hv[2] * w[4 * kq + 2] + hv[3] * w[4 * kq + 3];
       }
       const float gv = q == 2 ? tanhf(acc) : sigmoidf_(acc);
       gs[tid] = gv;
@@ -74,16 +104,23 @@ __global__ void __launch_bounds__(256) lstm_small_fwd(const float* __restrict__ 
     }
     __syncthreads();
   }
+    if (k + 1 < nch) {
+      commit((k + 1) & 1);
+      __syncthreads();
+    }
+  }
 }
 
 template <int HM>
 __global__ void __launch_bounds__(256) lstm_small_bwd(const float* __restrict__ dhout, const float* __restrict__ call,
                                                       const float* __restrict__ gall, const float* __restrict__ whh,
                                                       int T, int H, int dirs, float* __restrict__ dg) {
+  constexpr int RM = 7 * HM, NPF = (SC * RM + 255) / 256;
   const int b = blockIdx.x, d = blockIdx.y, tid = threadIdx.x;
-  const int G = 4 * H;
+  const int G = 4 * H, R = 7 * H;
   __shared__ float dhs[HM];
   __shared__ float dgs[4 * HM];
+  __shared__ float rs[2][SC * RM];  // per step: dh | c | c_prev | i f g o
   // k-role: thread (k = tid>>2, q = tid&3) holds W[q*H + g'][k], g' < H
   const int kk = tid >> 2, qq = tid & 3;
   float wc[HM];
@@ -97,28 +134,54 @@ __global__ void __launch_bounds__(256) lstm_small_bwd(const float* __restrict__ 
   // backward walks opposite to the forward recurrence
   const int t0 = d ? 0 : T - 1, dt = d ? 1 : -1;
   const int fwd_prev = d ? 1 : -1;  // offset of the forward's previous time step
-  float pdh = 0, pc = 0, pcp = 0, pi = 0, pf = 0, pg = 0, po = 0;
-  auto fetch = [&](int t) {
-    if (tid < H) {
-      const long long o = ((long long)b * T + t) * ldh + d * H + tid;
-      const long long og = ((long long)b * T + t) * ldg + d * G + tid;
-      pdh = dhout[o];
-      pc = call[o];
-      const int tp = t + fwd_prev;
-      pcp = (tp >= 0 && tp < T) ? call[((long long)b * T + tp) * ldh + d * H + tid] : 0.f;
-      pi = gall[og];
-      pf = gall[og + H];
-      pg = gall[og + 2 * H];
-      po = gall[og + 3 * H];
+  const float* dhb = dhout + (long long)b * T * ldh + d * H;
+  const float* cb = call + (long long)b * T * ldh + d * H;
+  const float* gb = gall + (long long)b * T * ldg + d * G;
+  // chunk element e: step s = k*SC + e/R, column e%R of the staged row
+  float pf[NPF];
+  auto issue = [&](int k) {
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int e = tid + 256 * i, si = e / R, col = e - si * R, s = k * SC + si;
+      float v = 0.f;
+      if (si < SC && s < T) {
+        const int t = t0 + dt * s, seg = col / H, u = col - seg * H;
+        if (seg == 0) {
+          v = dhb[(long long)t * ldh + u];
+        } else if (seg == 1) {
+          v = cb[(long long)t * ldh + u];
+        } else if (seg == 2) {
+          const int tp = t + fwd_prev;
+          v = (tp >= 0 && tp < T) ? cb[(long long)tp * ldh + u] : 0.f;
+        } else {
+          v = gb[(long long)t * ldg + (col - 3 * H)];
+        }
+      }
+      pf[i] = v;
     }
   };
-  fetch(t0);
+  auto commit = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int e = tid + 256 * i;
+      if (e < SC * R) rs[buf][e] = pf[i];
+    }
+  };
+  const int nch = (T + SC - 1) / SC;
+  issue(0);
+  commit(0);
   __syncthreads();
-  for (int s = 0; s < T; ++s) {
-    const int t = t0 + dt * s;
+  for (int k = 0; k < nch; ++k) {
+    if (k + 1 < nch) issue(k + 1);
+    const float* rk = rs[k & 1];
+    const int ns = min(SC, T - k * SC);
+  for (int i = 0; i < ns; ++i) {
+    const int t = t0 + dt * (k * SC + i);
     if (tid < H) {
-      const float dh = pdh + dhs[tid];
-      const float c = pc, cp = pcp, ig = pi, fg = pf, gg = pg, og = po;
+      const float* row = rk + i * R;
+      const float dh = row[tid] + dhs[tid];
+      const float c = row[H + tid], cp = row[2 * H + tid];
+      const float ig = row[3 * H + tid], fg = row[4 * H + tid], gg = row[5 * H + tid], og = row[6 * H + tid];
       const float tc = tanhf(c);
       const float do_ = dh * tc;
       float dcs = dc + dh * og * (1.f - tc * tc);
@@ -136,7 +199,6 @@ __global__ void __launch_bounds__(256) lstm_small_bwd(const float* __restrict__ 
       dgs[2 * H + tid] = a2;
       dgs[3 * H + tid] = a3;
     }
-    if (s + 1 < T) fetch(t + dt);
     __syncthreads();
     if (tid < 4 * H) {
       float p = 0.f;
@@ -148,6 +210,11 @@ __global__ void __launch_bounds__(256) lstm_small_bwd(const float* __restrict__ 
       if (qq == 0 && kk < H) dhs[kk] = p;
     }
     __syncthreads();
+  }
+    if (k + 1 < nch) {
+      commit((k + 1) & 1);
+      __syncthreads();
+    }
   }
 }
 
@@ -569,8 +636,42 @@ struct PersistArgs {
   float* gall;
   unsigned long long* xbuf;  // [2][B][H/2] granules, zeroed before launch
   unsigned* flag;            // timeout flag
+  unsigned long long* trace;  // diagnostics (avc_lstm_trace), null in production
   int B, T, ng;
 };
+
+// Diagnostics: avc_lstm_trace(buf) makes the persistent kernels record the 100 MHz REALTIME
+// clock at four points of every step of every workgroup into buf[(wg*T + step)*4 + j]:
+// j = 0 step start, 1 exchange complete, 2 recurrent product reduced, 3 step published.
+// The stamps go to that buffer only; nothing reads them inside the kernel.
+unsigned long long* g_trace = nullptr;
+
+__device__ __forceinline__ void stamp(unsigned long long* tr, int T, int s, int j) {
+  if (tr && threadIdx.x == 0) tr[((long long)blockIdx.x * T + s) * 4 + j] = __builtin_amdgcn_s_memrealtime();
+}
+
+// Wave 0 polls ONE granule per producing workgroup (lane r reads `src + r*stride`, the
+// granule that producer stores last) until all NR tags match, so waiting consumers re-read
+// NR words per pass instead of their whole gather (a full-sweep spin by every workgroup kept
+// the fabric busy with re-reads of granules that had not changed).  The full sweep that
+// follows still checks every tag.  Returns false (flag raised) after a spin timeout.
+__device__ __forceinline__ bool probe_producers(const unsigned long long* src, int stride, int NR, unsigned tag,
+                                                unsigned* flag) {
+  const int lane = threadIdx.x & 63;
+  unsigned spins = 0;
+  while (true) {
+    bool ok = true;
+    if (lane < NR)
+      ok = (unsigned)(__hip_atomic_load(src + (long long)lane * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >>
+                      32) == tag;
+    if (__all(ok)) return true;
+    if (++spins > PSPIN) {
+      if (lane == 0) atomicOr(flag, 1u);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
 
 __device__ __forceinline__ unsigned long long granule(unsigned tag, float a, float b) {
   bf16x2 h = {(bf16)a, (bf16)b};
@@ -650,6 +751,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
 
   for (int s = 0; s < T; ++s) {
     const int t = s;
+    stamp(a.trace, T, s, 0);
     float px[4] = {0.f, 0.f, 0.f, 0.f};
     if (pv) {
       const float* xp = a.xproj + ((long long)pb * T + t) * G + pj;
@@ -658,11 +760,16 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
     }
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     if (s > 0) {
-      // ---- gather the group's h_{t-1} (tag == s) into the LDS A tile
+      // ---- gather the group's h_{t-1} (tag == s) into the LDS A tile: wave 0 first waits
+      // for every member's last granule (row 0, pair 15 of its 32 units), then all sweep
       const unsigned long long* src = a.xbuf + (long long)((s - 1) & 1) * B * H2 + (long long)b0 * H2;
-      if (!gather_granules<NGR, H2, 16>(src, As, AP, need0, (unsigned)s, a.flag)) quit = 1;
+      if (w == 0 && !probe_producers(src + PJU / 2 - 1, PJU / 2, H / PJU, (unsigned)s, a.flag)) quit = 1;
       __syncthreads();
       if (quit) return;  // block-uniform exit after a spin timeout
+      if (!gather_granules<NGR, H2, 16>(src, As, AP, need0, (unsigned)s, a.flag)) quit = 1;
+      __syncthreads();
+      if (quit) return;
+      stamp(a.trace, T, s, 1);
 #pragma unroll
       for (int k = 0; k < NK; ++k) {
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + (lane & 15) * AP + 32 * k + 8 * (lane >> 4));
@@ -678,6 +785,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
       }
     }
     __syncthreads();
+    stamp(a.trace, T, s, 2);
     float h = 0.f, ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f;
     if (pv) {
       ig = sigmoidf_(px[0] + gs[pr][pu]);
@@ -691,6 +799,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
     if (pv && !(pu & 1) && s + 1 < T)
       __hip_atomic_store(a.xbuf + (long long)(s & 1) * B * H2 + (long long)pb * H2 + (pj >> 1),
                          granule((unsigned)(s + 1), h, hn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    stamp(a.trace, T, s, 3);
     if (pv) {
       const long long oh = ((long long)pb * T + t) * H + pj;
       a.hout[oh] = h;
@@ -724,6 +833,7 @@ struct PersistBwdArgs {
   bf16* dg16;          // (B,T,4H) or null
   unsigned long long* xbuf;  // [2][B][2H] granules, zeroed before launch
   unsigned* flag;
+  unsigned long long* trace;  // diagnostics (avc_lstm_trace), null in production
   int B, T, ng;
 };
 
@@ -764,6 +874,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
 
   for (int s = 0; s < T; ++s) {
     const int t = T - 1 - s;
+    stamp(a.trace, T, s, 0);
     // per-element inputs of this step (independent of the exchange: issued first)
     float dh = 0.f, ct = 0.f, cp = 0.f, gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f;
     if (pv) {
@@ -779,9 +890,15 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
     }
     if (s > 0) {
       const unsigned long long* src = a.xbuf + (long long)((s - 1) & 1) * B * G2 + (long long)b0 * G2;
-      if (!gather_granules<NGR, G2, 16>(src, As, AP, need0, (unsigned)s, a.flag)) *quit = 1;
+      // wave 0 waits for every member's last granule (row 0, gate o, pair 15), then all sweep
+      if (w == 0 && !probe_producers(src + 3 * H / 2 + PJU / 2 - 1, PJU / 2, H / PJU, (unsigned)s, a.flag))
+        *quit = 1;
       __syncthreads();
       if (*quit) return;  // block-uniform exit after a spin timeout
+      if (!gather_granules<NGR, G2, 16>(src, As, AP, need0, (unsigned)s, a.flag)) *quit = 1;
+      __syncthreads();
+      if (*quit) return;
+      stamp(a.trace, T, s, 1);
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
       const bf16* ap = As + arow * AP + w * H + 8 * (lane >> 4);
 #pragma unroll
@@ -799,6 +916,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
         }
       }
       __syncthreads();
+      stamp(a.trace, T, s, 2);
 #pragma unroll
       for (int ww = 0; ww < 4; ++ww) dh += red[(ww * PRG + pr) * (PJU + 1) + pu];
     }
@@ -822,6 +940,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
       __hip_atomic_store(dst + H, granule(tag, v2, n2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(dst + 3 * H / 2, granule(tag, v3, n3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    stamp(a.trace, T, s, 3);
     if (pv) {
       const long long og = ((long long)pb * T + t) * G + pj;
       a.dg[og] = v0;
@@ -867,6 +986,11 @@ void launch_small_bwd(dim3 g, hipStream_t s, const float* dh, const float* c, co
 
 }  // namespace
 
+extern "C" int avc_lstm_trace(void* buf) {
+  g_trace = reinterpret_cast<unsigned long long*>(buf);
+  return 0;
+}
+
 extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T, int H, int dirs, float* h,
                             void* h_bf16, float* c, float* gates, void* hbuf, int compute, void* stream) {
   AVC_CHECK_ARG(xproj && w_hh && h && c && gates && B > 0 && T > 0 && H > 0 && (dirs == 1 || dirs == 2),
@@ -911,6 +1035,7 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
     p.gall = gates;
     p.xbuf = reinterpret_cast<unsigned long long*>(hbuf);
     p.flag = reinterpret_cast<unsigned*>(p.xbuf + (size_t)2 * B * (H / 2));
+    p.trace = g_trace;
     p.B = B;
     p.T = T;
     p.ng = ng;
@@ -974,6 +1099,7 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
     p.dg16 = reinterpret_cast<bf16*>(dgates_bf16);
     p.xbuf = reinterpret_cast<unsigned long long*>(gbuf);
     p.flag = reinterpret_cast<unsigned*>(p.xbuf + (size_t)2 * B * (2 * H));
+    p.trace = g_trace;
     p.B = B;
     p.T = T;
     p.ng = ng;

@@ -141,6 +141,12 @@ int avc_lstm_bwd(const float* dh_out, const float* h, const float* c, const floa
                  const void* w_hh, const void* w_hh_t, int wdtype, int B, int T, int H, int dirs,
                  float* dgates, void* dgates_bf16, float* dcbuf, void* gbuf, int compute, void* stream);
 
+/* Diagnostics (no reference counterpart): with buf non-null, later persistent LSTM launches
+ * record the 100 MHz realtime clock at 4 points of every step of every workgroup into
+ * buf[(workgroup*T + step)*4 + j] (j: step start, exchange complete, product reduced,
+ * published; u64, caller-sized).  null switches it off (the default). */
+int avc_lstm_trace(void* buf);
+
 /* Elementwise / layout kernels of the model glue (AutoVC.py:46-48, 56-66, 197-207). */
 int avc_enc_concat(const float* mel, long long mel_ld, const float* emb, float* out, int B, int T,
                    int n_mel, int d_emb, void* stream);

@@ -218,7 +218,8 @@ def _lstm_case(B, T, In, H, dirs, comp):
 
 
 @pytest.mark.parametrize("B,T,In,H,dirs", [(4, 33, 512, 44, 2), (3, 20, 88, 44, 2), (5, 17, 344, 512, 1),
-                                           (20, 9, 512, 1024, 1), (2, 12, 96, 128, 2)])
+                                           (20, 9, 512, 1024, 1), (2, 12, 96, 128, 2), (2, 176, 96, 64, 1),
+                                           (3, 50, 40, 16, 2)])
 def test_lstm_layer_fp32(B, T, In, H, dirs):
     res = _lstm_case(B, T, In, H, dirs, "fp32")
     bad = {k: v for k, v in res.items() if v > 1e-4}
