@@ -27,31 +27,59 @@
 namespace {
 
 // =============================================================== small H: persistent
+// One workgroup owns one (utterance, direction) for all T steps; no inter-workgroup sync.
+// Thread (j, q) = (tid >> 2, tid & 3) owns gate q of hidden unit j, so the four gates of a
+// unit sit in one lane quad: the cell update reads them with DPP quad broadcasts and only
+// h_t (forward) / dG_t (backward) crosses lanes through LDS -- ONE workgroup barrier per
+// step, LDS double-buffered by step parity.  Forward: lane (j, q) keeps row q*H + j of W_hh
+// in registers; backward: lane (j', q) keeps column j' of gate block q, and the quad's four
+// partial products sum with DPP xor steps, leaving dh_rec[j'] in every lane of the quad.
 // The per-step inputs (xproj rows forward; dh, c, c_prev, gates backward) are staged in LDS
-// one chunk of SC steps ahead: each thread issues plain loads for chunk k+1 when chunk k
-// starts and writes them to the other LDS buffer when it ends, so the T-step dependency chain
-// only touches LDS and registers (a one-step prefetch left a global-memory round trip on
-// every step of the chain).
+// one chunk of SC steps ahead: plain loads for chunk k+1 are issued when chunk k starts and
+// written to LDS when it ends; the SC steps of a chunk are unrolled, so no loop boundary
+// makes the compiler drain those loads early.
 constexpr int SC = 16;
 
-template <int HM>
+__device__ __forceinline__ float fsig(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float ftanh(float x) { return 2.f * fsig(2.f * x) - 1.f; }
+// FAST (bf16 compute mode): v_exp_f32 / v_rcp_f32 forms; otherwise the IEEE library forms, so
+// the fp32 parity mode keeps the reference's activation arithmetic
+template <bool FAST>
+__device__ __forceinline__ float act_sig(float x) { return FAST ? fsig(x) : sigmoidf_(x); }
+template <bool FAST>
+__device__ __forceinline__ float act_tanh(float x) { return FAST ? ftanh(x) : tanhf(x); }
+
+// broadcast lane N of each lane quad (DPP quad_perm, no LDS traffic)
+template <int N>
+__device__ __forceinline__ float quad_bcast(float v) {
+  constexpr int ctl = N | (N << 2) | (N << 4) | (N << 6);
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctl, 0xf, 0xf, false));
+}
+// sum over the lane quad (xor 1, then xor 2, as quad_perm)
+__device__ __forceinline__ float quad_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xf, 0xf, false));
+  return v;
+}
+
+template <int HM, bool FAST>
 __global__ void __launch_bounds__(256) lstm_small_fwd(const float* __restrict__ xproj, const float* __restrict__ whh,
                                                       int T, int H, int dirs, float* __restrict__ hout,
                                                       float* __restrict__ cout, float* __restrict__ gout) {
   constexpr int GM = 4 * HM, NPF = (SC * GM + 255) / 256;
   const int b = blockIdx.x, d = blockIdx.y, tid = threadIdx.x;
   const int G = 4 * H;
-  __shared__ __attribute__((aligned(16))) float hs[HM];
-  __shared__ float gs[GM];
+  const int j = tid >> 2, q = tid & 3, row = q * H + j;
+  const bool act = j < H;
+  __shared__ __attribute__((aligned(16))) float hs[2][HM];
   __shared__ float xs[2][SC * GM];
   float w[HM];
   const float* W = whh + (long long)d * G * H;
 #pragma unroll
-  for (int k = 0; k < HM; ++k) w[k] = (tid < G && k < H) ? W[(long long)tid * H + k] : 0.f;
-  if (tid < HM) hs[tid] = 0.f;
+  for (int k = 0; k < HM; ++k) w[k] = (act && k < H) ? W[(long long)row * H + k] : 0.f;
+  if (tid < 2 * HM) hs[tid / HM][tid % HM] = 0.f;
   float c = 0.f;
   const long long ldx = (long long)dirs * G, ldh = (long long)dirs * H;
-  const int q = tid < G ? tid / H : 0;
   const int t0 = d ? T - 1 : 0, dt = d ? -1 : 1;
   const float* xb = xproj + (long long)b * T * ldx + d * G;
   // chunk element e: step s = k*SC + e/G, gate row e%G
@@ -78,32 +106,38 @@ __global__ void __launch_bounds__(256) lstm_small_fwd(const float* __restrict__ 
     if (k + 1 < nch) issue(k + 1);
     const float* xk = xs[k & 1];
     const int ns = min(SC, T - k * SC);
-  for (int i = 0; i < ns; ++i) {
-    const int t = t0 + dt * (k * SC + i);
-    if (tid < G) {
-      float acc = xk[i * G + tid];
-      const f32x4* h4 = reinterpret_cast<const f32x4*>(hs);
 #pragma unroll
-      for (int kq = 0; kq < HM / 4; ++kq) {
-        f32x4 hv = h4[kq];
-        acc += hv[0] * w[4 * kq] + hv[1] * w[4 * kq + 1] + hv[2] * w[4 * kq + 2] + hv[3] * w[4 * kq + 3];
+    for (int i = 0; i < SC; ++i) {
+      if (i < ns) {
+        const int s = k * SC + i, t = t0 + dt * s;
+        const f32x4* h4 = reinterpret_cast<const f32x4*>(hs[s & 1]);
+        float a0 = act ? xk[i * G + row] : 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+        for (int kq = 0; kq < HM / 4; ++kq) {
+          const f32x4 hv = h4[kq];
+          a0 += hv[0] * w[4 * kq];
+          a1 += hv[1] * w[4 * kq + 1];
+          a2 += hv[2] * w[4 * kq + 2];
+          a3 += hv[3] * w[4 * kq + 3];
+        }
+        const float pre = (a0 + a1) + (a2 + a3);
+        const float gv = q == 2 ? act_tanh<FAST>(pre) : act_sig<FAST>(pre);
+        const float ig = quad_bcast<0>(gv), fg = quad_bcast<1>(gv), gg = quad_bcast<2>(gv), og = quad_bcast<3>(gv);
+        c = fg * c + ig * gg;
+        const float h = og * act_tanh<FAST>(c);
+        if (act) {
+          const long long o = ((long long)b * T + t) * ldh + d * H + j;
+          if (q == 0) {
+            hs[(s + 1) & 1][j] = h;
+            hout[o] = h;
+          } else if (q == 1) {
+            cout[o] = c;
+          }
+          gout[((long long)b * T + t) * ldx + d * G + row] = gv;
+        }
+        __syncthreads();
       }
-      const float gv = q == 2 ? tanhf(acc) : sigmoidf_(acc);
-      gs[tid] = gv;
-      gout[((long long)b * T + t) * ldx + d * G + tid] = gv;
     }
-    __syncthreads();
-    if (tid < H) {
-      const float ig = gs[tid], fg = gs[H + tid], gg = gs[2 * H + tid], og = gs[3 * H + tid];
-      c = fg * c + ig * gg;
-      const float h = og * tanhf(c);
-      hs[tid] = h;
-      const long long o = ((long long)b * T + t) * ldh + d * H + tid;
-      hout[o] = h;
-      cout[o] = c;
-    }
-    __syncthreads();
-  }
     if (k + 1 < nch) {
       commit((k + 1) & 1);
       __syncthreads();
@@ -111,24 +145,23 @@ __global__ void __launch_bounds__(256) lstm_small_fwd(const float* __restrict__ 
   }
 }
 
-template <int HM>
+template <int HM, bool FAST>
 __global__ void __launch_bounds__(256) lstm_small_bwd(const float* __restrict__ dhout, const float* __restrict__ call,
                                                       const float* __restrict__ gall, const float* __restrict__ whh,
                                                       int T, int H, int dirs, float* __restrict__ dg) {
   constexpr int RM = 7 * HM, NPF = (SC * RM + 255) / 256;
   const int b = blockIdx.x, d = blockIdx.y, tid = threadIdx.x;
   const int G = 4 * H, R = 7 * H;
-  __shared__ float dhs[HM];
-  __shared__ float dgs[4 * HM];
+  const int j = tid >> 2, q = tid & 3;
+  const bool act = j < H;
+  __shared__ __attribute__((aligned(16))) float dgs[2][4 * HM];
   __shared__ float rs[2][SC * RM];  // per step: dh | c | c_prev | i f g o
-  // k-role: thread (k = tid>>2, q = tid&3) holds W[q*H + g'][k], g' < H
-  const int kk = tid >> 2, qq = tid & 3;
+  // lane (j, q) holds column j of gate block q: wc[g] = W[q*H + g][j]
   float wc[HM];
   const float* W = whh + (long long)d * G * H;
 #pragma unroll
-  for (int g = 0; g < HM; ++g) wc[g] = (kk < H && g < H) ? W[(long long)(qq * H + g) * H + kk] : 0.f;
-  if (tid < HM) dhs[tid] = 0.f;
-  for (int i = tid; i < 4 * HM; i += 256) dgs[i] = 0.f;
+  for (int g = 0; g < HM; ++g) wc[g] = (act && g < H) ? W[(long long)(q * H + g) * H + j] : 0.f;
+  for (int i = tid; i < 8 * HM; i += 256) dgs[i / (4 * HM)][i % (4 * HM)] = 0.f;
   float dc = 0.f;
   const long long ldg = (long long)dirs * G, ldh = (long long)dirs * H;
   // backward walks opposite to the forward recurrence
@@ -175,42 +208,44 @@ __global__ void __launch_bounds__(256) lstm_small_bwd(const float* __restrict__ 
     if (k + 1 < nch) issue(k + 1);
     const float* rk = rs[k & 1];
     const int ns = min(SC, T - k * SC);
-  for (int i = 0; i < ns; ++i) {
-    const int t = t0 + dt * (k * SC + i);
-    if (tid < H) {
-      const float* row = rk + i * R;
-      const float dh = row[tid] + dhs[tid];
-      const float c = row[H + tid], cp = row[2 * H + tid];
-      const float ig = row[3 * H + tid], fg = row[4 * H + tid], gg = row[5 * H + tid], og = row[6 * H + tid];
-      const float tc = tanhf(c);
-      const float do_ = dh * tc;
-      float dcs = dc + dh * og * (1.f - tc * tc);
-      const float di = dcs * gg, dgg = dcs * ig, df = dcs * cp;
-      dc = dcs * fg;
-      const float a0 = di * ig * (1.f - ig), a1 = df * fg * (1.f - fg), a2 = dgg * (1.f - gg * gg),
-                  a3 = do_ * og * (1.f - og);
-      const long long og_ = ((long long)b * T + t) * ldg + d * G + tid;
-      dg[og_] = a0;
-      dg[og_ + H] = a1;
-      dg[og_ + 2 * H] = a2;
-      dg[og_ + 3 * H] = a3;
-      dgs[tid] = a0;
-      dgs[H + tid] = a1;
-      dgs[2 * H + tid] = a2;
-      dgs[3 * H + tid] = a3;
-    }
-    __syncthreads();
-    if (tid < 4 * H) {
-      float p = 0.f;
-      const float* src = dgs + qq * H;
 #pragma unroll
-      for (int g = 0; g < HM; ++g) p += (g < H ? src[g] : 0.f) * wc[g];
-      p += __shfl_xor(p, 1, 64);
-      p += __shfl_xor(p, 2, 64);
-      if (qq == 0 && kk < H) dhs[kk] = p;
+    for (int i = 0; i < SC; ++i) {
+      if (i < ns) {
+        const int s = k * SC + i, t = t0 + dt * s;
+        // recurrent part dh_rec[j] = sum_{q', g} dG_{s-1}[q'*H + g] W[q'*H + g][j]: this lane
+        // sums gate block q (entries past H meet zero weights), the quad adds the four blocks
+        const float* gq = dgs[(s + 1) & 1] + q * H;
+        float p0 = 0.f, p1 = 0.f;
+        if (H % 4 == 0) {
+          const f32x4* g4 = reinterpret_cast<const f32x4*>(gq);
+#pragma unroll
+          for (int g = 0; g < HM / 4; ++g) {
+            const f32x4 v = g4[g];
+            p0 += v[0] * wc[4 * g] + v[2] * wc[4 * g + 2];
+            p1 += v[1] * wc[4 * g + 1] + v[3] * wc[4 * g + 3];
+          }
+        } else {
+#pragma unroll
+          for (int g = 0; g < HM; ++g) p0 += (g < H ? gq[g] : 0.f) * wc[g];
+        }
+        const float* rw = rk + i * R;
+        const float dh = (act ? rw[j] : 0.f) + quad_sum(p0 + p1);
+        if (act) {
+          const float c = rw[H + j], cp = rw[2 * H + j];
+          const float ig = rw[3 * H + j], fg = rw[4 * H + j], gg = rw[5 * H + j], og = rw[6 * H + j];
+          const float tc = act_tanh<FAST>(c);
+          const float dcs = dc + dh * og * (1.f - tc * tc);
+          const float v = q == 0 ? dcs * gg * ig * (1.f - ig)
+                        : q == 1 ? dcs * cp * fg * (1.f - fg)
+                        : q == 2 ? dcs * ig * (1.f - gg * gg)
+                                 : dh * tc * og * (1.f - og);
+          dc = dcs * fg;
+          dgs[s & 1][q * H + j] = v;
+          dg[((long long)b * T + t) * ldg + d * G + q * H + j] = v;
+        }
+        __syncthreads();
+      }
     }
-    __syncthreads();
-  }
     if (k + 1 < nch) {
       commit((k + 1) & 1);
       __syncthreads();
@@ -614,18 +649,39 @@ __global__ void __launch_bounds__(512) lstm_step_bwd_bf(StepArgs a) {
   }
 }
 
-// =============================================================== large H: persistent forward
-// One launch for all T steps.  Workgroups form NG groups of H/32; group g owns utterance
-// rows [8g, 8g+8), member r owns hidden units [32r, 32r+32) and keeps the matching
-// 128 rows of W_hh (all four gates) in VGPRs for the whole sequence (wave w = gate w).
-// h_t is exchanged inside the group through data-tagged 8-byte granules {tag = step+1,
-// two bf16}: one agent-scope (sc1) store per granule, consumers re-read with agent-scope
-// loads until every tag matches (MI355X_MICROARCH.md hand-off R2: no flag, no fence).
-// Groups are blockIdx % NG: with round-robin dispatch a group sits on one XCD and the
-// exchange stays in that XCD's L2 -- a speed assumption only, correctness holds for any
-// placement.  Every spin is bounded; on timeout the kernel raises a flag and exits.
-constexpr int PRG = 8, PJU = 32;
+// =============================================================== large H: persistent recurrences
+// One launch for all T steps of a dirs == 1 layer (decoder lstm1 H=512, lstm2 H=1024).
+// Workgroups form NG groups of H/32 members; group g owns utterance rows [8g, 8g+8), member r
+// owns hidden units [32r, 32r+32) and keeps the matching W_hh slice in VGPRs for the whole
+// sequence.  Every step each member needs the whole group's previous output (forward h_{t-1}:
+// 8 x H bf16; backward dG_{t+1}: 8 x 4H bf16), handed over inside the launch by the
+// write-through form of MI355X_MICROARCH.md "Valid forms" (table row 1):
+//   producer: its tile is staged in LDS, wave 0 stores it with 16-B sc1 (write-through)
+//             buffer stores, waits s_waitcnt vmcnt(0), then lane 0 stores the member's flag
+//             = step + 1 (agent-scope relaxed atomic store = an sc1 store);
+//   consumer: wave 0 polls the group's flags with sc1 loads until every member reached the
+//             step, the workgroup barrier releases the other waves, and every thread loads its
+//             16-B chunks with sc1 buffer loads (L1 bypassed; every handed-off byte is stored
+//             and loaded sc1, so no acquire fence).
+// Compared with 8-byte {tag, 2 x bf16} granules this moves half the bytes per consumer with
+// 16-B accesses, and a waiting consumer re-reads only the flag words.  The payload is
+// double-buffered by step parity: a member publishes step s+1 only after consuming step s-1
+// from every member, so no slot is overwritten while it is read.  Flags are monotone step
+// tags zeroed before every launch; every spin is bounded (timeout -> ctl[0] raised, exit).
+// Groups are blockIdx % NG: with round-robin dispatch a group shares one XCD -- a speed
+// assumption only, correctness holds for any placement.
+//
+// Scratch (hbuf forward / gbuf backward):
+//   u32 ctl[4] (ctl[0] = timeout flag) | u32 flags[NG][64] | pad to 256 B | bf16 payload [2][B][W]
+// with W = H (forward) or 4H (backward); only ctl + flags are zeroed per launch.
+constexpr int PRG = 8, PJU = 32, PFL = 64;
 constexpr unsigned PSPIN = 1u << 22;
+constexpr int AUX_SC1 = 16;  // buffer-instruction cache-policy bits: sc1
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+constexpr size_t px_ctl_bytes(int ng) { return 16 + (size_t)ng * PFL * 4; }
+constexpr size_t px_payload_off(int ng) { return (px_ctl_bytes(ng) + 255) & ~(size_t)255; }
 
 struct PersistArgs {
   const float* xproj;
@@ -634,8 +690,8 @@ struct PersistArgs {
   bf16* hout16;  // optional bf16 copy of h
   float* call;
   float* gall;
-  unsigned long long* xbuf;  // [2][B][H/2] granules, zeroed before launch
-  unsigned* flag;            // timeout flag
+  unsigned* ctl;              // scratch: ctl[0] timeout flag, flags from word 4
+  bf16* pay;                  // payload [2][B][H]
   unsigned long long* trace;  // diagnostics (avc_lstm_trace), null in production
   int B, T, ng;
 };
@@ -650,86 +706,89 @@ __device__ __forceinline__ void stamp(unsigned long long* tr, int T, int s, int 
   if (tr && threadIdx.x == 0) tr[((long long)blockIdx.x * T + s) * 4 + j] = __builtin_amdgcn_s_memrealtime();
 }
 
-// Wave 0 polls ONE granule per producing workgroup (lane r reads `src + r*stride`, the
-// granule that producer stores last) until all NR tags match, so waiting consumers re-read
-// NR words per pass instead of their whole gather (a full-sweep spin by every workgroup kept
-// the fabric busy with re-reads of granules that had not changed).  The full sweep that
-// follows still checks every tag.  Returns false (flag raised) after a spin timeout.
-__device__ __forceinline__ bool probe_producers(const unsigned long long* src, int stride, int NR, unsigned tag,
-                                                unsigned* flag) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+// Wave 0: poll the NR flag words of the group (one lane each, sc1 loads, s_sleep between
+// passes) until every member has published step `tag`.  false = spin timeout (flag raised).
+__device__ __forceinline__ bool poll_flags(unsigned* flags, int NR, unsigned tag, unsigned* ctl) {
   const int lane = threadIdx.x & 63;
+  gu32* f = (gu32*)flags;
   unsigned spins = 0;
   while (true) {
     bool ok = true;
-    if (lane < NR)
-      ok = (unsigned)(__hip_atomic_load(src + (long long)lane * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >>
-                      32) == tag;
+    if (lane < NR) ok = __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= tag;
     if (__all(ok)) return true;
     if (++spins > PSPIN) {
-      if (lane == 0) atomicOr(flag, 1u);
+      if (lane == 0) atomicOr(ctl, 1u);
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
   }
 }
 
-__device__ __forceinline__ unsigned long long granule(unsigned tag, float a, float b) {
-  bf16x2 h = {(bf16)a, (bf16)b};
-  return ((unsigned long long)tag << 32) | (unsigned long long)__builtin_bit_cast(unsigned, h);
+// Wave 0, after its write-through payload stores: drain them, then raise the member's flag.
+__device__ __forceinline__ void raise_flag(unsigned* flags, int r, unsigned tag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_store((gu32*)flags + r, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Gather the group's tagged granules of one step into LDS rows of `ap` bf16 pairs
-// (row = idx / PER, pair = idx % PER for idx = tid + 256 i).  Loads are issued CH at a time
-// unconditionally (all in flight together: a per-granule branch around each load made the
-// compiler wait for every load in turn), then matched against the tag; late granules are
-// re-read with the whole chunk.  Returns false after a spin timeout (flag raised).
-template <int NGR, int PER, int CH>
-__device__ __forceinline__ bool gather_granules(const unsigned long long* src, bf16* lds, int ap,
-                                                unsigned long long need, unsigned tag, unsigned* flag) {
+// Every thread: copy the group's `rows` payload rows of W bf16 (parity slot `slot`) into the
+// LDS tile (row stride ap), 16-B sc1 loads, NCH chunks per thread, all in flight together.
+template <int W, int NCH>
+__device__ __forceinline__ void load_group(__amdgpu_buffer_rsrc_t pay, int row0, int rows, bf16* lds, int ap) {
+  constexpr int CPR = W / 8;
   const int tid = threadIdx.x;
-  unsigned spins = 0;
+  u32x4_t v[NCH];
 #pragma unroll
-  for (int c0 = 0; c0 < NGR; c0 += CH) {
-    while (true) {
-      unsigned long long v[CH];
+  for (int i = 0; i < NCH; ++i) {
+    const int ch = tid + 256 * i, row = ch / CPR, col = ch - row * CPR;
+    v[i] = row < rows ? __builtin_amdgcn_raw_buffer_load_b128(pay, ((row0 + row) * W + col * 8) * 2, 0, AUX_SC1)
+                      : u32x4_t{0u, 0u, 0u, 0u};
+  }
 #pragma unroll
-      for (int i = 0; i < CH; ++i) {
-        const int idx = tid + 256 * (c0 + i), row = idx / PER, c2 = idx - row * PER;
-        // rows outside the batch are never needed: read row 0's slot instead (valid memory)
-        const int rr = ((need >> (c0 + i)) & 1ull) ? row : 0;
-        v[i] = __hip_atomic_load(src + (long long)rr * PER + c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+  for (int i = 0; i < NCH; ++i) {
+    const int ch = tid + 256 * i, row = ch / CPR, col = ch - row * CPR;
+    *reinterpret_cast<u32x4_t*>(lds + row * ap + col * 8) = v[i];
+  }
+}
+
+// acc_n += A . W_n over NK K-blocks of 32: A rows (16 per lane group) are read from LDS at
+// `a` + 32k, W fragments live in registers.  The A fragments are read eight K-blocks at a
+// time, all eight in flight before the group's first MFMA (one read per K-block left the
+// LDS latency on every link of the MFMA chain).
+template <int NK>
+__device__ __forceinline__ void mfma_rows(const bf16* a, const bf16x8 (&wf)[2][NK], f32x4& acc0, f32x4& acc1) {
+  constexpr int KG = NK < 8 ? NK : 8;
 #pragma unroll
-      for (int i = 0; i < CH; ++i) {
-        const int idx = tid + 256 * (c0 + i), row = idx / PER, c2 = idx - row * PER;
-        if (((need >> (c0 + i)) & 1ull) && (unsigned)(v[i] >> 32) == tag) {
-          reinterpret_cast<unsigned*>(lds + row * ap)[c2] = (unsigned)v[i];
-          need &= ~(1ull << (c0 + i));
-        }
-      }
-      const unsigned long long cm = (CH >= 64 ? ~0ull : ((1ull << CH) - 1ull)) << c0;
-      if (!(need & cm)) break;
-      if (++spins > PSPIN) {
-        atomicOr(flag, 1u);
-        return false;
-      }
-      __builtin_amdgcn_s_sleep(1);
+  for (int k0 = 0; k0 < NK; k0 += KG) {
+    bf16x8 af[KG];
+#pragma unroll
+    for (int i = 0; i < KG; ++i) af[i] = *reinterpret_cast<const bf16x8*>(a + 32 * (k0 + i));
+#pragma unroll
+    for (int i = 0; i < KG; ++i) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], wf[0][k0 + i], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], wf[1][k0 + i], acc1, 0, 0, 0);
     }
   }
-  return true;
 }
 
 template <int H>
 __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
-  constexpr int G = 4 * H, NK = H / 32, AP = H + 8, H2 = H / 2;
-  constexpr int NGR = PRG * H2 / 256;  // granules gathered per thread per step
+  constexpr int G = 4 * H, NK = H / 32, AP = H + 8;
+  constexpr int NCH = PRG * H / 8 / 256;  // 16-B payload chunks per thread per step
   __shared__ __attribute__((aligned(16))) bf16 As[16 * AP];
+  __shared__ __attribute__((aligned(16))) bf16 hs16[PRG * PJU];
   __shared__ float gs[PRG][4 * PJU + 1];
   __shared__ int quit;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
   const int j0 = r * PJU, b0 = g * PRG;
-  const int T = a.T, B = a.B;
+  const int T = a.T, B = a.B, rows = min(PRG, B - b0);
+  const __amdgpu_buffer_rsrc_t pay = rsrc_of(a.pay, (long long)2 * B * H * 2);
+  unsigned* flags = a.ctl + 4 + g * PFL;
 
   bf16x8 wf[2][NK];
 #pragma unroll
@@ -742,10 +801,6 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
   if (tid == 0) quit = 0;
   const int pr = tid >> 5, pu = tid & 31, pb = b0 + pr, pj = j0 + pu;
   const bool pv = pb < B;
-  unsigned need0 = 0;  // granules this thread gathers each step (rows inside the batch)
-#pragma unroll
-  for (int i = 0; i < NGR; ++i)
-    if (b0 + (tid + 256 * i) / H2 < B) need0 |= 1u << i;
   float c = 0.f;
   __syncthreads();
 
@@ -760,22 +815,14 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
     }
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     if (s > 0) {
-      // ---- gather the group's h_{t-1} (tag == s) into the LDS A tile: wave 0 first waits
-      // for every member's last granule (row 0, pair 15 of its 32 units), then all sweep
-      const unsigned long long* src = a.xbuf + (long long)((s - 1) & 1) * B * H2 + (long long)b0 * H2;
-      if (w == 0 && !probe_producers(src + PJU / 2 - 1, PJU / 2, H / PJU, (unsigned)s, a.flag)) quit = 1;
+      // ---- the group's h_{t-1} -> LDS A tile (rows past the batch stay zero)
+      if (w == 0 && !poll_flags(flags, H / PJU, (unsigned)s, a.ctl)) quit = 1;
       __syncthreads();
       if (quit) return;  // block-uniform exit after a spin timeout
-      if (!gather_granules<NGR, H2, 16>(src, As, AP, need0, (unsigned)s, a.flag)) quit = 1;
+      load_group<H, NCH>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
       __syncthreads();
-      if (quit) return;
       stamp(a.trace, T, s, 1);
-#pragma unroll
-      for (int k = 0; k < NK; ++k) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + (lane & 15) * AP + 32 * k + 8 * (lane >> 4));
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[0][k], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[1][k], acc1, 0, 0, 0);
-      }
+      mfma_rows<NK>(As + (lane & 15) * AP + 8 * (lane >> 4), wf, acc0, acc1);
     }
     if (lane < 32) {
 #pragma unroll
@@ -788,17 +835,26 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
     stamp(a.trace, T, s, 2);
     float h = 0.f, ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f;
     if (pv) {
-      ig = sigmoidf_(px[0] + gs[pr][pu]);
-      fg = sigmoidf_(px[1] + gs[pr][PJU + pu]);
-      gg = tanhf(px[2] + gs[pr][2 * PJU + pu]);
-      og = sigmoidf_(px[3] + gs[pr][3 * PJU + pu]);
+      ig = fsig(px[0] + gs[pr][pu]);
+      fg = fsig(px[1] + gs[pr][PJU + pu]);
+      gg = ftanh(px[2] + gs[pr][2 * PJU + pu]);
+      og = fsig(px[3] + gs[pr][3 * PJU + pu]);
       c = fg * c + ig * gg;
-      h = og * tanhf(c);
+      h = og * ftanh(c);
     }
-    const float hn = __shfl_down(h, 1, 64);
-    if (pv && !(pu & 1) && s + 1 < T)
-      __hip_atomic_store(a.xbuf + (long long)(s & 1) * B * H2 + (long long)pb * H2 + (pj >> 1),
-                         granule((unsigned)(s + 1), h, hn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // ---- publish h_t: 8 x 32 bf16 tile via LDS, wave 0 stores 4 chunks per row, flag
+    if (s + 1 < T) {
+      hs16[pr * PJU + pu] = (bf16)h;
+      __syncthreads();
+      if (w == 0) {
+        if (lane < 4 * rows) {
+          const int row = lane >> 2, c8 = lane & 3;
+          const u32x4_t v = *reinterpret_cast<const u32x4_t*>(hs16 + row * PJU + c8 * 8);
+          __builtin_amdgcn_raw_buffer_store_b128(v, pay, (((s & 1) * B + b0 + row) * H + j0 + c8 * 8) * 2, 0, AUX_SC1);
+        }
+        raise_flag(flags, r, (unsigned)(s + 1));
+      }
+    }
     stamp(a.trace, T, s, 3);
     if (pv) {
       const long long oh = ((long long)pb * T + t) * H + pj;
@@ -814,16 +870,13 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
   }
 }
 
-// =============================================================== large H: persistent backward
-// One launch for all T steps of dirs == 1 (the decoder LSTMs).  Same decomposition as the
-// forward: group g = utterances [8g, 8g+8), member r = hidden units [32r, 32r+32).  The
-// recurrent product dh_rec[b][j] = sum_q dG_{t+1}[b][q] W_hh[q][j] runs over all 4H gate
-// rows q, so each member keeps W_hh^T[j0..j0+32][0..4H) in VGPRs (wave w = the K-block of
-// gate w, 2 x H/32 bf16x8 fragments) and gathers the group's whole dG_{t+1} (8 x 4H bf16)
-// into LDS each step from tagged granules {tag = step + 1, two bf16}.  The four waves'
-// partial products are summed through LDS; the cell-gradient carry dc stays in a register
-// of the thread that owns (b, j) for the whole sequence.  Outputs: dG (fp32) and its bf16
-// twin for the input-gradient / weight-gradient GEMMs.  Bounded spins as in the forward.
+// Backward: same groups and members.  The recurrent product dh_rec[b][j] = sum_q
+// dG_{t+1}[b][q] W_hh[q][j] runs over all 4H gate rows q, so each member keeps
+// W_hh^T[j0..j0+32][0..4H) in VGPRs (wave w = the K-block of gate w, 2 x H/32 bf16x8
+// fragments) and loads the group's whole dG_{t+1} (8 x 4H bf16) into LDS each step.  The four
+// waves' partial products are summed through LDS; the cell-gradient carry dc stays in a
+// register of the thread that owns (b, j) for the whole sequence.  Outputs: dG (fp32) and its
+// bf16 twin for the input-gradient / weight-gradient GEMMs.
 struct PersistBwdArgs {
   const float* dhout;  // (B,T,H)
   const float* call;   // (B,T,H) cell states
@@ -831,25 +884,27 @@ struct PersistBwdArgs {
   const bf16* wt;      // W_hh^T [H][4H]
   float* dg;           // (B,T,4H)
   bf16* dg16;          // (B,T,4H) or null
-  unsigned long long* xbuf;  // [2][B][2H] granules, zeroed before launch
-  unsigned* flag;
+  unsigned* ctl;       // scratch: ctl[0] timeout flag, flags from word 4
+  bf16* pay;           // payload [2][B][4H]
   unsigned long long* trace;  // diagnostics (avc_lstm_trace), null in production
   int B, T, ng;
 };
 
 template <int H>
 __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
-  constexpr int G = 4 * H, NK = H / 32, AP = G + 8, G2 = G / 2;
-  constexpr int NGR = PRG * G2 / 256;  // granules gathered per thread per step
-  static_assert(NGR <= 64, "gather mask is 64 bits");
+  constexpr int G = 4 * H, NK = H / 32, AP = G + 8;
+  constexpr int NCH = PRG * G / 8 / 256;  // 16-B payload chunks per thread per step
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* As = reinterpret_cast<bf16*>(smem_raw);                          // [PRG + 1][AP], row PRG = zeros
   float* red = reinterpret_cast<float*>(smem_raw + (PRG + 1) * AP * 2);  // [4][PRG][PJU + 1]
-  int* quit = reinterpret_cast<int*>(red + 4 * PRG * (PJU + 1));
+  bf16* ds16 = reinterpret_cast<bf16*>(red + 4 * PRG * (PJU + 1));       // [PRG][4 * PJU] publish tile
+  int* quit = reinterpret_cast<int*>(ds16 + PRG * 4 * PJU);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
   const int j0 = r * PJU, b0 = g * PRG;
-  const int T = a.T, B = a.B;
+  const int T = a.T, B = a.B, rows = min(PRG, B - b0);
+  const __amdgpu_buffer_rsrc_t pay = rsrc_of(a.pay, (long long)2 * B * G * 2);
+  unsigned* flags = a.ctl + 4 + g * PFL;
 
   // W_hh^T fragments: B operand of the product, n = unit j0 + 16n + (lane&15), k = gate row
   bf16x8 wf[2][NK];
@@ -863,11 +918,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
   if (tid == 0) *quit = 0;
   const int pr = tid >> 5, pu = tid & 31, pb = b0 + pr, pj = j0 + pu;
   const bool pv = pb < B;
-  unsigned long long need0 = 0;
-#pragma unroll
-  for (int i = 0; i < NGR; ++i)
-    if (b0 + (tid + 256 * i) / G2 < B) need0 |= 1ull << i;
-  // MFMA A rows: 0..7 gathered utterances, 8..15 read the zero row
+  // MFMA A rows: 0..7 loaded utterances, 8..15 read the zero row
   const int arow = (lane & 15) < PRG ? (lane & 15) : PRG;
   float dc = 0.f;
   __syncthreads();
@@ -889,24 +940,14 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
       go = gp[3 * H];
     }
     if (s > 0) {
-      const unsigned long long* src = a.xbuf + (long long)((s - 1) & 1) * B * G2 + (long long)b0 * G2;
-      // wave 0 waits for every member's last granule (row 0, gate o, pair 15), then all sweep
-      if (w == 0 && !probe_producers(src + 3 * H / 2 + PJU / 2 - 1, PJU / 2, H / PJU, (unsigned)s, a.flag))
-        *quit = 1;
+      if (w == 0 && !poll_flags(flags, H / PJU, (unsigned)s, a.ctl)) *quit = 1;
       __syncthreads();
       if (*quit) return;  // block-uniform exit after a spin timeout
-      if (!gather_granules<NGR, G2, 16>(src, As, AP, need0, (unsigned)s, a.flag)) *quit = 1;
+      load_group<G, NCH>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
       __syncthreads();
-      if (*quit) return;
       stamp(a.trace, T, s, 1);
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      const bf16* ap = As + arow * AP + w * H + 8 * (lane >> 4);
-#pragma unroll
-      for (int k = 0; k < NK; ++k) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(ap + 32 * k);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[0][k], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[1][k], acc1, 0, 0, 0);
-      }
+      mfma_rows<NK>(As + arow * AP + w * H + 8 * (lane >> 4), wf, acc0, acc1);
       // rows 4*(lane>>4)+e < 8 only for lanes 0..31
       if (lane < 32) {
 #pragma unroll
@@ -922,7 +963,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
     }
     float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
     if (pv) {
-      const float tc = tanhf(ct);
+      const float tc = ftanh(ct);
       const float dcs = dc + dh * go * (1.f - tc * tc);
       v0 = dcs * gg * gi * (1.f - gi);        // d(pre i)
       v1 = dcs * cp * gf * (1.f - gf);        // d(pre f)
@@ -930,15 +971,27 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
       v3 = dh * tc * go * (1.f - go);         // d(pre o)
       dc = dcs * gf;
     }
-    const float n0 = __shfl_down(v0, 1, 64), n1 = __shfl_down(v1, 1, 64);
-    const float n2 = __shfl_down(v2, 1, 64), n3 = __shfl_down(v3, 1, 64);
-    if (pv && !(pu & 1) && s + 1 < T) {
-      unsigned long long* dst = a.xbuf + (long long)(s & 1) * B * G2 + (long long)pb * G2 + (pj >> 1);
-      const unsigned tag = (unsigned)(s + 1);
-      __hip_atomic_store(dst, granule(tag, v0, n0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(dst + H / 2, granule(tag, v1, n1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(dst + H, granule(tag, v2, n2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(dst + 3 * H / 2, granule(tag, v3, n3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // ---- publish dG_t: 8 x (4 gates x 32 units) bf16 tile via LDS, wave 0 stores 16 chunks
+    // per row (2 per lane), flag
+    if (s + 1 < T) {
+      bf16* dsr = ds16 + pr * (4 * PJU) + pu;
+      dsr[0] = (bf16)v0;
+      dsr[PJU] = (bf16)v1;
+      dsr[2 * PJU] = (bf16)v2;
+      dsr[3 * PJU] = (bf16)v3;
+      __syncthreads();
+      if (w == 0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int ch = lane + 64 * i, row = ch >> 4, q = (ch >> 2) & 3, c8 = ch & 3;
+          if (row < rows) {
+            const u32x4_t v = *reinterpret_cast<const u32x4_t*>(ds16 + row * (4 * PJU) + q * PJU + c8 * 8);
+            __builtin_amdgcn_raw_buffer_store_b128(v, pay, (((s & 1) * B + b0 + row) * G + q * H + j0 + c8 * 8) * 2,
+                                                   0, AUX_SC1);
+          }
+        }
+        raise_flag(flags, r, (unsigned)(s + 1));
+      }
     }
     stamp(a.trace, T, s, 3);
     if (pv) {
@@ -959,7 +1012,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
 
 template <int H>
 constexpr size_t persist_bwd_lds() {
-  return (size_t)(PRG + 1) * (4 * H + 8) * 2 + (size_t)4 * PRG * (PJU + 1) * 4 + 16;
+  return (size_t)(PRG + 1) * (4 * H + 8) * 2 + (size_t)4 * PRG * (PJU + 1) * 4 + (size_t)PRG * 4 * PJU * 2 + 16;
 }
 
 int g_num_cus = -1;
@@ -974,14 +1027,16 @@ int num_cus() {
 }
 
 template <int HM>
-void launch_small_fwd(dim3 g, hipStream_t s, const float* x, const float* w, int T, int H, int dirs, float* h, float* c,
-                      float* gt) {
-  lstm_small_fwd<HM><<<g, 256, 0, s>>>(x, w, T, H, dirs, h, c, gt);
+void launch_small_fwd(dim3 g, hipStream_t s, bool fast, const float* x, const float* w, int T, int H, int dirs,
+                      float* h, float* c, float* gt) {
+  if (fast) lstm_small_fwd<HM, true><<<g, 256, 0, s>>>(x, w, T, H, dirs, h, c, gt);
+  else lstm_small_fwd<HM, false><<<g, 256, 0, s>>>(x, w, T, H, dirs, h, c, gt);
 }
 template <int HM>
-void launch_small_bwd(dim3 g, hipStream_t s, const float* dh, const float* c, const float* gt, const float* w, int T,
-                      int H, int dirs, float* dg) {
-  lstm_small_bwd<HM><<<g, 256, 0, s>>>(dh, c, gt, w, T, H, dirs, dg);
+void launch_small_bwd(dim3 g, hipStream_t s, bool fast, const float* dh, const float* c, const float* gt,
+                      const float* w, int T, int H, int dirs, float* dg) {
+  if (fast) lstm_small_bwd<HM, true><<<g, 256, 0, s>>>(dh, c, gt, w, T, H, dirs, dg);
+  else lstm_small_bwd<HM, false><<<g, 256, 0, s>>>(dh, c, gt, w, T, H, dirs, dg);
 }
 
 }  // namespace
@@ -998,11 +1053,12 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
   hipStream_t s = as_stream(stream);
   if (H <= 64) {
     AVC_CHECK_ARG(wdtype == AVC_F32, "avc_lstm_fwd: small-H path takes fp32 W_hh");
+    const bool fast = compute == AVC_BF16;  // fp32 weights and state either way; fast activations in bf16 mode
     dim3 g(B, dirs);
-    if (H <= 16) launch_small_fwd<16>(g, s, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
-    else if (H <= 32) launch_small_fwd<32>(g, s, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
-    else if (H <= 48) launch_small_fwd<48>(g, s, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
-    else launch_small_fwd<64>(g, s, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
+    if (H <= 16) launch_small_fwd<16>(g, s, fast, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
+    else if (H <= 32) launch_small_fwd<32>(g, s, fast, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
+    else if (H <= 48) launch_small_fwd<48>(g, s, fast, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
+    else launch_small_fwd<64>(g, s, fast, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
     return avc_check_launch("avc_lstm_fwd(small)");
   }
   AVC_CHECK_ARG(H % 128 == 0, "avc_lstm_fwd: H must be <= 64 or a multiple of 128 (got %d)", H);
@@ -1025,7 +1081,7 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
   const int ng = (B + PRG - 1) / PRG;
   static const bool no_persist = getenv("AVC_LSTM_NO_PERSIST") != nullptr;
   if (bf && dirs == 1 && (H == 1024 || H == 512) && hbuf && !no_persist && ng * (H / PJU) <= num_cus()) {
-    // hbuf is the granule scratch (>= 2*B*H/2 u64 + a flag word) in this mode
+    // hbuf: control words + flags + the [2][B][H] bf16 payload in this mode (layout above)
     PersistArgs p;
     p.xproj = xproj;
     p.w = reinterpret_cast<const bf16*>(w_hh);
@@ -1033,13 +1089,13 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
     p.hout16 = reinterpret_cast<bf16*>(h_bf16);
     p.call = c;
     p.gall = gates;
-    p.xbuf = reinterpret_cast<unsigned long long*>(hbuf);
-    p.flag = reinterpret_cast<unsigned*>(p.xbuf + (size_t)2 * B * (H / 2));
+    p.ctl = reinterpret_cast<unsigned*>(hbuf);
+    p.pay = reinterpret_cast<bf16*>(reinterpret_cast<char*>(hbuf) + px_payload_off(ng));
     p.trace = g_trace;
     p.B = B;
     p.T = T;
     p.ng = ng;
-    (void)hipMemsetAsync(hbuf, 0, ((size_t)2 * B * (H / 2) + 2) * sizeof(unsigned long long), s);
+    (void)hipMemsetAsync(hbuf, 0, px_ctl_bytes(ng), s);
     if (H == 1024) lstm_persist_fwd<1024><<<ng * (H / PJU), 256, 0, s>>>(p);
     else lstm_persist_fwd<512><<<ng * (H / PJU), 256, 0, s>>>(p);
     return avc_check_launch("avc_lstm_fwd(persistent)");
@@ -1075,11 +1131,12 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
   hipStream_t s = as_stream(stream);
   if (H <= 64) {
     AVC_CHECK_ARG(w_hh && wdtype == AVC_F32, "avc_lstm_bwd: small-H path takes fp32 W_hh");
+    const bool fast = compute == AVC_BF16;
     dim3 g(B, dirs);
-    if (H <= 16) launch_small_bwd<16>(g, s, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
-    else if (H <= 32) launch_small_bwd<32>(g, s, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
-    else if (H <= 48) launch_small_bwd<48>(g, s, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
-    else launch_small_bwd<64>(g, s, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
+    if (H <= 16) launch_small_bwd<16>(g, s, fast, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
+    else if (H <= 32) launch_small_bwd<32>(g, s, fast, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
+    else if (H <= 48) launch_small_bwd<48>(g, s, fast, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
+    else launch_small_bwd<64>(g, s, fast, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
     return avc_check_launch("avc_lstm_bwd(small)");
   }
   AVC_CHECK_ARG(H % 128 == 0, "avc_lstm_bwd: H must be <= 64 or a multiple of 128 (got %d)", H);
@@ -1089,7 +1146,7 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
   const int ng = (B + PRG - 1) / PRG;
   static const bool no_persist = getenv("AVC_LSTM_NO_PERSIST") != nullptr;
   if (bf && dirs == 1 && (H == 1024 || H == 512) && !no_persist && ng * (H / PJU) <= num_cus()) {
-    // gbuf is the granule scratch (>= 2*B*2H u64 + a flag word) in this mode
+    // gbuf: control words + flags + the [2][B][4H] bf16 payload in this mode (layout above)
     PersistBwdArgs p;
     p.dhout = dh_out;
     p.call = c;
@@ -1097,13 +1154,13 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
     p.wt = reinterpret_cast<const bf16*>(w_hh_t);
     p.dg = dgates;
     p.dg16 = reinterpret_cast<bf16*>(dgates_bf16);
-    p.xbuf = reinterpret_cast<unsigned long long*>(gbuf);
-    p.flag = reinterpret_cast<unsigned*>(p.xbuf + (size_t)2 * B * (2 * H));
+    p.ctl = reinterpret_cast<unsigned*>(gbuf);
+    p.pay = reinterpret_cast<bf16*>(reinterpret_cast<char*>(gbuf) + px_payload_off(ng));
     p.trace = g_trace;
     p.B = B;
     p.T = T;
     p.ng = ng;
-    (void)hipMemsetAsync(gbuf, 0, ((size_t)2 * B * (2 * H) + 2) * sizeof(unsigned long long), s);
+    (void)hipMemsetAsync(gbuf, 0, px_ctl_bytes(ng), s);
     if (H == 1024) {
       static bool attr = false;
       if (!attr) {

@@ -195,12 +195,12 @@ def colsum(x, M, N, ld=None, out=None, accumulate=False):
 # ------------------------------------------------------------------------- LSTM
 def lstm_scratch(B, H, dirs, device):
     """bf16 scratch for the large-H recurrence: per-step ping-pong h (2*dirs*B*H bf16) or,
-    for the persistent kernel, 2*B*H/2 8-byte granules + a timeout flag word."""
+    for the persistent kernel, control words + per-member flags + a [2][B][H] bf16 payload."""
     return torch.zeros(max(2 * dirs * B * H, 4 * B * H + 32), device=device, dtype=torch.bfloat16)
 
 
 def lstm_timeout_flag(hbuf, B, H):
-    return int(hbuf.view(torch.int32)[2 * B * H].item())
+    return int(hbuf.view(torch.int32)[0].item())
 
 
 def lstm_persistent_fwd(B, H, dirs):
@@ -218,7 +218,7 @@ def lstm_fwd(xproj, w_hh, B, T, H, dirs, hbuf=None):
     if hbuf is not None and H > 64 and lstm_persistent_fwd(B, H, dirs):
         h16 = torch.empty(B * T, H, device=dev, dtype=torch.bfloat16)
     L.call("avc_lstm_fwd", xproj.data_ptr(), w_hh.data_ptr(), _dt(w_hh), B, T, H, dirs, h.data_ptr(), _ptr(h16),
-           c.data_ptr(), g.data_ptr(), _ptr(hbuf), _COMPUTE if H > 64 else F32, stream())
+           c.data_ptr(), g.data_ptr(), _ptr(hbuf), _COMPUTE, stream())
     return attach_twin(h, h16), c, g
 
 
@@ -243,7 +243,7 @@ def lstm_bwd_scratch(B, H, dirs, device):
 
 
 def lstm_bwd_timeout_flag(gbuf, B, H):
-    return int(gbuf.view(torch.int32)[8 * B * H].item())
+    return int(gbuf.view(torch.int32)[0].item())
 
 
 def lstm_bwd(dh, h, c, g, w_hh, w_hh_t, B, T, H, dirs, gbuf=None):
@@ -260,7 +260,7 @@ def lstm_bwd(dh, h, c, g, w_hh, w_hh_t, B, T, H, dirs, gbuf=None):
             if lstm_persistent_bwd(B, H, dirs):
                 dg16 = torch.empty(B * T, 4 * H, device=dev, dtype=torch.bfloat16)
     L.call("avc_lstm_bwd", dh.data_ptr(), h.data_ptr(), c.data_ptr(), g.data_ptr(), _ptr(w_hh), _ptr(w_hh_t), wdt, B,
-           T, H, dirs, dg.data_ptr(), _ptr(dg16), _ptr(dcbuf), _ptr(gbuf), _COMPUTE if H > 64 else F32, stream())
+           T, H, dirs, dg.data_ptr(), _ptr(dg16), _ptr(dcbuf), _ptr(gbuf), _COMPUTE, stream())
     return attach_twin(dg, dg16)
 
 

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 2
+#define AVC_ABI_VERSION 3
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -119,11 +119,13 @@ int avc_colsum(const float* x, long long ld, int M, int N, float* out, int accum
  * Replaces the time loop of nn.LSTM (AutoVC.py:43,55 encoder BiLSTM; :77,103 lstm1;
  * :96,110 lstm2).  xproj (B,T,dirs*4H) already holds x W_ih^T + b_ih + b_hh.
  * w_hh: dirs x [4H][H] in `wdtype`; outputs h (B,T,dirs*H) fp32, c (B,T,dirs*H),
- * gates (B,T,dirs*4H) activated.  hbuf (large H, bf16 compute): scratch of at least
+ * gates (B,T,dirs*4H) activated.  Small H (<= 64) keeps fp32 weights and state; `compute` ==
+ * AVC_BF16 selects its v_exp/v_rcp activation forms (IEEE library forms otherwise).  hbuf (large
+ * H, bf16 compute): scratch of at least
  * max(4*dirs*B*H, 8*B*H + 16) bytes.  For dirs == 1, H in {512, 1024} and enough CUs the
- * whole sequence runs as ONE persistent launch (W_hh slices register-resident, h_t
- * exchanged through tagged granules, bounded spins; timeout flag = u32 at byte 8*B*H of
- * hbuf); otherwise one fused kernel per time step.  The persistent launch can also write a
+ * whole sequence runs as ONE persistent launch (W_hh slices register-resident, h_t handed
+ * between workgroups as write-through payload + per-workgroup flags, bounded spins; timeout
+ * flag = u32 at byte 0 of hbuf); otherwise one fused kernel per time step.  The persistent launch can also write a
  * bf16 copy of h (h_bf16, the next GEMMs' operand; else null — other paths need null). */
 int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T, int H, int dirs,
                  float* h, void* h_bf16, float* c, float* gates, void* hbuf, int compute, void* stream);
@@ -133,8 +135,8 @@ int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T,
  * (small H, pass the same layout as avc_lstm_fwd). dcbuf: B*H*dirs fp32.  gbuf (large H,
  * bf16 compute): at least max(16*dirs*B*H, 32*B*H + 16) bytes.  For dirs == 1, H in
  * {512, 1024} and enough CUs the whole sequence is ONE persistent launch (W_hh^T slices
- * register-resident, dG_{t+1} exchanged through tagged granules, bounded spins; timeout
- * flag = u32 at byte 32*B*H of gbuf), which can also write a bf16 copy of dgates
+ * register-resident, dG_{t+1} handed over as write-through payload + flags, bounded spins;
+ * timeout flag = u32 at byte 0 of gbuf), which can also write a bf16 copy of dgates
  * (dgates_bf16, else null); otherwise one fused kernel per time step and dgates_bf16 must
  * be null. */
 int avc_lstm_bwd(const float* dh_out, const float* h, const float* c, const float* gates,
