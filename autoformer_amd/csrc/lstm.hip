@@ -737,28 +737,29 @@ __device__ __forceinline__ void raise_flag(unsigned* flags, int r, unsigned tag)
 
 // Every thread: copy the group's `rows` payload rows of W bf16 (parity slot `slot`) into the
 // LDS tile (row stride ap), 16-B sc1 loads, NCH chunks per thread, all in flight together.
-template <int W, int NCH>
+// Every thread of the NT-thread workgroup: copy the group's `rows` payload rows of W bf16
+// (parity slot row0) into the LDS tile (row stride ap), 16-B sc1 loads, NCH chunks per
+// thread, all in flight together.
+template <int W, int NCH, int NT>
 __device__ __forceinline__ void load_group(__amdgpu_buffer_rsrc_t pay, int row0, int rows, bf16* lds, int ap) {
   constexpr int CPR = W / 8;
   const int tid = threadIdx.x;
   u32x4_t v[NCH];
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
-    const int ch = tid + 256 * i, row = ch / CPR, col = ch - row * CPR;
+    const int ch = tid + NT * i, row = ch / CPR, col = ch - row * CPR;
     v[i] = row < rows ? __builtin_amdgcn_raw_buffer_load_b128(pay, ((row0 + row) * W + col * 8) * 2, 0, AUX_SC1)
                       : u32x4_t{0u, 0u, 0u, 0u};
   }
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
-    const int ch = tid + 256 * i, row = ch / CPR, col = ch - row * CPR;
+    const int ch = tid + NT * i, row = ch / CPR, col = ch - row * CPR;
     *reinterpret_cast<u32x4_t*>(lds + row * ap + col * 8) = v[i];
   }
 }
 
 // acc_n += A . W_n over NK K-blocks of 32: A rows (16 per lane group) are read from LDS at
-// `a` + 32k, W fragments live in registers.  The A fragments are read eight K-blocks at a
-// time, all eight in flight before the group's first MFMA (one read per K-block left the
-// LDS latency on every link of the MFMA chain).
+// `a` + 32k, W fragments live in registers; A fragments are read up to eight K-blocks ahead.
 template <int NK>
 __device__ __forceinline__ void mfma_rows(const bf16* a, const bf16x8 (&wf)[2][NK], f32x4& acc0, f32x4& acc1) {
   constexpr int KG = NK < 8 ? NK : 8;
@@ -775,32 +776,40 @@ __device__ __forceinline__ void mfma_rows(const bf16* a, const bf16x8 (&wf)[2][N
   }
 }
 
+// Workgroups of PNT = 512 threads: eight waves, two per SIMD.  Wave w takes gate (w & 3) and
+// half (w >> 2) of the K range, so it holds 128 registers of W fragments instead of 256 and
+// the SIMD's two waves hide each other's LDS fragment reads under MFMAs (with four waves of
+// 256 W registers the compiler had one A-fragment register left and waited on every read).
+// Threads 0..255 own the (utterance, unit) cells of the element-wise stages.
+constexpr int PNT = 512;
+
 template <int H>
-__global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
-  constexpr int G = 4 * H, NK = H / 32, AP = H + 8;
-  constexpr int NCH = PRG * H / 8 / 256;  // 16-B payload chunks per thread per step
+__global__ void __launch_bounds__(PNT, 1) lstm_persist_fwd(PersistArgs a) {
+  constexpr int G = 4 * H, NKH = H / 64, AP = H + 8, KH = H / 2;
+  constexpr int NCH = PRG * H / 8 / PNT;  // 16-B payload chunks per thread per step
   __shared__ __attribute__((aligned(16))) bf16 As[16 * AP];
   __shared__ __attribute__((aligned(16))) bf16 hs16[PRG * PJU];
-  __shared__ float gs[PRG][4 * PJU + 1];
+  __shared__ float gs[2][PRG][4 * PJU + 1];
   __shared__ int quit;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, gq = w & 3, kh = w >> 2;
   const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
   const int j0 = r * PJU, b0 = g * PRG;
   const int T = a.T, B = a.B, rows = min(PRG, B - b0);
   const __amdgpu_buffer_rsrc_t pay = rsrc_of(a.pay, (long long)2 * B * H * 2);
   unsigned* flags = a.ctl + 4 + g * PFL;
 
-  bf16x8 wf[2][NK];
+  // W_hh rows of gate gq for units j0 + 16n + (lane & 15), K half kh
+  bf16x8 wf[2][NKH];
 #pragma unroll
   for (int n = 0; n < 2; ++n) {
-    const bf16* row = a.w + (long long)(w * H + j0 + n * 16 + (lane & 15)) * H + 8 * (lane >> 4);
+    const bf16* row = a.w + (long long)(gq * H + j0 + n * 16 + (lane & 15)) * H + kh * KH + 8 * (lane >> 4);
 #pragma unroll
-    for (int k = 0; k < NK; ++k) wf[n][k] = *reinterpret_cast<const bf16x8*>(row + 32 * k);
+    for (int k = 0; k < NKH; ++k) wf[n][k] = *reinterpret_cast<const bf16x8*>(row + 32 * k);
   }
-  for (int i = tid; i < 16 * AP / 2; i += 256) reinterpret_cast<unsigned*>(As)[i] = 0u;
+  for (int i = tid; i < 16 * AP / 2; i += PNT) reinterpret_cast<unsigned*>(As)[i] = 0u;
   if (tid == 0) quit = 0;
-  const int pr = tid >> 5, pu = tid & 31, pb = b0 + pr, pj = j0 + pu;
-  const bool pv = pb < B;
+  const int pr = (tid >> 5) & (PRG - 1), pu = tid & 31, pb = b0 + pr, pj = j0 + pu;
+  const bool pv = tid < PRG * PJU && pb < B;
   float c = 0.f;
   __syncthreads();
 
@@ -819,32 +828,32 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
       if (w == 0 && !poll_flags(flags, H / PJU, (unsigned)s, a.ctl)) quit = 1;
       __syncthreads();
       if (quit) return;  // block-uniform exit after a spin timeout
-      load_group<H, NCH>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
+      load_group<H, NCH, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
       __syncthreads();
       stamp(a.trace, T, s, 1);
-      mfma_rows<NK>(As + (lane & 15) * AP + 8 * (lane >> 4), wf, acc0, acc1);
+      mfma_rows<NKH>(As + (lane & 15) * AP + kh * KH + 8 * (lane >> 4), wf, acc0, acc1);
     }
     if (lane < 32) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        gs[4 * (lane >> 4) + e][w * PJU + (lane & 15)] = acc0[e];
-        gs[4 * (lane >> 4) + e][w * PJU + 16 + (lane & 15)] = acc1[e];
+        gs[kh][4 * (lane >> 4) + e][gq * PJU + (lane & 15)] = acc0[e];
+        gs[kh][4 * (lane >> 4) + e][gq * PJU + 16 + (lane & 15)] = acc1[e];
       }
     }
     __syncthreads();
     stamp(a.trace, T, s, 2);
     float h = 0.f, ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f;
     if (pv) {
-      ig = fsig(px[0] + gs[pr][pu]);
-      fg = fsig(px[1] + gs[pr][PJU + pu]);
-      gg = ftanh(px[2] + gs[pr][2 * PJU + pu]);
-      og = fsig(px[3] + gs[pr][3 * PJU + pu]);
+      ig = fsig(px[0] + gs[0][pr][pu] + gs[1][pr][pu]);
+      fg = fsig(px[1] + gs[0][pr][PJU + pu] + gs[1][pr][PJU + pu]);
+      gg = ftanh(px[2] + gs[0][pr][2 * PJU + pu] + gs[1][pr][2 * PJU + pu]);
+      og = fsig(px[3] + gs[0][pr][3 * PJU + pu] + gs[1][pr][3 * PJU + pu]);
       c = fg * c + ig * gg;
       h = og * ftanh(c);
     }
     // ---- publish h_t: 8 x 32 bf16 tile via LDS, wave 0 stores 4 chunks per row, flag
     if (s + 1 < T) {
-      hs16[pr * PJU + pu] = (bf16)h;
+      if (tid < PRG * PJU) hs16[pr * PJU + pu] = (bf16)h;
       __syncthreads();
       if (w == 0) {
         if (lane < 4 * rows) {
@@ -872,11 +881,11 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_fwd(PersistArgs a) {
 
 // Backward: same groups and members.  The recurrent product dh_rec[b][j] = sum_q
 // dG_{t+1}[b][q] W_hh[q][j] runs over all 4H gate rows q, so each member keeps
-// W_hh^T[j0..j0+32][0..4H) in VGPRs (wave w = the K-block of gate w, 2 x H/32 bf16x8
-// fragments) and loads the group's whole dG_{t+1} (8 x 4H bf16) into LDS each step.  The four
-// waves' partial products are summed through LDS; the cell-gradient carry dc stays in a
-// register of the thread that owns (b, j) for the whole sequence.  Outputs: dG (fp32) and its
-// bf16 twin for the input-gradient / weight-gradient GEMMs.
+// W_hh^T[j0..j0+32][0..4H) in registers (wave w = half (w >> 2) of the K-block of gate
+// (w & 3), 2 x H/64 bf16x8 fragments) and loads the group's whole dG_{t+1} (8 x 4H bf16) into
+// LDS each step.  The eight waves' partial products are summed through LDS; the cell-gradient
+// carry dc stays in a register of the thread that owns (b, j) for the whole sequence.
+// Outputs: dG (fp32) and its bf16 twin for the input-gradient / weight-gradient GEMMs.
 struct PersistBwdArgs {
   const float* dhout;  // (B,T,H)
   const float* call;   // (B,T,H) cell states
@@ -891,15 +900,15 @@ struct PersistBwdArgs {
 };
 
 template <int H>
-__global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
-  constexpr int G = 4 * H, NK = H / 32, AP = G + 8;
-  constexpr int NCH = PRG * G / 8 / 256;  // 16-B payload chunks per thread per step
+__global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
+  constexpr int G = 4 * H, NKH = H / 64, AP = G + 8, KH = H / 2, NW = PNT / 64;
+  constexpr int NCH = PRG * G / 8 / PNT;  // 16-B payload chunks per thread per step
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* As = reinterpret_cast<bf16*>(smem_raw);                          // [PRG + 1][AP], row PRG = zeros
-  float* red = reinterpret_cast<float*>(smem_raw + (PRG + 1) * AP * 2);  // [4][PRG][PJU + 1]
-  bf16* ds16 = reinterpret_cast<bf16*>(red + 4 * PRG * (PJU + 1));       // [PRG][4 * PJU] publish tile
+  float* red = reinterpret_cast<float*>(smem_raw + (PRG + 1) * AP * 2);  // [NW][PRG][PJU + 1]
+  bf16* ds16 = reinterpret_cast<bf16*>(red + NW * PRG * (PJU + 1));      // [PRG][4 * PJU] publish tile
   int* quit = reinterpret_cast<int*>(ds16 + PRG * 4 * PJU);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, gq = w & 3, kh = w >> 2;
   const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
   const int j0 = r * PJU, b0 = g * PRG;
   const int T = a.T, B = a.B, rows = min(PRG, B - b0);
@@ -907,17 +916,17 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
   unsigned* flags = a.ctl + 4 + g * PFL;
 
   // W_hh^T fragments: B operand of the product, n = unit j0 + 16n + (lane&15), k = gate row
-  bf16x8 wf[2][NK];
+  bf16x8 wf[2][NKH];
 #pragma unroll
   for (int n = 0; n < 2; ++n) {
-    const bf16* row = a.wt + (long long)(j0 + n * 16 + (lane & 15)) * G + w * H + 8 * (lane >> 4);
+    const bf16* row = a.wt + (long long)(j0 + n * 16 + (lane & 15)) * G + gq * H + kh * KH + 8 * (lane >> 4);
 #pragma unroll
-    for (int k = 0; k < NK; ++k) wf[n][k] = *reinterpret_cast<const bf16x8*>(row + 32 * k);
+    for (int k = 0; k < NKH; ++k) wf[n][k] = *reinterpret_cast<const bf16x8*>(row + 32 * k);
   }
-  for (int i = tid; i < (PRG + 1) * AP / 2; i += 256) reinterpret_cast<unsigned*>(As)[i] = 0u;
+  for (int i = tid; i < (PRG + 1) * AP / 2; i += PNT) reinterpret_cast<unsigned*>(As)[i] = 0u;
   if (tid == 0) *quit = 0;
-  const int pr = tid >> 5, pu = tid & 31, pb = b0 + pr, pj = j0 + pu;
-  const bool pv = pb < B;
+  const int pr = (tid >> 5) & (PRG - 1), pu = tid & 31, pb = b0 + pr, pj = j0 + pu;
+  const bool pv = tid < PRG * PJU && pb < B;
   // MFMA A rows: 0..7 loaded utterances, 8..15 read the zero row
   const int arow = (lane & 15) < PRG ? (lane & 15) : PRG;
   float dc = 0.f;
@@ -943,11 +952,11 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
       if (w == 0 && !poll_flags(flags, H / PJU, (unsigned)s, a.ctl)) *quit = 1;
       __syncthreads();
       if (*quit) return;  // block-uniform exit after a spin timeout
-      load_group<G, NCH>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
+      load_group<G, NCH, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
       __syncthreads();
       stamp(a.trace, T, s, 1);
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      mfma_rows<NK>(As + arow * AP + w * H + 8 * (lane >> 4), wf, acc0, acc1);
+      mfma_rows<NKH>(As + arow * AP + gq * H + kh * KH + 8 * (lane >> 4), wf, acc0, acc1);
       // rows 4*(lane>>4)+e < 8 only for lanes 0..31
       if (lane < 32) {
 #pragma unroll
@@ -959,7 +968,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
       __syncthreads();
       stamp(a.trace, T, s, 2);
 #pragma unroll
-      for (int ww = 0; ww < 4; ++ww) dh += red[(ww * PRG + pr) * (PJU + 1) + pu];
+      for (int ww = 0; ww < NW; ++ww) dh += red[(ww * PRG + pr) * (PJU + 1) + pu];
     }
     float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
     if (pv) {
@@ -974,11 +983,13 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
     // ---- publish dG_t: 8 x (4 gates x 32 units) bf16 tile via LDS, wave 0 stores 16 chunks
     // per row (2 per lane), flag
     if (s + 1 < T) {
-      bf16* dsr = ds16 + pr * (4 * PJU) + pu;
-      dsr[0] = (bf16)v0;
-      dsr[PJU] = (bf16)v1;
-      dsr[2 * PJU] = (bf16)v2;
-      dsr[3 * PJU] = (bf16)v3;
+      if (tid < PRG * PJU) {
+        bf16* dsr = ds16 + pr * (4 * PJU) + pu;
+        dsr[0] = (bf16)v0;
+        dsr[PJU] = (bf16)v1;
+        dsr[2 * PJU] = (bf16)v2;
+        dsr[3 * PJU] = (bf16)v3;
+      }
       __syncthreads();
       if (w == 0) {
 #pragma unroll
@@ -1012,7 +1023,8 @@ __global__ void __launch_bounds__(256, 1) lstm_persist_bwd(PersistBwdArgs a) {
 
 template <int H>
 constexpr size_t persist_bwd_lds() {
-  return (size_t)(PRG + 1) * (4 * H + 8) * 2 + (size_t)4 * PRG * (PJU + 1) * 4 + (size_t)PRG * 4 * PJU * 2 + 16;
+  return (size_t)(PRG + 1) * (4 * H + 8) * 2 + (size_t)(PNT / 64) * PRG * (PJU + 1) * 4 + (size_t)PRG * 4 * PJU * 2 +
+         16;
 }
 
 int g_num_cus = -1;
@@ -1096,8 +1108,8 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
     p.T = T;
     p.ng = ng;
     (void)hipMemsetAsync(hbuf, 0, px_ctl_bytes(ng), s);
-    if (H == 1024) lstm_persist_fwd<1024><<<ng * (H / PJU), 256, 0, s>>>(p);
-    else lstm_persist_fwd<512><<<ng * (H / PJU), 256, 0, s>>>(p);
+    if (H == 1024) lstm_persist_fwd<1024><<<ng * (H / PJU), PNT, 0, s>>>(p);
+    else lstm_persist_fwd<512><<<ng * (H / PJU), PNT, 0, s>>>(p);
     return avc_check_launch("avc_lstm_fwd(persistent)");
   }
   AVC_CHECK_ARG(h_bf16 == nullptr, "avc_lstm_fwd: the bf16 h copy is produced by the persistent path only");
@@ -1168,9 +1180,9 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_bwd_lds<1024>());
         attr = true;
       }
-      lstm_persist_bwd<1024><<<ng * (H / PJU), 256, persist_bwd_lds<1024>(), s>>>(p);
+      lstm_persist_bwd<1024><<<ng * (H / PJU), PNT, persist_bwd_lds<1024>(), s>>>(p);
     } else {
-      lstm_persist_bwd<512><<<ng * (H / PJU), 256, persist_bwd_lds<512>(), s>>>(p);
+      lstm_persist_bwd<512><<<ng * (H / PJU), PNT, persist_bwd_lds<512>(), s>>>(p);
     }
     return avc_check_launch("avc_lstm_bwd(persistent)");
   }
