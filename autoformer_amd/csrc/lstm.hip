@@ -790,6 +790,7 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_fwd(PersistArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 As[16 * AP];
   __shared__ __attribute__((aligned(16))) bf16 hs16[PRG * PJU];
   __shared__ float gs[2][PRG][4 * PJU + 1];
+  __shared__ float outs[6 * PRG * PJU];  // the step's h, c, i, f, g, o per (utterance, unit) cell
   __shared__ int quit;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, gq = w & 3, kh = w >> 2;
   const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
@@ -851,11 +852,22 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_fwd(PersistArgs a) {
       c = fg * c + ig * gg;
       h = og * ftanh(c);
     }
-    // ---- publish h_t: 8 x 32 bf16 tile via LDS, wave 0 stores 4 chunks per row, flag
-    if (s + 1 < T) {
-      if (tid < PRG * PJU) hs16[pr * PJU + pu] = (bf16)h;
-      __syncthreads();
-      if (w == 0) {
+    // ---- publish h_t (8 x 32 bf16 tile via LDS; wave 0 stores 4 chunks per row, then the
+    // flag) while waves 4..7 write the step's outputs, staged in LDS, to HBM: the publishing
+    // wave issues nothing but the hand-off, so its drain waits for the payload alone
+    if (tid < PRG * PJU) {
+      hs16[pr * PJU + pu] = (bf16)h;
+      float* o = outs + tid;
+      o[0] = h;
+      o[PRG * PJU] = c;
+      o[2 * PRG * PJU] = ig;
+      o[3 * PRG * PJU] = fg;
+      o[4 * PRG * PJU] = gg;
+      o[5 * PRG * PJU] = og;
+    }
+    __syncthreads();
+    if (w == 0) {
+      if (s + 1 < T) {
         if (lane < 4 * rows) {
           const int row = lane >> 2, c8 = lane & 3;
           const u32x4_t v = *reinterpret_cast<const u32x4_t*>(hs16 + row * PJU + c8 * 8);
@@ -863,19 +875,22 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_fwd(PersistArgs a) {
         }
         raise_flag(flags, r, (unsigned)(s + 1));
       }
+    } else if (w >= 4) {
+      const int cell = tid - PRG * PJU, ob = b0 + (cell >> 5), oj = j0 + (cell & 31);
+      if (ob < B) {
+        const float* o = outs + cell;
+        const long long oh = ((long long)ob * T + t) * H + oj;
+        a.hout[oh] = o[0];
+        if (a.hout16) a.hout16[oh] = (bf16)o[0];
+        a.call[oh] = o[PRG * PJU];
+        float* gp = a.gall + ((long long)ob * T + t) * G + oj;
+        gp[0] = o[2 * PRG * PJU];
+        gp[H] = o[3 * PRG * PJU];
+        gp[2 * H] = o[4 * PRG * PJU];
+        gp[3 * H] = o[5 * PRG * PJU];
+      }
     }
     stamp(a.trace, T, s, 3);
-    if (pv) {
-      const long long oh = ((long long)pb * T + t) * H + pj;
-      a.hout[oh] = h;
-      if (a.hout16) a.hout16[oh] = (bf16)h;
-      a.call[oh] = c;
-      float* gp = a.gall + ((long long)pb * T + t) * G + pj;
-      gp[0] = ig;
-      gp[H] = fg;
-      gp[2 * H] = gg;
-      gp[3 * H] = og;
-    }
   }
 }
 
@@ -907,7 +922,8 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
   bf16* As = reinterpret_cast<bf16*>(smem_raw);                          // [PRG + 1][AP], row PRG = zeros
   float* red = reinterpret_cast<float*>(smem_raw + (PRG + 1) * AP * 2);  // [NW][PRG][PJU + 1]
   bf16* ds16 = reinterpret_cast<bf16*>(red + NW * PRG * (PJU + 1));      // [PRG][4 * PJU] publish tile
-  int* quit = reinterpret_cast<int*>(ds16 + PRG * 4 * PJU);
+  float* outs = reinterpret_cast<float*>(ds16 + PRG * 4 * PJU);         // [4][PRG * PJU] dG of the step
+  int* quit = reinterpret_cast<int*>(outs + 4 * PRG * PJU);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, gq = w & 3, kh = w >> 2;
   const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
   const int j0 = r * PJU, b0 = g * PRG;
@@ -980,18 +996,23 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
       v3 = dh * tc * go * (1.f - go);         // d(pre o)
       dc = dcs * gf;
     }
-    // ---- publish dG_t: 8 x (4 gates x 32 units) bf16 tile via LDS, wave 0 stores 16 chunks
-    // per row (2 per lane), flag
-    if (s + 1 < T) {
-      if (tid < PRG * PJU) {
-        bf16* dsr = ds16 + pr * (4 * PJU) + pu;
-        dsr[0] = (bf16)v0;
-        dsr[PJU] = (bf16)v1;
-        dsr[2 * PJU] = (bf16)v2;
-        dsr[3 * PJU] = (bf16)v3;
-      }
-      __syncthreads();
-      if (w == 0) {
+    // ---- publish dG_t (8 x (4 gates x 32 units) bf16 tile via LDS; wave 0 stores 16 chunks
+    // per row, 2 per lane, then the flag) while waves 4..7 write dG to HBM from LDS
+    if (tid < PRG * PJU) {
+      bf16* dsr = ds16 + pr * (4 * PJU) + pu;
+      dsr[0] = (bf16)v0;
+      dsr[PJU] = (bf16)v1;
+      dsr[2 * PJU] = (bf16)v2;
+      dsr[3 * PJU] = (bf16)v3;
+      float* o = outs + tid;
+      o[0] = v0;
+      o[PRG * PJU] = v1;
+      o[2 * PRG * PJU] = v2;
+      o[3 * PRG * PJU] = v3;
+    }
+    __syncthreads();
+    if (w == 0) {
+      if (s + 1 < T) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int ch = lane + 64 * i, row = ch >> 4, q = (ch >> 2) & 3, c8 = ch & 3;
@@ -1003,28 +1024,27 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
         }
         raise_flag(flags, r, (unsigned)(s + 1));
       }
-    }
-    stamp(a.trace, T, s, 3);
-    if (pv) {
-      const long long og = ((long long)pb * T + t) * G + pj;
-      a.dg[og] = v0;
-      a.dg[og + H] = v1;
-      a.dg[og + 2 * H] = v2;
-      a.dg[og + 3 * H] = v3;
-      if (a.dg16) {
-        a.dg16[og] = (bf16)v0;
-        a.dg16[og + H] = (bf16)v1;
-        a.dg16[og + 2 * H] = (bf16)v2;
-        a.dg16[og + 3 * H] = (bf16)v3;
+    } else if (w >= 4) {
+      const int cell = tid - PRG * PJU, ob = b0 + (cell >> 5), oj = j0 + (cell & 31);
+      if (ob < B) {
+        const float* o = outs + cell;
+        const long long og = ((long long)ob * T + t) * G + oj;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a.dg[og + q * H] = o[q * PRG * PJU];
+        if (a.dg16) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) a.dg16[og + q * H] = (bf16)o[q * PRG * PJU];
+        }
       }
     }
+    stamp(a.trace, T, s, 3);
   }
 }
 
 template <int H>
 constexpr size_t persist_bwd_lds() {
   return (size_t)(PRG + 1) * (4 * H + 8) * 2 + (size_t)(PNT / 64) * PRG * (PJU + 1) * 4 + (size_t)PRG * 4 * PJU * 2 +
-         16;
+         (size_t)4 * PRG * PJU * 4 + 16;
 }
 
 int g_num_cus = -1;
