@@ -24,8 +24,9 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "mel-frames/sec fwd+bwd, AutoVC 80×128 mel, batch=64, at 1/2/4/8 GPUs"
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3     # f32 MFMA
-# algorithmic work of one train.py step per mel frame (torch flop counter on the reference)
-FLOP_PER_FRAME = {(128, 16): 191.55e6, (176, 22): 191.59e6}
+# algorithmic work of one train step per mel frame (torch flop counter on the reference)
+FLOP_PER_FRAME = {("AutoVC", 128, 16): 191.55e6, ("AutoVC", 176, 22): 191.59e6, ("AutoVC+D", 176, 22): 191.87e6,
+                  ("MetaConv", 176, 22): 1044.41e6, ("MetaPool", 176, 22): 981.86e6}
 
 
 def synthetic_batch(B, T, rank, device):
@@ -119,8 +120,12 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64)
-    ap.add_argument("--len-crop", type=int, default=128)
-    ap.add_argument("--freq", type=int, default=16)
+    ap.add_argument("--len-crop", type=int, default=None, help="default 128 (AutoVC), 176 (MetaConv/MetaPool/--disc)")
+    ap.add_argument("--freq", type=int, default=None, help="default 16 at T=128, 22 at T=176")
+    ap.add_argument("--model", default="AutoVC", choices=["AutoVC", "MetaConv", "MetaPool"],
+                    help="factory plugin (train.py --model_name); MetaConv/MetaPool hard-wire T=176")
+    ap.add_argument("--disc", action="store_true",
+                    help="AutoVC + Discriminator two-model step (train_with_discriminator.py), T=176")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--graph", action="store_true",
                     help="replay the fwd+bwd as one hipGraph (serialises the side-stream wgrad branch on ROCm 7)")
@@ -128,23 +133,40 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
 
+    import importlib
+
     from autoformer_amd import dist as D
     from autoformer_amd import set_compute
     from autoformer_amd.detinit import det_init_
-    from autoformer_amd.factory.AutoVC import AutoVC
-    from autoformer_amd.train import TrainStep
+    from autoformer_amd.train import TrainStep, gan_extra
 
     rank, world, local = D.init_from_env("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     set_compute(args.dtype)
-    B, T, freq = args.batch, args.len_crop, args.freq
+    if args.disc and args.model != "AutoVC":
+        raise SystemExit("--disc pairs the Discriminator with AutoVC (train_with_discriminator.py)")
+    wide = args.model != "AutoVC" or args.disc
+    B = args.batch
+    T = args.len_crop if args.len_crop is not None else (176 if wide else 128)
+    freq = args.freq if args.freq is not None else (22 if T == 176 else 16)
+    name = "AutoVC+D" if args.disc else args.model
 
-    model = AutoVC(44, 256, 512, freq)
+    # the reference's plugin lookup (train.py:45-47)
+    cls = getattr(importlib.import_module(f"autoformer_amd.factory.{args.model}"), args.model)
+    model = cls(44, 256, 512, freq)
     det_init_(model)
     model = model.to(dev).train()
     x, e = synthetic_batch(B, T, rank, dev)
-    trainer = TrainStep(model, lr=1e-4)
+    if args.disc:
+        from autoformer_amd.factory.Discriminator import Discriminator
+
+        disc = Discriminator(crop_len=T)
+        det_init_(disc)
+        disc = disc.to(dev).train()
+        trainer = TrainStep(model, lr=1e-4, extra=gan_extra(disc), extra_modules=[disc])
+    else:
+        trainer = TrainStep(model, lr=1e-4)
 
     for _ in range(args.warmup):
         trainer.step(x, e)
@@ -176,18 +198,23 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
-    fpf = FLOP_PER_FRAME.get((T, freq), 191.55e6)
+    fpf = FLOP_PER_FRAME.get((name, T, freq))
     peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
-    out = {"metric": METRIC, "value": round(value, 1), "unit": "mel-frames/s", "n_gpus": world,
+    step = ("train_with_discriminator.py step (G fwd + encoder re-pass + D on real/fake + 2xMSE + L1 + 2xBCE + "
+            "one bwd + both Adams)" if args.disc else
+            "train.py step (fwd + encoder re-pass + 2xMSE + L1 + bwd + Adam)")
+    default = name == "AutoVC" and (T, freq) == (128, 16)
+    metric = METRIC if default else f"mel-frames/sec fwd+bwd, {name} 80\u00d7{T} mel, batch={B}"
+    out = {"metric": metric, "value": round(value, 1), "unit": "mel-frames/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
-           "config": {"workload": f"AutoVC train.py step (fwd + encoder re-pass + 2xMSE + L1 + bwd + Adam), "
-                                  f"B={B}/GPU, T={T}, freq={freq}, dim_neck=44, dim_emb=256, dim_pre=512",
+           "config": {"workload": f"{name} {step}, B={B}/GPU, T={T}, freq={freq}, dim_neck=44, dim_emb=256, "
+                                  f"dim_pre=512",
                       "global_batch": B * world, "seq_len": T, "freq": freq, "parallelism": f"dp{world}",
                       "graph": bool(args.graph)},
-           "step_mfma_frac": round(value * fpf / (world * peak * 1e12), 5),
+           "step_mfma_frac": round(value * fpf / (world * peak * 1e12), 5) if fpf else None,
            "final_loss": loss_v}
-    if not args.no_kernel_timing:
+    if not args.no_kernel_timing and args.model == "AutoVC":
         kt = kernel_timing(model, B, T)
         ach = kt["bytes"] / (kt["avg_us"] * 1e-6) / 1e9
         traffic, src = pmc_traffic(DOMINANT)
@@ -195,7 +222,7 @@ def main():
                            "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": traffic, "kernel": kt["kernel"],
                            "avg_us": round(kt["avg_us"], 3), "alg_bytes_per_launch": kt["bytes"],
                            "flop_per_launch": kt["flops"], "traffic_source": src}
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and default:
         out["cpu_baseline"] = cpu_baseline(B, T, freq)
     print(json.dumps(out), flush=True)
     if world > 1:
