@@ -10,6 +10,9 @@
 // 16x16 tiles.  Operands are staged global -> registers -> LDS (register staging lets
 // the loader apply the conv window / zero padding and the fp32->bf16 conversion), LDS is
 // double-buffered with one barrier per K-tile.
+#include <cstdio>
+#include <cstdlib>
+
 #include "gemm_internal.h"
 
 namespace {
@@ -740,6 +743,11 @@ extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
     return avc_check_launch("avc_gemm(fast)");
   }
   AVC_CHECK_ARG(!g.c16, "avc_gemm: c_bf16 output needs the fast path (bf16 compute, vectorisable operands)");
+  static const bool trace_generic = getenv("AVC_GEMM_TRACE") != nullptr;
+  if (trace_generic && bf)
+    fprintf(stderr, "avc_gemm generic: M=%d N=%d K=%d batch=%d split=%d aks=%d bks=%d avec=%d bvec=%d awin=%d chans=%d\n",
+            g.M, g.N, g.K, g.batch, g.split_k, (int)aks, (int)bks, (int)g.a.vec, (int)g.b.vec, (int)g.a.win,
+            g.a.chans);
   dim3 grid(cdiv(g.N, BN), cdiv(g.M, BM), g.batch * g.split_k);
   size_t lds = bf ? 2 * (BM + BN) * Traits<true>::LDK * sizeof(bf16) : 2 * (BM + BN) * Traits<false>::LDK * sizeof(float);
 #define AVC_GEMM_LAUNCH(BFV, A, B) gemm_generic_kernel<BFV, A, B><<<grid, NT, lds, s>>>(g)

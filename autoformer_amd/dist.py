@@ -28,23 +28,35 @@ def init_from_env(backend: str = "nccl"):
     return dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", "0"))
 
 
+PARAM_ALIGN = 64  # elements (256 B): every parameter view starts on a 16-B multiple, so the
+                  # GEMMs' vectorised (buffer-load / LDS-DMA) operand paths accept it in place
+
+
+def param_offsets(params):
+    """Start offset of each parameter in the flat buffer and the buffer length."""
+    offs, off = [], 0
+    for p in params:
+        offs.append(off)
+        off += -(-p.numel() // PARAM_ALIGN) * PARAM_ALIGN
+    return offs, off
+
+
 def flatten_params_(module, device=None):
     """Move every parameter into one contiguous fp32 buffer (and its .grad into another)
-    so the optimizer and the all-reduce are single kernels over 28.5M values.  Returns
-    (params, flat, gflat)."""
+    so the optimizer and the all-reduce are single kernels over 28.5M values.  Each view
+    starts PARAM_ALIGN-aligned; the few padding elements stay zero (zero gradient, so Adam
+    leaves them at zero).  Returns (params, flat, gflat)."""
     params = [p for p in module.parameters() if p.requires_grad]
     device = device or params[0].device
-    n = sum(p.numel() for p in params)
-    flat = torch.empty(n, device=device, dtype=torch.float32)
+    offs, n = param_offsets(params)
+    flat = torch.zeros(n, device=device, dtype=torch.float32)
     gflat = torch.zeros(n, device=device, dtype=torch.float32)
-    off = 0
     with torch.no_grad():
-        for p in params:
+        for p, off in zip(params, offs):
             k = p.numel()
             flat[off:off + k].copy_(p.detach().reshape(-1))
             p.data = flat[off:off + k].view_as(p)
             p.grad = gflat[off:off + k].view_as(p)
-            off += k
     return params, flat, gflat
 
 

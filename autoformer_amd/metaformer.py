@@ -160,6 +160,14 @@ def enc_embed(mel2d, emb, proj, cache, B, T):
 
 
 # ------------------------------------------------------------------------------ MLP-Mixer
+def _token_mix_weights(mix, w1, w2, NP):
+    """(W1^T (NP x 4NP), W2 (NP x 4NP)) in the compute dtype, rebuilt when w1 / w2 change."""
+    def build():
+        dt = K.compute()
+        return K.transpose(w1.view(4 * NP, NP), dt), K.convert(w2.view(NP, 4 * NP), dt)
+    return mix.tm_cache.get([w1, w2], build)
+
+
 def _lin(x, M, N, Kd, w, b=None, residual=None, out=None):
     """y = x (M x Kd, row-major) . w^T (w: N x Kd) + b (+ residual)."""
     y = torch.empty(M, N, device=x.device) if out is None else out
@@ -182,15 +190,16 @@ class _MLPMixerFn(torch.autograd.Function):
         P = K.patchify(nf, B, Lf, C, ps)                       # (B*NP, ps^2)
         Z = _lin(P, B * NP, D, ps * ps, we, be)                 # (B*NP, D)
         Y1, m1, r1 = K.layer_norm_fwd(Z, g1, b1n, mix.ln_eps[0])
-        # token mixing: UT_b (D x 4NP) = Y1_b^T . W1^T + b1   (Conv1d(NP -> 4NP, k1) on (B, NP, D))
-        W1 = w1.view(4 * NP, NP)
-        W2 = w2.view(NP, 4 * NP)
+        # token mixing: UT_b (D x 4NP) = Y1_b^T . W1^T + b1   (Conv1d(NP -> 4NP, k1) on (B, NP, D)).
+        # NP (121 / 1849 patches) is never the contiguous dimension of a GEMM operand: W1 is
+        # used as its transpose W1T (NP x 4NP), so every product takes the vectorised kernels.
+        W1T, W2c = _token_mix_weights(mix, w1, w2, NP)
         UT = torch.empty(B * D, 4 * NP, device=dev)
-        K.gemm(D, 4 * NP, NP, operand(Y1, D, kstrided=True, batch_stride=NP * D), operand(W1, NP), UT, bias=bb1,
-               batch=B, c_batch_stride=D * 4 * NP)
+        K.gemm(D, 4 * NP, NP, operand(Y1, D, kstrided=True, batch_stride=NP * D), operand(W1T, 4 * NP, kstrided=True),
+               UT, bias=bb1, batch=B, c_batch_stride=D * 4 * NP)
         V = K.act_fwd(UT, K.ACT_GELU)
         RT = torch.empty(B * D, NP, device=dev)
-        K.gemm(D, NP, 4 * NP, operand(V, 4 * NP, batch_stride=D * 4 * NP), operand(W2, 4 * NP), RT, bias=bb2,
+        K.gemm(D, NP, 4 * NP, operand(V, 4 * NP, batch_stride=D * 4 * NP), operand(W2c, 4 * NP), RT, bias=bb2,
                batch=B, c_batch_stride=D * NP)
         Z1 = K.transpose_batched(RT, B, D, NP, out=K.convert(Z, K.F32), accumulate=True).view(B * NP, D)
         Y2, m2, r2 = K.layer_norm_fwd(Z1, g2, b2n, mix.ln_eps[1])
@@ -239,23 +248,23 @@ class _MLPMixerFn(torch.autograd.Function):
         dg2 = torch.empty(D, device=dev)
         db2n = torch.empty(D, device=dev)
         dZ1 = K.add(dZ2, K.layer_norm_bwd(dY2, Z1, g2, m2, r2, dg2, db2n))
-        # token FF: Z1 = Z + (GELU(Y1^T W1^T + b1) W2^T + b2)^T   per utterance
-        W1 = w1.view(4 * NP, NP)
-        W2 = w2.view(NP, 4 * NP)
-        dRT = K.transpose_batched(dZ1, B, NP, D).view(B * D, NP)
+        # token FF: Z1 = Z + (GELU(Y1^T W1^T + b1) W2^T + b2)^T   per utterance.  dRT_b = dZ1_b^T is
+        # read in place from dZ1 (as the transposed operand), so NP is never a contiguous dimension.
+        W1T, W2c = _token_mix_weights(mix, w1, w2, NP)
         dW2 = torch.empty(NP, 4 * NP, device=dev)
-        K.gemm(NP, 4 * NP, D, operand(dRT, NP, kstrided=True, batch_stride=D * NP),
+        K.gemm(NP, 4 * NP, D, operand(dZ1, D, batch_stride=NP * D),
                operand(V, 4 * NP, kstrided=True, batch_stride=D * 4 * NP), dW2, batch=B, c_batch_stride=0)
-        dbb2 = K.colsum(dRT, B * D, NP)
+        dbb2 = K.colsum(K.transpose_batched(dZ1, B, NP, D).view(B * D, NP), B * D, NP)
         dV = torch.empty(B * D, 4 * NP, device=dev)
-        K.gemm(B * D, 4 * NP, NP, operand(dRT, NP), operand(W2, 4 * NP, kstrided=True), dV)
+        K.gemm(D, 4 * NP, NP, operand(dZ1, D, kstrided=True, batch_stride=NP * D), operand(W2c, 4 * NP, kstrided=True),
+               dV, batch=B, c_batch_stride=D * 4 * NP)
         dUT = K.gelu_bwd(dV, UT)
         dW1 = torch.empty(4 * NP, NP, device=dev)
         K.gemm(4 * NP, NP, D, operand(dUT, 4 * NP, kstrided=True, batch_stride=D * 4 * NP),
                operand(Y1, D, batch_stride=NP * D), dW1, batch=B, c_batch_stride=0)
         dbb1 = K.colsum(dUT, B * D, 4 * NP)
         dY1T = torch.empty(B * D, NP, device=dev)
-        K.gemm(B * D, NP, 4 * NP, operand(dUT, 4 * NP), operand(W1, NP, kstrided=True), dY1T)
+        K.gemm(B * D, NP, 4 * NP, operand(dUT, 4 * NP), operand(W1T, 4 * NP), dY1T)
         dY1 = K.transpose_batched(dY1T, B, D, NP).view(M, D)
         dg1 = torch.empty(D, device=dev)
         db1n = torch.empty(D, device=dev)

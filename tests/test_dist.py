@@ -29,8 +29,9 @@ def _worker(rank, world, port, q):
         torch.manual_seed(100 + rank)  # ranks start from different weights
         m = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.Conv1d(5, 3, 3))
         params, flat, gflat = D.flatten_params_(m, device=torch.device("cpu"))
-        assert flat.numel() == sum(p.numel() for p in m.parameters())
+        assert flat.numel() == D.param_offsets(params)[1] >= sum(p.numel() for p in m.parameters())
         assert all(p.data_ptr() >= flat.data_ptr() for p in params)
+        assert all((p.data_ptr() - flat.data_ptr()) % (4 * D.PARAM_ALIGN) == 0 for p in params)
         D.broadcast_(flat)
         # gradients: rank-dependent, averaged in 3 small buckets (bucket_bytes=64 -> 16 floats)
         gflat.copy_(torch.arange(gflat.numel(), dtype=torch.float32) * (rank + 1))
@@ -64,7 +65,7 @@ def test_dp_broadcast_and_allreduce_world2():
     expect = torch.arange(n, dtype=torch.float32) * 1.5  # mean of (1x, 2x)
     for r in (0, 1):
         torch.testing.assert_close(res[r][1], expect)
-        torch.testing.assert_close(res[r][2].reshape(-1), expect[:35])  # .grad views the flat buffer
+        torch.testing.assert_close(res[r][2].reshape(-1), expect[:35])  # .grad views the flat buffer (offset 0)
 
 
 def test_single_process_is_a_noop(monkeypatch):
