@@ -65,19 +65,41 @@ def broadcast_(flat: torch.Tensor, src: int = 0):
         dist.broadcast(flat, src)
 
 
-def allreduce_mean_(gflat: torch.Tensor, bucket_bytes: int = BUCKET_BYTES):
-    """Average gradients over ranks in ~32 MB buckets (xGMI ring: per-link bound, so a few
-    large collectives beat many small ones)."""
-    if not (dist.is_initialized() and dist.get_world_size() > 1):
-        return
-    world = dist.get_world_size()
+def allreduce_mean_async_(g: torch.Tensor, bucket_bytes: int = BUCKET_BYTES):
+    """Start averaging `g` over ranks in ~32 MB buckets (xGMI ring: per-link bound, so a few
+    large collectives beat many small ones).  Returns a handle for finish_allreduce_()."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1) or g.numel() == 0:
+        return None
     use_avg = dist.get_backend() == "nccl"
-    step = max(1, bucket_bytes // gflat.element_size())
-    works = []
-    for off in range(0, gflat.numel(), step):
-        chunk = gflat[off:off + step]
-        works.append(dist.all_reduce(chunk, op=dist.ReduceOp.AVG if use_avg else dist.ReduceOp.SUM, async_op=True))
+    step = max(1, bucket_bytes // g.element_size())
+    works = [dist.all_reduce(g[off:off + step], op=dist.ReduceOp.AVG if use_avg else dist.ReduceOp.SUM,
+                             async_op=True) for off in range(0, g.numel(), step)]
+    return works, g, use_avg
+
+
+def finish_allreduce_(handle):
+    """Wait for allreduce_mean_async_ (RCCL: the current stream waits on the collective)."""
+    if handle is None:
+        return
+    works, g, use_avg = handle
     for w in works:
         w.wait()
     if not use_avg:
-        gflat.mul_(1.0 / world)
+        g.mul_(1.0 / dist.get_world_size())
+
+
+def allreduce_mean_(gflat: torch.Tensor, bucket_bytes: int = BUCKET_BYTES):
+    """Average gradients over ranks (blocking form of allreduce_mean_async_)."""
+    finish_allreduce_(allreduce_mean_async_(gflat, bucket_bytes))
+
+
+def split_offset(params, first_late):
+    """Flat-buffer offset where parameter `first_late` (in flatten_params_ order) starts: the
+    gradients below it (the encoder, used by both the full pass and the re-pass) complete last,
+    the ones from it on (decoder, postnet, discriminator) are final before the encoder
+    backward runs and are all-reduced while it runs."""
+    offs, _ = param_offsets(params)
+    for p, off in zip(params, offs):
+        if p is first_late:
+            return off
+    raise ValueError("parameter not in the flattened list")

@@ -143,6 +143,10 @@ class MetaConv(nn.Module):
         B, T = xs.shape[0], xs.shape[1]
         cd = 2 * self.dim_neck
         enc_out = Lyr.dec_concat(codes, c_trg.contiguous(), B, T, codes.shape[1] // cd, cd)
+        hook = getattr(self, "_decoder_bwd_done", None)
+        if hook is not None and enc_out.requires_grad:
+            # fires once the backward has produced every decoder / postnet gradient
+            enc_out.register_hook(lambda g: hook())
         mel = self.decoder.frames(enc_out, B, T)
         mel_postnet = self.postnet.frames(mel, B, T, residual=mel)
         return mel.view(B, 1, T, -1), mel_postnet.view(B, 1, T, -1), codes

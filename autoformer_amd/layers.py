@@ -38,6 +38,11 @@ def sink_on() -> bool:
     return _SINK["on"]
 
 
+def side_stream():
+    """The weight-gradient stream (None before set_grad_sink(True))."""
+    return _SINK["side"]
+
+
 def mark():
     """Event on the current stream (sink mode): a later _Side(after=...) starts from here, so
     the critical-path kernels launched in between (data gradients) are not delayed behind

@@ -22,7 +22,7 @@ import torch
 
 from . import dist as D
 from . import kernels as K
-from .layers import join_side, set_grad_sink, weights_changed
+from .layers import join_side, set_grad_sink, side_stream, weights_changed
 
 
 # ------------------------------------------------------------------------- losses
@@ -153,24 +153,59 @@ class TrainStep:
         self.graph_fb = None
         self.world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
         self.loss = None
+        # Data parallel: the decoder / postnet (/ discriminator) gradients are final once the
+        # backward reaches the decoder input; they are averaged on a communication stream while
+        # the encoder backward (full pass + re-pass gradients) still runs, and only the encoder
+        # slice is averaged after the backward.
+        self.split = None
+        if self.world > 1 and hasattr(model, "decoder"):
+            self.split = D.split_offset(self.params, next(model.decoder.parameters()))
+            self.comm = torch.cuda.Stream()
+        self._early = None
 
-    def _fwd_bwd(self, x, emb):
+    def _decoder_done(self):
+        main = torch.cuda.current_stream()
+        self.comm.wait_stream(main)
+        side = side_stream()
+        if side is not None:
+            self.comm.wait_stream(side)
+        with torch.cuda.stream(self.comm):
+            self._early = D.allreduce_mean_async_(self.gflat[self.split:])
+
+    def _fwd_bwd(self, x, emb, overlap=False):
         self.gflat.zero_()
-        loss, parts, x_psnt = vc_losses(self.model, x, emb, self.lambda_cd)
-        if self.extra is not None:
-            loss = loss + self.extra(x, emb, x_psnt)
-        loss.backward()
+        self.model._decoder_bwd_done = self._decoder_done if overlap else None
+        try:
+            loss, parts, x_psnt = vc_losses(self.model, x, emb, self.lambda_cd)
+            if self.extra is not None:
+                loss = loss + self.extra(x, emb, x_psnt)
+            loss.backward()
+        finally:
+            self.model._decoder_bwd_done = None
         join_side()  # weight-gradient GEMMs ran on the side stream
         return loss
+
+    def _allreduce(self):
+        if self._early is None:  # no overlapped part (graph replay, or no hook fired)
+            D.allreduce_mean_(self.gflat)
+            return
+        main = torch.cuda.current_stream()
+        self.comm.wait_stream(main)
+        with torch.cuda.stream(self.comm):
+            late = D.allreduce_mean_async_(self.gflat[:self.split])
+            D.finish_allreduce_(self._early)
+            D.finish_allreduce_(late)
+        main.wait_stream(self.comm)
+        self._early = None
 
     def step(self, x, emb):
         if self.graph_fb is not None:
             self.graph_fb.replay()
             loss = self.loss
         else:
-            loss = self._fwd_bwd(x, emb)
+            loss = self._fwd_bwd(x, emb, overlap=self.split is not None)
         if self.world > 1:
-            D.allreduce_mean_(self.gflat)
+            self._allreduce()
         self.opt.step()
         return loss
 

@@ -36,6 +36,15 @@ def _worker(rank, world, port, q):
         # gradients: rank-dependent, averaged in 3 small buckets (bucket_bytes=64 -> 16 floats)
         gflat.copy_(torch.arange(gflat.numel(), dtype=torch.float32) * (rank + 1))
         D.allreduce_mean_(gflat, bucket_bytes=64)
+        # overlapped form: the late slice [split:] first, then the head, as TrainStep does
+        split = D.split_offset(params, params[2])  # the conv weight starts the "decoder" part
+        assert split == D.param_offsets(params)[0][2]
+        g2 = torch.arange(gflat.numel(), dtype=torch.float32) * (rank + 1)
+        early = D.allreduce_mean_async_(g2[split:], bucket_bytes=64)
+        late = D.allreduce_mean_async_(g2[:split], bucket_bytes=64)
+        D.finish_allreduce_(early)
+        D.finish_allreduce_(late)
+        torch.testing.assert_close(g2, torch.arange(gflat.numel(), dtype=torch.float32) * 1.5)
         q.put((rank, flat.clone(), gflat.clone(), m[0].weight.grad.clone()))
         dist.barrier()
         dist.destroy_process_group()

@@ -1,0 +1,88 @@
+"""Data-parallel TrainStep on the MI355X with two ranks sharing one GPU (gloo backend, fp32
+compute so the per-step LSTM kernels run instead of the whole-GPU persistent ones): with
+identical batches on both ranks the overlapped gradient average (decoder/postnet slice during
+the encoder backward, encoder slice after it) must leave the parameters exactly where a
+single-process step puts them."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+B, T, FREQ = 2, 32, 16
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run_steps(steps=2):
+    import autoformer_amd as A
+    from autoformer_amd.detinit import det_init_, det_inputs
+    from autoformer_amd.factory.AutoVC import AutoVC
+    from autoformer_amd.layers import set_grad_sink
+    from autoformer_amd.train import TrainStep
+
+    A.set_compute("fp32")
+    m = AutoVC(44, 256, 512, FREQ)
+    det_init_(m)
+    m = m.to("cuda:0").train()
+    x, e = det_inputs(B, T, seed=11)
+    x, e = torch.from_numpy(x).cuda(), torch.from_numpy(e).cuda()
+    ts = TrainStep(m, lr=1e-4)
+    try:
+        for _ in range(steps):
+            ts.step(x, e)
+        torch.cuda.synchronize()
+        overlapped = ts.split is not None
+    finally:
+        set_grad_sink(False)
+    return ts.flat.cpu().numpy(), overlapped  # numpy: pickled by value through the queue
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from autoformer_amd import dist as D
+
+    try:
+        D.init_from_env("gloo")
+        flat, overlapped = _run_steps()
+        q.put((rank, flat, overlapped))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as exc:  # surface worker failures to the parent
+        q.put((rank, repr(exc), None))
+        raise
+
+
+@pytest.mark.timeout(240)
+def test_dp_world2_overlapped_allreduce_matches_single_process():
+    single, _ = _run_steps()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        rank, flat, overlapped = q.get(timeout=200)
+        assert not isinstance(flat, str), flat
+        assert overlapped, "the decoder-slice all-reduce was not overlapped with the backward"
+        res[rank] = flat
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    r0, r1, single = (torch.from_numpy(a) for a in (res[0], res[1], single))
+    torch.testing.assert_close(r0, r1, rtol=0, atol=0)
+    torch.testing.assert_close(r0, single, rtol=1e-5, atol=1e-7)
