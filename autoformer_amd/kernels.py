@@ -93,12 +93,14 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     L.check(L.lib().avc_gemm(d, stream()), "avc_gemm")
 
 
-def auto_split_k(M, N, K, target=256, min_k=1024):
+def auto_split_k(M, N, K, target=384, min_k=256):
+    """Split-K factor for the weight-gradient GEMMs (K = frames): about `target` workgroups
+    over the 128x128 output tiles (1.5 per CU: a K-loop alone is latency-bound, ~1.4 us per
+    64-deep step), each split at least `min_k` long.  Chosen from a split-K sweep of every
+    weight-gradient shape of the AutoVC step on MI355X (tools/gemm_census.py --sweep)."""
     tiles = math.ceil(M / 128) * math.ceil(N / 128)
-    if tiles >= target // 2:
-        return 1
-    s = max(1, min(target // max(tiles, 1), K // min_k))
-    return s
+    s = int(target / max(tiles, 1) + 0.5)
+    return max(1, min(s, K // min_k))
 
 
 # ------------------------------------------------------------------------- BN

@@ -12,6 +12,8 @@ per training step.
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from . import kernels as K
@@ -98,20 +100,64 @@ def weights_changed() -> None:
     _EPOCH[0] += 1
 
 
+_PLAN = []  # every PackCache in first-use order (the next step's prefetch plan)
+
+
+def _pack_key(params):
+    return (_EPOCH[0], K.compute(), tuple((p.data_ptr(), p._version) for p in params))
+
+
 class PackCache:
-    __slots__ = ("key", "val")
+    """Derived copy of some parameters (packed / transposed / bf16 weights), rebuilt when
+    they change.  prefetch_packs() builds the next step's copies on the side stream right
+    after the optimizer step; get() then only orders the current stream after that build."""
+    __slots__ = ("key", "val", "pending", "params", "build", "__weakref__")
 
     def __init__(self):
         self.key = None
         self.val = None
+        self.pending = None
+        self.params = None
+        self.build = None
 
     def get(self, params, build):
-        key = (_EPOCH[0], K.compute(), tuple((p.data_ptr(), p._version) for p in params))
+        key = _pack_key(params)
         if key != self.key:
-            with torch.no_grad():
-                self.val = build()
+            pend, self.pending = self.pending, None
+            if pend is not None and pend[0] == key:
+                torch.cuda.current_stream().wait_event(pend[2])
+                self.val = pend[1]
+            else:
+                with torch.no_grad():
+                    self.val = build()
             self.key = key
+            if self.build is None:
+                _PLAN.append(weakref.ref(self))
+            self.params, self.build = params, build
         return self.val
+
+
+def prefetch_packs() -> None:
+    """After the optimizer step: rebuild every weight pack of the plan on the side stream, in
+    the order the forward will ask for them (the encoder's first, so the forward's first
+    wait is short and the rest are ready long before the decoder / postnet need them)."""
+    side = _SINK["side"]
+    if side is None or not _PLAN:
+        return
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side), torch.no_grad():
+        for ref in list(_PLAN):
+            c = ref()
+            if c is None:
+                _PLAN.remove(ref)
+                continue
+            key = _pack_key(c.params)
+            if key == c.key:
+                continue
+            val = c.build()
+            ev = torch.cuda.Event()
+            ev.record(side)
+            c.pending = (key, val, ev)
 
 
 def _need(t):

@@ -22,7 +22,7 @@ import torch
 
 from . import dist as D
 from . import kernels as K
-from .layers import join_side, set_grad_sink, side_stream, weights_changed
+from .layers import join_side, prefetch_packs, set_grad_sink, side_stream, weights_changed
 
 
 # ------------------------------------------------------------------------- losses
@@ -207,6 +207,8 @@ class TrainStep:
         if self.world > 1:
             self._allreduce()
         self.opt.step()
+        if self.graph_fb is None:
+            prefetch_packs()  # next step's weight packs, on the side stream
         return loss
 
     def capture(self, x, emb, warmup=2):
