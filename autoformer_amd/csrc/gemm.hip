@@ -733,6 +733,7 @@ extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
     int klf = (d->K + g.split_k - 1) / g.split_k;
     g.klen = ((klf + FBK - 1) / FBK) * FBK;
     if (g.klen <= 0) g.klen = FBK;
+    if (!aks && !bks && gemm_conv_launch(g, s)) return avc_check_launch("avc_gemm(conv)");
     if (!aks && !bks && gemm_nt_launch(g, s)) return avc_check_launch("avc_gemm(nt)");
     if (aks && bks && gemm_tt_launch(g, s)) return avc_check_launch("avc_gemm(tt)");
     const long long t128 = (long long)cdiv(g.M, BM) * cdiv(g.N, 128) * g.batch * g.split_k;

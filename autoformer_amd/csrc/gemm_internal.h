@@ -133,6 +133,8 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
 // Entry of the NT (both operands K-contiguous, bf16) LDS-DMA pipelined kernel (gemm_nt.hip).
 // Returns false when the shape/operands do not qualify (caller falls back).
 bool gemm_nt_launch(const GemmArgs& g, hipStream_t s);
+// Entry of the halo-reuse Conv1d kernel (5 taps, 'same' padding, bf16; gemm_conv.hip).
+bool gemm_conv_launch(const GemmArgs& g, hipStream_t s);
 // Entry of the TT (both operands K-strided, bf16) weight-gradient kernel (gemm_tt.hip).
 bool gemm_tt_launch(const GemmArgs& g, hipStream_t s);
 

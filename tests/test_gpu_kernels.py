@@ -86,7 +86,7 @@ def test_gemm_bias_accumulate_splitk_batch():
 
 
 @pytest.mark.parametrize("B,T,Cin,Cout,Kw,pad", [(2, 176, 336, 512, 5, 2), (3, 37, 80, 96, 5, 2), (2, 80, 176, 88, 3, 0),
-                                                  (2, 30, 44, 22, 3, 0)])
+                                                  (2, 30, 44, 22, 3, 0), (4, 64, 512, 96, 5, 2), (3, 40, 64, 512, 5, 2)])
 @pytest.mark.parametrize("comp", ["fp32", "bf16"])
 def test_conv_gemm_fwd_dgrad_wgrad(B, T, Cin, Cout, Kw, pad, comp):
     """Conv1d as a windowed GEMM: forward, data- and weight-gradient vs F.conv1d autograd."""
@@ -104,6 +104,8 @@ def test_conv_gemm_fwd_dgrad_wgrad(B, T, Cin, Cout, Kw, pad, comp):
     y.backward(gy)
     dt = Kr.BF16 if comp == "bf16" else Kr.F32
     xf = x.detach().transpose(1, 2).reshape(B * T, Cin).contiguous().to(DEV)
+    if comp == "bf16":  # bf16 activations: the forms the halo conv kernel (gemm_conv.hip) takes
+        xf = xf.to(torch.bfloat16)
     wd = w.detach().to(DEV)
     Wf = Kr.conv_pack(wd, 0, dt)
     Wd = Kr.conv_pack(wd, 1, dt)
@@ -111,6 +113,8 @@ def test_conv_gemm_fwd_dgrad_wgrad(B, T, Cin, Cout, Kw, pad, comp):
     Kr.gemm(B * To, Cout, Kw * Cin, Kr.operand(xf, Cin, window=(Kw, pad, To, T, Cin)), Kr.operand(Wf, Kw * Cin), out)
     assert relf(out, y.detach().transpose(1, 2).reshape(B * To, Cout)) < tol
     gyf = gy.transpose(1, 2).reshape(B * To, Cout).contiguous().to(DEV)
+    if comp == "bf16":
+        gyf = gyf.to(torch.bfloat16)
     dx = torch.empty(B * T, Cin, device=DEV)
     Kr.gemm(B * T, Cin, Kw * Cout, Kr.operand(gyf, Cout, window=(Kw, Kw - 1 - pad, T, To, Cout)),
             Kr.operand(Wd, Kw * Cout), dx)
@@ -354,9 +358,13 @@ def test_gemm_nt_lds_pipeline_bf16_operands(M, N, K, split):
     assert relf(c, ref) < 1e-5, relf(c, ref)
 
 
-@pytest.mark.parametrize("B,T,Cin,Cout,Kw,pad", [(3, 37, 64, 96, 5, 2), (64, 128, 512, 512, 5, 2), (2, 9, 8, 24, 3, 1)])
+@pytest.mark.parametrize("B,T,Cin,Cout,Kw,pad", [(3, 37, 64, 96, 5, 2), (64, 128, 512, 512, 5, 2), (2, 9, 8, 24, 3, 1),
+                                                 (8, 176, 512, 80, 5, 2), (5, 50, 96, 136, 5, 2), (1, 3, 32, 64, 5, 2)])
 def test_gemm_nt_conv_window_and_bn_stats(B, T, Cin, Cout, Kw, pad):
-    """Windowed (im2col) A operand through the NT kernel + the BN partial-statistics epilogue."""
+    """Windowed (im2col) A operand + the BN partial-statistics epilogue.  Five-tap 'same' convs
+    with Cin % 32 == 0 take the halo-reuse conv kernel (gemm_conv.hip): tiles inside one
+    utterance (T=128), tiles spanning utterances (T=37, 50, 176), utterances shorter than the
+    halo (T=3), and output-channel tails (80, 96, 136)."""
     import autoformer_amd as A
     from autoformer_amd import kernels as Kr
 
