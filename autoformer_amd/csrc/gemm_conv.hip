@@ -29,12 +29,6 @@ namespace {
 
 __device__ __attribute__((aligned(16))) unsigned int g_zero16_cv[4] = {0u, 0u, 0u, 0u};
 
-constexpr int CBK = 32;                 // channels per stage
-constexpr int CROW = CBK * 2;           // 64-B LDS rows
-constexpr int CBN = 64;                 // output columns per tile
-constexpr int AROWS = 192;              // halo rows reserved per stage: 3 glds per thread
-constexpr int CA_BYTES = AROWS * CROW;  // 12 KiB
-
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 
@@ -47,22 +41,30 @@ __device__ __forceinline__ void wait_vm() {
 }
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
-__device__ __forceinline__ int cswz(int row) { return (row >> 1) & 3; }
-
-template <int TAPS>
+// CBK channels per stage (LDS rows of 2*CBK bytes), CBN output columns per tile.
+template <int TAPS, int CBK, int CBN>
 struct ConvCfg {
-  static constexpr int B_BYTES = TAPS * CBN * CROW;
-  static constexpr int STAGE = CA_BYTES + B_BYTES;
-  static constexpr int BI = TAPS * CBN / 16 / 4;  // weight glds per thread per stage
-  static constexpr int LPT = 3 + BI;              // glds per thread per stage
-  static_assert(TAPS * CBN % 64 == 0, "weight rows must split over four waves");
-  static_assert(BM + TAPS - 1 <= AROWS, "halo does not fit");
+  static constexpr int ROW = 2 * CBK;             // bytes per LDS row
+  static constexpr int CPR = ROW / 16;            // 16-B chunks per row
+  static constexpr int RPI = 1024 / ROW;          // rows per glds wave-instruction
+  static constexpr int AI = ((BM + TAPS - 1 + RPI - 1) / RPI + 3) / 4 * 4;  // halo instructions (x4 waves)
+  static constexpr int A_BYTES = AI * 1024;
+  static constexpr int BI = TAPS * CBN / RPI;     // weight instructions
+  static constexpr int B_BYTES = BI * 1024;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int LPT = AI / 4 + BI / 4;     // glds per thread per stage
+  static constexpr int NJ = CBN / 32;
+  static_assert(BI % 4 == 0, "weight rows must split over four waves");
+  static_assert(CBN % 32 == 0 && (CBK == 32 || CBK == 64), "tile shape");
+  // slot of chunk c in row r (XOR swizzle on the 16-B chunk index)
+  __device__ static __forceinline__ int swz(int r) { return (r >> 1) & (CPR - 1); }
 };
 
-template <int TAPS, int CNST>
+template <int TAPS, int NST, int CBK, int CBN>
 __global__ void __launch_bounds__(256, 2) gemm_conv_kernel(GemmArgs g) {
-  using Cfg = ConvCfg<TAPS>;
-  constexpr int STAGE = Cfg::STAGE, LPT = Cfg::LPT, BI = Cfg::BI, P = CNST - 1;
+  using C = ConvCfg<TAPS, CBK, CBN>;
+  constexpr int STAGE = C::STAGE, LPT = C::LPT, AI4 = C::AI / 4, BI4 = C::BI / 4, P = NST - 1;
+  constexpr int ROW = C::ROW, CPR = C::CPR, RPI = C::RPI, NJ = C::NJ, KB = CBK / 32;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -83,36 +85,36 @@ __global__ void __launch_bounds__(256, 2) gemm_conv_kernel(GemmArgs g) {
   const long long lda = A.ld, ldb = Bo.ld;
   const int nst = chans / CBK;
 
-  // ---- loader: halo row hr = 16*(3*wid + i) + (lane >> 2), slot lane & 3
-  long long aoff[3];
-  bool aok[3];
+  // ---- loader: instruction ins writes LDS [ins*1KiB, +1KiB) = rows RPI*ins + lane / CPR,
+  // slot lane % CPR, which holds global chunk slot ^ swz(row)
+  const int lrow = lane / CPR, lslot = lane % CPR;
+  long long aoff[AI4];
+  bool aok[AI4];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int hr = 16 * (3 * wid + i) + (lane >> 2);
+  for (int i = 0; i < AI4; ++i) {
+    const int hr = RPI * (AI4 * wid + i) + lrow;
     const int f = m0 - pad + hr;
     aok[i] = hr < BM + TAPS - 1 && f >= 0 && f < g.M;
-    aoff[i] = (long long)(aok[i] ? f : 0) * lda + 8 * ((lane & 3) ^ cswz(hr));
+    aoff[i] = (long long)(aok[i] ? f : 0) * lda + 8 * (lslot ^ C::swz(hr));
   }
-  // weight row wr = 16*((wid*BI + i) % 4) + (lane >> 2) of tap (wid*BI + i) / 4
-  long long boff[BI];
-  bool bok[BI];
+  long long boff[BI4];
+  bool bok[BI4];
 #pragma unroll
-  for (int i = 0; i < BI; ++i) {
-    const int ins = wid * BI + i, tap = ins >> 2, wr = 16 * (ins & 3) + (lane >> 2);
-    const int n = n0 + wr;
+  for (int i = 0; i < BI4; ++i) {
+    const int ins = wid * BI4 + i, wr = RPI * ins + lrow, tap = wr / CBN, n = n0 + (wr - tap * CBN);
     bok[i] = n < g.N;
-    boff[i] = (long long)(bok[i] ? n : 0) * ldb + (long long)tap * chans + 8 * ((lane & 3) ^ cswz(wr));
+    boff[i] = (long long)(bok[i] ? n : 0) * ldb + (long long)tap * chans + 8 * (lslot ^ C::swz(wr));
   }
   auto issue = [&](int st, int cs) {
     char* base = smem_raw + st * STAGE;
     const int c0 = cs * CBK;
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
-      glds16(aok[i] ? (const void*)(xa + aoff[i] + c0) : (const void*)g_zero16_cv, base + (3 * wid + i) * 1024);
+    for (int i = 0; i < AI4; ++i)
+      glds16(aok[i] ? (const void*)(xa + aoff[i] + c0) : (const void*)g_zero16_cv, base + (AI4 * wid + i) * 1024);
 #pragma unroll
-    for (int i = 0; i < BI; ++i)
+    for (int i = 0; i < BI4; ++i)
       glds16(bok[i] ? (const void*)(wb + boff[i] + c0) : (const void*)g_zero16_cv,
-             base + CA_BYTES + (wid * BI + i) * 1024);
+             base + C::A_BYTES + (wid * BI4 + i) * 1024);
   };
 
   // ---- fragment addressing and the per-tap validity of this lane's four A rows
@@ -131,18 +133,15 @@ __global__ void __launch_bounds__(256, 2) gemm_conv_kernel(GemmArgs g) {
       if (t2 >= 0 && t2 < T) vmask |= 1u << (i * 8 + k);
     }
   }
-  int bfo[2];
+  int brow[NJ];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int r = wn * 32 + j * 16 + fr;
-    bfo[j] = CA_BYTES + r * CROW + 16 * (ch ^ cswz(r));
-  }
+  for (int j = 0; j < NJ; ++j) brow[j] = wn * (CBN / 2) + j * 16 + fr;
 
-  f32x4 acc[4][2];
+  f32x4 acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
   for (int p = 0; p < P; ++p)
@@ -161,40 +160,49 @@ __global__ void __launch_bounds__(256, 2) gemm_conv_kernel(GemmArgs g) {
       wait_vm<0>();
     }
     raw_barrier();
-    if (cs + P < nst) issue((cs + P) % CNST, cs + P);
-    const char* st = smem_raw + (cs % CNST) * STAGE;
+    if (cs + P < nst) issue((cs + P) % NST, cs + P);
+    const char* st = smem_raw + (cs % NST) * STAGE;
 #pragma unroll
     for (int k = 0; k < TAPS; ++k) {
-      bf16x8 af[4], bfr[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = arow[i] + k;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(st + r * CROW + 16 * (ch ^ cswz(r)));
-        af[i] = ((vmask >> (i * 8 + k)) & 1u) ? v : bf16x8{};
+      for (int kb = 0; kb < KB; ++kb) {
+        bf16x8 af[4], bfr[NJ];
+        const int cc = 4 * kb + ch;  // this lane's 16-B chunk of K block kb
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = arow[i] + k;
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(st + r * ROW + 16 * (cc ^ C::swz(r)));
+          af[i] = ((vmask >> (i * 8 + k)) & 1u) ? v : bf16x8{};
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int r = k * CBN + brow[j];
+          bfr[j] = *reinterpret_cast<const bf16x8*>(st + C::A_BYTES + r * ROW + 16 * (cc ^ C::swz(r)));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(st + k * CBN * CROW + bfo[j]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   }
   __syncthreads();  // last wait was vmcnt(0); every fragment read done before the epilogue reuses LDS
   fast_epilogue<CBN>(g, acc, m0, n0, mt, 0, 0, smem_raw);
 }
 
-template <int TAPS, int CNST>
-void launch(const GemmArgs& g, int nblocks, hipStream_t s) {
-  const size_t lds = (size_t)CNST * ConvCfg<TAPS>::STAGE;
+template <int NST, int CBK, int CBN>
+void launch(const GemmArgs& g, hipStream_t s) {
+  using C = ConvCfg<5, CBK, CBN>;
+  const size_t lds = (size_t)NST * C::STAGE;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_conv_kernel<TAPS, CNST>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_conv_kernel<5, NST, CBK, CBN>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  gemm_conv_kernel<TAPS, CNST><<<nblocks, 256, lds, s>>>(g);
+  const int nb = ((g.M + BM - 1) / BM) * ((g.N + CBN - 1) / CBN);
+  gemm_conv_kernel<5, NST, CBK, CBN><<<nb, 256, lds, s>>>(g);
 }
 
 bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -202,20 +210,46 @@ bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 }  // namespace
 
 bool gemm_conv_launch(const GemmArgs& g, hipStream_t s) {
-  // AVC_CONV_HALO: 0 = off (window stream through gemm_nt), 2 / 3 / 4 = LDS stages
-  static const int mode = getenv("AVC_CONV_HALO") ? atoi(getenv("AVC_CONV_HALO")) : 2;
-  if (!mode) return false;
+  // AVC_CONV_CFG = "stages,channels,columns" (benchmarking); "0" = off (window stream, gemm_nt)
+  static int cfg[3] = {-1, 0, 0};
+  if (cfg[0] < 0) {
+    cfg[0] = 2;  // measured (tools/gemm_census.py, AVC_CONV_CFG sweep): two 32-KiB stages, 32 channels,
+    cfg[1] = 32; // 64 columns -- two workgroups per CU -- beat 64-channel stages (44-47 us) and
+    cfg[2] = 64; // three or four stages at one workgroup per CU (50-69 us) on 8192x512x2560
+    if (const char* e = getenv("AVC_CONV_CFG")) {
+      int a0 = 0, a1 = 0, a2 = 0;
+      const int n = sscanf(e, "%d,%d,%d", &a0, &a1, &a2);
+      cfg[0] = a0;
+      if (n == 3) {
+        cfg[1] = a1;
+        cfg[2] = a2;
+      }
+    }
+  }
+  if (cfg[0] == 0) return false;
   const OpDev& a = g.a;
   const OpDev& b = g.b;
   if (!a.win || a.taps != 5 || a.t_in != a.t_out || 2 * a.pad != a.taps - 1) return false;
-  if (a.chans % CBK || g.K != a.taps * a.chans || g.batch != 1 || g.split_k != 1) return false;
+  if (g.K != a.taps * a.chans || g.batch != 1 || g.split_k != 1) return false;
   if (a.dtype != AVC_BF16 || b.dtype != AVC_BF16 || b.win) return false;
   if (!ok16(a.ptr) || !ok16(b.ptr) || a.ld % 8 || b.ld % 8) return false;
-  const int nb = ((g.M + BM - 1) / BM) * ((g.N + CBN - 1) / CBN);
-  if (mode == 3) launch<5, 3>(g, nb, s);
-  else if (mode == 4) launch<5, 4>(g, nb, s);
-  else launch<5, 2>(g, nb, s);
-  return true;
+  int ns = cfg[0], bk = cfg[1], bn = cfg[2];
+  if (a.chans % bk) bk = 32;  // 32-channel stages for channel counts that are not 64-multiples
+  if (a.chans % bk) return false;
+  if (bk == 32 && bn == 32) bn = 64;
+#define CONV_CASE(NS, BK, BN)                  \
+  if (ns == NS && bk == BK && bn == BN) {      \
+    launch<NS, BK, BN>(g, s);                  \
+    return true;                               \
+  }
+  CONV_CASE(2, 32, 64) CONV_CASE(3, 32, 64) CONV_CASE(4, 32, 64) CONV_CASE(2, 64, 32) CONV_CASE(3, 64, 32)
+  CONV_CASE(2, 64, 64)
+#undef CONV_CASE
+  if (bk == 32) {
+    launch<2, 32, 64>(g, s);
+    return true;
+  }
+  return false;
 }
 
 }  // namespace avcg
