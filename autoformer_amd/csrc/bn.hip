@@ -18,6 +18,30 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 // (independent loads, no serial chain).  Merge = two passes over the partials:
 //   mean = sum_t s_t / n;   M2 = sum_t [ q_t + n_t (s_t / n_t - mean)^2 ]   (Chan, parallel form)
 constexpr int FG = 16;  // row groups of the finalize reductions (1024 threads = 64 channels x 16)
+constexpr int FU = 8;   // partial rows per thread loaded together (independent loads in flight)
+
+// sum over b = grp, grp + FG, ... < nrb of NV consecutive floats at ws[(b*ld + c)*NV + v]:
+// FU rows' loads are issued before any is added (one memory latency per FU*FG rows, not per row)
+template <int NV>
+__device__ __forceinline__ void strided_sums(const float* __restrict__ ws, int nrb, long long ld, int c, int grp,
+                                             float (&out)[NV]) {
+#pragma unroll
+  for (int v = 0; v < NV; ++v) out[v] = 0.f;
+  for (int b0 = grp; b0 < nrb; b0 += FG * FU) {
+    float x[FU][NV];
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      const int b = b0 + u * FG;
+      const float* p = ws + ((long long)(b < nrb ? b : 0) * ld + c) * NV;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) x[u][v] = b < nrb ? p[v] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < FU; ++u)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) out[v] += x[u][v];
+  }
+}
 
 __global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restrict__ partial, int M, int C,
                                                           const float* gamma, const float* beta, float* rmean,
@@ -30,10 +54,9 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restri
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
   const int nt = (M + PTILE - 1) / PTILE;
   const bool cv = c < C;
-  float s = 0.f;
-  if (cv)
-    for (int t = grp; t < nt; t += FG) s += partial[((long long)t * C + c) * 2];
-  red[grp][cl] = s;
+  float sq[2] = {0.f, 0.f};
+  if (cv) strided_sums<2>(partial, nt, C, c, grp, sq);
+  red[grp][cl] = sq[0];
   __syncthreads();
   const float n = (float)M;
   float tot = 0.f;
@@ -42,12 +65,28 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restri
   const float mean = tot / n;
   __syncthreads();
   float q = 0.f;
-  if (cv)
-    for (int t = grp; t < nt; t += FG) {
-      const float nb = (float)min(PTILE, M - t * PTILE);
-      const float d = partial[((long long)t * C + c) * 2] / nb - mean;
-      q += partial[((long long)t * C + c) * 2 + 1] + nb * d * d;
+  if (cv) {
+    // second pass over the (L2-resident) partials, FU tiles' loads in flight together
+    for (int t0 = grp; t0 < nt; t0 += FG * FU) {
+      float ps[FU], pq[FU];
+#pragma unroll
+      for (int u = 0; u < FU; ++u) {
+        const int t = t0 + u * FG;
+        const float* p = partial + ((long long)(t < nt ? t : 0) * C + c) * 2;
+        ps[u] = p[0];
+        pq[u] = p[1];
+      }
+#pragma unroll
+      for (int u = 0; u < FU; ++u) {
+        const int t = t0 + u * FG;
+        if (t < nt) {
+          const float nb = (float)min(PTILE, M - t * PTILE);
+          const float d = ps[u] / nb - mean;
+          q += pq[u] + nb * d * d;
+        }
+      }
     }
+  }
   red[grp][cl] = q;
   __syncthreads();
   if (grp != 0 || !cv) return;
@@ -232,14 +271,9 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __re
   __shared__ float red[3][FG][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-  if (c < C)
-    for (int b = grp; b < nrb; b += FG) {
-      const float* p = ws + ((long long)b * C + c) * 3;
-      s0 += p[0];
-      s1 += p[1];
-      s2 += p[2];
-    }
+  float sv[3] = {0.f, 0.f, 0.f};
+  if (c < C) strided_sums<3>(ws, nrb, C, c, grp, sv);
+  float s0 = sv[0], s1 = sv[1], s2 = sv[2];
   red[0][grp][cl] = s0;
   red[1][grp][cl] = s1;
   red[2][grp][cl] = s2;
@@ -357,9 +391,9 @@ __global__ void __launch_bounds__(1024) colsum_final_kernel(const float* __restr
   __shared__ float red[FG][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
-  float s = 0.f;
-  if (c < N)
-    for (int b = grp; b < nrb; b += FG) s += ws[(long long)b * N + c];
+  float sv[1] = {0.f};
+  if (c < N) strided_sums<1>(ws, nrb, N, c, grp, sv);
+  float s = sv[0];
   red[grp][cl] = s;
   __syncthreads();
   if (grp != 0 || c >= N) return;

@@ -232,9 +232,10 @@ bool gemm_nt_launch(const GemmArgs& g, hipStream_t s) {
   int bn = env_cfg(0), nst = env_cfg(1);
   if (bn == 0) return false;
   const long long t128 = (long long)((g.M + BM - 1) / BM) * ((g.N + 127) / 128) * g.batch * g.split_k;
-  // measured (tools/nt_sweep.sh): more resident workgroups beat deeper stages on these shapes,
-  // so 2 stages; 128-wide tiles only when there are >= 4 of them per CU
-  if (bn != 64 && bn != 128) bn = (g.N > 64 && t128 >= 1024) ? 128 : 64;
+  // measured (tools/nt_sweep.sh, tools/gemm_census.py with AVC_NT_CFG): more resident
+  // workgroups beat deeper stages on these shapes, so 2 stages; 128-wide tiles when there are
+  // >= 4 of them per CU, or for long-K wide products (8192x1024x4096: 75 vs 98 us)
+  if (bn != 64 && bn != 128) bn = (g.N > 64 && (t128 >= 1024 || (g.N >= 1024 && g.K >= 2048))) ? 128 : 64;
   if (nst < 2 || nst > 4) nst = 2;
   const int nb = ((g.M + BM - 1) / BM) * ((g.N + bn - 1) / bn) * g.batch * g.split_k;
   const bool win = g.a.win != 0;

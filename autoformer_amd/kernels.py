@@ -31,8 +31,15 @@ def compute_torch_dtype():
     return torch.bfloat16 if _COMPUTE == BF16 else torch.float32
 
 
+_raw_stream = torch._C._cuda_getCurrentRawStream
+_cur_device = torch._C._cuda_getDevice
+
+
 def stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    """Raw handle of torch's current stream on the current device (every launch goes there).
+    The direct C binding: torch.cuda.current_stream() costs ~9 us of Python per call, about
+    1 ms of host time per AutoVC step at ~130 launches."""
+    return _raw_stream(_cur_device())
 
 
 def _ptr(t):
