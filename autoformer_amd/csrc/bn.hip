@@ -175,10 +175,22 @@ __global__ void bn_apply1_kernel(const float* __restrict__ y, const float* __res
 // 256 threads = 16 channel quads (float4, one 256-B row segment) x 16 row lanes; the 4 rows
 // of a lane are loaded together (12 independent 16-B loads in flight per thread).
 constexpr int RB = 64;
+
+// dz = dA * act'(.): from the stored activation output a (FROM_PRE = false) or from the
+// pre-activation z = yhat*gamma + beta recomputed from y (FROM_PRE = true: one fewer
+// activation-sized read in each of the two passes)
+template <bool FROM_PRE>
+__device__ __forceinline__ float bn_dz(float g, float av, float yh, float gm, float bt, int act) {
+  return FROM_PRE ? act_bwd_from_pre(g, yh * gm + bt, act) : act_bwd_from_out(g, av, act);
+}
+
+template <bool FROM_PRE>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const float* __restrict__ dA, const float* __restrict__ a,
                                                             const float* __restrict__ y,
                                                             const float* __restrict__ mean,
-                                                            const float* __restrict__ rstd, int M, int C, int act,
+                                                            const float* __restrict__ rstd,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, int M, int C, int act,
                                                             float* ws) {
   __shared__ float red[3][16][65];
   const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
@@ -188,13 +200,18 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const float* __restr
   if (c < C) {
     const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + c);
     const f32x4 rs = *reinterpret_cast<const f32x4*>(rstd + c);
+    f32x4 gm = {1.f, 1.f, 1.f, 1.f}, bt = {0.f, 0.f, 0.f, 0.f};
+    if (FROM_PRE) {
+      if (gamma) gm = *reinterpret_cast<const f32x4*>(gamma + c);
+      if (beta) bt = *reinterpret_cast<const f32x4*>(beta + c);
+    }
     f32x4 g[4], av[4], yv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = r0 + rl + 16 * i;
       const long long idx = (long long)(r < M ? r : 0) * C + c;
       g[i] = *reinterpret_cast<const f32x4*>(dA + idx);
-      av[i] = *reinterpret_cast<const f32x4*>(a + idx);
+      if (!FROM_PRE) av[i] = *reinterpret_cast<const f32x4*>(a + idx);
       yv[i] = *reinterpret_cast<const f32x4*>(y + idx);
     }
 #pragma unroll
@@ -202,8 +219,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const float* __restr
       if (r0 + rl + 16 * i >= M) continue;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float dz = act_bwd_from_out(g[i][k], av[i][k], act);
         const float yh = (yv[i][k] - mu[k]) * rs[k];
+        const float dz = bn_dz<FROM_PRE>(g[i][k], FROM_PRE ? 0.f : av[i][k], yh, gm[k], bt[k], act);
         s0[k] += dz;
         s1[k] += dz * yh;
         s2[k] += yh;
@@ -230,10 +247,13 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const float* __restr
 }
 
 // scalar variant (C % 4 != 0): 64 channels x 4 row lanes
+template <bool FROM_PRE>
 __global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const float* __restrict__ dA, const float* __restrict__ a,
                                                              const float* __restrict__ y,
                                                              const float* __restrict__ mean,
-                                                             const float* __restrict__ rstd, int M, int C, int act,
+                                                             const float* __restrict__ rstd,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, int M, int C, int act,
                                                              float* ws) {
   __shared__ float red[3][4][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
@@ -242,11 +262,12 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const float* __rest
   float s0 = 0.f, s1 = 0.f, s2 = 0.f;
   if (c < C) {
     const float mu = mean[c], rs = rstd[c];
+    const float gm = (FROM_PRE && gamma) ? gamma[c] : 1.f, bt = (FROM_PRE && beta) ? beta[c] : 0.f;
     const int r1 = min(M, r0 + RB);
     for (int r = r0 + rl; r < r1; r += 4) {
       const long long idx = (long long)r * C + c;
-      const float dz = act_bwd_from_out(dA[idx], a[idx], act);
       const float yh = (y[idx] - mu) * rs;
+      const float dz = bn_dz<FROM_PRE>(dA[idx], FROM_PRE ? 0.f : a[idx], yh, gm, bt, act);
       s0 += dz;
       s1 += dz * yh;
       s2 += yh;
@@ -266,7 +287,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const float* __rest
 
 // one block per 64 channels, 4 row groups reduce the per-block partials in parallel
 __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __restrict__ ws, int nrb, int M, int C,
-                                                               const float* gamma, const float* rstd, float* coef,
+                                                               const float* gamma, const float* beta,
+                                                               const float* mean, const float* rstd, float* coef,
                                                                float* dgamma, float* dbeta, float* dbias, int acc) {
   __shared__ float red[3][FG][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
@@ -287,51 +309,64 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __re
     s2 += red[2][i][cl];
   }
   const float g = gamma ? gamma[c] : 1.f;
-  const float k1 = g * rstd[c];
+  const float rs = rstd[c], mu = mean[c];
+  const float k1 = g * rs;
   const float invn = 1.f / (float)M;
-  coef[c * 3 + 0] = k1;
-  coef[c * 3 + 1] = s0 * invn;
-  coef[c * 3 + 2] = s1 * invn;
+  const float m1 = s0 * invn, m2 = s1 * invn;
+  // planar per-channel constants of the apply pass (one 16-B load per plane per 4 channels):
+  //   yhat = (y - mu)*rs,  z = (y - mu)*k1 + beta,  dy = k1*(dz - m1 - yhat*m2)
+  coef[c] = k1;
+  coef[C + c] = m1;
+  coef[2 * C + c] = m2;
+  coef[3 * C + c] = mu;
+  coef[4 * C + c] = rs;
+  coef[5 * C + c] = beta ? beta[c] : 0.f;
   const float gb = -k1 * s1 * s2 * invn;
   if (dgamma) dgamma[c] = acc ? dgamma[c] + s1 : s1;
   if (dbeta) dbeta[c] = acc ? dbeta[c] + s0 : s0;
   if (dbias) dbias[c] = acc ? dbias[c] + gb : gb;
 }
 
+template <bool FROM_PRE>
 __global__ void bn_bwd_apply_kernel(const float* __restrict__ dA, const float* __restrict__ a,
-                                    const float* __restrict__ y, const float* __restrict__ mean,
-                                    const float* __restrict__ rstd, const float* __restrict__ coef, long long total4,
+                                    const float* __restrict__ y, const float* __restrict__ coef, long long total4,
                                     int C, int act, float* __restrict__ dy, bf16* __restrict__ dy16) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total4) return;
   long long e = i * 4;
   int c = (int)(e % C);
   f32x4 g = *reinterpret_cast<const f32x4*>(dA + e);
-  f32x4 av = *reinterpret_cast<const f32x4*>(a + e);
+  f32x4 av = {0.f, 0.f, 0.f, 0.f};
+  if (!FROM_PRE) av = *reinterpret_cast<const f32x4*>(a + e);
   f32x4 yv = *reinterpret_cast<const f32x4*>(y + e);
+  const f32x4 k1 = *reinterpret_cast<const f32x4*>(coef + c);
+  const f32x4 m1 = *reinterpret_cast<const f32x4*>(coef + C + c);
+  const f32x4 m2 = *reinterpret_cast<const f32x4*>(coef + 2 * C + c);
+  const f32x4 mu = *reinterpret_cast<const f32x4*>(coef + 3 * C + c);
+  const f32x4 rs = *reinterpret_cast<const f32x4*>(coef + 4 * C + c);
+  f32x4 bt = {0.f, 0.f, 0.f, 0.f};
+  if (FROM_PRE) bt = *reinterpret_cast<const f32x4*>(coef + 5 * C + c);
   f32x4 o;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const float* cf = coef + (c + k) * 3;
-    float dz = act_bwd_from_out(g[k], av[k], act);
-    float yh = (yv[k] - mean[c + k]) * rstd[c + k];
-    o[k] = cf[0] * (dz - cf[1] - yh * cf[2]);
+    const float yc = yv[k] - mu[k];
+    const float dz = FROM_PRE ? act_bwd_from_pre(g[k], yc * k1[k] + bt[k], act) : act_bwd_from_out(g[k], av[k], act);
+    o[k] = k1[k] * (dz - m1[k] - yc * rs[k] * m2[k]);
   }
   *reinterpret_cast<f32x4*>(dy + e) = o;
   if (dy16) *reinterpret_cast<bf16x4*>(dy16 + e) = bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
 }
 
+template <bool FROM_PRE>
 __global__ void bn_bwd_apply1_kernel(const float* __restrict__ dA, const float* __restrict__ a,
-                                     const float* __restrict__ y, const float* __restrict__ mean,
-                                     const float* __restrict__ rstd, const float* __restrict__ coef, long long total,
+                                     const float* __restrict__ y, const float* __restrict__ coef, long long total,
                                      int C, int act, float* __restrict__ dy, bf16* __restrict__ dy16) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int c = (int)(i % C);
-  const float* cf = coef + c * 3;
-  const float dz = act_bwd_from_out(dA[i], a[i], act);
-  const float yh = (y[i] - mean[c]) * rstd[c];
-  const float o = cf[0] * (dz - cf[1] - yh * cf[2]);
+  const float yc = y[i] - coef[3 * C + c], k1 = coef[c];
+  const float dz = FROM_PRE ? act_bwd_from_pre(dA[i], yc * k1 + coef[5 * C + c], act) : act_bwd_from_out(dA[i], a[i], act);
+  const float o = k1 * (dz - coef[C + c] - yc * coef[4 * C + c] * coef[2 * C + c]);
   dy[i] = o;
   if (dy16) dy16[i] = (bf16)o;
 }
@@ -445,29 +480,43 @@ extern "C" int avc_bn_apply(const float* y, const float* scale, const float* shi
   return avc_check_launch("avc_bn_apply");
 }
 
-extern "C" size_t avc_bn_bwd_ws(int M, int C) { return (size_t)cdiv(M, RB) * C * 3 + (size_t)C * 3; }
+extern "C" size_t avc_bn_bwd_ws(int M, int C) { return (size_t)cdiv(M, RB) * C * 3 + (size_t)C * 6 + 4; }
 
 extern "C" int avc_bn_bwd(const float* dA, const float* a, const float* y, const float* mean, const float* rstd,
-                          const float* gamma, int M, int C, int act, float* dy, void* dy_bf16, float* dgamma,
-                          float* dbeta, float* dbias, int accumulate, float* ws, void* stream) {
+                          const float* gamma, const float* beta, int M, int C, int act, float* dy, void* dy_bf16,
+                          float* dgamma, float* dbeta, float* dbias, int accumulate, float* ws, void* stream) {
   bf16* d16 = reinterpret_cast<bf16*>(dy_bf16);
-  AVC_CHECK_ARG(dA && a && y && mean && rstd && dy && ws && C > 0, "avc_bn_bwd: bad args");
+  AVC_CHECK_ARG(dA && y && mean && rstd && dy && ws && C > 0, "avc_bn_bwd: bad args");
   hipStream_t s = as_stream(stream);
+  const bool pre = a == nullptr;  // activation derivative from the recomputed pre-activation
   const int nrb = cdiv(M, RB);
   dim3 grid(cdiv(C, 64), nrb);
-  if (C % 4 == 0 && aligned16(dA) && aligned16(a) && aligned16(y)) {
-    bn_bwd_reduce_kernel<<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, M, C, act, ws);
+  const bool v4 = C % 4 == 0 && aligned16(dA) && aligned16(y) && (pre || aligned16(a)) &&
+                  (!gamma || aligned16(gamma)) && (!beta || aligned16(beta));
+  if (v4) {
+    if (pre) bn_bwd_reduce_kernel<true><<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, gamma, beta, M, C, act, ws);
+    else bn_bwd_reduce_kernel<false><<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, gamma, beta, M, C, act, ws);
   } else {
-    bn_bwd_reduce1_kernel<<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, M, C, act, ws);
+    if (pre) bn_bwd_reduce1_kernel<true><<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, gamma, beta, M, C, act, ws);
+    else bn_bwd_reduce1_kernel<false><<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, gamma, beta, M, C, act, ws);
   }
-  float* coef = ws + (size_t)nrb * C * 3;
-  bn_bwd_finalize_kernel<<<cdiv(C, 64), 1024, 0, s>>>(ws, nrb, M, C, gamma, rstd, coef, dgamma, dbeta, dbias,
-                                                       accumulate);
+  // per-channel apply constants, planar [6][C], 16-B aligned
+  const size_t coff = ((size_t)nrb * C * 3 + 3) & ~(size_t)3;
+  float* coef = ws + coff;
+  bn_bwd_finalize_kernel<<<cdiv(C, 64), 1024, 0, s>>>(ws, nrb, M, C, gamma, beta, mean, rstd, coef, dgamma, dbeta,
+                                                       dbias, accumulate);
   const long long total = (long long)M * C;
-  if (C % 4 == 0)
-    bn_bwd_apply_kernel<<<cdiv(total / 4, 256), 256, 0, s>>>(dA, a, y, mean, rstd, coef, total / 4, C, act, dy, d16);
-  else
-    bn_bwd_apply1_kernel<<<cdiv(total, 256), 256, 0, s>>>(dA, a, y, mean, rstd, coef, total, C, act, dy, d16);
+  if (v4) {
+    if (pre)
+      bn_bwd_apply_kernel<true><<<cdiv(total / 4, 256), 256, 0, s>>>(dA, a, y, coef, total / 4, C, act, dy, d16);
+    else
+      bn_bwd_apply_kernel<false><<<cdiv(total / 4, 256), 256, 0, s>>>(dA, a, y, coef, total / 4, C, act, dy, d16);
+  } else {
+    if (pre)
+      bn_bwd_apply1_kernel<true><<<cdiv(total, 256), 256, 0, s>>>(dA, a, y, coef, total, C, act, dy, d16);
+    else
+      bn_bwd_apply1_kernel<false><<<cdiv(total, 256), 256, 0, s>>>(dA, a, y, coef, total, C, act, dy, d16);
+  }
   return avc_check_launch("avc_bn_bwd");
 }
 

@@ -78,6 +78,24 @@ __device__ __forceinline__ float act_bwd_from_out(float g, float a, int act) {
   }
 }
 
+// the same derivatives from the pre-activation z (recomputed as yhat*gamma + beta), so the
+// BatchNorm backward need not read the activation output
+__device__ __forceinline__ float act_bwd_from_pre(float g, float z, int act) {
+  switch (act) {
+    case AVC_ACT_RELU: return z > 0.f ? g : 0.f;
+    case AVC_ACT_TANH: {
+      const float t = tanhf(z);
+      return g * (1.f - t * t);
+    }
+    case AVC_ACT_LEAKY: return z > 0.f ? g : 0.01f * g;
+    case AVC_ACT_SIGMOID: {
+      const float sg = 1.f / (1.f + expf(-z));
+      return g * sg * (1.f - sg);
+    }
+    default: return g;
+  }
+}
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -321,7 +321,9 @@ extern "C" int avc_add(const float* a, const float* b, float* o, long long n, vo
 static int loss_launch(const float* a, const float* b, long long n, float* out, int mode, void* stream) {
   AVC_CHECK_ARG(a && b && out && n > 0, "avc loss: bad args");
   (void)hipMemsetAsync(out, 0, sizeof(float), as_stream(stream));
-  int grid = (int)std::min<long long>(1024, cdiv(n, 256));
+  // 256 blocks: enough loads in flight for the 655 K mel values, and 256 same-word atomicAdds
+  // (≈12 ns each at the L2) instead of 1024
+  int grid = (int)std::min<long long>(256, cdiv(n, 1024));
   loss_kernel<<<grid, 256, 0, as_stream(stream)>>>(a, b, n, out, mode);
   return avc_check_launch("avc loss");
 }

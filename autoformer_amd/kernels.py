@@ -173,8 +173,9 @@ def bn_apply(y, scale, shift, act, residual=None, out=None, twin16=None):
     return attach_twin(out, o16)
 
 
-def bn_bwd(dA, a, y, mean, rstd, gamma, act, need_dbias=True, into=None, twin16=None):
-    """into = (dgamma, dbeta, dbias) buffers to accumulate into (direct gradient sink)."""
+def bn_bwd(dA, a, y, mean, rstd, gamma, act, need_dbias=True, into=None, twin16=None, beta=None):
+    """into = (dgamma, dbeta, dbias) buffers to accumulate into (direct gradient sink).
+    a = None: the activation derivative comes from the pre-activation (y-mean)*rstd*gamma + beta."""
     M, C = y.shape
     dev = y.device
     dy = torch.empty_like(y)
@@ -186,9 +187,9 @@ def bn_bwd(dA, a, y, mean, rstd, gamma, act, need_dbias=True, into=None, twin16=
         dbeta = torch.empty(C, device=dev)
         dbias = torch.empty(C, device=dev) if need_dbias else None
     ws = torch.empty(int(L.lib().avc_bn_bwd_ws(M, C)), device=dev)
-    L.call("avc_bn_bwd", dA.data_ptr(), a.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), _ptr(gamma), M,
-           C, int(act), dy.data_ptr(), _ptr(d16), _ptr(dgamma), _ptr(dbeta), _ptr(dbias), int(into is not None),
-           ws.data_ptr(), stream())
+    L.call("avc_bn_bwd", dA.data_ptr(), _ptr(a), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), _ptr(gamma),
+           _ptr(beta), M, C, int(act), dy.data_ptr(), _ptr(d16), _ptr(dgamma), _ptr(dbeta), _ptr(dbias),
+           int(into is not None), ws.data_ptr(), stream())
     return attach_twin(dy, d16), dgamma, dbeta, dbias
 
 

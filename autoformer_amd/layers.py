@@ -250,7 +250,8 @@ class ConvBNCore:
         M = B * T_out
         sink = _SINK["on"]
         into = (_grad_of(bn.weight), _grad_of(bn.bias), _grad_of(conv.bias)) if sink else None
-        dy, dgamma, dbeta, dbias = K.bn_bwd(dA, a, y, mean, rstd, bn.weight, self.act, into=into)
+        # act' from the recomputed pre-activation: the activation output `a` is not re-read
+        dy, dgamma, dbeta, dbias = K.bn_bwd(dA, None, y, mean, rstd, bn.weight, self.act, into=into, beta=bn.bias)
 
         def wgrad():
             dWf = torch.empty(Co, Kw * Ci, device=x.device)

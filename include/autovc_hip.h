@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 3
+#define AVC_ABI_VERSION 4
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -101,14 +101,17 @@ int avc_bn_stats(const float* y, long long ld, int M, int C, float* partial, voi
 int avc_bn_apply(const float* y, const float* scale, const float* shift, const float* residual,
                  float* out, void* out_bf16, int M, int C, int act, void* stream);
 
-/* BatchNorm1d + activation backward.  dz = dA * act'(a); yhat = (y-mean)*rstd.
+/* BatchNorm1d + activation backward.  yhat = (y-mean)*rstd; dz = dA * act'(.), taken from the
+ * stored activation output `a` when it is given, else (a == NULL) from the pre-activation
+ * yhat*gamma + beta recomputed here (one activation-sized read fewer per pass; also right
+ * when a residual was added after the activation).
  * Writes dy = gamma*rstd*(dz - sum(dz)/N - yhat*sum(dz*yhat)/N), and dgamma, dbeta and
  * the (analytically ~0) bias gradient of the producing conv (accumulate != 0: added into them).
  * `ws` >= avc_bn_bwd_ws floats. */
 size_t avc_bn_bwd_ws(int M, int C);
 int avc_bn_bwd(const float* dA, const float* a, const float* y, const float* mean, const float* rstd,
-               const float* gamma, int M, int C, int act, float* dy, void* dy_bf16, float* dgamma,
-               float* dbeta, float* dbias, int accumulate, float* ws, void* stream);
+               const float* gamma, const float* beta, int M, int C, int act, float* dy, void* dy_bf16,
+               float* dgamma, float* dbeta, float* dbias, int accumulate, float* ws, void* stream);
 
 /* out[n] (+)= sum_m x[m*ld + n] (bias gradients). ws >= avc_colsum_ws floats. */
 size_t avc_colsum_ws(int M, int N);

@@ -167,10 +167,14 @@ def test_bn_stats_epilogue_and_finalize(M, C):
 
 
 @pytest.mark.parametrize("act", [0, 1, 2])
-def test_bn_act_forward_backward(act):
+@pytest.mark.parametrize("from_pre", [False, True])
+@pytest.mark.parametrize("C", [96, 90])
+def test_bn_act_forward_backward(act, from_pre, C):
+    """BN + activation backward; from_pre: act' recomputed from yhat*gamma + beta (a = None),
+    C = 90 takes the scalar (C % 4 != 0) kernels."""
     from autoformer_amd import kernels as Kr
 
-    M, C = 1000, 96
+    M = 1000
     y = torch.randn(M, C) * 2 + 1
     gamma, beta = torch.rand(C) + 0.5, torch.randn(C)
     yt = y.clone().requires_grad_(True)
@@ -185,7 +189,10 @@ def test_bn_act_forward_backward(act):
     mean, rstd, scale, shift = Kr.bn_finalize(part, M, C, gamma.to(DEV), beta.to(DEV), None, None, None, 0.1, 1e-5)
     a = Kr.bn_apply(yd, scale, shift, act)
     assert rinf(a, a_ref.detach()) < 1e-5
-    dy, dgam, dbet, dbias = Kr.bn_bwd(dA.to(DEV), a, yd, mean, rstd, gamma.to(DEV), act)
+    if from_pre:
+        dy, dgam, dbet, dbias = Kr.bn_bwd(dA.to(DEV), None, yd, mean, rstd, gamma.to(DEV), act, beta=beta.to(DEV))
+    else:
+        dy, dgam, dbet, dbias = Kr.bn_bwd(dA.to(DEV), a, yd, mean, rstd, gamma.to(DEV), act)
     assert relf(dy, yt.grad) < 1e-4
     assert relf(dgam, g_t.grad) < 1e-5
     assert relf(dbet, b_t.grad) < 1e-5
