@@ -35,9 +35,11 @@ namespace {
 // in registers; backward: lane (j', q) keeps column j' of gate block q, and the quad's four
 // partial products sum with DPP xor steps, leaving dh_rec[j'] in every lane of the quad.
 // The per-step inputs (xproj rows forward; dh, c, c_prev, gates backward) are staged in LDS
-// one chunk of SC steps ahead: plain loads for chunk k+1 are issued when chunk k starts and
-// written to LDS when it ends; the SC steps of a chunk are unrolled, so no loop boundary
-// makes the compiler drain those loads early.
+// one chunk of SC steps ahead, and the per-step outputs are collected in LDS and written to
+// HBM once per chunk: a step issues no global memory operation at all.  (A global store per
+// step made the next step's reuse of its address registers wait on vmcnt(0) -- for the
+// store AND the whole in-flight prefetch -- every step.)  The SC steps of a chunk are
+// unrolled, so no loop boundary makes the compiler drain the prefetch early.
 constexpr int SC = 16;
 
 __device__ __forceinline__ float fsig(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
@@ -73,6 +75,7 @@ __global__ void __launch_bounds__(256) lstm_small_fwd(const float* __restrict__ 
   const bool act = j < H;
   __shared__ __attribute__((aligned(16))) float hs[2][HM];
   __shared__ float xs[2][SC * GM];
+  __shared__ float gst[SC * GM], hst[SC * HM], cst[SC * HM];  // the chunk's outputs, flushed at its end
   float w[HM];
   const float* W = whh + (long long)d * G * H;
 #pragma unroll
@@ -98,18 +101,39 @@ __global__ void __launch_bounds__(256) lstm_small_fwd(const float* __restrict__ 
       if (e < SC * G) xs[buf][e] = pf[i];
     }
   };
+  // write chunk k's ns steps of gates, h and c from LDS to HBM (coalesced rows)
+  auto flush = [&](int k, int ns) {
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int e = tid + 256 * i, si = e / G;
+      if (si < ns) {
+        const int t = t0 + dt * (k * SC + si);
+        gout[((long long)b * T + t) * ldx + d * G + (e - si * G)] = gst[e];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < (SC * HM + 255) / 256; ++i) {
+      const int e = tid + 256 * i, si = e / H;
+      if (si < ns) {
+        const int t = t0 + dt * (k * SC + si);
+        const long long o = ((long long)b * T + t) * ldh + d * H + (e - si * H);
+        hout[o] = hst[e];
+        cout[o] = cst[e];
+      }
+    }
+  };
   const int nch = (T + SC - 1) / SC;
   issue(0);
   commit(0);
   __syncthreads();
+  if (nch > 1) issue(1);
   for (int k = 0; k < nch; ++k) {
-    if (k + 1 < nch) issue(k + 1);
     const float* xk = xs[k & 1];
     const int ns = min(SC, T - k * SC);
 #pragma unroll
     for (int i = 0; i < SC; ++i) {
       if (i < ns) {
-        const int s = k * SC + i, t = t0 + dt * s;
+        const int s = k * SC + i;
         const f32x4* h4 = reinterpret_cast<const f32x4*>(hs[s & 1]);
         float a0 = act ? xk[i * G + row] : 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
 #pragma unroll
@@ -126,22 +150,24 @@ __global__ void __launch_bounds__(256) lstm_small_fwd(const float* __restrict__ 
         c = fg * c + ig * gg;
         const float h = og * act_tanh<FAST>(c);
         if (act) {
-          const long long o = ((long long)b * T + t) * ldh + d * H + j;
           if (q == 0) {
             hs[(s + 1) & 1][j] = h;
-            hout[o] = h;
+            hst[i * H + j] = h;
           } else if (q == 1) {
-            cout[o] = c;
+            cst[i * H + j] = c;
           }
-          gout[((long long)b * T + t) * ldx + d * G + row] = gv;
+          gst[i * G + row] = gv;
         }
         __syncthreads();
       }
     }
-    if (k + 1 < nch) {
-      commit((k + 1) & 1);
-      __syncthreads();
-    }
+    // chunk end: the steps issued no global memory operation, so nothing above waited on the
+    // prefetch; now commit chunk k+1, then the output stores, then chunk k+2's loads (loads
+    // last: the next step's register reuse then only waits for the stores, vmcnt(NPF))
+    if (k + 1 < nch) commit((k + 1) & 1);
+    flush(k, ns);
+    if (k + 2 < nch) issue(k + 2);
+    __syncthreads();
   }
 }
 
@@ -156,6 +182,7 @@ __global__ void __launch_bounds__(256) lstm_small_bwd(const float* __restrict__ 
   const bool act = j < H;
   __shared__ __attribute__((aligned(16))) float dgs[2][4 * HM];
   __shared__ float rs[2][SC * RM];  // per step: dh | c | c_prev | i f g o
+  __shared__ float dgst[SC * 4 * HM];  // the chunk's dG rows, flushed at its end
   // lane (j, q) holds column j of gate block q: wc[g] = W[q*H + g][j]
   float wc[HM];
   const float* W = whh + (long long)d * G * H;
@@ -200,18 +227,28 @@ __global__ void __launch_bounds__(256) lstm_small_bwd(const float* __restrict__ 
       if (e < SC * R) rs[buf][e] = pf[i];
     }
   };
+  auto flush = [&](int k, int ns) {
+#pragma unroll
+    for (int i = 0; i < (SC * 4 * HM + 255) / 256; ++i) {
+      const int e = tid + 256 * i, si = e / G;
+      if (si < ns) {
+        const int t = t0 + dt * (k * SC + si);
+        dg[((long long)b * T + t) * ldg + d * G + (e - si * G)] = dgst[e];
+      }
+    }
+  };
   const int nch = (T + SC - 1) / SC;
   issue(0);
   commit(0);
   __syncthreads();
+  if (nch > 1) issue(1);
   for (int k = 0; k < nch; ++k) {
-    if (k + 1 < nch) issue(k + 1);
     const float* rk = rs[k & 1];
     const int ns = min(SC, T - k * SC);
 #pragma unroll
     for (int i = 0; i < SC; ++i) {
       if (i < ns) {
-        const int s = k * SC + i, t = t0 + dt * s;
+        const int s = k * SC + i;
         // recurrent part dh_rec[j] = sum_{q', g} dG_{s-1}[q'*H + g] W[q'*H + g][j]: this lane
         // sums gate block q (entries past H meet zero weights), the quad adds the four blocks
         const float* gq = dgs[(s + 1) & 1] + q * H;
@@ -241,15 +278,17 @@ __global__ void __launch_bounds__(256) lstm_small_bwd(const float* __restrict__ 
                                  : dh * tc * og * (1.f - og);
           dc = dcs * fg;
           dgs[s & 1][q * H + j] = v;
-          dg[((long long)b * T + t) * ldg + d * G + q * H + j] = v;
+          dgst[i * G + q * H + j] = v;
         }
         __syncthreads();
       }
     }
-    if (k + 1 < nch) {
-      commit((k + 1) & 1);
-      __syncthreads();
-    }
+    // chunk end, as in the forward: commit the next chunk's inputs, flush this chunk's dG,
+    // then issue the prefetch after next
+    if (k + 1 < nch) commit((k + 1) & 1);
+    flush(k, ns);
+    if (k + 2 < nch) issue(k + 2);
+    __syncthreads();
   }
 }
 
