@@ -256,6 +256,13 @@ def lstm_bwd_timeout_flag(gbuf, B, H):
     return int(gbuf.view(torch.int32)[0].item())
 
 
+# Diagnostics for bench.py's roofline: when this is a list, every persistent backward
+# recurrence launch with H == LAUNCH_TIMING_H appends a (start, end) HIP event pair recorded
+# on the launch stream around it (no synchronisation; read after the timed region).
+LAUNCH_TIMING = None
+LAUNCH_TIMING_H = 1024
+
+
 def lstm_bwd(dh, h, c, g, w_hh, w_hh_t, B, T, H, dirs, gbuf=None):
     """dL/d(pre-activation gates); in the persistent bf16 mode also its bf16 twin."""
     dev = dh.device
@@ -269,8 +276,15 @@ def lstm_bwd(dh, h, c, g, w_hh, w_hh_t, B, T, H, dirs, gbuf=None):
                 gbuf = lstm_bwd_scratch(B, H, dirs, dev)
             if lstm_persistent_bwd(B, H, dirs):
                 dg16 = torch.empty(B * T, 4 * H, device=dev, dtype=torch.bfloat16)
+    timed = LAUNCH_TIMING is not None and dg16 is not None and H == LAUNCH_TIMING_H
+    if timed:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
     L.call("avc_lstm_bwd", dh.data_ptr(), h.data_ptr(), c.data_ptr(), g.data_ptr(), _ptr(w_hh), _ptr(w_hh_t), wdt, B,
            T, H, dirs, dg.data_ptr(), _ptr(dg16), _ptr(dcbuf), _ptr(gbuf), _COMPUTE, stream())
+    if timed:
+        ev[1].record()
+        LAUNCH_TIMING.append(ev)
     return attach_twin(dg, dg16)
 
 
