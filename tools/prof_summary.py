@@ -1,3 +1,8 @@
+"""Top kernels of a rocprofv3 --stats kernel_stats.csv.  The optional divisor is the number of
+train steps the profiled command ran (warm-up + timed), to print per-step figures.
+
+  python tools/prof_summary.py <run_kernel_stats.csv> [steps] [top]
+"""
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 div = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
