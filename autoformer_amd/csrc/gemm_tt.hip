@@ -195,6 +195,155 @@ void launch(const GemmArgs& g, int nblocks, hipStream_t s) {
 
 bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// ------------------------------------------------------------------ halo form of the conv dW
+// dW[co][tap*Ci + ci] = sum_f dy[f][co] . x[f + tap - pad][ci] for a 5-tap 'same' Conv1d whose
+// utterance length is a multiple of the 64-frame K-tile (so a K-tile never spans utterances).
+// The window operand above fetches a 64 x 128 tile of x per (tap, 128-channel) column block --
+// five copies of the same rows shifted by one.  Here a workgroup owns 128 output channels x
+// (5 taps x 32 input channels): per K-tile it stages the dy tile (64 x 128, as above) and ONE
+// x halo tile of 68 frames x 32 channels (64-B rows), and tap k reads the halo k rows down.
+// Halo rows outside the tile's utterance are loaded as zeros, which is exactly the conv
+// padding.  Transposed reads (ds_read_b64_tr_b16) of the 64-B rows use the chunk swizzle
+// chunk ^ ((row >> 2) & 2): the two 16-lane groups of a half read rows 8 apart, which then
+// take the two different 32-B halves of the row -- conflict-free.
+constexpr int HROW = 64;                 // bytes per halo row (32 channels)
+constexpr int HROWS = 128;               // halo rows reserved: 2 glds of 16 rows per wave
+constexpr int HB_BYTES = HROWS * HROW;   // 8 KiB
+constexpr int HSTAGE = TSTAGE_OP + HB_BYTES;
+
+__device__ __forceinline__ int hswz(int row) { return (row >> 2) & 2; }
+
+__device__ __forceinline__ bf16x8 tr_frag_h(const char* tile, int rlo, int chunk0, int p) {
+  const int rhi = rlo + 4;
+  const int olo = rlo * HROW + 16 * ((chunk0 + (p >> 1)) ^ hswz(rlo)) + 8 * (p & 1);
+  const int ohi = rhi * HROW + 16 * ((chunk0 + (p >> 1)) ^ hswz(rhi)) + 8 * (p & 1);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(tile + olo));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(tile + ohi));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int NST>
+__global__ void __launch_bounds__(256, 2) gemm_tt_halo_kernel(GemmArgs g) {
+  constexpr int TAPS = 5, CW = 32, P = NST - 1, LPT = 6;  // glds per thread per K-tile: 4 dy + 2 halo
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
+  const int lid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (bid >> 3);
+  const OpDev& X = g.b;
+  const int chans = X.chans, pad = X.pad, T = X.t_out;
+  const int nC = chans / CW, nM = (g.M + BM - 1) / BM;
+  const int ks = lid / (nC * nM);
+  const int rem = lid - ks * nC * nM;
+  const int mt = rem / nC, ct = rem - mt * nC;
+  const int m0 = mt * BM, c0 = ct * CW;
+  const int kbeg = ks * g.klen;
+  const int kend = min(g.K, kbeg + g.klen);
+  const int nkt = kend > kbeg ? (kend - kbeg + FBK - 1) / FBK : 0;
+
+  TtLoader<false> la;
+  la.init(g.a, m0, 0);
+  // halo loader: instruction i (0, 1) of wave w writes rows 16*(2w + i) + (lane >> 2), slot lane & 3
+  const bf16* xb = reinterpret_cast<const bf16*>(X.ptr);
+  const long long ldx = X.ld;
+  int hrow[2], hchk[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    hrow[i] = 16 * (2 * wid + i) + (lane >> 2);
+    hchk[i] = 8 * ((lane & 3) ^ hswz(hrow[i]));
+  }
+  auto issue_halo = [&](char* tile, int f0) {
+    const int u0 = (f0 / T) * T;  // the K-tile's utterance: frames [u0, u0 + T)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int f = f0 - pad + hrow[i];
+      const bool ok = hrow[i] < FBK + TAPS - 1 && f >= u0 && f < u0 + T && f < g.K;
+      const void* src = ok ? (const void*)(xb + (long long)f * ldx + c0 + hchk[i]) : (const void*)g_zero16_tt;
+      glds16(src, tile + (2 * wid + i) * 1024);
+    }
+  };
+
+  f32x4 acc[4][TAPS];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < TAPS; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int ao0[4], ao1[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) tr_offsets(wm * 8 + 2 * i, ao0[i], ao1[i]);
+  const int grp = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+    if (p < nkt) {
+      la.issue(smem_raw + p * HSTAGE, kbeg + p * FBK, kend);
+      issue_halo(smem_raw + p * HSTAGE + TSTAGE_OP, kbeg + p * FBK);
+    }
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int ahead = min(P - 1, nkt - 1 - kt);  // K-tiles allowed to stay in flight
+    if constexpr (P >= 2) {
+      if (ahead >= 1) wait_vm<LPT>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    raw_barrier();
+    if (kt + P < nkt) {
+      char* st = smem_raw + ((kt + P) % NST) * HSTAGE;
+      la.issue(st, kbeg + (kt + P) * FBK, kend);
+      issue_halo(st + TSTAGE_OP, kbeg + (kt + P) * FBK);
+    }
+    const char* As = smem_raw + (kt % NST) * HSTAGE;
+    const char* Hs = As + TSTAGE_OP;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = tr_frag(As + h * 32 * TROW, ao0[i], ao1[i]);
+#pragma unroll
+      for (int k = 0; k < TAPS; ++k) {
+        const bf16x8 bfr = tr_frag_h(Hs, h * 32 + 8 * grp + qq + k, 2 * wn, pp);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][k], 0, 0, 0);
+      }
+    }
+  }
+  // epilogue: row m0 + wm*64 + 16i + 4*(lane>>4) + e, column tap*chans + c0 + 16*wn + (lane & 15)
+  const int rbase = m0 + wm * 64 + 4 * (lane >> 4);
+  const int cl = c0 + 16 * wn + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = rbase + i * 16 + e;
+      if (row >= g.M) continue;
+#pragma unroll
+      for (int k = 0; k < TAPS; ++k) {
+        float* cp = g.c + (long long)row * g.ldc + k * chans + cl;
+        const float v = acc[i][k][e];
+        if (g.atomic) atomicAdd(cp, v);
+        else *cp = g.accumulate ? *cp + v : v;
+      }
+    }
+}
+
+template <int NST>
+void launch_halo(const GemmArgs& g, hipStream_t s) {
+  const size_t lds = NST * (size_t)HSTAGE;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tt_halo_kernel<NST>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const int nb = ((g.M + BM - 1) / BM) * (g.b.chans / 32) * g.split_k;
+  gemm_tt_halo_kernel<NST><<<nb, 256, lds, s>>>(g);
+}
+
 }  // namespace
 
 bool gemm_tt_launch(const GemmArgs& g, hipStream_t s) {
@@ -204,6 +353,16 @@ bool gemm_tt_launch(const GemmArgs& g, hipStream_t s) {
     if (o->dtype != AVC_BF16 || !ok16(o->ptr) || o->ld % 8 || o->bstride % 8) return false;
   if (g.a.win) return false;
   if (g.b.win && g.b.chans % 8) return false;
+  // AVC_TT_HALO: 0 = off (window stream), 2 / 3 = LDS stages of the halo kernel
+  static const int halo = getenv("AVC_TT_HALO") ? atoi(getenv("AVC_TT_HALO")) : 2;
+  const bool halo_off = halo == 0;
+  const OpDev& x = g.b;
+  if (!halo_off && x.win && x.taps == 5 && x.t_in == x.t_out && 2 * x.pad == x.taps - 1 && x.chans % 32 == 0 &&
+      x.t_out % FBK == 0 && g.batch == 1 && g.N == x.taps * x.chans && !g.res && !g.c16 && !g.bias) {
+    if (halo == 2) launch_halo<2>(g, s);
+    else launch_halo<3>(g, s);
+    return true;
+  }
   const int nb = ((g.M + BM - 1) / BM) * ((g.N + 127) / 128) * g.batch * g.split_k;
   if (g.b.win) launch<true>(g, nb, s);
   else launch<false>(g, nb, s);

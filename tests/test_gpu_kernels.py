@@ -465,8 +465,13 @@ def test_gemm_tt_lds_transposed_reads(M, N, K, split):
     assert relf(c, ref) < 1e-5, relf(c, ref)
 
 
-@pytest.mark.parametrize("B,T,Cin,Cout,Kw,pad", [(4, 37, 64, 96, 5, 2), (64, 128, 512, 512, 5, 2), (3, 20, 88, 176, 3, 1)])
-def test_gemm_tt_conv_weight_gradient_window(B, T, Cin, Cout, Kw, pad):
+@pytest.mark.parametrize("B,T,Cin,Cout,Kw,pad", [(4, 37, 64, 96, 5, 2), (64, 128, 512, 512, 5, 2), (3, 20, 88, 176, 3, 1),
+                                                 (3, 64, 96, 80, 5, 2), (2, 192, 32, 200, 5, 2)])
+@pytest.mark.parametrize("split", ["auto", 1])
+def test_gemm_tt_conv_weight_gradient_window(B, T, Cin, Cout, Kw, pad, split):
+    """Conv dW through the TT kernel.  5-tap 'same' convs with T % 64 == 0 and Cin % 32 == 0 take
+    the halo form (one x tile for all taps; utterance edges zero-filled at load), the others the
+    window stream; split-K (atomics) and single-pass (plain stores) epilogues."""
     import autoformer_amd as A
     from autoformer_amd import kernels as Kr
 
@@ -478,7 +483,7 @@ def test_gemm_tt_conv_weight_gradient_window(B, T, Cin, Cout, Kw, pad):
     c = torch.empty(M, N, device=DEV)
     Kr.gemm(M, N, B * T, Kr.operand(dy.to(DEV), Cout, kstrided=True),
             Kr.operand(x.to(DEV), Cin, kstrided=True, window=(Kw, pad, T, T, Cin)), c,
-            split_k=Kr.auto_split_k(M, N, B * T))
+            split_k=Kr.auto_split_k(M, N, B * T) if split == "auto" else split)
     assert relf(c, ref) < 1e-5, relf(c, ref)
 
 
