@@ -162,29 +162,33 @@ __global__ void __launch_bounds__(256, 2) gemm_conv_kernel(GemmArgs g) {
     raw_barrier();
     if (cs + P < nst) issue((cs + P) % NST, cs + P);
     const char* st = smem_raw + (cs % NST) * STAGE;
+    // fragments of tap k+1 are read while tap k's MFMAs run (two register sets), so the LDS
+    // latency is exposed once per stage rather than once per tap
+    bf16x8 af[2][4], bfr[2][NJ];
+    auto read_tap = [&](int k, int kb, int slot) {
+      const int cc = 4 * kb + ch;  // this lane's 16-B chunk of K block kb
 #pragma unroll
-    for (int k = 0; k < TAPS; ++k) {
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-        bf16x8 af[4], bfr[NJ];
-        const int cc = 4 * kb + ch;  // this lane's 16-B chunk of K block kb
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = arow[i] + k;
-          const bf16x8 v = *reinterpret_cast<const bf16x8*>(st + r * ROW + 16 * (cc ^ C::swz(r)));
-          af[i] = ((vmask >> (i * 8 + k)) & 1u) ? v : bf16x8{};
-        }
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int r = k * CBN + brow[j];
-          bfr[j] = *reinterpret_cast<const bf16x8*>(st + C::A_BYTES + r * ROW + 16 * (cc ^ C::swz(r)));
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < 4; ++i) {
+        const int r = arow[i] + k;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(st + r * ROW + 16 * (cc ^ C::swz(r)));
+        af[slot][i] = ((vmask >> (i * 8 + k)) & 1u) ? v : bf16x8{};
       }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int r = k * CBN + brow[j];
+        bfr[slot][j] = *reinterpret_cast<const bf16x8*>(st + C::A_BYTES + r * ROW + 16 * (cc ^ C::swz(r)));
+      }
+    };
+    read_tap(0, 0, 0);
+#pragma unroll
+    for (int kk = 0; kk < TAPS * KB; ++kk) {
+      const int slot = kk & 1;
+      if (kk + 1 < TAPS * KB) read_tap((kk + 1) / KB, (kk + 1) % KB, slot ^ 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[slot][i], bfr[slot][j], acc[i][j], 0, 0, 0);
     }
   }
   __syncthreads();  // last wait was vmcnt(0); every fragment read done before the epilogue reuses LDS

@@ -301,15 +301,18 @@ __global__ void __launch_bounds__(256, 2) gemm_tt_halo_kernel(GemmArgs g) {
     const char* Hs = As + TSTAGE_OP;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      bf16x8 af[4];
+      // all 18 fragment reads of the K-half in flight before the 20 MFMAs: one LDS latency
+      // per K-half instead of one per tap
+      bf16x8 af[4], bfr[TAPS];
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = tr_frag(As + h * 32 * TROW, ao0[i], ao1[i]);
 #pragma unroll
-      for (int k = 0; k < TAPS; ++k) {
-        const bf16x8 bfr = tr_frag_h(Hs, h * 32 + 8 * grp + qq + k, 2 * wn, pp);
+      for (int k = 0; k < TAPS; ++k) bfr[k] = tr_frag_h(Hs, h * 32 + 8 * grp + qq + k, 2 * wn, pp);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][k], 0, 0, 0);
-      }
+      for (int k = 0; k < TAPS; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[k], acc[i][k], 0, 0, 0);
     }
   }
   // epilogue: row m0 + wm*64 + 16i + 4*(lane>>4) + e, column tap*chans + c0 + 16*wn + (lane & 15)
