@@ -145,7 +145,15 @@ __global__ void __launch_bounds__(256) lstm_small_fwd(const float* __restrict__ 
           a3 += hv[3] * w[4 * kq + 3];
         }
         const float pre = (a0 + a1) + (a2 + a3);
-        const float gv = q == 2 ? act_tanh<FAST>(pre) : act_sig<FAST>(pre);
+        // FAST: tanh(x) = 2*sig(2x) - 1 is exactly how ftanh is formed, so the gate lanes of a
+        // quad share one exp + rcp with no divergent branch (bit-identical to the branch form)
+        float gv;
+        if (FAST) {
+          const float sg = fsig((q == 2 ? 2.f : 1.f) * pre);
+          gv = q == 2 ? 2.f * sg - 1.f : sg;
+        } else {
+          gv = q == 2 ? act_tanh<FAST>(pre) : act_sig<FAST>(pre);
+        }
         const float ig = quad_bcast<0>(gv), fg = quad_bcast<1>(gv), gg = quad_bcast<2>(gv), og = quad_bcast<3>(gv);
         c = fg * c + ig * gg;
         const float h = og * act_tanh<FAST>(c);
