@@ -12,6 +12,7 @@ per training step.
 """
 from __future__ import annotations
 
+import os
 import weakref
 
 import torch
@@ -20,6 +21,7 @@ from . import kernels as K
 from .kernels import operand
 
 _EPOCH = [0]
+_LAST_WGRAD_MAIN = os.environ.get("AVC_LAST_WGRAD_MAIN", "1") != "0"
 
 # ---------------------------------------------------------------- gradient sink / side stream
 # In "sink" mode (set by TrainStep) parameter gradients are accumulated by the kernels
@@ -266,10 +268,16 @@ class ConvBNCore:
             dx = torch.empty(B * T_in, n_dx, device=x.device)
             K.gemm(B * T_in, n_dx, Kw * Co, operand(dy, Co, window=(Kw, Kw - 1 - self.pad, T_in, T_out, Co)),
                    operand(Wd, Kw * Co), dx)
-        if sink:
+        if sink and (n_dx or not _LAST_WGRAD_MAIN):
             with _Side(ev) as sd:
                 sd.keep(dy, x)
                 wgrad()
+            dW = dgamma = dbeta = dbias = None
+        elif sink:
+            # no data gradient: this is the last layer of the backward (the encoder's first
+            # conv), after which the main stream would only wait for the side stream -- its
+            # weight gradient runs here, beside the side stream's remaining backlog
+            wgrad()
             dW = dgamma = dbeta = dbias = None
         else:
             dW = wgrad()
