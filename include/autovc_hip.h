@@ -227,6 +227,30 @@ int avc_transpose_batched(const float* src, float* dst, int B, int R, int C, int
 int avc_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
              float beta2, float eps, float* state, void* stream);
 
+/* AdaIN / speaker-embedding-adjust variants (variants.hip).
+ * Whole-tensor moments of x.mean(), x.std() (unbiased) — factory/AutoVC2.py:58-60,
+ * factory/Norm.py:84-91 — as out = [mean, std] (device).  ws >= avc_moments_ws() doubles. */
+size_t avc_moments_ws(void);
+int avc_moments(const float* x, long long n, double* ws, float* out, void* stream);
+/* dx = dmean/n + dstd*(x - mean)/((n-1) std) (+ acc); dmean / dstd / acc nullable (device). */
+int avc_moments_bwd(const float* x, long long n, const float* mom, const float* dmean, const float* dstd,
+                    const float* acc, float* dx, void* stream);
+/* AdaIN (Norm.py:84-91): y = (x - mom[0]) / mom[1] * sigma + mu; mom from avc_moments(x). */
+int avc_adain_fwd(const float* x, long long n, const float* mom, const float* mu, const float* sigma, float* y,
+                  void* stream);
+/* AdaIN backward: dx, dmu = sum g, dsigma = sum g*xhat (sums: 2 floats scratch). */
+int avc_adain_bwd(const float* g, const float* x, long long n, const float* mom, const float* sigma, double* ws,
+                  float* sums, float* dx, float* dmu, float* dsigma, void* stream);
+/* out[b][c] (+)= sum_t x[(b*T + t)*ld + c]: the gradient of a speaker embedding broadcast
+ * over time into a concat (AutoVC_Adjust.py:178-189 trains it through Adjust). */
+int avc_segsum(const float* x, long long ld, int B, int T, int C, float* out, int accumulate, void* stream);
+/* scatter = 0: dst[b][c] = src[(b*T + t)*C + c] (nn.LSTM output [:, t, :], Adjust.py:39);
+ * scatter = 1: dst (B*T x C) = that step's gradient, zero elsewhere. */
+int avc_step_select(const float* src, float* dst, int B, int T, int t, int C, int scatter, void* stream);
+/* Row L2 normalisation (Adjust.py:40-42) and its backward dx = (dy - y (y.dy)) / norm. */
+int avc_rownorm_fwd(const float* x, int R, int C, float* y, float* norms, void* stream);
+int avc_rownorm_bwd(const float* dy, const float* y, const float* norms, int R, int C, float* dx, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

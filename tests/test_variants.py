@@ -1,0 +1,211 @@
+"""AdaIN ("2") and speaker-embedding-adjust ("_Adjust") variants.
+
+CPU: the oracle restatement (oracle/variants_cpu.py) against the goldens made from the
+reference modules by tests/golden/make_variant_goldens.py — state_dict layout, one training
+step (outputs, losses, gradients, BN running stats), the conversion forwards.
+GPU: the drop-in modules (factory.<Variant>) in fp32 parity mode against the same goldens,
+and the HIP moment / AdaIN / rownorm / segsum kernels against plain PyTorch fp32.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import autovc_cpu as A
+from oracle import variants_cpu as V
+
+from .conftest import GOLDEN
+from .helpers import bn_state_mismatches, grad_mismatches, rel_inf
+
+torch.set_num_threads(min(8, os.cpu_count() or 1))
+
+NAMES = ["AutoVC2", "AutoVC_Adjust", "MetaConv2", "MetaPool2", "MetaConv_Adjust", "MetaPool_Adjust"]
+CPU_NAMES = NAMES
+
+
+def _golden(name):
+    return np.load(os.path.join(GOLDEN, f"variant_{name}.npz"))
+
+
+def _oracle_fwd(name, sd, freq):
+    if name.endswith("_Adjust"):
+        return lambda x, c, t, **kw: V.adjust_forward(name, sd, x, c, t, freq=freq, **kw)
+    return lambda x, c, t, **kw: V.adain_forward(name, sd, x, c, t, freq=freq, **kw)
+
+
+def _step(name, fwd, x, e):
+    if name.endswith("_Adjust"):
+        losses, total, outs = V.adjust_step_losses(fwd, x, e)
+        return losses, total, outs[1:], outs[0]
+    losses, total, outs = V.adain_step_losses(fwd, x, e)
+    return losses, total, outs, None
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_variant_spec_matches_reference_layout(name):
+    g = _golden(name)
+    assert list(V.SPECS[name]().keys()) == [str(k) for k in g["keys"]]
+
+
+@pytest.mark.parametrize("name", CPU_NAMES)
+def test_variant_oracle_step(name):
+    g = _golden(name)
+    freq = int(g["freq"])
+    sd = A.make_state(V.SPECS[name]())
+    x, e = torch.from_numpy(g["x"]), torch.from_numpy(g["emb"])
+    losses, total, outs, emb_adj = _step(name, _oracle_fwd(name, sd, freq), x, e)
+    total.backward()
+    for key, t in zip(("step_mel", "step_mel_psnt", "step_codes", "step_codes_re"), outs):
+        assert rel_inf(t.detach().numpy(), g[key]) < 1e-5, key
+    if emb_adj is not None:
+        assert rel_inf(emb_adj.detach().numpy(), g["step_emb_adj"]) < 1e-5
+    np.testing.assert_allclose([v.item() for v in losses], g["step_losses"], rtol=1e-5)
+    for k, t in sd.items():
+        if t.requires_grad:
+            gn = float(g["step_gnorm/" + k])
+            ours = t.grad.norm().item()
+            assert abs(ours - gn) <= 1e-3 * gn + 1e-6, (k, ours, gn)
+            head = t.grad.reshape(-1)[:64].numpy()
+            ref = g["step_ghead/" + k]
+            assert np.abs(head - ref).max() <= 1e-3 * max(np.abs(ref).max(), 1e-3), k
+        elif "running" in k or "num_batches" in k:
+            np.testing.assert_allclose(t.numpy(), g["step_bn/" + k], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", CPU_NAMES)
+def test_variant_oracle_conversion(name):
+    g = _golden(name)
+    freq = int(g["freq"])
+    sd = A.make_state(V.SPECS[name]())
+    x, e, x2, e2 = (torch.from_numpy(g[k]) for k in ("x", "emb", "x2", "emb2"))
+    fwd = _oracle_fwd(name, sd, freq)
+    with torch.no_grad():
+        if name.endswith("_Adjust"):
+            c_adj, mel, psnt, codes = fwd(x, e, e2, isConvert=True, x_target=x2)
+            assert rel_inf(c_adj.numpy(), g["conv_emb_adj"]) < 1e-5
+        else:
+            tf = [[torch.tensor(a), torch.tensor(b)] for a, b in g["conv_target_feature"]]
+            mel, psnt, codes = fwd(x, e, e2, target_feature=tf)
+            _, feats = fwd(x, e, None)
+            np.testing.assert_allclose(np.array([[float(a), float(b)] for a, b in feats]), g["feats"], rtol=1e-5)
+    assert rel_inf(mel.numpy(), g["conv_mel"]) < 1e-5
+    assert rel_inf(psnt.numpy(), g["conv_mel_psnt"]) < 1e-5
+    assert rel_inf(codes.numpy(), g["conv_codes"]) < 1e-5
+
+
+# =============================================================================== GPU
+def _variant_model(name, dev):
+    import importlib
+
+    import autoformer_amd as AA
+    from autoformer_amd.detinit import det_init_
+
+    AA.set_compute("fp32")
+    cls = getattr(importlib.import_module(f"factory.{name}"), name)
+    m = cls(44, 256, 512, 22)
+    det_init_(m)
+    return m.to(dev).train()
+
+
+def _variant_bn_fed_bias(n):
+    # conv biases that feed a training-mode BatchNorm: analytically zero gradient
+    return "conv.bias" in n and "feature_last_combine" not in n and "postnet.convolutions.4" not in n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_gpu_variant_step_matches_reference(name):
+    dev = torch.device("cuda:0")
+    g = _golden(name)
+    m = _variant_model(name, dev)
+    x, e = (torch.from_numpy(g[k]).to(dev) for k in ("x", "emb"))
+    losses, total, outs, emb_adj = _step(name, lambda a, b, c, **kw: m(a, b, c, **kw), x, e)
+    m.zero_grad()
+    total.backward()
+    torch.cuda.synchronize()
+    for key, t in zip(("step_mel", "step_mel_psnt", "step_codes", "step_codes_re"), outs):
+        assert rel_inf(t.detach().cpu().numpy(), g[key]) < 1e-3, key
+    if emb_adj is not None:
+        assert rel_inf(emb_adj.detach().cpu().numpy(), g["step_emb_adj"]) < 1e-3
+    np.testing.assert_allclose([v.item() for v in losses], g["step_losses"], rtol=1e-4)
+    bad = grad_mismatches(m, {k[5:]: g[k] for k in g.files if k.startswith("step_g")},
+                          bn_fed_bias=_variant_bn_fed_bias)
+    assert not bad, bad
+    assert not bn_state_mismatches(m, {k[5:]: g[k] for k in g.files if k.startswith("step_bn/")})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_gpu_variant_conversion_matches_reference(name):
+    dev = torch.device("cuda:0")
+    g = _golden(name)
+    m = _variant_model(name, dev)
+    x, e, x2, e2 = (torch.from_numpy(g[k]).to(dev) for k in ("x", "emb", "x2", "emb2"))
+    with torch.no_grad():
+        if name.endswith("_Adjust"):
+            c_adj, mel, psnt, codes = m(x, e, e2, isConvert=True, x_target=x2)
+            assert rel_inf(c_adj.cpu().numpy(), g["conv_emb_adj"]) < 1e-3
+        else:
+            tf = [[torch.tensor(a, device=dev), torch.tensor(b, device=dev)] for a, b in g["conv_target_feature"]]
+            mel, psnt, codes = m(x, e, e2, target_feature=tf)
+            m2 = _variant_model(name, dev)
+            _, feats = m2(x, e, None)
+            np.testing.assert_allclose(np.array([[float(a), float(b)] for a, b in feats]), g["feats"], rtol=1e-4)
+    assert rel_inf(mel.cpu().numpy(), g["conv_mel"]) < 1e-3
+    assert rel_inf(psnt.cpu().numpy(), g["conv_mel_psnt"]) < 1e-3
+    assert rel_inf(codes.cpu().numpy(), g["conv_codes"]) < 1e-3
+
+
+@pytest.mark.gpu
+def test_gpu_moment_kernels_match_torch():
+    from autoformer_amd import variants as VV
+
+    dev = torch.device("cuda:0")
+    gen = torch.Generator().manual_seed(7)
+    for n_rows in (1, 37, 2 * 176):
+        x = (torch.randn(n_rows, 80, generator=gen) * 1.7 - 2.5).to(dev).requires_grad_(True)
+        mu = torch.tensor(0.3, device=dev, requires_grad=True)
+        sd = torch.tensor(1.9, device=dev, requires_grad=True)
+        w = torch.randn(n_rows, 80, generator=gen).to(dev)
+        mom = VV.moments(x)
+        y = VV.adain(x, mu, sd)
+        loss = (y * w).sum() + 0.7 * mom[0] - 1.3 * mom[1]
+        loss.backward()
+        gx, gmu, gsd = x.grad.clone(), mu.grad.clone(), sd.grad.clone()
+        x.grad = mu.grad = sd.grad = None
+        xr = x.detach().double().requires_grad_(True)
+        mur, sdr = mu.detach().double().requires_grad_(True), sd.detach().double().requires_grad_(True)
+        yr = (xr - xr.mean()) / xr.std() * sdr + mur
+        lr = (yr * w.double()).sum() + 0.7 * xr.mean() - 1.3 * xr.std()
+        lr.backward()
+        assert rel_inf(y.detach().cpu(), yr.detach().cpu()) < 1e-5
+        assert abs(mom[0].item() - xr.mean().item()) < 1e-5 and abs(mom[1].item() - xr.std().item()) < 1e-5
+        assert rel_inf(gx.cpu(), xr.grad.cpu()) < 1e-4
+        assert abs(gmu.item() - mur.grad.item()) <= 1e-4 * abs(mur.grad.item()) + 1e-4
+        assert abs(gsd.item() - sdr.grad.item()) <= 1e-4 * abs(sdr.grad.item()) + 1e-4
+
+
+@pytest.mark.gpu
+def test_gpu_rownorm_step_select_segsum_match_torch():
+    from autoformer_amd import kernels as K
+    from autoformer_amd import variants as VV
+
+    dev = torch.device("cuda:0")
+    gen = torch.Generator().manual_seed(11)
+    B, T, C = 3, 19, 70
+    h = torch.randn(B * T, C, generator=gen).to(dev).requires_grad_(True)
+    last = VV.step_select(h, B, T, T - 1)
+    e = VV.rownorm(last)
+    w = torch.randn(B, C, generator=gen).to(dev)
+    (e * w).sum().backward()
+    hr = h.detach().double().requires_grad_(True)
+    lr = hr.view(B, T, C)[:, -1, :]
+    er = lr / lr.norm(dim=-1, keepdim=True)
+    (er * w.double()).sum().backward()
+    assert rel_inf(e.detach().cpu(), er.detach().cpu()) < 1e-6
+    assert rel_inf(h.grad.cpu(), hr.grad.cpu()) < 1e-5
+    x = torch.randn(B * T, 336, generator=gen).to(dev)
+    out = K.segsum(x[:, 80:], B, T, 256, ld=336)
+    ref = x.view(B, T, 336)[:, :, 80:].double().sum(1)
+    assert rel_inf(out.cpu(), ref.cpu()) < 1e-5
