@@ -50,6 +50,10 @@ class Encoder(nn.Module):
 
     def codes_flat(self, x, c_org):
         mel, B, T = _frames(x)
+        return self.codes_frames(mel, c_org, B, T)
+
+    def codes_frames(self, mel, c_org, B, T):
+        """Frame-major mel (B*T, 80) -> codes (B, T/freq * 2*dim_neck)."""
         if T % self.freq:
             # the reference indexes out_forward[:, i + freq - 1] past T here (AutoVC.py:63)
             raise IndexError(f"len_crop {T} is not a multiple of freq {self.freq}")
@@ -130,14 +134,24 @@ class AutoVC(nn.Module):
         codes = self.encoder.codes_flat(x, c_org)
         if c_trg is None:
             return codes
-        xs = x.squeeze(1) if x.dim() == 4 else x
-        B, T = xs.shape[0], xs.shape[1]
-        cd = 2 * self.dim_neck
-        enc_out = Lyr.dec_concat(codes, c_trg.contiguous(), B, T, codes.shape[1] // cd, cd)
-        hook = getattr(self, "_decoder_bwd_done", None)
-        if hook is not None and enc_out.requires_grad:
-            # fires once the backward has produced every decoder / postnet gradient
-            enc_out.register_hook(lambda g: hook())
-        mel = self.decoder.frames(enc_out, B, T)
-        mel_postnet = self.postnet.frames(mel, B, T, residual=mel)
-        return mel.view(B, 1, T, -1), mel_postnet.view(B, 1, T, -1), codes
+        return decode(self, x, codes, c_trg)
+
+
+def decode(model, x, codes, c_trg, features=None):
+    """Code expansion + c_trg concat, decoder, postnet (+ residual) (AutoVC.py:197-211);
+    shared by every model family and variant.  `features`: the AdaIN postnet's statistics
+    (AutoVC2.py:231-237)."""
+    xs = x.squeeze(1) if x.dim() == 4 else x
+    B, T = xs.shape[0], xs.shape[1]
+    cd = 2 * model.dim_neck
+    enc_out = Lyr.dec_concat(codes, c_trg.contiguous(), B, T, codes.shape[1] // cd, cd)
+    hook = getattr(model, "_decoder_bwd_done", None)
+    if hook is not None and enc_out.requires_grad:
+        # fires once the backward has produced every decoder / postnet gradient
+        enc_out.register_hook(lambda g: hook())
+    mel = model.decoder.frames(enc_out, B, T)
+    if features is None:
+        mel_postnet = model.postnet.frames(mel, B, T, residual=mel)
+    else:
+        mel_postnet = model.postnet.frames(mel, B, T, features, residual=mel)
+    return mel.view(B, 1, T, -1), mel_postnet.view(B, 1, T, -1), codes

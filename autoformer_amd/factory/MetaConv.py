@@ -12,7 +12,7 @@ import torch.nn as nn
 from .. import kernels as K
 from .. import layers as Lyr
 from .. import metaformer as MF
-from .AutoVC import Postnet, _frames
+from .AutoVC import Postnet, _frames, decode
 from .MLPMixer import MLPMixer
 from .Norm import ConvNorm, GroupNorm, LinearNorm, PatchEmbed
 
@@ -77,6 +77,9 @@ class Encoder(nn.Module):
 
     def codes_flat(self, x, c_org):
         mel, B, T = _frames(x)
+        return self.codes_frames(mel, c_org, B, T)
+
+    def codes_frames(self, mel, c_org, B, T):
         if T % self.freq:
             raise IndexError(f"len_crop {T} is not a multiple of freq {self.freq}")
         h = MF.enc_embed(mel, c_org.contiguous(), self.embding.proj, self._emb, B, T)
@@ -139,14 +142,4 @@ class MetaConv(nn.Module):
         codes = self.encoder.codes_flat(x, c_org)
         if c_trg is None:
             return codes
-        xs = x.squeeze(1) if x.dim() == 4 else x
-        B, T = xs.shape[0], xs.shape[1]
-        cd = 2 * self.dim_neck
-        enc_out = Lyr.dec_concat(codes, c_trg.contiguous(), B, T, codes.shape[1] // cd, cd)
-        hook = getattr(self, "_decoder_bwd_done", None)
-        if hook is not None and enc_out.requires_grad:
-            # fires once the backward has produced every decoder / postnet gradient
-            enc_out.register_hook(lambda g: hook())
-        mel = self.decoder.frames(enc_out, B, T)
-        mel_postnet = self.postnet.frames(mel, B, T, residual=mel)
-        return mel.view(B, 1, T, -1), mel_postnet.view(B, 1, T, -1), codes
+        return decode(self, x, codes, c_trg)

@@ -83,3 +83,26 @@ class LSTMParams(nn.Module):
 
     def forward(self, *a, **k):  # pragma: no cover
         raise RuntimeError("LSTMParams is driven by its parent model's HIP forward")
+
+
+class AdaIN(nn.Module):
+    """AdaIN (Norm.py:84-91): (content - content.mean()) / content.std() * std + mu, with
+    whole-tensor statistics; HIP moments + apply kernels (variants.hip)."""
+
+    def forward(self, content, mu, std):
+        from .. import variants as V
+
+        return V.adain(content, mu, std)
+
+
+class IN(nn.Module):
+    """IN (Norm.py:94-104): ((content - mu) / std, mu expanded, std)."""
+
+    def forward(self, content):
+        import torch
+
+        from .. import variants as V
+
+        m = V.moments(content)
+        y = V.adain(content, torch.zeros((), device=content.device), torch.ones((), device=content.device))
+        return y, m[0].expand(content.size()), m[1]

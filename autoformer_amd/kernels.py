@@ -473,3 +473,77 @@ def transpose_batched(src, B, R, C, out=None, accumulate=False):
     dst = torch.empty(B * C * R, device=src.device) if out is None else out
     L.call("avc_transpose_batched", src.data_ptr(), dst.data_ptr(), B, R, C, int(accumulate), stream())
     return dst
+
+
+# ------------------------------------------------------------------------- AdaIN / Adjust variants
+def moments(x, out=None):
+    """[x.mean(), x.std()] (unbiased) of the whole tensor, on device (variants.hip)."""
+    _dev(x)
+    out = torch.empty(2, device=x.device) if out is None else out
+    ws = torch.empty(int(L.lib().avc_moments_ws()), device=x.device, dtype=torch.float64)
+    L.call("avc_moments", x.data_ptr(), x.numel(), ws.data_ptr(), out.data_ptr(), stream())
+    return out
+
+
+def moments_bwd(x, mom, dmean, dstd):
+    """dx of the two moments; dmean / dstd are device scalars (views) or None."""
+    dx = torch.empty_like(x)
+    L.call("avc_moments_bwd", x.data_ptr(), x.numel(), mom.data_ptr(), _ptr(dmean), _ptr(dstd), None,
+           dx.data_ptr(), stream())
+    return dx
+
+
+def adain_fwd(x, mom, mu, sigma):
+    y = torch.empty_like(x)
+    L.call("avc_adain_fwd", x.data_ptr(), x.numel(), mom.data_ptr(), mu.data_ptr(), sigma.data_ptr(), y.data_ptr(),
+           stream())
+    return y
+
+
+def adain_bwd(g, x, mom, sigma):
+    """(dx, dmu, dsigma) of y = (x - mean x) / std x * sigma + mu."""
+    dev = x.device
+    dx = torch.empty_like(x)
+    sums = torch.empty(2, device=dev)
+    dmu, dsig = torch.empty((), device=dev), torch.empty((), device=dev)
+    ws = torch.empty(int(L.lib().avc_moments_ws()), device=dev, dtype=torch.float64)
+    L.call("avc_adain_bwd", g.data_ptr(), x.data_ptr(), x.numel(), mom.data_ptr(), sigma.data_ptr(), ws.data_ptr(),
+           sums.data_ptr(), dx.data_ptr(), dmu.data_ptr(), dsig.data_ptr(), stream())
+    return dx, dmu, dsig
+
+
+def segsum(x, B, T, C, ld, out=None, accumulate=False):
+    """out (B, C) = per-utterance sum over T of a C-column block of frame-major rows ld apart."""
+    _dev(x)
+    out = torch.empty(B, C, device=x.device) if out is None else out
+    L.call("avc_segsum", x.data_ptr(), int(ld), B, T, C, out.data_ptr(), int(accumulate), stream())
+    return out
+
+
+def step_select(h, B, T, t):
+    C = h.shape[1]
+    out = torch.empty(B, C, device=h.device)
+    L.call("avc_step_select", h.data_ptr(), out.data_ptr(), B, T, t, C, 0, stream())
+    return out
+
+
+def step_scatter(d, B, T, t):
+    C = d.shape[1]
+    out = torch.empty(B * T, C, device=d.device)
+    L.call("avc_step_select", d.data_ptr(), out.data_ptr(), B, T, t, C, 1, stream())
+    return out
+
+
+def rownorm_fwd(x):
+    R, C = x.shape
+    y = torch.empty_like(x)
+    norms = torch.empty(R, device=x.device)
+    L.call("avc_rownorm_fwd", x.data_ptr(), R, C, y.data_ptr(), norms.data_ptr(), stream())
+    return y, norms
+
+
+def rownorm_bwd(dy, y, norms):
+    R, C = y.shape
+    dx = torch.empty_like(y)
+    L.call("avc_rownorm_bwd", dy.data_ptr(), y.data_ptr(), norms.data_ptr(), R, C, dx.data_ptr(), stream())
+    return dx

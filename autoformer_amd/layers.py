@@ -316,8 +316,6 @@ class _EncConv0Fn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, mel2d, emb, core, B, T, w, b, gamma, beta):
-        if emb.requires_grad:
-            raise NotImplementedError("gradients w.r.t. the speaker embedding are not supported")
         x = K.enc_concat(mel2d, emb, B, T)
         a, saved = core.forward(x, B, T)
         ctx.core, ctx.B, ctx.T, ctx.saved, ctx.n_mel = core, B, T, saved, mel2d.shape[1]
@@ -329,9 +327,17 @@ class _EncConv0Fn(torch.autograd.Function):
     def backward(ctx, dA):
         x, a = ctx.saved_tensors
         K.attach_twin(x, ctx.x16)
-        n_dx = ctx.n_mel if ctx.needs_input_grad[0] else 0
+        # a trained speaker embedding (the *_Adjust variants feed Adjust's output here,
+        # AutoVC_Adjust.py:179-181) takes the full-width data gradient, summed over time
+        nm = ctx.n_mel
+        demb_needed = ctx.needs_input_grad[1]
+        n_dx = x.shape[1] if demb_needed else (nm if ctx.needs_input_grad[0] else 0)
         dx, dW, db, dg, dbe = ctx.core.backward(dA.contiguous(), x, a, ctx.saved, ctx.B, ctx.T, n_dx)
-        return dx, None, None, None, None, dW, db, dg, dbe
+        demb = None
+        if demb_needed:
+            demb = K.segsum(dx[:, nm:], ctx.B, ctx.T, x.shape[1] - nm, ld=x.shape[1])
+            dx = dx[:, :nm] if ctx.needs_input_grad[0] else None
+        return dx, demb, None, None, None, dW, db, dg, dbe
 
 
 def enc_conv0(core, mel2d, emb, B, T):
@@ -553,15 +559,17 @@ class _DecConcatFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, codes, emb, B, T, nc, cd):
-        if emb.requires_grad:
-            raise NotImplementedError("gradients w.r.t. the speaker embedding are not supported")
         ctx.args = (B, T, nc, cd, emb.shape[1])
         return K.dec_concat(codes, emb, B, T, nc, cd)
 
     @staticmethod
     def backward(ctx, dout):
         B, T, nc, cd, de = ctx.args
-        return K.dec_concat_bwd(dout.contiguous(), B, T, nc, cd, de), None, None, None, None, None
+        dout = dout.contiguous()
+        dcodes = K.dec_concat_bwd(dout, B, T, nc, cd, de) if ctx.needs_input_grad[0] else None
+        # c_trg trained through Adjust (AutoVC_Adjust.py:184-189): sum over the broadcast frames
+        demb = K.segsum(dout[:, cd:], B, T, de, ld=cd + de) if ctx.needs_input_grad[1] else None
+        return dcodes, demb, None, None, None, None
 
 
 def dec_concat(codes, emb, B, T, nc, cd):

@@ -127,12 +127,10 @@ def conv(x, conv_mod, cache, B, T_in):
 
 
 class _EncEmbedFn(torch.autograd.Function):
-    """cat(mel, c_org broadcast) -> PatchEmbed conv (MetaConv.py:108-112); dL/dmel only."""
+    """cat(mel, c_org broadcast) -> PatchEmbed conv (MetaConv.py:108-112)."""
 
     @staticmethod
     def forward(ctx, mel2d, emb, cache, B, T, w, b):
-        if emb.requires_grad:
-            raise NotImplementedError("gradients w.r.t. the speaker embedding are not supported")
         x = K.enc_concat(mel2d, emb, B, T)
         Wf, _ = Lyr.conv_packs(cache, w)
         y, _ = Lyr.conv_fwd(x, B, T, w, b, w.shape[-1] // 2, Wf)
@@ -148,11 +146,16 @@ class _EncEmbedFn(torch.autograd.Function):
         dy = dy.contiguous()
         dW = Lyr.conv_wgrad(dy, x, B, T, T, w, pad)
         db = K.colsum(dy, B * T, w.shape[0])
-        dmel = None
-        if ctx.needs_input_grad[0]:
+        dmel = demb = None
+        nm, Cin = ctx.n_mel, x.shape[1]
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             _, Wd = Lyr.conv_packs(ctx.cache, w)
-            dmel = Lyr.conv_dgrad(dy, B, T, T, w, pad, Wd, n_dx=ctx.n_mel)
-        return dmel, None, None, None, None, dW, db
+            # a trained c_org (MetaConv_Adjust.py:256) takes the full-width data gradient
+            dx = Lyr.conv_dgrad(dy, B, T, T, w, pad, Wd, n_dx=Cin if ctx.needs_input_grad[1] else nm)
+            if ctx.needs_input_grad[1]:
+                demb = K.segsum(dx[:, nm:], B, T, Cin - nm, ld=Cin)
+            dmel = dx[:, :nm] if ctx.needs_input_grad[0] else None
+        return dmel, demb, None, None, None, dW, db
 
 
 def enc_embed(mel2d, emb, proj, cache, B, T):

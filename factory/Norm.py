@@ -1,1 +1,1 @@
-from autoformer_amd.factory.Norm import ConvNorm, GroupNorm, LinearNorm, PatchEmbed  # noqa: F401
+from autoformer_amd.factory.Norm import ConvNorm, GroupNorm, LinearNorm, PatchEmbed, AdaIN, IN  # noqa: F401

@@ -110,7 +110,7 @@ def _variant_model(name, dev):
 
 def _variant_bn_fed_bias(n):
     # conv biases that feed a training-mode BatchNorm: analytically zero gradient
-    return "conv.bias" in n and "feature_last_combine" not in n and "postnet.convolutions.4" not in n
+    return "conv.bias" in n and "feature_last_combine" not in n
 
 
 @pytest.mark.gpu
@@ -129,8 +129,16 @@ def test_gpu_variant_step_matches_reference(name):
     if emb_adj is not None:
         assert rel_inf(emb_adj.detach().cpu().numpy(), g["step_emb_adj"]) < 1e-3
     np.testing.assert_allclose([v.item() for v in losses], g["step_losses"], rtol=1e-4)
-    bad = grad_mismatches(m, {k[5:]: g[k] for k in g.files if k.startswith("step_g")},
-                          bn_fed_bias=_variant_bn_fed_bias)
+    # bars of tests/test_gpu_metaformer.py for the MetaFormer families (the reference's own
+    # fp32 heads sit up to 1.4e-2 from fp64 there); analytically zero: conv biases feeding a
+    # training-mode BN, MetaPool's GroupNorm norm1.bias (annihilated by pool(x) - x)
+    meta = name.startswith("Meta")
+
+    def zero_grad(n):
+        return _variant_bn_fed_bias(n) or (name.startswith("MetaPool") and n.endswith("norm1.bias"))
+
+    bad = grad_mismatches(m, {k[5:]: g[k] for k in g.files if k.startswith("step_g")}, tol=1e-2,
+                          head_tol=5e-2 if meta else 1e-2, bn_fed_bias=zero_grad)
     assert not bad, bad
     assert not bn_state_mismatches(m, {k[5:]: g[k] for k in g.files if k.startswith("step_bn/")})
 
@@ -151,7 +159,9 @@ def test_gpu_variant_conversion_matches_reference(name):
             mel, psnt, codes = m(x, e, e2, target_feature=tf)
             m2 = _variant_model(name, dev)
             _, feats = m2(x, e, None)
-            np.testing.assert_allclose(np.array([[float(a), float(b)] for a, b in feats]), g["feats"], rtol=1e-4)
+            # means of BN outputs are ~1e-9 (fp32 noise): an absolute floor
+            np.testing.assert_allclose(np.array([[float(a), float(b)] for a, b in feats]), g["feats"], rtol=1e-4,
+                                       atol=1e-6)
     assert rel_inf(mel.cpu().numpy(), g["conv_mel"]) < 1e-3
     assert rel_inf(psnt.cpu().numpy(), g["conv_mel_psnt"]) < 1e-3
     assert rel_inf(codes.cpu().numpy(), g["conv_codes"]) < 1e-3
@@ -209,3 +219,16 @@ def test_gpu_rownorm_step_select_segsum_match_torch():
     out = K.segsum(x[:, 80:], B, T, 256, ld=336)
     ref = x.view(B, T, 336)[:, :, 80:].double().sum(1)
     assert rel_inf(out.cpu(), ref.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_build_module_state_dict_matches_reference(name):
+    """The drop-in module (factory.<name>) registers the reference's keys in its order."""
+    import importlib
+
+    g = _golden(name)
+    cls = getattr(importlib.import_module(f"factory.{name}"), name)
+    m = cls(44, 256, 512, 22)
+    assert list(m.state_dict().keys()) == [str(k) for k in g["keys"]]
+    ref_shapes = V.SPECS[name]()
+    assert all(tuple(v.shape) == tuple(ref_shapes[k]) for k, v in m.state_dict().items())
