@@ -4,6 +4,7 @@
   losses and logging format) so existing scripts can switch by import.
 * ``GANSolver`` mirrors train_with_discriminator.py:13-145 (ONE loss for both models and
   both Adams stepping on the same backward — kept as in the reference, not "fixed").
+* ``AdjustSolver`` mirrors train_with_adjust.py:16-145 (the *_Adjust models, 4 losses).
 * ``TrainStep`` is the benchmark/production step: flat parameter and gradient buffers,
   HIP MSE/L1 losses, fused HIP Adam, optional RCCL gradient all-reduce and hipGraph
   capture of the whole step.
@@ -113,6 +114,39 @@ def vc_losses(model, x_real, emb, lambda_cd=1.0):
     return l_id + l_id_psnt + lambda_cd * l_cd, (l_id, l_id_psnt, l_cd), x_id_psnt
 
 
+def adain_losses(model, x_real, emb, lambda_cd=1.0):
+    """train.py's loss block for the AdaIN variants (AutoVC2 & co.), whose c_trg=None pass
+    returns (codes, features) (AutoVC2.py:219-220): the re-pass codes are its first element."""
+    x_id, x_id_psnt, code_real = model(x_real, emb, emb)
+    l_id = mse_loss(x_real, x_id.squeeze())
+    l_id_psnt = mse_loss(x_real, x_id_psnt.squeeze())
+    code_re, _ = model(x_id_psnt, emb, None)
+    l_cd = l1_loss(code_real, code_re)
+    return l_id + l_id_psnt + lambda_cd * l_cd, (l_id, l_id_psnt, l_cd), x_id_psnt
+
+
+def adjust_losses(model, x_real, emb, lambda_cd=1.0, lambda_ad=1.0):
+    """The loss block of train_with_adjust.py:Solver.train (train_with_adjust.py:96-124)."""
+    emb_adjust, x_id, x_id_psnt, code_real = model(x_real, emb, emb)
+    l_id = mse_loss(x_real, x_id.squeeze())
+    l_id_psnt = mse_loss(x_real, x_id_psnt.squeeze())
+    code_re = model(x_id_psnt, emb, None)
+    l_cd = l1_loss(code_real, code_re)
+    l_ad = l1_loss(emb_adjust, emb)
+    return (l_id + l_id_psnt + lambda_cd * l_cd + lambda_ad * l_ad, (l_id, l_id_psnt, l_cd, l_ad), x_id_psnt)
+
+
+def losses_for(model):
+    """The step's loss block by model family (plain / AdaIN variant / Adjust variant)."""
+    from .factory._variants import AdaINModel, AdjustModel
+
+    if isinstance(model, AdjustModel):
+        return adjust_losses
+    if isinstance(model, AdaINModel):
+        return adain_losses
+    return vc_losses
+
+
 # ------------------------------------------------------------------------- optimizer
 class FusedAdam:
     """torch.optim.Adam (defaults, no weight decay) as one HIP kernel over a flat buffer."""
@@ -158,7 +192,10 @@ class TrainStep:
         # the encoder backward (full pass + re-pass gradients) still runs, and only the encoder
         # slice is averaged after the backward.
         self.split = None
-        if self.world > 1 and hasattr(model, "decoder"):
+        self.loss_fn = losses_for(model)
+        # the Adjust variants register `adjust` after the postnet and its gradients complete
+        # only with the encoder's: no early (overlapped) slice for them
+        if self.world > 1 and hasattr(model, "decoder") and self.loss_fn is not adjust_losses:
             self.split = D.split_offset(self.params, next(model.decoder.parameters()))
             self.comm = torch.cuda.Stream()
         self._early = None
@@ -176,7 +213,7 @@ class TrainStep:
         self.gflat.zero_()
         self.model._decoder_bwd_done = self._decoder_done if overlap else None
         try:
-            loss, parts, x_psnt = vc_losses(self.model, x, emb, self.lambda_cd)
+            loss, parts, x_psnt = self.loss_fn(self.model, x, emb, self.lambda_cd)
             if self.extra is not None:
                 loss = loss + self.extra(x, emb, x_psnt)
             loss.backward()
@@ -276,6 +313,44 @@ class Solver:
             vc_loss, parts, _ = vc_losses(self.VC, x_real, emb_org, self.lambda_cd)
             self.reset_grad()
             vc_loss.backward()
+            self.vc_optimizer.step()
+            loss = {k: p.item() for k, p in zip(keys, parts)}
+            history.append([loss[k] for k in keys])
+            if (i + 1) % self.log_step == 0:
+                et = str(datetime.timedelta(seconds=time.time() - start_time))[:-7]
+                log = "Elapsed [{}], Iteration [{}/{}]".format(et, i + 1, self.num_iters)
+                for tag in keys:
+                    log += ", {}: {:.4f}".format(tag, loss[tag])
+                print(log)
+        return history
+
+
+class AdjustSolver(Solver):
+    """Mirror of train_with_adjust.py:Solver (train_with_adjust.py:16-145): the train.py loop
+    plus the speaker-embedding loss L1(emb_adjust, emb_org) weighted by lambda_ad."""
+
+    def __init__(self, vcc_loader, config):
+        self.lambda_ad = getattr(config, "lambda_ad", 1.0)
+        super().__init__(vcc_loader, config)
+
+    def train(self):
+        keys = ["G/loss_id", "G/loss_id_psnt", "G/loss_cd", "A/loss_adjust"]
+        print("Start training...")
+        start_time = time.time()
+        data_iter = None
+        history = []
+        for i in range(self.num_iters):
+            try:
+                x_real, emb_org = next(data_iter)
+            except Exception:
+                data_iter = iter(self.vcc_loader)
+                x_real, emb_org = next(data_iter)
+            x_real = x_real.to(self.device)
+            emb_org = emb_org.to(self.device)
+            self.VC = self.VC.train()
+            g_loss, parts, _ = adjust_losses(self.VC, x_real, emb_org, self.lambda_cd, self.lambda_ad)
+            self.reset_grad()
+            g_loss.backward()
             self.vc_optimizer.step()
             loss = {k: p.item() for k, p in zip(keys, parts)}
             history.append([loss[k] for k in keys])

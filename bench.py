@@ -26,7 +26,13 @@ PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3     # f32 MFMA
 # algorithmic work of one train step per mel frame (torch flop counter on the reference)
 FLOP_PER_FRAME = {("AutoVC", 128, 16): 191.55e6, ("AutoVC", 176, 22): 191.59e6, ("AutoVC+D", 176, 22): 191.87e6,
-                  ("MetaConv", 176, 22): 1044.41e6, ("MetaPool", 176, 22): 981.86e6}
+                  ("MetaConv", 176, 22): 1044.41e6, ("MetaPool", 176, 22): 981.86e6,
+                  # model variants, same counter: tools/variant_flops.py
+                  ("AutoVC2", 128, 16): 194.93e6, ("AutoVC2", 176, 22): 194.98e6,
+                  ("AutoVC_Adjust", 128, 16): 492.84e6, ("AutoVC_Adjust", 176, 22): 492.97e6,
+                  ("MetaConv2", 176, 22): 1047.80e6, ("MetaPool2", 176, 22): 985.24e6,
+                  ("MetaConv_Adjust", 176, 22): 1345.79e6, ("MetaPool_Adjust", 176, 22): 1081.17e6}
+VARIANTS = ["AutoVC2", "AutoVC_Adjust", "MetaConv2", "MetaPool2", "MetaConv_Adjust", "MetaPool_Adjust"]
 
 
 def synthetic_batch(B, T, rank, device):
@@ -123,8 +129,9 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--len-crop", type=int, default=None, help="default 128 (AutoVC), 176 (MetaConv/MetaPool/--disc)")
     ap.add_argument("--freq", type=int, default=None, help="default 16 at T=128, 22 at T=176")
-    ap.add_argument("--model", default="AutoVC", choices=["AutoVC", "MetaConv", "MetaPool"],
-                    help="factory plugin (train.py --model_name); MetaConv/MetaPool hard-wire T=176")
+    ap.add_argument("--model", default="AutoVC", choices=["AutoVC", "MetaConv", "MetaPool"] + VARIANTS,
+                    help="factory plugin (train.py / train_with_adjust.py --model_name); the MetaFormer "
+                         "families hard-wire T=176")
     ap.add_argument("--disc", action="store_true",
                     help="AutoVC + Discriminator two-model step (train_with_discriminator.py), T=176")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -147,7 +154,7 @@ def main():
     set_compute(args.dtype)
     if args.disc and args.model != "AutoVC":
         raise SystemExit("--disc pairs the Discriminator with AutoVC (train_with_discriminator.py)")
-    wide = args.model != "AutoVC" or args.disc
+    wide = args.model.startswith("Meta") or args.disc
     B = args.batch
     T = args.len_crop if args.len_crop is not None else (176 if wide else 128)
     freq = args.freq if args.freq is not None else (22 if T == 176 else 16)
@@ -207,6 +214,8 @@ def main():
     peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
     step = ("train_with_discriminator.py step (G fwd + encoder re-pass + D on real/fake + 2xMSE + L1 + 2xBCE + "
             "one bwd + both Adams)" if args.disc else
+            "train_with_adjust.py step (fwd with 2 Adjust passes + encoder re-pass with 1 + 2xMSE + 2xL1 + bwd + "
+            "Adam)" if args.model.endswith("_Adjust") else
             "train.py step (fwd + encoder re-pass + 2xMSE + L1 + bwd + Adam)")
     default = name == "AutoVC" and (T, freq) == (128, 16)
     metric = METRIC if default else f"mel-frames/sec fwd+bwd, {name} 80\u00d7{T} mel, batch={B}"

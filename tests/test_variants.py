@@ -232,3 +232,33 @@ def test_build_module_state_dict_matches_reference(name):
     assert list(m.state_dict().keys()) == [str(k) for k in g["keys"]]
     ref_shapes = V.SPECS[name]()
     assert all(tuple(v.shape) == tuple(ref_shapes[k]) for k, v in m.state_dict().items())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["AutoVC2", "AutoVC_Adjust", "MetaPool_Adjust"])
+def test_gpu_variant_trainstep_matches_reference(name):
+    """The production step (flat buffers, gradient sink, side-stream weight gradients, fused
+    HIP losses + Adam) on a variant: the first step's loss and gradients equal the reference's."""
+    from autoformer_amd.train import TrainStep
+
+    dev = torch.device("cuda:0")
+    g = _golden(name)
+    m = _variant_model(name, dev)
+    x, e = (torch.from_numpy(g[k]).to(dev) for k in ("x", "emb"))
+    ts = TrainStep(m, lr=1e-4)
+    try:
+        loss = ts.step(x, e)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(loss.item(), g["step_losses"].sum(), rtol=1e-4)
+        meta = name.startswith("Meta")
+
+        def zero_grad(n):
+            return _variant_bn_fed_bias(n) or (name.startswith("MetaPool") and n.endswith("norm1.bias"))
+        bad = grad_mismatches(m, {k[5:]: g[k] for k in g.files if k.startswith("step_g")}, tol=1e-2,
+                              head_tol=5e-2 if meta else 1e-2, bn_fed_bias=zero_grad)
+        assert not bad, bad
+        loss2 = ts.step(x, e)
+        assert np.isfinite(loss2.item()) and loss2.item() < loss.item()
+    finally:
+        from autoformer_amd.layers import set_grad_sink
+        set_grad_sink(False)
