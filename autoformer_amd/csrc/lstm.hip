@@ -801,7 +801,8 @@ __device__ __forceinline__ void load_group(__amdgpu_buffer_rsrc_t pay, int row0,
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
     const int ch = tid + NT * i, row = ch / CPR, col = ch - row * CPR;
-    *reinterpret_cast<u32x4_t*>(lds + row * ap + col * 8) = v[i];
+    // NCH is rounded up when NT does not divide the tile (H = 768): skip the overhang
+    if (NCH * NT == PRG * CPR || row < PRG) *reinterpret_cast<u32x4_t*>(lds + row * ap + col * 8) = v[i];
   }
 }
 
@@ -809,7 +810,8 @@ __device__ __forceinline__ void load_group(__amdgpu_buffer_rsrc_t pay, int row0,
 // `a` + 32k, W fragments live in registers; A fragments are read up to eight K-blocks ahead.
 template <int NK>
 __device__ __forceinline__ void mfma_rows(const bf16* a, const bf16x8 (&wf)[2][NK], f32x4& acc0, f32x4& acc1) {
-  constexpr int KG = NK < 8 ? NK : 8;
+  // K-blocks per fragment batch: the largest divisor of NK up to 8 (NK = 12 at H = 768)
+  constexpr int KG = NK % 8 == 0 ? 8 : NK % 6 == 0 ? 6 : NK % 4 == 0 ? 4 : NK < 8 ? NK : 1;
 #pragma unroll
   for (int k0 = 0; k0 < NK; k0 += KG) {
     bf16x8 af[KG];
@@ -833,7 +835,7 @@ constexpr int PNT = 512;
 template <int H>
 __global__ void __launch_bounds__(PNT, 1) lstm_persist_fwd(PersistArgs a) {
   constexpr int G = 4 * H, NKH = H / 64, AP = H + 8, KH = H / 2;
-  constexpr int NCH = PRG * H / 8 / PNT;  // 16-B payload chunks per thread per step
+  constexpr int NCH = (PRG * H / 8 + PNT - 1) / PNT;  // 16-B payload chunks per thread per step
   __shared__ __attribute__((aligned(16))) bf16 As[16 * AP];
   __shared__ __attribute__((aligned(16))) bf16 hs16[PRG * PJU];
   __shared__ float gs[2][PRG][4 * PJU + 1];
@@ -964,7 +966,7 @@ struct PersistBwdArgs {
 template <int H>
 __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
   constexpr int G = 4 * H, NKH = H / 64, AP = G + 8, KH = H / 2, NW = PNT / 64;
-  constexpr int NCH = PRG * G / 8 / PNT;  // 16-B payload chunks per thread per step
+  constexpr int NCH = (PRG * G / 8 + PNT - 1) / PNT;  // 16-B payload chunks per thread per step
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* As = reinterpret_cast<bf16*>(smem_raw);                          // [PRG + 1][AP], row PRG = zeros
   float* red = reinterpret_cast<float*>(smem_raw + (PRG + 1) * AP * 2);  // [NW][PRG][PJU + 1]
@@ -1159,7 +1161,7 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
   a.dirs = dirs;
   const int ng = (B + PRG - 1) / PRG;
   static const bool no_persist = getenv("AVC_LSTM_NO_PERSIST") != nullptr;
-  if (bf && dirs == 1 && (H == 1024 || H == 512) && hbuf && !no_persist && ng * (H / PJU) <= num_cus()) {
+  if (bf && dirs == 1 && (H == 1024 || H == 768 || H == 512) && hbuf && !no_persist && ng * (H / PJU) <= num_cus()) {
     // hbuf: control words + flags + the [2][B][H] bf16 payload in this mode (layout above)
     PersistArgs p;
     p.xproj = xproj;
@@ -1176,6 +1178,7 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
     p.ng = ng;
     (void)hipMemsetAsync(hbuf, 0, px_ctl_bytes(ng), s);
     if (H == 1024) lstm_persist_fwd<1024><<<ng * (H / PJU), PNT, 0, s>>>(p);
+    else if (H == 768) lstm_persist_fwd<768><<<ng * (H / PJU), PNT, 0, s>>>(p);  // Adjust.py:30
     else lstm_persist_fwd<512><<<ng * (H / PJU), PNT, 0, s>>>(p);
     return avc_check_launch("avc_lstm_fwd(persistent)");
   }
@@ -1224,7 +1227,7 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
   AVC_CHECK_ARG(!bf || (wdtype == AVC_BF16 && gbuf), "avc_lstm_bwd: bf16 compute needs bf16 W_hh^T and gbuf");
   const int ng = (B + PRG - 1) / PRG;
   static const bool no_persist = getenv("AVC_LSTM_NO_PERSIST") != nullptr;
-  if (bf && dirs == 1 && (H == 1024 || H == 512) && !no_persist && ng * (H / PJU) <= num_cus()) {
+  if (bf && dirs == 1 && (H == 1024 || H == 768 || H == 512) && !no_persist && ng * (H / PJU) <= num_cus()) {
     // gbuf: control words + flags + the [2][B][4H] bf16 payload in this mode (layout above)
     PersistBwdArgs p;
     p.dhout = dh_out;
@@ -1248,6 +1251,14 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
         attr = true;
       }
       lstm_persist_bwd<1024><<<ng * (H / PJU), PNT, persist_bwd_lds<1024>(), s>>>(p);
+    } else if (H == 768) {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_persist_bwd<768>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_bwd_lds<768>());
+        attr = true;
+      }
+      lstm_persist_bwd<768><<<ng * (H / PJU), PNT, persist_bwd_lds<768>(), s>>>(p);
     } else {
       lstm_persist_bwd<512><<<ng * (H / PJU), PNT, persist_bwd_lds<512>(), s>>>(p);
     }

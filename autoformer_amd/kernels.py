@@ -215,7 +215,7 @@ def lstm_timeout_flag(hbuf, B, H):
 
 def lstm_persistent_fwd(B, H, dirs):
     """Whether avc_lstm_fwd takes the one-launch persistent path (mirrors lstm.hip)."""
-    return _COMPUTE == BF16 and dirs == 1 and H in (512, 1024) and os.environ.get("AVC_LSTM_NO_PERSIST") is None \
+    return _COMPUTE == BF16 and dirs == 1 and H in (512, 768, 1024) and os.environ.get("AVC_LSTM_NO_PERSIST") is None \
         and ((B + 7) // 8) * (H // 32) <= num_cus()
 
 
@@ -234,7 +234,7 @@ def lstm_fwd(xproj, w_hh, B, T, H, dirs, hbuf=None):
 
 def lstm_persistent_bwd(B, H, dirs):
     """Whether avc_lstm_bwd takes the one-launch persistent path (mirrors lstm.hip)."""
-    return _COMPUTE == BF16 and dirs == 1 and H in (512, 1024) and os.environ.get("AVC_LSTM_NO_PERSIST") is None \
+    return _COMPUTE == BF16 and dirs == 1 and H in (512, 768, 1024) and os.environ.get("AVC_LSTM_NO_PERSIST") is None \
         and ((B + 7) // 8) * (H // 32) <= num_cus()
 
 

@@ -309,7 +309,7 @@ def test_gemm_fast_bf16_copy_and_mixed_dtypes():
             assert relf(c16.float(), ref) < 5e-3
 
 
-@pytest.mark.parametrize("B,H", [(64, 1024), (20, 1024), (64, 512), (3, 512)])
+@pytest.mark.parametrize("B,H", [(64, 1024), (20, 1024), (64, 512), (3, 512), (64, 768), (2, 768)])
 def test_lstm_persistent_forward_matches_per_step(B, H):
     """The persistent recurrence (bf16) equals the per-step kernels within bf16 rounding and
     never raises its spin-timeout flag."""
@@ -394,7 +394,7 @@ def test_gemm_nt_conv_window_and_bn_stats(B, T, Cin, Cout, Kw, pad):
     assert rinf(1.0 / rstd.double() ** 2 - 1e-5, refv) < 1e-3
 
 
-@pytest.mark.parametrize("B,H", [(64, 1024), (20, 1024), (64, 512), (3, 512)])
+@pytest.mark.parametrize("B,H", [(64, 1024), (20, 1024), (64, 512), (3, 512), (64, 768), (2, 768)])
 def test_lstm_persistent_backward(B, H):
     """The one-launch backward recurrence (bf16 products, fp32 cell math) against an fp32
     CPU loop that rounds dG_{t+1} to bf16 for the recurrent product, as the kernel does;
