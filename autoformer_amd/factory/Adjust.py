@@ -25,11 +25,19 @@ class Adjust(nn.Module):
         self._lstm = [Lyr.LSTMLayerCore(self.lstm, layer) for layer in range(3)]
         self._lin = Lyr.PackCache()
 
-    def forward(self, x, emb):
+    def forward(self, x, emb, stat_updates=1):
+        """stat_updates = 2: this call stands for two reference calls on identical inputs (the
+        outputs are identical; each BatchNorm's running statistics move twice, as there)."""
         mel, B, T = _frames(x)
-        h = Lyr.enc_conv0(self._convs[0], mel, emb.contiguous(), B, T)
-        for core in self._convs[1:]:
-            h = Lyr.conv_bn(core, h, B, T)
+        for core in self._convs:
+            core.stat_updates = stat_updates
+        try:
+            h = Lyr.enc_conv0(self._convs[0], mel, emb.contiguous(), B, T)
+            for core in self._convs[1:]:
+                h = Lyr.conv_bn(core, h, B, T)
+        finally:
+            for core in self._convs:
+                core.stat_updates = 1
         h = Lyr.lstm(self.lstm, self._lstm, h, B, T)
         last = V.step_select(h, B, T, T - 1)
         lin = self.embedding.linear_layer

@@ -108,13 +108,20 @@ class AdjustModel(nn.Module):
         self.adjust = Adjust(dim_emb)
 
     def forward(self, x, c_org, c_trg, isConvert=False, x_target=None):
+        # train_with_adjust.py:99 passes emb_org as both c_org and c_trg, so the reference runs
+        # Adjust twice on identical inputs (AutoVC_Adjust.py:179, :189): identical outputs, and
+        # each BatchNorm's running statistics moved twice.  One pass with two statistics
+        # updates gives the same forward, buffers and (summed) gradient at half the cost.
+        shared = self.adjusts_org and c_trg is c_org and not isConvert
         if self.adjusts_org:
-            c_org = self.adjust(x, c_org)
+            c_org = self.adjust(x, c_org, stat_updates=2 if shared else 1)
         codes = self.encoder.codes_flat(x, c_org)
         if c_trg is None:
             return codes
         elif isConvert:
             c_trg = self.adjust(x_target, c_trg)
+        elif shared:
+            c_trg = c_org
         else:
             # in training c_trg is c_org; in conversion pass the target mel (AutoVC_Adjust.py:186-189)
             c_trg = self.adjust(x, c_trg)

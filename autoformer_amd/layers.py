@@ -212,6 +212,9 @@ class ConvBNCore:
         self.conv, self.bn, self.act = conv, bn, act
         self.pad = conv.padding[0]
         self.cache = PackCache()
+        # running-statistics updates per forward: 2 when one forward stands for two identical
+        # reference passes (the *_Adjust models' c_org / c_trg Adjust calls)
+        self.stat_updates = 1
 
     def packs(self):
         w = self.conv.weight
@@ -237,6 +240,8 @@ class ConvBNCore:
             mom = bn.momentum if bn.momentum is not None else 0.1
             stats = K.bn_finalize(partial, M, Co, bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, mom,
                                   bn.eps)
+            for _ in range(self.stat_updates - 1):  # the same batch statistics, applied again
+                K.bn_finalize(partial, M, Co, bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, mom, bn.eps)
         else:
             stats = K.bn_eval(bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.eps)
         mean, rstd, scale, shift = stats

@@ -262,3 +262,28 @@ def test_gpu_variant_trainstep_matches_reference(name):
     finally:
         from autoformer_amd.layers import set_grad_sink
         set_grad_sink(False)
+
+
+@pytest.mark.gpu
+def test_gpu_adjust_shared_pass_equals_two_passes():
+    """c_trg is c_org (train_with_adjust.py:99): one Adjust pass with doubled BN statistics
+    updates equals the reference's two passes (c_trg a distinct, equal tensor)."""
+    dev = torch.device("cuda:0")
+    g = _golden("AutoVC_Adjust")
+    x, e = (torch.from_numpy(g[k]).to(dev) for k in ("x", "emb"))
+    outs = []
+    for c_trg in ("same", "copy"):
+        m = _variant_model("AutoVC_Adjust", dev)
+        o = m(x, e, e if c_trg == "same" else e.clone())
+        loss = sum(t.float().square().mean() for t in o)
+        loss.backward()
+        torch.cuda.synchronize()
+        outs.append(([t.detach().cpu() for t in o], {k: v.detach().cpu().clone() for k, v in m.state_dict().items()},
+                     {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters()}))
+    (o1, s1, g1), (o2, s2, g2) = outs
+    for a, b in zip(o1, o2):
+        assert torch.equal(a, b)
+    for k in s1:
+        assert torch.equal(s1[k], s2[k]), k
+    for n in g1:
+        torch.testing.assert_close(g1[n], g2[n], rtol=1e-4, atol=1e-6)
