@@ -100,6 +100,7 @@ _SIGS = {
     "avc_step_select": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_rownorm_fwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "avc_rownorm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "avc_pad_cols": (c_int, [c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
 }
 
 _lib = None

@@ -229,6 +229,18 @@ __global__ void __launch_bounds__(256) rownorm_bwd_kernel(const float* __restric
   for (int c = l; c < C; c += 64) dx[o + c] = (dy[o + c] - y[o + c] * d) * inv;
 }
 
+// dst[r][c] (row length Cd) = c < C ? src[r*lds + c] : 0, converted to dtype: zero-pads
+// (Cd > C) or crops (Cd < C) the columns of a row-major matrix.
+template <typename TO>
+__global__ void pad_cols_kernel(const float* __restrict__ src, long long lds, TO* __restrict__ dst, int R, int C,
+                                int Cd) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)R * Cd) return;
+  const int c = (int)(i % Cd);
+  const long long r = i / Cd;
+  dst[i] = (TO)(c < C ? src[r * lds + c] : 0.f);
+}
+
 inline int blocks_for(long long n, int per) { return (int)((n + per - 1) / per); }
 
 int reduce2(const float* x, const float* g, long long n, const float* mom, int mode, double* ws, float* out,
@@ -304,4 +316,17 @@ extern "C" int avc_rownorm_bwd(const float* dy, const float* y, const float* nor
   AVC_CHECK_ARG(R > 0 && C > 0, "avc_rownorm_bwd: bad shape R=%d C=%d", R, C);
   rownorm_bwd_kernel<<<(R + 3) / 4, 256, 0, (hipStream_t)stream>>>(dy, y, norms, R, C, dx);
   return avc_check_launch("avc_rownorm_bwd");
+}
+
+extern "C" int avc_pad_cols(const float* src, long long lds, void* dst, int dtype, int R, int C, int Cd,
+                            void* stream) {
+  AVC_CHECK_ARG(src && dst && R > 0 && C > 0 && Cd > 0 && lds >= C, "avc_pad_cols: bad shape R=%d C=%d Cd=%d", R,
+                C, Cd);
+  const long long n = (long long)R * Cd;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == AVC_BF16)
+    pad_cols_kernel<bf16><<<blocks_for(n, 256), 256, 0, s>>>(src, lds, reinterpret_cast<bf16*>(dst), R, C, Cd);
+  else
+    pad_cols_kernel<float><<<blocks_for(n, 256), 256, 0, s>>>(src, lds, reinterpret_cast<float*>(dst), R, C, Cd);
+  return avc_check_launch("avc_pad_cols");
 }

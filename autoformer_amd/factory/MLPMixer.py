@@ -47,6 +47,7 @@ class MLPMixer(nn.Sequential):
         self.ps = patch_size
         self.cache = Lyr.PackCache()
         self.tm_cache = Lyr.PackCache()  # token-mixing weights: W1^T and W2 in the compute dtype
+        self.cf_cache = Lyr.PackCache()  # patch-embedding / channel-FF weights in the compute dtype
 
     @property
     def ln_eps(self):

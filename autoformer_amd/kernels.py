@@ -547,3 +547,13 @@ def rownorm_bwd(dy, y, norms):
     dx = torch.empty_like(y)
     L.call("avc_rownorm_bwd", dy.data_ptr(), y.data_ptr(), norms.data_ptr(), R, C, dx.data_ptr(), stream())
     return dx
+
+
+def pad_cols(src, Cd, dtype=F32, C=None):
+    """(R, Cd) copy of the first C columns of the row-major 2-D src, zero-padded (or cropped)."""
+    R, lds = src.shape
+    C = lds if C is None else C
+    tdt = torch.bfloat16 if dtype == BF16 else torch.float32
+    out = torch.empty(R, Cd, device=src.device, dtype=tdt)
+    L.call("avc_pad_cols", src.data_ptr(), lds, out.data_ptr(), dtype, R, C, Cd, stream())
+    return out

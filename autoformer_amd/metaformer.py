@@ -171,6 +171,37 @@ def _token_mix_weights(mix, w1, w2, NP):
     return mix.tm_cache.get([w1, w2], build)
 
 
+def _cf_weights(mix, we, w3, w4):
+    """Patch-embedding and channel-FF weights in the compute dtype (bf16 in bf16 mode, so the
+    products take the LDS-DMA bf16 kernels instead of the fp32-operand path)."""
+    def build():
+        dt = K.compute()
+        return K.convert(we, dt), K.convert(w3, dt), K.convert(w4, dt)
+    return mix.cf_cache.get([we, w3, w4], build)
+
+
+def _out_conv_packs(mix, wc):
+    """Packs of the mixer output conv Conv1d(NP -> O, k5) with NP zero-padded to a multiple of
+    8 (1849 -> 1856 / 121 -> 128 patches): the padded channels meet zero weights, and the
+    bf16 LDS-DMA conv / weight-gradient kernels replace the generic path (2.3 ms -> see
+    DESIGN.md).  Returns ((Wf, Wd), padded weight) with the padded weight used for shapes."""
+    O, NP, Kw = wc.shape
+    NPp = (NP + 7) // 8 * 8
+    if NPp == NP:
+        return Lyr.conv_packs(mix.cache, wc), wc
+
+    def build():
+        dt = K.compute()
+        wp = K.pad_cols(wc.view(O, NP * Kw), NPp * Kw).view(O, NPp, Kw)
+        return K.conv_pack(wp, 0, dt), K.conv_pack(wp, 1, dt), wp
+    Wf, Wd, wp = mix.cache.get([wc], build)
+    return (Wf, Wd), wp
+
+
+def _twins(*ts):
+    return tuple(getattr(t, "_bf16", None) for t in ts)
+
+
 def _lin(x, M, N, Kd, w, b=None, residual=None, out=None):
     """y = x (M x Kd, row-major) . w^T (w: N x Kd) + b (+ residual)."""
     y = torch.empty(M, N, device=x.device) if out is None else out
@@ -190,8 +221,9 @@ class _MLPMixerFn(torch.autograd.Function):
         NP = (C // ps) * (Lf // ps)
         D = we.shape[0]
         dev = nf.device
-        P = K.patchify(nf, B, Lf, C, ps)                       # (B*NP, ps^2)
-        Z = _lin(P, B * NP, D, ps * ps, we, be)                 # (B*NP, D)
+        P = K.twin(K.patchify(nf, B, Lf, C, ps))               # (B*NP, ps^2)
+        weC, w3C, w4C = _cf_weights(mix, we, w3, w4)
+        Z = _lin(P, B * NP, D, ps * ps, weC, be)                # (B*NP, D)
         Y1, m1, r1 = K.layer_norm_fwd(Z, g1, b1n, mix.ln_eps[0])
         # token mixing: UT_b (D x 4NP) = Y1_b^T . W1^T + b1   (Conv1d(NP -> 4NP, k1) on (B, NP, D)).
         # NP (121 / 1849 patches) is never the contiguous dimension of a GEMM operand: W1 is
@@ -206,15 +238,18 @@ class _MLPMixerFn(torch.autograd.Function):
                batch=B, c_batch_stride=D * NP)
         Z1 = K.transpose_batched(RT, B, D, NP, out=K.convert(Z, K.F32), accumulate=True).view(B * NP, D)
         Y2, m2, r2 = K.layer_norm_fwd(Z1, g2, b2n, mix.ln_eps[1])
-        U2 = _lin(Y2, B * NP, 4 * D, D, w3, bb3)
+        U2 = _lin(K.twin(Y2), B * NP, 4 * D, D, w3C, bb3)
         V2 = K.act_fwd(U2, K.ACT_GELU)
-        Z2 = _lin(V2, B * NP, D, 4 * D, w4, bb4, residual=Z1)
+        Z2 = _lin(K.twin(V2), B * NP, D, 4 * D, w4C, bb4, residual=Z1)
         Z2T = K.transpose_batched(Z2, B, NP, D).view(B * D, NP)
-        Wf, _ = Lyr.conv_packs(mix.cache, wc)
-        out, _ = Lyr.conv_fwd(Z2T, B, D, wc, bc, wc.shape[-1] // 2, Wf)
+        (Wf, _), wp = _out_conv_packs(mix, wc)
+        if wp.shape[1] != NP:  # padded patch channels, written once in the compute dtype
+            Z2T = K.pad_cols(Z2T, wp.shape[1], dtype=K.compute())
+        out, _ = Lyr.conv_fwd(Z2T, B, D, wp, bc, wc.shape[-1] // 2, Wf)
         ctx.mix, ctx.dims = mix, (B, Lf, C, ps, NP, D)
         ctx.stats = (m1, r1, m2, r2)
         ctx.save_for_backward(P, Z, Y1, UT, V, Z1, Y2, U2, V2, Z2T, *params)
+        ctx.twins = _twins(P, Y2, V2)  # saved tensors come back as new objects: carry the twins
         return out
 
     @staticmethod
@@ -224,15 +259,21 @@ class _MLPMixerFn(torch.autograd.Function):
         mix = ctx.mix
         B, Lf, C, ps, NP, D = ctx.dims
         m1, r1, m2, r2 = ctx.stats
+        for t, t16 in zip((P, Y2, V2), ctx.twins):
+            K.attach_twin(t, t16)
+        weC, w3C, w4C = _cf_weights(mix, we, w3, w4)
         dev = dout.device
         dout = dout.contiguous()
         pad = wc.shape[-1] // 2
         # output conv (NP -> O, k5) over the D frames
-        dwc = Lyr.conv_wgrad(dout, Z2T, B, D, D, wc, pad)
+        (_, Wd), wp = _out_conv_packs(mix, wc)
+        O, NPp, Kw = wp.shape
+        dwc = Lyr.conv_wgrad(K.twin(dout), Z2T, B, D, D, wp, pad)
+        if NPp != NP:
+            dwc = K.pad_cols(dwc.view(O, NPp * Kw), NP * Kw).view(O, NP, Kw)
         dbc = K.colsum(dout, B * D, wc.shape[0])
-        _, Wd = Lyr.conv_packs(mix.cache, wc)
-        dZ2T = Lyr.conv_dgrad(dout, B, D, D, wc, pad, Wd)
-        dZ2 = K.transpose_batched(dZ2T, B, D, NP).view(B * NP, D)
+        dZ2T = Lyr.conv_dgrad(dout, B, D, D, wp, pad, Wd, n_dx=NP)
+        dZ2 = K.twin(K.transpose_batched(dZ2T, B, D, NP).view(B * NP, D))
         M = B * NP
         # channel FF: Z2 = GELU(LN2(Z1) W3^T + b3) W4^T + b4 + Z1
         dw4 = torch.empty_like(w4)
@@ -240,14 +281,14 @@ class _MLPMixerFn(torch.autograd.Function):
                split_k=K.auto_split_k(D, 4 * D, M))
         dbb4 = K.colsum(dZ2, M, D)
         dV2 = torch.empty(M, 4 * D, device=dev)
-        K.gemm(M, 4 * D, D, operand(dZ2, D), operand(w4, 4 * D, kstrided=True), dV2)
-        dU2 = K.gelu_bwd(dV2, U2)
+        K.gemm(M, 4 * D, D, operand(dZ2, D), operand(w4C, 4 * D, kstrided=True), dV2)
+        dU2 = K.twin(K.gelu_bwd(dV2, U2))
         dw3 = torch.empty_like(w3)
         K.gemm(4 * D, D, M, operand(dU2, 4 * D, kstrided=True), operand(Y2, D, kstrided=True), dw3,
                split_k=K.auto_split_k(4 * D, D, M))
         dbb3 = K.colsum(dU2, M, 4 * D)
         dY2 = torch.empty(M, D, device=dev)
-        K.gemm(M, D, 4 * D, operand(dU2, 4 * D), operand(w3, D, kstrided=True), dY2)
+        K.gemm(M, D, 4 * D, operand(dU2, 4 * D), operand(w3C, D, kstrided=True), dY2)
         dg2 = torch.empty(D, device=dev)
         db2n = torch.empty(D, device=dev)
         dZ1 = K.add(dZ2, K.layer_norm_bwd(dY2, Z1, g2, m2, r2, dg2, db2n))
@@ -271,7 +312,7 @@ class _MLPMixerFn(torch.autograd.Function):
         dY1 = K.transpose_batched(dY1T, B, D, NP).view(M, D)
         dg1 = torch.empty(D, device=dev)
         db1n = torch.empty(D, device=dev)
-        dZ = K.add(dZ1, K.layer_norm_bwd(dY1, Z, g1, m1, r1, dg1, db1n))
+        dZ = K.twin(K.add(dZ1, K.layer_norm_bwd(dY1, Z, g1, m1, r1, dg1, db1n)))
         # patch embedding
         pp = ps * ps
         dwe = torch.empty_like(we)
@@ -281,7 +322,7 @@ class _MLPMixerFn(torch.autograd.Function):
         dnf = None
         if ctx.needs_input_grad[0]:
             dP = torch.empty(M, pp, device=dev)
-            K.gemm(M, pp, D, operand(dZ, D), operand(we, pp, kstrided=True), dP)
+            K.gemm(M, pp, D, operand(dZ, D), operand(weC, pp, kstrided=True), dP)
             dnf = K.patchify(dP, B, Lf, C, ps, backward=True)
         return (dnf, None, None, None, dwe, dbe, dg1, db1n, dW1.view_as(w1), dbb1, dW2.view_as(w2), dbb2, dg2, db2n,
                 dw3, dbb3, dw4, dbb4, dwc, dbc)

@@ -250,6 +250,10 @@ int avc_step_select(const float* src, float* dst, int B, int T, int t, int C, in
 /* Row L2 normalisation (Adjust.py:40-42) and its backward dx = (dy - y (y.dy)) / norm. */
 int avc_rownorm_fwd(const float* x, int R, int C, float* y, float* norms, void* stream);
 int avc_rownorm_bwd(const float* dy, const float* y, const float* norms, int R, int C, float* dx, void* stream);
+/* dst (R x Cd, dtype) = the first min(C, Cd) columns of src (rows lds apart), zero-filled to
+ * Cd: pads the MLP-Mixer output convolution's NP channels (1849 / 121 patches) to a multiple
+ * of 8 for the bf16 LDS-DMA kernels (MLPMixer.py:88-90) and crops its gradients back. */
+int avc_pad_cols(const float* src, long long lds, void* dst, int dtype, int R, int C, int Cd, void* stream);
 
 #ifdef __cplusplus
 }
