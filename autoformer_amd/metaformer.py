@@ -163,12 +163,29 @@ def enc_embed(mel2d, emb, proj, cache, B, T):
 
 
 # ------------------------------------------------------------------------------ MLP-Mixer
+def _pad8(n):
+    return (n + 7) // 8 * 8
+
+
 def _token_mix_weights(mix, w1, w2, NP):
-    """(W1^T (NP x 4NP), W2 (NP x 4NP)) in the compute dtype, rebuilt when w1 / w2 change."""
+    """(W1^T, W2) as (NPp x 4NPp) zero-padded matrices in the compute dtype, NPp = NP rounded
+    up to a multiple of 8 (121 -> 128, 1849 -> 1856 patches), rebuilt when w1 / w2 change.
+    The padding makes every token-mixing operand 8-aligned in K and in its row stride, which
+    the bf16 LDS-DMA GEMM kernels need; padded rows / columns are zero, so the products over
+    them add nothing."""
     def build():
         dt = K.compute()
-        return K.transpose(w1.view(4 * NP, NP), dt), K.convert(w2.view(NP, 4 * NP), dt)
+        NPp = _pad8(NP)
+        w1t = K.pad_cols(K.transpose(w1.view(4 * NP, NP), K.F32), 4 * NPp)   # (NP, 4NPp)
+        w2p = K.pad_cols(w2.view(NP, 4 * NP), 4 * NPp)                         # (NP, 4NPp)
+        rows = lambda t: K.pad_cols(t.view(1, NP * 4 * NPp), NPp * 4 * NPp, dtype=dt).view(NPp, 4 * NPp)  # noqa: E731
+        return rows(w1t), rows(w2p)
     return mix.tm_cache.get([w1, w2], build)
+
+
+def _pad_rows(x, B, NP, D, NPp):
+    """Frame-major (B*NP, D) -> (B*NPp, D) in the compute dtype, zero rows appended per utterance."""
+    return K.pad_cols(x.view(B, NP * D), NPp * D, dtype=K.compute()).view(B * NPp, D)
 
 
 def _cf_weights(mix, we, w3, w4):
@@ -228,13 +245,18 @@ class _MLPMixerFn(torch.autograd.Function):
         # token mixing: UT_b (D x 4NP) = Y1_b^T . W1^T + b1   (Conv1d(NP -> 4NP, k1) on (B, NP, D)).
         # NP (121 / 1849 patches) is never the contiguous dimension of a GEMM operand: W1 is
         # used as its transpose W1T (NP x 4NP), so every product takes the vectorised kernels.
+        # Patch counts are zero-padded to NPp (_token_mix_weights): UT / V carry 4NPp columns
+        # (padded ones stay 0: zero weights, zero bias, GELU(0) = 0), Y1 gets NPp rows.
         W1T, W2c = _token_mix_weights(mix, w1, w2, NP)
-        UT = torch.empty(B * D, 4 * NP, device=dev)
-        K.gemm(D, 4 * NP, NP, operand(Y1, D, kstrided=True, batch_stride=NP * D), operand(W1T, 4 * NP, kstrided=True),
-               UT, bias=bb1, batch=B, c_batch_stride=D * 4 * NP)
-        V = K.act_fwd(UT, K.ACT_GELU)
+        NPp = W1T.shape[0]
+        Y1 = _pad_rows(Y1, B, NP, D, NPp)
+        bb1p = K.pad_cols(bb1.view(1, 4 * NP), 4 * NPp).view(-1)
+        UT = torch.empty(B * D, 4 * NPp, device=dev)
+        K.gemm(D, 4 * NPp, NPp, operand(Y1, D, kstrided=True, batch_stride=NPp * D),
+               operand(W1T, 4 * NPp, kstrided=True), UT, bias=bb1p, batch=B, c_batch_stride=D * 4 * NPp)
+        V = K.twin(K.act_fwd(UT, K.ACT_GELU))
         RT = torch.empty(B * D, NP, device=dev)
-        K.gemm(D, NP, 4 * NP, operand(V, 4 * NP, batch_stride=D * 4 * NP), operand(W2c, 4 * NP), RT, bias=bb2,
+        K.gemm(D, NP, 4 * NPp, operand(V, 4 * NPp, batch_stride=D * 4 * NPp), operand(W2c, 4 * NPp), RT, bias=bb2,
                batch=B, c_batch_stride=D * NP)
         Z1 = K.transpose_batched(RT, B, D, NP, out=K.convert(Z, K.F32), accumulate=True).view(B * NP, D)
         Y2, m2, r2 = K.layer_norm_fwd(Z1, g2, b2n, mix.ln_eps[1])
@@ -249,7 +271,7 @@ class _MLPMixerFn(torch.autograd.Function):
         ctx.mix, ctx.dims = mix, (B, Lf, C, ps, NP, D)
         ctx.stats = (m1, r1, m2, r2)
         ctx.save_for_backward(P, Z, Y1, UT, V, Z1, Y2, U2, V2, Z2T, *params)
-        ctx.twins = _twins(P, Y2, V2)  # saved tensors come back as new objects: carry the twins
+        ctx.twins = _twins(P, Y2, V2, V)  # saved tensors come back as new objects: carry the twins
         return out
 
     @staticmethod
@@ -259,7 +281,7 @@ class _MLPMixerFn(torch.autograd.Function):
         mix = ctx.mix
         B, Lf, C, ps, NP, D = ctx.dims
         m1, r1, m2, r2 = ctx.stats
-        for t, t16 in zip((P, Y2, V2), ctx.twins):
+        for t, t16 in zip((P, Y2, V2, V), ctx.twins):
             K.attach_twin(t, t16)
         weC, w3C, w4C = _cf_weights(mix, we, w3, w4)
         dev = dout.device
@@ -295,20 +317,22 @@ class _MLPMixerFn(torch.autograd.Function):
         # token FF: Z1 = Z + (GELU(Y1^T W1^T + b1) W2^T + b2)^T   per utterance.  dRT_b = dZ1_b^T is
         # read in place from dZ1 (as the transposed operand), so NP is never a contiguous dimension.
         W1T, W2c = _token_mix_weights(mix, w1, w2, NP)
+        NPp = W1T.shape[0]
+        dZ1p = _pad_rows(dZ1, B, NP, D, NPp)
         dW2 = torch.empty(NP, 4 * NP, device=dev)
-        _batch_summed_gemm(NP, 4 * NP, D, operand(dZ1, D, batch_stride=NP * D),
-                           operand(V, 4 * NP, kstrided=True, batch_stride=D * 4 * NP), B, dW2)
+        _batch_summed_gemm(NP, 4 * NP, D, operand(dZ1p, D, batch_stride=NPp * D),
+                           operand(V, 4 * NPp, kstrided=True, batch_stride=D * 4 * NPp), B, dW2)
         dbb2 = K.colsum(K.transpose_batched(dZ1, B, NP, D).view(B * D, NP), B * D, NP)
-        dV = torch.empty(B * D, 4 * NP, device=dev)
-        K.gemm(D, 4 * NP, NP, operand(dZ1, D, kstrided=True, batch_stride=NP * D), operand(W2c, 4 * NP, kstrided=True),
-               dV, batch=B, c_batch_stride=D * 4 * NP)
-        dUT = K.gelu_bwd(dV, UT)
+        dV = torch.empty(B * D, 4 * NPp, device=dev)
+        K.gemm(D, 4 * NPp, NPp, operand(dZ1p, D, kstrided=True, batch_stride=NPp * D),
+               operand(W2c, 4 * NPp, kstrided=True), dV, batch=B, c_batch_stride=D * 4 * NPp)
+        dUT = K.twin(K.gelu_bwd(dV, UT))
         dW1 = torch.empty(4 * NP, NP, device=dev)
-        _batch_summed_gemm(4 * NP, NP, D, operand(dUT, 4 * NP, kstrided=True, batch_stride=D * 4 * NP),
-                           operand(Y1, D, batch_stride=NP * D), B, dW1)
-        dbb1 = K.colsum(dUT, B * D, 4 * NP)
+        _batch_summed_gemm(4 * NP, NP, D, operand(dUT, 4 * NPp, kstrided=True, batch_stride=D * 4 * NPp),
+                           operand(Y1, D, batch_stride=NPp * D), B, dW1)
+        dbb1 = K.colsum(dUT, B * D, 4 * NP, ld=4 * NPp)
         dY1T = torch.empty(B * D, NP, device=dev)
-        K.gemm(B * D, NP, 4 * NP, operand(dUT, 4 * NP), operand(W1T, 4 * NP), dY1T)
+        K.gemm(B * D, NP, 4 * NPp, operand(dUT, 4 * NPp), operand(W1T, 4 * NPp), dY1T)
         dY1 = K.transpose_batched(dY1T, B, D, NP).view(M, D)
         dg1 = torch.empty(D, device=dev)
         db1n = torch.empty(D, device=dev)
