@@ -249,6 +249,8 @@ class _MLPMixerFn(torch.autograd.Function):
         # (padded ones stay 0: zero weights, zero bias, GELU(0) = 0), Y1 gets NPp rows.
         W1T, W2c = _token_mix_weights(mix, w1, w2, NP)
         NPp = W1T.shape[0]
+        # Y1^T per utterance, (B*D, NPp): the K = B*D operand of the dW1 product (backward)
+        Y1T = K.pad_cols(K.transpose_batched(Y1, B, NP, D).view(B * D, NP), NPp, dtype=K.compute())
         Y1 = _pad_rows(Y1, B, NP, D, NPp)
         bb1p = K.pad_cols(bb1.view(1, 4 * NP), 4 * NPp).view(-1)
         UT = torch.empty(B * D, 4 * NPp, device=dev)
@@ -270,13 +272,13 @@ class _MLPMixerFn(torch.autograd.Function):
         out, _ = Lyr.conv_fwd(Z2T, B, D, wp, bc, wc.shape[-1] // 2, Wf)
         ctx.mix, ctx.dims = mix, (B, Lf, C, ps, NP, D)
         ctx.stats = (m1, r1, m2, r2)
-        ctx.save_for_backward(P, Z, Y1, UT, V, Z1, Y2, U2, V2, Z2T, *params)
+        ctx.save_for_backward(P, Z, Y1T, UT, V, Z1, Y2, U2, V2, Z2T, *params)
         ctx.twins = _twins(P, Y2, V2, V)  # saved tensors come back as new objects: carry the twins
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        (P, Z, Y1, UT, V, Z1, Y2, U2, V2, Z2T, we, be, g1, b1n, w1, bb1, w2, bb2, g2, b2n, w3, bb3, w4, bb4, wc,
+        (P, Z, Y1T, UT, V, Z1, Y2, U2, V2, Z2T, we, be, g1, b1n, w1, bb1, w2, bb2, g2, b2n, w3, bb3, w4, bb4, wc,
          bc) = ctx.saved_tensors
         mix = ctx.mix
         B, Lf, C, ps, NP, D = ctx.dims
@@ -319,17 +321,24 @@ class _MLPMixerFn(torch.autograd.Function):
         W1T, W2c = _token_mix_weights(mix, w1, w2, NP)
         NPp = W1T.shape[0]
         dZ1p = _pad_rows(dZ1, B, NP, D, NPp)
-        dW2 = torch.empty(NP, 4 * NP, device=dev)
-        _batch_summed_gemm(NP, 4 * NP, D, operand(dZ1p, D, batch_stride=NPp * D),
-                           operand(V, 4 * NPp, kstrided=True, batch_stride=D * 4 * NPp), B, dW2)
-        dbb2 = K.colsum(K.transpose_batched(dZ1, B, NP, D).view(B * D, NP), B * D, NP)
+        # Token-mixing weight gradients sum over utterances AND the D positions: with the
+        # per-utterance transposes (B*D rows) that sum is the K dimension of ONE product
+        # (K = B*D, both operands K-strided), with no per-utterance slabs to reduce.
+        dRT = K.transpose_batched(dZ1, B, NP, D).view(B * D, NP)
+        dbb2 = K.colsum(dRT, B * D, NP)
+        dRTp = K.pad_cols(dRT, NPp, dtype=K.compute())
+        dW2p = torch.empty(NPp, 4 * NPp, device=dev)
+        K.gemm(NPp, 4 * NPp, B * D, operand(dRTp, NPp, kstrided=True), operand(V, 4 * NPp, kstrided=True), dW2p,
+               split_k=K.auto_split_k(NPp, 4 * NPp, B * D))
+        dW2 = K.pad_cols(dW2p, 4 * NP)[:NP]
         dV = torch.empty(B * D, 4 * NPp, device=dev)
         K.gemm(D, 4 * NPp, NPp, operand(dZ1p, D, kstrided=True, batch_stride=NPp * D),
                operand(W2c, 4 * NPp, kstrided=True), dV, batch=B, c_batch_stride=D * 4 * NPp)
         dUT = K.twin(K.gelu_bwd(dV, UT))
-        dW1 = torch.empty(4 * NP, NP, device=dev)
-        _batch_summed_gemm(4 * NP, NP, D, operand(dUT, 4 * NPp, kstrided=True, batch_stride=D * 4 * NPp),
-                           operand(Y1, D, batch_stride=NPp * D), B, dW1)
+        dW1p = torch.empty(4 * NPp, NPp, device=dev)
+        K.gemm(4 * NPp, NPp, B * D, operand(dUT, 4 * NPp, kstrided=True), operand(Y1T, NPp, kstrided=True), dW1p,
+               split_k=K.auto_split_k(4 * NPp, NPp, B * D))
+        dW1 = K.pad_cols(dW1p, NP)[:4 * NP]
         dbb1 = K.colsum(dUT, B * D, 4 * NP, ld=4 * NPp)
         dY1T = torch.empty(B * D, NP, device=dev)
         K.gemm(B * D, NP, 4 * NPp, operand(dUT, 4 * NPp), operand(W1T, 4 * NPp), dY1T)
@@ -350,17 +359,6 @@ class _MLPMixerFn(torch.autograd.Function):
             dnf = K.patchify(dP, B, Lf, C, ps, backward=True)
         return (dnf, None, None, None, dwe, dbe, dg1, db1n, dW1.view_as(w1), dbb1, dW2.view_as(w2), dbb2, dg2, db2n,
                 dw3, dbb3, dw4, dbb4, dwc, dbc)
-
-
-def _batch_summed_gemm(M, N, Kd, a, b, B, out):
-    """out = sum_b A_b . B_b for a batched operand pair.  One C per batch element into a
-    scratch slab, then one column-sum pass over the B slabs: a batch-summed GEMM with atomics
-    on a shared C moves every tile's 64 KB through L2 atomics once per batch element (3.6 GB for
-    the MetaConv token-mixing weight gradients, ~5 ms), the slab costs one write + one read."""
-    tmp = torch.empty(B, M, N, device=out.device)
-    K.gemm(M, N, Kd, a, b, tmp, batch=B, c_batch_stride=M * N)
-    K.colsum(tmp.view(B, M * N), B, M * N, out=out.view(-1))
-    return out
 
 
 def mlp_mixer(nf, mixer, B, Lf):
