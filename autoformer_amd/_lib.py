@@ -101,6 +101,7 @@ _SIGS = {
     "avc_rownorm_fwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "avc_rownorm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "avc_pad_cols": (c_int, [c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "avc_gelu_twin": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p]),
 }
 
 _lib = None

@@ -241,6 +241,37 @@ __global__ void pad_cols_kernel(const float* __restrict__ src, long long lds, TO
   dst[i] = (TO)(c < C ? src[r * lds + c] : 0.f);
 }
 
+// GELU (erf form, MLPMixer.py:9-14 nn.GELU) forward (bwd = 0: v = gelu(x)) or backward
+// (bwd = 1: v = g * gelu'(x)) writing the fp32 result and/or its bf16 GEMM-operand twin in
+// the same pass (either pointer may be null), four elements per thread.
+__global__ void gelu_twin_kernel(const float* __restrict__ g, const float* __restrict__ x, float* __restrict__ y,
+                                 bf16* __restrict__ y16, long long n, int bwd) {
+  const long long i0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i0 >= n) return;
+  float v[4];
+  const bool full = i0 + 3 < n;
+  if (full) {
+    const f32x4 xv = *reinterpret_cast<const f32x4*>(x + i0);
+    f32x4 gv = {1.f, 1.f, 1.f, 1.f};
+    if (bwd) gv = *reinterpret_cast<const f32x4*>(g + i0);
+    for (int k = 0; k < 4; ++k) {
+      const float a = xv[k];
+      const float cdf = 0.5f * (1.f + erff(a * 0.70710678118654752f));
+      v[k] = bwd ? gv[k] * (cdf + a * 0.39894228040143267794f * expf(-0.5f * a * a)) : a * cdf;
+    }
+    if (y) *reinterpret_cast<f32x4*>(y + i0) = f32x4{v[0], v[1], v[2], v[3]};
+    if (y16) *reinterpret_cast<bf16x4*>(y16 + i0) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  } else {
+    for (long long i = i0; i < n; ++i) {
+      const float a = x[i];
+      const float cdf = 0.5f * (1.f + erff(a * 0.70710678118654752f));
+      const float r = bwd ? g[i] * (cdf + a * 0.39894228040143267794f * expf(-0.5f * a * a)) : a * cdf;
+      if (y) y[i] = r;
+      if (y16) y16[i] = (bf16)r;
+    }
+  }
+}
+
 inline int blocks_for(long long n, int per) { return (int)((n + per - 1) / per); }
 
 int reduce2(const float* x, const float* g, long long n, const float* mom, int mode, double* ws, float* out,
@@ -329,4 +360,14 @@ extern "C" int avc_pad_cols(const float* src, long long lds, void* dst, int dtyp
   else
     pad_cols_kernel<float><<<blocks_for(n, 256), 256, 0, s>>>(src, lds, reinterpret_cast<float*>(dst), R, C, Cd);
   return avc_check_launch("avc_pad_cols");
+}
+
+extern "C" int avc_gelu_twin(const float* g, const float* x, float* y, void* y16, long long n, int bwd,
+                             void* stream) {
+  AVC_CHECK_ARG(x && (y || y16) && n > 0 && (!bwd || g), "avc_gelu_twin: bad arguments (n=%lld)", n);
+  AVC_CHECK_ARG((((uintptr_t)x | (uintptr_t)y | (uintptr_t)g) & 15) == 0 && ((uintptr_t)y16 & 7) == 0,
+                "avc_gelu_twin: unaligned operand");
+  gelu_twin_kernel<<<blocks_for(n, 4 * 256), 256, 0, (hipStream_t)stream>>>(g, x, y, reinterpret_cast<bf16*>(y16), n,
+                                                                             bwd);
+  return avc_check_launch("avc_gelu_twin");
 }

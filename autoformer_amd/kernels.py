@@ -557,3 +557,21 @@ def pad_cols(src, Cd, dtype=F32, C=None):
     out = torch.empty(R, Cd, device=src.device, dtype=tdt)
     L.call("avc_pad_cols", src.data_ptr(), lds, out.data_ptr(), dtype, R, C, Cd, stream())
     return out
+
+
+def gelu_fwd_operand(x):
+    """GELU(x) as a GEMM operand: in bf16 mode only the bf16 tensor is written (the fp32
+    activation is never read by anything but GEMMs); fp32 mode: the fp32 result."""
+    if _COMPUTE != BF16:
+        return act_fwd(x, ACT_GELU)
+    y16 = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)
+    L.call("avc_gelu_twin", None, x.data_ptr(), None, y16.data_ptr(), x.numel(), 0, stream())
+    return y16
+
+
+def gelu_bwd_twin(g, x):
+    """g * GELU'(x) in fp32 with its bf16 twin attached (bf16 mode), one pass."""
+    dx = torch.empty_like(x)
+    d16 = _twin_buf(dx, None)
+    L.call("avc_gelu_twin", g.data_ptr(), x.data_ptr(), dx.data_ptr(), _ptr(d16), x.numel(), 1, stream())
+    return attach_twin(dx, d16)

@@ -256,15 +256,15 @@ class _MLPMixerFn(torch.autograd.Function):
         UT = torch.empty(B * D, 4 * NPp, device=dev)
         K.gemm(D, 4 * NPp, NPp, operand(Y1, D, kstrided=True, batch_stride=NPp * D),
                operand(W1T, 4 * NPp, kstrided=True), UT, bias=bb1p, batch=B, c_batch_stride=D * 4 * NPp)
-        V = K.twin(K.act_fwd(UT, K.ACT_GELU))
+        V = K.gelu_fwd_operand(UT)
         RT = torch.empty(B * D, NP, device=dev)
         K.gemm(D, NP, 4 * NPp, operand(V, 4 * NPp, batch_stride=D * 4 * NPp), operand(W2c, 4 * NPp), RT, bias=bb2,
                batch=B, c_batch_stride=D * NP)
         Z1 = K.transpose_batched(RT, B, D, NP, out=K.convert(Z, K.F32), accumulate=True).view(B * NP, D)
         Y2, m2, r2 = K.layer_norm_fwd(Z1, g2, b2n, mix.ln_eps[1])
         U2 = _lin(K.twin(Y2), B * NP, 4 * D, D, w3C, bb3)
-        V2 = K.act_fwd(U2, K.ACT_GELU)
-        Z2 = _lin(K.twin(V2), B * NP, D, 4 * D, w4C, bb4, residual=Z1)
+        V2 = K.gelu_fwd_operand(U2)
+        Z2 = _lin(V2, B * NP, D, 4 * D, w4C, bb4, residual=Z1)
         Z2T = K.transpose_batched(Z2, B, NP, D).view(B * D, NP)
         (Wf, _), wp = _out_conv_packs(mix, wc)
         if wp.shape[1] != NP:  # padded patch channels, written once in the compute dtype
@@ -306,7 +306,7 @@ class _MLPMixerFn(torch.autograd.Function):
         dbb4 = K.colsum(dZ2, M, D)
         dV2 = torch.empty(M, 4 * D, device=dev)
         K.gemm(M, 4 * D, D, operand(dZ2, D), operand(w4C, 4 * D, kstrided=True), dV2)
-        dU2 = K.twin(K.gelu_bwd(dV2, U2))
+        dU2 = K.gelu_bwd_twin(dV2, U2)
         dw3 = torch.empty_like(w3)
         K.gemm(4 * D, D, M, operand(dU2, 4 * D, kstrided=True), operand(Y2, D, kstrided=True), dw3,
                split_k=K.auto_split_k(4 * D, D, M))
@@ -334,7 +334,7 @@ class _MLPMixerFn(torch.autograd.Function):
         dV = torch.empty(B * D, 4 * NPp, device=dev)
         K.gemm(D, 4 * NPp, NPp, operand(dZ1p, D, kstrided=True, batch_stride=NPp * D),
                operand(W2c, 4 * NPp, kstrided=True), dV, batch=B, c_batch_stride=D * 4 * NPp)
-        dUT = K.twin(K.gelu_bwd(dV, UT))
+        dUT = K.gelu_bwd_twin(dV, UT)
         dW1p = torch.empty(4 * NPp, NPp, device=dev)
         K.gemm(4 * NPp, NPp, B * D, operand(dUT, 4 * NPp, kstrided=True), operand(Y1T, NPp, kstrided=True), dW1p,
                split_k=K.auto_split_k(4 * NPp, NPp, B * D))

@@ -254,6 +254,10 @@ int avc_rownorm_bwd(const float* dy, const float* y, const float* norms, int R, 
  * Cd: pads the MLP-Mixer output convolution's NP channels (1849 / 121 patches) to a multiple
  * of 8 for the bf16 LDS-DMA kernels (MLPMixer.py:88-90) and crops its gradients back. */
 int avc_pad_cols(const float* src, long long lds, void* dst, int dtype, int R, int C, int Cd, void* stream);
+/* GELU forward (bwd = 0: y = gelu(x)) or backward (bwd = 1: y = g * gelu'(x)) with the
+ * fp32 result and/or its bf16 GEMM-operand twin from one pass (y or y16 may be null):
+ * the MLP-Mixer hidden activations (MLPMixer.py:9-14) feed only GEMMs and bias sums. */
+int avc_gelu_twin(const float* g, const float* x, float* y, void* y16, long long n, int bwd, void* stream);
 
 #ifdef __cplusplus
 }
