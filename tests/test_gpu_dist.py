@@ -23,15 +23,16 @@ def _free_port():
     return p
 
 
-def _run_steps(steps=2):
+def _run_steps(name="AutoVC", steps=2):
+    import importlib
+
     import autoformer_amd as A
     from autoformer_amd.detinit import det_init_, det_inputs
-    from autoformer_amd.factory.AutoVC import AutoVC
     from autoformer_amd.layers import set_grad_sink
     from autoformer_amd.train import TrainStep
 
     A.set_compute("fp32")
-    m = AutoVC(44, 256, 512, FREQ)
+    m = getattr(importlib.import_module(f"autoformer_amd.factory.{name}"), name)(44, 256, 512, FREQ)
     det_init_(m)
     m = m.to("cuda:0").train()
     x, e = det_inputs(B, T, seed=11)
@@ -47,7 +48,7 @@ def _run_steps(steps=2):
     return ts.flat.cpu().numpy(), overlapped  # numpy: pickled by value through the queue
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, name):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     import torch.distributed as dist
@@ -56,7 +57,7 @@ def _worker(rank, world, port, q):
 
     try:
         D.init_from_env("gloo")
-        flat, overlapped = _run_steps()
+        flat, overlapped = _run_steps(name)
         q.put((rank, flat, overlapped))
         dist.barrier()
         dist.destroy_process_group()
@@ -65,20 +66,24 @@ def _worker(rank, world, port, q):
         raise
 
 
+# AutoVC and the AdaIN variant overlap the decoder-slice all-reduce with the encoder backward;
+# the Adjust variant's `adjust` gradients complete only with the encoder's, so it averages
+# everything after the backward (TrainStep.split is None)
 @pytest.mark.timeout(240)
-def test_dp_world2_overlapped_allreduce_matches_single_process():
-    single, _ = _run_steps()
+@pytest.mark.parametrize("name,expect_overlap", [("AutoVC", True), ("AutoVC2", True), ("AutoVC_Adjust", False)])
+def test_dp_world2_overlapped_allreduce_matches_single_process(name, expect_overlap):
+    single, _ = _run_steps(name)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, name)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
     for _ in range(2):
         rank, flat, overlapped = q.get(timeout=200)
         assert not isinstance(flat, str), flat
-        assert overlapped, "the decoder-slice all-reduce was not overlapped with the backward"
+        assert overlapped == expect_overlap, "unexpected all-reduce overlap mode"
         res[rank] = flat
     for p in procs:
         p.join(60)
