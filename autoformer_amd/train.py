@@ -115,8 +115,8 @@ def vc_losses(model, x_real, emb, lambda_cd=1.0):
 
 
 def adain_losses(model, x_real, emb, lambda_cd=1.0):
-    """train.py's loss block for the AdaIN variants (AutoVC2 & co.), whose c_trg=None pass
-    returns (codes, features) (AutoVC2.py:219-220): the re-pass codes are its first element."""
+    """train.py's loss block with isadain=True (train.py:89-92) for the AdaIN variants
+    (AutoVC2 & co.), whose c_trg=None pass returns (codes, features) (AutoVC2.py:219-220)."""
     x_id, x_id_psnt, code_real = model(x_real, emb, emb)
     l_id = mse_loss(x_real, x_id.squeeze())
     l_id_psnt = mse_loss(x_real, x_id_psnt.squeeze())
@@ -310,7 +310,9 @@ class Solver:
             x_real = x_real.to(self.device)
             emb_org = emb_org.to(self.device)
             self.VC = self.VC.train()
-            vc_loss, parts, _ = vc_losses(self.VC, x_real, emb_org, self.lambda_cd)
+            # train.py:89-92: with isadain the re-pass returns (codes, features)
+            step_losses = adain_losses if self.isadain else vc_losses
+            vc_loss, parts, _ = step_losses(self.VC, x_real, emb_org, self.lambda_cd)
             self.reset_grad()
             vc_loss.backward()
             self.vc_optimizer.step()

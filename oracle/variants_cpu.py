@@ -200,9 +200,8 @@ def adjust_step_losses(forward, x, emb, lambda_cd=1.0, lambda_ad=1.0):
 
 
 def adain_step_losses(forward, x, emb):
-    """A train.py-shaped step for the AdaIN variants: the reference has no trainer for them
-    (train.py:92 would receive a (codes, features) tuple), so the re-pass takes its codes
-    from the first element — the loss formula of train.py:84-96 otherwise."""
+    """train.py's step with isadain=True (train.py:89-92, `--use_adain`): the re-pass returns
+    (codes, features) and its codes are the first element; the loss formula of train.py:84-96."""
     x_id, x_id_psnt, code_real = forward(x, emb, emb)
     l_id = F.mse_loss(x, x_id.squeeze())
     l_id_psnt = F.mse_loss(x, x_id_psnt.squeeze())

@@ -11,8 +11,8 @@ closed-form weights of autoformer_amd.detinit and records, per model, B=2, T=176
   step_*               one training step's outputs, losses, gradient norms / heads and BN
                        running stats:
                          *_Adjust: the train_with_adjust.py:96-124 formula (4 losses)
-                         *2:       train.py's formula with the re-pass codes taken from the
-                                   (codes, features) tuple (no reference trainer drives them)
+                         *2:       train.py's formula with isadain=True (train.py:89-92:
+                                   the re-pass codes from the (codes, features) tuple)
   feats                (*2) the 6 feature scalars [mean, std] x 3 of the step's full pass
   conv_*               a forward of a freshly initialised model in train mode:
                          *2:       target_feature from a second utterance batch

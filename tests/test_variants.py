@@ -287,3 +287,30 @@ def test_gpu_adjust_shared_pass_equals_two_passes():
         assert torch.equal(s1[k], s2[k]), k
     for n in g1:
         torch.testing.assert_close(g1[n], g2[n], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["AutoVC2", "AutoVC_Adjust"])
+def test_gpu_solver_mirrors_reference_trainers(name):
+    """train.Solver with isadain=True (train.py:89-92) drives the AdaIN variant and
+    train.AdjustSolver (train_with_adjust.py) the Adjust variant: the first iteration's
+    losses equal the reference step's."""
+    from types import SimpleNamespace
+
+    import autoformer_amd as AA
+    from autoformer_amd.detinit import det_init_
+    from autoformer_amd.layers import set_grad_sink
+    from autoformer_amd.train import AdjustSolver, Solver
+
+    set_grad_sink(False)
+    AA.set_compute("fp32")
+    g = _golden(name)
+    x, e = torch.from_numpy(g["x"]), torch.from_numpy(g["emb"])
+    cfg = SimpleNamespace(lambda_cd=1, lambda_ad=1, dim_neck=44, dim_emb=256, dim_pre=512, freq=22,
+                          isadain=name == "AutoVC2", model_name=name, batch_size=2, num_iters=2,
+                          device=torch.device("cuda:0"), log_step=1)
+    solver = (AdjustSolver if name.endswith("_Adjust") else Solver)([(x, e)], cfg)
+    det_init_(solver.VC)
+    hist = solver.train()
+    np.testing.assert_allclose(hist[0], g["step_losses"], rtol=1e-4)
+    assert np.all(np.isfinite(hist[1]))
