@@ -234,11 +234,19 @@ __global__ void __launch_bounds__(256) rownorm_bwd_kernel(const float* __restric
 template <typename TO>
 __global__ void pad_cols_kernel(const float* __restrict__ src, long long lds, TO* __restrict__ dst, int R, int C,
                                 int Cd) {
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long long)R * Cd) return;
-  const int c = (int)(i % Cd);
-  const long long r = i / Cd;
-  dst[i] = (TO)(c < C ? src[r * lds + c] : 0.f);
+  // rows on grid.y (strided past 65535), four consecutive columns per thread: no 64-bit
+  // division per element
+  const int c0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (c0 >= Cd) return;
+  for (int r = blockIdx.y; r < R; r += gridDim.y) {
+    const float* s = src + (long long)r * lds;
+    TO* d = dst + (long long)r * Cd;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = c0 + k;
+      if (c < Cd) d[c] = (TO)(c < C ? s[c] : 0.f);
+    }
+  }
 }
 
 // GELU (erf form, MLPMixer.py:9-14 nn.GELU) forward (bwd = 0: v = gelu(x)) or backward
@@ -353,12 +361,12 @@ extern "C" int avc_pad_cols(const float* src, long long lds, void* dst, int dtyp
                             void* stream) {
   AVC_CHECK_ARG(src && dst && R > 0 && C > 0 && Cd > 0 && lds >= C, "avc_pad_cols: bad shape R=%d C=%d Cd=%d", R,
                 C, Cd);
-  const long long n = (long long)R * Cd;
   hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)((Cd + 1023) / 1024), (unsigned)std::min(R, 65535));
   if (dtype == AVC_BF16)
-    pad_cols_kernel<bf16><<<blocks_for(n, 256), 256, 0, s>>>(src, lds, reinterpret_cast<bf16*>(dst), R, C, Cd);
+    pad_cols_kernel<bf16><<<grid, 256, 0, s>>>(src, lds, reinterpret_cast<bf16*>(dst), R, C, Cd);
   else
-    pad_cols_kernel<float><<<blocks_for(n, 256), 256, 0, s>>>(src, lds, reinterpret_cast<float*>(dst), R, C, Cd);
+    pad_cols_kernel<float><<<grid, 256, 0, s>>>(src, lds, reinterpret_cast<float*>(dst), R, C, Cd);
   return avc_check_launch("avc_pad_cols");
 }
 
