@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip"]
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -58,6 +58,9 @@ _SIGS = {
     "avc_lstm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                              c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "avc_lstm_trace": (c_int, [c_void_p]),
+    "avc_set_fault_word": (c_int, [c_void_p]),
+    "avc_lstm_set_spin": (c_int, [ctypes.c_uint]),
+    "avc_lstm_persistent": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "avc_enc_concat": (c_int, [c_void_p, c_ll, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_codes_gather": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_codes_scatter": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
@@ -112,8 +115,11 @@ def build(verbose: bool = False, force: bool = False) -> str:
     """Compile csrc/*.hip for gfx950 into libautovc_hip.so (in-tree)."""
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     if not force and os.path.exists(LIB_PATH):
-        newest = max(os.path.getmtime(p) for p in srcs + [os.path.join(CSRC, "common.h"),
-                                                          os.path.join(HERE, "..", "include", "autovc_hip.h")])
+        import glob
+
+        # every header a translation unit includes (csrc/*.h, the public ABI header)
+        deps = srcs + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(HERE, "..", "include", "autovc_hip.h")]
+        newest = max(os.path.getmtime(p) for p in deps)
         if os.path.getmtime(LIB_PATH) >= newest:
             return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

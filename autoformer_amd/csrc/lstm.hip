@@ -20,7 +20,9 @@
 //    grid-wide sync (cheaper on gfx950 than a software grid barrier at 256 workgroups,
 //    MI355X_MICROARCH.md rows "boundary" vs "barrier-xcd"); the host loop is
 //    graph-capturable.
+#include <atomic>
 #include <cstdlib>
+#include <mutex>
 
 #include "common.h"
 
@@ -740,6 +742,8 @@ struct PersistArgs {
   unsigned* ctl;              // scratch: ctl[0] timeout flag, flags from word 4
   bf16* pay;                  // payload [2][B][H]
   unsigned long long* trace;  // diagnostics (avc_lstm_trace), null in production
+  unsigned* fault;            // process fault word (avc_set_fault_word), bit 0 on a spin timeout; nullable
+  unsigned spin;              // spin bound per wait (PSPIN unless avc_lstm_set_spin / AVC_LSTM_SPIN)
   int B, T, ng;
 };
 
@@ -758,8 +762,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, long lo
 }
 
 // Wave 0: poll the NR flag words of the group (one lane each, sc1 loads, s_sleep between
-// passes) until every member has published step `tag`.  false = spin timeout (flag raised).
-__device__ __forceinline__ bool poll_flags(unsigned* flags, int NR, unsigned tag, unsigned* ctl) {
+// passes) until every member has published step `tag`.  false = spin timeout: the launch's
+// ctl[0] and the process fault word (when registered) get bit 0, so the host sees the
+// failure at its next fault check instead of training on the unfinished outputs.
+__device__ __forceinline__ bool poll_flags(unsigned* flags, int NR, unsigned tag, unsigned* ctl, unsigned* fault,
+                                           unsigned spin) {
   const int lane = threadIdx.x & 63;
   gu32* f = (gu32*)flags;
   unsigned spins = 0;
@@ -767,8 +774,11 @@ __device__ __forceinline__ bool poll_flags(unsigned* flags, int NR, unsigned tag
     bool ok = true;
     if (lane < NR) ok = __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= tag;
     if (__all(ok)) return true;
-    if (++spins > PSPIN) {
-      if (lane == 0) atomicOr(ctl, 1u);
+    if (++spins > spin) {
+      if (lane == 0) {
+        atomicOr(ctl, 1u);
+        if (fault) atomicOr(fault, 1u);
+      }
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -875,7 +885,7 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_fwd(PersistArgs a) {
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     if (s > 0) {
       // ---- the group's h_{t-1} -> LDS A tile (rows past the batch stay zero)
-      if (w == 0 && !poll_flags(flags, H / PJU, (unsigned)s, a.ctl)) quit = 1;
+      if (w == 0 && !poll_flags(flags, H / PJU, (unsigned)s, a.ctl, a.fault, a.spin)) quit = 1;
       __syncthreads();
       if (quit) return;  // block-uniform exit after a spin timeout
       load_group<H, NCH, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
@@ -960,6 +970,8 @@ struct PersistBwdArgs {
   unsigned* ctl;       // scratch: ctl[0] timeout flag, flags from word 4
   bf16* pay;           // payload [2][B][4H]
   unsigned long long* trace;  // diagnostics (avc_lstm_trace), null in production
+  unsigned* fault;            // as PersistArgs
+  unsigned spin;
   int B, T, ng;
 };
 
@@ -1014,7 +1026,7 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
       go = gp[3 * H];
     }
     if (s > 0) {
-      if (w == 0 && !poll_flags(flags, H / PJU, (unsigned)s, a.ctl)) *quit = 1;
+      if (w == 0 && !poll_flags(flags, H / PJU, (unsigned)s, a.ctl, a.fault, a.spin)) *quit = 1;
       __syncthreads();
       if (*quit) return;  // block-uniform exit after a spin timeout
       load_group<G, NCH, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
@@ -1096,15 +1108,112 @@ constexpr size_t persist_bwd_lds() {
          (size_t)4 * PRG * PJU * 4 + 16;
 }
 
-int g_num_cus = -1;
+// ---------------------------------------------------------------- host-side launch state
+// Everything below is process-wide and set up under std::call_once / a mutex: forward calls
+// come from the Python thread, backward calls from PyTorch's autograd device thread.
+constexpr int MAXDEV = 64;
+
 int num_cus() {
-  if (g_num_cus < 0) {
-    int dev = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXDEV) return 0;
+  static std::once_flag once[MAXDEV];
+  static int cus[MAXDEV];
+  std::call_once(once[dev], [dev] {
     hipDeviceProp_t prop;
-    g_num_cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-                    ? prop.multiProcessorCount : 0;
+    cus[dev] = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 0;
+  });
+  return cus[dev];
+}
+
+std::atomic<unsigned*> g_fault[MAXDEV];  // per-device fault word (avc_set_fault_word)
+std::atomic<unsigned> g_spin{0};         // 0 = PSPIN (or AVC_LSTM_SPIN)
+
+unsigned* fault_word() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXDEV) return nullptr;
+  return g_fault[dev].load(std::memory_order_acquire);
+}
+
+unsigned spin_bound() {
+  static const unsigned env = [] {
+    const char* v = getenv("AVC_LSTM_SPIN");
+    return v ? (unsigned)strtoul(v, nullptr, 10) : 0u;
+  }();
+  const unsigned s = g_spin.load(std::memory_order_relaxed);
+  return s ? s : env ? env : PSPIN;
+}
+
+// Dynamic-LDS attribute of the persistent backward kernels, set once per (kernel, device).
+template <int H>
+void set_bwd_lds_attr() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  static std::once_flag once[MAXDEV];
+  std::call_once(once[dev & (MAXDEV - 1)], [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_persist_bwd<H>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_bwd_lds<H>());
+  });
+}
+
+// Co-residency of a persistent grid: every workgroup must be resident at once (the members
+// wait on each other), so the launch is taken only when the occupancy API admits `grid`
+// workgroups over the device's CUs.  Cached per (kernel, device).
+bool fits_resident(const void* fn, int threads, size_t lds, int grid) {
+  static std::mutex mu;
+  struct Entry {
+    const void* fn;
+    int dev;
+    int blocks;
+  };
+  static Entry cache[64];
+  static int n = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  int blocks = -1;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    for (int i = 0; i < n; ++i)
+      if (cache[i].fn == fn && cache[i].dev == dev) blocks = cache[i].blocks;
+    if (blocks < 0) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, threads, lds) != hipSuccess) nb = 0;
+      (void)hipGetLastError();
+      blocks = nb;
+      if (n < 64) cache[n++] = Entry{fn, dev, nb};
+    }
   }
-  return g_num_cus;
+  return (long long)blocks * num_cus() >= grid;
+}
+
+bool no_persist_env() {
+  static const bool v = getenv("AVC_LSTM_NO_PERSIST") != nullptr;
+  return v;
+}
+
+// Whether the one-launch persistent recurrence applies (the same test the launches make).
+bool persistent_path(int B, int H, int dirs, bool bf, bool bwd) {
+  if (!bf || dirs != 1 || !(H == 1024 || H == 768 || H == 512) || no_persist_env()) return false;
+  const int ng = (B + PRG - 1) / PRG, grid = ng * (H / PJU);
+  if (grid > num_cus()) return false;
+  const void* fn;
+  size_t lds = 0;
+  if (!bwd) {
+    fn = H == 1024 ? reinterpret_cast<const void*>(&lstm_persist_fwd<1024>)
+       : H == 768  ? reinterpret_cast<const void*>(&lstm_persist_fwd<768>)
+                   : reinterpret_cast<const void*>(&lstm_persist_fwd<512>);
+  } else if (H == 1024) {
+    set_bwd_lds_attr<1024>();
+    fn = reinterpret_cast<const void*>(&lstm_persist_bwd<1024>);
+    lds = persist_bwd_lds<1024>();
+  } else if (H == 768) {
+    set_bwd_lds_attr<768>();
+    fn = reinterpret_cast<const void*>(&lstm_persist_bwd<768>);
+    lds = persist_bwd_lds<768>();
+  } else {
+    fn = reinterpret_cast<const void*>(&lstm_persist_bwd<512>);
+    lds = persist_bwd_lds<512>();
+  }
+  return fits_resident(fn, PNT, lds, grid);
 }
 
 template <int HM>
@@ -1125,6 +1234,22 @@ void launch_small_bwd(dim3 g, hipStream_t s, bool fast, const float* dh, const f
 extern "C" int avc_lstm_trace(void* buf) {
   g_trace = reinterpret_cast<unsigned long long*>(buf);
   return 0;
+}
+
+extern "C" int avc_set_fault_word(void* word) {
+  int dev = 0;
+  AVC_CHECK_ARG(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < MAXDEV, "avc_set_fault_word: no device");
+  g_fault[dev].store(reinterpret_cast<unsigned*>(word), std::memory_order_release);
+  return 0;
+}
+
+extern "C" int avc_lstm_set_spin(unsigned spins) {
+  g_spin.store(spins, std::memory_order_relaxed);
+  return 0;
+}
+
+extern "C" int avc_lstm_persistent(int B, int H, int dirs, int compute, int backward) {
+  return persistent_path(B, H, dirs, compute == AVC_BF16, backward != 0) ? 1 : 0;
 }
 
 extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T, int H, int dirs, float* h,
@@ -1160,8 +1285,7 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
   a.H = H;
   a.dirs = dirs;
   const int ng = (B + PRG - 1) / PRG;
-  static const bool no_persist = getenv("AVC_LSTM_NO_PERSIST") != nullptr;
-  if (bf && dirs == 1 && (H == 1024 || H == 768 || H == 512) && hbuf && !no_persist && ng * (H / PJU) <= num_cus()) {
+  if (hbuf && persistent_path(B, H, dirs, bf, false)) {
     // hbuf: control words + flags + the [2][B][H] bf16 payload in this mode (layout above)
     PersistArgs p;
     p.xproj = xproj;
@@ -1173,6 +1297,8 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
     p.ctl = reinterpret_cast<unsigned*>(hbuf);
     p.pay = reinterpret_cast<bf16*>(reinterpret_cast<char*>(hbuf) + px_payload_off(ng));
     p.trace = g_trace;
+    p.fault = fault_word();
+    p.spin = spin_bound();
     p.B = B;
     p.T = T;
     p.ng = ng;
@@ -1226,8 +1352,7 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
   const bool bf = compute == AVC_BF16;
   AVC_CHECK_ARG(!bf || (wdtype == AVC_BF16 && gbuf), "avc_lstm_bwd: bf16 compute needs bf16 W_hh^T and gbuf");
   const int ng = (B + PRG - 1) / PRG;
-  static const bool no_persist = getenv("AVC_LSTM_NO_PERSIST") != nullptr;
-  if (bf && dirs == 1 && (H == 1024 || H == 768 || H == 512) && !no_persist && ng * (H / PJU) <= num_cus()) {
+  if (persistent_path(B, H, dirs, bf, true)) {
     // gbuf: control words + flags + the [2][B][4H] bf16 payload in this mode (layout above)
     PersistBwdArgs p;
     p.dhout = dh_out;
@@ -1239,25 +1364,16 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
     p.ctl = reinterpret_cast<unsigned*>(gbuf);
     p.pay = reinterpret_cast<bf16*>(reinterpret_cast<char*>(gbuf) + px_payload_off(ng));
     p.trace = g_trace;
+    p.fault = fault_word();
+    p.spin = spin_bound();
     p.B = B;
     p.T = T;
     p.ng = ng;
     (void)hipMemsetAsync(gbuf, 0, px_ctl_bytes(ng), s);
+    // (persistent_path above set the dynamic-LDS attributes)
     if (H == 1024) {
-      static bool attr = false;
-      if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_persist_bwd<1024>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_bwd_lds<1024>());
-        attr = true;
-      }
       lstm_persist_bwd<1024><<<ng * (H / PJU), PNT, persist_bwd_lds<1024>(), s>>>(p);
     } else if (H == 768) {
-      static bool attr = false;
-      if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_persist_bwd<768>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_bwd_lds<768>());
-        attr = true;
-      }
       lstm_persist_bwd<768><<<ng * (H / PJU), PNT, persist_bwd_lds<768>(), s>>>(p);
     } else {
       lstm_persist_bwd<512><<<ng * (H / PJU), PNT, persist_bwd_lds<512>(), s>>>(p);

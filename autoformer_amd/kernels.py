@@ -214,9 +214,57 @@ def lstm_timeout_flag(hbuf, B, H):
 
 
 def lstm_persistent_fwd(B, H, dirs):
-    """Whether avc_lstm_fwd takes the one-launch persistent path (mirrors lstm.hip)."""
-    return _COMPUTE == BF16 and dirs == 1 and H in (512, 768, 1024) and os.environ.get("AVC_LSTM_NO_PERSIST") is None \
-        and ((B + 7) // 8) * (H // 32) <= num_cus()
+    """Whether avc_lstm_fwd takes the one-launch persistent path (asked of lstm.hip: shape,
+    compute mode and the occupancy check of the whole grid)."""
+    return bool(L.lib().avc_lstm_persistent(int(B), int(H), int(dirs), _COMPUTE, 0))
+
+
+# ------------------------------------------------------------------------- fault word
+_FAULT = {}
+
+
+def fault_word(device=None):
+    """The per-device u32 fault word registered with the library (avc_set_fault_word): bit 0
+    = a persistent LSTM recurrence timed out its bounded spin and left its outputs unfinished.
+    Created (zeroed) and registered on first use; every persistent launch reports into it."""
+    idx = None if device is None else torch.device(device).index
+    dev = torch.device("cuda", torch.cuda.current_device() if idx is None else idx)
+    w = _FAULT.get(dev.index)
+    if w is None:
+        with torch.cuda.device(dev):
+            w = torch.zeros(1, device=dev, dtype=torch.int32)
+            L.call("avc_set_fault_word", w.data_ptr())
+        _FAULT[dev.index] = w
+    return w
+
+
+class DeviceFault(RuntimeError):
+    """A HIP kernel reported a failure through the fault word (see fault_word)."""
+
+
+FAULT_BITS = {1: "persistent LSTM recurrence spin timeout (a workgroup of the grid was not resident or stalled; "
+                 "the step's outputs are invalid)"}
+
+
+def raise_on_fault(value):
+    v = int(value)
+    if v:
+        what = "; ".join(msg for bit, msg in FAULT_BITS.items() if v & bit) or "unknown fault bits"
+        raise DeviceFault(f"autoformer_amd device fault word = {v:#x}: {what}")
+
+
+def check_faults(device=None):
+    """Synchronous check of the fault word (reads it back; raises DeviceFault if set)."""
+    raise_on_fault(fault_word(device).item())
+
+
+def clear_faults(device=None):
+    fault_word(device).zero_()
+
+
+def lstm_set_spin(spins: int) -> None:
+    """Debug: spin bound of the persistent recurrences (0 restores the default)."""
+    L.call("avc_lstm_set_spin", int(spins))
 
 
 def lstm_fwd(xproj, w_hh, B, T, H, dirs, hbuf=None):
@@ -225,6 +273,8 @@ def lstm_fwd(xproj, w_hh, B, T, H, dirs, hbuf=None):
     c = torch.empty(B * T, dirs * H, device=dev)
     g = torch.empty(B * T, dirs * 4 * H, device=dev)
     h16 = None
+    if H > 64:
+        fault_word(dev)
     if hbuf is not None and H > 64 and lstm_persistent_fwd(B, H, dirs):
         h16 = torch.empty(B * T, H, device=dev, dtype=torch.bfloat16)
     L.call("avc_lstm_fwd", xproj.data_ptr(), w_hh.data_ptr(), _dt(w_hh), B, T, H, dirs, h.data_ptr(), _ptr(h16),
@@ -233,9 +283,8 @@ def lstm_fwd(xproj, w_hh, B, T, H, dirs, hbuf=None):
 
 
 def lstm_persistent_bwd(B, H, dirs):
-    """Whether avc_lstm_bwd takes the one-launch persistent path (mirrors lstm.hip)."""
-    return _COMPUTE == BF16 and dirs == 1 and H in (512, 768, 1024) and os.environ.get("AVC_LSTM_NO_PERSIST") is None \
-        and ((B + 7) // 8) * (H // 32) <= num_cus()
+    """Whether avc_lstm_bwd takes the one-launch persistent path (asked of lstm.hip)."""
+    return bool(L.lib().avc_lstm_persistent(int(B), int(H), int(dirs), _COMPUTE, 1))
 
 
 def num_cus():
@@ -270,6 +319,7 @@ def lstm_bwd(dh, h, c, g, w_hh, w_hh_t, B, T, H, dirs, gbuf=None):
     dcbuf = dg16 = None
     wdt = _dt(w_hh if w_hh_t is None else w_hh_t)
     if H > 64:
+        fault_word(dev)
         dcbuf = torch.empty(dirs * B * H, device=dev)
         if _COMPUTE == BF16:
             if gbuf is None:

@@ -3,7 +3,8 @@
 * ``Solver`` mirrors /root/reference/train.py:13-132 (same constructor, same loop, same
   losses and logging format) so existing scripts can switch by import.
 * ``GANSolver`` mirrors train_with_discriminator.py:13-145 (ONE loss for both models and
-  both Adams stepping on the same backward — kept as in the reference, not "fixed").
+  both Adams stepping on the same backward — kept as in the reference, not "fixed"); the
+  benchmark form of the same step is ``TrainStep(G, extra=gan_extra(D), extra_modules=[D])``.
 * ``AdjustSolver`` mirrors train_with_adjust.py:16-145 (the *_Adjust models, 4 losses).
 * ``TrainStep`` is the benchmark/production step: flat parameter and gradient buffers,
   HIP MSE/L1 losses, fused HIP Adam, optional RCCL gradient all-reduce and hipGraph
@@ -24,6 +25,12 @@ import torch
 from . import dist as D
 from . import kernels as K
 from .layers import join_side, prefetch_packs, set_grad_sink, side_stream, weights_changed
+
+
+def _load_state(model, path, device):
+    """torch.load(path, map_location=device) into model (train_with_adjust.py:50-54); a
+    tensors-only loader (weights_only) -- a state_dict needs nothing else."""
+    model.load_state_dict(torch.load(path, map_location=device, weights_only=True))
 
 
 # ------------------------------------------------------------------------- losses
@@ -199,6 +206,27 @@ class TrainStep:
             self.split = D.split_offset(self.params, next(model.decoder.parameters()))
             self.comm = torch.cuda.Stream()
         self._early = None
+        # fault word (kernels.fault_word): read back asynchronously after every step into a
+        # pinned word and checked at the next step, so a failed persistent recurrence raises
+        # within one step without a host sync; check() is the synchronous form
+        self._fault = K.fault_word(self.flat.device)
+        self._fault_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._fault_ev = None
+        # optional exposed all-reduce time: a list of (start, end) HIP event pairs recorded on
+        # the main stream around its wait for the collective (bench.py's allreduce_ms)
+        self.comm_timing = None
+
+    def _probe_fault(self):
+        if self._fault_ev is not None and self._fault_ev.query():
+            K.raise_on_fault(self._fault_host.item())
+        self._fault_host.copy_(self._fault, non_blocking=True)
+        self._fault_ev = torch.cuda.Event()
+        self._fault_ev.record()
+
+    def check(self):
+        """Raise DeviceFault if any kernel of the steps so far reported a fault (synchronises)."""
+        torch.cuda.synchronize()
+        K.raise_on_fault(self._fault.item())
 
     def _decoder_done(self):
         main = torch.cuda.current_stream()
@@ -223,17 +251,24 @@ class TrainStep:
         return loss
 
     def _allreduce(self):
+        timed = self.comm_timing is not None
+        if timed:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         if self._early is None:  # no overlapped part (graph replay, or no hook fired)
             D.allreduce_mean_(self.gflat)
-            return
-        main = torch.cuda.current_stream()
-        self.comm.wait_stream(main)
-        with torch.cuda.stream(self.comm):
-            late = D.allreduce_mean_async_(self.gflat[:self.split])
-            D.finish_allreduce_(self._early)
-            D.finish_allreduce_(late)
-        main.wait_stream(self.comm)
-        self._early = None
+        else:
+            main = torch.cuda.current_stream()
+            self.comm.wait_stream(main)
+            with torch.cuda.stream(self.comm):
+                late = D.allreduce_mean_async_(self.gflat[:self.split])
+                D.finish_allreduce_(self._early)
+                D.finish_allreduce_(late)
+            main.wait_stream(self.comm)
+            self._early = None
+        if timed:
+            ev[1].record()
+            self.comm_timing.append(ev)
 
     def step(self, x, emb):
         if self.graph_fb is not None:
@@ -246,6 +281,7 @@ class TrainStep:
         self.opt.step()
         if self.graph_fb is None:
             prefetch_packs()  # next step's weight packs, on the side stream
+        self._probe_fault()
         return loss
 
     def capture(self, x, emb, warmup=2):
@@ -288,9 +324,26 @@ class Solver:
     def build_model(self):
         self.VC = getattr(importlib.import_module(f"autoformer_amd.factory.{self.model_name}"), self.model_name)(
             self.dim_neck, self.dim_emb, self.dim_pre, self.freq)
+        if getattr(self, "use_pretrained_weight", False):
+            print(f"Load Pre-trained Weight --- {self.pretrained_weight_path}")
+            _load_state(self.VC, self.pretrained_weight_path, self.device)
         self.VC.to(self.device)
         _, flat, gflat = D.flatten_params_(self.VC)
         self.vc_optimizer = FusedAdam(flat, gflat, 0.0001)
+
+    def _optimize(self, loss):
+        """reset_grad; backward; Adam (train.py:97-99).  The weight-gradient kernels may still be
+        writing .grad on the side stream (gradient-sink mode): join it before Adam reads it."""
+        self.reset_grad()
+        loss.backward()
+        join_side()
+        self.vc_optimizer.step()
+
+    def _read(self, keys, parts):
+        """loss.item() of each term (train.py:103-105) plus the device fault check."""
+        loss = {k: p.item() for k, p in zip(keys, parts)}
+        K.check_faults(parts[0].device)
+        return loss
 
     def reset_grad(self):
         self.vc_optimizer.zero_grad()
@@ -313,10 +366,8 @@ class Solver:
             # train.py:89-92: with isadain the re-pass returns (codes, features)
             step_losses = adain_losses if self.isadain else vc_losses
             vc_loss, parts, _ = step_losses(self.VC, x_real, emb_org, self.lambda_cd)
-            self.reset_grad()
-            vc_loss.backward()
-            self.vc_optimizer.step()
-            loss = {k: p.item() for k, p in zip(keys, parts)}
+            self._optimize(vc_loss)
+            loss = self._read(keys, parts)
             history.append([loss[k] for k in keys])
             if (i + 1) % self.log_step == 0:
                 et = str(datetime.timedelta(seconds=time.time() - start_time))[:-7]
@@ -333,6 +384,9 @@ class AdjustSolver(Solver):
 
     def __init__(self, vcc_loader, config):
         self.lambda_ad = getattr(config, "lambda_ad", 1.0)
+        # train_with_adjust.py:32-33,50-54 (the flag is bool(str) there: any non-empty string)
+        self.use_pretrained_weight = bool(getattr(config, "use_pretrained_weight", False))
+        self.pretrained_weight_path = getattr(config, "pretrained_weight_path", None)
         super().__init__(vcc_loader, config)
 
     def train(self):
@@ -351,10 +405,67 @@ class AdjustSolver(Solver):
             emb_org = emb_org.to(self.device)
             self.VC = self.VC.train()
             g_loss, parts, _ = adjust_losses(self.VC, x_real, emb_org, self.lambda_cd, self.lambda_ad)
+            self._optimize(g_loss)
+            loss = self._read(keys, parts)
+            history.append([loss[k] for k in keys])
+            if (i + 1) % self.log_step == 0:
+                et = str(datetime.timedelta(seconds=time.time() - start_time))[:-7]
+                log = "Elapsed [{}], Iteration [{}/{}]".format(et, i + 1, self.num_iters)
+                for tag in keys:
+                    log += ", {}: {:.4f}".format(tag, loss[tag])
+                print(log)
+        return history
+
+
+class GANSolver(Solver):
+    """Mirror of train_with_discriminator.py:Solver (train_with_discriminator.py:13-145): the
+    generator step of train.py plus Discriminator() on the real and the reconstructed mel,
+    d_loss = BCE(D(x_real), 1) + BCE(D(x_psnt), 0) added to the generator loss, ONE backward,
+    then g_optimizer.step() and d_optimizer.step() (:102-111) -- the discriminator minimises
+    the same loss the generator does, as in the reference.  wandb logging (:126-134) is
+    replaced by the same line printed to stdout."""
+
+    def build_model(self):
+        from .factory.Discriminator import Discriminator
+
+        super().build_model()
+        self.G = self.VC
+        self.g_optimizer = self.vc_optimizer
+        self.D = Discriminator().to(self.device)
+        _, dflat, dgflat = D.flatten_params_(self.D)
+        self.d_optimizer = FusedAdam(dflat, dgflat, 0.0001)
+
+    def reset_grad(self):
+        self.g_optimizer.zero_grad()
+        self.d_optimizer.zero_grad()
+
+    def discriminator_loss(self, real, fake):
+        return discriminator_loss(real, fake)
+
+    def train(self):
+        keys = ["G/loss_id", "G/loss_id_psnt", "G/loss_cd", "D/loss_d"]
+        print("Start training...")
+        start_time = time.time()
+        data_iter = None
+        history = []
+        for i in range(self.num_iters):
+            try:
+                x_real, emb_org = next(data_iter)
+            except Exception:
+                data_iter = iter(self.vcc_loader)
+                x_real, emb_org = next(data_iter)
+            x_real = x_real.to(self.device)
+            emb_org = emb_org.to(self.device)
+            self.G = self.G.train()
+            g_loss, (l_id, l_id_psnt, l_cd), x_psnt = vc_losses(self.G, x_real, emb_org, self.lambda_cd)
+            d_loss = self.discriminator_loss(self.D(x_real), self.D(x_psnt.squeeze()))
+            g_loss = g_loss + d_loss
             self.reset_grad()
             g_loss.backward()
-            self.vc_optimizer.step()
-            loss = {k: p.item() for k, p in zip(keys, parts)}
+            join_side()
+            self.g_optimizer.step()
+            self.d_optimizer.step()
+            loss = self._read(keys, (l_id, l_id_psnt, l_cd, d_loss))
             history.append([loss[k] for k in keys])
             if (i + 1) % self.log_step == 0:
                 et = str(datetime.timedelta(seconds=time.time() - start_time))[:-7]

@@ -6,6 +6,11 @@ GPU, data parallel, RCCL gradient all-reduce).
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+With --gpus N > 1 and no launcher environment (WORLD_SIZE unset) the script starts the N
+ranks itself: N child processes of this script with RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 / MASTER_PORT set, started before this process touches the GPU.  Every
+rank checks that the process group it joined has exactly N ranks.
+
 Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
 """
 import argparse
@@ -104,9 +109,34 @@ def pmc_traffic(kernel):
     return None, None
 
 
-def cpu_baseline(B, T, freq, steps=2):
+def host_cores():
+    """(physical cores of the host, CPUs this process may run on)."""
+    phys = set()
+    try:
+        cur = {}
+        for line in open("/proc/cpuinfo"):
+            if ":" not in line:
+                if cur:
+                    phys.add((cur.get("physical id"), cur.get("core id")))
+                cur = {}
+                continue
+            k, v = (x.strip() for x in line.split(":", 1))
+            cur[k] = v
+        if cur:
+            phys.add((cur.get("physical id"), cur.get("core id")))
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count()
+    return len(phys) or None, aff
+
+
+def cpu_baseline(B, T, freq, steps=3):
     """The CPU oracle (oracle/autovc_cpu.py, the pinned restatement of the reference) timed on
-    this box's host cores: same step, fp32, bounded sample of 1 warm-up + `steps` steps."""
+    this box's host cores: same step, fp32, bounded sample of 1 warm-up + `steps` steps
+    (SURVEY.md §8(d)).  `cores` = the intra-op threads torch ran the oracle with."""
     from oracle import autovc_cpu as O
 
     x, e = synthetic_batch(B, T, 0, "cpu")
@@ -116,9 +146,52 @@ def cpu_baseline(B, T, freq, steps=2):
     for _ in range(steps):
         s.step(x, e)
     dt = (time.perf_counter() - t0) / steps
+    phys, aff = host_cores()
     return {"value": round(B * T / dt, 1), "unit": "mel-frames/s", "cores": torch.get_num_threads(),
-            "kind": "port", "sample": f"oracle train step B={B} T={T} freq={freq} fp32, 1 warm-up + {steps} timed "
-                                      f"steps ({dt * 1e3:.0f} ms/step)"}
+            "kind": "port", "host_physical_cores": phys, "host_cpus_allowed": aff,
+            "sample": f"oracle train step B={B} T={T} freq={freq} fp32, 1 warm-up + {steps} timed "
+                      f"steps ({dt * 1e3:.0f} ms/step), {torch.get_num_threads()} intra-op threads"}
+
+
+def launch_ranks(n):
+    """Start n ranks of this script (one per GPU) and wait for them; returns the exit code.
+    The parent never touches the GPU (torch.cuda.device_count() does not initialise HIP on
+    this image), so no process that initialised the GPU forks or execs."""
+    import socket
+    import subprocess
+
+    have = torch.cuda.device_count()
+    if have < n:
+        print(f"bench.py: --gpus {n} needs {n} visible GPUs, this node has {have}", file=sys.stderr, flush=True)
+        return 2
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                c = p.poll()
+                if c is None:
+                    continue
+                pending.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c
+                    for q in pending:  # one rank failed: the others would wait on it forever
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
 
 
 def main():
@@ -140,6 +213,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
 
     import importlib
 
@@ -148,7 +225,17 @@ def main():
     from autoformer_amd.detinit import det_init_
     from autoformer_amd.train import TrainStep, gan_extra
 
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {env_world} rank(s) "
+                         f"(WORLD_SIZE={os.environ.get('WORLD_SIZE')})")
+    if args.gpus > 1:
+        # RCCL binds the communicator to the current device when the group is created
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     rank, world, local = D.init_from_env("nccl")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {world} rank(s) "
+                         f"(WORLD_SIZE={os.environ.get('WORLD_SIZE')})")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     set_compute(args.dtype)
@@ -189,6 +276,8 @@ def main():
 
     # dominant-kernel launches inside the timed region, timed by HIP events on their stream
     K.LAUNCH_TIMING = [] if (not args.no_kernel_timing and args.model == "AutoVC") else None
+    if world > 1:
+        trainer.comm_timing = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = trainer.step(x, e)
@@ -196,10 +285,14 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    comm_ms = 0.0
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        comm_ms = sum(a.elapsed_time(b) for a, b in trainer.comm_timing) / args.steps
+        trainer.comm_timing = None
+        t = torch.tensor([elapsed, comm_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        elapsed, comm_ms = t[0].item(), t[1].item()
+    trainer.check()  # a persistent recurrence that timed out invalidates the run: raise
     loss_v = float(loss.item())
     ms = elapsed / args.steps * 1e3
     frames = world * B * T
@@ -228,6 +321,12 @@ def main():
                       "graph": bool(args.graph)},
            "step_mfma_frac": round(value * fpf / (world * peak * 1e12), 5) if fpf else None,
            "final_loss": loss_v}
+    if world > 1:
+        # main-stream time per step spent waiting for the gradient average after the backward
+        # (the decoder / postnet slice overlaps the encoder backward), max over ranks
+        out["allreduce_ms"] = round(comm_ms, 4)
+        out["allreduce_bytes_per_step"] = trainer.gflat.numel() * trainer.gflat.element_size()
+        out["collective"] = f"{dist.get_backend()} all_reduce AVG, {D.BUCKET_BYTES >> 20} MiB buckets"
     if not args.no_kernel_timing and args.model == "AutoVC":
         evs, K.LAUNCH_TIMING = K.LAUNCH_TIMING or [], None
         kt = kernel_timing(model, B, T)  # isolated replays (also: algorithmic bytes / FLOP)
@@ -235,13 +334,16 @@ def main():
             step_us = sum(a.elapsed_time(b) for a, b in evs) * 1e3 / len(evs)
         else:
             step_us = kt["avg_us"]
-        ach = kt["bytes"] / (step_us * 1e-6) / 1e9
+        # the path's roofline is dense bf16 MFMA; HBM is the secondary counter
+        tfs = kt["flops"] / (step_us * 1e-6) / 1e12
+        gbs = kt["bytes"] / (step_us * 1e-6) / 1e9
         traffic, src = pmc_traffic(DOMINANT)
-        out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                           "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": traffic, "kernel": kt["kernel"],
+        out["roofline"] = {"bound": "mfma", "achieved": round(tfs, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(tfs / PEAK_BF16_TFLOPS, 5), "traffic": traffic, "kernel": kt["kernel"],
                            "avg_us": round(step_us, 3), "launches_timed": len(evs),
-                           "avg_us_isolated": round(kt["avg_us"], 3), "alg_bytes_per_launch": kt["bytes"],
-                           "flop_per_launch": kt["flops"], "traffic_source": src}
+                           "avg_us_isolated": round(kt["avg_us"], 3), "flop_per_launch": kt["flops"],
+                           "alg_bytes_per_launch": kt["bytes"], "hbm_achieved_gbs": round(gbs, 1),
+                           "hbm_frac": round(gbs / PEAK_HBM_GBS, 5), "traffic_source": src}
     if world == 1 and not args.no_cpu_baseline and default:
         out["cpu_baseline"] = cpu_baseline(B, T, freq)
     print(json.dumps(out), flush=True)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 4
+#define AVC_ABI_VERSION 5
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -151,6 +151,24 @@ int avc_lstm_bwd(const float* dh_out, const float* h, const float* c, const floa
  * buf[(workgroup*T + step)*4 + j] (j: step start, exchange complete, product reduced,
  * published; u64, caller-sized).  null switches it off (the default). */
 int avc_lstm_trace(void* buf);
+
+/* Fault reporting (no reference counterpart; nn.LSTM cannot fail this way).  `word` is a
+ * caller-owned device u32 for the CURRENT device (null unregisters).  A persistent LSTM
+ * launch whose bounded spin times out -- a workgroup of its grid never became resident, or
+ * a member died -- ORs bit 0 into it (as well as into the launch's own ctl[0]) and exits;
+ * the host reads the word where it reads the loss and raises.  Sticky until the caller
+ * clears it. */
+int avc_set_fault_word(void* word);
+
+/* Debug: spin bound of the persistent recurrences' waits (0 = the built-in bound, or the
+ * AVC_LSTM_SPIN environment variable when set).  A tiny bound forces the timeout path. */
+int avc_lstm_set_spin(unsigned spins);
+
+/* 1 when avc_lstm_fwd (backward = 0) / avc_lstm_bwd (backward = 1) take the one-launch
+ * persistent path for this shape on the current device: bf16 compute, dirs == 1, H in
+ * {512, 768, 1024}, and the occupancy API admits the whole grid (ceil(B/8) * H/32
+ * workgroups of 512 threads) resident at once.  0 otherwise (per-step kernels). */
+int avc_lstm_persistent(int B, int H, int dirs, int compute, int backward);
 
 /* Elementwise / layout kernels of the model glue (AutoVC.py:46-48, 56-66, 197-207). */
 int avc_enc_concat(const float* mel, long long mel_ld, const float* emb, float* out, int B, int T,
