@@ -75,7 +75,7 @@ _SIGS = {
     "avc_l1_loss": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_void_p]),
     "avc_loss_grad": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_int, c_void_p, c_float, c_void_p]),
     "avc_adam": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_float, c_float, c_float, c_float, c_void_p,
-                         c_void_p]),
+                         c_int, c_void_p]),
     "avc_act_fwd": (c_int, [c_void_p, c_void_p, c_ll, c_int, c_void_p]),
     "avc_act_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p]),
     "avc_bce_loss": (c_int, [c_void_p, c_ll, c_float, c_void_p, c_void_p]),

@@ -343,10 +343,11 @@ extern "C" int avc_loss_grad(const float* a, const float* b, long long n, const 
 }
 
 extern "C" int avc_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
-                        float eps, float* state, void* stream) {
+                        float eps, float* state, int advance, void* stream) {
   AVC_CHECK_ARG(p && g && m && v && state, "avc_adam: null");
   hipStream_t s = as_stream(stream);
-  adam_prep_kernel<<<1, 1, 0, s>>>(state, lr, beta1, beta2);
+  if (advance) adam_prep_kernel<<<1, 1, 0, s>>>(state, lr, beta1, beta2);
+  if (n == 0) return avc_check_launch("avc_adam");
   int grid = (int)std::min<long long>(4096, cdiv(n, 256));
   adam_kernel<<<grid, 256, 0, s>>>(p, g, m, v, n, beta1, beta2, eps, state);
   return avc_check_launch("avc_adam");

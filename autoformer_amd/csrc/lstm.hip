@@ -29,20 +29,7 @@
 namespace {
 
 // =============================================================== small H: persistent
-// One workgroup owns one (utterance, direction) for all T steps; no inter-workgroup sync.
-// Thread (j, q) = (tid >> 2, tid & 3) owns gate q of hidden unit j, so the four gates of a
-// unit sit in one lane quad: the cell update reads them with DPP quad broadcasts and only
-// h_t (forward) / dG_t (backward) crosses lanes through LDS -- ONE workgroup barrier per
-// step, LDS double-buffered by step parity.  Forward: lane (j, q) keeps row q*H + j of W_hh
-// in registers; backward: lane (j', q) keeps column j' of gate block q, and the quad's four
-// partial products sum with DPP xor steps, leaving dh_rec[j'] in every lane of the quad.
-// The per-step inputs (xproj rows forward; dh, c, c_prev, gates backward) are staged in LDS
-// one chunk of SC steps ahead, and the per-step outputs are collected in LDS and written to
-// HBM once per chunk: a step issues no global memory operation at all.  (A global store per
-// step made the next step's reuse of its address registers wait on vmcnt(0) -- for the
-// store AND the whole in-flight prefetch -- every step.)  The SC steps of a chunk are
-// unrolled, so no loop boundary makes the compiler drain the prefetch early.
-constexpr int SC = 16;
+// (the encoder BiLSTM, H = 44; no inter-workgroup sync -- design at lstm_small_fwd below)
 
 __device__ __forceinline__ float fsig(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float ftanh(float x) { return 2.f * fsig(2.f * x) - 1.f; }
@@ -66,91 +53,157 @@ __device__ __forceinline__ float quad_sum(float v) {
   return v;
 }
 
-template <int HM, bool FAST>
-__global__ void __launch_bounds__(256) lstm_small_fwd(const float* __restrict__ xproj, const float* __restrict__ whh,
-                                                      int T, int H, int dirs, float* __restrict__ hout,
-                                                      float* __restrict__ cout, float* __restrict__ gout) {
-  constexpr int GM = 4 * HM, NPF = (SC * GM + 255) / 256;
-  const int b = blockIdx.x, d = blockIdx.y, tid = threadIdx.x;
-  const int G = 4 * H;
-  const int j = tid >> 2, q = tid & 3, row = q * H + j;
-  const bool act = j < H;
-  __shared__ __attribute__((aligned(16))) float hs[2][HM];
-  __shared__ float xs[2][SC * GM];
-  __shared__ float gst[SC * GM], hst[SC * HM], cst[SC * HM];  // the chunk's outputs, flushed at its end
-  float w[HM];
-  const float* W = whh + (long long)d * G * H;
+// One workgroup = one (utterance, direction) for all T steps: 4 COMPUTE waves + 1 FLUSH wave.
+// Compute lane (j, q) = (tid >> 2, tid & 3) owns gate q of hidden unit j.  Per step it
+//  * takes its step inputs from a register ring it keeps SD steps ahead with its own global loads
+//    (one x-projection element forward; dh, c, c_prev and the unit's four gates backward) -- the
+//    loads are unconditional (clamped addresses), so the compiler's vmcnt bookkeeping waits only
+//    for the slot being consumed, never for the loads still in flight;
+//  * issues ALL its LDS reads of h_{s-1} / dG_{s-1} before the first FMA (one LDS latency per
+//    step, not one per 4-wide slice) and runs the product as packed fp32 FMAs (v_pk_fma_f32);
+//  * combines the quad's gates with DPP and writes its outputs into an LDS chunk buffer.
+// The compute waves issue no stores at all: the flush wave writes each finished chunk of SC steps
+// to HBM (fp32, plus an optional bf16 twin for the next GEMMs) while the next chunk runs, so no
+// compute wave ever waits on a store.  One workgroup barrier per step orders everything.
+constexpr int SNT = 320;  // 4 compute waves + 1 flush wave
+constexpr int SD = 4;     // input lead, steps
+constexpr int SC = 16;    // output chunk, steps
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Diagnostic timeline (TRACE builds only, avc_lstm_trace): lane 0 of the given wave records the
+// 100 MHz realtime clock into tr[(block*Tp + s)*8 + j] once the value `dep` exists (the asm's
+// input operand orders the stamp after the code that produces it).
+__device__ __forceinline__ void sstamp(unsigned long long* tr, int Tp, int s, int j, float dep) {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "v"(dep));
+  if ((threadIdx.x & 63) == 0)
+    tr[((long long)(blockIdx.y * gridDim.x + blockIdx.x) * Tp + s) * 8 + j] = t;
+}
+
+constexpr int OOB = 0x7FFFFFF0;  // buffer offset past every buffer here: the store is dropped
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4b_t __attribute__((ext_vector_type(4)));
+
+// Raw buffer resource over `bytes` bytes (0 for a null pointer: every store dropped).  The flush
+// wave predicates its stores with it (out-of-range offsets are dropped), so its unrolled flush has
+// no branches and every store keeps its own registers: no store waits for an earlier one.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, p ? (int)bytes : 0, 0x00020000);
+}
+
+// sum_k w[k] * v[k] over HM/4 float4 LDS slices of v; every slice is read before the first FMA
+template <int HM>
+__device__ __forceinline__ float dot_lds(const float* __restrict__ v, const f32x2 (&w)[HM / 2]) {
+  const f32x4* v4 = reinterpret_cast<const f32x4*>(v);
+  f32x4 hv[HM / 4];
 #pragma unroll
-  for (int k = 0; k < HM; ++k) w[k] = (act && k < H) ? W[(long long)row * H + k] : 0.f;
-  if (tid < 2 * HM) hs[tid / HM][tid % HM] = 0.f;
-  float c = 0.f;
+  for (int k = 0; k < HM / 4; ++k) hv[k] = v4[k];
+  // four independent accumulation chains, so no packed FMA waits on its predecessor's result
+  f32x2 a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+  for (int k = 0; k < HM / 4; ++k) {
+    a[(2 * k) & 3] = __builtin_elementwise_fma(f32x2{hv[k][0], hv[k][1]}, w[2 * k], a[(2 * k) & 3]);
+    a[(2 * k + 1) & 3] = __builtin_elementwise_fma(f32x2{hv[k][2], hv[k][3]}, w[2 * k + 1], a[(2 * k + 1) & 3]);
+  }
+  const f32x2 t = (a[0] + a[1]) + (a[2] + a[3]);
+  return t[0] + t[1];
+}
+
+// Forward.  T is padded to a multiple of SC with ghost steps that are never written out.
+template <int HM, bool FAST, bool TRACE>
+__global__ void __launch_bounds__(SNT) lstm_small_fwd(const float* __restrict__ xproj, const float* __restrict__ whh,
+                                                      int T, int H, int dirs, float* __restrict__ hout,
+                                                      bf16* __restrict__ hout16, float* __restrict__ cout,
+                                                      float* __restrict__ gout, unsigned long long* tr) {
+  constexpr int GM = 4 * HM;
+  const int b = blockIdx.x, d = blockIdx.y, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int G = 4 * H;
+  __shared__ __attribute__((aligned(16))) float hs[2][HM];
+  __shared__ __attribute__((aligned(16))) float gst[2][SC][GM];  // output chunks
+  __shared__ __attribute__((aligned(16))) float hst[2][SC][HM], cst[2][SC][HM];
   const long long ldx = (long long)dirs * G, ldh = (long long)dirs * H;
   const int t0 = d ? T - 1 : 0, dt = d ? -1 : 1;
-  const float* xb = xproj + (long long)b * T * ldx + d * G;
-  // chunk element e: step s = k*SC + e/G, gate row e%G
-  float pf[NPF];
-  auto issue = [&](int k) {
+  const int Tp = (T + SC - 1) / SC * SC;
+
+  const int j = tid >> 2, q = tid & 3, row = q * H + j;
+  const bool act = w < 4 && j < H;
+  f32x2 wv[HM / 2];
+  float c = 0.f, ring[SD];
+  // this lane's x-projection element of step sn (clamped: the surplus lanes / steps load a valid
+  // element that is never used)
+  const float* xl = xproj + (long long)b * T * ldx + d * G + min(row, G - 1);
+  auto xload = [&](int sn) { return xl[(long long)(t0 + dt * min(sn, T - 1)) * ldx]; };
+  // flush chunk k (steps k*SC .. k*SC+SC-1) from buffer k & 1 (flush wave): fully unrolled,
+  // branch-free buffer stores (gates as 16-B chunks)
+  const __amdgpu_buffer_rsrc_t gr = brsrc(gout, (long long)gridDim.x * T * ldx * 4);
+  const __amdgpu_buffer_rsrc_t hr = brsrc(hout, (long long)gridDim.x * T * ldh * 4);
+  const __amdgpu_buffer_rsrc_t cr = brsrc(cout, (long long)gridDim.x * T * ldh * 4);
+  const __amdgpu_buffer_rsrc_t h16r = brsrc(hout16, (long long)gridDim.x * T * ldh * 2);
+  auto flush = [&](int k) {
+    const int kb = k & 1;
 #pragma unroll
-    for (int i = 0; i < NPF; ++i) {
-      const int e = tid + 256 * i, si = e / G, s = k * SC + si;
-      pf[i] = (si < SC && s < T) ? xb[(long long)(t0 + dt * s) * ldx + (e - si * G)] : 0.f;
+    for (int it = 0; it < SC * GM / 4 / 64; ++it) {
+      const int idx = it * 64 + lane, i = idx / (GM / 4), c4 = idx % (GM / 4), st = k * SC + i;
+      const bool ok = 4 * c4 < G && st < T;
+      const long long o = ((long long)b * T + t0 + dt * st) * ldx + d * G + 4 * c4;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4b_t, *reinterpret_cast<const f32x4*>(&gst[kb][i][4 * c4])),
+                                             gr, ok ? (int)(o * 4) : OOB, 0, 0);
     }
-  };
-  auto commit = [&](int buf) {
+    if (H % 4 == 0) {  // h, c as 16-B chunks, the bf16 h twin as 8-B chunks
 #pragma unroll
-    for (int i = 0; i < NPF; ++i) {
-      const int e = tid + 256 * i;
-      if (e < SC * G) xs[buf][e] = pf[i];
-    }
-  };
-  // write chunk k's ns steps of gates, h and c from LDS to HBM (coalesced rows)
-  auto flush = [&](int k, int ns) {
+      for (int it = 0; it < (SC * HM / 4 + 63) / 64; ++it) {
+        const int idx = it * 64 + lane, i = min(idx / (HM / 4), SC - 1), u4 = idx % (HM / 4), st = k * SC + i;
+        const bool ok = idx < SC * HM / 4 && 4 * u4 < H && st < T;
+        const long long o = ((long long)b * T + t0 + dt * st) * ldh + d * H + 4 * u4;
+        const f32x4 hv = *reinterpret_cast<const f32x4*>(&hst[kb][i][4 * u4]);
+        const f32x4 cv = *reinterpret_cast<const f32x4*>(&cst[kb][i][4 * u4]);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4b_t, hv), hr, ok ? (int)(o * 4) : OOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4b_t, cv), cr, ok ? (int)(o * 4) : OOB, 0, 0);
+        const bf16x4 h16 = {(bf16)hv[0], (bf16)hv[1], (bf16)hv[2], (bf16)hv[3]};
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, h16), h16r, ok ? (int)(o * 2) : OOB, 0, 0);
+      }
+    } else {
 #pragma unroll
-    for (int i = 0; i < NPF; ++i) {
-      const int e = tid + 256 * i, si = e / G;
-      if (si < ns) {
-        const int t = t0 + dt * (k * SC + si);
-        gout[((long long)b * T + t) * ldx + d * G + (e - si * G)] = gst[e];
+      for (int it = 0; it < SC * HM / 64; ++it) {
+        const int idx = it * 64 + lane, i = idx / HM, u = idx % HM, st = k * SC + i;
+        const bool ok = u < H && st < T;
+        const long long o = ((long long)b * T + t0 + dt * st) * ldh + d * H + u;
+        const float hv = hst[kb][i][u], cv = cst[kb][i][u];
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, hv), hr, ok ? (int)(o * 4) : OOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, cv), cr, ok ? (int)(o * 4) : OOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (bf16)hv), h16r,
+                                              ok ? (int)(o * 2) : OOB, 0, 0);
       }
     }
-#pragma unroll
-    for (int i = 0; i < (SC * HM + 255) / 256; ++i) {
-      const int e = tid + 256 * i, si = e / H;
-      if (si < ns) {
-        const int t = t0 + dt * (k * SC + si);
-        const long long o = ((long long)b * T + t) * ldh + d * H + (e - si * H);
-        hout[o] = hst[e];
-        cout[o] = cst[e];
-      }
-    }
   };
-  const int nch = (T + SC - 1) / SC;
-  issue(0);
-  commit(0);
+  if (w < 4) {
+    const float* W = whh + (long long)d * G * H + (long long)min(row, G - 1) * H;
+#pragma unroll
+    for (int k = 0; k < HM / 2; ++k)
+      wv[k] = f32x2{(act && 2 * k < H) ? W[2 * k] : 0.f, (act && 2 * k + 1 < H) ? W[2 * k + 1] : 0.f};
+    if (tid < 2 * HM) hs[tid / HM][tid % HM] = 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < SD; ++r) ring[r] = xload(r);
   __syncthreads();
-  if (nch > 1) issue(1);
-  for (int k = 0; k < nch; ++k) {
-    const float* xk = xs[k & 1];
-    const int ns = min(SC, T - k * SC);
+
+  for (int k = 0; k * SC < Tp; ++k) {
+    if (w == 4 && k > 0) flush(k - 1);
 #pragma unroll
     for (int i = 0; i < SC; ++i) {
-      if (i < ns) {
-        const int s = k * SC + i;
-        const f32x4* h4 = reinterpret_cast<const f32x4*>(hs[s & 1]);
-        float a0 = act ? xk[i * G + row] : 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-#pragma unroll
-        for (int kq = 0; kq < HM / 4; ++kq) {
-          const f32x4 hv = h4[kq];
-          a0 += hv[0] * w[4 * kq];
-          a1 += hv[1] * w[4 * kq + 1];
-          a2 += hv[2] * w[4 * kq + 2];
-          a3 += hv[3] * w[4 * kq + 3];
-        }
-        const float pre = (a0 + a1) + (a2 + a3);
-        // FAST: tanh(x) = 2*sig(2x) - 1 is exactly how ftanh is formed, so the gate lanes of a
-        // quad share one exp + rcp with no divergent branch (bit-identical to the branch form)
+      const int s = k * SC + i;
+      // the ring advances in every wave (the flush wave's loads are harmless and unused): a ring
+      // slot written only inside the role branch would need a copy at the branch join, and that
+      // copy waits for the load just issued
+      const float xv = ring[i % SD];
+      ring[i % SD] = xload(s + SD);
+      if (TRACE && w == 0) sstamp(tr, Tp, s, 0, 0.f);
+      if (w < 4) {
+        const float pre = (act ? xv : 0.f) + dot_lds<HM>(hs[s & 1], wv);
+        if (TRACE && w == 0) sstamp(tr, Tp, s, 1, pre);
         float gv;
-        if (FAST) {
+        if (FAST) {  // tanh(x) = 2 sig(2x) - 1: one exp + rcp for all four gate lanes
           const float sg = fsig((q == 2 ? 2.f : 1.f) * pre);
           gv = q == 2 ? 2.f * sg - 1.f : sg;
         } else {
@@ -159,147 +212,127 @@ __global__ void __launch_bounds__(256) lstm_small_fwd(const float* __restrict__ 
         const float ig = quad_bcast<0>(gv), fg = quad_bcast<1>(gv), gg = quad_bcast<2>(gv), og = quad_bcast<3>(gv);
         c = fg * c + ig * gg;
         const float h = og * act_tanh<FAST>(c);
+        if (TRACE && w == 0) sstamp(tr, Tp, s, 2, h);
         if (act) {
+          gst[k & 1][i][row] = gv;
           if (q == 0) {
             hs[(s + 1) & 1][j] = h;
-            hst[i * H + j] = h;
+            hst[k & 1][i][j] = h;
           } else if (q == 1) {
-            cst[i * H + j] = c;
+            cst[k & 1][i][j] = c;
           }
-          gst[i * G + row] = gv;
         }
-        __syncthreads();
       }
+      if (TRACE && w < 4) sstamp(tr, Tp, s, w == 0 ? 3 : 4 + w, 0.f);
+      __syncthreads();
     }
-    // chunk end: the steps issued no global memory operation, so nothing above waited on the
-    // prefetch; now commit chunk k+1, then the output stores, then chunk k+2's loads (loads
-    // last: the next step's register reuse then only waits for the stores, vmcnt(NPF))
-    if (k + 1 < nch) commit((k + 1) & 1);
-    flush(k, ns);
-    if (k + 2 < nch) issue(k + 2);
-    __syncthreads();
   }
+  if (w == 4) flush(Tp / SC - 1);
 }
 
-template <int HM, bool FAST>
-__global__ void __launch_bounds__(256) lstm_small_bwd(const float* __restrict__ dhout, const float* __restrict__ call,
+// Backward: compute lane (j, q) holds column j of gate block q (wc[g] = W[q*H + g][j]) and sums
+// dG_{s-1}[q*H + g] * wc[g] over g; the quad's four partial sums (DPP xor steps) give dh_rec[j].
+// Its ring holds dh, c, c_prev and the four gates of unit j for the next SD steps.
+template <int HM, bool FAST, bool TRACE>
+__global__ void __launch_bounds__(SNT) lstm_small_bwd(const float* __restrict__ dhout, const float* __restrict__ call,
                                                       const float* __restrict__ gall, const float* __restrict__ whh,
-                                                      int T, int H, int dirs, float* __restrict__ dg) {
-  constexpr int RM = 7 * HM, NPF = (SC * RM + 255) / 256;
-  const int b = blockIdx.x, d = blockIdx.y, tid = threadIdx.x;
-  const int G = 4 * H, R = 7 * H;
-  const int j = tid >> 2, q = tid & 3;
-  const bool act = j < H;
-  __shared__ __attribute__((aligned(16))) float dgs[2][4 * HM];
-  __shared__ float rs[2][SC * RM];  // per step: dh | c | c_prev | i f g o
-  __shared__ float dgst[SC * 4 * HM];  // the chunk's dG rows, flushed at its end
-  // lane (j, q) holds column j of gate block q: wc[g] = W[q*H + g][j]
-  float wc[HM];
-  const float* W = whh + (long long)d * G * H;
-#pragma unroll
-  for (int g = 0; g < HM; ++g) wc[g] = (act && g < H) ? W[(long long)(q * H + g) * H + j] : 0.f;
-  for (int i = tid; i < 8 * HM; i += 256) dgs[i / (4 * HM)][i % (4 * HM)] = 0.f;
-  float dc = 0.f;
+                                                      int T, int H, int dirs, float* __restrict__ dg,
+                                                      bf16* __restrict__ dg16, unsigned long long* tr) {
+  constexpr int GM = 4 * HM;
+  const int b = blockIdx.x, d = blockIdx.y, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int G = 4 * H;
+  __shared__ __attribute__((aligned(16))) float dgs[2][GM];  // dG of a step, block q at q*HM
+  __shared__ __attribute__((aligned(16))) float ost[2][SC][GM];  // output chunks (block q at q*H)
   const long long ldg = (long long)dirs * G, ldh = (long long)dirs * H;
   // backward walks opposite to the forward recurrence
   const int t0 = d ? 0 : T - 1, dt = d ? 1 : -1;
   const int fwd_prev = d ? 1 : -1;  // offset of the forward's previous time step
-  const float* dhb = dhout + (long long)b * T * ldh + d * H;
-  const float* cb = call + (long long)b * T * ldh + d * H;
-  const float* gb = gall + (long long)b * T * ldg + d * G;
-  // chunk element e: step s = k*SC + e/R, column e%R of the staged row
-  float pf[NPF];
-  auto issue = [&](int k) {
+  const int Tp = (T + SC - 1) / SC * SC;
+
+  const int j = tid >> 2, q = tid & 3, jc = min(j, H - 1);
+  const bool act = w < 4 && j < H;
+  f32x2 wc[HM / 2];
+  float dc = 0.f;
+  struct In {
+    float dh, c, cp, i, f, g, o;
+  };
+  In ring[SD];
+  const float* dhb = dhout + (long long)b * T * ldh + d * H + jc;
+  const float* cb = call + (long long)b * T * ldh + d * H + jc;
+  const float* gb = gall + (long long)b * T * ldg + d * G + jc;
+  auto fetch = [&](int sn) {  // unconditional loads; c_prev past the sequence start is zeroed at use
+    const int t = t0 + dt * min(sn, T - 1), tp = min(max(t + fwd_prev, 0), T - 1);
+    In v;
+    v.dh = dhb[(long long)t * ldh];
+    v.c = cb[(long long)t * ldh];
+    v.cp = cb[(long long)tp * ldh];
+    const float* g = gb + (long long)t * ldg;
+    v.i = g[0];
+    v.f = g[H];
+    v.g = g[2 * H];
+    v.o = g[3 * H];
+    return v;
+  };
+  const __amdgpu_buffer_rsrc_t dgr = brsrc(dg, (long long)gridDim.x * T * ldg * 4);
+  const __amdgpu_buffer_rsrc_t dg16r = brsrc(dg16, (long long)gridDim.x * T * ldg * 2);
+  auto flush = [&](int k) {  // fully unrolled, branch-free buffer stores (see the forward)
+    const int kb = k & 1;
 #pragma unroll
-    for (int i = 0; i < NPF; ++i) {
-      const int e = tid + 256 * i, si = e / R, col = e - si * R, s = k * SC + si;
-      float v = 0.f;
-      if (si < SC && s < T) {
-        const int t = t0 + dt * s, seg = col / H, u = col - seg * H;
-        if (seg == 0) {
-          v = dhb[(long long)t * ldh + u];
-        } else if (seg == 1) {
-          v = cb[(long long)t * ldh + u];
-        } else if (seg == 2) {
-          const int tp = t + fwd_prev;
-          v = (tp >= 0 && tp < T) ? cb[(long long)tp * ldh + u] : 0.f;
-        } else {
-          v = gb[(long long)t * ldg + (col - 3 * H)];
-        }
-      }
-      pf[i] = v;
+    for (int it = 0; it < SC * GM / 4 / 64; ++it) {
+      const int idx = it * 64 + lane, i = idx / (GM / 4), c4 = idx % (GM / 4), st = k * SC + i;
+      const bool ok = 4 * c4 < G && st < T;
+      const long long o = ((long long)b * T + t0 + dt * st) * ldg + d * G + 4 * c4;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(&ost[kb][i][4 * c4]);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4b_t, v), dgr, ok ? (int)(o * 4) : OOB, 0, 0);
+      const bf16x4 v16 = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v16), dg16r, ok ? (int)(o * 2) : OOB, 0, 0);
     }
   };
-  auto commit = [&](int buf) {
+  if (w < 4) {
+    const float* W = whh + (long long)d * G * H;
 #pragma unroll
-    for (int i = 0; i < NPF; ++i) {
-      const int e = tid + 256 * i;
-      if (e < SC * R) rs[buf][e] = pf[i];
-    }
-  };
-  auto flush = [&](int k, int ns) {
+    for (int k = 0; k < HM / 2; ++k)
+      wc[k] = f32x2{(act && 2 * k < H) ? W[(long long)(q * H + 2 * k) * H + j] : 0.f,
+                    (act && 2 * k + 1 < H) ? W[(long long)(q * H + 2 * k + 1) * H + j] : 0.f};
+    for (int i = tid; i < 2 * GM; i += 256) dgs[i / GM][i % GM] = 0.f;
+  }
 #pragma unroll
-    for (int i = 0; i < (SC * 4 * HM + 255) / 256; ++i) {
-      const int e = tid + 256 * i, si = e / G;
-      if (si < ns) {
-        const int t = t0 + dt * (k * SC + si);
-        dg[((long long)b * T + t) * ldg + d * G + (e - si * G)] = dgst[e];
-      }
-    }
-  };
-  const int nch = (T + SC - 1) / SC;
-  issue(0);
-  commit(0);
+  for (int r = 0; r < SD; ++r) ring[r] = fetch(r);
   __syncthreads();
-  if (nch > 1) issue(1);
-  for (int k = 0; k < nch; ++k) {
-    const float* rk = rs[k & 1];
-    const int ns = min(SC, T - k * SC);
+
+  for (int k = 0; k * SC < Tp; ++k) {
+    if (w == 4 && k > 0) flush(k - 1);
 #pragma unroll
     for (int i = 0; i < SC; ++i) {
-      if (i < ns) {
-        const int s = k * SC + i;
-        // recurrent part dh_rec[j] = sum_{q', g} dG_{s-1}[q'*H + g] W[q'*H + g][j]: this lane
-        // sums gate block q (entries past H meet zero weights), the quad adds the four blocks
-        const float* gq = dgs[(s + 1) & 1] + q * H;
-        float p0 = 0.f, p1 = 0.f;
-        if (H % 4 == 0) {
-          const f32x4* g4 = reinterpret_cast<const f32x4*>(gq);
-#pragma unroll
-          for (int g = 0; g < HM / 4; ++g) {
-            const f32x4 v = g4[g];
-            p0 += v[0] * wc[4 * g] + v[2] * wc[4 * g + 2];
-            p1 += v[1] * wc[4 * g + 1] + v[3] * wc[4 * g + 3];
-          }
-        } else {
-#pragma unroll
-          for (int g = 0; g < HM; ++g) p0 += (g < H ? gq[g] : 0.f) * wc[g];
-        }
-        const float* rw = rk + i * R;
-        const float dh = (act ? rw[j] : 0.f) + quad_sum(p0 + p1);
+      const int s = k * SC + i;
+      const In in = ring[i % SD];  // advanced in every wave (see the forward)
+      ring[i % SD] = fetch(s + SD);
+      if (TRACE && (w == 0 || w == 4)) sstamp(tr, Tp, s, w == 0 ? 0 : 4, 0.f);
+      if (w < 4) {
+        // recurrent part dh_rec[j] = sum_{q', g} dG_{s-1}[q'*H + g] W[q'*H + g][j]: this lane sums
+        // gate block q (entries past H meet zero weights), the quad adds the four blocks
+        const float p = dot_lds<HM>(dgs[(s + 1) & 1] + q * HM, wc);
+        const float dh = (act ? in.dh : 0.f) + quad_sum(p);
+        if (TRACE && w == 0) sstamp(tr, Tp, s, 1, dh);
         if (act) {
-          const float c = rw[H + j], cp = rw[2 * H + j];
-          const float ig = rw[3 * H + j], fg = rw[4 * H + j], gg = rw[5 * H + j], og = rw[6 * H + j];
-          const float tc = act_tanh<FAST>(c);
-          const float dcs = dc + dh * og * (1.f - tc * tc);
-          const float v = q == 0 ? dcs * gg * ig * (1.f - ig)
-                        : q == 1 ? dcs * cp * fg * (1.f - fg)
-                        : q == 2 ? dcs * ig * (1.f - gg * gg)
-                                 : dh * tc * og * (1.f - og);
-          dc = dcs * fg;
-          dgs[s & 1][q * H + j] = v;
-          dgst[i * G + q * H + j] = v;
+          const float cp = s == T - 1 ? 0.f : in.cp;  // the forward's c_{-1} = 0
+          const float tc = act_tanh<FAST>(in.c);
+          const float dcs = dc + dh * in.o * (1.f - tc * tc);
+          const float v = q == 0 ? dcs * in.g * in.i * (1.f - in.i)
+                        : q == 1 ? dcs * cp * in.f * (1.f - in.f)
+                        : q == 2 ? dcs * in.i * (1.f - in.g * in.g)
+                                 : dh * tc * in.o * (1.f - in.o);
+          dc = dcs * in.f;
+          dgs[s & 1][q * HM + j] = v;  // gate blocks HM apart: 16-B aligned slices, zero tails
+          ost[k & 1][i][q * H + j] = v;
         }
-        __syncthreads();
+        if (TRACE && w == 0) sstamp(tr, Tp, s, 2, dc);
       }
+      if (TRACE && (w == 0 || w == 4)) sstamp(tr, Tp, s, w == 0 ? 3 : 5, 0.f);
+      __syncthreads();
     }
-    // chunk end, as in the forward: commit the next chunk's inputs, flush this chunk's dG,
-    // then issue the prefetch after next
-    if (k + 1 < nch) commit((k + 1) & 1);
-    flush(k, ns);
-    if (k + 2 < nch) issue(k + 2);
-    __syncthreads();
   }
+  if (w == 4) flush(Tp / SC - 1);
 }
 
 // =============================================================== large H: per-step kernels
@@ -1218,15 +1251,17 @@ bool persistent_path(int B, int H, int dirs, bool bf, bool bwd) {
 
 template <int HM>
 void launch_small_fwd(dim3 g, hipStream_t s, bool fast, const float* x, const float* w, int T, int H, int dirs,
-                      float* h, float* c, float* gt) {
-  if (fast) lstm_small_fwd<HM, true><<<g, 256, 0, s>>>(x, w, T, H, dirs, h, c, gt);
-  else lstm_small_fwd<HM, false><<<g, 256, 0, s>>>(x, w, T, H, dirs, h, c, gt);
+                      float* h, bf16* h16, float* c, float* gt) {
+  if (g_trace) lstm_small_fwd<HM, true, true><<<g, SNT, 0, s>>>(x, w, T, H, dirs, h, h16, c, gt, g_trace);
+  else if (fast) lstm_small_fwd<HM, true, false><<<g, SNT, 0, s>>>(x, w, T, H, dirs, h, h16, c, gt, nullptr);
+  else lstm_small_fwd<HM, false, false><<<g, SNT, 0, s>>>(x, w, T, H, dirs, h, h16, c, gt, nullptr);
 }
 template <int HM>
 void launch_small_bwd(dim3 g, hipStream_t s, bool fast, const float* dh, const float* c, const float* gt,
-                      const float* w, int T, int H, int dirs, float* dg) {
-  if (fast) lstm_small_bwd<HM, true><<<g, 256, 0, s>>>(dh, c, gt, w, T, H, dirs, dg);
-  else lstm_small_bwd<HM, false><<<g, 256, 0, s>>>(dh, c, gt, w, T, H, dirs, dg);
+                      const float* w, int T, int H, int dirs, float* dg, bf16* dg16) {
+  if (g_trace) lstm_small_bwd<HM, true, true><<<g, SNT, 0, s>>>(dh, c, gt, w, T, H, dirs, dg, dg16, g_trace);
+  else if (fast) lstm_small_bwd<HM, true, false><<<g, SNT, 0, s>>>(dh, c, gt, w, T, H, dirs, dg, dg16, nullptr);
+  else lstm_small_bwd<HM, false, false><<<g, SNT, 0, s>>>(dh, c, gt, w, T, H, dirs, dg, dg16, nullptr);
 }
 
 }  // namespace
@@ -1260,11 +1295,12 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
   if (H <= 64) {
     AVC_CHECK_ARG(wdtype == AVC_F32, "avc_lstm_fwd: small-H path takes fp32 W_hh");
     const bool fast = compute == AVC_BF16;  // fp32 weights and state either way; fast activations in bf16 mode
+    bf16* h16 = reinterpret_cast<bf16*>(h_bf16);
     dim3 g(B, dirs);
-    if (H <= 16) launch_small_fwd<16>(g, s, fast, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
-    else if (H <= 32) launch_small_fwd<32>(g, s, fast, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
-    else if (H <= 48) launch_small_fwd<48>(g, s, fast, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
-    else launch_small_fwd<64>(g, s, fast, xproj, (const float*)w_hh, T, H, dirs, h, c, gates);
+    if (H <= 16) launch_small_fwd<16>(g, s, fast, xproj, (const float*)w_hh, T, H, dirs, h, h16, c, gates);
+    else if (H <= 32) launch_small_fwd<32>(g, s, fast, xproj, (const float*)w_hh, T, H, dirs, h, h16, c, gates);
+    else if (H <= 48) launch_small_fwd<48>(g, s, fast, xproj, (const float*)w_hh, T, H, dirs, h, h16, c, gates);
+    else launch_small_fwd<64>(g, s, fast, xproj, (const float*)w_hh, T, H, dirs, h, h16, c, gates);
     return avc_check_launch("avc_lstm_fwd(small)");
   }
   AVC_CHECK_ARG(H % 128 == 0, "avc_lstm_fwd: H must be <= 64 or a multiple of 128 (got %d)", H);
@@ -1340,11 +1376,12 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
   if (H <= 64) {
     AVC_CHECK_ARG(w_hh && wdtype == AVC_F32, "avc_lstm_bwd: small-H path takes fp32 W_hh");
     const bool fast = compute == AVC_BF16;
+    bf16* dg16 = reinterpret_cast<bf16*>(dgates_bf16);
     dim3 g(B, dirs);
-    if (H <= 16) launch_small_bwd<16>(g, s, fast, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
-    else if (H <= 32) launch_small_bwd<32>(g, s, fast, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
-    else if (H <= 48) launch_small_bwd<48>(g, s, fast, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
-    else launch_small_bwd<64>(g, s, fast, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates);
+    if (H <= 16) launch_small_bwd<16>(g, s, fast, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates, dg16);
+    else if (H <= 32) launch_small_bwd<32>(g, s, fast, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates, dg16);
+    else if (H <= 48) launch_small_bwd<48>(g, s, fast, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates, dg16);
+    else launch_small_bwd<64>(g, s, fast, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates, dg16);
     return avc_check_launch("avc_lstm_bwd(small)");
   }
   AVC_CHECK_ARG(H % 128 == 0, "avc_lstm_bwd: H must be <= 64 or a multiple of 128 (got %d)", H);

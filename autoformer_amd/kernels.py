@@ -275,8 +275,10 @@ def lstm_fwd(xproj, w_hh, B, T, H, dirs, hbuf=None):
     h16 = None
     if H > 64:
         fault_word(dev)
-    if hbuf is not None and H > 64 and lstm_persistent_fwd(B, H, dirs):
-        h16 = torch.empty(B * T, H, device=dev, dtype=torch.bfloat16)
+    # the bf16 twin of h (the next GEMMs' operand) comes out of the recurrence itself: always on
+    # the small-H path in bf16 mode, and on the persistent large-H path
+    if (H <= 64 and _COMPUTE == BF16) or (hbuf is not None and H > 64 and lstm_persistent_fwd(B, H, dirs)):
+        h16 = torch.empty(B * T, dirs * H, device=dev, dtype=torch.bfloat16)
     L.call("avc_lstm_fwd", xproj.data_ptr(), w_hh.data_ptr(), _dt(w_hh), B, T, H, dirs, h.data_ptr(), _ptr(h16),
            c.data_ptr(), g.data_ptr(), _ptr(hbuf), _COMPUTE, stream())
     return attach_twin(h, h16), c, g
@@ -326,6 +328,8 @@ def lstm_bwd(dh, h, c, g, w_hh, w_hh_t, B, T, H, dirs, gbuf=None):
                 gbuf = lstm_bwd_scratch(B, H, dirs, dev)
             if lstm_persistent_bwd(B, H, dirs):
                 dg16 = torch.empty(B * T, 4 * H, device=dev, dtype=torch.bfloat16)
+    elif _COMPUTE == BF16:
+        dg16 = torch.empty(B * T, dirs * 4 * H, device=dev, dtype=torch.bfloat16)
     timed = LAUNCH_TIMING is not None and dg16 is not None and H == LAUNCH_TIMING_H
     if timed:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -428,9 +432,9 @@ def loss_grad(a, b, dloss, mode, sign):
     return g
 
 
-def adam(p, g, m, v, lr, beta1, beta2, eps, state):
+def adam(p, g, m, v, lr, beta1, beta2, eps, state, advance=True):
     L.call("avc_adam", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), float(lr), float(beta1),
-           float(beta2), float(eps), state.data_ptr(), stream())
+           float(beta2), float(eps), state.data_ptr(), int(advance), stream())
 
 
 def act_fwd(x, act, out=None):

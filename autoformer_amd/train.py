@@ -172,6 +172,13 @@ class FusedAdam:
         K.adam(self.flat, self.gflat, self.m, self.v, self.lr, self.betas[0], self.betas[1], self.eps, self.state)
         weights_changed()
 
+    def step_slice(self, lo, hi, advance):
+        """Adam over flat[lo:hi] only; `advance` on the step's first slice (the step count and
+        bias corrections live in self.state; later slices must be stream-ordered after it)."""
+        sl = slice(lo, hi)
+        K.adam(self.flat[sl], self.gflat[sl], self.m[sl], self.v[sl], self.lr, self.betas[0], self.betas[1],
+               self.eps, self.state, advance=advance)
+
 
 # ------------------------------------------------------------------------- bench step
 class TrainStep:
@@ -194,18 +201,20 @@ class TrainStep:
         self.graph_fb = None
         self.world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
         self.loss = None
-        # Data parallel: the decoder / postnet (/ discriminator) gradients are final once the
-        # backward reaches the decoder input; they are averaged on a communication stream while
-        # the encoder backward (full pass + re-pass gradients) still runs, and only the encoder
-        # slice is averaged after the backward.
+        # The decoder / postnet (/ discriminator) gradients are final once the backward reaches
+        # the decoder input (encoder parameters precede them in the flat buffer).  From that
+        # point, on a second stream and beside the encoder backward (full pass + re-pass, the
+        # latency-bound BiLSTM recurrences), their slice is averaged over ranks (data parallel)
+        # and stepped by Adam; after the backward only the encoder slice (13 %) is left.
         self.split = None
         self.loss_fn = losses_for(model)
         # the Adjust variants register `adjust` after the postnet and its gradients complete
         # only with the encoder's: no early (overlapped) slice for them
-        if self.world > 1 and hasattr(model, "decoder") and self.loss_fn is not adjust_losses:
+        if hasattr(model, "decoder") and self.loss_fn is not adjust_losses:
             self.split = D.split_offset(self.params, next(model.decoder.parameters()))
             self.comm = torch.cuda.Stream()
         self._early = None
+        self._early_adam = False
         # fault word (kernels.fault_word): read back asynchronously after every step into a
         # pinned word and checked at the next step, so a failed persistent recurrence raises
         # within one step without a host sync; check() is the synchronous form
@@ -235,7 +244,12 @@ class TrainStep:
         if side is not None:
             self.comm.wait_stream(side)
         with torch.cuda.stream(self.comm):
-            self._early = D.allreduce_mean_async_(self.gflat[self.split:])
+            if self.world > 1:
+                # RCCL: the comm stream waits for the collective; the Adam slice follows it
+                self._early = D.allreduce_mean_async_(self.gflat[self.split:])
+                D.finish_allreduce_(self._early)
+            self.opt.step_slice(self.split, self.flat.numel(), advance=True)
+        self._early_adam = True
 
     def _fwd_bwd(self, x, emb, overlap=False):
         self.gflat.zero_()
@@ -250,24 +264,31 @@ class TrainStep:
         join_side()  # weight-gradient GEMMs ran on the side stream
         return loss
 
-    def _allreduce(self):
-        timed = self.comm_timing is not None
+    def _finish(self):
+        """After the backward: average what is left over ranks and run Adam on it."""
+        timed = self.comm_timing is not None and self.world > 1
         if timed:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        if self._early is None:  # no overlapped part (graph replay, or no hook fired)
-            D.allreduce_mean_(self.gflat)
+        main = torch.cuda.current_stream()
+        if not self._early_adam:  # no overlapped part (graph replay, or no hook fired)
+            if self.world > 1:
+                D.allreduce_mean_(self.gflat)
+            if timed:
+                ev[1].record()
+            self.opt.step()
         else:
-            main = torch.cuda.current_stream()
-            self.comm.wait_stream(main)
-            with torch.cuda.stream(self.comm):
-                late = D.allreduce_mean_async_(self.gflat[:self.split])
-                D.finish_allreduce_(self._early)
-                D.finish_allreduce_(late)
-            main.wait_stream(self.comm)
-            self._early = None
+            if self.world > 1:
+                self.comm.wait_stream(main)
+                with torch.cuda.stream(self.comm):
+                    D.finish_allreduce_(D.allreduce_mean_async_(self.gflat[:self.split]))
+            main.wait_stream(self.comm)  # the early slice's Adam (and its step-count advance)
+            if timed:
+                ev[1].record()
+            self.opt.step_slice(0, self.split, advance=False)
+            weights_changed()
+            self._early, self._early_adam = None, False
         if timed:
-            ev[1].record()
             self.comm_timing.append(ev)
 
     def step(self, x, emb):
@@ -276,9 +297,7 @@ class TrainStep:
             loss = self.loss
         else:
             loss = self._fwd_bwd(x, emb, overlap=self.split is not None)
-        if self.world > 1:
-            self._allreduce()
-        self.opt.step()
+        self._finish()
         if self.graph_fb is None:
             prefetch_packs()  # next step's weight packs, on the side stream
         self._probe_fault()

@@ -128,8 +128,9 @@ int avc_colsum(const float* x, long long ld, int M, int N, float* out, int accum
  * max(4*dirs*B*H, 8*B*H + 16) bytes.  For dirs == 1, H in {512, 1024} and enough CUs the
  * whole sequence runs as ONE persistent launch (W_hh slices register-resident, h_t handed
  * between workgroups as write-through payload + per-workgroup flags, bounded spins; timeout
- * flag = u32 at byte 0 of hbuf); otherwise one fused kernel per time step.  The persistent launch can also write a
- * bf16 copy of h (h_bf16, the next GEMMs' operand; else null — other paths need null). */
+ * flag = u32 at byte 0 of hbuf); otherwise one fused kernel per time step.  The small-H and the
+ * persistent launches can also write a bf16 copy of h (h_bf16, (B,T,dirs*H), the next GEMMs'
+ * operand; else null — the per-step path needs null). */
 int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T, int H, int dirs,
                  float* h, void* h_bf16, float* c, float* gates, void* hbuf, int compute, void* stream);
 
@@ -139,9 +140,8 @@ int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T,
  * bf16 compute): at least max(16*dirs*B*H, 32*B*H + 16) bytes.  For dirs == 1, H in
  * {512, 1024} and enough CUs the whole sequence is ONE persistent launch (W_hh^T slices
  * register-resident, dG_{t+1} handed over as write-through payload + flags, bounded spins;
- * timeout flag = u32 at byte 0 of gbuf), which can also write a bf16 copy of dgates
- * (dgates_bf16, else null); otherwise one fused kernel per time step and dgates_bf16 must
- * be null. */
+ * timeout flag = u32 at byte 0 of gbuf).  The small-H and persistent launches can also write a
+ * bf16 copy of dgates (dgates_bf16, else null); the per-step path needs null. */
 int avc_lstm_bwd(const float* dh_out, const float* h, const float* c, const float* gates,
                  const void* w_hh, const void* w_hh_t, int wdtype, int B, int T, int H, int dirs,
                  float* dgates, void* dgates_bf16, float* dcbuf, void* gbuf, int compute, void* stream);
@@ -240,10 +240,12 @@ int avc_patchify(const float* src, float* dst, int B, int L, int C, int ps, int 
 /* dst[b] (+)= src[b]^T for B row-major R x C matrices. */
 int avc_transpose_batched(const float* src, float* dst, int B, int R, int C, int accumulate, void* stream);
 
-/* Fused Adam (torch.optim.Adam defaults, train.py:49,99) over one flat fp32 buffer.
- * state[0] = step count (float), updated on device (graph-replayable). */
+/* Fused Adam (torch.optim.Adam defaults, train.py:49,99) over a slice of one flat fp32 buffer.
+ * state[0] = step count (float), state[1..2] = this step's bias corrections, updated on device
+ * (graph-replayable) when `advance` != 0.  A step split over several slices advances on its
+ * first slice only; the later slices run on a stream ordered after it. */
 int avc_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
-             float beta2, float eps, float* state, void* stream);
+             float beta2, float eps, float* state, int advance, void* stream);
 
 /* AdaIN / speaker-embedding-adjust variants (variants.hip).
  * Whole-tensor moments of x.mean(), x.std() (unbiased) — factory/AutoVC2.py:58-60,
