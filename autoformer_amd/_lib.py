@@ -52,7 +52,7 @@ _SIGS = {
     "avc_bn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "avc_colsum_ws": (c_size, [c_int, c_int]),
-    "avc_colsum": (c_int, [c_void_p, c_ll, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "avc_colsum": (c_int, [c_void_p, c_ll, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "avc_lstm_fwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p, c_int, c_void_p]),
     "avc_lstm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

@@ -422,7 +422,7 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const float* __rest
 }
 
 __global__ void __launch_bounds__(1024) colsum_final_kernel(const float* __restrict__ ws, int nrb, int N, float* out,
-                                                            int accumulate) {
+                                                            float* out2, int accumulate) {
   __shared__ float red[FG][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -436,6 +436,7 @@ __global__ void __launch_bounds__(1024) colsum_final_kernel(const float* __restr
 #pragma unroll
   for (int i = 0; i < FG; ++i) s += red[i][cl];
   out[c] = accumulate ? out[c] + s : s;
+  if (out2) out2[c] = accumulate ? out2[c] + s : s;  // b_ih and b_hh take the same gradient
 }
 
 }  // namespace
@@ -522,8 +523,8 @@ extern "C" int avc_bn_bwd(const float* dA, const float* a, const float* y, const
 
 extern "C" size_t avc_colsum_ws(int M, int N) { return (size_t)cdiv(M, RB) * N; }
 
-extern "C" int avc_colsum(const float* x, long long ld, int M, int N, float* out, int accumulate, float* ws,
-                          void* stream) {
+extern "C" int avc_colsum(const float* x, long long ld, int M, int N, float* out, float* out2, int accumulate,
+                          float* ws, void* stream) {
   AVC_CHECK_ARG(x && out && ws && ld >= N, "avc_colsum: bad args");
   hipStream_t s = as_stream(stream);
   const int nrb = cdiv(M, RB);
@@ -531,6 +532,6 @@ extern "C" int avc_colsum(const float* x, long long ld, int M, int N, float* out
     colsum_partial_kernel<true><<<dim3(cdiv(N, 64), nrb), 256, 0, s>>>(x, ld, M, N, ws);
   else
     colsum_partial_kernel<false><<<dim3(cdiv(N, 64), nrb), 256, 0, s>>>(x, ld, M, N, ws);
-  colsum_final_kernel<<<cdiv(N, 64), 1024, 0, s>>>(ws, nrb, N, out, accumulate);
+  colsum_final_kernel<<<cdiv(N, 64), 1024, 0, s>>>(ws, nrb, N, out, out2, accumulate);
   return avc_check_launch("avc_colsum");
 }

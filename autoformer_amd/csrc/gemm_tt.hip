@@ -39,11 +39,13 @@ __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "me
 
 __device__ __forceinline__ int tswz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
-// One K-strided operand: tile of 64 frame rows x 128 columns [col0, col0 + 128).  Wave w,
-// instruction i covers rows 4*(4i + w) .. +4; lane L writes row +(L>>4), slot L&15, holding
-// global chunk (L&15) ^ tswz(row) = (L&15) ^ (((L>>4)<<2) | w): one fixed column per lane.
-template <bool WIN>
+// One K-strided operand: tile of 64 frame rows x 128 columns [col0, col0 + 128), loaded by NW
+// waves.  Wave w, instruction i covers rows 4*(NW*i + w) .. +4; lane L writes row +(L>>4), slot
+// L&15, holding global chunk (L&15) ^ tswz(row) = (L&15) ^ (((L>>4)<<2) | (w&3)) (NW is a
+// multiple of 4): one fixed column per lane.
+template <bool WIN, int NW = 4>
 struct TtLoader {
+  static constexpr int NI = 16 / NW;
   const bf16* base;
   int col_ok;          // this lane's 8 columns lie inside the operand
   int coff;            // element offset of the lane's column inside a frame row
@@ -75,8 +77,8 @@ struct TtLoader {
   __device__ __forceinline__ void issue(char* lds_tile, int kbase, int kend) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 4 * (4 * i + w) + (lane >> 4);
+    for (int i = 0; i < NI; ++i) {
+      const int r = 4 * (NW * i + w) + (lane >> 4);
       const int k = kbase + r;
       bool ok = col_ok && k < kend;
       long long frame = k;
@@ -87,7 +89,7 @@ struct TtLoader {
         frame = (long long)b * t_in + t2;
       }
       const void* src = ok ? (const void*)(base + frame * ld + coff) : (const void*)g_zero16_tt;
-      glds16(src, lds_tile + 4 * (4 * i + w) * TROW);
+      glds16(src, lds_tile + 4 * (NW * i + w) * TROW);
     }
   }
 };
@@ -108,6 +110,27 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int o0, int o1) {
   typedef short s16x8 __attribute__((ext_vector_type(8)));
   const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
+}
+
+// The same fragment read issued as inline asm.  hipcc treats ds_read_tr16_b64 (the builtin) as
+// possibly aliasing any in-flight LDS DMA and waits `vmcnt(0)` before it -- which drains the
+// prefetch just issued and serialises every K-tile behind its own global load.  The asm form
+// is invisible to that bookkeeping: the caller orders it after the landed stage (counted vmcnt
+// + barrier) and waits for the reads itself (tr_wait) before the MFMAs use them.
+__device__ __forceinline__ unsigned lds_addr(const char* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ bf16x8 tr_frag_asm(const char* tile, int o0, int o1) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x4 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(lds_addr(tile + o0)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(lds_addr(tile + o1)));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ void tr_wait() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);  // nothing (an MFMA on the read registers) moves above the wait
 }
 
 template <bool WINB>
@@ -167,9 +190,10 @@ __global__ void __launch_bounds__(256, 2) gemm_tt_kernel(GemmArgs g) {
       const int ko = h * 32 * TROW;
       bf16x8 af[4], bfr[NJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = tr_frag(As + ko, ao0[i], ao1[i]);
+      for (int i = 0; i < 4; ++i) af[i] = tr_frag_asm(As + ko, ao0[i], ao1[i]);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bfr[j] = tr_frag(Bs + ko, bo0[j], bo1[j]);
+      for (int j = 0; j < NJ; ++j) bfr[j] = tr_frag_asm(Bs + ko, bo0[j], bo1[j]);
+      tr_wait();
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -191,6 +215,142 @@ void launch(const GemmArgs& g, int nblocks, hipStream_t s) {
     attr = true;
   }
   gemm_tt_kernel<WINB><<<nblocks, 256, lds, s>>>(g);
+}
+
+// ------------------------------------------------------------------ pipelined TT kernel
+// BMT x 128 tile (BMT = 128: 4 waves as 2x2; 256: 8 waves as 4x2, each wave 64 x 64), BK = 64,
+// NST LDS stages with NST-1 K-tiles in flight: a counted `s_waitcnt vmcnt` + raw s_barrier per
+// K-tile, never vmcnt(0) inside the loop (cdna_hip_programming.md §5 "Pipelining across
+// barriers") -- the two-stage kernel above waits for the tile it just issued, one L2/HBM round
+// trip per 64 frames.  A is staged as BMT/128 column halves of the same 256-B-row image.
+template <int N>
+__device__ __forceinline__ void wait_vm_n(int ahead) {
+  // ahead = K-tiles allowed to stay in flight; N = glds per thread per K-tile
+  if (ahead >= 2) wait_vm<2 * N>();
+  else if (ahead == 1) wait_vm<N>();
+  else wait_vm<0>();
+}
+
+template <bool WINB, int BMT, int NST>
+__global__ void __launch_bounds__(BMT * 2, 1) gemm_tt2_kernel(GemmArgs g) {
+  constexpr int NW = BMT / 32, NT = NW * 64, NH = BMT / 128;
+  constexpr int A_BYTES = NH * TSTAGE_OP, STAGE = A_BYTES + TSTAGE_OP;
+  constexpr int LPT = (NH + 1) * (16 / NW);  // glds per thread per K-tile
+  constexpr int P = NST - 1;
+  static_assert(P <= 3, "at most 3 K-tiles in flight");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int nN = (g.N + 127) / 128, nM = (g.M + BMT - 1) / BMT;
+  const int z = lid / (nN * nM);
+  const int rem = lid - z * nN * nM;
+  const int mt = rem / nN, nt = rem - mt * nN;
+  const int m0 = mt * BMT, n0 = nt * 128;
+  const int bz = z / g.split_k, ks = z - bz * g.split_k;
+  const int kbeg = ks * g.klen;
+  const int kend = min(g.K, kbeg + g.klen);
+  const int nkt = kend > kbeg ? (kend - kbeg + FBK - 1) / FBK : 0;
+
+  TtLoader<false, NW> la[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) la[h].init(g.a, m0 + 128 * h, bz);
+  TtLoader<WINB, NW> lb;
+  lb.init(g.b, n0, bz);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // wave (wm, wn): rows wm*64 .. +64 = half wm/2, column block (wm&1)*64 of that half
+  int ao0[4], ao1[4], bo0[4], bo1[4];
+  const int ahalf = (wm >> 1) * TSTAGE_OP;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) tr_offsets((wm & 1) * 8 + 2 * i, ao0[i], ao1[i]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) tr_offsets(wn * 8 + 2 * j, bo0[j], bo1[j]);
+
+  auto issue = [&](int kt) {
+    char* st = smem_raw + (kt % NST) * STAGE;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) la[h].issue(st + h * TSTAGE_OP, kbeg + kt * FBK, kend);
+    lb.issue(st + A_BYTES, kbeg + kt * FBK, kend);
+  };
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+    if (p < nkt) issue(p);
+  for (int kt = 0; kt < nkt; ++kt) {
+    wait_vm_n<LPT>(min(P - 1, nkt - 1 - kt));
+    raw_barrier();
+    if (kt + P < nkt) issue(kt + P);
+    const char* As = smem_raw + (kt % NST) * STAGE + ahalf;
+    const char* Bs = smem_raw + (kt % NST) * STAGE + A_BYTES;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ko = h * 32 * TROW;
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = tr_frag_asm(As + ko, ao0[i], ao1[i]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = tr_frag_asm(Bs + ko, bo0[j], bo1[j]);
+      tr_wait();
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // epilogue (weight gradients: plain store, accumulate, or split-K atomics)
+  const int rbase = m0 + wm * 64 + 4 * (lane >> 4), cbase = n0 + wn * 64 + (lane & 15);
+  float* C = g.c + (long long)bz * g.cbs;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = rbase + i * 16 + e;
+      if (row >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = cbase + j * 16;
+        if (col >= g.N) continue;
+        float* cp = C + (long long)row * g.ldc + col;
+        const float v = acc[i][j][e];
+        if (g.atomic) atomicAdd(cp, v);
+        else *cp = g.accumulate ? *cp + v : v;
+      }
+    }
+}
+
+template <bool WINB, int BMT, int NST>
+void launch2(const GemmArgs& g, hipStream_t s) {
+  const size_t lds = (size_t)NST * (BMT / 128 + 1) * TSTAGE_OP;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tt2_kernel<WINB, BMT, NST>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const int nb = ((g.M + BMT - 1) / BMT) * ((g.N + 127) / 128) * g.batch * g.split_k;
+  gemm_tt2_kernel<WINB, BMT, NST><<<nb, BMT * 2, lds, s>>>(g);
+}
+
+// AVC_TT_CFG = "BMT,NST" selects the pipelined kernel (benchmarking); "0" keeps the two-stage one
+void tt_cfg(int& bmt, int& nst) {
+  static int cfg[2] = {-1, -1};
+  if (cfg[0] == -1) {
+    cfg[0] = 0;
+    cfg[1] = 0;
+    const char* e = getenv("AVC_TT_CFG");
+    if (e) sscanf(e, "%d,%d", &cfg[0], &cfg[1]);
+  }
+  bmt = cfg[0];
+  nst = cfg[1];
 }
 
 bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -222,6 +382,13 @@ __device__ __forceinline__ bf16x8 tr_frag_h(const char* tile, int rlo, int chunk
   typedef short s16x8 __attribute__((ext_vector_type(8)));
   const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ bf16x8 tr_frag_h_asm(const char* tile, int rlo, int chunk0, int p) {
+  const int rhi = rlo + 4;
+  const int olo = rlo * HROW + 16 * ((chunk0 + (p >> 1)) ^ hswz(rlo)) + 8 * (p & 1);
+  const int ohi = rhi * HROW + 16 * ((chunk0 + (p >> 1)) ^ hswz(rhi)) + 8 * (p & 1);
+  return tr_frag_asm(tile, olo, ohi);
 }
 
 template <int NST>
@@ -305,9 +472,10 @@ __global__ void __launch_bounds__(256, 2) gemm_tt_halo_kernel(GemmArgs g) {
       // per K-half instead of one per tap
       bf16x8 af[4], bfr[TAPS];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = tr_frag(As + h * 32 * TROW, ao0[i], ao1[i]);
+      for (int i = 0; i < 4; ++i) af[i] = tr_frag_asm(As + h * 32 * TROW, ao0[i], ao1[i]);
 #pragma unroll
-      for (int k = 0; k < TAPS; ++k) bfr[k] = tr_frag_h(Hs, h * 32 + 8 * grp + qq + k, 2 * wn, pp);
+      for (int k = 0; k < TAPS; ++k) bfr[k] = tr_frag_h_asm(Hs, h * 32 + 8 * grp + qq + k, 2 * wn, pp);
+      tr_wait();
 #pragma unroll
       for (int k = 0; k < TAPS; ++k)
 #pragma unroll
@@ -366,6 +534,17 @@ bool gemm_tt_launch(const GemmArgs& g, hipStream_t s) {
     else launch_halo<3>(g, s);
     return true;
   }
+  int bmt, nst;
+  tt_cfg(bmt, nst);
+  if (g.c16 || g.res || g.bias || g.bn_partial) bmt = 0;  // the pipelined kernel has the plain epilogue only
+#define TT2_CASE(BMV, NSV)                               \
+  if (bmt == BMV && nst == NSV) {                        \
+    if (g.b.win) launch2<true, BMV, NSV>(g, s);          \
+    else launch2<false, BMV, NSV>(g, s);                 \
+    return true;                                         \
+  }
+  TT2_CASE(128, 2) TT2_CASE(128, 3) TT2_CASE(128, 4) TT2_CASE(256, 2) TT2_CASE(256, 3)
+#undef TT2_CASE
   const int nb = ((g.M + BM - 1) / BM) * ((g.N + 127) / 128) * g.batch * g.split_k;
   if (g.b.win) launch<true>(g, nb, s);
   else launch<false>(g, nb, s);

@@ -193,12 +193,13 @@ def bn_bwd(dA, a, y, mean, rstd, gamma, act, need_dbias=True, into=None, twin16=
     return attach_twin(dy, d16), dgamma, dbeta, dbias
 
 
-def colsum(x, M, N, ld=None, out=None, accumulate=False):
+def colsum(x, M, N, ld=None, out=None, accumulate=False, out2=None):
+    """Column sums of an (M, N) block (rows ld apart) into out (and the same into out2)."""
     dev = x.device
     out = torch.empty(N, device=dev) if out is None else out
     ws = torch.empty(int(L.lib().avc_colsum_ws(M, N)), device=dev)
-    L.call("avc_colsum", x.data_ptr(), int(N if ld is None else ld), M, N, out.data_ptr(), int(accumulate),
-           ws.data_ptr(), stream())
+    L.call("avc_colsum", x.data_ptr(), int(N if ld is None else ld), M, N, out.data_ptr(), _ptr(out2),
+           int(accumulate), ws.data_ptr(), stream())
     return out
 
 

@@ -22,6 +22,8 @@ from .kernels import operand
 
 _EPOCH = [0]
 _LAST_WGRAD_MAIN = os.environ.get("AVC_LAST_WGRAD_MAIN", "1") != "0"
+# diagnostics only (tools/ablate.sh): skip the side-stream weight-gradient GEMMs (wrong gradients)
+_ABLATE_WGRAD = os.environ.get("AVC_ABLATE_WGRAD") == "1"
 
 # ---------------------------------------------------------------- gradient sink / side stream
 # In "sink" mode (set by TrainStep) parameter gradients are accumulated by the kernels
@@ -276,7 +278,8 @@ class ConvBNCore:
         if sink and (n_dx or not _LAST_WGRAD_MAIN):
             with _Side(ev) as sd:
                 sd.keep(dy, x)
-                wgrad()
+                if not _ABLATE_WGRAD:
+                    wgrad()
             dW = dgamma = dbeta = dbias = None
         elif sink:
             # no data gradient: this is the last layer of the backward (the encoder's first
@@ -442,8 +445,7 @@ class LSTMLayerCore:
                        split_k=K.auto_split_k(4 * H, H, M), accumulate=sink)
                 dg32 = dg if dirs == 1 else dg[:, d * 4 * H:]
                 if sink:
-                    K.colsum(dg32, M, 4 * H, ld=G, out=_grad_of(b_ih), accumulate=True)
-                    K.colsum(dg32, M, 4 * H, ld=G, out=_grad_of(b_hh), accumulate=True)
+                    K.colsum(dg32, M, 4 * H, ld=G, out=_grad_of(b_ih), out2=_grad_of(b_hh), accumulate=True)
                     continue
                 dbd = K.colsum(dg32, M, 4 * H, ld=G)
                 # b_ih and b_hh receive the same gradient but must not share storage
@@ -457,7 +459,8 @@ class LSTMLayerCore:
         if sink:
             with _Side(ev) as sd:
                 sd.keep(dg, x, h, dg_op, h_op)
-                wgrads()
+                if not _ABLATE_WGRAD:
+                    wgrads()
             grads = [None] * (4 * dirs)
         else:
             grads = wgrads()
@@ -529,7 +532,8 @@ class _LinearFn(torch.autograd.Function):
         if sink:
             with _Side(ev) as sd:
                 sd.keep(dy, x)
-                wgrad()
+                if not _ABLATE_WGRAD:
+                    wgrad()
             dw = db = None
         else:
             dw, db = wgrad()

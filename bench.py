@@ -133,6 +133,25 @@ def host_cores():
     return len(phys) or None, aff
 
 
+def pmc_mfma(kernel):
+    """MFMA counters of `kernel` from the newest committed counter pass (profiles/r*_pmc_mfma_step.json,
+    tools/gpu_pmc.sh + tools/pmc_mfma.py): bf16 MFMA TFLOP/s from SQ_INSTS_VALU_MFMA_MOPS_BF16 over the
+    dispatch time, the fraction of wave cycles waiting (SQ_WAIT_ANY), and its source file."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_mfma_step.json")))
+    if not files:
+        return None
+    data = json.load(open(files[-1]))
+    for name, e in data.items():
+        if kernel in name:
+            return {"mfma_instr_tflops": round(e.get("bf16_tflops", 0.0), 1),
+                    "mfma_instr_frac": round(e.get("bf16_tflops", 0.0) / PEAK_BF16_TFLOPS, 4),
+                    "wave_wait_frac": round(e.get("wait", 0.0), 3), "source": os.path.relpath(files[-1], ROOT),
+                    "note": "MFMA instruction rate (16-row tiles, 8 of 16 rows are utterances: 2x the useful FLOPs)"}
+    return None
+
+
 def cpu_baseline(B, T, freq, steps=3):
     """The CPU oracle (oracle/autovc_cpu.py, the pinned restatement of the reference) timed on
     this box's host cores: same step, fp32, bounded sample of 1 warm-up + `steps` steps
@@ -343,7 +362,8 @@ def main():
                            "avg_us": round(step_us, 3), "launches_timed": len(evs),
                            "avg_us_isolated": round(kt["avg_us"], 3), "flop_per_launch": kt["flops"],
                            "alg_bytes_per_launch": kt["bytes"], "hbm_achieved_gbs": round(gbs, 1),
-                           "hbm_frac": round(gbs / PEAK_HBM_GBS, 5), "traffic_source": src}
+                           "hbm_frac": round(gbs / PEAK_HBM_GBS, 5), "traffic_source": src,
+                           "counters": pmc_mfma(DOMINANT)}
     if world == 1 and not args.no_cpu_baseline and default:
         out["cpu_baseline"] = cpu_baseline(B, T, freq)
     print(json.dumps(out), flush=True)

@@ -113,9 +113,10 @@ int avc_bn_bwd(const float* dA, const float* a, const float* y, const float* mea
                const float* gamma, const float* beta, int M, int C, int act, float* dy, void* dy_bf16,
                float* dgamma, float* dbeta, float* dbias, int accumulate, float* ws, void* stream);
 
-/* out[n] (+)= sum_m x[m*ld + n] (bias gradients). ws >= avc_colsum_ws floats. */
+/* out[n] (+)= sum_m x[m*ld + n] (bias gradients); out2 (nullable) receives the same sums (an
+ * LSTM's b_ih and b_hh share one gradient, nn.LSTM AutoVC.py:43,77,96).  ws >= avc_colsum_ws floats. */
 size_t avc_colsum_ws(int M, int N);
-int avc_colsum(const float* x, long long ld, int M, int N, float* out, int accumulate, float* ws,
+int avc_colsum(const float* x, long long ld, int M, int N, float* out, float* out2, int accumulate, float* ws,
                void* stream);
 
 /* LSTM layer recurrence (both directions of a bidirectional layer in one call).

@@ -6,7 +6,7 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows = sorted(((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]), int(r["Queue_Id"]))
                for r in rows), key=lambda r: r[1])
-ad = [i for i, r in enumerate(rows) if "adam_kernel" in r[0]]
+ad = [i for i, r in enumerate(rows) if "adam_prep_kernel" in r[0]]  # one per step
 seg = [r for r in rows[ad[-3] + 1:ad[-2] + 1] if r[3] == int(sys.argv[2] if len(sys.argv) > 2 else 1)]
 
 

@@ -22,10 +22,22 @@ def load(path):
 def main():
     rows = load(sys.argv[1])
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-    ad = [i for i, r in enumerate(rows) if "adam_kernel" in r[0]]
+    # one adam_prep_kernel per step (Adam may run as several slices)
+    ad = [i for i, r in enumerate(rows) if "adam_prep_kernel" in r[0]]
     seg = rows[ad[-3] + 1:ad[-2] + 1]
-    t0, t1 = seg[0][1], seg[-1][2]
+    t0, t1 = seg[0][1], max(r[2] for r in seg)
     print(f"step span {(t1 - t0) / 1e6:.3f} ms, {len(seg)} kernels")
+    # union of busy intervals over all queues: the time no kernel at all runs is host / launch bound
+    iv = sorted((s, e) for _, s, e, _ in seg)
+    busy, cs, ce = 0, iv[0][0], iv[0][1]
+    for s, e in iv[1:]:
+        if s > ce:
+            busy += ce - cs
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    busy += ce - cs
+    print(f"some kernel running {busy / 1e6:.3f} ms; no kernel running {(t1 - t0 - busy) / 1e6:.3f} ms")
     for q in sorted(set(r[3] for r in seg)):
         d = defaultdict(lambda: [0, 0])
         for n, s, e, qq in seg:
