@@ -34,7 +34,15 @@ class GemmDesc(ctypes.Structure):
     _fields_ = [("M", c_int), ("N", c_int), ("K", c_int), ("batch", c_int), ("a", Operand), ("b", Operand),
                 ("c", c_void_p), ("ldc", c_ll), ("c_batch_stride", c_ll), ("bias", c_void_p),
                 ("accumulate", c_int), ("split_k", c_int), ("bn_partial", c_void_p), ("compute", c_int),
-                ("c_bf16", c_void_p), ("residual", c_void_p)]
+                ("c_bf16", c_void_p), ("residual", c_void_p), ("cperm", c_int)]
+
+
+class PackOp(ctypes.Structure):
+    _fields_ = [("src", c_void_p), ("src2", c_void_p), ("dst", c_void_p), ("kind", c_int), ("out_dtype", c_int),
+                ("d0", c_int), ("d1", c_int), ("d2", c_int), ("pad_", c_int), ("ld_out", c_ll)]
+
+
+PACK_COPY, PACK_TRANSPOSE, PACK_CONV_F, PACK_CONV_D, PACK_ADD = 0, 1, 2, 3, 4
 
 
 _SIGS = {
@@ -74,6 +82,7 @@ _SIGS = {
     "avc_mse_loss": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_void_p]),
     "avc_l1_loss": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_void_p]),
     "avc_loss_grad": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_int, c_void_p, c_float, c_void_p]),
+    "avc_pack_batch": (c_int, [c_void_p, c_void_p, c_int, c_ll, c_void_p]),
     "avc_adam": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_float, c_float, c_float, c_float, c_void_p,
                          c_int, c_void_p]),
     "avc_act_fwd": (c_int, [c_void_p, c_void_p, c_ll, c_int, c_void_p]),

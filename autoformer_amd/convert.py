@@ -1,7 +1,10 @@
 """Voice conversion with a trained plugin model (reference util/evaluate.py:36-94,
-Evaluator.crop_mel / get_trans_mel, AutoVC path): crop or zero-pad the source mel to
-`len_crop`, run the model with the source and target speaker embeddings, and cut the
-converted mel back to the source's real length when it was padded (the `isPlay` branch).
+Evaluator.crop_mel / get_trans_mel): crop or zero-pad the source (and target) mel to
+`len_crop`, run the model with the source and target speaker embeddings -- dispatched like
+get_trans_mel over the three model families (plain: model(x, e_org, e_trg); isAdjust:
+model(x, e_org, e_trg, True, mel_target), 4 outputs; isAdain: features of the source first,
+model(x, e_org, None, None), then model(x, e_org, e_trg, feature)) -- and cut the converted mel
+back to the source's real length when it was padded (the `isPlay` branch).
 
 Same kernels as training, forward only under `torch.no_grad()`; the model stays in whatever
 BatchNorm mode the caller left it in (the reference converts with the model in train mode, so
@@ -36,14 +39,44 @@ class Converter:
         self.len_crop = len_crop
         self.device = torch.device(device)
 
+    def _dev(self, a):
+        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).unsqueeze(0).to(self.device)
+
     @torch.no_grad()
-    def convert(self, mel_source: np.ndarray, emb_org: np.ndarray, emb_trg: np.ndarray, trim: bool = True):
-        mel, pad = crop_mel(mel_source, self.len_crop)
-        x = torch.from_numpy(np.ascontiguousarray(mel, dtype=np.float32)).unsqueeze(0).to(self.device)
-        eo = torch.from_numpy(np.asarray(emb_org, dtype=np.float32)).unsqueeze(0).to(self.device)
-        et = torch.from_numpy(np.asarray(emb_trg, dtype=np.float32)).unsqueeze(0).to(self.device)
-        _, mel_trans, _ = self.model(x, eo, et)
-        out = mel_trans.squeeze(1)[0]
-        if trim and pad > 0:
-            out = out[: self.len_crop - pad]
-        return out.float().cpu().numpy()
+    def get_trans_mel(self, mel_source: np.ndarray, mel_target, emb_org: np.ndarray, emb_trg: np.ndarray,
+                      isAdjust: bool = False, isAdain: bool = False, isPlay: bool = False):
+        """util/evaluate.py:56-94 on host mels: returns (mel_source, mel_target, mel_trans) device
+        tensors (1, T, 80) exactly as the reference does; the source is cropped before the target
+        (the reference's rng order).  mel_target may be None unless isAdjust."""
+        src, pad_s = crop_mel(mel_source, self.len_crop)
+        x = self._dev(src)
+        y, pad_t = (None, 0)
+        if mel_target is not None:
+            tgt, pad_t = crop_mel(mel_target, self.len_crop)
+            y = self._dev(tgt)
+        eo, et = self._dev(emb_org), self._dev(emb_trg)
+        if isAdjust:
+            if y is None:
+                raise ValueError("isAdjust conversion needs the target mel (evaluate.py:79)")
+            _, _, mel_trans, _ = self.model(x, eo, et, True, y)
+        elif isAdain:
+            _, feature = self.model(x, eo, None, None)
+            _, mel_trans, _ = self.model(x, eo, et, feature)
+        else:
+            _, mel_trans, _ = self.model(x, eo, et)
+        mel_trans = mel_trans.squeeze(1)
+        if isPlay:
+            if pad_s > 0:
+                x = x[:, : self.len_crop - pad_s, :]
+                mel_trans = mel_trans[:, : self.len_crop - pad_s, :]
+            if y is not None and pad_t > 0:
+                y = y[:, : self.len_crop - pad_t, :]
+        return x, y, mel_trans
+
+    @torch.no_grad()
+    def convert(self, mel_source: np.ndarray, emb_org: np.ndarray, emb_trg: np.ndarray, trim: bool = True,
+                mel_target=None, isAdjust: bool = False, isAdain: bool = False):
+        """The converted mel (T', 80) on the host (trimmed to the source length when padded)."""
+        _, _, mel_trans = self.get_trans_mel(mel_source, mel_target, emb_org, emb_trg, isAdjust, isAdain,
+                                             isPlay=trim)
+        return mel_trans[0].float().cpu().numpy()

@@ -178,6 +178,71 @@ __global__ void loss_grad_kernel(const float* a, const float* b, long long n, co
   g[i] = sign * dloss[0] * f / (float)n;
 }
 
+// Batched weight packing (avc_pack_batch).  The launch is cut into UNITS: 1024 elements of an
+// elementwise op (copy / add / conv re-layout, walked along the source, 4 per thread), or one
+// 32 x 32 tile of a transpose (staged through LDS so both the fp32 reads and the bf16 writes are
+// coalesced).  prefix[i] = first unit of op i; a block finds its op by one block-uniform binary
+// search per unit (<= 128 ops).
+constexpr int PACK_MAX_OPS = 128;
+
+__global__ void __launch_bounds__(256) pack_batch_kernel(const avc_pack_op* __restrict__ ops,
+                                                         const long long* __restrict__ prefix, int nops,
+                                                         long long total) {
+  __shared__ float tile[32][33];
+  __shared__ long long pre[PACK_MAX_OPS + 1];
+  __shared__ avc_pack_op sops[PACK_MAX_OPS];
+  const int tid = threadIdx.x;
+  // the op table and its prefix, once per block: the per-unit search then costs LDS reads only
+  for (int i = tid; i <= nops; i += 256) pre[i] = prefix[i];
+  for (int i = tid; i < nops; i += 256) sops[i] = ops[i];
+  __syncthreads();
+  for (long long u = blockIdx.x; u < total; u += gridDim.x) {
+    int lo = 0, hi = nops;  // largest i with pre[i] <= u
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (pre[mid] <= u) lo = mid;
+      else hi = mid;
+    }
+    const avc_pack_op& op = sops[lo];
+    const long long lu = u - pre[lo];
+    if (op.kind == AVC_PACK_TRANSPOSE) {  // dst[c*ld + r] = src[r*C + c], src [R][C]
+      const int R = op.d0, C = op.d1, tcn = (C + 31) / 32;
+      const int r0 = (int)(lu / tcn) * 32, c0 = (int)(lu % tcn) * 32;
+      const int tx = tid & 31, ty = tid >> 5;
+#pragma unroll
+      for (int y = ty; y < 32; y += 8) {
+        const int r = r0 + y, c = c0 + tx;
+        tile[y][tx] = (r < R && c < C) ? op.src[(long long)r * C + c] : 0.f;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int y = ty; y < 32; y += 8) {
+        const int c = c0 + y, r = r0 + tx;
+        if (c < C && r < R) putd(op.dst, (long long)c * op.ld_out + r, tile[tx][y], op.out_dtype);
+      }
+      __syncthreads();  // the tile is reused by the next unit
+      continue;
+    }
+    const long long n = (op.kind == AVC_PACK_CONV_F || op.kind == AVC_PACK_CONV_D) ? (long long)op.d0 * op.d1 * op.d2
+                                                                                  : op.d0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long long i = lu * 1024 + j * 256 + tid;
+      if (i >= n) break;
+      float v = op.src[i];
+      long long o = i;
+      if (op.kind == AVC_PACK_ADD) {
+        v += op.src2[i];
+      } else if (op.kind == AVC_PACK_CONV_F || op.kind == AVC_PACK_CONV_D) {  // source W[co][ci][k]
+        const int K = op.d2, Ci = op.d1, Co = op.d0;
+        const int ii = (int)i, k = ii % K, ci = (ii / K) % Ci, co = ii / (K * Ci);
+        o = op.kind == AVC_PACK_CONV_F ? ((long long)co * K + k) * Ci + ci : ((long long)ci * K + (K - 1 - k)) * Co + co;
+      }
+      putd(op.dst, o, v, op.out_dtype);
+    }
+  }
+}
+
 __global__ void adam_prep_kernel(float* state, float lr, float beta1, float beta2) {
   float step = state[0] + 1.f;
   state[0] = step;
@@ -340,6 +405,15 @@ extern "C" int avc_loss_grad(const float* a, const float* b, long long n, const 
   AVC_CHECK_ARG(a && b && dloss && g, "avc_loss_grad: null");
   loss_grad_kernel<<<GRID1(n)>>>(a, b, n, dloss, mode, g, sign);
   return avc_check_launch("avc_loss_grad");
+}
+
+extern "C" int avc_pack_batch(const avc_pack_op* ops, const long long* prefix, int nops, long long total,
+                              void* stream) {
+  AVC_CHECK_ARG(ops && prefix && nops > 0 && nops <= PACK_MAX_OPS && total >= 0, "avc_pack_batch: bad args");
+  if (total == 0) return 0;
+  const int grid = (int)std::min<long long>(2048, total);
+  pack_batch_kernel<<<grid, 256, 0, as_stream(stream)>>>(ops, prefix, nops, total);
+  return avc_check_launch("avc_pack_batch");
 }
 
 extern "C" int avc_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,

@@ -305,7 +305,7 @@ __global__ void __launch_bounds__(NT) gemm_generic_kernel(GemmArgs g) {
       for (int j = 0; j < 4; ++j) {
         int col = cbase + j * 16;
         if (col >= g.N) continue;
-        float* p = C + (long long)row * g.ldc + col;
+        float* p = C + (long long)row * g.ldc + out_col(g, col);
         float v = acc[i][j][e];
         if (g.res && ks == 0) v += g.res[(long long)bz * g.cbs + (long long)row * g.ldc + col];
         if (g.atomic) atomicAdd(p, v);
@@ -716,6 +716,10 @@ extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
   // over the batch, e.g. a weight gradient of a per-utterance product), accumulate atomically
   g.atomic = g.split_k > 1 || (g.batch > 1 && d->c_batch_stride == 0);
   g.bn_partial = d->bn_partial;
+  g.cperm = d->cperm > 1 ? d->cperm : 0;
+  AVC_CHECK_ARG(!g.cperm || (d->N % g.cperm == 0 && !g.bias && !g.res && !g.c16 && !g.bn_partial),
+                "avc_gemm: cperm needs N %% taps == 0 and no bias / residual / bf16 / BN epilogue");
+  g.cpd = make_fastdiv(g.cperm ? (uint32_t)(d->N / g.cperm) : 1u);
   AVC_CHECK_ARG(!(g.bn_partial && (g.split_k > 1 || g.batch > 1 || d->accumulate)),
                 "avc_gemm: bn_partial needs split_k == 1, batch == 1, accumulate == 0");
   hipStream_t s = as_stream(stream);

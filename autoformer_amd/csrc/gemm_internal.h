@@ -26,7 +26,16 @@ struct GemmArgs {
   const float* bias;
   int accumulate, atomic;
   float* bn_partial;
+  int cperm;     // 0, or taps: column n = tap*chans + ch is stored at ch*taps + tap (conv weight layout)
+  FastDiv cpd;   // divide a column by chans = N / cperm
 };
+
+// Column offset of output column `col` (cperm: the Conv1d [Co][Ci][K] layout).
+__device__ __forceinline__ long long out_col(const GemmArgs& g, int col) {
+  if (!g.cperm) return col;
+  const int tap = (int)fdiv((uint32_t)col, g.cpd), ch = col - tap * (int)g.cpd.d;
+  return (long long)ch * g.cperm + tap;
+}
 
 
 // Accumulator layout shared by the fast kernels: 4 waves as 2 (M) x 2 (N); wave (wm, wn) owns
@@ -63,7 +72,7 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
       for (int j = 0; j < NJ; ++j) {
         const int col = cbase + j * 16;
         if (col >= g.N) continue;
-        const long long o = (long long)row * g.ldc + col;
+        const long long o = (long long)row * g.ldc + out_col(g, col);
         float v = acc[i][j][e];
         if (g.res && ks == 0) v += g.res[(long long)bz * g.cbs + o];
         if (g.atomic) {

@@ -319,7 +319,7 @@ __global__ void __launch_bounds__(BMT * 2, 1) gemm_tt2_kernel(GemmArgs g) {
       for (int j = 0; j < 4; ++j) {
         const int col = cbase + j * 16;
         if (col >= g.N) continue;
-        float* cp = C + (long long)row * g.ldc + col;
+        float* cp = C + (long long)row * g.ldc + out_col(g, col);
         const float v = acc[i][j][e];
         if (g.atomic) atomicAdd(cp, v);
         else *cp = g.accumulate ? *cp + v : v;
@@ -494,7 +494,7 @@ __global__ void __launch_bounds__(256, 2) gemm_tt_halo_kernel(GemmArgs g) {
       if (row >= g.M) continue;
 #pragma unroll
       for (int k = 0; k < TAPS; ++k) {
-        float* cp = g.c + (long long)row * g.ldc + k * chans + cl;
+        float* cp = g.c + (long long)row * g.ldc + (g.cperm ? (long long)cl * TAPS + k : (long long)k * chans + cl);
         const float v = acc[i][k][e];
         if (g.atomic) atomicAdd(cp, v);
         else *cp = g.accumulate ? *cp + v : v;

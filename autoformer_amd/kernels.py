@@ -81,7 +81,9 @@ def operand(t: torch.Tensor, ld: int, kstrided: bool = False, window=None, batch
 
 
 def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=None, accumulate=False, split_k=1,
-         bn_partial=None, batch=1, c_batch_stride=0, comp=None, c_bf16=None, residual=None):
+         bn_partial=None, batch=1, c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0):
+    """cperm = taps > 1: C's columns are (tap, channel) pairs written in nn.Conv1d's [Co][Ci][K]
+    weight layout (a conv weight gradient straight into .grad)."""
     _dev(c, bias, bn_partial, c_bf16, residual)
     assert c.dtype == torch.float32
     d = L.GemmDesc()
@@ -97,6 +99,7 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     d.compute = _COMPUTE if comp is None else comp
     d.c_bf16 = _ptr(c_bf16)
     d.residual = _ptr(residual)
+    d.cperm = int(cperm)
     L.check(L.lib().avc_gemm(d, stream()), "avc_gemm")
 
 

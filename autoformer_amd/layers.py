@@ -24,6 +24,11 @@ _EPOCH = [0]
 _LAST_WGRAD_MAIN = os.environ.get("AVC_LAST_WGRAD_MAIN", "1") != "0"
 # diagnostics only (tools/ablate.sh): skip the side-stream weight-gradient GEMMs (wrong gradients)
 _ABLATE_WGRAD = os.environ.get("AVC_ABLATE_WGRAD") == "1"
+# weight packs rebuilt by batched avc_pack_batch launches instead of one kernel per pack: fewer
+# launches, but measured +0.12 ms per C2 step (its few per-group events let the next forward
+# start later than the per-pack events do), so off unless asked for
+_PACK_BATCH = os.environ.get("AVC_PACK_BATCH", "0") == "1"
+_CONV_DW_DIRECT = os.environ.get("AVC_CONV_DW_DIRECT", "1") != "0"
 
 # ---------------------------------------------------------------- gradient sink / side stream
 # In "sink" mode (set by TrainStep) parameter gradients are accumulated by the kernels
@@ -115,7 +120,7 @@ class PackCache:
     """Derived copy of some parameters (packed / transposed / bf16 weights), rebuilt when
     they change.  prefetch_packs() builds the next step's copies on the side stream right
     after the optimizer step; get() then only orders the current stream after that build."""
-    __slots__ = ("key", "val", "pending", "params", "build", "__weakref__")
+    __slots__ = ("key", "val", "pending", "params", "build", "ops", "__weakref__")
 
     def __init__(self):
         self.key = None
@@ -123,8 +128,11 @@ class PackCache:
         self.pending = None
         self.params = None
         self.build = None
+        self.ops = None  # optional: val -> list of pack ops rebuilding val in place (batched prefetch)
 
-    def get(self, params, build):
+    def get(self, params, build, ops=None):
+        if ops is not None:
+            self.ops = ops
         key = _pack_key(params)
         if key != self.key:
             pend, self.pending = self.pending, None
@@ -141,15 +149,76 @@ class PackCache:
         return self.val
 
 
+_BATCH = {}       # group index -> device op table of that group of packs
+_PACK_GROUP = 6   # caches per batched launch
+
+
+def _op_struct(o):
+    from ._lib import PackOp
+
+    st = PackOp()
+    st.src = o["src"]
+    st.src2 = o.get("src2") or None
+    st.dst = o["dst"]
+    st.kind = o["kind"]
+    st.out_dtype = o["dtype"]
+    d = list(o["dims"]) + [0, 0, 0]
+    st.d0, st.d1, st.d2 = d[0], d[1], d[2]
+    st.ld_out = o.get("ld", 0)
+    return st
+
+
+def _op_len(o):
+    """Units of an op in avc_pack_batch: 1024 elements, or a 32 x 32 transpose tile."""
+    from ._lib import PACK_CONV_D, PACK_CONV_F, PACK_TRANSPOSE
+
+    d = o["dims"]
+    if o["kind"] == PACK_TRANSPOSE:
+        return -(-d[0] // 32) * -(-d[1] // 32)
+    n = d[0] * d[1] * d[2] if o["kind"] in (PACK_CONV_F, PACK_CONV_D) else d[0]
+    return -(-n // 1024)
+
+
+def _batch_plan(caches, group=0):
+    """Device op table (avc_pack_op[]) + unit prefix for the caches that describe their packs;
+    rebuilt only when a cache's buffers or parameters moved."""
+    import ctypes
+
+    sig = tuple((id(c), tuple(p.data_ptr() for p in c.params),
+                 tuple(t.data_ptr() for t in c.val if t is not None) if isinstance(c.val, tuple) else c.val.data_ptr())
+                for c in caches)
+    plan = _BATCH.get(group)
+    if plan is not None and plan["sig"] == sig:
+        return plan
+    ops = [o for c in caches for o in c.ops(c.val)]
+    arr = (_op_struct_type() * len(ops))(*[_op_struct(o) for o in ops])
+    prefix = [0]
+    for o in ops:
+        prefix.append(prefix[-1] + _op_len(o))
+    dev = caches[0].params[0].device
+    raw = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(arr), ctypes.sizeof(arr))), dtype=torch.uint8)
+    plan = {"sig": sig, "ops": raw.to(dev), "prefix": torch.tensor(prefix, dtype=torch.int64).to(dev), "n": len(ops),
+            "total": prefix[-1]}
+    _BATCH[group] = plan
+    return plan
+
+
+def _op_struct_type():
+    from ._lib import PackOp
+    return PackOp
+
+
 def prefetch_packs() -> None:
     """After the optimizer step: rebuild every weight pack of the plan on the side stream, in
-    the order the forward will ask for them (the encoder's first, so the forward's first
-    wait is short and the rest are ready long before the decoder / postnet need them)."""
+    the order the forward will ask for them.  The packs whose cache describes them (conv, LSTM,
+    linear: `PackCache.ops`) are rewritten IN PLACE by one batched launch (avc_pack_batch);
+    the others are rebuilt one by one (the encoder's first, so the forward's first wait is short)."""
     side = _SINK["side"]
     if side is None or not _PLAN:
         return
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side), torch.no_grad():
+        batched = []
         for ref in list(_PLAN):
             c = ref()
             if c is None:
@@ -158,10 +227,24 @@ def prefetch_packs() -> None:
             key = _pack_key(c.params)
             if key == c.key:
                 continue
+            if _PACK_BATCH and c.ops is not None and c.val is not None and c.key is not None and c.key[1] == key[1]:
+                batched.append((c, key))
+                continue
             val = c.build()
             ev = torch.cuda.Event()
             ev.record(side)
             c.pending = (key, val, ev)
+        # a few launches in first-use order, each with its own event: the next forward waits for
+        # the encoder's packs only, not for the whole batch
+        for gi in range(0, len(batched), _PACK_GROUP):
+            grp = batched[gi:gi + _PACK_GROUP]
+            plan = _batch_plan([c for c, _ in grp], gi)
+            K.L.call("avc_pack_batch", plan["ops"].data_ptr(), plan["prefix"].data_ptr(), plan["n"], plan["total"],
+                     K.stream())
+            ev = torch.cuda.Event()
+            ev.record(side)
+            for c, key in grp:
+                c.pending = (key, c.val, ev)
 
 
 def _need(t):
@@ -169,12 +252,21 @@ def _need(t):
 
 
 # =============================================================================== plain conv helpers
+def conv_pack_ops(w, val):
+    """Batched-pack ops (avc_pack_batch) rewriting (Wf, Wd) of conv weight w in place."""
+    from ._lib import PACK_CONV_D, PACK_CONV_F
+
+    Co, Ci, Kw = w.shape
+    return [{"src": w.data_ptr(), "dst": t.data_ptr(), "kind": kind, "dtype": K._dt(t), "dims": (Co, Ci, Kw)}
+            for t, kind in zip(val, (PACK_CONV_F, PACK_CONV_D))]
+
+
 def conv_packs(cache, w):
     """(Wf [Co][Kw*Ci], Wd [Ci][Kw*Co]) in the compute dtype, rebuilt when w changes."""
     def build():
         dt = K.compute()
         return K.conv_pack(w, 0, dt), K.conv_pack(w, 1, dt)
-    return cache.get([w], build)
+    return cache.get([w], build, ops=lambda val: conv_pack_ops(w, val))
 
 
 def conv_fwd(x, B, T_in, w, bias, pad, Wf, out=None):
@@ -188,12 +280,24 @@ def conv_fwd(x, B, T_in, w, bias, pad, Wf, out=None):
 
 
 def conv_wgrad(dy, x, B, T_in, T_out, w, pad, into=None):
+    """dW of a Conv1d, written by the GEMM epilogue straight into the [Co][Ci][K] layout
+    (accumulated into `into`, e.g. the parameter's .grad, when given)."""
     Co, Ci, Kw = w.shape
     M = B * T_out
-    dWf = torch.empty(Co, Kw * Ci, device=x.device)
+    sk = K.auto_split_k(Co, Kw * Ci, M)
+    # the direct [Co][Ci][K] epilogue scatters its columns 4*Kw bytes apart: with split-K atomics
+    # that is ~Kw x the atomic requests of the packed layout (measured +0.9 ms per C2 step), so
+    # split products go through the packed dWf and one unpack pass instead
+    if not _CONV_DW_DIRECT or (sk > 1 and Kw > 1):
+        dWf = torch.empty(Co, Kw * Ci, device=x.device)
+        K.gemm(Co, Kw * Ci, M, operand(dy, Co, kstrided=True),
+               operand(x, Ci, kstrided=True, window=(Kw, pad, T_out, T_in, Ci)), dWf, split_k=sk)
+        return K.conv_grad_unpack(dWf, Co, Ci, Kw, into=into)
+    dW = torch.empty(Co, Ci, Kw, device=x.device) if into is None else into
     K.gemm(Co, Kw * Ci, M, operand(dy, Co, kstrided=True),
-           operand(x, Ci, kstrided=True, window=(Kw, pad, T_out, T_in, Ci)), dWf, split_k=K.auto_split_k(Co, Kw * Ci, M))
-    return K.conv_grad_unpack(dWf, Co, Ci, Kw, into=into)
+           operand(x, Ci, kstrided=True, window=(Kw, pad, T_out, T_in, Ci)), dW.view(Co, Ci * Kw),
+           split_k=sk, accumulate=into is not None, cperm=Kw)
+    return dW
 
 
 def conv_dgrad(dy, B, T_in, T_out, w, pad, Wd, n_dx=None):
@@ -224,7 +328,7 @@ class ConvBNCore:
         def build():
             dt = K.compute()
             return K.conv_pack(w, 0, dt), K.conv_pack(w, 1, dt)
-        return self.cache.get([w], build)
+        return self.cache.get([w], build, ops=lambda val: conv_pack_ops(w, val))
 
     def forward(self, x, B, T_in, residual=None):
         conv, bn = self.conv, self.bn
@@ -263,11 +367,8 @@ class ConvBNCore:
         dy, dgamma, dbeta, dbias = K.bn_bwd(dA, None, y, mean, rstd, bn.weight, self.act, into=into, beta=bn.bias)
 
         def wgrad():
-            dWf = torch.empty(Co, Kw * Ci, device=x.device)
-            sk = K.auto_split_k(Co, Kw * Ci, M)
-            K.gemm(Co, Kw * Ci, M, operand(dy, Co, kstrided=True),
-                   operand(x, Ci, kstrided=True, window=(Kw, self.pad, T_out, T_in, Ci)), dWf, split_k=sk)
-            return K.conv_grad_unpack(dWf, Co, Ci, Kw, into=_grad_of(conv.weight) if sink else None)
+            return conv_wgrad(dy, x, B, T_in, T_out, conv.weight, self.pad,
+                              into=_grad_of(conv.weight) if sink else None)
         ev = mark()
         dx = None
         if n_dx:
@@ -396,7 +497,30 @@ class LSTMLayerCore:
             for d in range(dirs):
                 K.transpose(ps[4 * d], dt, out=wih_t[:, d * 4 * H:], ld_out=dirs * 4 * H)
             return wih, bsum, whh, whh_t, wih_t
-        return self.cache.get(ps, build)
+
+        def ops(val):
+            from ._lib import PACK_ADD, PACK_COPY, PACK_TRANSPOSE
+
+            wih, bsum, whh, whh_t, wih_t = val
+            H, dirs = self.H, self.dirs
+            G = 4 * H
+            out = []
+            for d in range(dirs):
+                w_ih, w_hh, b_ih, b_hh = ps[4 * d: 4 * d + 4]
+                In = w_ih.shape[1]
+                out.append({"src": w_ih.data_ptr(), "dst": wih[d * G:].data_ptr(), "kind": PACK_COPY,
+                            "dtype": K._dt(wih), "dims": (G * In,)})
+                out.append({"src": b_ih.data_ptr(), "src2": b_hh.data_ptr(), "dst": bsum[d * G:].data_ptr(),
+                            "kind": PACK_ADD, "dtype": K.F32, "dims": (G,)})
+                out.append({"src": w_hh.data_ptr(), "dst": whh[d * G:].data_ptr(), "kind": PACK_COPY,
+                            "dtype": K._dt(whh), "dims": (G * H,)})
+                if whh_t is not None:
+                    out.append({"src": w_hh.data_ptr(), "dst": whh_t[d * H:].data_ptr(), "kind": PACK_TRANSPOSE,
+                                "dtype": K._dt(whh_t), "dims": (G, H), "ld": G})
+                out.append({"src": w_ih.data_ptr(), "dst": wih_t[:, d * G:].data_ptr(), "kind": PACK_TRANSPOSE,
+                            "dtype": K._dt(wih_t), "dims": (G, In), "ld": dirs * G})
+            return out
+        return self.cache.get(ps, build, ops=ops)
 
     def forward(self, x, B, T):
         H, dirs = self.H, self.dirs
@@ -493,6 +617,13 @@ def lstm(mod, cores, x, B, T):
 
 
 # =============================================================================== linear
+def copy_pack_ops(w, val):
+    """Batched-pack op: val = w cast to the compute dtype."""
+    from ._lib import PACK_COPY
+
+    return [{"src": w.data_ptr(), "dst": val.data_ptr(), "kind": PACK_COPY, "dtype": K._dt(val), "dims": (w.numel(),)}]
+
+
 class _LinearFn(torch.autograd.Function):
     """LinearNorm (Norm.py:40-50) on frame-major rows."""
 
@@ -500,7 +631,7 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b, cache):
         M, In = x.shape
         Out = w.shape[0]
-        wc = cache.get([w], lambda: K.convert(w, K.compute()))
+        wc = cache.get([w], lambda: K.convert(w, K.compute()), ops=lambda val: copy_pack_ops(w, val))
         y = torch.empty(M, Out, device=x.device)
         K.gemm(M, Out, In, operand(x, In), operand(wc, In), y, bias=b)
         ctx.cache = cache

@@ -70,6 +70,9 @@ typedef struct {
   int compute;
   void* c_bf16;         /* nullable: also store C rounded to bf16 (same ldc), for the next GEMM */
   const float* residual; /* nullable: C = A.B + bias + residual (same ldc / batch stride) */
+  int cperm;             /* 0, or taps > 1: columns are (tap, channel) pairs, n = tap*(N/taps) + ch, and
+                            land at C[m*ldc + ch*taps + tap] -- a Conv1d weight gradient written straight
+                            into nn.Conv1d's [Co][Ci][K] layout (no bias / residual / bf16 / BN epilogue) */
 } avc_gemm_desc;
 
 int avc_abi_version(void);
@@ -240,6 +243,28 @@ int avc_pool3_mixer(const float* x, float* y, int B, int L, int C, int backward,
 int avc_patchify(const float* src, float* dst, int B, int L, int C, int ps, int backward, void* stream);
 /* dst[b] (+)= src[b]^T for B row-major R x C matrices. */
 int avc_transpose_batched(const float* src, float* dst, int B, int R, int C, int accumulate, void* stream);
+
+/* Batched weight packing: every bf16 / re-laid-out copy of the parameters the kernels read
+ * (conv Wf / Wd, LSTM W_ih / W_hh / W_hh^T / W_ih^T, b_ih + b_hh, linear W) rebuilt after the
+ * optimizer step in ONE launch instead of one small kernel per copy.  `ops` and `prefix`
+ * (device memory, caller-owned): op i covers UNITS [prefix[i], prefix[i+1]) of the launch, a
+ * unit being 1024 elements of a copy / add / conv re-layout (ceil(n / 1024) units) or one
+ * 32 x 32 tile of a transpose (ceil(d0 / 32) * ceil(d1 / 32) units); total = prefix[nops];
+ * nops <= 128. */
+enum { AVC_PACK_COPY = 0, AVC_PACK_TRANSPOSE = 1, AVC_PACK_CONV_F = 2, AVC_PACK_CONV_D = 3, AVC_PACK_ADD = 4 };
+typedef struct {
+  const float* src;   /* the fp32 parameter */
+  const float* src2;  /* AVC_PACK_ADD: second addend (b_hh), else null */
+  void* dst;
+  int kind;           /* AVC_PACK_* */
+  int out_dtype;      /* AVC_F32 / AVC_BF16 */
+  int d0, d1, d2;     /* COPY / ADD: n = d0.  TRANSPOSE: src [d0][d1] -> dst[c*ld_out + r].
+                         CONV_F: W [d0=Co][d1=Ci][d2=K] -> dst[co][k*Ci + ci];
+                         CONV_D: -> dst[ci][(K-1-k)*Co + co] (flipped taps: the data-gradient operand) */
+  int pad_;
+  long long ld_out;   /* TRANSPOSE: destination row stride (>= d0) */
+} avc_pack_op;
+int avc_pack_batch(const avc_pack_op* ops, const long long* prefix, int nops, long long total, void* stream);
 
 /* Fused Adam (torch.optim.Adam defaults, train.py:49,99) over a slice of one flat fp32 buffer.
  * state[0] = step count (float), state[1..2] = this step's bias corrections, updated on device

@@ -65,7 +65,8 @@ def test_struct_layout_matches_header(tmp_path):
 
     from autoformer_amd import _lib
 
-    fields = {"avc_operand": [f[0] for f in _lib.Operand._fields_], "avc_gemm_desc": [f[0] for f in _lib.GemmDesc._fields_]}
+    fields = {"avc_operand": [f[0] for f in _lib.Operand._fields_], "avc_gemm_desc": [f[0] for f in _lib.GemmDesc._fields_],
+              "avc_pack_op": [f[0] for f in _lib.PackOp._fields_]}
     src = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
     for st, fs in fields.items():
         src.append(f'printf("{st} %zu\\n", sizeof({st}));')
@@ -78,7 +79,7 @@ def test_struct_layout_matches_header(tmp_path):
     subprocess.run(["gcc", str(c), "-o", str(exe)], check=True)
     out = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
                                                                check=True).stdout.split("\n") if line)
-    for st, cls in (("avc_operand", _lib.Operand), ("avc_gemm_desc", _lib.GemmDesc)):
+    for st, cls in (("avc_operand", _lib.Operand), ("avc_gemm_desc", _lib.GemmDesc), ("avc_pack_op", _lib.PackOp)):
         assert int(out[st]) == ctypes.sizeof(cls), st
         for f in fields[st]:
             assert int(out[f"{st}.{f}"]) == getattr(cls, f).offset, (st, f)

@@ -53,3 +53,34 @@ def test_convert_matches_oracle_with_other_target_speaker():
     ref = outs[1].squeeze(1)[0, : T - 10].numpy()
     rel = np.abs(got - ref).max() / np.abs(ref).max()
     assert rel < 1e-3, rel
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["AutoVC_Adjust", "AutoVC2", "MetaConv2"])
+def test_converter_dispatch_matches_reference_get_trans_mel(name):
+    """Converter.get_trans_mel dispatches like util/evaluate.py:77-83: isAdjust ->
+    model(x, e_org, e_trg, True, mel_target); isAdain -> model(x, e_org, None, None) for the
+    source features, then model(x, e_org, e_trg, feature).  Same result as those calls made by
+    hand on an identically initialised model (train-mode BN, as the reference converts)."""
+    from autoformer_amd.convert import Converter
+    from tests.test_variants import _golden, _variant_model
+
+    dev = torch.device("cuda:0")
+    g = _golden(name)
+    x, e, x2, e2 = (g[k] for k in ("x", "emb", "x2", "emb2"))
+    T = x.shape[1]
+    adjust = name.endswith("_Adjust")
+    m1, m2 = _variant_model(name, dev), _variant_model(name, dev)
+    src, mt, trans = Converter(m1, T, dev).get_trans_mel(x[0], x2[0], e[0], e2[0], isAdjust=adjust,
+                                                         isAdain=not adjust)
+    xs, xt = torch.from_numpy(x[:1]).to(dev), torch.from_numpy(x2[:1]).to(dev)
+    eo, et = torch.from_numpy(e[:1]).to(dev), torch.from_numpy(e2[:1]).to(dev)
+    with torch.no_grad():
+        if adjust:
+            _, _, ref, _ = m2(xs, eo, et, True, xt)
+        else:
+            _, feature = m2(xs, eo, None, None)
+            _, ref, _ = m2(xs, eo, et, feature)
+    torch.testing.assert_close(src, xs)
+    torch.testing.assert_close(mt, xt)
+    torch.testing.assert_close(trans, ref.squeeze(1), rtol=1e-5, atol=1e-5)

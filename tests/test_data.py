@@ -95,3 +95,39 @@ def test_device_feed_matches_host_batches(vctk_like):
     for (hx, he), (dx, de) in zip(host, dev):
         torch.testing.assert_close(dx, hx, rtol=0, atol=0)
         torch.testing.assert_close(de, he, rtol=0, atol=0)
+
+
+# ---------------------------------------------------------------- pinned to the reference itself
+# tests/golden/data_ref.npz was written by the reference's own util/data_loader.py
+# (tests/golden/make_data_goldens.py) over the tree build_tree() makes.
+def _ref_tree(tmp_path):
+    from tests.golden.make_data_goldens import build_tree
+
+    root = str(tmp_path)
+    build_tree(root)
+    return root
+
+
+def test_items_match_reference_loader_fixture(tmp_path, golden):
+    from autoformer_amd.data import Utterances
+    from tests.golden.make_data_goldens import LEN_CROP as LC
+
+    g = golden("data_ref.npz")
+    ds = Utterances(_ref_tree(tmp_path), LC)
+    np.random.seed(1234)
+    got = [ds[int(i)] for i in g["order"]]
+    np.testing.assert_array_equal(np.stack([u for u, _ in got]), g["item_uttr"])
+    np.testing.assert_array_equal(np.stack([e for _, e in got]), g["item_emb"])
+
+
+def test_loader_epoch_matches_reference_loader_fixture(tmp_path, golden):
+    from autoformer_amd.data import get_loader
+    from tests.golden.make_data_goldens import LEN_CROP as LC
+
+    g = golden("data_ref.npz")
+    root = _ref_tree(tmp_path)
+    torch.manual_seed(99)
+    np.random.seed(4321)
+    batches = list(get_loader(root, batch_size=2, len_crop=LC))
+    np.testing.assert_array_equal(np.stack([x.numpy() for x, _ in batches]), g["epoch_x"])
+    np.testing.assert_array_equal(np.stack([e.numpy() for _, e in batches]), g["epoch_emb"])

@@ -504,3 +504,39 @@ def test_gemm_tt_time_shift_window():
     Kr.gemm(G, H, B * T, Kr.operand(dg.to(DEV), G, kstrided=True),
             Kr.operand(h.to(DEV), H, kstrided=True, window=(1, 1, T, T, H)), c)
     assert relf(c, ref) < 1e-5, relf(c, ref)
+
+
+@pytest.mark.gpu
+def test_pack_batch_matches_individual_packs():
+    """avc_pack_batch (one launch for many packs) == the per-pack kernels it replaces."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+    from autoformer_amd import layers as Lyr
+
+    A.set_compute("bf16")
+    dev = "cuda:0"
+    w = torch.randn(96, 40, 5, device=dev)
+    wih, whh = torch.randn(176, 72, device=dev), torch.randn(176, 44, device=dev)
+    bih, bhh = torch.randn(176, device=dev), torch.randn(176, device=dev)
+    ref = [Kr.conv_pack(w, 0, Kr.BF16), Kr.conv_pack(w, 1, Kr.BF16), Kr.convert(wih, Kr.BF16),
+           Kr.transpose(whh, Kr.BF16), Kr.add(bih, bhh)]
+    outs = [torch.empty_like(t) for t in ref]
+    from autoformer_amd._lib import PACK_ADD, PACK_CONV_D, PACK_CONV_F, PACK_COPY, PACK_TRANSPOSE
+    ops = [{"src": w.data_ptr(), "dst": outs[0].data_ptr(), "kind": PACK_CONV_F, "dtype": Kr.BF16, "dims": (96, 40, 5)},
+           {"src": w.data_ptr(), "dst": outs[1].data_ptr(), "kind": PACK_CONV_D, "dtype": Kr.BF16, "dims": (96, 40, 5)},
+           {"src": wih.data_ptr(), "dst": outs[2].data_ptr(), "kind": PACK_COPY, "dtype": Kr.BF16, "dims": (176 * 72,)},
+           {"src": whh.data_ptr(), "dst": outs[3].data_ptr(), "kind": PACK_TRANSPOSE, "dtype": Kr.BF16,
+            "dims": (176, 44), "ld": 176},
+           {"src": bih.data_ptr(), "src2": bhh.data_ptr(), "dst": outs[4].data_ptr(), "kind": PACK_ADD,
+            "dtype": Kr.F32, "dims": (176,)}]
+
+    class _C:  # the PackCache surface _batch_plan reads
+        pass
+    c = _C()
+    c.params, c.val, c.ops = [w, wih, whh, bih, bhh], tuple(outs), lambda val: ops
+    plan = Lyr._batch_plan([c], group=99)
+    Kr.L.call("avc_pack_batch", plan["ops"].data_ptr(), plan["prefix"].data_ptr(), plan["n"], plan["total"],
+              Kr.stream())
+    torch.cuda.synchronize()
+    for a, b in zip(outs, ref):
+        assert torch.equal(a, b)
