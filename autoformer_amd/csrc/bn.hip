@@ -8,6 +8,8 @@
 // activations is needed on the forward.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int PTILE = 128;  // rows per partial (must match gemm.hip BM)
@@ -17,7 +19,10 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 // One block per 64 channels; 4 row-groups of 64 threads stride over the per-tile partials
 // (independent loads, no serial chain).  Merge = two passes over the partials:
 //   mean = sum_t s_t / n;   M2 = sum_t [ q_t + n_t (s_t / n_t - mean)^2 ]   (Chan, parallel form)
-constexpr int FG = 16;  // row groups of the finalize reductions (1024 threads = 64 channels x 16)
+// 256-thread blocks: a 1024-thread finalize block needs 16 free wave slots on one CU and waits
+// behind the side stream's weight-gradient GEMMs (measured 14.8 us per backward finalize in the
+// C2 step); 4 row groups x 64 channels start anywhere
+constexpr int FG = 4;  // row groups of the finalize reductions (256 threads = 64 channels x 4)
 constexpr int FU = 8;   // partial rows per thread loaded together (independent loads in flight)
 
 // sum over b = grp, grp + FG, ... < nrb of NV consecutive floats at ws[(b*ld + c)*NV + v]:
@@ -43,7 +48,7 @@ __device__ __forceinline__ void strided_sums(const float* __restrict__ ws, int n
   }
 }
 
-__global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restrict__ partial, int M, int C,
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ partial, int M, int C,
                                                           const float* gamma, const float* beta, float* rmean,
                                                           float* rvar, long long* nbt, float momentum, float eps,
                                                           float* mean_out, float* rstd_out, float* scale,
@@ -138,42 +143,54 @@ __global__ void bn_stats_kernel(const float* y, long long ld, int M, int C, floa
   partial[((long long)blockIdx.y * C + c) * 2 + 1] = q;
 }
 
-__global__ void bn_apply_kernel(const float* __restrict__ y, const float* __restrict__ scale,
+// typed loads: activations / gradients stored fp32 or bf16 (bf16 compute mode keeps the
+// conv outputs y, the BN outputs and their gradients in bf16 -- half the bytes of every pass)
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ f32x4 ld4(const bf16* p) {
+  const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const bf16* p) { return (float)*p; }
+__device__ __forceinline__ void st4(float* o32, bf16* o16, long long e, f32x4 o) {
+  if (o32) *reinterpret_cast<f32x4*>(o32 + e) = o;
+  if (o16) *reinterpret_cast<bf16x4*>(o16 + e) = bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+}
+
+template <typename TY>
+__global__ void bn_apply_kernel(const TY* __restrict__ y, const float* __restrict__ scale,
                                 const float* __restrict__ shift, const float* __restrict__ res, float* __restrict__ out,
                                 bf16* __restrict__ out16, long long total4, int C, int act) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total4) return;
   long long e = i * 4;
   int c = (int)(e % C);
-  f32x4 v = *reinterpret_cast<const f32x4*>(y + e);
+  f32x4 v = ld4(y + e);
   f32x4 sc = *reinterpret_cast<const f32x4*>(scale + c);
   f32x4 sh = *reinterpret_cast<const f32x4*>(shift + c);
   f32x4 o;
 #pragma unroll
   for (int k = 0; k < 4; ++k) o[k] = act_fwd(v[k] * sc[k] + sh[k], act);
-  if (res) {
-    f32x4 r = *reinterpret_cast<const f32x4*>(res + e);
-    o += r;
-  }
-  *reinterpret_cast<f32x4*>(out + e) = o;
-  if (out16) *reinterpret_cast<bf16x4*>(out16 + e) = bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+  if (res) o += *reinterpret_cast<const f32x4*>(res + e);
+  st4(out, out16, e, o);
 }
 
-__global__ void bn_apply1_kernel(const float* __restrict__ y, const float* __restrict__ scale,
+template <typename TY>
+__global__ void bn_apply1_kernel(const TY* __restrict__ y, const float* __restrict__ scale,
                                  const float* __restrict__ shift, const float* __restrict__ res, float* __restrict__ out,
                                  bf16* __restrict__ out16, long long total, int C, int act) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int c = (int)(i % C);
-  float o = act_fwd(y[i] * scale[c] + shift[c], act);
+  float o = act_fwd(ld1(y + i) * scale[c] + shift[c], act);
   o = res ? o + res[i] : o;
-  out[i] = o;
+  if (out) out[i] = o;
   if (out16) out16[i] = (bf16)o;
 }
 
 // backward reduce: per (64-row block, 64 channels) partial sums of dz, dz*yhat, yhat.
-// 256 threads = 16 channel quads (float4, one 256-B row segment) x 16 row lanes; the 4 rows
-// of a lane are loaded together (12 independent 16-B loads in flight per thread).
+// 256 threads = 16 channel quads (4 channels, one 16-B fp32 / 8-B bf16 load) x 16 row lanes;
+// the 4 rows of a lane are loaded together (independent loads in flight).
 constexpr int RB = 64;
 
 // dz = dA * act'(.): from the stored activation output a (FROM_PRE = false) or from the
@@ -184,9 +201,9 @@ __device__ __forceinline__ float bn_dz(float g, float av, float yh, float gm, fl
   return FROM_PRE ? act_bwd_from_pre(g, yh * gm + bt, act) : act_bwd_from_out(g, av, act);
 }
 
-template <bool FROM_PRE>
-__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const float* __restrict__ dA, const float* __restrict__ a,
-                                                            const float* __restrict__ y,
+template <bool FROM_PRE, typename TD, typename TY>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TD* __restrict__ dA, const float* __restrict__ a,
+                                                            const TY* __restrict__ y,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd,
                                                             const float* __restrict__ gamma,
@@ -210,9 +227,9 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const float* __restr
     for (int i = 0; i < 4; ++i) {
       const int r = r0 + rl + 16 * i;
       const long long idx = (long long)(r < M ? r : 0) * C + c;
-      g[i] = *reinterpret_cast<const f32x4*>(dA + idx);
-      if (!FROM_PRE) av[i] = *reinterpret_cast<const f32x4*>(a + idx);
-      yv[i] = *reinterpret_cast<const f32x4*>(y + idx);
+      g[i] = ld4(dA + idx);
+      if (!FROM_PRE) av[i] = ld4(a + idx);
+      yv[i] = ld4(y + idx);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -247,9 +264,9 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const float* __restr
 }
 
 // scalar variant (C % 4 != 0): 64 channels x 4 row lanes
-template <bool FROM_PRE>
-__global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const float* __restrict__ dA, const float* __restrict__ a,
-                                                             const float* __restrict__ y,
+template <bool FROM_PRE, typename TD, typename TY>
+__global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const TD* __restrict__ dA, const float* __restrict__ a,
+                                                             const TY* __restrict__ y,
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ rstd,
                                                              const float* __restrict__ gamma,
@@ -266,8 +283,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const float* __rest
     const int r1 = min(M, r0 + RB);
     for (int r = r0 + rl; r < r1; r += 4) {
       const long long idx = (long long)r * C + c;
-      const float yh = (y[idx] - mu) * rs;
-      const float dz = bn_dz<FROM_PRE>(dA[idx], FROM_PRE ? 0.f : a[idx], yh, gm, bt, act);
+      const float yh = (ld1(y + idx) - mu) * rs;
+      const float dz = bn_dz<FROM_PRE>(ld1(dA + idx), FROM_PRE ? 0.f : a[idx], yh, gm, bt, act);
       s0 += dz;
       s1 += dz * yh;
       s2 += yh;
@@ -286,10 +303,10 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const float* __rest
 }
 
 // one block per 64 channels, 4 row groups reduce the per-block partials in parallel
-__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __restrict__ ws, int nrb, int M, int C,
-                                                               const float* gamma, const float* beta,
-                                                               const float* mean, const float* rstd, float* coef,
-                                                               float* dgamma, float* dbeta, float* dbias, int acc) {
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ ws, int nrb, int M, int C,
+                                                              const float* gamma, const float* beta,
+                                                              const float* mean, const float* rstd, float* coef,
+                                                              float* dgamma, float* dbeta, float* dbias, int acc) {
   __shared__ float red[3][FG][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -327,18 +344,18 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __re
   if (dbias) dbias[c] = acc ? dbias[c] + gb : gb;
 }
 
-template <bool FROM_PRE>
-__global__ void bn_bwd_apply_kernel(const float* __restrict__ dA, const float* __restrict__ a,
-                                    const float* __restrict__ y, const float* __restrict__ coef, long long total4,
+template <bool FROM_PRE, typename TD, typename TY>
+__global__ void bn_bwd_apply_kernel(const TD* __restrict__ dA, const float* __restrict__ a,
+                                    const TY* __restrict__ y, const float* __restrict__ coef, long long total4,
                                     int C, int act, float* __restrict__ dy, bf16* __restrict__ dy16) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total4) return;
   long long e = i * 4;
   int c = (int)(e % C);
-  f32x4 g = *reinterpret_cast<const f32x4*>(dA + e);
+  f32x4 g = ld4(dA + e);
   f32x4 av = {0.f, 0.f, 0.f, 0.f};
-  if (!FROM_PRE) av = *reinterpret_cast<const f32x4*>(a + e);
-  f32x4 yv = *reinterpret_cast<const f32x4*>(y + e);
+  if (!FROM_PRE) av = ld4(a + e);
+  f32x4 yv = ld4(y + e);
   const f32x4 k1 = *reinterpret_cast<const f32x4*>(coef + c);
   const f32x4 m1 = *reinterpret_cast<const f32x4*>(coef + C + c);
   const f32x4 m2 = *reinterpret_cast<const f32x4*>(coef + 2 * C + c);
@@ -353,21 +370,21 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ dA, const float* _
     const float dz = FROM_PRE ? act_bwd_from_pre(g[k], yc * k1[k] + bt[k], act) : act_bwd_from_out(g[k], av[k], act);
     o[k] = k1[k] * (dz - m1[k] - yc * rs[k] * m2[k]);
   }
-  *reinterpret_cast<f32x4*>(dy + e) = o;
-  if (dy16) *reinterpret_cast<bf16x4*>(dy16 + e) = bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+  st4(dy, dy16, e, o);
 }
 
-template <bool FROM_PRE>
-__global__ void bn_bwd_apply1_kernel(const float* __restrict__ dA, const float* __restrict__ a,
-                                     const float* __restrict__ y, const float* __restrict__ coef, long long total,
+template <bool FROM_PRE, typename TD, typename TY>
+__global__ void bn_bwd_apply1_kernel(const TD* __restrict__ dA, const float* __restrict__ a,
+                                     const TY* __restrict__ y, const float* __restrict__ coef, long long total,
                                      int C, int act, float* __restrict__ dy, bf16* __restrict__ dy16) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int c = (int)(i % C);
-  const float yc = y[i] - coef[3 * C + c], k1 = coef[c];
-  const float dz = FROM_PRE ? act_bwd_from_pre(dA[i], yc * k1 + coef[5 * C + c], act) : act_bwd_from_out(dA[i], a[i], act);
+  const float yc = ld1(y + i) - coef[3 * C + c], k1 = coef[c];
+  const float g = ld1(dA + i);
+  const float dz = FROM_PRE ? act_bwd_from_pre(g, yc * k1 + coef[5 * C + c], act) : act_bwd_from_out(g, a[i], act);
   const float o = k1 * (dz - coef[C + c] - yc * coef[4 * C + c] * coef[2 * C + c]);
-  dy[i] = o;
+  if (dy) dy[i] = o;
   if (dy16) dy16[i] = (bf16)o;
 }
 
@@ -421,7 +438,7 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const float* __rest
   }
 }
 
-__global__ void __launch_bounds__(1024) colsum_final_kernel(const float* __restrict__ ws, int nrb, int N, float* out,
+__global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restrict__ ws, int nrb, int N, float* out,
                                                             float* out2, int accumulate) {
   __shared__ float red[FG][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
@@ -445,7 +462,7 @@ extern "C" int avc_bn_finalize(const float* partial, int M, int C, const float* 
                                float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
                                float* mean, float* rstd, float* scale, float* shift, void* stream) {
   AVC_CHECK_ARG(partial && mean && rstd && scale && shift && M > 0 && C > 0, "avc_bn_finalize: bad args");
-  bn_finalize_kernel<<<cdiv(C, 64), 1024, 0, as_stream(stream)>>>(partial, M, C, gamma, beta, running_mean,
+  bn_finalize_kernel<<<cdiv(C, 64), 256, 0, as_stream(stream)>>>(partial, M, C, gamma, beta, running_mean,
                                                                    running_var, nbt, momentum, eps, mean, rstd,
                                                                    scale, shift);
   return avc_check_launch("avc_bn_finalize");
@@ -466,58 +483,87 @@ extern "C" int avc_bn_stats(const float* y, long long ld, int M, int C, float* p
   return avc_check_launch("avc_bn_stats");
 }
 
-extern "C" int avc_bn_apply(const float* y, const float* scale, const float* shift, const float* residual, float* out,
-                            void* out_bf16, int M, int C, int act, void* stream) {
+namespace {
+// dtype dispatch of the typed BN kernels: F(TY) / F(TD, TY) with float or bf16 pointers
+template <typename Fn>
+void with_type(int dt, Fn&& fn) {
+  if (dt == AVC_BF16) fn(static_cast<const bf16*>(nullptr));
+  else fn(static_cast<const float*>(nullptr));
+}
+}  // namespace
+
+extern "C" int avc_bn_apply(const void* y, int y_dtype, const float* scale, const float* shift,
+                            const float* residual, float* out, void* out_bf16, int M, int C, int act, void* stream) {
   bf16* o16 = reinterpret_cast<bf16*>(out_bf16);
-  AVC_CHECK_ARG(y && scale && shift && out && C > 0, "avc_bn_apply: bad args");
+  AVC_CHECK_ARG(y && scale && shift && (out || o16) && C > 0 && (y_dtype == AVC_F32 || y_dtype == AVC_BF16),
+                "avc_bn_apply: bad args");
   const long long total = (long long)M * C;
   if (total == 0) return 0;
-  if (C % 4 == 0)
-    bn_apply_kernel<<<cdiv(total / 4, 256), 256, 0, as_stream(stream)>>>(y, scale, shift, residual, out, o16, total / 4,
-                                                                        C, act);
-  else
-    bn_apply1_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(y, scale, shift, residual, out, o16, total, C,
-                                                                      act);
+  hipStream_t s = as_stream(stream);
+  const bool v4 = C % 4 == 0;
+  with_type(y_dtype, [&](auto tag) {
+    using TY = std::remove_const_t<std::remove_pointer_t<decltype(tag)>>;
+    const TY* yp = static_cast<const TY*>(y);
+    if (v4)
+      bn_apply_kernel<TY><<<cdiv(total / 4, 256), 256, 0, s>>>(yp, scale, shift, residual, out, o16, total / 4, C,
+                                                              act);
+    else
+      bn_apply1_kernel<TY><<<cdiv(total, 256), 256, 0, s>>>(yp, scale, shift, residual, out, o16, total, C, act);
+  });
   return avc_check_launch("avc_bn_apply");
 }
 
 extern "C" size_t avc_bn_bwd_ws(int M, int C) { return (size_t)cdiv(M, RB) * C * 3 + (size_t)C * 6 + 4; }
 
-extern "C" int avc_bn_bwd(const float* dA, const float* a, const float* y, const float* mean, const float* rstd,
-                          const float* gamma, const float* beta, int M, int C, int act, float* dy, void* dy_bf16,
-                          float* dgamma, float* dbeta, float* dbias, int accumulate, float* ws, void* stream) {
+extern "C" int avc_bn_bwd(const void* dA, int dA_dtype, const float* a, const void* y, int y_dtype,
+                          const float* mean, const float* rstd, const float* gamma, const float* beta, int M, int C,
+                          int act, float* dy, void* dy_bf16, float* dgamma, float* dbeta, float* dbias,
+                          int accumulate, float* ws, void* stream) {
   bf16* d16 = reinterpret_cast<bf16*>(dy_bf16);
-  AVC_CHECK_ARG(dA && y && mean && rstd && dy && ws && C > 0, "avc_bn_bwd: bad args");
+  AVC_CHECK_ARG(dA && y && mean && rstd && (dy || d16) && ws && C > 0 &&
+                    (dA_dtype == AVC_F32 || dA_dtype == AVC_BF16) && (y_dtype == AVC_F32 || y_dtype == AVC_BF16),
+                "avc_bn_bwd: bad args");
   hipStream_t s = as_stream(stream);
   const bool pre = a == nullptr;  // activation derivative from the recomputed pre-activation
   const int nrb = cdiv(M, RB);
   dim3 grid(cdiv(C, 64), nrb);
-  const bool v4 = C % 4 == 0 && aligned16(dA) && aligned16(y) && (pre || aligned16(a)) &&
-                  (!gamma || aligned16(gamma)) && (!beta || aligned16(beta));
-  if (v4) {
-    if (pre) bn_bwd_reduce_kernel<true><<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, gamma, beta, M, C, act, ws);
-    else bn_bwd_reduce_kernel<false><<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, gamma, beta, M, C, act, ws);
-  } else {
-    if (pre) bn_bwd_reduce1_kernel<true><<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, gamma, beta, M, C, act, ws);
-    else bn_bwd_reduce1_kernel<false><<<grid, 256, 0, s>>>(dA, a, y, mean, rstd, gamma, beta, M, C, act, ws);
-  }
+  // 4-wide loads: 8-B (bf16) / 16-B (fp32) aligned rows
+  auto al = [](const void* p, int dt) { return (reinterpret_cast<uintptr_t>(p) & (dt == AVC_BF16 ? 7 : 15)) == 0; };
+  const bool v4 = C % 4 == 0 && al(dA, dA_dtype) && al(y, y_dtype) && (pre || aligned16(a)) &&
+                  (!gamma || aligned16(gamma)) && (!beta || aligned16(beta)) && (!dy || aligned16(dy)) &&
+                  (!d16 || al(d16, AVC_BF16));
   // per-channel apply constants, planar [6][C], 16-B aligned
   const size_t coff = ((size_t)nrb * C * 3 + 3) & ~(size_t)3;
   float* coef = ws + coff;
-  bn_bwd_finalize_kernel<<<cdiv(C, 64), 1024, 0, s>>>(ws, nrb, M, C, gamma, beta, mean, rstd, coef, dgamma, dbeta,
-                                                       dbias, accumulate);
   const long long total = (long long)M * C;
-  if (v4) {
-    if (pre)
-      bn_bwd_apply_kernel<true><<<cdiv(total / 4, 256), 256, 0, s>>>(dA, a, y, coef, total / 4, C, act, dy, d16);
-    else
-      bn_bwd_apply_kernel<false><<<cdiv(total / 4, 256), 256, 0, s>>>(dA, a, y, coef, total / 4, C, act, dy, d16);
-  } else {
-    if (pre)
-      bn_bwd_apply1_kernel<true><<<cdiv(total, 256), 256, 0, s>>>(dA, a, y, coef, total, C, act, dy, d16);
-    else
-      bn_bwd_apply1_kernel<false><<<cdiv(total, 256), 256, 0, s>>>(dA, a, y, coef, total, C, act, dy, d16);
-  }
+  with_type(dA_dtype, [&](auto dtag) {
+    using TD = std::remove_const_t<std::remove_pointer_t<decltype(dtag)>>;
+    with_type(y_dtype, [&](auto ytag) {
+      using TY = std::remove_const_t<std::remove_pointer_t<decltype(ytag)>>;
+      const TD* dp = static_cast<const TD*>(dA);
+      const TY* yp = static_cast<const TY*>(y);
+      if (v4) {
+        if (pre) bn_bwd_reduce_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws);
+        else bn_bwd_reduce_kernel<false, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws);
+      } else {
+        if (pre) bn_bwd_reduce1_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws);
+        else bn_bwd_reduce1_kernel<false, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws);
+      }
+      bn_bwd_finalize_kernel<<<cdiv(C, 64), 256, 0, s>>>(ws, nrb, M, C, gamma, beta, mean, rstd, coef, dgamma, dbeta,
+                                                          dbias, accumulate);
+      if (v4) {
+        if (pre)
+          bn_bwd_apply_kernel<true, TD, TY><<<cdiv(total / 4, 256), 256, 0, s>>>(dp, a, yp, coef, total / 4, C, act, dy, d16);
+        else
+          bn_bwd_apply_kernel<false, TD, TY><<<cdiv(total / 4, 256), 256, 0, s>>>(dp, a, yp, coef, total / 4, C, act, dy, d16);
+      } else {
+        if (pre)
+          bn_bwd_apply1_kernel<true, TD, TY><<<cdiv(total, 256), 256, 0, s>>>(dp, a, yp, coef, total, C, act, dy, d16);
+        else
+          bn_bwd_apply1_kernel<false, TD, TY><<<cdiv(total, 256), 256, 0, s>>>(dp, a, yp, coef, total, C, act, dy, d16);
+      }
+    });
+  });
   return avc_check_launch("avc_bn_bwd");
 }
 
@@ -532,6 +578,6 @@ extern "C" int avc_colsum(const float* x, long long ld, int M, int N, float* out
     colsum_partial_kernel<true><<<dim3(cdiv(N, 64), nrb), 256, 0, s>>>(x, ld, M, N, ws);
   else
     colsum_partial_kernel<false><<<dim3(cdiv(N, 64), nrb), 256, 0, s>>>(x, ld, M, N, ws);
-  colsum_final_kernel<<<cdiv(N, 64), 1024, 0, s>>>(ws, nrb, N, out, out2, accumulate);
+  colsum_final_kernel<<<cdiv(N, 64), 256, 0, s>>>(ws, nrb, N, out, out2, accumulate);
   return avc_check_launch("avc_colsum");
 }

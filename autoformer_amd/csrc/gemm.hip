@@ -693,7 +693,7 @@ extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
   AVC_CHECK_ARG(d != nullptr, "avc_gemm: null desc");
   AVC_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0, "avc_gemm: negative dims");
   if (d->M == 0 || d->N == 0) return 0;
-  AVC_CHECK_ARG(d->c != nullptr, "avc_gemm: null C");
+  AVC_CHECK_ARG(d->c != nullptr || d->c_bf16 != nullptr, "avc_gemm: null C");
   GemmArgs g;
   g.M = d->M;
   g.N = d->N;
@@ -722,6 +722,8 @@ extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
   g.cpd = make_fastdiv(g.cperm ? (uint32_t)(d->N / g.cperm) : 1u);
   AVC_CHECK_ARG(!(g.bn_partial && (g.split_k > 1 || g.batch > 1 || d->accumulate)),
                 "avc_gemm: bn_partial needs split_k == 1, batch == 1, accumulate == 0");
+  AVC_CHECK_ARG(g.c || (!g.atomic && !d->accumulate && !g.cperm),
+                "avc_gemm: a bf16-only C (c == NULL) cannot accumulate, split K, sum a batch or permute");
   hipStream_t s = as_stream(stream);
   AVC_CHECK_ARG(!(g.res && g.atomic && g.batch > 1 && d->c_batch_stride == 0),
                 "avc_gemm: residual with a batch-summed output is not supported");

@@ -51,7 +51,7 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
   const int wm = wid >> 1, wn = wid & 1;
   const int rbase = m0 + wm * 64 + 4 * (lane >> 4);
   const int cbase = n0 + wn * WN + (lane & 15);
-  float* C = g.c + (long long)bz * g.cbs;
+  float* C = g.c ? g.c + (long long)bz * g.cbs : nullptr;  // null: bf16-only output
   bf16* C16 = g.c16 ? g.c16 + (long long)bz * g.cbs : nullptr;
   if (g.bias && ks == 0) {
 #pragma unroll
@@ -79,7 +79,7 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
           atomicAdd(C + o, v);
         } else {
           if (g.accumulate) v += C[o];
-          C[o] = v;
+          if (C) C[o] = v;
           if (C16) C16[o] = (bf16)v;
         }
       }

@@ -57,9 +57,10 @@ class Encoder(nn.Module):
         if T % self.freq:
             # the reference indexes out_forward[:, i + freq - 1] past T here (AutoVC.py:63)
             raise IndexError(f"len_crop {T} is not a multiple of freq {self.freq}")
-        h = Lyr.enc_conv0(self._convs[0], mel, c_org.contiguous(), B, T)
+        # conv outputs feed only the next conv / the BiLSTM input projection: bf16 storage
+        h = Lyr.enc_conv0(self._convs[0], mel, c_org.contiguous(), B, T, out_bf16=True)
         for core in self._convs[1:]:
-            h = Lyr.conv_bn(core, h, B, T)
+            h = Lyr.conv_bn(core, h, B, T, out_bf16=True)
         h = Lyr.lstm(self.lstm, self._lstm, h, B, T)
         return Lyr.codes(h, B, T, self.dim_neck, self.freq)
 
@@ -84,7 +85,7 @@ class Decoder(nn.Module):
     def frames(self, x, B, T):
         h = Lyr.lstm(self.lstm1, self._lstm1, x, B, T)
         for core in self._convs:
-            h = Lyr.conv_bn(core, h, B, T)
+            h = Lyr.conv_bn(core, h, B, T, out_bf16=True)
         h = Lyr.lstm(self.lstm2, self._lstm2, h, B, T)
         lin = self.linear_projection.linear_layer
         return Lyr.linear(h, lin.weight, lin.bias, self._lin)
@@ -110,7 +111,7 @@ class Postnet(nn.Module):
     def frames(self, mel, B, T, residual=None):
         h = mel
         for core in self._convs[:-1]:
-            h = Lyr.conv_bn(core, h, B, T)
+            h = Lyr.conv_bn(core, h, B, T, out_bf16=True)
         return Lyr.conv_bn(self._convs[-1], h, B, T, residual=residual)
 
     def forward(self, x):

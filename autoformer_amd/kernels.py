@@ -85,11 +85,15 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     """cperm = taps > 1: C's columns are (tap, channel) pairs written in nn.Conv1d's [Co][Ci][K]
     weight layout (a conv weight gradient straight into .grad)."""
     _dev(c, bias, bn_partial, c_bf16, residual)
-    assert c.dtype == torch.float32
+    if c.dtype == torch.bfloat16:  # bf16-only output
+        assert c_bf16 is None and not accumulate and split_k == 1 and not cperm
+        c, c_bf16 = None, c
+    else:
+        assert c.dtype == torch.float32
     d = L.GemmDesc()
     d.M, d.N, d.K, d.batch = int(M), int(N), int(K), int(batch)
     d.a, d.b = a, b
-    d.c = c.data_ptr()
+    d.c = _ptr(c)
     d.ldc = int(N if ldc is None else ldc)
     d.c_batch_stride = int(c_batch_stride)
     d.bias = _ptr(bias)
@@ -167,22 +171,35 @@ def twin(t):
     return t
 
 
-def bn_apply(y, scale, shift, act, residual=None, out=None, twin16=None):
+def bn_apply(y, scale, shift, act, residual=None, out=None, twin16=None, out_bf16=False):
+    """act(y*scale + shift) (+ residual); y fp32 or bf16.  out_bf16: the result is a bf16 tensor
+    (no fp32 copy -- an inter-layer activation only ever read as a bf16 GEMM operand); otherwise
+    fp32 with a bf16 twin in bf16 compute mode."""
     M, C = y.shape
-    out = torch.empty_like(y) if out is None else out
+    if out_bf16:
+        o16 = torch.empty(M, C, device=y.device, dtype=torch.bfloat16)
+        L.call("avc_bn_apply", y.data_ptr(), _dt(y), scale.data_ptr(), shift.data_ptr(), _ptr(residual), None,
+               o16.data_ptr(), M, C, int(act), stream())
+        return o16
+    out = torch.empty(M, C, device=y.device) if out is None else out
     o16 = _twin_buf(out, twin16)
-    L.call("avc_bn_apply", y.data_ptr(), scale.data_ptr(), shift.data_ptr(), _ptr(residual), out.data_ptr(), _ptr(o16),
-           M, C, int(act), stream())
+    L.call("avc_bn_apply", y.data_ptr(), _dt(y), scale.data_ptr(), shift.data_ptr(), _ptr(residual), out.data_ptr(),
+           _ptr(o16), M, C, int(act), stream())
     return attach_twin(out, o16)
 
 
-def bn_bwd(dA, a, y, mean, rstd, gamma, act, need_dbias=True, into=None, twin16=None, beta=None):
+def bn_bwd(dA, a, y, mean, rstd, gamma, act, need_dbias=True, into=None, twin16=None, beta=None, dy_bf16=False):
     """into = (dgamma, dbeta, dbias) buffers to accumulate into (direct gradient sink).
-    a = None: the activation derivative comes from the pre-activation (y-mean)*rstd*gamma + beta."""
+    a = None: the activation derivative comes from the pre-activation (y-mean)*rstd*gamma + beta.
+    dA and y may be fp32 or bf16; dy_bf16: dy is returned as a bf16 tensor only (it feeds bf16
+    GEMMs alone), else fp32 with a bf16 twin in bf16 compute mode."""
     M, C = y.shape
     dev = y.device
-    dy = torch.empty_like(y)
-    d16 = _twin_buf(dy, twin16)
+    if dy_bf16:
+        dy, d16 = None, torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+    else:
+        dy = torch.empty(M, C, device=dev)
+        d16 = _twin_buf(dy, twin16)
     if into is not None:
         dgamma, dbeta, dbias = into
     else:
@@ -190,10 +207,11 @@ def bn_bwd(dA, a, y, mean, rstd, gamma, act, need_dbias=True, into=None, twin16=
         dbeta = torch.empty(C, device=dev)
         dbias = torch.empty(C, device=dev) if need_dbias else None
     ws = torch.empty(int(L.lib().avc_bn_bwd_ws(M, C)), device=dev)
-    L.call("avc_bn_bwd", dA.data_ptr(), _ptr(a), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), _ptr(gamma),
-           _ptr(beta), M, C, int(act), dy.data_ptr(), _ptr(d16), _ptr(dgamma), _ptr(dbeta), _ptr(dbias),
+    L.call("avc_bn_bwd", dA.data_ptr(), _dt(dA), _ptr(a), y.data_ptr(), _dt(y), mean.data_ptr(), rstd.data_ptr(),
+           _ptr(gamma), _ptr(beta), M, C, int(act), _ptr(dy), _ptr(d16), _ptr(dgamma), _ptr(dbeta), _ptr(dbias),
            int(into is not None), ws.data_ptr(), stream())
-    return attach_twin(dy, d16), dgamma, dbeta, dbias
+    out = d16 if dy_bf16 else attach_twin(dy, d16)
+    return out, dgamma, dbeta, dbias
 
 
 def colsum(x, M, N, ld=None, out=None, accumulate=False, out2=None):

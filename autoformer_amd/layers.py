@@ -330,14 +330,20 @@ class ConvBNCore:
             return K.conv_pack(w, 0, dt), K.conv_pack(w, 1, dt)
         return self.cache.get([w], build, ops=lambda val: conv_pack_ops(w, val))
 
-    def forward(self, x, B, T_in, residual=None):
+    def forward(self, x, B, T_in, residual=None, out_bf16=False):
+        """out_bf16 (bf16 compute only): the activation is returned as a bf16 tensor -- for a
+        layer whose output is read by bf16 GEMMs alone (the next conv / an LSTM input
+        projection); its gradient then arrives in bf16 too.  In bf16 mode the conv output y
+        (kept for the BN backward) is stored in bf16; the BN statistics come from the fp32
+        accumulators in the GEMM epilogue."""
         conv, bn = self.conv, self.bn
         Co, Ci, Kw = conv.weight.shape
         T_out = T_in + 2 * self.pad - Kw + 1
         M = B * T_out
         Wf, _ = self.packs()
         x = K.twin(x)
-        y = torch.empty(M, Co, device=x.device)
+        bf = K.compute() == K.BF16
+        y = torch.empty(M, Co, device=x.device, dtype=torch.bfloat16 if bf else torch.float32)
         partial = K.bn_partial_buffer(M, Co, x.device) if bn.training else None
         K.gemm(M, Co, Kw * Ci, operand(x, Ci, window=(Kw, self.pad, T_out, T_in, Ci)), operand(Wf, Kw * Ci), y,
                bias=conv.bias, bn_partial=partial)
@@ -351,7 +357,7 @@ class ConvBNCore:
         else:
             stats = K.bn_eval(bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.eps)
         mean, rstd, scale, shift = stats
-        a = K.bn_apply(y, scale, shift, self.act, residual)
+        a = K.bn_apply(y, scale, shift, self.act, residual, out_bf16=out_bf16 and bf and residual is None)
         return a, (y, mean, rstd, T_out)
 
     def backward(self, dA, x, a, saved, B, T_in, n_dx):
@@ -364,7 +370,9 @@ class ConvBNCore:
         sink = _SINK["on"]
         into = (_grad_of(bn.weight), _grad_of(bn.bias), _grad_of(conv.bias)) if sink else None
         # act' from the recomputed pre-activation: the activation output `a` is not re-read
-        dy, dgamma, dbeta, dbias = K.bn_bwd(dA, None, y, mean, rstd, bn.weight, self.act, into=into, beta=bn.bias)
+        # bf16 mode: dy feeds the two bf16 GEMMs below only -> stored in bf16 alone
+        dy, dgamma, dbeta, dbias = K.bn_bwd(dA, None, y, mean, rstd, bn.weight, self.act, into=into, beta=bn.bias,
+                                            dy_bf16=K.compute() == K.BF16)
 
         def wgrad():
             return conv_wgrad(dy, x, B, T_in, T_out, conv.weight, self.pad,
@@ -373,7 +381,7 @@ class ConvBNCore:
         dx = None
         if n_dx:
             _, Wd = self.packs()
-            dx = torch.empty(B * T_in, n_dx, device=x.device)
+            dx = torch.empty(B * T_in, n_dx, device=x.device, dtype=x.dtype)
             K.gemm(B * T_in, n_dx, Kw * Co, operand(dy, Co, window=(Kw, Kw - 1 - self.pad, T_in, T_out, Co)),
                    operand(Wd, Kw * Co), dx)
         if sink and (n_dx or not _LAST_WGRAD_MAIN):
@@ -395,8 +403,8 @@ class ConvBNCore:
 
 class _ConvBNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, core, B, T_in, residual, w, b, gamma, beta):
-        a, saved = core.forward(x, B, T_in, residual)
+    def forward(ctx, x, core, B, T_in, residual, out_bf16, w, b, gamma, beta):
+        a, saved = core.forward(x, B, T_in, residual, out_bf16)
         ctx.core, ctx.B, ctx.T_in, ctx.saved = core, B, T_in, saved
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, a)
@@ -411,12 +419,14 @@ class _ConvBNFn(torch.autograd.Function):
         n_dx = x.shape[1] if ctx.needs_input_grad[0] else 0
         dx, dW, db, dg, dbe = ctx.core.backward(dA, x, a, ctx.saved, ctx.B, ctx.T_in, n_dx)
         dres = dA if ctx.has_res and ctx.needs_input_grad[4] else None
-        return dx, None, None, None, dres, dW, db, dg, dbe
+        return dx, None, None, None, dres, None, dW, db, dg, dbe
 
 
-def conv_bn(core: ConvBNCore, x, B, T_in, residual=None):
+def conv_bn(core: ConvBNCore, x, B, T_in, residual=None, out_bf16=False):
+    """out_bf16: the caller feeds the result only to another conv_bn / lstm (bf16 storage in
+    bf16 compute mode, see ConvBNCore.forward)."""
     c, bn = core.conv, core.bn
-    return _ConvBNFn.apply(x, core, B, T_in, residual, c.weight, c.bias, bn.weight, bn.bias)
+    return _ConvBNFn.apply(x, core, B, T_in, residual, out_bf16, c.weight, c.bias, bn.weight, bn.bias)
 
 
 class _EncConv0Fn(torch.autograd.Function):
@@ -424,9 +434,9 @@ class _EncConv0Fn(torch.autograd.Function):
     data-gradient GEMM restricted to the 80 mel channels."""
 
     @staticmethod
-    def forward(ctx, mel2d, emb, core, B, T, w, b, gamma, beta):
+    def forward(ctx, mel2d, emb, core, B, T, out_bf16, w, b, gamma, beta):
         x = K.enc_concat(mel2d, emb, B, T)
-        a, saved = core.forward(x, B, T)
+        a, saved = core.forward(x, B, T, None, out_bf16)
         ctx.core, ctx.B, ctx.T, ctx.saved, ctx.n_mel = core, B, T, saved, mel2d.shape[1]
         ctx.save_for_backward(x, a)
         ctx.x16 = getattr(x, "_bf16", None)
@@ -446,12 +456,12 @@ class _EncConv0Fn(torch.autograd.Function):
         if demb_needed:
             demb = K.segsum(dx[:, nm:], ctx.B, ctx.T, x.shape[1] - nm, ld=x.shape[1])
             dx = dx[:, :nm] if ctx.needs_input_grad[0] else None
-        return dx, demb, None, None, None, dW, db, dg, dbe
+        return dx, demb, None, None, None, None, dW, db, dg, dbe
 
 
-def enc_conv0(core, mel2d, emb, B, T):
+def enc_conv0(core, mel2d, emb, B, T, out_bf16=False):
     c, bn = core.conv, core.bn
-    return _EncConv0Fn.apply(mel2d, emb, core, B, T, c.weight, c.bias, bn.weight, bn.bias)
+    return _EncConv0Fn.apply(mel2d, emb, core, B, T, out_bf16, c.weight, c.bias, bn.weight, bn.bias)
 
 
 # =============================================================================== LSTM
@@ -578,7 +588,7 @@ class LSTMLayerCore:
         ev = mark()
         dx = None
         if need_dx:
-            dx = torch.empty(M, In, device=x.device)
+            dx = torch.empty(M, In, device=x.device, dtype=x.dtype)  # bf16 for a bf16-stored input
             K.gemm(M, In, G, operand(dg, G), operand(wih_t, G), dx)
         if sink:
             with _Side(ev) as sd:

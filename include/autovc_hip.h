@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 5
+#define AVC_ABI_VERSION 6
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -68,7 +68,8 @@ typedef struct {
   int split_k;
   float* bn_partial;
   int compute;
-  void* c_bf16;         /* nullable: also store C rounded to bf16 (same ldc), for the next GEMM */
+  void* c_bf16;         /* nullable: also store C rounded to bf16 (same ldc), for the next GEMM; with c == NULL
+                            (no accumulate / split-K / batch-sum / cperm) C is stored in bf16 only */
   const float* residual; /* nullable: C = A.B + bias + residual (same ldc / batch stride) */
   int cperm;             /* 0, or taps > 1: columns are (tap, channel) pairs, n = tap*(N/taps) + ch, and
                             land at C[m*ldc + ch*taps + tap] -- a Conv1d weight gradient written straight
@@ -100,8 +101,10 @@ int avc_bn_eval(const float* running_mean, const float* running_var, const float
 /* Per-channel statistics pass for inputs that did not come out of avc_gemm (ld >= C). */
 int avc_bn_stats(const float* y, long long ld, int M, int C, float* partial, void* stream);
 
-/* out[r][c] = act(y[r][c]*scale[c] + shift[c]) (+ residual[r][c]); rows of length C. */
-int avc_bn_apply(const float* y, const float* scale, const float* shift, const float* residual,
+/* out[r][c] = act(y[r][c]*scale[c] + shift[c]) (+ residual[r][c]); rows of length C.
+ * y is fp32 or bf16 (y_dtype = AVC_F32 / AVC_BF16); out (fp32) and out_bf16 are each nullable,
+ * not both (bf16 compute mode stores inter-layer activations in bf16 only). */
+int avc_bn_apply(const void* y, int y_dtype, const float* scale, const float* shift, const float* residual,
                  float* out, void* out_bf16, int M, int C, int act, void* stream);
 
 /* BatchNorm1d + activation backward.  yhat = (y-mean)*rstd; dz = dA * act'(.), taken from the
@@ -110,11 +113,12 @@ int avc_bn_apply(const float* y, const float* scale, const float* shift, const f
  * when a residual was added after the activation).
  * Writes dy = gamma*rstd*(dz - sum(dz)/N - yhat*sum(dz*yhat)/N), and dgamma, dbeta and
  * the (analytically ~0) bias gradient of the producing conv (accumulate != 0: added into them).
+ * dA and y are fp32 or bf16 (their dtype arguments); dy (fp32) and dy_bf16 are each nullable, not both.
  * `ws` >= avc_bn_bwd_ws floats. */
 size_t avc_bn_bwd_ws(int M, int C);
-int avc_bn_bwd(const float* dA, const float* a, const float* y, const float* mean, const float* rstd,
-               const float* gamma, const float* beta, int M, int C, int act, float* dy, void* dy_bf16,
-               float* dgamma, float* dbeta, float* dbias, int accumulate, float* ws, void* stream);
+int avc_bn_bwd(const void* dA, int dA_dtype, const float* a, const void* y, int y_dtype, const float* mean,
+               const float* rstd, const float* gamma, const float* beta, int M, int C, int act, float* dy,
+               void* dy_bf16, float* dgamma, float* dbeta, float* dbias, int accumulate, float* ws, void* stream);
 
 /* out[n] (+)= sum_m x[m*ld + n] (bias gradients); out2 (nullable) receives the same sums (an
  * LSTM's b_ih and b_hh share one gradient, nn.LSTM AutoVC.py:43,77,96).  ws >= avc_colsum_ws floats. */

@@ -168,13 +168,12 @@ def test_bn_stats_epilogue_and_finalize(M, C):
 
 @pytest.mark.parametrize("act", [0, 1, 2])
 @pytest.mark.parametrize("from_pre", [False, True])
-@pytest.mark.parametrize("C", [96, 90])
-def test_bn_act_forward_backward(act, from_pre, C):
+@pytest.mark.parametrize("M,C", [(1000, 96), (1000, 90), (8192, 512), (300, 80)])
+def test_bn_act_forward_backward(act, from_pre, M, C):
     """BN + activation backward; from_pre: act' recomputed from yhat*gamma + beta (a = None),
-    C = 90 takes the scalar (C % 4 != 0) kernels."""
+    C = 90 takes the scalar (C % 4 != 0) kernels, the others the fused reduce/apply pair."""
     from autoformer_amd import kernels as Kr
 
-    M = 1000
     y = torch.randn(M, C) * 2 + 1
     gamma, beta = torch.rand(C) + 0.5, torch.randn(C)
     yt = y.clone().requires_grad_(True)
@@ -197,6 +196,53 @@ def test_bn_act_forward_backward(act, from_pre, C):
     assert relf(dgam, g_t.grad) < 1e-5
     assert relf(dbet, b_t.grad) < 1e-5
     assert float(dbias.abs().max()) < 1e-3
+
+
+@pytest.mark.parametrize("act", [1, 2])
+@pytest.mark.parametrize("M,C", [(8192, 512), (1000, 90), (300, 80)])
+def test_bn_bf16_storage(act, M, C):
+    """bf16-stored y / dA / outputs (bf16 compute mode): the kernels compute in fp32 from the
+    bf16 values, so they must match the fp32 path run on the same bf16-rounded inputs to fp32
+    rounding, and the bf16-only outputs must be those results rounded once."""
+    from autoformer_amd import kernels as Kr
+
+    y = (torch.randn(M, C) * 2 + 1).bfloat16()
+    dA = torch.randn(M, C).bfloat16()
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C)
+    yd, y32 = y.to(DEV), y.float().to(DEV)
+    part = Kr.bn_stats(y32, M, C)
+    mean, rstd, scale, shift = Kr.bn_finalize(part, M, C, gamma.to(DEV), beta.to(DEV), None, None, None, 0.1, 1e-5)
+    a32 = Kr.bn_apply(y32, scale, shift, act)
+    a16 = Kr.bn_apply(yd, scale, shift, act, out_bf16=True)
+    assert a16.dtype == torch.bfloat16
+    assert torch.equal(a16, a32.bfloat16())
+    g_, b_ = gamma.to(DEV), beta.to(DEV)
+    dy32, dg32, db32, _ = Kr.bn_bwd(dA.float().to(DEV), None, y32, mean, rstd, g_, act, beta=b_)
+    dy16, dg16, db16, _ = Kr.bn_bwd(dA.to(DEV), None, yd, mean, rstd, g_, act, beta=b_, dy_bf16=True)
+    assert dy16.dtype == torch.bfloat16
+    assert torch.equal(dy16, dy32.bfloat16())
+    assert torch.equal(dg16, dg32) and torch.equal(db16, db32)
+
+
+def test_gemm_bf16_only_output():
+    """c dtype bf16: the epilogue stores only the bf16 rounding of the fp32 result (with bias
+    and BN partial statistics taken from the fp32 accumulators)."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute("bf16")
+    M, N, Kd = 1024, 512, 320
+    x = torch.randn(M, Kd, device=DEV).bfloat16()
+    w = torch.randn(N, Kd, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    c32 = torch.empty(M, N, device=DEV)
+    p32 = Kr.bn_partial_buffer(M, N, DEV)
+    Kr.gemm(M, N, Kd, Kr.operand(x, Kd), Kr.operand(w, Kd), c32, bias=bias, bn_partial=p32)
+    c16 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    p16 = Kr.bn_partial_buffer(M, N, DEV)
+    Kr.gemm(M, N, Kd, Kr.operand(x, Kd), Kr.operand(w, Kd), c16, bias=bias, bn_partial=p16)
+    assert torch.equal(c16, c32.bfloat16())
+    assert torch.equal(p16, p32)
 
 
 def _lstm_case(B, T, In, H, dirs, comp):
