@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip"]
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -37,6 +37,12 @@ class GemmDesc(ctypes.Structure):
                 ("c_bf16", c_void_p), ("residual", c_void_p), ("cperm", c_int)]
 
 
+class BnFin(ctypes.Structure):
+    _fields_ = [("gamma", c_void_p), ("beta", c_void_p), ("running_mean", c_void_p), ("running_var", c_void_p),
+                ("num_batches_tracked", c_void_p), ("momentum", c_float), ("eps", c_float), ("nupd", c_int),
+                ("mean", c_void_p), ("rstd", c_void_p), ("scale", c_void_p), ("shift", c_void_p)]
+
+
 class PackOp(ctypes.Structure):
     _fields_ = [("src", c_void_p), ("src2", c_void_p), ("dst", c_void_p), ("kind", c_int), ("out_dtype", c_int),
                 ("d0", c_int), ("d1", c_int), ("d2", c_int), ("pad_", c_int), ("ld_out", c_ll)]
@@ -49,6 +55,7 @@ _SIGS = {
     "avc_abi_version": (c_int, []),
     "avc_last_error": (ctypes.c_char_p, []),
     "avc_gemm": (c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
+    "avc_gemm_bn": (c_int, [ctypes.POINTER(GemmDesc), ctypes.POINTER(BnFin), c_void_p]),
     "avc_bn_finalize": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
                                 c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "avc_bn_eval": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_void_p,

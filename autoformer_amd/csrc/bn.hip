@@ -8,6 +8,8 @@
 // activations is needed on the forward.
 #include "common.h"
 
+#include <atomic>
+#include <mutex>
 #include <type_traits>
 
 namespace {
@@ -27,22 +29,22 @@ constexpr int FU = 8;   // partial rows per thread loaded together (independent 
 
 // sum over b = grp, grp + FG, ... < nrb of NV consecutive floats at ws[(b*ld + c)*NV + v]:
 // FU rows' loads are issued before any is added (one memory latency per FU*FG rows, not per row)
-template <int NV>
+template <int NV, bool SC1 = false, int FUN = FU>  // SC1: partials handed over within the launch
 __device__ __forceinline__ void strided_sums(const float* __restrict__ ws, int nrb, long long ld, int c, int grp,
                                              float (&out)[NV]) {
 #pragma unroll
   for (int v = 0; v < NV; ++v) out[v] = 0.f;
-  for (int b0 = grp; b0 < nrb; b0 += FG * FU) {
-    float x[FU][NV];
+  for (int b0 = grp; b0 < nrb; b0 += FG * FUN) {
+    float x[FUN][NV];
 #pragma unroll
-    for (int u = 0; u < FU; ++u) {
+    for (int u = 0; u < FUN; ++u) {
       const int b = b0 + u * FG;
       const float* p = ws + ((long long)(b < nrb ? b : 0) * ld + c) * NV;
 #pragma unroll
-      for (int v = 0; v < NV; ++v) x[u][v] = b < nrb ? p[v] : 0.f;
+      for (int v = 0; v < NV; ++v) x[u][v] = b < nrb ? (SC1 ? ld_sc1(p + v) : p[v]) : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < FU; ++u)
+    for (int u = 0; u < FUN; ++u)
 #pragma unroll
       for (int v = 0; v < NV; ++v) out[v] += x[u][v];
   }
@@ -53,51 +55,16 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
                                                           float* rvar, long long* nbt, float momentum, float eps,
                                                           float* mean_out, float* rstd_out, float* scale,
                                                           float* shift) {
-  __shared__ float red[FG][64];
+  __shared__ float red[FG * 64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
   const int nt = (M + PTILE - 1) / PTILE;
   const bool cv = c < C;
-  float sq[2] = {0.f, 0.f};
-  if (cv) strided_sums<2>(partial, nt, C, c, grp, sq);
-  red[grp][cl] = sq[0];
-  __syncthreads();
-  const float n = (float)M;
-  float tot = 0.f;
-#pragma unroll
-  for (int i = 0; i < FG; ++i) tot += red[i][cl];
-  const float mean = tot / n;
-  __syncthreads();
-  float q = 0.f;
-  if (cv) {
-    // second pass over the (L2-resident) partials, FU tiles' loads in flight together
-    for (int t0 = grp; t0 < nt; t0 += FG * FU) {
-      float ps[FU], pq[FU];
-#pragma unroll
-      for (int u = 0; u < FU; ++u) {
-        const int t = t0 + u * FG;
-        const float* p = partial + ((long long)(t < nt ? t : 0) * C + c) * 2;
-        ps[u] = p[0];
-        pq[u] = p[1];
-      }
-#pragma unroll
-      for (int u = 0; u < FU; ++u) {
-        const int t = t0 + u * FG;
-        if (t < nt) {
-          const float nb = (float)min(PTILE, M - t * PTILE);
-          const float d = ps[u] / nb - mean;
-          q += pq[u] + nb * d * d;
-        }
-      }
-    }
-  }
-  red[grp][cl] = q;
-  __syncthreads();
+  float mean, m2;
+  chan_merge<16, false>(partial, nt, C, c, cv, grp, FG, cl, 64, M, PTILE, red, mean, m2);
   if (grp != 0 || !cv) return;
-  float m2 = 0.f;
-#pragma unroll
-  for (int i = 0; i < FG; ++i) m2 += red[i][cl];
+  const float n = (float)M;
   const float var = m2 / n;
   const float rstd = 1.f / sqrtf(var + eps);
   const float g = gamma ? gamma[c] : 1.f;
@@ -188,10 +155,80 @@ __global__ void bn_apply1_kernel(const TY* __restrict__ y, const float* __restri
   if (out16) out16[i] = (bf16)o;
 }
 
+// Backward finalize of one 64-channel strip by one 256-thread block (4 row groups reduce the
+// per-row-block partials in parallel): apply coefficients + dgamma / dbeta / conv-bias gradient.
+struct BwdFin {
+  const float* gamma;
+  const float* beta;
+  const float* mean;
+  const float* rstd;
+  float* coef;
+  float* dgamma;
+  float* dbeta;
+  float* dbias;
+  int acc;
+};
+
+template <bool SC1>
+__device__ __forceinline__ void bwd_finalize_strip(const float* ws, int nrb, int M, int C, int strip,
+                                                   const BwdFin& f) {
+  __shared__ float red[3][FG][64];
+  const float* gamma = f.gamma;
+  const float* beta = f.beta;
+  float* coef = f.coef;
+  float* dgamma = f.dgamma;
+  float* dbeta = f.dbeta;
+  float* dbias = f.dbias;
+  const int acc = f.acc;
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = strip * 64 + cl;
+  float sv[3] = {0.f, 0.f, 0.f};
+  if (c < C) strided_sums<3, SC1, 32>(ws, nrb, C, c, grp, sv);
+  float s0 = sv[0], s1 = sv[1], s2 = sv[2];
+  red[0][grp][cl] = s0;
+  red[1][grp][cl] = s1;
+  red[2][grp][cl] = s2;
+  __syncthreads();
+  if (grp != 0 || c >= C) return;
+  s0 = s1 = s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < FG; ++i) {
+    s0 += red[0][i][cl];
+    s1 += red[1][i][cl];
+    s2 += red[2][i][cl];
+  }
+  const float g = gamma ? gamma[c] : 1.f;
+  const float rs = f.rstd[c], mu = f.mean[c];
+  const float k1 = g * rs;
+  const float invn = 1.f / (float)M;
+  const float m1 = s0 * invn, m2 = s1 * invn;
+  // planar per-channel constants of the apply pass (one 16-B load per plane per 4 channels):
+  //   yhat = (y - mu)*rs,  z = (y - mu)*k1 + beta,  dy = k1*(dz - m1 - yhat*m2)
+  coef[c] = k1;
+  coef[C + c] = m1;
+  coef[2 * C + c] = m2;
+  coef[3 * C + c] = mu;
+  coef[4 * C + c] = rs;
+  coef[5 * C + c] = beta ? beta[c] : 0.f;
+  const float gb = -k1 * s1 * s2 * invn;
+  if (dgamma) dgamma[c] = acc ? dgamma[c] + s1 : s1;
+  if (dbeta) dbeta[c] = acc ? dbeta[c] + s0 : s0;
+  if (dbias) dbias[c] = acc ? dbias[c] + gb : gb;
+}
+
+// standalone finalize (no counter pool): one block per strip
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ ws, int nrb, int M, int C,
+                                                              BwdFin f) {
+  bwd_finalize_strip<false>(ws, nrb, M, C, blockIdx.x, f);
+}
+
 // backward reduce: per (64-row block, 64 channels) partial sums of dz, dz*yhat, yhat.
 // 256 threads = 16 channel quads (4 channels, one 16-B fp32 / 8-B bf16 load) x 16 row lanes;
 // the 4 rows of a lane are loaded together (independent loads in flight).
 constexpr int RB = 64;
+// 64-row sub-blocks per block of the vectorised reduce.  4 (256 rows, 4x fewer partials for the
+// finalize) measured slower in the C2 step: 15.6 + 6.9 us vs 11.6 + 8.5 us per BN backward
+constexpr int RBN = 1;
 
 // dz = dA * act'(.): from the stored activation output a (FROM_PRE = false) or from the
 // pre-activation z = yhat*gamma + beta recomputed from y (FROM_PRE = true: one fewer
@@ -208,11 +245,11 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TD* __restrict
                                                             const float* __restrict__ rstd,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta, int M, int C, int act,
-                                                            float* ws) {
+                                                            float* ws, unsigned* cnt, BwdFin fin) {
   __shared__ float red[3][16][65];
   const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
   const int c = blockIdx.x * 64 + cq * 4;
-  const int r0 = blockIdx.y * RB;
+  const int r0 = blockIdx.y * RB * RBN;
   f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0;
   if (c < C) {
     const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + c);
@@ -222,25 +259,29 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TD* __restrict
       if (gamma) gm = *reinterpret_cast<const f32x4*>(gamma + c);
       if (beta) bt = *reinterpret_cast<const f32x4*>(beta + c);
     }
-    f32x4 g[4], av[4], yv[4];
+#pragma unroll 2
+    for (int sub = 0; sub < RBN; ++sub) {
+      const int rs0 = r0 + sub * RB + rl;
+      f32x4 g[4], av[4], yv[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = r0 + rl + 16 * i;
-      const long long idx = (long long)(r < M ? r : 0) * C + c;
-      g[i] = ld4(dA + idx);
-      if (!FROM_PRE) av[i] = ld4(a + idx);
-      yv[i] = ld4(y + idx);
-    }
+      for (int i = 0; i < 4; ++i) {
+        const int r = rs0 + 16 * i;
+        const long long idx = (long long)(r < M ? r : 0) * C + c;
+        g[i] = ld4(dA + idx);
+        if (!FROM_PRE) av[i] = ld4(a + idx);
+        yv[i] = ld4(y + idx);
+      }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (r0 + rl + 16 * i >= M) continue;
+      for (int i = 0; i < 4; ++i) {
+        if (rs0 + 16 * i >= M) continue;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float yh = (yv[i][k] - mu[k]) * rs[k];
-        const float dz = bn_dz<FROM_PRE>(g[i][k], FROM_PRE ? 0.f : av[i][k], yh, gm[k], bt[k], act);
-        s0[k] += dz;
-        s1[k] += dz * yh;
-        s2[k] += yh;
+        for (int k = 0; k < 4; ++k) {
+          const float yh = (yv[i][k] - mu[k]) * rs[k];
+          const float dz = bn_dz<FROM_PRE>(g[i][k], FROM_PRE ? 0.f : av[i][k], yh, gm[k], bt[k], act);
+          s0[k] += dz;
+          s1[k] += dz * yh;
+          s2[k] += yh;
+        }
       }
     }
   }
@@ -258,9 +299,12 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TD* __restrict
       float t = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) t += red[q][i][cl];
-      ws[((long long)blockIdx.y * C + cc) * 3 + q] = t;
+      if (cnt) st_sc1(ws + ((long long)blockIdx.y * C + cc) * 3 + q, t);
+      else ws[((long long)blockIdx.y * C + cc) * 3 + q] = t;
     }
   }
+  // the last row block of this channel strip merges all partials (no finalize launch)
+  if (cnt && arrive_last(cnt + blockIdx.x, gridDim.y)) bwd_finalize_strip<true>(ws, gridDim.y, M, C, blockIdx.x, fin);
 }
 
 // scalar variant (C % 4 != 0): 64 channels x 4 row lanes
@@ -271,7 +315,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const TD* __restric
                                                              const float* __restrict__ rstd,
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, int M, int C, int act,
-                                                             float* ws) {
+                                                             float* ws, unsigned* cnt, BwdFin fin) {
   __shared__ float red[3][4][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -296,53 +340,18 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const TD* __restric
   __syncthreads();
   if (rl == 0 && c < C) {
     float* p = ws + ((long long)blockIdx.y * C + c) * 3;
-    p[0] = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
-    p[1] = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
-    p[2] = red[2][0][cl] + red[2][1][cl] + red[2][2][cl] + red[2][3][cl];
+    float v[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) v[q] = red[q][0][cl] + red[q][1][cl] + red[q][2][cl] + red[q][3][cl];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      if (cnt) st_sc1(p + q, v[q]);
+      else p[q] = v[q];
+    }
   }
+  if (cnt && arrive_last(cnt + blockIdx.x, gridDim.y)) bwd_finalize_strip<true>(ws, gridDim.y, M, C, blockIdx.x, fin);
 }
 
-// one block per 64 channels, 4 row groups reduce the per-block partials in parallel
-__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ ws, int nrb, int M, int C,
-                                                              const float* gamma, const float* beta,
-                                                              const float* mean, const float* rstd, float* coef,
-                                                              float* dgamma, float* dbeta, float* dbias, int acc) {
-  __shared__ float red[3][FG][64];
-  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  float sv[3] = {0.f, 0.f, 0.f};
-  if (c < C) strided_sums<3>(ws, nrb, C, c, grp, sv);
-  float s0 = sv[0], s1 = sv[1], s2 = sv[2];
-  red[0][grp][cl] = s0;
-  red[1][grp][cl] = s1;
-  red[2][grp][cl] = s2;
-  __syncthreads();
-  if (grp != 0 || c >= C) return;
-  s0 = s1 = s2 = 0.f;
-#pragma unroll
-  for (int i = 0; i < FG; ++i) {
-    s0 += red[0][i][cl];
-    s1 += red[1][i][cl];
-    s2 += red[2][i][cl];
-  }
-  const float g = gamma ? gamma[c] : 1.f;
-  const float rs = rstd[c], mu = mean[c];
-  const float k1 = g * rs;
-  const float invn = 1.f / (float)M;
-  const float m1 = s0 * invn, m2 = s1 * invn;
-  // planar per-channel constants of the apply pass (one 16-B load per plane per 4 channels):
-  //   yhat = (y - mu)*rs,  z = (y - mu)*k1 + beta,  dy = k1*(dz - m1 - yhat*m2)
-  coef[c] = k1;
-  coef[C + c] = m1;
-  coef[2 * C + c] = m2;
-  coef[3 * C + c] = mu;
-  coef[4 * C + c] = rs;
-  coef[5 * C + c] = beta ? beta[c] : 0.f;
-  const float gb = -k1 * s1 * s2 * invn;
-  if (dgamma) dgamma[c] = acc ? dgamma[c] + s1 : s1;
-  if (dbeta) dbeta[c] = acc ? dbeta[c] + s0 : s0;
-  if (dbias) dbias[c] = acc ? dbias[c] + gb : gb;
-}
 
 template <bool FROM_PRE, typename TD, typename TY>
 __global__ void bn_bwd_apply_kernel(const TD* __restrict__ dA, const float* __restrict__ a,
@@ -444,7 +453,7 @@ __global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restri
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   float sv[1] = {0.f};
-  if (c < N) strided_sums<1>(ws, nrb, N, c, grp, sv);
+  if (c < N) strided_sums<1, false, 32>(ws, nrb, N, c, grp, sv);
   float s = sv[0];
   red[grp][cl] = s;
   __syncthreads();
@@ -481,6 +490,49 @@ extern "C" int avc_bn_stats(const float* y, long long ld, int M, int C, float* p
   dim3 grid(cdiv(C, 256), cdiv(M, PTILE));
   bn_stats_kernel<<<grid, 256, 0, as_stream(stream)>>>(y, ld, M, C, partial);
   return avc_check_launch("avc_bn_stats");
+}
+
+// AVC_LAST_BLOCK=1: the backward finalize by the reduce's last-arriving row block instead of its
+// own launch.  Off by default: measured 22.8 us per BN backward reduce+finalize vs 11.6 + 8.5 us
+// as two launches in the C2 step (the single last block's serial merge sits on the critical path).
+static bool last_block_finalize() {
+  static const bool on = [] {
+    const char* e = getenv("AVC_LAST_BLOCK");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+unsigned* avc_counter_slots(int n, hipStream_t s) {
+  constexpr unsigned POOL = 1u << 16;
+  constexpr int MAXD = 64;
+  static std::mutex mu;
+  static std::atomic<unsigned*> pool[MAXD];
+  static std::atomic<unsigned> next[MAXD];
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXD || n <= 0 || (unsigned)n > POOL) {
+    avc_set_error("avc_counter_slots: no device / bad size");
+    return nullptr;
+  }
+  if (!pool[dev].load(std::memory_order_acquire)) {
+    std::lock_guard<std::mutex> lk(mu);
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (!pool[dev].load() && hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusNone) {
+      unsigned* p = nullptr;
+      if (hipMalloc(&p, POOL * sizeof(unsigned)) == hipSuccess &&
+          hipMemset(p, 0, POOL * sizeof(unsigned)) == hipSuccess && hipDeviceSynchronize() == hipSuccess)
+        pool[dev].store(p, std::memory_order_release);
+    }
+  }
+  unsigned* base = pool[dev].load(std::memory_order_acquire);
+  if (!base) {
+    avc_set_error("avc_counter_slots: counter pool not created (first use inside a stream capture? run one "
+                  "eager step first)");
+    return nullptr;
+  }
+  unsigned b = next[dev].fetch_add((unsigned)n) % POOL;
+  if (b + (unsigned)n > POOL) b = 0;
+  return base + b;
 }
 
 namespace {
@@ -525,17 +577,21 @@ extern "C" int avc_bn_bwd(const void* dA, int dA_dtype, const float* a, const vo
                 "avc_bn_bwd: bad args");
   hipStream_t s = as_stream(stream);
   const bool pre = a == nullptr;  // activation derivative from the recomputed pre-activation
-  const int nrb = cdiv(M, RB);
-  dim3 grid(cdiv(C, 64), nrb);
   // 4-wide loads: 8-B (bf16) / 16-B (fp32) aligned rows
   auto al = [](const void* p, int dt) { return (reinterpret_cast<uintptr_t>(p) & (dt == AVC_BF16 ? 7 : 15)) == 0; };
   const bool v4 = C % 4 == 0 && al(dA, dA_dtype) && al(y, y_dtype) && (pre || aligned16(a)) &&
                   (!gamma || aligned16(gamma)) && (!beta || aligned16(beta)) && (!dy || aligned16(dy)) &&
                   (!d16 || al(d16, AVC_BF16));
+  const int nrb = cdiv(M, v4 ? RB * RBN : RB);
+  dim3 grid(cdiv(C, 64), nrb);
   // per-channel apply constants, planar [6][C], 16-B aligned
   const size_t coff = ((size_t)nrb * C * 3 + 3) & ~(size_t)3;
   float* coef = ws + coff;
   const long long total = (long long)M * C;
+  const BwdFin fin{gamma, beta, mean, rstd, coef, dgamma, dbeta, dbias, accumulate};
+  // one arrival counter per channel strip: the reduce's last row block finalizes the strip
+  unsigned* cnt = last_block_finalize() ? avc_counter_slots(cdiv(C, 64), s) : nullptr;
+  if (last_block_finalize() && !cnt) return -1;
   with_type(dA_dtype, [&](auto dtag) {
     using TD = std::remove_const_t<std::remove_pointer_t<decltype(dtag)>>;
     with_type(y_dtype, [&](auto ytag) {
@@ -543,14 +599,13 @@ extern "C" int avc_bn_bwd(const void* dA, int dA_dtype, const float* a, const vo
       const TD* dp = static_cast<const TD*>(dA);
       const TY* yp = static_cast<const TY*>(y);
       if (v4) {
-        if (pre) bn_bwd_reduce_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws);
-        else bn_bwd_reduce_kernel<false, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws);
+        if (pre) bn_bwd_reduce_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws, cnt, fin);
+        else bn_bwd_reduce_kernel<false, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws, cnt, fin);
       } else {
-        if (pre) bn_bwd_reduce1_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws);
-        else bn_bwd_reduce1_kernel<false, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws);
+        if (pre) bn_bwd_reduce1_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws, cnt, fin);
+        else bn_bwd_reduce1_kernel<false, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws, cnt, fin);
       }
-      bn_bwd_finalize_kernel<<<cdiv(C, 64), 256, 0, s>>>(ws, nrb, M, C, gamma, beta, mean, rstd, coef, dgamma, dbeta,
-                                                          dbias, accumulate);
+      if (!cnt) bn_bwd_finalize_kernel<<<cdiv(C, 64), 256, 0, s>>>(ws, nrb, M, C, fin);
       if (v4) {
         if (pre)
           bn_bwd_apply_kernel<true, TD, TY><<<cdiv(total / 4, 256), 256, 0, s>>>(dp, a, yp, coef, total / 4, C, act, dy, d16);

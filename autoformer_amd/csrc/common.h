@@ -104,3 +104,103 @@ __device__ __forceinline__ float warp_sum(float v) {
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// ------------------------------------------------------------------ last-block reductions
+// Per-device pool of zeroed arrival counters for "the last block to arrive finalizes"
+// reductions (bn.hip).  Returns n consecutive slots, or nullptr with the error recorded (first
+// use inside a stream capture, allocation failure).  The last arrival of a launch resets its
+// slot to 0, so slots are reused without a reset pass.
+unsigned* avc_counter_slots(int n, hipStream_t s);
+
+// Agent-coherent (sc1) scalar store / load: the data handed from block to block through an
+// arrival counter bypasses the per-XCD L2 on both sides, so no fence (an agent-scope release
+// fence writes back the whole L2 on gfx950 -- measured +1 ms per C2 step when every reduce
+// block issued one).
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Arrival of a block at counter `cnt` expecting `arrivals` blocks.  Every thread calls it after
+// its hand-off stores, which must be st_sc1 stores: they are waited for (vmcnt(0)), one lane
+// increments the counter (agent-scope relaxed atomic), and the block that arrives last resets it
+// and returns true; it then reads the hand-off data with ld_sc1.
+__device__ __forceinline__ bool arrive_last(unsigned* cnt, unsigned arrivals) {
+  __shared__ unsigned s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old == arrivals - 1;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = last ? 1u : 0u;
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
+// 8-byte load of a (sum, M2) pair; SC1: handed over within the launch (agent-coherent load)
+template <bool SC1>
+__device__ __forceinline__ float2 ld_pair(const float* p) {
+  if (SC1) {
+    const unsigned long long u =
+        __hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<float*>(p)), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+    return make_float2(__uint_as_float((unsigned)u), __uint_as_float((unsigned)(u >> 32)));
+  }
+  return *reinterpret_cast<const float2*>(p);
+}
+
+// Chan's parallel merge of per-tile (sum, M2) pairs at P[(t*ld + col)*2], t < nt, tiles of `tile`
+// rows (the last one M - t*tile):  mean = sum_t s_t / M,  M2 = sum_t [q_t + n_t (s_t/n_t - mean)^2].
+// Thread (grp < ng, cl < nc) covers tiles grp, grp + ng, ...; its first U tiles are loaded in ONE
+// round and kept in registers for both passes (the finalize is latency-bound: one memory round
+// instead of one per pass and per 8 tiles); further tiles (nt > ng*U) take extra rounds.  red:
+// ng*nc floats of LDS.  Every thread of the block calls it; mean / m2 come back in all of them.
+template <int U, bool SC1>
+__device__ __forceinline__ void chan_merge(const float* P, int nt, long long ld, int col, bool cv, int grp, int ng,
+                                           int cl, int nc, int M, int tile, float* red, float& mean, float& m2) {
+  float2 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int t = grp + u * ng;
+    v[u] = (cv && t < nt) ? ld_pair<SC1>(P + ((long long)t * ld + col) * 2) : make_float2(0.f, 0.f);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) s += v[u].x;
+  if (cv)
+    for (int t = grp + U * ng; t < nt; t += ng) s += ld_pair<SC1>(P + ((long long)t * ld + col) * 2).x;
+  const bool act = grp < ng;
+  __syncthreads();
+  if (act) red[grp * nc + cl] = s;
+  __syncthreads();
+  float tot = 0.f;
+  for (int i = 0; i < ng; ++i) tot += red[i * nc + cl];
+  mean = tot / (float)M;
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int t = grp + u * ng;
+    if (cv && t < nt) {
+      const float nb = (float)min(tile, M - t * tile);
+      const float d = v[u].x / nb - mean;
+      q += v[u].y + nb * d * d;
+    }
+  }
+  if (cv)
+    for (int t = grp + U * ng; t < nt; t += ng) {
+      const float2 w = ld_pair<SC1>(P + ((long long)t * ld + col) * 2);
+      const float nb = (float)min(tile, M - t * tile);
+      const float d = w.x / nb - mean;
+      q += w.y + nb * d * d;
+    }
+  __syncthreads();
+  if (act) red[grp * nc + cl] = q;
+  __syncthreads();
+  m2 = 0.f;
+  for (int i = 0; i < ng; ++i) m2 += red[i * nc + cl];
+  __syncthreads();
+}

@@ -689,7 +689,24 @@ bool fits32(const OpDev& o, int rows, int K, bool ks) {
 
 }  // namespace
 
-extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
+// AVC_GEMM_BNFIN=0: finalize launches after the GEMM instead of its last row tiles (A/B check)
+static bool gemm_bnfin() {
+  static const bool on = [] {
+    const char* e = getenv("AVC_GEMM_BNFIN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+static int bn_finalize_after(const GemmArgs& g, const avc_bn_fin* f, void* stream) {
+  for (int k = 0; k < f->nupd; ++k)
+    if (avc_bn_finalize(g.bn_partial, g.M, g.N, f->gamma, f->beta, f->running_mean, f->running_var,
+                        f->num_batches_tracked, f->momentum, f->eps, f->mean, f->rstd, f->scale, f->shift, stream))
+      return -1;
+  return 0;
+}
+
+static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream) {
   AVC_CHECK_ARG(d != nullptr, "avc_gemm: null desc");
   AVC_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0, "avc_gemm: negative dims");
   if (d->M == 0 || d->N == 0) return 0;
@@ -720,6 +737,24 @@ extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
   AVC_CHECK_ARG(!g.cperm || (d->N % g.cperm == 0 && !g.bias && !g.res && !g.c16 && !g.bn_partial),
                 "avc_gemm: cperm needs N %% taps == 0 and no bias / residual / bf16 / BN epilogue");
   g.cpd = make_fastdiv(g.cperm ? (uint32_t)(d->N / g.cperm) : 1u);
+  g.bn_cnt = nullptr;
+  if (f) {
+    AVC_CHECK_ARG(g.bn_partial && f->mean && f->rstd && f->scale && f->shift && f->nupd >= 1 &&
+                      (!f->running_mean == !f->running_var),
+                  "avc_gemm_bn: needs bn_partial, mean / rstd / scale / shift, nupd >= 1");
+    g.bn_gamma = f->gamma;
+    g.bn_beta = f->beta;
+    g.bn_rmean = f->running_mean;
+    g.bn_rvar = f->running_var;
+    g.bn_nbt = f->num_batches_tracked;
+    g.bn_mean = f->mean;
+    g.bn_rstd = f->rstd;
+    g.bn_scale = f->scale;
+    g.bn_shift = f->shift;
+    g.bn_momentum = f->momentum;
+    g.bn_eps = f->eps;
+    g.bn_nupd = f->nupd;
+  }
   AVC_CHECK_ARG(!(g.bn_partial && (g.split_k > 1 || g.batch > 1 || d->accumulate)),
                 "avc_gemm: bn_partial needs split_k == 1, batch == 1, accumulate == 0");
   AVC_CHECK_ARG(g.c || (!g.atomic && !d->accumulate && !g.cperm),
@@ -739,15 +774,23 @@ extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
     int klf = (d->K + g.split_k - 1) / g.split_k;
     g.klen = ((klf + FBK - 1) / FBK) * FBK;
     if (g.klen <= 0) g.klen = FBK;
-    if (!aks && !bks && gemm_conv_launch(g, s)) return avc_check_launch("avc_gemm(conv)");
-    if (!aks && !bks && gemm_nt_launch(g, s)) return avc_check_launch("avc_gemm(nt)");
-    if (aks && bks && gemm_tt_launch(g, s)) return avc_check_launch("avc_gemm(tt)");
-    const long long t128 = (long long)cdiv(g.M, BM) * cdiv(g.N, 128) * g.batch * g.split_k;
-    const bool narrow = g.N <= 64 || t128 < 384;
-    const int nb = narrow ? cdiv(g.M, BM) * cdiv(g.N, 64) * g.batch * g.split_k : (int)t128;
-    if (narrow) launch_fast_layout<64>(g, aks, bks, nb, s);
-    else launch_fast_layout<128>(g, aks, bks, nb, s);
-    return avc_check_launch("avc_gemm(fast)");
+    if (f && gemm_bnfin()) {  // the BN finalize rides on the fast kernels' epilogue (one counter per 64 columns)
+      g.bn_cnt = avc_counter_slots(cdiv(g.N, 64), s);
+      if (!g.bn_cnt) return -1;
+    }
+    const char* what = "avc_gemm(fast)";
+    if (!aks && !bks && gemm_conv_launch(g, s)) what = "avc_gemm(conv)";
+    else if (!aks && !bks && gemm_nt_launch(g, s)) what = "avc_gemm(nt)";
+    else if (aks && bks && gemm_tt_launch(g, s)) what = "avc_gemm(tt)";
+    else {
+      const long long t128 = (long long)cdiv(g.M, BM) * cdiv(g.N, 128) * g.batch * g.split_k;
+      const bool narrow = g.N <= 64 || t128 < 384;
+      const int nb = narrow ? cdiv(g.M, BM) * cdiv(g.N, 64) * g.batch * g.split_k : (int)t128;
+      if (narrow) launch_fast_layout<64>(g, aks, bks, nb, s);
+      else launch_fast_layout<128>(g, aks, bks, nb, s);
+    }
+    if (avc_check_launch(what)) return -1;
+    return (f && !g.bn_cnt) ? bn_finalize_after(g, f, stream) : 0;
   }
   AVC_CHECK_ARG(!g.c16, "avc_gemm: c_bf16 output needs the fast path (bf16 compute, vectorisable operands)");
   static const bool trace_generic = getenv("AVC_GEMM_TRACE") != nullptr;
@@ -770,5 +813,13 @@ extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) {
     else AVC_GEMM_LAUNCH(false, true, true);
   }
 #undef AVC_GEMM_LAUNCH
-  return avc_check_launch("avc_gemm");
+  if (avc_check_launch("avc_gemm")) return -1;
+  return f ? bn_finalize_after(g, f, stream) : 0;  // generic kernels: finalize launch(es) after the GEMM
+}
+
+extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) { return gemm_impl(d, nullptr, stream); }
+
+extern "C" int avc_gemm_bn(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream) {
+  AVC_CHECK_ARG(f != nullptr, "avc_gemm_bn: null finalize args");
+  return gemm_impl(d, f, stream);
 }

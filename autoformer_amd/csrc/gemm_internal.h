@@ -28,7 +28,57 @@ struct GemmArgs {
   float* bn_partial;
   int cperm;     // 0, or taps: column n = tap*chans + ch is stored at ch*taps + tap (conv weight layout)
   FastDiv cpd;   // divide a column by chans = N / cperm
+  // BatchNorm finalize by the last row tile of each column tile (bn_cnt != null, bn_partial set):
+  // mean / rstd / scale / shift and the running statistics of the tile's columns (avc_gemm_bn)
+  unsigned* bn_cnt;
+  const float* bn_gamma;
+  const float* bn_beta;
+  float* bn_rmean;
+  float* bn_rvar;
+  long long* bn_nbt;
+  float* bn_mean;
+  float* bn_rstd;
+  float* bn_scale;
+  float* bn_shift;
+  float bn_momentum, bn_eps;
+  int bn_nupd;
 };
+
+// Last-arriving row tile of a column tile: merge the per-row-tile (sum, M2) partials of columns
+// n0 .. n0+BN_-1 (Chan's parallel form, two passes over the L2/MALL-resident partials) and
+// publish the BatchNorm coefficients -- the separate finalize launch of the forward is gone.
+template <int BN_>
+__device__ __forceinline__ void bn_finalize_cols(const GemmArgs& g, int n0, float* red) {
+  const int nthr = blockDim.x, ng = nthr / BN_;
+  const int tid = threadIdx.x, cl = tid % BN_, grp = tid / BN_;
+  const int col = n0 + cl;
+  const bool cv = col < g.N && grp < ng;
+  const int nt = (g.M + BM - 1) / BM;
+  const float n = (float)g.M;
+  float mean, m2;
+  chan_merge<64 / (256 / BN_), true>(g.bn_partial, nt, g.N, col, cv, grp, ng, cl, BN_, g.M, BM, red, mean, m2);
+  if (grp == 0 && col < g.N) {
+    const float var = m2 / n;
+    const float rstd = 1.f / sqrtf(var + g.bn_eps);
+    const float ga = g.bn_gamma ? g.bn_gamma[col] : 1.f;
+    const float be = g.bn_beta ? g.bn_beta[col] : 0.f;
+    g.bn_mean[col] = mean;
+    g.bn_rstd[col] = rstd;
+    g.bn_scale[col] = ga * rstd;
+    g.bn_shift[col] = be - mean * ga * rstd;
+    if (g.bn_rmean) {
+      const float unb = n > 1.f ? m2 / (n - 1.f) : var;
+      float rm = g.bn_rmean[col], rv = g.bn_rvar[col];
+      for (int k = 0; k < g.bn_nupd; ++k) {
+        rm = (1.f - g.bn_momentum) * rm + g.bn_momentum * mean;
+        rv = (1.f - g.bn_momentum) * rv + g.bn_momentum * unb;
+      }
+      g.bn_rmean[col] = rm;
+      g.bn_rvar[col] = rv;
+    }
+  }
+  if (tid == 0 && n0 == 0 && g.bn_nbt) *g.bn_nbt += g.bn_nupd;
+}
 
 // Column offset of output column `col` (cperm: the Conv1d [Co][Ci][K] layout).
 __device__ __forceinline__ long long out_col(const GemmArgs& g, int col) {
@@ -132,10 +182,17 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
       const int col = n0 + tid;
       if (col < g.N) {
         float* p = g.bn_partial + ((long long)mt * g.N + col) * 2;
-        p[0] = red[tid] + red[BN_ + tid];
-        p[1] = red2[tid] + red2[BN_ + tid];
+        // sc1 when another block merges them (bn_cnt): no L2-wide release fence needed
+        if (g.bn_cnt) {
+          st_sc1(p, red[tid] + red[BN_ + tid]);
+          st_sc1(p + 1, red2[tid] + red2[BN_ + tid]);
+        } else {
+          p[0] = red[tid] + red[BN_ + tid];
+          p[1] = red2[tid] + red2[BN_ + tid];
+        }
       }
     }
+    if (g.bn_cnt && arrive_last(g.bn_cnt + n0 / BN_, (g.M + BM - 1) / BM)) bn_finalize_cols<BN_>(g, n0, red);
   }
 }
 

@@ -529,7 +529,7 @@ bool gemm_tt_launch(const GemmArgs& g, hipStream_t s) {
   const bool halo_off = halo == 0;
   const OpDev& x = g.b;
   if (!halo_off && x.win && x.taps == 5 && x.t_in == x.t_out && 2 * x.pad == x.taps - 1 && x.chans % 32 == 0 &&
-      x.t_out % FBK == 0 && g.batch == 1 && g.N == x.taps * x.chans && !g.res && !g.c16 && !g.bias) {
+      x.t_out % FBK == 0 && g.batch == 1 && g.N == x.taps * x.chans && !g.res && !g.c16 && !g.bias && !g.bn_partial) {
     if (halo == 2) launch_halo<2>(g, s);
     else launch_halo<3>(g, s);
     return true;

@@ -81,9 +81,11 @@ def operand(t: torch.Tensor, ld: int, kstrided: bool = False, window=None, batch
 
 
 def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=None, accumulate=False, split_k=1,
-         bn_partial=None, batch=1, c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0):
+         bn_partial=None, batch=1, c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0, bn_fin=None):
     """cperm = taps > 1: C's columns are (tap, channel) pairs written in nn.Conv1d's [Co][Ci][K]
-    weight layout (a conv weight gradient straight into .grad)."""
+    weight layout (a conv weight gradient straight into .grad).
+    bn_fin = (gamma, beta, running_mean, running_var, nbt, momentum, eps, nupd): the BatchNorm
+    finalize of bn_partial fused into the GEMM (avc_gemm_bn); returns (mean, rstd, scale, shift)."""
     _dev(c, bias, bn_partial, c_bf16, residual)
     if c.dtype == torch.bfloat16:  # bf16-only output
         assert c_bf16 is None and not accumulate and split_k == 1 and not cperm
@@ -104,7 +106,19 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     d.c_bf16 = _ptr(c_bf16)
     d.residual = _ptr(residual)
     d.cperm = int(cperm)
-    L.check(L.lib().avc_gemm(d, stream()), "avc_gemm")
+    if bn_fin is None:
+        L.check(L.lib().avc_gemm(d, stream()), "avc_gemm")
+        return None
+    gamma, beta, rmean, rvar, nbt, momentum, eps, nupd = bn_fin
+    dev = bn_partial.device
+    stats = tuple(torch.empty(int(N), device=dev) for _ in range(4))
+    f = L.BnFin()
+    f.gamma, f.beta, f.running_mean, f.running_var, f.num_batches_tracked = (_ptr(gamma), _ptr(beta), _ptr(rmean),
+                                                                            _ptr(rvar), _ptr(nbt))
+    f.momentum, f.eps, f.nupd = float(momentum), float(eps), int(nupd)
+    f.mean, f.rstd, f.scale, f.shift = (t.data_ptr() for t in stats)
+    L.check(L.lib().avc_gemm_bn(d, f, stream()), "avc_gemm_bn")
+    return stats
 
 
 def auto_split_k(M, N, K, target=384, min_k=256):

@@ -344,17 +344,18 @@ class ConvBNCore:
         x = K.twin(x)
         bf = K.compute() == K.BF16
         y = torch.empty(M, Co, device=x.device, dtype=torch.bfloat16 if bf else torch.float32)
-        partial = K.bn_partial_buffer(M, Co, x.device) if bn.training else None
-        K.gemm(M, Co, Kw * Ci, operand(x, Ci, window=(Kw, self.pad, T_out, T_in, Ci)), operand(Wf, Kw * Ci), y,
-               bias=conv.bias, bn_partial=partial)
+        xop, wop = operand(x, Ci, window=(Kw, self.pad, T_out, T_in, Ci)), operand(Wf, Kw * Ci)
         if bn.training:
+            # batch statistics from the epilogue, finalized by the GEMM's last row tiles; the
+            # running statistics take stat_updates updates (the *_Adjust double pass)
+            partial = K.bn_partial_buffer(M, Co, x.device)
             nbt = bn.num_batches_tracked if bn.track_running_stats else None
             mom = bn.momentum if bn.momentum is not None else 0.1
-            stats = K.bn_finalize(partial, M, Co, bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, mom,
-                                  bn.eps)
-            for _ in range(self.stat_updates - 1):  # the same batch statistics, applied again
-                K.bn_finalize(partial, M, Co, bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, mom, bn.eps)
+            stats = K.gemm(M, Co, Kw * Ci, xop, wop, y, bias=conv.bias, bn_partial=partial,
+                           bn_fin=(bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, mom, bn.eps,
+                                   self.stat_updates))
         else:
+            K.gemm(M, Co, Kw * Ci, xop, wop, y, bias=conv.bias)
             stats = K.bn_eval(bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.eps)
         mean, rstd, scale, shift = stats
         a = K.bn_apply(y, scale, shift, self.act, residual, out_bf16=out_bf16 and bf and residual is None)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 6
+#define AVC_ABI_VERSION 7
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -93,6 +93,26 @@ int avc_bn_finalize(const float* partial, int M, int C, const float* gamma, cons
                     float* running_mean, float* running_var, long long* num_batches_tracked,
                     float momentum, float eps, float* mean, float* rstd, float* scale, float* shift,
                     void* stream);
+
+/* avc_gemm with the train-mode BatchNorm1d finalize of avc_bn_finalize fused in: the GEMM's
+ * bn_partial statistics are merged by the last row tile of each column tile (bf16 fast kernels;
+ * other paths launch avc_bn_finalize after the GEMM) -- same outputs, running statistics updated
+ * nupd times, num_batches_tracked += nupd.  gamma / beta / running stats / nbt are nullable.
+ * Replaces nn.BatchNorm1d.forward (train mode) at AutoVC.py:38,91,138,154,169 with its conv. */
+typedef struct {
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  long long* num_batches_tracked;
+  float momentum, eps;
+  int nupd;
+  float* mean;
+  float* rstd;
+  float* scale;
+  float* shift;
+} avc_bn_fin;
+int avc_gemm_bn(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream);
 
 /* Eval-mode coefficients from the running statistics (nn.BatchNorm1d in .eval()). */
 int avc_bn_eval(const float* running_mean, const float* running_var, const float* gamma, const float* beta, int C,

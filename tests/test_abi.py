@@ -44,7 +44,7 @@ def test_python_binding_covers_header(lib):
 
 
 def test_abi_version_and_error_channel(lib):
-    assert lib.avc_abi_version() == 6
+    assert lib.avc_abi_version() == 7
     assert isinstance(lib.avc_last_error(), bytes)
 
 
@@ -66,7 +66,7 @@ def test_struct_layout_matches_header(tmp_path):
     from autoformer_amd import _lib
 
     fields = {"avc_operand": [f[0] for f in _lib.Operand._fields_], "avc_gemm_desc": [f[0] for f in _lib.GemmDesc._fields_],
-              "avc_pack_op": [f[0] for f in _lib.PackOp._fields_]}
+              "avc_pack_op": [f[0] for f in _lib.PackOp._fields_], "avc_bn_fin": [f[0] for f in _lib.BnFin._fields_]}
     src = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
     for st, fs in fields.items():
         src.append(f'printf("{st} %zu\\n", sizeof({st}));')
@@ -79,7 +79,8 @@ def test_struct_layout_matches_header(tmp_path):
     subprocess.run(["gcc", str(c), "-o", str(exe)], check=True)
     out = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
                                                                check=True).stdout.split("\n") if line)
-    for st, cls in (("avc_operand", _lib.Operand), ("avc_gemm_desc", _lib.GemmDesc), ("avc_pack_op", _lib.PackOp)):
+    for st, cls in (("avc_operand", _lib.Operand), ("avc_gemm_desc", _lib.GemmDesc), ("avc_pack_op", _lib.PackOp),
+                    ("avc_bn_fin", _lib.BnFin)):
         assert int(out[st]) == ctypes.sizeof(cls), st
         for f in fields[st]:
             assert int(out[f"{st}.{f}"]) == getattr(cls, f).offset, (st, f)

@@ -166,6 +166,45 @@ def test_bn_stats_epilogue_and_finalize(M, C):
     assert int(nbt.item()) == 1
 
 
+@pytest.mark.parametrize("M,C,Kd", [(8192, 512, 2560), (352, 80, 64), (300, 176, 64), (1000, 1024, 128)])
+@pytest.mark.parametrize("comp,nupd", [("bf16", 1), ("bf16", 2), ("fp32", 2)])
+def test_gemm_bn_fused_finalize(M, C, Kd, comp, nupd):
+    """avc_gemm_bn: the BN finalize done by the GEMM's last-arriving row tile of each column tile
+    (bf16 fast kernels) or by finalize launches after it (fp32 generic kernel) == the separate
+    avc_bn_finalize on the same partials; running statistics updated nupd times."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute(comp)
+    try:
+        x = (torch.randn(M, Kd, device=DEV) * 3)
+        w = torch.randn(C, Kd, device=DEV)
+        bias = torch.full((C,), 5.0, device=DEV)
+        gamma, beta = (torch.rand(C) + 0.5).to(DEV), torch.randn(C).to(DEV)
+        rm0, rv0 = torch.randn(C).to(DEV), (torch.rand(C) + 0.5).to(DEV)
+        y1 = torch.empty(M, C, device=DEV)
+        p1 = Kr.bn_partial_buffer(M, C, DEV)
+        rm1, rv1, n1 = rm0.clone(), rv0.clone(), torch.zeros((), dtype=torch.long, device=DEV)
+        st1 = Kr.gemm(M, C, Kd, Kr.operand(x, Kd), Kr.operand(w, Kd), y1, bias=bias, bn_partial=p1,
+                      bn_fin=(gamma, beta, rm1, rv1, n1, 0.1, 1e-5, nupd))
+        y2 = torch.empty(M, C, device=DEV)
+        p2 = Kr.bn_partial_buffer(M, C, DEV)
+        rm2, rv2, n2 = rm0.clone(), rv0.clone(), torch.zeros((), dtype=torch.long, device=DEV)
+        Kr.gemm(M, C, Kd, Kr.operand(x, Kd), Kr.operand(w, Kd), y2, bias=bias, bn_partial=p2)
+        for _ in range(nupd):
+            st2 = Kr.bn_finalize(p2, M, C, gamma, beta, rm2, rv2, n2, 0.1, 1e-5)
+        assert torch.equal(y1, y2) and torch.equal(p1, p2)
+        for a, b in zip(st1, st2):
+            assert rinf(a, b) < 1e-6
+        assert rinf(rm1, rm2) < 1e-6 and rinf(rv1, rv2) < 1e-6
+        assert int(n1.item()) == nupd == int(n2.item())
+        yf = y2.double().cpu()
+        assert rinf(st1[0], yf.mean(0)) < 1e-5
+        assert rinf(st1[1], 1 / torch.sqrt(yf.var(0, unbiased=False) + 1e-5)) < 1e-4
+    finally:
+        A.set_compute("bf16")
+
+
 @pytest.mark.parametrize("act", [0, 1, 2])
 @pytest.mark.parametrize("from_pre", [False, True])
 @pytest.mark.parametrize("M,C", [(1000, 96), (1000, 90), (8192, 512), (300, 80)])
