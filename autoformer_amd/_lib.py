@@ -55,6 +55,7 @@ _SIGS = {
     "avc_abi_version": (c_int, []),
     "avc_last_error": (ctypes.c_char_p, []),
     "avc_gemm": (c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
+    "avc_expand_codes": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_gemm_bn": (c_int, [ctypes.POINTER(GemmDesc), ctypes.POINTER(BnFin), c_void_p]),
     "avc_bn_finalize": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
                                 c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -79,6 +79,21 @@ __global__ void dec_concat_kernel(const float* codes, const float* emb, float* o
   out[i] = c < cd ? codes[((long long)b * nc + t / rep) * cd + c] : emb[(long long)b * de + (c - cd)];
 }
 
+// The decoder LSTM's input projection folded per code and per utterance:
+//   out[b*T + t][g] = pc[b*nc + t/rep][g] + pe[b][g]      (rep = T / nc, float4 over g)
+// pc = codes . W_ih[:, :cd]^T (one row per code), pe = c_trg . W_ih[:, cd:]^T + b (one row per
+// utterance): W_ih . cat(code_expand, c_trg) + b without the (B*T, cd+de) concat or its GEMM.
+__global__ void expand_codes_kernel(const f32x4* __restrict__ pc, const f32x4* __restrict__ pe, f32x4* __restrict__ out,
+                                    int T, int nc, int G4, long long n4) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const int g = (int)(i % G4);
+  const long long r = i / G4;
+  const int t = (int)(r % T), b = (int)(r / T);
+  const int rep = T / nc;
+  out[i] = pc[((long long)b * nc + t / rep) * G4 + g] + pe[(long long)b * G4 + g];
+}
+
 __global__ void dec_concat_bwd_kernel(const float* dout, float* dcodes, int B, int T, int nc, int cd, int de) {
   const int C = cd + de;
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -345,6 +360,18 @@ extern "C" int avc_dec_concat_bwd(const float* dout, float* dcodes, int B, int T
   long long n = (long long)B * nc * cd;
   dec_concat_bwd_kernel<<<GRID1(n)>>>(dout, dcodes, B, T, nc, cd, de);
   return avc_check_launch("avc_dec_concat_bwd");
+}
+
+extern "C" int avc_expand_codes(const float* pc, const float* pe, float* out, int B, int T, int nc, int G,
+                                void* stream) {
+  AVC_CHECK_ARG(pc && pe && out && B > 0 && nc > 0 && T % nc == 0 && G % 4 == 0 &&
+                    ((reinterpret_cast<uintptr_t>(pc) | reinterpret_cast<uintptr_t>(pe) |
+                      reinterpret_cast<uintptr_t>(out)) & 15) == 0,
+                "avc_expand_codes: bad args");
+  const long long n4 = (long long)B * T * (G / 4);
+  expand_codes_kernel<<<GRID1(n4)>>>(reinterpret_cast<const f32x4*>(pc), reinterpret_cast<const f32x4*>(pe),
+                                     reinterpret_cast<f32x4*>(out), T, nc, G / 4, n4);
+  return avc_check_launch("avc_expand_codes");
 }
 
 extern "C" int avc_conv_pack(const float* w, void* out, int dtype, int Co, int Ci, int K, int mode, void* stream) {

@@ -14,12 +14,18 @@ Every op runs as a HIP kernel from libautovc_hip.so:
   Postnet  AutoVC.py:117-179-> 5x conv_bn (tanh x4, none x1 with the residual add fused)
 Activations are frame-major (B*T, C); the reference's (B, C, T) transposes disappear.
 """
+import os
+
 import torch
 import torch.nn as nn
 
 from .. import kernels as K
 from .. import layers as Lyr
 from .Norm import ConvNorm, LinearNorm, LSTMParams
+
+
+# AVC_FOLD=0: the unfolded concat + lstm1 path (A/B and parity diagnostics)
+_FOLD = os.environ.get("AVC_FOLD", "1") != "0"
 
 
 def _conv_bn_block(cin, cout, gain):
@@ -83,7 +89,15 @@ class Decoder(nn.Module):
         self._lin = Lyr.PackCache()
 
     def frames(self, x, B, T):
-        h = Lyr.lstm(self.lstm1, self._lstm1, x, B, T)
+        return self._after_lstm1(Lyr.lstm(self.lstm1, self._lstm1, x, B, T), B, T)
+
+    def frames_codes(self, codes, c_trg, B, T, nc, cd, hook=None):
+        """frames(cat(code expansion, c_trg broadcast)) with lstm1's input projection folded per
+        code and per utterance (layers._LSTM1FoldFn); hook: see decode()."""
+        h = Lyr.lstm1_folded(self.lstm1, self._lstm1[0], codes, c_trg, B, T, nc, cd, hook)
+        return self._after_lstm1(h, B, T)
+
+    def _after_lstm1(self, h, B, T):
         for core in self._convs:
             h = Lyr.conv_bn(core, h, B, T, out_bf16=True)
         h = Lyr.lstm(self.lstm2, self._lstm2, h, B, T)
@@ -145,12 +159,16 @@ def decode(model, x, codes, c_trg, features=None):
     xs = x.squeeze(1) if x.dim() == 4 else x
     B, T = xs.shape[0], xs.shape[1]
     cd = 2 * model.dim_neck
-    enc_out = Lyr.dec_concat(codes, c_trg.contiguous(), B, T, codes.shape[1] // cd, cd)
+    nc = codes.shape[1] // cd
+    # fires once the backward has produced every decoder / postnet gradient
     hook = getattr(model, "_decoder_bwd_done", None)
-    if hook is not None and enc_out.requires_grad:
-        # fires once the backward has produced every decoder / postnet gradient
-        enc_out.register_hook(lambda g: hook())
-    mel = model.decoder.frames(enc_out, B, T)
+    if hasattr(model.decoder, "frames_codes") and _FOLD:
+        mel = model.decoder.frames_codes(codes, c_trg.contiguous(), B, T, nc, cd, hook)
+    else:
+        enc_out = Lyr.dec_concat(codes, c_trg.contiguous(), B, T, nc, cd)
+        if hook is not None and enc_out.requires_grad:
+            enc_out.register_hook(lambda g: hook())
+        mel = model.decoder.frames(enc_out, B, T)
     if features is None:
         mel_postnet = model.postnet.frames(mel, B, T, residual=mel)
     else:

@@ -405,6 +405,15 @@ def dec_concat(codes, emb, B, T, nc, cd):
     return out
 
 
+def expand_codes(pc, pe, B, T, nc):
+    """(B*T, G) rows pc[b*nc + t // (T/nc)] + pe[b] (lstm1 input projection folded per code)."""
+    _dev(pc, pe)
+    G = pc.shape[1]
+    out = torch.empty(B * T, G, device=pc.device)
+    L.call("avc_expand_codes", pc.data_ptr(), pe.data_ptr(), out.data_ptr(), B, T, nc, G, stream())
+    return out
+
+
 def dec_concat_bwd(dout, B, T, nc, cd, de):
     dcodes = torch.empty(B, nc * cd, device=dout.device)
     L.call("avc_dec_concat_bwd", dout.data_ptr(), dcodes.data_ptr(), B, T, nc, cd, de, stream())

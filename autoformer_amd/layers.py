@@ -627,6 +627,107 @@ def lstm(mod, cores, x, B, T):
     return x
 
 
+class _LSTM1FoldFn(torch.autograd.Function):
+    """Decoder lstm1 on cat(code expansion, c_trg broadcast) (AutoVC.py:96,103,197-204) with the
+    input projection folded per code and per utterance: W_ih . [code_j ; e] + b =
+    Wc . code_j + (We . e + b), computed once per code (B*nc rows) and once per utterance (B
+    rows) and expanded to the B*T frames, instead of a (B*T, cd+de) concat and its B*T x 4H x
+    (cd+de) GEMM.  The backward is folded the same way: the gate gradients dG are summed over
+    each code's frames (S_code) and each utterance (S_utt) first, then
+      dcodes = S_code . Wc,  dc_trg = S_utt . We,  dWc = S_code^T codes,  dWe = S_utt^T c_trg,
+      db_ih = db_hh = colsum(S_code).
+    `hook` (nullable) runs once every decoder / postnet gradient has been enqueued (the
+    training step's overlapped decoder-slice all-reduce and Adam, train.py)."""
+
+    @staticmethod
+    def forward(ctx, codes, emb, core, B, T, nc, cd, hook, *params):
+        H = core.H
+        G = 4 * H
+        de = emb.shape[1]
+        In = cd + de
+        wih, bsum, whh, _, _ = core.packs()
+        dev = codes.device
+        c2 = codes.reshape(B * nc, cd)
+        pc = torch.empty(B * nc, G, device=dev)
+        K.gemm(B * nc, G, cd, operand(c2, cd), operand(wih, In), pc)
+        pe = torch.empty(B, G, device=dev)
+        K.gemm(B, G, de, operand(emb, de), operand(wih[:, cd:], In), pe, bias=bsum)
+        xproj = K.expand_codes(pc, pe, B, T, nc)
+        hbuf = K.lstm_scratch(B, H, 1, dev) if H > 64 and K.compute() == K.BF16 else None
+        h, c, g = K.lstm_fwd(xproj, whh, B, T, H, 1, hbuf)
+        ctx.core, ctx.args, ctx.hook = core, (B, T, nc, cd), hook
+        ctx.saved = (c, g)
+        ctx.save_for_backward(codes, emb, h)
+        ctx.h16 = getattr(h, "_bf16", None)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        codes, emb, h = ctx.saved_tensors
+        K.attach_twin(h, ctx.h16)
+        core = ctx.core
+        B, T, nc, cd = ctx.args
+        c, g = ctx.saved
+        H = core.H
+        G = 4 * H
+        de = emb.shape[1]
+        In = cd + de
+        _, _, whh, whh_t, wih_t = core.packs()
+        dev = h.device
+        dg = K.lstm_bwd(dh.contiguous(), h, c, g, whh if H <= 64 else None, whh_t, B, T, H, 1)
+        M = B * T
+        c2 = codes.reshape(B * nc, cd)
+        s_code = K.segsum(dg, B * nc, T // nc, G, ld=G)  # (B*nc, G): dG summed over each code's frames
+        s_utt = K.segsum(s_code, B, nc, G, ld=G)          # (B, G): ... and over each utterance
+        dcodes = demb = None
+        # few output tiles, K = 4H: split K (atomic fp32 accumulation into zeroed outputs)
+        if ctx.needs_input_grad[0]:
+            dcodes = torch.empty(B * nc, cd, device=dev)
+            K.gemm(B * nc, cd, G, operand(s_code, G), operand(wih_t, G), dcodes,
+                   split_k=K.auto_split_k(B * nc, cd, G))
+            dcodes = dcodes.view(B, nc * cd)
+        if ctx.needs_input_grad[1]:
+            demb = torch.empty(B, de, device=dev)
+            K.gemm(B, de, G, operand(s_utt, G), operand(wih_t[cd:], G), demb, split_k=K.auto_split_k(B, de, G))
+        sink = _SINK["on"]
+        w_ih, w_hh, b_ih, b_hh = core.params()
+        h_op = getattr(h, "_bf16", None) if K.compute() == K.BF16 else None
+        h_op = h if h_op is None else h_op
+
+        def wgrads():
+            dwih = _grad_of(w_ih) if sink else torch.zeros(G, In, device=dev)
+            K.gemm(G, cd, B * nc, operand(s_code, G, kstrided=True), operand(c2, cd, kstrided=True), dwih, ldc=In,
+                   accumulate=True, split_k=K.auto_split_k(G, cd, B * nc))
+            K.gemm(G, de, B, operand(s_utt, G, kstrided=True), operand(emb, de, kstrided=True), dwih[:, cd:],
+                   ldc=In, accumulate=True)
+            dwhh = _grad_of(w_hh) if sink else torch.empty(G, H, device=dev)
+            K.gemm(G, H, M, operand(dg, G, kstrided=True), operand(h_op, H, kstrided=True, window=(1, 1, T, T, H)),
+                   dwhh, split_k=K.auto_split_k(G, H, M), accumulate=sink)
+            if sink:
+                K.colsum(s_code, B * nc, G, out=_grad_of(b_ih), out2=_grad_of(b_hh), accumulate=True)
+                return [None] * 4
+            dbd = K.colsum(s_code, B * nc, G)
+            return [dwih, dwhh, dbd, K.convert(dbd, K.F32)]
+        ev = mark()
+        if sink:
+            with _Side(ev) as sd:
+                sd.keep(dg, h, h_op, s_code, s_utt, c2, emb)
+                if not _ABLATE_WGRAD:
+                    wgrads()
+            grads = [None] * 4
+        else:
+            grads = wgrads()
+        if ctx.hook is not None:
+            ctx.hook()
+        return (dcodes, demb, None, None, None, None, None, None, *grads)
+
+
+def lstm1_folded(mod, core, codes, emb, B, T, nc, cd, hook=None):
+    """Decoder lstm1 over cat(code expansion, emb) with the per-code / per-utterance input
+    projection (see _LSTM1FoldFn); h (B*T, H)."""
+    return _LSTM1FoldFn.apply(codes, emb, core, B, T, nc, cd, hook, *core.params())
+
+
 # =============================================================================== linear
 def copy_pack_ops(w, val):
     """Batched-pack op: val = w cast to the compute dtype."""

@@ -210,6 +210,13 @@ int avc_dec_concat(const float* codes, const float* emb, float* out, int B, int 
 int avc_dec_concat_bwd(const float* dout, float* dcodes, int B, int T, int n_codes, int code_dim,
                        int d_emb, void* stream);
 
+/* Decoder lstm1 input projection folded per code and per utterance:
+ * out[b*T+t][:] = pc[b*nc + t/(T/nc)][:] + pe[b][:], pc = codes . W_ih[:, :cd]^T (B*nc x G),
+ * pe = c_trg . W_ih[:, cd:]^T + b_ih + b_hh (B x G): the x_t . W_ih^T + b of nn.LSTM at
+ * AutoVC.py:96,103 on the concat of AutoVC.py:197-204, without the concat or its (B*T x G x cd+de)
+ * GEMM.  G % 4 == 0, 16-B aligned. */
+int avc_expand_codes(const float* pc, const float* pe, float* out, int B, int T, int nc, int G, void* stream);
+
 /* Weight repacks (and fp32 -> compute dtype).  conv: W[co][ci][k] ->
  *   mode 0: Wf[co][k][ci] (forward im2col order)
  *   mode 1: Wd[ci][k'][co] with k' = K-1-k (data-gradient order)
