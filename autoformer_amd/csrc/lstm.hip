@@ -757,6 +757,7 @@ __global__ void __launch_bounds__(512) lstm_step_bwd_bf(StepArgs a) {
 //   u32 ctl[4] (ctl[0] = timeout flag) | u32 flags[NG][64] | pad to 256 B | bf16 payload [2][B][W]
 // with W = H (forward) or 4H (backward); only ctl + flags are zeroed per launch.
 constexpr int PRG = 8, PJU = 32, PFL = 64;
+constexpr int GRAN_DEFAULT = 0;  // AVC_LSTM_GRAN default (bit 0 forward, bit 1 backward)
 constexpr unsigned PSPIN = 1u << 22;
 constexpr int AUX_SC1 = 16;  // buffer-instruction cache-policy bits: sc1
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
@@ -849,6 +850,62 @@ __device__ __forceinline__ void load_group(__amdgpu_buffer_rsrc_t pay, int row0,
   }
 }
 
+// Granule form (MI355X_MICROARCH.md "Valid forms", R2; cdna_hip_programming.md G16 recipe):
+// the payload IS the flag.  Each 8-byte granule {u32 data = 2 bf16, u32 tag = step + 1} is
+// written by one sc1 store (two granules per 16-B store, whose 8-B halves land untorn), so
+// the producer needs no drain and no flag, and a consumer needs no flag poll before loading:
+// every thread re-reads its own 16-B chunks (sc1, L1 bypassed) until both tags match, then
+// stages the data in LDS.  Twice the bytes of the bf16 payload, one fabric round trip fewer
+// on both sides.  Chunks I0 .. I0+NCH-1 of the thread (chunk = 2 granules = 4 values; a row
+// of W values has W/4 chunks).  false = spin timeout (ctl[0] / fault word raised).
+template <int W, int NCH, int I0, int NT>
+__device__ __forceinline__ bool sweep_group(__amdgpu_buffer_rsrc_t pay, int row0, int rows, bf16* lds, int ap,
+                                            unsigned tag, unsigned spin, unsigned* ctl, unsigned* fault) {
+  constexpr int CPR = W / 4;
+  const int tid = threadIdx.x;
+  u32x4_t v[NCH];
+  bool ok[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) ok[i] = (tid + NT * (I0 + i)) / CPR >= rows;
+  for (unsigned spins = 0;; ++spins) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int ch = tid + NT * (I0 + i), row = ch / CPR, col = ch - row * CPR;
+      if (!ok[i]) v[i] = __builtin_amdgcn_raw_buffer_load_b128(pay, ((row0 + row) * (W / 2) + col * 2) * 8, 0, AUX_SC1);
+    }
+    bool all = true;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      ok[i] = ok[i] || (v[i][1] == tag && v[i][3] == tag);
+      all = all && ok[i];
+    }
+    if (__all(all)) break;
+    if (spins >= spin) {
+      if ((threadIdx.x & 63) == 0) {
+        atomicOr(ctl, 1u);
+        if (fault) atomicOr(fault, 1u);
+      }
+      return false;
+    }
+    asm volatile("" ::: "memory");  // the re-reads are real loads, never hoisted
+  }
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int ch = tid + NT * (I0 + i), row = ch / CPR, col = ch - row * CPR;
+    if (row < rows) {
+      typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u32x2_t*>(lds + row * ap + col * 4) = u32x2_t{v[i][0], v[i][2]};
+    }
+  }
+  return true;
+}
+
+// One 16-B sc1 store of two granules: values (d0, d1) = 4 bf16 at granule index gi (even).
+__device__ __forceinline__ void store_granules(__amdgpu_buffer_rsrc_t pay, long long gi, unsigned d0, unsigned d1,
+                                               unsigned tag) {
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{d0, tag, d1, tag}, pay, (int)(gi * 8), 0, AUX_SC1);
+}
+
 // acc_n += A . W_n over NK K-blocks of 32: A rows (16 per lane group) are read from LDS at
 // `a` + 32k, W fragments live in registers; A fragments are read up to eight K-blocks ahead.
 template <int NK>
@@ -875,10 +932,12 @@ __device__ __forceinline__ void mfma_rows(const bf16* a, const bf16x8 (&wf)[2][N
 // Threads 0..255 own the (utterance, unit) cells of the element-wise stages.
 constexpr int PNT = 512;
 
-template <int H>
+template <int H, bool GR>
 __global__ void __launch_bounds__(PNT, 1) lstm_persist_fwd(PersistArgs a) {
   constexpr int G = 4 * H, NKH = H / 64, AP = H + 8, KH = H / 2;
   constexpr int NCH = (PRG * H / 8 + PNT - 1) / PNT;  // 16-B payload chunks per thread per step
+  constexpr int NCG = PRG * H / 4 / PNT;              // granule form: 16-B chunks per thread
+  static_assert(!GR || NCG * PNT * 4 == PRG * H, "granule chunks must tile the group payload");
   __shared__ __attribute__((aligned(16))) bf16 As[16 * AP];
   __shared__ __attribute__((aligned(16))) bf16 hs16[PRG * PJU];
   __shared__ float gs[2][PRG][4 * PJU + 1];
@@ -888,7 +947,7 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_fwd(PersistArgs a) {
   const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
   const int j0 = r * PJU, b0 = g * PRG;
   const int T = a.T, B = a.B, rows = min(PRG, B - b0);
-  const __amdgpu_buffer_rsrc_t pay = rsrc_of(a.pay, (long long)2 * B * H * 2);
+  const __amdgpu_buffer_rsrc_t pay = rsrc_of(a.pay, (long long)2 * B * H * (GR ? 4 : 2));
   unsigned* flags = a.ctl + 4 + g * PFL;
 
   // W_hh rows of gate gq for units j0 + 16n + (lane & 15), K half kh
@@ -918,11 +977,19 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_fwd(PersistArgs a) {
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     if (s > 0) {
       // ---- the group's h_{t-1} -> LDS A tile (rows past the batch stay zero)
-      if (w == 0 && !poll_flags(flags, H / PJU, (unsigned)s, a.ctl, a.fault, a.spin)) quit = 1;
-      __syncthreads();
-      if (quit) return;  // block-uniform exit after a spin timeout
-      load_group<H, NCH, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
-      __syncthreads();
+      if constexpr (GR) {
+        if (!sweep_group<H, NCG, 0, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP, (unsigned)s, a.spin, a.ctl,
+                                         a.fault))
+          quit = 1;
+        __syncthreads();
+        if (quit) return;
+      } else {
+        if (w == 0 && !poll_flags(flags, H / PJU, (unsigned)s, a.ctl, a.fault, a.spin)) quit = 1;
+        __syncthreads();
+        if (quit) return;  // block-uniform exit after a spin timeout
+        load_group<H, NCH, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
+        __syncthreads();
+      }
       stamp(a.trace, T, s, 1);
       mfma_rows<NKH>(As + (lane & 15) * AP + kh * KH + 8 * (lane >> 4), wf, acc0, acc1);
     }
@@ -960,12 +1027,23 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_fwd(PersistArgs a) {
     __syncthreads();
     if (w == 0) {
       if (s + 1 < T) {
-        if (lane < 4 * rows) {
-          const int row = lane >> 2, c8 = lane & 3;
-          const u32x4_t v = *reinterpret_cast<const u32x4_t*>(hs16 + row * PJU + c8 * 8);
-          __builtin_amdgcn_raw_buffer_store_b128(v, pay, (((s & 1) * B + b0 + row) * H + j0 + c8 * 8) * 2, 0, AUX_SC1);
+        if constexpr (GR) {
+          // 8 lanes per row, two granules (4 units) each: the stores are the publication
+          const int row = lane >> 3, c4 = lane & 7;
+          if (row < rows) {
+            const unsigned* hv = reinterpret_cast<const unsigned*>(hs16 + row * PJU + c4 * 4);
+            store_granules(pay, ((long long)((s & 1) * B + b0 + row) * H + j0 + c4 * 4) / 2, hv[0], hv[1],
+                           (unsigned)(s + 1));
+          }
+        } else {
+          if (lane < 4 * rows) {
+            const int row = lane >> 2, c8 = lane & 3;
+            const u32x4_t v = *reinterpret_cast<const u32x4_t*>(hs16 + row * PJU + c8 * 8);
+            __builtin_amdgcn_raw_buffer_store_b128(v, pay, (((s & 1) * B + b0 + row) * H + j0 + c8 * 8) * 2, 0,
+                                                   AUX_SC1);
+          }
+          raise_flag(flags, r, (unsigned)(s + 1));
         }
-        raise_flag(flags, r, (unsigned)(s + 1));
       }
     } else if (w >= 4) {
       const int cell = tid - PRG * PJU, ob = b0 + (cell >> 5), oj = j0 + (cell & 31);
@@ -1008,10 +1086,12 @@ struct PersistBwdArgs {
   int B, T, ng;
 };
 
-template <int H>
+template <int H, bool GR>
 __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
   constexpr int G = 4 * H, NKH = H / 64, AP = G + 8, KH = H / 2, NW = PNT / 64;
   constexpr int NCH = (PRG * G / 8 + PNT - 1) / PNT;  // 16-B payload chunks per thread per step
+  constexpr int NCG = PRG * G / 4 / PNT;              // granule form: 16-B chunks per thread
+  static_assert(!GR || (NCG * PNT * 4 == PRG * G && NCG % 2 == 0), "granule chunks must tile the payload");
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* As = reinterpret_cast<bf16*>(smem_raw);                          // [PRG + 1][AP], row PRG = zeros
   float* red = reinterpret_cast<float*>(smem_raw + (PRG + 1) * AP * 2);  // [NW][PRG][PJU + 1]
@@ -1022,7 +1102,7 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
   const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
   const int j0 = r * PJU, b0 = g * PRG;
   const int T = a.T, B = a.B, rows = min(PRG, B - b0);
-  const __amdgpu_buffer_rsrc_t pay = rsrc_of(a.pay, (long long)2 * B * G * 2);
+  const __amdgpu_buffer_rsrc_t pay = rsrc_of(a.pay, (long long)2 * B * G * (GR ? 4 : 2));
   unsigned* flags = a.ctl + 4 + g * PFL;
 
   // W_hh^T fragments: B operand of the product, n = unit j0 + 16n + (lane&15), k = gate row
@@ -1059,11 +1139,21 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
       go = gp[3 * H];
     }
     if (s > 0) {
-      if (w == 0 && !poll_flags(flags, H / PJU, (unsigned)s, a.ctl, a.fault, a.spin)) *quit = 1;
-      __syncthreads();
-      if (*quit) return;  // block-uniform exit after a spin timeout
-      load_group<G, NCH, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
-      __syncthreads();
+      if constexpr (GR) {
+        // two half sweeps keep the in-flight chunk registers at NCG / 2 per thread
+        const int row0 = ((s - 1) & 1) * B + b0;
+        if (!sweep_group<G, NCG / 2, 0, PNT>(pay, row0, rows, As, AP, (unsigned)s, a.spin, a.ctl, a.fault) ||
+            !sweep_group<G, NCG / 2, NCG / 2, PNT>(pay, row0, rows, As, AP, (unsigned)s, a.spin, a.ctl, a.fault))
+          *quit = 1;
+        __syncthreads();
+        if (*quit) return;
+      } else {
+        if (w == 0 && !poll_flags(flags, H / PJU, (unsigned)s, a.ctl, a.fault, a.spin)) *quit = 1;
+        __syncthreads();
+        if (*quit) return;  // block-uniform exit after a spin timeout
+        load_group<G, NCH, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
+        __syncthreads();
+      }
       stamp(a.trace, T, s, 1);
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
       mfma_rows<NKH>(As + arow * AP + gq * H + kh * KH + 8 * (lane >> 4), wf, acc0, acc1);
@@ -1107,16 +1197,30 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
     __syncthreads();
     if (w == 0) {
       if (s + 1 < T) {
+        if constexpr (GR) {
+          // 32 two-granule chunks (4 values) per row: 8 rows x 4 gates x 8 chunks, 4 per lane
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int ch = lane + 64 * i, row = ch >> 4, q = (ch >> 2) & 3, c8 = ch & 3;
-          if (row < rows) {
-            const u32x4_t v = *reinterpret_cast<const u32x4_t*>(ds16 + row * (4 * PJU) + q * PJU + c8 * 8);
-            __builtin_amdgcn_raw_buffer_store_b128(v, pay, (((s & 1) * B + b0 + row) * G + q * H + j0 + c8 * 8) * 2,
-                                                   0, AUX_SC1);
+          for (int i = 0; i < 4; ++i) {
+            const int ch = lane + 64 * i, row = ch >> 5, q = (ch >> 3) & 3, c4 = ch & 7;
+            if (row < rows) {
+              const unsigned* dv = reinterpret_cast<const unsigned*>(ds16 + row * (4 * PJU) + q * PJU + c4 * 4);
+              store_granules(pay, ((long long)((s & 1) * B + b0 + row) * G + q * H + j0 + c4 * 4) / 2, dv[0], dv[1],
+                             (unsigned)(s + 1));
+            }
           }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int ch = lane + 64 * i, row = ch >> 4, q = (ch >> 2) & 3, c8 = ch & 3;
+            if (row < rows) {
+              const u32x4_t v = *reinterpret_cast<const u32x4_t*>(ds16 + row * (4 * PJU) + q * PJU + c8 * 8);
+              __builtin_amdgcn_raw_buffer_store_b128(v, pay,
+                                                     (((s & 1) * B + b0 + row) * G + q * H + j0 + c8 * 8) * 2, 0,
+                                                     AUX_SC1);
+            }
+          }
+          raise_flag(flags, r, (unsigned)(s + 1));
         }
-        raise_flag(flags, r, (unsigned)(s + 1));
       }
     } else if (w >= 4) {
       const int cell = tid - PRG * PJU, ob = b0 + (cell >> 5), oj = j0 + (cell & 31);
@@ -1177,15 +1281,40 @@ unsigned spin_bound() {
 }
 
 // Dynamic-LDS attribute of the persistent backward kernels, set once per (kernel, device).
-template <int H>
+template <int H, bool GR>
 void set_bwd_lds_attr() {
   int dev = 0;
   (void)hipGetDevice(&dev);
   static std::once_flag once[MAXDEV];
   std::call_once(once[dev & (MAXDEV - 1)], [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_persist_bwd<H>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_persist_bwd<H, GR>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_bwd_lds<H>());
   });
+}
+
+// Hand-off form per direction (AVC_LSTM_GRAN bit 0 = forward, bit 1 = backward use the
+// granule form; default: the measured faster form per direction)
+int gran_mask() {
+  static const int v = [] {
+    const char* e = getenv("AVC_LSTM_GRAN");
+    return e ? atoi(e) : GRAN_DEFAULT;
+  }();
+  return v;
+}
+bool gran(bool bwd) { return (gran_mask() >> (bwd ? 1 : 0)) & 1; }
+
+template <int H>
+const void* persist_fn(bool bwd) {
+  if (bwd) {
+    if (gran(true)) {
+      set_bwd_lds_attr<H, true>();
+      return reinterpret_cast<const void*>(&lstm_persist_bwd<H, true>);
+    }
+    set_bwd_lds_attr<H, false>();
+    return reinterpret_cast<const void*>(&lstm_persist_bwd<H, false>);
+  }
+  return gran(false) ? reinterpret_cast<const void*>(&lstm_persist_fwd<H, true>)
+                     : reinterpret_cast<const void*>(&lstm_persist_fwd<H, false>);
 }
 
 // Co-residency of a persistent grid: every workgroup must be resident at once (the members
@@ -1228,24 +1357,11 @@ bool persistent_path(int B, int H, int dirs, bool bf, bool bwd) {
   if (!bf || dirs != 1 || !(H == 1024 || H == 768 || H == 512) || no_persist_env()) return false;
   const int ng = (B + PRG - 1) / PRG, grid = ng * (H / PJU);
   if (grid > num_cus()) return false;
-  const void* fn;
-  size_t lds = 0;
-  if (!bwd) {
-    fn = H == 1024 ? reinterpret_cast<const void*>(&lstm_persist_fwd<1024>)
-       : H == 768  ? reinterpret_cast<const void*>(&lstm_persist_fwd<768>)
-                   : reinterpret_cast<const void*>(&lstm_persist_fwd<512>);
-  } else if (H == 1024) {
-    set_bwd_lds_attr<1024>();
-    fn = reinterpret_cast<const void*>(&lstm_persist_bwd<1024>);
-    lds = persist_bwd_lds<1024>();
-  } else if (H == 768) {
-    set_bwd_lds_attr<768>();
-    fn = reinterpret_cast<const void*>(&lstm_persist_bwd<768>);
-    lds = persist_bwd_lds<768>();
-  } else {
-    fn = reinterpret_cast<const void*>(&lstm_persist_bwd<512>);
-    lds = persist_bwd_lds<512>();
-  }
+  const void* fn = H == 1024 ? persist_fn<1024>(bwd) : H == 768 ? persist_fn<768>(bwd) : persist_fn<512>(bwd);
+  const size_t lds = !bwd ? 0
+                     : H == 1024 ? persist_bwd_lds<1024>()
+                     : H == 768  ? persist_bwd_lds<768>()
+                                 : persist_bwd_lds<512>();
   return fits_resident(fn, PNT, lds, grid);
 }
 
@@ -1338,10 +1454,13 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
     p.B = B;
     p.T = T;
     p.ng = ng;
-    (void)hipMemsetAsync(hbuf, 0, px_ctl_bytes(ng), s);
-    if (H == 1024) lstm_persist_fwd<1024><<<ng * (H / PJU), PNT, 0, s>>>(p);
-    else if (H == 768) lstm_persist_fwd<768><<<ng * (H / PJU), PNT, 0, s>>>(p);  // Adjust.py:30
-    else lstm_persist_fwd<512><<<ng * (H / PJU), PNT, 0, s>>>(p);
+    const bool gr = gran(false);
+    // flag form: only ctl + flags are polled; granule form: every tag of the payload too
+    (void)hipMemsetAsync(hbuf, 0, gr ? px_payload_off(ng) + (size_t)8 * B * H : px_ctl_bytes(ng), s);
+    const dim3 grid(ng * (H / PJU));
+    if (H == 1024) gr ? lstm_persist_fwd<1024, true><<<grid, PNT, 0, s>>>(p) : lstm_persist_fwd<1024, false><<<grid, PNT, 0, s>>>(p);
+    else if (H == 768) gr ? lstm_persist_fwd<768, true><<<grid, PNT, 0, s>>>(p) : lstm_persist_fwd<768, false><<<grid, PNT, 0, s>>>(p);  // Adjust.py:30
+    else gr ? lstm_persist_fwd<512, true><<<grid, PNT, 0, s>>>(p) : lstm_persist_fwd<512, false><<<grid, PNT, 0, s>>>(p);
     return avc_check_launch("avc_lstm_fwd(persistent)");
   }
   AVC_CHECK_ARG(h_bf16 == nullptr, "avc_lstm_fwd: the bf16 h copy is produced by the persistent path only");
@@ -1406,14 +1525,19 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
     p.B = B;
     p.T = T;
     p.ng = ng;
-    (void)hipMemsetAsync(gbuf, 0, px_ctl_bytes(ng), s);
+    const bool gr = gran(true);
+    (void)hipMemsetAsync(gbuf, 0, gr ? px_payload_off(ng) + (size_t)32 * B * H : px_ctl_bytes(ng), s);
     // (persistent_path above set the dynamic-LDS attributes)
+    const dim3 grid(ng * (H / PJU));
     if (H == 1024) {
-      lstm_persist_bwd<1024><<<ng * (H / PJU), PNT, persist_bwd_lds<1024>(), s>>>(p);
+      gr ? lstm_persist_bwd<1024, true><<<grid, PNT, persist_bwd_lds<1024>(), s>>>(p)
+         : lstm_persist_bwd<1024, false><<<grid, PNT, persist_bwd_lds<1024>(), s>>>(p);
     } else if (H == 768) {
-      lstm_persist_bwd<768><<<ng * (H / PJU), PNT, persist_bwd_lds<768>(), s>>>(p);
+      gr ? lstm_persist_bwd<768, true><<<grid, PNT, persist_bwd_lds<768>(), s>>>(p)
+         : lstm_persist_bwd<768, false><<<grid, PNT, persist_bwd_lds<768>(), s>>>(p);
     } else {
-      lstm_persist_bwd<512><<<ng * (H / PJU), PNT, persist_bwd_lds<512>(), s>>>(p);
+      gr ? lstm_persist_bwd<512, true><<<grid, PNT, persist_bwd_lds<512>(), s>>>(p)
+         : lstm_persist_bwd<512, false><<<grid, PNT, persist_bwd_lds<512>(), s>>>(p);
     }
     return avc_check_launch("avc_lstm_bwd(persistent)");
   }

@@ -241,8 +241,9 @@ def colsum(x, M, N, ld=None, out=None, accumulate=False, out2=None):
 # ------------------------------------------------------------------------- LSTM
 def lstm_scratch(B, H, dirs, device):
     """bf16 scratch for the large-H recurrence: per-step ping-pong h (2*dirs*B*H bf16) or,
-    for the persistent kernel, control words + per-member flags + a [2][B][H] bf16 payload."""
-    return torch.zeros(max(2 * dirs * B * H, 4 * B * H + 32), device=device, dtype=torch.bfloat16)
+    for the persistent kernel, control words + per-member flags (< 8 KB) + a [2][B][H] payload
+    of bf16 (flag form) or of 8-byte {2 x bf16, tag} granules (granule form: 8*B*H bytes)."""
+    return torch.zeros(max(2 * dirs * B * H, 4 * B * H + 4096), device=device, dtype=torch.bfloat16)
 
 
 def lstm_timeout_flag(hbuf, B, H):
@@ -335,7 +336,7 @@ _CACHE = {}
 
 
 def lstm_bwd_scratch(B, H, dirs, device):
-    nbytes = max(16 * dirs * B * H, 32 * B * H + 16)
+    nbytes = max(16 * dirs * B * H, 32 * B * H + 8192)  # granule form: [2][B][4H/2] x 8 B + control
     return torch.empty((nbytes + 1) // 2, device=device, dtype=torch.bfloat16)
 
 

@@ -680,15 +680,19 @@ class _LSTM1FoldFn(torch.autograd.Function):
         s_code = K.segsum(dg, B * nc, T // nc, G, ld=G)  # (B*nc, G): dG summed over each code's frames
         s_utt = K.segsum(s_code, B, nc, G, ld=G)          # (B, G): ... and over each utterance
         dcodes = demb = None
-        # few output tiles, K = 4H: split K (atomic fp32 accumulation into zeroed outputs)
+        # few output tiles, K = 4H: split K (atomic fp32 accumulation into zeroed outputs).  More
+        # than two atomic partials make the sum order-dependent, so the fp32 parity mode keeps
+        # these data gradients unsplit: its encoder gradients stay bit-reproducible (DP test)
+        det = K.compute() == K.F32
         if ctx.needs_input_grad[0]:
             dcodes = torch.empty(B * nc, cd, device=dev)
             K.gemm(B * nc, cd, G, operand(s_code, G), operand(wih_t, G), dcodes,
-                   split_k=K.auto_split_k(B * nc, cd, G))
+                   split_k=1 if det else K.auto_split_k(B * nc, cd, G))
             dcodes = dcodes.view(B, nc * cd)
         if ctx.needs_input_grad[1]:
             demb = torch.empty(B, de, device=dev)
-            K.gemm(B, de, G, operand(s_utt, G), operand(wih_t[cd:], G), demb, split_k=K.auto_split_k(B, de, G))
+            K.gemm(B, de, G, operand(s_utt, G), operand(wih_t[cd:], G), demb,
+                   split_k=1 if det else K.auto_split_k(B, de, G))
         sink = _SINK["on"]
         w_ih, w_hh, b_ih, b_hh = core.params()
         h_op = getattr(h, "_bf16", None) if K.compute() == K.BF16 else None

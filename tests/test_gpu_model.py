@@ -10,6 +10,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
@@ -177,6 +178,12 @@ def test_trainstep_sink_graph_matches_plain_autograd(golden):
 
 
 def test_trainstep_graph_replay_equals_eager():
+    """hipGraph replay of the step equals the eager step.  The bf16 step is not bit-reproducible
+    (split-K atomics reorder run to run, and Adam's first updates turn sign flips of tiny
+    gradients into whole-lr moves: two EAGER runs differ by up to 3 lr after 3 steps,
+    tools/replay_diff.py), so the parameters are held fixed (lr = 0) and the third step's
+    losses and per-tensor gradients are compared (rel-Frobenius 1e-2: bf16 run-to-run spread
+    1.3e-3 measured); a missing or stale kernel in the replay shows as an O(1) error."""
     from autoformer_amd.detinit import det_inputs
     from autoformer_amd.layers import set_grad_sink
     from autoformer_amd.train import TrainStep
@@ -184,7 +191,7 @@ def test_trainstep_graph_replay_equals_eager():
     x, e = det_inputs(4, 64, seed=3)
     x, e = torch.from_numpy(x).to(DEV), torch.from_numpy(e).to(DEV)
     ma, mb = _model(16, "bf16"), _model(16, "bf16")
-    ta, tb = TrainStep(ma), TrainStep(mb)
+    ta, tb = TrainStep(ma, lr=0.0), TrainStep(mb, lr=0.0)
     try:
         for _ in range(3):
             la = ta.step(x, e)
@@ -193,7 +200,12 @@ def test_trainstep_graph_replay_equals_eager():
         tb.step(x, e)               # replay = step 2
         lb = tb.step(x, e)          # replay = step 3
         torch.cuda.synchronize()
-        assert abs(la.item() - lb.item()) <= 1e-3 * abs(la.item())
-        assert torch.allclose(ta.flat, tb.flat, rtol=1e-3, atol=1e-5)
+        assert abs(la.item() - lb.item()) <= 1e-4 * abs(la.item())
+        assert torch.equal(ta.flat, tb.flat)  # lr = 0: nothing moved
+        for (n, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+            ga, gb = pa.grad.double(), pb.grad.double()
+            assert (ga - gb).norm() <= 1e-2 * ga.norm() + 1e-6, n  # SURVEY 8(c) gradient bar
+        for (n, ba), (_, bb) in zip(ma.named_buffers(), mb.named_buffers()):
+            assert torch.allclose(ba.double(), bb.double(), rtol=1e-4, atol=1e-6), n
     finally:
         set_grad_sink(False)
