@@ -757,7 +757,6 @@ __global__ void __launch_bounds__(512) lstm_step_bwd_bf(StepArgs a) {
 //   u32 ctl[4] (ctl[0] = timeout flag) | u32 flags[NG][64] | pad to 256 B | bf16 payload [2][B][W]
 // with W = H (forward) or 4H (backward); only ctl + flags are zeroed per launch.
 constexpr int PRG = 8, PJU = 32, PFL = 64;
-constexpr int GRAN_DEFAULT = 0;  // AVC_LSTM_GRAN default (bit 0 forward, bit 1 backward)
 constexpr unsigned PSPIN = 1u << 22;
 constexpr int AUX_SC1 = 16;  // buffer-instruction cache-policy bits: sc1
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
@@ -778,6 +777,7 @@ struct PersistArgs {
   unsigned long long* trace;  // diagnostics (avc_lstm_trace), null in production
   unsigned* fault;            // process fault word (avc_set_fault_word), bit 0 on a spin timeout; nullable
   unsigned spin;              // spin bound per wait (PSPIN unless avc_lstm_set_spin / AVC_LSTM_SPIN)
+  int nap;                    // granule form: s_sleep(1)s between failed sweeps (AVC_LSTM_NAP)
   int B, T, ng;
 };
 
@@ -860,7 +860,8 @@ __device__ __forceinline__ void load_group(__amdgpu_buffer_rsrc_t pay, int row0,
 // of W values has W/4 chunks).  false = spin timeout (ctl[0] / fault word raised).
 template <int W, int NCH, int I0, int NT>
 __device__ __forceinline__ bool sweep_group(__amdgpu_buffer_rsrc_t pay, int row0, int rows, bf16* lds, int ap,
-                                            unsigned tag, unsigned spin, unsigned* ctl, unsigned* fault) {
+                                            unsigned tag, unsigned spin, unsigned* ctl, unsigned* fault,
+                                            int nap) {
   constexpr int CPR = W / 4;
   const int tid = threadIdx.x;
   u32x4_t v[NCH];
@@ -887,6 +888,7 @@ __device__ __forceinline__ bool sweep_group(__amdgpu_buffer_rsrc_t pay, int row0
       }
       return false;
     }
+    for (int k = 0; k < nap; ++k) __builtin_amdgcn_s_sleep(1);  // back-off between passes
     asm volatile("" ::: "memory");  // the re-reads are real loads, never hoisted
   }
 #pragma unroll
@@ -979,7 +981,7 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_fwd(PersistArgs a) {
       // ---- the group's h_{t-1} -> LDS A tile (rows past the batch stay zero)
       if constexpr (GR) {
         if (!sweep_group<H, NCG, 0, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP, (unsigned)s, a.spin, a.ctl,
-                                         a.fault))
+                                         a.fault, a.nap))
           quit = 1;
         __syncthreads();
         if (quit) return;
@@ -1083,6 +1085,7 @@ struct PersistBwdArgs {
   unsigned long long* trace;  // diagnostics (avc_lstm_trace), null in production
   unsigned* fault;            // as PersistArgs
   unsigned spin;
+  int nap;
   int B, T, ng;
 };
 
@@ -1139,11 +1142,14 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
       go = gp[3 * H];
     }
     if (s > 0) {
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
       if constexpr (GR) {
         // two half sweeps keep the in-flight chunk registers at NCG / 2 per thread
         const int row0 = ((s - 1) & 1) * B + b0;
-        if (!sweep_group<G, NCG / 2, 0, PNT>(pay, row0, rows, As, AP, (unsigned)s, a.spin, a.ctl, a.fault) ||
-            !sweep_group<G, NCG / 2, NCG / 2, PNT>(pay, row0, rows, As, AP, (unsigned)s, a.spin, a.ctl, a.fault))
+        if (!sweep_group<G, NCG / 2, 0, PNT>(pay, row0, rows, As, AP, (unsigned)s, a.spin, a.ctl, a.fault,
+                                             a.nap) ||
+            !sweep_group<G, NCG / 2, NCG / 2, PNT>(pay, row0, rows, As, AP, (unsigned)s, a.spin, a.ctl, a.fault,
+                                                    a.nap))
           *quit = 1;
         __syncthreads();
         if (*quit) return;
@@ -1155,7 +1161,6 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
         __syncthreads();
       }
       stamp(a.trace, T, s, 1);
-      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
       mfma_rows<NKH>(As + arow * AP + gq * H + kh * KH + 8 * (lane >> 4), wf, acc0, acc1);
       // rows 4*(lane>>4)+e < 8 only for lanes 0..31
       if (lane < 32) {
@@ -1292,28 +1297,39 @@ void set_bwd_lds_attr() {
   });
 }
 
-// Hand-off form per direction (AVC_LSTM_GRAN bit 0 = forward, bit 1 = backward use the
-// granule form; default: the measured faster form per direction)
+// Hand-off form.  Default (measured): granules where a consumer's granule
+// payload is at most 16 KB -- the forward at H <= 512 (lstm1: 2.24 -> 1.74 us per step) --
+// and the flag form above that (H = 1024 forward 3.08 vs 3.26 us, backward 4.03 vs 4.43 us:
+// the doubled payload fetch costs more than the drain and the flag round trip it saves).
+// AVC_LSTM_GRAN overrides: bit 0 = forward, bit 1 = backward in the granule form.
 int gran_mask() {
   static const int v = [] {
     const char* e = getenv("AVC_LSTM_GRAN");
-    return e ? atoi(e) : GRAN_DEFAULT;
+    return e ? atoi(e) : -1;
   }();
   return v;
 }
-bool gran(bool bwd) { return (gran_mask() >> (bwd ? 1 : 0)) & 1; }
+bool gran(bool bwd, int H) {
+  const int m = gran_mask();
+  if (m >= 0) return (m >> (bwd ? 1 : 0)) & 1;
+  return !bwd && (size_t)PRG * H * 4 <= 16384;
+}
+int nap() {
+  static const int v = getenv("AVC_LSTM_NAP") ? atoi(getenv("AVC_LSTM_NAP")) : 0;
+  return v;
+}
 
 template <int H>
 const void* persist_fn(bool bwd) {
   if (bwd) {
-    if (gran(true)) {
+    if (gran(true, H)) {
       set_bwd_lds_attr<H, true>();
       return reinterpret_cast<const void*>(&lstm_persist_bwd<H, true>);
     }
     set_bwd_lds_attr<H, false>();
     return reinterpret_cast<const void*>(&lstm_persist_bwd<H, false>);
   }
-  return gran(false) ? reinterpret_cast<const void*>(&lstm_persist_fwd<H, true>)
+  return gran(false, H) ? reinterpret_cast<const void*>(&lstm_persist_fwd<H, true>)
                      : reinterpret_cast<const void*>(&lstm_persist_fwd<H, false>);
 }
 
@@ -1363,6 +1379,12 @@ bool persistent_path(int B, int H, int dirs, bool bf, bool bwd) {
                      : H == 768  ? persist_bwd_lds<768>()
                                  : persist_bwd_lds<512>();
   return fits_resident(fn, PNT, lds, grid);
+}
+
+template <int H>
+void launch_persist_bwd(dim3 grid, hipStream_t s, bool gr, const PersistBwdArgs& p) {
+  if (gr) lstm_persist_bwd<H, true><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
+  else lstm_persist_bwd<H, false><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
 }
 
 template <int HM>
@@ -1451,10 +1473,11 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
     p.trace = g_trace;
     p.fault = fault_word();
     p.spin = spin_bound();
+    p.nap = nap();
     p.B = B;
     p.T = T;
     p.ng = ng;
-    const bool gr = gran(false);
+    const bool gr = gran(false, H);
     // flag form: only ctl + flags are polled; granule form: every tag of the payload too
     (void)hipMemsetAsync(hbuf, 0, gr ? px_payload_off(ng) + (size_t)8 * B * H : px_ctl_bytes(ng), s);
     const dim3 grid(ng * (H / PJU));
@@ -1522,23 +1545,17 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
     p.trace = g_trace;
     p.fault = fault_word();
     p.spin = spin_bound();
+    p.nap = nap();
     p.B = B;
     p.T = T;
     p.ng = ng;
-    const bool gr = gran(true);
+    const bool gr = gran(true, H);
     (void)hipMemsetAsync(gbuf, 0, gr ? px_payload_off(ng) + (size_t)32 * B * H : px_ctl_bytes(ng), s);
     // (persistent_path above set the dynamic-LDS attributes)
     const dim3 grid(ng * (H / PJU));
-    if (H == 1024) {
-      gr ? lstm_persist_bwd<1024, true><<<grid, PNT, persist_bwd_lds<1024>(), s>>>(p)
-         : lstm_persist_bwd<1024, false><<<grid, PNT, persist_bwd_lds<1024>(), s>>>(p);
-    } else if (H == 768) {
-      gr ? lstm_persist_bwd<768, true><<<grid, PNT, persist_bwd_lds<768>(), s>>>(p)
-         : lstm_persist_bwd<768, false><<<grid, PNT, persist_bwd_lds<768>(), s>>>(p);
-    } else {
-      gr ? lstm_persist_bwd<512, true><<<grid, PNT, persist_bwd_lds<512>(), s>>>(p)
-         : lstm_persist_bwd<512, false><<<grid, PNT, persist_bwd_lds<512>(), s>>>(p);
-    }
+    if (H == 1024) launch_persist_bwd<1024>(grid, s, gr, p);
+    else if (H == 768) launch_persist_bwd<768>(grid, s, gr, p);
+    else launch_persist_bwd<512>(grid, s, gr, p);
     return avc_check_launch("avc_lstm_bwd(persistent)");
   }
   AVC_CHECK_ARG(dgates_bf16 == nullptr, "avc_lstm_bwd: the bf16 dG twin is produced by the persistent path only");
