@@ -16,8 +16,8 @@ import torch  # noqa: F401  (must precede the HIP library)
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip"]
-ABI_VERSION = 7
+SOURCES = ["gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip"]
+ABI_VERSION = 8
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -118,6 +118,13 @@ _SIGS = {
     "avc_adain_bwd": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p]),
     "avc_segsum": (c_int, [c_void_p, c_ll, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "avc_mg_gather": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
+                              c_void_p, c_int, c_void_p]),
+    "avc_mg_act": (c_int, [c_void_p, c_ll, c_float, c_void_p, c_void_p, c_void_p]),
+    "avc_mg_wn_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                               c_int, c_void_p, c_void_p]),
+    "avc_mg_conv_out": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p,
+                                c_void_p]),
     "avc_step_select": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_rownorm_fwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "avc_rownorm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),

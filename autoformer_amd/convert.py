@@ -8,8 +8,9 @@ back to the source's real length when it was padded (the `isPlay` branch).
 
 Same kernels as training, forward only under `torch.no_grad()`; the model stays in whatever
 BatchNorm mode the caller left it in (the reference converts with the model in train mode, so
-BN uses the statistics of the one utterance).  The MelGAN vocoder that turns the mel into a
-waveform is out of scope.
+BN uses the statistics of the one utterance).  `get_wavs` (evaluate.py:96-98) turns a converted
+mel into a waveform with the HIP MelGAN generator (autoformer_amd.melgan.MelVocoder) when the
+Converter was given one.
 """
 from __future__ import annotations
 
@@ -34,10 +35,21 @@ def crop_mel(mel: np.ndarray, len_crop: int, rng=np.random):
 class Converter:
     """convert(mel_source, emb_org, emb_trg) -> converted mel (T', 80) on the host."""
 
-    def __init__(self, model, len_crop: int, device="cuda:0"):
+    def __init__(self, model, len_crop: int, device="cuda:0", vocoder=None):
         self.model = model
         self.len_crop = len_crop
         self.device = torch.device(device)
+        self.vocoder = vocoder  # autoformer_amd.melgan.MelVocoder (evaluate.py:24) or None
+
+    @torch.no_grad()
+    def get_wavs(self, mel):
+        """evaluate.py:96-98: (1, 80, T) mel -> (1, T*256) waveform.  A frame-major (1, T, 80)
+        mel, the layout get_trans_mel returns, goes straight in without the transpose."""
+        if self.vocoder is None:
+            raise RuntimeError("Converter was built without a vocoder (pass vocoder=MelVocoder(...))")
+        if mel.dim() == 3 and mel.shape[-1] == 80 and mel.shape[1] != 80:
+            return self.vocoder.inverse_frames(mel)
+        return self.vocoder.inverse(mel)
 
     def _dev(self, a):
         return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).unsqueeze(0).to(self.device)

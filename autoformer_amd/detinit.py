@@ -113,3 +113,32 @@ def det_inputs(batch: int, T: int, dim_emb: int = 256, seed: int = 1234):
     e = e.reshape(batch, dim_emb)
     e = e / np.linalg.norm(e, axis=1, keepdims=True)
     return x, e.astype(np.float32)
+
+
+def det_melgan_state(shapes, gain=(0.7, 1.2)) -> "OrderedDict[str, np.ndarray]":
+    """Closed-form weights for the MelGAN generator (melgan/modules.py:88-131) from its
+    state_dict (key, shape) list: weight_v as any >= 2-D weight (Xavier bound), weight_g uniform
+    in [gain) (positive: each output channel's weight then has that norm; (0.7, 1.2) keeps the 17
+    layers' output unsaturated, max |audio| 0.75, std 0.16), bias 1/sqrt(fan_in of
+    the sibling weight_v).  Same splitmix64 stream as det_values, keyed by entry index."""
+    shapes = OrderedDict((k, tuple(s)) for k, s in shapes)
+    out = OrderedDict()
+    for k, (key, shape) in enumerate(shapes.items()):
+        n = int(np.prod(shape))
+        u = uniform24(k, n) / float(1 << 24)
+        if key.endswith(".weight_g"):
+            w = gain[0] + (gain[1] - gain[0]) * u
+        elif key.endswith(".bias"):
+            v = shapes[key[: -len("bias")] + "weight_v"]
+            fan_in = v[1] * int(np.prod(v[2:]))
+            w = (2.0 * u - 1.0) / math.sqrt(fan_in)
+        else:
+            w = det_values(key, k, shape, shapes).reshape(-1).astype(np.float64)
+        out[key] = w.astype(np.float32).reshape(shape)
+    return out
+
+
+def det_mel(batch: int, C: int, T: int, seed: int = 4321):
+    """Deterministic (B, C, T) log10-mel-like vocoder input in [-5, 2] (the Converter's range)."""
+    u = uniform24(0xC0000 + seed, batch * C * T) / float(1 << 24)
+    return (-5.0 + 7.0 * u).reshape(batch, C, T).astype(np.float32)

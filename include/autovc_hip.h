@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 7
+#define AVC_ABI_VERSION 8
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -335,6 +335,31 @@ int avc_pad_cols(const float* src, long long lds, void* dst, int dtype, int R, i
  * fp32 result and/or its bf16 GEMM-operand twin from one pass (y or y16 may be null):
  * the MLP-Mixer hidden activations (MLPMixer.py:9-14) feed only GEMMs and bias sums. */
 int avc_gelu_twin(const float* g, const float* x, float* y, void* y16, long long n, int bwd, void* stream);
+
+/* MelGAN vocoder generator, inference (melgan.hip).  Replaces the forward of
+ * melgan/modules.py:88-131 Generator (called by melgan/interface.py:47-53 MelVocoder.inverse,
+ * util/evaluate.py:98); the convolutions themselves run on avc_gemm.
+ * Gather: out[(b*Lo + t)][k*C + c] = act(x[b][src][c]), src = t + k*dil - pad reflected into
+ * [0, L) (reflect = 1, nn.ReflectionPad1d, modules.py:76,95,124) or zero outside (reflect = 0);
+ * Lo = L + 2 pad - dil (taps - 1); act = 1: LeakyReLU(slope) (modules.py:75,78,108,123).
+ * x / out dtypes AVC_F32 / AVC_BF16; C % 4 == 0. */
+int avc_mg_gather(const void* x, int x_dtype, int B, int L, int C, int taps, int dil, int pad, int reflect, int act,
+                  float slope, void* out, int out_dtype, void* stream);
+/* LeakyReLU(slope) of n floats (n % 4 == 0) into out (fp32) and/or out_bf16 (either nullable). */
+int avc_mg_act(const float* x, long long n, float slope, float* out, void* out_bf16, void* stream);
+/* weight_norm (torch.nn.utils.weight_norm, dim 0: w = g v / ||v||, modules.py:18-23) folded into a
+ * GEMM B operand (N x K rows, dtype out_dtype).  stride = 0: Conv1d v [d0 = Co][d1 = Ci][K] ->
+ * out [Co][K*Ci] (tap-major, the avc_mg_gather column order).  stride = r: ConvTranspose1d
+ * v [d0 = Ci][d1 = Co][K = 2r], padding `pad` (modules.py:101-108) -> polyphase out [r*Co][3*Ci]
+ * over the zero-padded 3-tap window (j-1, j, j+1), and bias_out[p*Co + co] = bias[co].
+ * norms: d0 floats of scratch (device). */
+int avc_mg_wn_pack(const float* v, const float* g, const float* bias, int d0, int d1, int K, int stride, int pad,
+                   float* norms, void* out, int out_dtype, float* bias_out, void* stream);
+/* The generator's last layer (modules.py:122-126): LeakyReLU(slope), ReflectionPad1d(3),
+ * Conv1d(C -> 1, k 7) with w [7][C] (avc_mg_wn_pack, stride 0, fp32) and device bias[1], Tanh:
+ * out[b*L + t] = tanh(bias + sum_k,c w[k][c] act(x[b][reflect(t + k - 3)][c])). */
+int avc_mg_conv_out(const float* x, int B, int L, int C, int taps, const float* w, const float* bias, float slope,
+                    float* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -84,3 +84,39 @@ def test_converter_dispatch_matches_reference_get_trans_mel(name):
     torch.testing.assert_close(src, xs)
     torch.testing.assert_close(mt, xt)
     torch.testing.assert_close(trans, ref.squeeze(1), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_converter_get_wavs_end_to_end():
+    """evaluate.py:56-98 in one chain on the device: convert (AutoVC, padded source, other target
+    speaker), trim, vocode the frame-major converted mel with the HIP MelGAN generator; the
+    waveform equals the oracle generator on the same converted mel (fp32 compute mode), and the
+    (1, 80, T) entry of get_wavs gives the same samples."""
+    import autoformer_amd as A
+    from autoformer_amd.convert import Converter
+    from autoformer_amd.detinit import det_init_, det_inputs, det_melgan_state
+    from autoformer_amd.factory.AutoVC import AutoVC
+    from autoformer_amd.melgan import Generator, MelVocoder
+    from oracle import melgan_cpu as OM
+
+    T, freq = 64, 16
+    x, e = det_inputs(2, T, seed=23)
+    A.set_compute("fp32")
+    try:
+        m = AutoVC(44, 256, 512, freq)
+        det_init_(m)
+        g = Generator(80, 32, 3)
+        sd = {k: torch.from_numpy(v) for k, v in
+              det_melgan_state([(k, tuple(v.shape)) for k, v in g.state_dict().items()]).items()}
+        g.load_state_dict(sd)
+        conv = Converter(m.cuda().train(), T, vocoder=MelVocoder(generator=g))
+        _, _, mel = conv.get_trans_mel(x[0][: T - 6], None, e[0], e[1], isPlay=True)  # (1, T-6, 80)
+        wav = conv.get_wavs(mel)
+        wav2 = conv.get_wavs(mel.transpose(1, 2).contiguous())
+        torch.cuda.synchronize()
+        assert wav.shape == (1, (T - 6) * 256)
+        ref = OM.generator(sd, mel.transpose(1, 2).cpu()).squeeze(1)
+        assert (wav.cpu() - ref).abs().max() / ref.abs().max() < 1e-4
+        assert torch.equal(wav, wav2)
+    finally:
+        A.set_compute("bf16")
