@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip"]
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -128,6 +128,7 @@ _SIGS = {
     "avc_step_select": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_rownorm_fwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "avc_rownorm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "avc_crop_add": (c_int, [c_void_p, c_ll, c_void_p, c_int, c_int, c_void_p]),
     "avc_pad_cols": (c_int, [c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_gelu_twin": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p]),
 }

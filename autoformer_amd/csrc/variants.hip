@@ -357,6 +357,27 @@ extern "C" int avc_rownorm_bwd(const float* dy, const float* y, const float* nor
   return avc_check_launch("avc_rownorm_bwd");
 }
 
+// dst[r][c] += src[r*lds + c] for c < C (row length C): a padded product's crop accumulated into a
+// gradient in one pass
+__global__ void crop_add_kernel(const float* __restrict__ src, long long lds, float* __restrict__ dst, int R, int C) {
+  const int c0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (c0 >= C) return;
+  for (int r = blockIdx.y; r < R; r += gridDim.y) {
+    const float* s = src + (long long)r * lds;
+    float* d = dst + (long long)r * C;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c0 + k < C) d[c0 + k] += s[c0 + k];
+  }
+}
+
+extern "C" int avc_crop_add(const float* src, long long lds, float* dst, int R, int C, void* stream) {
+  AVC_CHECK_ARG(src && dst && R > 0 && C > 0 && lds >= C, "avc_crop_add: bad shape R=%d C=%d", R, C);
+  const dim3 grid((unsigned)((C + 1023) / 1024), (unsigned)std::min(R, 65535));
+  crop_add_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(src, lds, dst, R, C);
+  return avc_check_launch("avc_crop_add");
+}
+
 extern "C" int avc_pad_cols(const float* src, long long lds, void* dst, int dtype, int R, int C, int Cd,
                             void* stream) {
   AVC_CHECK_ARG(src && dst && R > 0 && C > 0 && Cd > 0 && lds >= C, "avc_pad_cols: bad shape R=%d C=%d Cd=%d", R,

@@ -659,6 +659,14 @@ def pad_cols(src, Cd, dtype=F32, C=None):
     return out
 
 
+def crop_add(src, dst, C=None):
+    """dst (R, C) += src[:, :C] (src rows may be longer): a padded product cropped into .grad."""
+    R, lds = src.shape
+    C = dst.shape[-1] if C is None else C
+    L.call("avc_crop_add", src.data_ptr(), lds, dst.data_ptr(), R, C, stream())
+    return dst
+
+
 def gelu_fwd_operand(x):
     """GELU(x) as a GEMM operand: in bf16 mode only the bf16 tensor is written (the fp32
     activation is never read by anything but GEMMs); fp32 mode: the fp32 result."""

@@ -20,6 +20,12 @@ from . import layers as Lyr
 from .kernels import operand
 
 
+def _sink(p):
+    """p.grad when the gradient sink is on (TrainStep: kernels accumulate straight into the flat
+    gradient buffer and the autograd functions return None for parameters), else None."""
+    return Lyr._grad_of(p) if Lyr.sink_on() else None
+
+
 # ------------------------------------------------------------------------------ elementwise
 class _AddFn(torch.autograd.Function):
     @staticmethod
@@ -61,13 +67,17 @@ class _GroupNormFn(torch.autograd.Function):
         C = x.shape[1]
         y, mean, rstd = K.group_norm_fwd(x, B, C, gamma, beta, eps)
         ctx.save_for_backward(x, gamma, mean, rstd)
-        ctx.B = B
+        ctx.B, ctx.beta = B, beta
         return y
 
     @staticmethod
     def backward(ctx, g):
         x, gamma, mean, rstd = ctx.saved_tensors
         C = x.shape[1]
+        if Lyr.sink_on():
+            dx = K.group_norm_bwd(g.contiguous(), x, gamma, mean, rstd, ctx.B, C, _sink(gamma), _sink(ctx.beta),
+                                  accumulate=True)
+            return dx, None, None, None, None
         dgamma = torch.empty(C, device=x.device)
         dbeta = torch.empty(C, device=x.device)
         dx = K.group_norm_bwd(g.contiguous(), x, gamma, mean, rstd, ctx.B, C, dgamma, dbeta)
@@ -104,7 +114,7 @@ class _ConvFn(torch.autograd.Function):
     def forward(ctx, x, cache, B, T_in, pad, w, b):
         Wf, _ = Lyr.conv_packs(cache, w)
         y, T_out = Lyr.conv_fwd(x, B, T_in, w, b, pad, Wf)
-        ctx.cache, ctx.args = cache, (B, T_in, T_out, pad)
+        ctx.cache, ctx.args, ctx.bias = cache, (B, T_in, T_out, pad), b
         ctx.save_for_backward(x, w)
         return y
 
@@ -113,13 +123,14 @@ class _ConvFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         B, T_in, T_out, pad = ctx.args
         dy = dy.contiguous()
-        dW = Lyr.conv_wgrad(dy, x, B, T_in, T_out, w, pad)
-        db = K.colsum(dy, B * T_out, w.shape[0])
+        sink = Lyr.sink_on()
+        dW = Lyr.conv_wgrad(dy, x, B, T_in, T_out, w, pad, into=_sink(w))
+        db = K.colsum(dy, B * T_out, w.shape[0], out=_sink(ctx.bias), accumulate=sink)
         dx = None
         if ctx.needs_input_grad[0]:
             _, Wd = Lyr.conv_packs(ctx.cache, w)
             dx = Lyr.conv_dgrad(dy, B, T_in, T_out, w, pad, Wd)
-        return dx, None, None, None, None, dW, db
+        return (dx, None, None, None, None) + ((None, None) if sink else (dW, db))
 
 
 def conv(x, conv_mod, cache, B, T_in):
@@ -134,7 +145,7 @@ class _EncEmbedFn(torch.autograd.Function):
         x = K.enc_concat(mel2d, emb, B, T)
         Wf, _ = Lyr.conv_packs(cache, w)
         y, _ = Lyr.conv_fwd(x, B, T, w, b, w.shape[-1] // 2, Wf)
-        ctx.cache, ctx.args, ctx.n_mel = cache, (B, T), mel2d.shape[1]
+        ctx.cache, ctx.args, ctx.n_mel, ctx.bias = cache, (B, T), mel2d.shape[1], b
         ctx.save_for_backward(x, w)
         return y
 
@@ -144,8 +155,11 @@ class _EncEmbedFn(torch.autograd.Function):
         B, T = ctx.args
         pad = w.shape[-1] // 2
         dy = dy.contiguous()
-        dW = Lyr.conv_wgrad(dy, x, B, T, T, w, pad)
-        db = K.colsum(dy, B * T, w.shape[0])
+        sink = Lyr.sink_on()
+        dW = Lyr.conv_wgrad(dy, x, B, T, T, w, pad, into=_sink(w))
+        db = K.colsum(dy, B * T, w.shape[0], out=_sink(ctx.bias), accumulate=sink)
+        if sink:
+            dW = db = None
         dmel = demb = None
         nm, Cin = ctx.n_mel, x.shape[1]
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
@@ -226,6 +240,22 @@ def _lin(x, M, N, Kd, w, b=None, residual=None, out=None):
     return y
 
 
+def _gelu_gemm(M, N, Kd, a, b, bias, dev, batch=1):
+    """(U, V): U = a . b^T + bias (the pre-activation the backward needs), V = GELU(U) as the next
+    GEMM's operand (bf16 only in bf16 mode).  GELU in the GEMM epilogue was measured slower
+    (DESIGN.md section 8): the per-element epilogue stalls the GEMM tail."""
+    U = torch.empty(batch * M, N, device=dev)
+    K.gemm(M, N, Kd, a, b, U, bias=bias, batch=batch, c_batch_stride=M * N)
+    return U, K.gelu_fwd_operand(U)
+
+
+def _dgelu_gemm(M, N, Kd, a, b, U, dev, batch=1):
+    """dU = (a . b^T) * GELU'(U), fp32 with its bf16 operand twin."""
+    dU = torch.empty(batch * M, N, device=dev)
+    K.gemm(M, N, Kd, a, b, dU, batch=batch, c_batch_stride=M * N)
+    return K.gelu_bwd_twin(dU, U)
+
+
 class _MLPMixerFn(torch.autograd.Function):
     """MLPMixer(image C x L (rows = channels of the frame-major input), patch ps, dim D,
     depth 1, out_dim O) -> frame-major (B*D, O)  [reference: (B, O, D)]."""
@@ -253,17 +283,14 @@ class _MLPMixerFn(torch.autograd.Function):
         Y1T = K.pad_cols(K.transpose_batched(Y1, B, NP, D).view(B * D, NP), NPp, dtype=K.compute())
         Y1 = _pad_rows(Y1, B, NP, D, NPp)
         bb1p = K.pad_cols(bb1.view(1, 4 * NP), 4 * NPp).view(-1)
-        UT = torch.empty(B * D, 4 * NPp, device=dev)
-        K.gemm(D, 4 * NPp, NPp, operand(Y1, D, kstrided=True, batch_stride=NPp * D),
-               operand(W1T, 4 * NPp, kstrided=True), UT, bias=bb1p, batch=B, c_batch_stride=D * 4 * NPp)
-        V = K.gelu_fwd_operand(UT)
+        UT, V = _gelu_gemm(D, 4 * NPp, NPp, operand(Y1, D, kstrided=True, batch_stride=NPp * D),
+                           operand(W1T, 4 * NPp, kstrided=True), bb1p, dev, batch=B)
         RT = torch.empty(B * D, NP, device=dev)
         K.gemm(D, NP, 4 * NPp, operand(V, 4 * NPp, batch_stride=D * 4 * NPp), operand(W2c, 4 * NPp), RT, bias=bb2,
                batch=B, c_batch_stride=D * NP)
         Z1 = K.transpose_batched(RT, B, D, NP, out=K.convert(Z, K.F32), accumulate=True).view(B * NP, D)
         Y2, m2, r2 = K.layer_norm_fwd(Z1, g2, b2n, mix.ln_eps[1])
-        U2 = _lin(K.twin(Y2), B * NP, 4 * D, D, w3C, bb3)
-        V2 = K.gelu_fwd_operand(U2)
+        U2, V2 = _gelu_gemm(B * NP, 4 * D, D, operand(K.twin(Y2), D), operand(w3C, D), bb3, dev)
         Z2 = _lin(V2, B * NP, D, 4 * D, w4C, bb4, residual=Z1)
         Z2T = K.transpose_batched(Z2, B, NP, D).view(B * D, NP)
         (Wf, _), wp = _out_conv_packs(mix, wc)
@@ -292,30 +319,35 @@ class _MLPMixerFn(torch.autograd.Function):
         # output conv (NP -> O, k5) over the D frames
         (_, Wd), wp = _out_conv_packs(mix, wc)
         O, NPp, Kw = wp.shape
-        dwc = Lyr.conv_wgrad(K.twin(dout), Z2T, B, D, D, wp, pad)
+        # gradient sink (TrainStep): every parameter gradient below accumulates straight into
+        # .grad (GEMM accumulate / atomics, colsum and LayerNorm accumulate, crop_add for the
+        # zero-padded products) and the function returns None for the parameters -- no autograd
+        # accumulation pass per parameter
+        sink = Lyr.sink_on()
         if NPp != NP:
-            dwc = K.pad_cols(dwc.view(O, NPp * Kw), NP * Kw).view(O, NP, Kw)
-        dbc = K.colsum(dout, B * D, wc.shape[0])
+            dwc = Lyr.conv_wgrad(K.twin(dout), Z2T, B, D, D, wp, pad)
+            dwc = (K.crop_add(dwc.view(O, NPp * Kw), _sink(wc).view(O, NP * Kw)) if sink
+                   else K.pad_cols(dwc.view(O, NPp * Kw), NP * Kw).view(O, NP, Kw))
+        else:
+            dwc = Lyr.conv_wgrad(K.twin(dout), Z2T, B, D, D, wp, pad, into=_sink(wc))
+        dbc = K.colsum(dout, B * D, wc.shape[0], out=_sink(bc), accumulate=sink)
         dZ2T = Lyr.conv_dgrad(dout, B, D, D, wp, pad, Wd, n_dx=NP)
         dZ2 = K.twin(K.transpose_batched(dZ2T, B, D, NP).view(B * NP, D))
         M = B * NP
         # channel FF: Z2 = GELU(LN2(Z1) W3^T + b3) W4^T + b4 + Z1
-        dw4 = torch.empty_like(w4)
+        dw4 = _sink(w4) if sink else torch.empty_like(w4)
         K.gemm(D, 4 * D, M, operand(dZ2, D, kstrided=True), operand(V2, 4 * D, kstrided=True), dw4,
-               split_k=K.auto_split_k(D, 4 * D, M))
-        dbb4 = K.colsum(dZ2, M, D)
-        dV2 = torch.empty(M, 4 * D, device=dev)
-        K.gemm(M, 4 * D, D, operand(dZ2, D), operand(w4C, 4 * D, kstrided=True), dV2)
-        dU2 = K.gelu_bwd_twin(dV2, U2)
-        dw3 = torch.empty_like(w3)
+               split_k=K.auto_split_k(D, 4 * D, M), accumulate=sink)
+        dbb4 = K.colsum(dZ2, M, D, out=_sink(bb4), accumulate=sink)
+        dU2 = _dgelu_gemm(M, 4 * D, D, operand(dZ2, D), operand(w4C, 4 * D, kstrided=True), U2, dev)
+        dw3 = _sink(w3) if sink else torch.empty_like(w3)
         K.gemm(4 * D, D, M, operand(dU2, 4 * D, kstrided=True), operand(Y2, D, kstrided=True), dw3,
-               split_k=K.auto_split_k(4 * D, D, M))
-        dbb3 = K.colsum(dU2, M, 4 * D)
+               split_k=K.auto_split_k(4 * D, D, M), accumulate=sink)
+        dbb3 = K.colsum(dU2, M, 4 * D, out=_sink(bb3), accumulate=sink)
         dY2 = torch.empty(M, D, device=dev)
         K.gemm(M, D, 4 * D, operand(dU2, 4 * D), operand(w3C, D, kstrided=True), dY2)
-        dg2 = torch.empty(D, device=dev)
-        db2n = torch.empty(D, device=dev)
-        dZ1 = K.add(dZ2, K.layer_norm_bwd(dY2, Z1, g2, m2, r2, dg2, db2n))
+        dg2, db2n = (_sink(g2), _sink(b2n)) if sink else (torch.empty(D, device=dev), torch.empty(D, device=dev))
+        dZ1 = K.add(dZ2, K.layer_norm_bwd(dY2, Z1, g2, m2, r2, dg2, db2n, accumulate=sink))
         # token FF: Z1 = Z + (GELU(Y1^T W1^T + b1) W2^T + b2)^T   per utterance.  dRT_b = dZ1_b^T is
         # read in place from dZ1 (as the transposed operand), so NP is never a contiguous dimension.
         W1T, W2c = _token_mix_weights(mix, w1, w2, NP)
@@ -325,38 +357,37 @@ class _MLPMixerFn(torch.autograd.Function):
         # per-utterance transposes (B*D rows) that sum is the K dimension of ONE product
         # (K = B*D, both operands K-strided), with no per-utterance slabs to reduce.
         dRT = K.transpose_batched(dZ1, B, NP, D).view(B * D, NP)
-        dbb2 = K.colsum(dRT, B * D, NP)
+        dbb2 = K.colsum(dRT, B * D, NP, out=_sink(bb2), accumulate=sink)
         dRTp = K.pad_cols(dRT, NPp, dtype=K.compute())
         dW2p = torch.empty(NPp, 4 * NPp, device=dev)
         K.gemm(NPp, 4 * NPp, B * D, operand(dRTp, NPp, kstrided=True), operand(V, 4 * NPp, kstrided=True), dW2p,
                split_k=K.auto_split_k(NPp, 4 * NPp, B * D))
-        dW2 = K.pad_cols(dW2p, 4 * NP)[:NP]
-        dV = torch.empty(B * D, 4 * NPp, device=dev)
-        K.gemm(D, 4 * NPp, NPp, operand(dZ1p, D, kstrided=True, batch_stride=NPp * D),
-               operand(W2c, 4 * NPp, kstrided=True), dV, batch=B, c_batch_stride=D * 4 * NPp)
-        dUT = K.gelu_bwd_twin(dV, UT)
+        dW2 = K.crop_add(dW2p[:NP], _sink(w2).view(NP, 4 * NP)) if sink else K.pad_cols(dW2p, 4 * NP)[:NP]
+        dUT = _dgelu_gemm(D, 4 * NPp, NPp, operand(dZ1p, D, kstrided=True, batch_stride=NPp * D),
+                          operand(W2c, 4 * NPp, kstrided=True), UT, dev, batch=B)
         dW1p = torch.empty(4 * NPp, NPp, device=dev)
         K.gemm(4 * NPp, NPp, B * D, operand(dUT, 4 * NPp, kstrided=True), operand(Y1T, NPp, kstrided=True), dW1p,
                split_k=K.auto_split_k(4 * NPp, NPp, B * D))
-        dW1 = K.pad_cols(dW1p, NP)[:4 * NP]
-        dbb1 = K.colsum(dUT, B * D, 4 * NP, ld=4 * NPp)
+        dW1 = K.crop_add(dW1p[:4 * NP], _sink(w1).view(4 * NP, NP)) if sink else K.pad_cols(dW1p, NP)[:4 * NP]
+        dbb1 = K.colsum(dUT, B * D, 4 * NP, ld=4 * NPp, out=_sink(bb1), accumulate=sink)
         dY1T = torch.empty(B * D, NP, device=dev)
         K.gemm(B * D, NP, 4 * NPp, operand(dUT, 4 * NPp), operand(W1T, 4 * NPp), dY1T)
         dY1 = K.transpose_batched(dY1T, B, D, NP).view(M, D)
-        dg1 = torch.empty(D, device=dev)
-        db1n = torch.empty(D, device=dev)
-        dZ = K.twin(K.add(dZ1, K.layer_norm_bwd(dY1, Z, g1, m1, r1, dg1, db1n)))
+        dg1, db1n = (_sink(g1), _sink(b1n)) if sink else (torch.empty(D, device=dev), torch.empty(D, device=dev))
+        dZ = K.twin(K.add(dZ1, K.layer_norm_bwd(dY1, Z, g1, m1, r1, dg1, db1n, accumulate=sink)))
         # patch embedding
         pp = ps * ps
-        dwe = torch.empty_like(we)
+        dwe = _sink(we) if sink else torch.empty_like(we)
         K.gemm(D, pp, M, operand(dZ, D, kstrided=True), operand(P, pp, kstrided=True), dwe,
-               split_k=K.auto_split_k(D, pp, M))
-        dbe = K.colsum(dZ, M, D)
+               split_k=K.auto_split_k(D, pp, M), accumulate=sink)
+        dbe = K.colsum(dZ, M, D, out=_sink(be), accumulate=sink)
         dnf = None
         if ctx.needs_input_grad[0]:
             dP = torch.empty(M, pp, device=dev)
             K.gemm(M, pp, D, operand(dZ, D), operand(weC, pp, kstrided=True), dP)
             dnf = K.patchify(dP, B, Lf, C, ps, backward=True)
+        if sink:
+            return (dnf, None, None, None) + (None,) * 16
         return (dnf, None, None, None, dwe, dbe, dg1, db1n, dW1.view_as(w1), dbb1, dW2.view_as(w2), dbb2, dg2, db2n,
                 dw3, dbb3, dw4, dbb4, dwc, dbc)
 

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 8
+#define AVC_ABI_VERSION 9
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -331,6 +331,9 @@ int avc_rownorm_bwd(const float* dy, const float* y, const float* norms, int R, 
  * Cd: pads the MLP-Mixer output convolution's NP channels (1849 / 121 patches) to a multiple
  * of 8 for the bf16 LDS-DMA kernels (MLPMixer.py:88-90) and crops its gradients back. */
 int avc_pad_cols(const float* src, long long lds, void* dst, int dtype, int R, int C, int Cd, void* stream);
+/* dst[r][c] += src[r*lds + c], c < C (dst rows C apart): the zero-padded token-mixing weight
+ * gradients (MLPMixer.py:79-80, NP padded to a multiple of 8) cropped into .grad in one pass. */
+int avc_crop_add(const float* src, long long lds, float* dst, int R, int C, void* stream);
 /* GELU forward (bwd = 0: y = gelu(x)) or backward (bwd = 1: y = g * gelu'(x)) with the
  * fp32 result and/or its bf16 GEMM-operand twin from one pass (y or y16 may be null):
  * the MLP-Mixer hidden activations (MLPMixer.py:9-14) feed only GEMMs and bias sums. */
