@@ -20,6 +20,7 @@
 //    grid-wide sync (cheaper on gfx950 than a software grid barrier at 256 workgroups,
 //    MI355X_MICROARCH.md rows "boundary" vs "barrier-xcd"); the host loop is
 //    graph-capturable.
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <mutex>
@@ -1244,6 +1245,369 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
   }
 }
 
+// Backward with the NARROW side handed over (partial-sum exchange).  The recurrent product
+// dh_rec[b][j] = sum_q dG_{t+1}[b][q] W_hh[q][j] contracts over the 4H gate rows, and member r
+// already holds 128 of them (its own dG columns: 4 gates x 32 units).  So instead of gathering
+// the group's whole dG_{t+1} (8 x 4H bf16 = 64 KB per consumer per step at H = 1024) before a
+// K = 4H product, each member multiplies its OWN dG tile (in LDS, no wait) by
+// W_hh[own 128 rows][all H columns] and publishes the fp32 partial dh (8 x H); consumer r then
+// reads, from each of the H/32 producers, only the 8 x 32 block of its own units (1 KB) and sums
+// them: 32 KB per consumer per step at H = 1024, half the bytes, and the product's LDS operand
+// is the 8 x 128 own tile (4 KB per wave) instead of the group tile (16 KB per wave).
+//   product:   wave w owns dh columns [w*H/8, (w+1)*H/8) as H/128 16-row MFMA tiles (A = W_hh^T
+//              rows in VGPRs for the whole sequence, K = the 4 gate k-blocks of the member's
+//              units); B = the dG tile (utterances as the 16 columns, 8 valid); each lane ends
+//              with 4 consecutive dh columns of one utterance = one 16-B sc1 store.
+//   partials:  fp32 [2 parities][NG][NR producers][NR consumers][8][32] (1 KB blocks).
+//   hand-off:  every wave drains its stores, workgroup barrier, wave 0 raises the member's
+//              flag (write-through form as above); consumers poll the group's flags with
+//              wave 0, then wave w sums producers w, w+8, ... with 16-B sc1 loads and the eight
+//              waves' sums meet in LDS.
+// The parity argument of the forward holds unchanged (a member publishes step s+2 into the
+// slot of step s only after every member published step s+1, i.e. consumed step s).
+constexpr size_t ps_bytes(int ng, int H) { return (size_t)2 * ng * (H / PJU) * (H / PJU) * PRG * PJU * 4; }
+
+template <int H>
+__global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd_ps(PersistBwdArgs a) {
+  constexpr int G = 4 * H, NR = H / PJU, NT = H / 128, NPW = NR / 8, DP = 4 * PJU + 8, CW = H / 8;
+  static_assert(NR % 8 == 0 && PRG * PJU == 256 && PNT == 512, "partial-sum layout");
+  __shared__ __attribute__((aligned(16))) bf16 ds16[(PRG + 1) * DP];  // dG_t tile, row PRG = zeros
+  __shared__ __attribute__((aligned(16))) float red[8 * PRG * PJU];   // per-wave producer sums
+  __shared__ float outs[4 * PRG * PJU];                               // dG of the step (HBM copy)
+  __shared__ int quit;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
+  const int j0 = r * PJU, b0 = g * PRG;
+  const int T = a.T, B = a.B, rows = min(PRG, B - b0);
+  const __amdgpu_buffer_rsrc_t prs = rsrc_of(a.pay, (long long)ps_bytes(a.ng, H));
+  unsigned* flags = a.ctl + 4 + g * PFL;
+
+  // A fragments: W_hh^T[j][q*H + j0 + 8*(lane>>4) .. +8], j = w*CW + 16m + (lane & 15)
+  bf16x8 wf[NT][4];
+#pragma unroll
+  for (int m = 0; m < NT; ++m) {
+    const bf16* row = a.wt + (long long)(w * CW + 16 * m + (lane & 15)) * G + j0 + 8 * (lane >> 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wf[m][q] = *reinterpret_cast<const bf16x8*>(row + q * H);
+  }
+  for (int i = tid; i < (PRG + 1) * DP / 2; i += PNT) reinterpret_cast<unsigned*>(ds16)[i] = 0u;
+  if (tid == 0) quit = 0;
+  const int pr = (tid >> 5) & (PRG - 1), pu = tid & 31, pb = b0 + pr, pj = j0 + pu;
+  const bool pv = tid < PRG * PJU && pb < B;
+  const int bcol = lane & 15, brow = bcol < PRG ? bcol : PRG;  // B operand: utterance columns
+  // float offset of this member's outgoing partial block for consumer rd, utterance bcol
+  const long long pbase = ((long long)g * NR + r) * NR * (PRG * PJU);
+  const long long pslot = (long long)a.ng * NR * NR * (PRG * PJU);
+  float dc = 0.f;
+  __syncthreads();
+
+  for (int s = 0; s < T; ++s) {
+    const int t = T - 1 - s;
+    stamp(a.trace, T, s, 0);
+    float dh = 0.f, ct = 0.f, cp = 0.f, gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f;
+    if (pv) {
+      const long long oh = ((long long)pb * T + t) * H + pj;
+      dh = a.dhout[oh];
+      ct = a.call[oh];
+      cp = t > 0 ? a.call[oh - H] : 0.f;
+      const float* gp = a.gall + ((long long)pb * T + t) * G + pj;
+      gi = gp[0];
+      gf = gp[H];
+      gg = gp[2 * H];
+      go = gp[3 * H];
+    }
+    if (s > 0) {
+      if (w == 0 && !poll_flags(flags, NR, (unsigned)s, a.ctl, a.fault, a.spin)) quit = 1;
+      __syncthreads();
+      if (quit) return;  // block-uniform exit after a spin timeout
+      // wave w: producers w, w + 8, ...; lane = one 16-B chunk of the 8 x 32 block
+      const long long src = ((s - 1) & 1) * pslot + ((long long)g * NR * NR + r) * (PRG * PJU) + 4 * lane;
+      f32x4 v[NPW];
+#pragma unroll
+      for (int i = 0; i < NPW; ++i)
+        v[i] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)((src + (long long)(w + 8 * i) * NR * (PRG * PJU)) * 4),
+                                                         0, AUX_SC1));
+      f32x4 sum = v[0];
+#pragma unroll
+      for (int i = 1; i < NPW; ++i) sum += v[i];
+      *reinterpret_cast<f32x4*>(red + w * (PRG * PJU) + 4 * lane) = sum;
+      __syncthreads();
+      stamp(a.trace, T, s, 1);
+      if (pv) {
+#pragma unroll
+        for (int ww = 0; ww < 8; ++ww) dh += red[ww * (PRG * PJU) + pr * PJU + pu];
+      }
+    }
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+    if (pv) {
+      const float tc = ftanh(ct);
+      const float dcs = dc + dh * go * (1.f - tc * tc);
+      v0 = dcs * gg * gi * (1.f - gi);  // d(pre i)
+      v1 = dcs * cp * gf * (1.f - gf);  // d(pre f)
+      v2 = dcs * gi * (1.f - gg * gg);  // d(pre g)
+      v3 = dh * tc * go * (1.f - go);   // d(pre o)
+      dc = dcs * gf;
+    }
+    if (tid < PRG * PJU) {
+      bf16* dsr = ds16 + pr * DP + pu;
+      dsr[0] = (bf16)v0;
+      dsr[PJU] = (bf16)v1;
+      dsr[2 * PJU] = (bf16)v2;
+      dsr[3 * PJU] = (bf16)v3;
+      float* o = outs + tid;
+      o[0] = v0;
+      o[PRG * PJU] = v1;
+      o[2 * PRG * PJU] = v2;
+      o[3 * PRG * PJU] = v3;
+    }
+    __syncthreads();
+    stamp(a.trace, T, s, 2);
+    if (s + 1 < T) {
+      // ---- partial dh of the next step from the own dG tile, published to every consumer
+      bf16x8 bfr[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bfr[q] = *reinterpret_cast<const bf16x8*>(ds16 + brow * DP + q * PJU + 8 * (lane >> 4));
+      f32x4 acc[NT];
+#pragma unroll
+      for (int m = 0; m < NT; ++m) {
+        acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[m][q], bfr[q], acc[m], 0, 0, 0);
+      }
+      if (bcol < rows) {
+        const long long dst = (s & 1) * pslot + pbase + bcol * PJU;
+#pragma unroll
+        for (int m = 0; m < NT; ++m) {
+          const int jj = w * CW + 16 * m + 4 * (lane >> 4);  // 4 consecutive dh columns
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[m]), prs,
+                                                 (int)((dst + (long long)(jj >> 5) * (PRG * PJU) + (jj & 31)) * 4), 0,
+                                                 AUX_SC1);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (w == 0) raise_flag(flags, r, (unsigned)(s + 1));
+    }
+    // ---- dG of the step to HBM (after the hand-off: its stores never delay the drain)
+    if (w >= 4) {
+      const int cell = tid - PRG * PJU, ob = b0 + (cell >> 5), oj = j0 + (cell & 31);
+      if (ob < B) {
+        const float* o = outs + cell;
+        const long long og = ((long long)ob * T + t) * G + oj;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a.dg[og + q * H] = o[q * PRG * PJU];
+        if (a.dg16) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) a.dg16[og + q * H] = (bf16)o[q * PRG * PJU];
+        }
+      }
+    }
+    stamp(a.trace, T, s, 3);
+  }
+}
+
+// =============================================================== two stacked layers, one launch
+// Decoder lstm2 (nn.LSTM(512 -> 1024, num_layers=2), AutoVC.py:96,110) forward as a layer
+// WAVEFRONT: tick k runs layer 0 at step k and layer 1 at step k - 1, so both layers share one
+// hand-off per tick -- T + 1 hand-offs instead of 2T -- and layer 1's input projection
+// h0_t W_ih1^T happens inside the recurrence (no separate 8192 x 4096 x 1024 GEMM).
+// Register budget forces the shape: three H x 4H bf16 matrices (W_hh0, W_ih1, W_hh1) live in
+// VGPRs, replicated once per utterance group, so groups are 16 utterances (a full MFMA tile, no
+// padding rows: ceil(B/16) groups x H/16 members = 256 workgroups at B = 64, H = 1024) and a
+// member owns 16 hidden units of EACH layer: 3 x 64 gate columns x H = 192 VGPRs per thread.
+// Per tick every member needs the group's h0_{k-1} and h1_{k-2} (16 x H bf16 each) in LDS;
+// wave w = (gate pair w & 1, K quarter w >> 1) multiplies each A fragment it reads against six
+// weight fragments (P0 = h0 W_hh0^T, P1 = h0 W_ih1^T + h1 W_hh1^T for its two gates), so every
+// A element is read from LDS once per tick; the four K quarters meet in LDS.  Thread tid is
+// the cell (layer tid >> 8, utterance (tid >> 4) & 15, unit tid & 15).  Hand-off: the
+// write-through flag form above, one flag per member per tick covering both layers' tiles.
+struct Persist2Args {
+  const float* xproj;  // (B,T,4H) layer-0 input projection incl. b_ih0 + b_hh0
+  const bf16* w0;      // W_hh0 [4H][H]
+  const bf16* wi1;     // W_ih1 [4H][H]
+  const bf16* w1;      // W_hh1 [4H][H]
+  const float* bias1;  // b_ih1 + b_hh1 (4H)
+  float* hout[2];
+  bf16* hout16[2];
+  float* call[2];
+  float* gall[2];
+  unsigned* ctl;
+  bf16* pay;  // [layer][2 parities][B][H]
+  unsigned long long* trace;
+  unsigned* fault;
+  unsigned spin;
+  int B, T, ng;
+};
+
+constexpr int QRG = 16, QJU = 16;  // utterances per group, units per member and layer
+constexpr int NLW = 2;             // W_hh1 fragments per wave kept in LDS instead of VGPRs
+
+template <int H>
+constexpr size_t persist2_lds() {
+  return (size_t)2 * QRG * (H + 8) * 2 + (size_t)4 * 2 * 4 * QRG * QJU * 4 + (size_t)2 * QRG * QJU * 2 +
+         (size_t)8 * NLW * 64 * 16 + 16;
+}
+
+template <int H>
+__global__ void __launch_bounds__(PNT, 1) lstm2_persist_fwd(Persist2Args a) {
+  constexpr int G = 4 * H, AP = H + 8, NR = H / QJU, NKQ = H / 128;  // k-blocks per K quarter
+  constexpr int NCH = 2 * QRG * H / 8 / PNT;                          // 16-B chunks per thread
+  static_assert(NCH * PNT * 8 == 2 * QRG * H && NR <= 64, "two-layer tiling");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16* As = reinterpret_cast<bf16*>(smem_raw);                          // [2 layers][16][AP]
+  float* red = reinterpret_cast<float*>(smem_raw + 2 * QRG * AP * 2);    // [kq][L][q][16][16]
+  bf16* hs16 = reinterpret_cast<bf16*>(red + 4 * 2 * 4 * QRG * QJU);     // [L][16][16] publish tile
+  int* quit = reinterpret_cast<int*>(reinterpret_cast<char*>(hs16 + 2 * QRG * QJU) + (size_t)8 * NLW * 64 * 16);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, gp = w & 1, kq = w >> 1;
+  const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
+  const int j0 = r * QJU, b0 = g * QRG;
+  const int T = a.T, B = a.B, rows = min(QRG, B - b0);
+  const __amdgpu_buffer_rsrc_t pay = rsrc_of(a.pay, (long long)4 * B * H * 2);
+  unsigned* flags = a.ctl + 4 + g * PFL;
+
+  // weight fragments (B operand): gate q = 2gp + i, unit j0 + (lane & 15), k-block kq*NKQ + k.
+  // The last NLW W_hh1 fragments of gate 2gp+1 live in LDS (wl, per wave and lane): with all 48
+  // in VGPRs the compiler spilled two to scratch and waited on their reload every tick.
+  bf16x8 f0[2][NKQ], fi[2][NKQ], f1a[NKQ], f1b[NKQ - NLW];  // W_hh1: gate 2gp (a), 2gp + 1 (b)
+  bf16x8* wl = reinterpret_cast<bf16x8*>(hs16 + 2 * QRG * QJU) + (w * NLW) * 64 + lane;  // [w][NLW][64]
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long long ro = (long long)((2 * gp + i) * H + j0 + (lane & 15)) * H + kq * NKQ * 32 + 8 * (lane >> 4);
+#pragma unroll
+    for (int k = 0; k < NKQ; ++k) {
+      f0[i][k] = *reinterpret_cast<const bf16x8*>(a.w0 + ro + 32 * k);
+      fi[i][k] = *reinterpret_cast<const bf16x8*>(a.wi1 + ro + 32 * k);
+      const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(a.w1 + ro + 32 * k);
+      if (i == 0) f1a[k] = v1;
+      else if (k < NKQ - NLW) f1b[k < NKQ - NLW ? k : 0] = v1;
+      else wl[(k - (NKQ - NLW)) * 64] = v1;
+    }
+  }
+  for (int i = tid; i < 2 * QRG * AP / 2; i += PNT) reinterpret_cast<unsigned*>(As)[i] = 0u;
+  if (tid == 0) *quit = 0;
+  // cell of this thread
+  const int L = tid >> 8, cr = (tid >> 4) & 15, cu = tid & 15, cb = b0 + cr, cj = j0 + cu;
+  const bool cv = cb < B;
+  float c = 0.f;
+  __syncthreads();
+
+  for (int k = 0; k <= T; ++k) {
+    const int t = L == 0 ? k : k - 1;  // this thread's step
+    const bool act = L == 0 ? k < T : k >= 1;
+    if (k < T) stamp(a.trace, T, k, 0);
+    // gate inputs besides the recurrent products: layer 0 the x projection of its step (loaded
+    // ahead of the exchange), layer 1 its bias (L1-resident re-loads)
+    float px[4] = {0.f, 0.f, 0.f, 0.f};
+    if (act && cv) {
+      const float* xp = L == 0 ? a.xproj + ((long long)cb * T + t) * G + cj : a.bias1 + cj;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) px[q] = xp[q * H];
+    }
+    f32x4 p0[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x4 p1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    if (k > 0) {
+      if (w == 0 && !poll_flags(flags, NR, (unsigned)k, a.ctl, a.fault, a.spin)) *quit = 1;
+      __syncthreads();
+      if (*quit) return;  // block-uniform exit after a spin timeout
+      // h0_{k-1} -> As[0], h1_{k-2} -> As[1] (k >= 2); rows past the batch stay zero
+      // (two halves of NCH / 2 chunks in flight: the weight fragments leave few registers)
+      const int slot = (k - 1) & 1;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        u32x4_t v[NCH / 2];
+#pragma unroll
+        for (int i = 0; i < NCH / 2; ++i) {
+          const int ch = tid + PNT * (hf * NCH / 2 + i), l = ch / (QRG * H / 8), rem = ch - l * (QRG * H / 8),
+                    row = rem / (H / 8), col = rem - row * (H / 8);
+          v[i] = row < rows && (l == 0 || k >= 2)
+                     ? __builtin_amdgcn_raw_buffer_load_b128(pay, (((l * 2 + slot) * B + b0 + row) * H + col * 8) * 2,
+                                                             0, AUX_SC1)
+                     : u32x4_t{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int i = 0; i < NCH / 2; ++i) {
+          const int ch = tid + PNT * (hf * NCH / 2 + i), l = ch / (QRG * H / 8), rem = ch - l * (QRG * H / 8),
+                    row = rem / (H / 8), col = rem - row * (H / 8);
+          *reinterpret_cast<u32x4_t*>(As + (l * QRG + row) * AP + col * 8) = v[i];
+        }
+      }
+      __syncthreads();
+      if (k < T) stamp(a.trace, T, k, 1);
+      const bf16* a0p = As + (lane & 15) * AP + kq * NKQ * 32 + 8 * (lane >> 4);
+      const bf16* a1p = a0p + QRG * AP;
+#pragma unroll
+      for (int kk = 0; kk < NKQ; ++kk) {
+        const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(a0p + 32 * kk);
+        const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(a1p + 32 * kk);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          p0[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, f0[i][kk], p0[i], 0, 0, 0);
+          p1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, fi[i][kk], p1[i], 0, 0, 0);
+          const bf16x8 wb = i == 0                ? f1a[kk]
+                            : kk < NKQ - NLW      ? f1b[kk < NKQ - NLW ? kk : 0]
+                                                  : wl[(kk - (NKQ - NLW)) * 64];
+          p1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, wb, p1[i], 0, 0, 0);
+        }
+        // keep at most two k-blocks of A fragments in flight (the weights hold 192 VGPRs)
+        if (kk % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // K-quarter partials -> LDS: red[((kq * 2 + L) * 4 + q) * 256 + row * 16 + unit]
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float* d0 = red + ((kq * 2 + 0) * 4 + 2 * gp + i) * (QRG * QJU) + (lane & 15);
+      float* d1 = red + ((kq * 2 + 1) * 4 + 2 * gp + i) * (QRG * QJU) + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        d0[(4 * (lane >> 4) + e) * QJU] = p0[i][e];
+        d1[(4 * (lane >> 4) + e) * QJU] = p1[i][e];
+      }
+    }
+    __syncthreads();
+    if (k < T) stamp(a.trace, T, k, 2);
+    float pre[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float s = px[q];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) s += red[((kk * 2 + L) * 4 + q) * (QRG * QJU) + cr * QJU + cu];
+      pre[q] = s;
+    }
+    const float ig = fsig(pre[0]), fg = fsig(pre[1]), gg = ftanh(pre[2]), og = fsig(pre[3]);
+    float h = 0.f;
+    if (act) {
+      c = fg * c + ig * gg;
+      h = og * ftanh(c);
+    }
+    hs16[(L * QRG + cr) * QJU + cu] = (bf16)h;
+    __syncthreads();
+    // ---- publish h0_k and h1_{k-1} (wave 0: lanes 0..31 layer 0, 32..63 layer 1; 16 B each),
+    // needed by tick k + 1 (none after tick T - 1); the other waves store their outputs meanwhile
+    if (w == 0 && k < T) {
+      const int l = lane >> 5, row = (lane >> 1) & 15, half = lane & 1;
+      if (row < rows) {
+        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(hs16 + (l * QRG + row) * QJU + half * 8);
+        __builtin_amdgcn_raw_buffer_store_b128(v, pay, (((l * 2 + (k & 1)) * B + b0 + row) * H + j0 + half * 8) * 2, 0,
+                                               AUX_SC1);
+      }
+      raise_flag(flags, r, (unsigned)(k + 1));
+    }
+    if (act && cv) {
+      const long long oh = ((long long)cb * T + t) * H + cj;
+      a.hout[L][oh] = h;
+      a.hout16[L][oh] = (bf16)h;
+      a.call[L][oh] = c;
+      float* gpo = a.gall[L] + ((long long)cb * T + t) * G + cj;
+      gpo[0] = ig;
+      gpo[H] = fg;
+      gpo[2 * H] = gg;
+      gpo[3 * H] = og;
+    }
+    if (k < T) stamp(a.trace, T, k, 3);
+  }
+}
+
 template <int H>
 constexpr size_t persist_bwd_lds() {
   return (size_t)(PRG + 1) * (4 * H + 8) * 2 + (size_t)(PNT / 64) * PRG * (PJU + 1) * 4 + (size_t)PRG * 4 * PJU * 2 +
@@ -1319,8 +1683,18 @@ int nap() {
   return v;
 }
 
+// Backward form: partial-sum exchange (lstm_persist_bwd_ps, default) or the dG gather
+// (lstm_persist_bwd); AVC_LSTM_BWD_PS=0 selects the gather form.
+std::atomic<int> g_bwd_form{-1};  // avc_lstm_set_bwd_form; -1 = environment / default
+bool ps_bwd() {
+  static const bool env = getenv("AVC_LSTM_BWD_PS") && atoi(getenv("AVC_LSTM_BWD_PS")) == 1;
+  const int f = g_bwd_form.load(std::memory_order_relaxed);
+  return f < 0 ? env : f == 1;
+}
+
 template <int H>
 const void* persist_fn(bool bwd) {
+  if (bwd && ps_bwd()) return reinterpret_cast<const void*>(&lstm_persist_bwd_ps<H>);
   if (bwd) {
     if (gran(true, H)) {
       set_bwd_lds_attr<H, true>();
@@ -1374,7 +1748,7 @@ bool persistent_path(int B, int H, int dirs, bool bf, bool bwd) {
   const int ng = (B + PRG - 1) / PRG, grid = ng * (H / PJU);
   if (grid > num_cus()) return false;
   const void* fn = H == 1024 ? persist_fn<1024>(bwd) : H == 768 ? persist_fn<768>(bwd) : persist_fn<512>(bwd);
-  const size_t lds = !bwd ? 0
+  const size_t lds = !bwd || ps_bwd() ? 0
                      : H == 1024 ? persist_bwd_lds<1024>()
                      : H == 768  ? persist_bwd_lds<768>()
                                  : persist_bwd_lds<512>();
@@ -1383,7 +1757,8 @@ bool persistent_path(int B, int H, int dirs, bool bf, bool bwd) {
 
 template <int H>
 void launch_persist_bwd(dim3 grid, hipStream_t s, bool gr, const PersistBwdArgs& p) {
-  if (gr) lstm_persist_bwd<H, true><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
+  if (ps_bwd()) lstm_persist_bwd_ps<H><<<grid, PNT, 0, s>>>(p);
+  else if (gr) lstm_persist_bwd<H, true><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
   else lstm_persist_bwd<H, false><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
 }
 
@@ -1419,6 +1794,82 @@ extern "C" int avc_set_fault_word(void* word) {
 extern "C" int avc_lstm_set_spin(unsigned spins) {
   g_spin.store(spins, std::memory_order_relaxed);
   return 0;
+}
+
+// Two-layer wavefront forward (lstm2_persist_fwd): shape, compute mode and residency.
+bool persist2_path(int B, int H, int In1, bool bf) {
+  if (!bf || H != 1024 || In1 != H || no_persist_env() || getenv("AVC_LSTM2_OFF")) return false;
+  const int ng = (B + QRG - 1) / QRG, grid = ng * (H / QJU);
+  if (grid > num_cus()) return false;
+  static std::once_flag once[MAXDEV];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::call_once(once[dev & (MAXDEV - 1)], [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm2_persist_fwd<1024>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist2_lds<1024>());
+  });
+  return fits_resident(reinterpret_cast<const void*>(&lstm2_persist_fwd<1024>), PNT, persist2_lds<1024>(), grid);
+}
+
+extern "C" int avc_lstm2_persistent(int B, int H, int in1, int compute) {
+  return persist2_path(B, H, in1, compute == AVC_BF16) ? 1 : 0;
+}
+
+extern "C" size_t avc_lstm2_scratch_bytes(int B, int H) {
+  if (B <= 0 || H <= 0) return 0;
+  return px_payload_off((B + QRG - 1) / QRG) + (size_t)8 * B * H;
+}
+
+extern "C" int avc_lstm2_fwd(const float* xproj0, const void* w_hh0, const void* w_ih1, const void* w_hh1,
+                             const float* bias1, int B, int T, int H, float* h0, void* h0_bf16, float* c0,
+                             float* gates0, float* h1, void* h1_bf16, float* c1, float* gates1, void* buf,
+                             void* stream) {
+  AVC_CHECK_ARG(xproj0 && w_hh0 && w_ih1 && w_hh1 && bias1 && h0 && h0_bf16 && c0 && gates0 && h1 && h1_bf16 && c1 &&
+                    gates1 && buf && B > 0 && T > 0,
+                "avc_lstm2_fwd: bad args");
+  AVC_CHECK_ARG(persist2_path(B, H, H, true), "avc_lstm2_fwd: shape B=%d H=%d not supported (see avc_lstm2_persistent)",
+                B, H);
+  hipStream_t s = as_stream(stream);
+  const int ng = (B + QRG - 1) / QRG;
+  Persist2Args p;
+  p.xproj = xproj0;
+  p.w0 = reinterpret_cast<const bf16*>(w_hh0);
+  p.wi1 = reinterpret_cast<const bf16*>(w_ih1);
+  p.w1 = reinterpret_cast<const bf16*>(w_hh1);
+  p.bias1 = bias1;
+  p.hout[0] = h0;
+  p.hout[1] = h1;
+  p.hout16[0] = reinterpret_cast<bf16*>(h0_bf16);
+  p.hout16[1] = reinterpret_cast<bf16*>(h1_bf16);
+  p.call[0] = c0;
+  p.call[1] = c1;
+  p.gall[0] = gates0;
+  p.gall[1] = gates1;
+  p.ctl = reinterpret_cast<unsigned*>(buf);
+  p.pay = reinterpret_cast<bf16*>(reinterpret_cast<char*>(buf) + px_payload_off(ng));
+  p.trace = g_trace;
+  p.fault = fault_word();
+  p.spin = spin_bound();
+  p.B = B;
+  p.T = T;
+  p.ng = ng;
+  (void)hipMemsetAsync(buf, 0, px_ctl_bytes(ng), s);
+  lstm2_persist_fwd<1024><<<dim3(ng * (H / QJU)), PNT, persist2_lds<1024>(), s>>>(p);
+  return avc_check_launch("avc_lstm2_fwd");
+}
+
+extern "C" int avc_lstm_set_bwd_form(int form) {
+  AVC_CHECK_ARG(form >= -1 && form <= 1, "avc_lstm_set_bwd_form: form must be -1, 0 or 1");
+  g_bwd_form.store(form, std::memory_order_relaxed);
+  return 0;
+}
+
+extern "C" size_t avc_lstm_bwd_scratch_bytes(int B, int H, int dirs) {
+  if (B <= 0 || H <= 0 || dirs <= 0) return 0;
+  const int ng = (B + PRG - 1) / PRG;
+  size_t n = std::max((size_t)16 * dirs * B * H, (size_t)32 * B * H + 8192);
+  if (H % PJU == 0) n = std::max(n, px_payload_off(ng) + ps_bytes(ng, H));
+  return n;
 }
 
 extern "C" int avc_lstm_persistent(int B, int H, int dirs, int compute, int backward) {
@@ -1549,7 +2000,7 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
     p.B = B;
     p.T = T;
     p.ng = ng;
-    const bool gr = gran(true, H);
+    const bool gr = gran(true, H) && !ps_bwd();
     (void)hipMemsetAsync(gbuf, 0, gr ? px_payload_off(ng) + (size_t)32 * B * H : px_ctl_bytes(ng), s);
     // (persistent_path above set the dynamic-LDS attributes)
     const dim3 grid(ng * (H / PJU));

@@ -321,6 +321,28 @@ def lstm_fwd(xproj, w_hh, B, T, H, dirs, hbuf=None):
     return attach_twin(h, h16), c, g
 
 
+def lstm2_persistent(B, H, in1):
+    """Whether avc_lstm2_fwd (two stacked layers, one wavefront launch) applies to this shape."""
+    return bool(L.lib().avc_lstm2_persistent(int(B), int(H), int(in1), _COMPUTE))
+
+
+def lstm2_fwd(xproj0, w_hh0, w_ih1, w_hh1, bias1, B, T, H):
+    """Forward of two stacked unidirectional layers in one persistent launch (layer wavefront).
+    Returns (h0, c0, gates0, h1, c1, gates1); h0/h1 carry their bf16 twins."""
+    dev = xproj0.device
+    fault_word(dev)
+    outs = []
+    for _ in range(2):
+        outs += [torch.empty(B * T, H, device=dev), torch.empty(B * T, H, device=dev, dtype=torch.bfloat16),
+                 torch.empty(B * T, H, device=dev), torch.empty(B * T, 4 * H, device=dev)]
+    buf = torch.empty(int(L.lib().avc_lstm2_scratch_bytes(int(B), int(H))), device=dev, dtype=torch.uint8)
+    L.call("avc_lstm2_fwd", xproj0.data_ptr(), w_hh0.data_ptr(), w_ih1.data_ptr(), w_hh1.data_ptr(),
+           bias1.data_ptr(), B, T, H, *[o.data_ptr() for o in outs], buf.data_ptr(), stream())
+    h0, h0b, c0, g0, h1, h1b, c1, g1 = outs
+    _CACHE["lstm2_buf"] = buf  # diagnostics (timeout flag at byte 0); kept alive until the next call
+    return attach_twin(h0, h0b), c0, g0, attach_twin(h1, h1b), c1, g1
+
+
 def lstm_persistent_bwd(B, H, dirs):
     """Whether avc_lstm_bwd takes the one-launch persistent path (asked of lstm.hip)."""
     return bool(L.lib().avc_lstm_persistent(int(B), int(H), int(dirs), _COMPUTE, 1))
@@ -336,8 +358,13 @@ _CACHE = {}
 
 
 def lstm_bwd_scratch(B, H, dirs, device):
-    nbytes = max(16 * dirs * B * H, 32 * B * H + 8192)  # granule form: [2][B][4H/2] x 8 B + control
+    nbytes = int(L.lib().avc_lstm_bwd_scratch_bytes(int(B), int(H), int(dirs)))
     return torch.empty((nbytes + 1) // 2, device=device, dtype=torch.bfloat16)
+
+
+def lstm_set_bwd_form(form: int) -> None:
+    """Debug / A-B: persistent backward form (1 partial-sum exchange, 0 dG gather, -1 default)."""
+    L.call("avc_lstm_set_bwd_form", int(form))
 
 
 def lstm_bwd_timeout_flag(gbuf, B, H):

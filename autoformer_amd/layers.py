@@ -621,7 +621,52 @@ class _LSTMLayerFn(torch.autograd.Function):
         return (dx, None, None, None, *grads)
 
 
+def _pair_ok(cores, x, B):
+    """Two stacked unidirectional layers that the one-launch wavefront kernel takes."""
+    if len(cores) != 2 or _PAIR_OFF or K.compute() != K.BF16:
+        return False
+    c0, c1 = cores
+    return (c0.dirs == 1 and c1.dirs == 1 and c0.H == c1.H and x.is_cuda
+            and K.lstm2_persistent(B, c0.H, c1.params()[0].shape[1]))
+
+
+class _LSTMPairFn(torch.autograd.Function):
+    """Two stacked layers of one nn.LSTM (decoder lstm2, AutoVC.py:96,110): forward as ONE
+    wavefront launch (avc_lstm2_fwd; layer 1's input projection inside the recurrence), backward
+    layer by layer exactly as two _LSTMLayerFn nodes would run it."""
+
+    @staticmethod
+    def forward(ctx, x, c0, c1, B, T, *params):
+        H = c0.H
+        In = x.shape[1]
+        wih0, bsum0, whh0, _, _ = c0.packs()
+        wih1, bsum1, whh1, _, _ = c1.packs()
+        x = K.twin(x)
+        xproj = torch.empty(B * T, 4 * H, device=x.device)
+        K.gemm(B * T, 4 * H, In, operand(x, In), operand(wih0, In), xproj, bias=bsum0)
+        h0, cs0, g0, h1, cs1, g1 = K.lstm2_fwd(xproj, whh0, wih1, whh1, bsum1, B, T, H)
+        ctx.cores, ctx.B, ctx.T, ctx.saved = (c0, c1), B, T, ((cs0, g0), (cs1, g1))
+        ctx.save_for_backward(x, h0, h1)
+        ctx.twins = (getattr(x, "_bf16", None), h0._bf16, h1._bf16)
+        return h1
+
+    @staticmethod
+    def backward(ctx, dh1):
+        x, h0, h1 = ctx.saved_tensors
+        for t, tw in zip((x, h0, h1), ctx.twins):
+            K.attach_twin(t, tw)
+        c0, c1 = ctx.cores
+        dh0, g1 = c1.backward(dh1.contiguous(), h0, h1, ctx.saved[1], ctx.B, ctx.T, True)
+        dx, g0 = c0.backward(dh0, x, h0, ctx.saved[0], ctx.B, ctx.T, ctx.needs_input_grad[0])
+        return (dx, None, None, None, None, *g0, *g1)
+
+
+_PAIR_OFF = bool(os.environ.get("AVC_LSTM2_OFF"))
+
+
 def lstm(mod, cores, x, B, T):
+    if _pair_ok(cores, x, B):
+        return _LSTMPairFn.apply(x, cores[0], cores[1], B, T, *cores[0].params(), *cores[1].params())
     for core in cores:
         x = _LSTMLayerFn.apply(x, core, B, T, *core.params())
     return x

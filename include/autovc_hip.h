@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 9
+#define AVC_ABI_VERSION 10
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -165,14 +165,40 @@ int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T,
 /* Backward recurrence.  dh_out (B,T,dirs*H) = dL/dh; writes dgates (B,T,dirs*4H)
  * (pre-activation).  w_hh_t: dirs x [H][4H] transposed copy (large H) or w_hh itself
  * (small H, pass the same layout as avc_lstm_fwd). dcbuf: B*H*dirs fp32.  gbuf (large H,
- * bf16 compute): at least max(16*dirs*B*H, 32*B*H + 16) bytes.  For dirs == 1, H in
- * {512, 1024} and enough CUs the whole sequence is ONE persistent launch (W_hh^T slices
- * register-resident, dG_{t+1} handed over as write-through payload + flags, bounded spins;
+ * bf16 compute): at least avc_lstm_bwd_scratch_bytes(B, H, dirs) bytes.  For dirs == 1, H in
+ * {512, 768, 1024} and enough CUs the whole sequence is ONE persistent launch (W_hh^T slices
+ * register-resident; each workgroup multiplies its own dG_{t+1} columns by its W_hh rows and
+ * hands the fp32 partial dh over as write-through payload + flags, bounded spins;
  * timeout flag = u32 at byte 0 of gbuf).  The small-H and persistent launches can also write a
  * bf16 copy of dgates (dgates_bf16, else null); the per-step path needs null. */
+/* Bytes of the backward scratch gbuf for (B, H, dirs) -- the persistent partial-sum form needs
+ * 2*ceil(B/8)*(H/32)^2 KB of fp32 partials besides the control words (16.8 MB at B=64, H=1024). */
+size_t avc_lstm_bwd_scratch_bytes(int B, int H, int dirs);
+
+/* Debug / A-B: form of the persistent backward recurrence.  1 = partial-sum exchange (each
+ * workgroup publishes its fp32 partial dh; the default), 0 = dG gather (each workgroup gathers
+ * the group's bf16 dG_{t+1}), -1 = back to the default (AVC_LSTM_BWD_PS=0 selects 0). */
+int avc_lstm_set_bwd_form(int form);
+
 int avc_lstm_bwd(const float* dh_out, const float* h, const float* c, const float* gates,
                  const void* w_hh, const void* w_hh_t, int wdtype, int B, int T, int H, int dirs,
                  float* dgates, void* dgates_bf16, float* dcbuf, void* gbuf, int compute, void* stream);
+
+/* Two stacked unidirectional layers of one nn.LSTM (decoder lstm2, AutoVC.py:96,110: 512 -> 1024,
+ * num_layers=2) forward in ONE persistent launch, as a layer wavefront (tick k = layer 0 step k
+ * beside layer 1 step k-1; layer 1's input projection inside the recurrence).  xproj0 (B,T,4H) =
+ * x W_ih0^T + b_ih0 + b_hh0; w_hh0, w_ih1, w_hh1: [4H][H] bf16; bias1 = b_ih1 + b_hh1 (4H fp32).
+ * Outputs per layer as avc_lstm_fwd (h fp32 + bf16 twin, c, activated gates).  buf: at least
+ * avc_lstm2_scratch_bytes(B, H) bytes (control words + flags zeroed by the call, then a
+ * [2 layers][2][B][H] bf16 payload); timeout flag = u32 at byte 0, fault word as avc_lstm_fwd.
+ * Only where avc_lstm2_persistent(B, H, In1 = H, AVC_BF16) is 1 (H = 1024, bf16, whole grid
+ * ceil(B/16) * H/16 workgroups resident); the caller runs the layers one by one otherwise. */
+int avc_lstm2_persistent(int B, int H, int in1, int compute);
+size_t avc_lstm2_scratch_bytes(int B, int H);
+int avc_lstm2_fwd(const float* xproj0, const void* w_hh0, const void* w_ih1, const void* w_hh1,
+                  const float* bias1, int B, int T, int H, float* h0, void* h0_bf16, float* c0,
+                  float* gates0, float* h1, void* h1_bf16, float* c1, float* gates1, void* buf,
+                  void* stream);
 
 /* Diagnostics (no reference counterpart): with buf non-null, later persistent LSTM launches
  * record the 100 MHz realtime clock at 4 points of every step of every workgroup into

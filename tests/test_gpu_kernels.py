@@ -479,15 +479,27 @@ def test_gemm_nt_conv_window_and_bn_stats(B, T, Cin, Cout, Kw, pad):
     assert rinf(1.0 / rstd.double() ** 2 - 1e-5, refv) < 1e-3
 
 
+@pytest.mark.parametrize("form", [1, 0])
 @pytest.mark.parametrize("B,H", [(64, 1024), (20, 1024), (64, 512), (3, 512), (64, 768), (2, 768)])
-def test_lstm_persistent_backward(B, H):
+def test_lstm_persistent_backward(B, H, form):
     """The one-launch backward recurrence (bf16 products, fp32 cell math) against an fp32
     CPU loop that rounds dG_{t+1} to bf16 for the recurrent product, as the kernel does;
-    its bf16 dG twin equals the fp32 output rounded; the spin-timeout flag stays clear."""
+    its bf16 dG twin equals the fp32 output rounded; the spin-timeout flag stays clear.
+    Both hand-off forms: partial-sum exchange (1, default) and dG gather (0)."""
     import autoformer_amd as A
     from autoformer_amd import kernels as Kr
 
     A.set_compute("bf16")
+    Kr.lstm_set_bwd_form(form)
+    try:
+        _persistent_backward_case(B, H)
+    finally:
+        Kr.lstm_set_bwd_form(-1)
+
+
+def _persistent_backward_case(B, H):
+    from autoformer_amd import kernels as Kr
+
     assert Kr.lstm_persistent_bwd(B, H, 1)
     T = 29
     G = 4 * H
@@ -625,3 +637,82 @@ def test_pack_batch_matches_individual_packs():
     torch.cuda.synchronize()
     for a, b in zip(outs, ref):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B", [64, 20])
+def test_lstm2_wavefront_forward(B):
+    """Two stacked layers in one wavefront launch (decoder lstm2, AutoVC.py:96,110) against an
+    fp32 CPU loop of the two layers with the kernel's roundings (h of both layers rounded to
+    bf16 for the products, bf16 weights); the spin-timeout flag stays clear."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute("bf16")
+    H, T = 1024, 29
+    G = 4 * H
+    assert Kr.lstm2_persistent(B, H, H)
+    torch.manual_seed(5)
+    xproj = torch.randn(B * T, G) * 0.5
+    ws = [(torch.randn(G, H) * (1.0 / H ** 0.5)).bfloat16() for _ in range(3)]
+    bias1 = torch.randn(G) * 0.1
+    h0, c0, g0, h1, c1, g1 = Kr.lstm2_fwd(xproj.to(DEV), *[w.to(DEV) for w in ws], bias1.to(DEV), B, T, H)
+    torch.cuda.synchronize()
+    assert int(Kr._CACHE["lstm2_buf"].view(torch.int32)[0].item()) == 0
+    torch.testing.assert_close(h0._bf16.float(), h0.to(torch.bfloat16).float(), rtol=0, atol=0)
+    w0, wi1, w1 = [w.float() for w in ws]
+    xp = xproj.view(B, T, G)
+    hs = [torch.zeros(B, H), torch.zeros(B, H)]
+    cs = [torch.zeros(B, H), torch.zeros(B, H)]
+    outs = [[], []]
+    gts_out = [[], []]
+    for t in range(T):
+        for L in range(2):
+            if L == 0:
+                pre = xp[:, t] + hs[0].bfloat16().float() @ w0.t()
+            else:
+                pre = bias1 + outs[0][t].bfloat16().float() @ wi1.t() + hs[1].bfloat16().float() @ w1.t()
+            i, f, gg, o = pre.chunk(4, 1)
+            i, f, gg, o = torch.sigmoid(i), torch.sigmoid(f), torch.tanh(gg), torch.sigmoid(o)
+            cs[L] = f * cs[L] + i * gg
+            hs[L] = o * torch.tanh(cs[L])
+            outs[L].append(hs[L])
+            gts_out[L].append(torch.cat([i, f, gg, o], 1))
+    for L, (h, c, g) in enumerate(((h0, c0, g0), (h1, c1, g1))):
+        ref = torch.stack(outs[L], 1).reshape(B * T, H)
+        assert relf(h, ref) < 3e-3, (L, relf(h, ref))
+        assert relf(c.cpu().view(B, T, H)[:, -1], cs[L]) < 3e-3
+        assert relf(g, torch.stack(gts_out[L], 1).reshape(B * T, G)) < 3e-3
+
+
+def test_lstm2_wavefront_autograd_matches_layerwise():
+    """layers.lstm over nn.LSTM(512, 1024, num_layers=2): the wavefront pair node gives the same
+    output and parameter / input gradients as the layer-by-layer nodes (bf16 tolerance)."""
+    import autoformer_amd as A
+    from autoformer_amd import layers as Ly
+
+    A.set_compute("bf16")
+    Ly.set_grad_sink(False)
+    B, T = 64, 24
+    torch.manual_seed(6)
+    mod = torch.nn.LSTM(512, 1024, num_layers=2, batch_first=True).to(DEV)
+    cores = [Ly.LSTMLayerCore(mod, 0), Ly.LSTMLayerCore(mod, 1)]
+    x0 = torch.randn(B * T, 512, device=DEV)
+    res = []
+    for off in (False, True):
+        Ly._PAIR_OFF = off
+        try:
+            assert Ly._pair_ok(cores, x0, B) == (not off)
+            mod.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            y = Ly.lstm(mod, cores, x, B, T)
+            (y * torch.linspace(-1, 1, 1024, device=DEV)).sum().backward()
+            Ly.join_side()
+            torch.cuda.synchronize()
+            res.append((y.detach().clone(), x.grad.clone(), [p.grad.clone() for p in mod.parameters()]))
+        finally:
+            Ly._PAIR_OFF = False
+    (ya, dxa, ga), (yb, dxb, gb) = res
+    assert relf(ya, yb) < 1e-2, relf(ya, yb)
+    assert relf(dxa, dxb) < 2e-2, relf(dxa, dxb)
+    for a, b in zip(ga, gb):
+        assert relf(a, b) < 2e-2, relf(a, b)

@@ -87,6 +87,19 @@ for H in (1024, 512):
     report(f"H={H} bwd", traced(lambda: K.lstm_bwd(dh, h, c, g, None, whht, B, T, H, 1, gbuf=gbuf), nwg), ng)
     assert K.lstm_timeout_flag(hbuf, B, H) == 0 and K.lstm_bwd_timeout_flag(gbuf, B, H) == 0
 
+# decoder lstm2 as ONE two-layer wavefront launch (T + 1 ticks; stamps of ticks 0..T-1)
+H = 1024
+G = 4 * H
+if K.lstm2_persistent(B, H, H):
+    xproj = torch.randn(B * T, G, device=dev) * 0.1
+    ws = [(torch.randn(G, H, device=dev) * 0.02).bfloat16() for _ in range(3)]
+    bias1 = torch.randn(G, device=dev) * 0.1
+    ng = (B + 15) // 16
+    nwg = ng * (H // 16)
+    us = ev_time(lambda: K.lstm2_fwd(xproj, *ws, bias1, B, T, H))
+    print(f"lstm2 wavefront fwd events {us:8.1f} us ({us / (T + 1):5.2f} us/tick, 2 layers)", flush=True)
+    report("lstm2 wavefront fwd", traced(lambda: K.lstm2_fwd(xproj, *ws, bias1, B, T, H), nwg), ng)
+
 # encoder BiLSTM (small-H kernels, both directions in one launch)
 H = 44
 xproj = torch.randn(B * T, 2 * 4 * H, device=dev) * 0.1
