@@ -1441,15 +1441,37 @@ struct Persist2Args {
 };
 
 constexpr int QRG = 16, QJU = 16;  // utterances per group, units per member and layer
-constexpr int NLW = 2;             // W_hh1 fragments per wave kept in LDS instead of VGPRs
+constexpr int NLW = 4;             // W_hh1 fragments per wave kept in LDS instead of VGPRs
 
 template <int H>
 constexpr size_t persist2_lds() {
   return (size_t)2 * QRG * (H + 8) * 2 + (size_t)4 * 2 * 4 * QRG * QJU * 4 + (size_t)2 * QRG * QJU * 2 +
-         (size_t)8 * NLW * 64 * 16 + 16;
+         (size_t)8 * NLW * 64 * 16 + (size_t)6 * 512 * 4 + 16;
 }
 
+// Waves 1..7: the staged outputs of tick kp (all 512 cells) to HBM.  (16-B value-major stores
+// of the same bytes measured slower per tick: 5.18 vs 4.99 us.)
 template <int H>
+__device__ __forceinline__ void lstm2_store_outputs(const Persist2Args& a, const float* outs, int kp, int b0, int j0) {
+  constexpr int G = 4 * H;
+  for (int cell = threadIdx.x - 64; cell < 2 * QRG * QJU; cell += PNT - 64) {
+    const int L = cell >> 8, cb = b0 + ((cell >> 4) & 15), cj = j0 + (cell & 15);
+    const int t = L == 0 ? kp : kp - 1;
+    if (!(L == 0 ? kp < a.T : kp >= 1) || cb >= a.B) continue;
+    const float* o = outs + cell;
+    const long long oh = ((long long)cb * a.T + t) * H + cj;
+    a.hout[L][oh] = o[0];
+    a.hout16[L][oh] = (bf16)o[0];
+    a.call[L][oh] = o[PNT];
+    float* gpo = a.gall[L] + ((long long)cb * a.T + t) * G + cj;
+    gpo[0] = o[2 * PNT];
+    gpo[H] = o[3 * PNT];
+    gpo[2 * H] = o[4 * PNT];
+    gpo[3 * H] = o[5 * PNT];
+  }
+}
+
+template <int H, int SB, int LB, bool OS>
 __global__ void __launch_bounds__(PNT, 1) lstm2_persist_fwd(Persist2Args a) {
   constexpr int G = 4 * H, AP = H + 8, NR = H / QJU, NKQ = H / 128;  // k-blocks per K quarter
   constexpr int NCH = 2 * QRG * H / 8 / PNT;                          // 16-B chunks per thread
@@ -1458,7 +1480,10 @@ __global__ void __launch_bounds__(PNT, 1) lstm2_persist_fwd(Persist2Args a) {
   bf16* As = reinterpret_cast<bf16*>(smem_raw);                          // [2 layers][16][AP]
   float* red = reinterpret_cast<float*>(smem_raw + 2 * QRG * AP * 2);    // [kq][L][q][16][16]
   bf16* hs16 = reinterpret_cast<bf16*>(red + 4 * 2 * 4 * QRG * QJU);     // [L][16][16] publish tile
-  int* quit = reinterpret_cast<int*>(reinterpret_cast<char*>(hs16 + 2 * QRG * QJU) + (size_t)8 * NLW * 64 * 16);
+  // the tick's outputs (h, c, i, f, g, o per cell), stored to HBM by waves 1..7 during the NEXT
+  // tick (after its products), so they never queue in front of wave 0's hand-off
+  float* outs = reinterpret_cast<float*>(reinterpret_cast<char*>(hs16 + 2 * QRG * QJU) + (size_t)8 * NLW * 64 * 16);
+  int* quit = reinterpret_cast<int*>(outs + 6 * PNT);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, gp = w & 1, kq = w >> 1;
   const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
   const int j0 = r * QJU, b0 = g * QRG;
@@ -1511,23 +1536,25 @@ __global__ void __launch_bounds__(PNT, 1) lstm2_persist_fwd(Persist2Args a) {
       __syncthreads();
       if (*quit) return;  // block-uniform exit after a spin timeout
       // h0_{k-1} -> As[0], h1_{k-2} -> As[1] (k >= 2); rows past the batch stay zero
-      // (two halves of NCH / 2 chunks in flight: the weight fragments leave few registers)
+      // (NCH / LB chunks in flight per batch: the weight fragments leave few registers)
       const int slot = (k - 1) & 1;
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        u32x4_t v[NCH / 2];
+      for (int hf = 0; hf < LB; ++hf) {
+        u32x4_t v[NCH / LB];
 #pragma unroll
-        for (int i = 0; i < NCH / 2; ++i) {
-          const int ch = tid + PNT * (hf * NCH / 2 + i), l = ch / (QRG * H / 8), rem = ch - l * (QRG * H / 8),
+        for (int i = 0; i < NCH / LB; ++i) {
+          const int ch = tid + PNT * (hf * NCH / LB + i), l = ch / (QRG * H / 8), rem = ch - l * (QRG * H / 8),
                     row = rem / (H / 8), col = rem - row * (H / 8);
           v[i] = row < rows && (l == 0 || k >= 2)
                      ? __builtin_amdgcn_raw_buffer_load_b128(pay, (((l * 2 + slot) * B + b0 + row) * H + col * 8) * 2,
                                                              0, AUX_SC1)
                      : u32x4_t{0u, 0u, 0u, 0u};
         }
+        // OS: the previous tick's outputs leave while this tick's payload loads are in flight
+        if (OS && hf == 0 && w > 0) lstm2_store_outputs<H>(a, outs, k - 1, b0, j0);
 #pragma unroll
-        for (int i = 0; i < NCH / 2; ++i) {
-          const int ch = tid + PNT * (hf * NCH / 2 + i), l = ch / (QRG * H / 8), rem = ch - l * (QRG * H / 8),
+        for (int i = 0; i < NCH / LB; ++i) {
+          const int ch = tid + PNT * (hf * NCH / LB + i), l = ch / (QRG * H / 8), rem = ch - l * (QRG * H / 8),
                     row = rem / (H / 8), col = rem - row * (H / 8);
           *reinterpret_cast<u32x4_t*>(As + (l * QRG + row) * AP + col * 8) = v[i];
         }
@@ -1549,8 +1576,8 @@ __global__ void __launch_bounds__(PNT, 1) lstm2_persist_fwd(Persist2Args a) {
                                                   : wl[(kk - (NKQ - NLW)) * 64];
           p1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, wb, p1[i], 0, 0, 0);
         }
-        // keep at most two k-blocks of A fragments in flight (the weights hold 192 VGPRs)
-        if (kk % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+        // SB > 0: at most SB k-blocks of A fragments in flight (the weights hold 184 VGPRs)
+        if (SB > 0 && kk % SB == SB - 1) __builtin_amdgcn_sched_barrier(0);
       }
     }
     // K-quarter partials -> LDS: red[((kq * 2 + L) * 4 + q) * 256 + row * 16 + unit]
@@ -1564,6 +1591,7 @@ __global__ void __launch_bounds__(PNT, 1) lstm2_persist_fwd(Persist2Args a) {
         d1[(4 * (lane >> 4) + e) * QJU] = p1[i][e];
       }
     }
+    if (!OS && k > 0 && w > 0) lstm2_store_outputs<H>(a, outs, k - 1, b0, j0);
     __syncthreads();
     if (k < T) stamp(a.trace, T, k, 2);
     float pre[4];
@@ -1581,6 +1609,12 @@ __global__ void __launch_bounds__(PNT, 1) lstm2_persist_fwd(Persist2Args a) {
       h = og * ftanh(c);
     }
     hs16[(L * QRG + cr) * QJU + cu] = (bf16)h;
+    outs[tid] = h;
+    outs[PNT + tid] = c;
+    outs[2 * PNT + tid] = ig;
+    outs[3 * PNT + tid] = fg;
+    outs[4 * PNT + tid] = gg;
+    outs[5 * PNT + tid] = og;
     __syncthreads();
     // ---- publish h0_k and h1_{k-1} (wave 0: lanes 0..31 layer 0, 32..63 layer 1; 16 B each),
     // needed by tick k + 1 (none after tick T - 1); the other waves store their outputs meanwhile
@@ -1593,19 +1627,9 @@ __global__ void __launch_bounds__(PNT, 1) lstm2_persist_fwd(Persist2Args a) {
       }
       raise_flag(flags, r, (unsigned)(k + 1));
     }
-    if (act && cv) {
-      const long long oh = ((long long)cb * T + t) * H + cj;
-      a.hout[L][oh] = h;
-      a.hout16[L][oh] = (bf16)h;
-      a.call[L][oh] = c;
-      float* gpo = a.gall[L] + ((long long)cb * T + t) * G + cj;
-      gpo[0] = ig;
-      gpo[H] = fg;
-      gpo[2 * H] = gg;
-      gpo[3 * H] = og;
-    }
     if (k < T) stamp(a.trace, T, k, 3);
   }
+  if (w > 0) lstm2_store_outputs<H>(a, outs, T, b0, j0);  // the last tick's (staged above its barrier)
 }
 
 template <int H>
@@ -1649,6 +1673,14 @@ unsigned spin_bound() {
   return s ? s : env ? env : PSPIN;
 }
 
+// AVC_LSTM_EXCL=1 (A/B): persistent recurrences claim the whole LDS of their CU, so no
+// side-stream GEMM workgroup can share the CU with them (they wait for the recurrence instead).
+constexpr size_t LDS_ALL = 160 * 1024;
+size_t excl_lds(size_t need) {
+  static const bool ex = getenv("AVC_LSTM_EXCL") && atoi(getenv("AVC_LSTM_EXCL")) == 1;
+  return ex ? LDS_ALL : need;
+}
+
 // Dynamic-LDS attribute of the persistent backward kernels, set once per (kernel, device).
 template <int H, bool GR>
 void set_bwd_lds_attr() {
@@ -1657,7 +1689,7 @@ void set_bwd_lds_attr() {
   static std::once_flag once[MAXDEV];
   std::call_once(once[dev & (MAXDEV - 1)], [] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_persist_bwd<H, GR>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_bwd_lds<H>());
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)excl_lds(persist_bwd_lds<H>()));
   });
 }
 
@@ -1749,17 +1781,17 @@ bool persistent_path(int B, int H, int dirs, bool bf, bool bwd) {
   if (grid > num_cus()) return false;
   const void* fn = H == 1024 ? persist_fn<1024>(bwd) : H == 768 ? persist_fn<768>(bwd) : persist_fn<512>(bwd);
   const size_t lds = !bwd || ps_bwd() ? 0
-                     : H == 1024 ? persist_bwd_lds<1024>()
-                     : H == 768  ? persist_bwd_lds<768>()
-                                 : persist_bwd_lds<512>();
+                     : H == 1024 ? excl_lds(persist_bwd_lds<1024>())
+                     : H == 768  ? excl_lds(persist_bwd_lds<768>())
+                                 : excl_lds(persist_bwd_lds<512>());
   return fits_resident(fn, PNT, lds, grid);
 }
 
 template <int H>
 void launch_persist_bwd(dim3 grid, hipStream_t s, bool gr, const PersistBwdArgs& p) {
   if (ps_bwd()) lstm_persist_bwd_ps<H><<<grid, PNT, 0, s>>>(p);
-  else if (gr) lstm_persist_bwd<H, true><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
-  else lstm_persist_bwd<H, false><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
+  else if (gr) lstm_persist_bwd<H, true><<<grid, PNT, excl_lds(persist_bwd_lds<H>()), s>>>(p);
+  else lstm_persist_bwd<H, false><<<grid, PNT, excl_lds(persist_bwd_lds<H>()), s>>>(p);
 }
 
 template <int HM>
@@ -1797,6 +1829,7 @@ extern "C" int avc_lstm_set_spin(unsigned spins) {
 }
 
 // Two-layer wavefront forward (lstm2_persist_fwd): shape, compute mode and residency.
+#define L2FN(LB, OS) reinterpret_cast<const void*>(&lstm2_persist_fwd<1024, 2, LB, OS>)
 bool persist2_path(int B, int H, int In1, bool bf) {
   if (!bf || H != 1024 || In1 != H || no_persist_env() || getenv("AVC_LSTM2_OFF")) return false;
   const int ng = (B + QRG - 1) / QRG, grid = ng * (H / QJU);
@@ -1805,10 +1838,10 @@ bool persist2_path(int B, int H, int In1, bool bf) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::call_once(once[dev & (MAXDEV - 1)], [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm2_persist_fwd<1024>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist2_lds<1024>());
+    for (const void* f : {L2FN(1, false), L2FN(2, false), L2FN(1, true), L2FN(2, true)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)excl_lds(persist2_lds<1024>()));
   });
-  return fits_resident(reinterpret_cast<const void*>(&lstm2_persist_fwd<1024>), PNT, persist2_lds<1024>(), grid);
+  return fits_resident(L2FN(2, false), PNT, excl_lds(persist2_lds<1024>()), grid);
 }
 
 extern "C" int avc_lstm2_persistent(int B, int H, int in1, int compute) {
@@ -1854,7 +1887,19 @@ extern "C" int avc_lstm2_fwd(const float* xproj0, const void* w_hh0, const void*
   p.T = T;
   p.ng = ng;
   (void)hipMemsetAsync(buf, 0, px_ctl_bytes(ng), s);
-  lstm2_persist_fwd<1024><<<dim3(ng * (H / QJU)), PNT, persist2_lds<1024>(), s>>>(p);
+  // scheduling fence every 2 k-blocks of the product (without one the compiler hoists the A
+  // fragment reads and spills weight fragments).  AVC_LSTM2_CFG = LB*10 + OS (A/B): payload loads
+  // in LB batches (1 or 2); OS = 1 stores the previous tick's outputs under the payload loads
+  // instead of after the products
+  static const int cfg = getenv("AVC_LSTM2_CFG") ? atoi(getenv("AVC_LSTM2_CFG")) : 20;
+  const dim3 grid(ng * (H / QJU));
+  const size_t lds = excl_lds(persist2_lds<1024>());
+  switch (cfg) {
+    case 10: lstm2_persist_fwd<1024, 2, 1, false><<<grid, PNT, lds, s>>>(p); break;
+    case 11: lstm2_persist_fwd<1024, 2, 1, true><<<grid, PNT, lds, s>>>(p); break;
+    case 21: lstm2_persist_fwd<1024, 2, 2, true><<<grid, PNT, lds, s>>>(p); break;
+    default: lstm2_persist_fwd<1024, 2, 2, false><<<grid, PNT, lds, s>>>(p); break;
+  }
   return avc_check_launch("avc_lstm2_fwd");
 }
 
