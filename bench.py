@@ -93,6 +93,13 @@ def kernel_timing(model, B, T, reps=3):
             % (T, B, H), "avg_us": avg_us, "bytes": float(alg_bytes), "flops": 2.0 * B * G * H * T}
 
 
+def _names(kernel, name):
+    """Whether a profiler kernel name is `kernel` ("f<1024>") with any further template
+    arguments ("f<1024, false>"), and not another kernel sharing its prefix ("f_ps<1024>")."""
+    base, args = kernel.rstrip(">").split("<")
+    return f"{base}<{args}>" in name or f"{base}<{args}," in name
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/r*_pmc_traffic.json, written by tools/rocpd_summary.py from separate
@@ -104,7 +111,7 @@ def pmc_traffic(kernel):
         return None, None
     data = json.load(open(files[-1]))["kernels"]
     for name, e in data.items():
-        if kernel in name and "hbm_bytes_per_launch" in e:
+        if _names(kernel, name) and "hbm_bytes_per_launch" in e:
             return e["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
     return None, None
 
@@ -144,7 +151,7 @@ def pmc_mfma(kernel):
         return None
     data = json.load(open(files[-1]))
     for name, e in data.items():
-        if kernel in name:
+        if _names(kernel, name):
             return {"mfma_instr_tflops": round(e.get("bf16_tflops", 0.0), 1),
                     "mfma_instr_frac": round(e.get("bf16_tflops", 0.0) / PEAK_BF16_TFLOPS, 4),
                     "wave_wait_frac": round(e.get("wait", 0.0), 3), "source": os.path.relpath(files[-1], ROOT),
