@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip"]
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -43,6 +43,12 @@ class BnFin(ctypes.Structure):
                 ("mean", c_void_p), ("rstd", c_void_p), ("scale", c_void_p), ("shift", c_void_p)]
 
 
+class BnbArgs(ctypes.Structure):
+    _fields_ = [("y", c_void_p), ("y_dtype", c_int), ("mean", c_void_p), ("rstd", c_void_p), ("gamma", c_void_p),
+                ("beta", c_void_p), ("act", c_int), ("coef", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p),
+                ("dbias", c_void_p), ("accumulate", c_int), ("ws", c_void_p)]
+
+
 class PackOp(ctypes.Structure):
     _fields_ = [("src", c_void_p), ("src2", c_void_p), ("dst", c_void_p), ("kind", c_int), ("out_dtype", c_int),
                 ("d0", c_int), ("d1", c_int), ("d2", c_int), ("pad_", c_int), ("ld_out", c_ll)]
@@ -64,6 +70,10 @@ _SIGS = {
     "avc_bn_stats": (c_int, [c_void_p, c_ll, c_int, c_int, c_void_p, c_void_p]),
     "avc_bn_apply": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                               c_void_p]),
+    "avc_gemm_bnb_ws": (c_size, [c_int, c_int]),
+    "avc_gemm_bnb": (c_int, [ctypes.POINTER(GemmDesc), ctypes.POINTER(BnbArgs), c_void_p]),
+    "avc_bn_bwd_apply": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                 c_void_p]),
     "avc_bn_bwd_ws": (c_size, [c_int, c_int]),
     "avc_bn_bwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                            c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,

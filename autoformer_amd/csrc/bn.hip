@@ -7,12 +7,15 @@
 // are merged here with Chan's parallel-variance formula, so no extra pass over the
 // activations is needed on the forward.
 #include "common.h"
+#include "bn_internal.h"
 
 #include <atomic>
 #include <mutex>
 #include <type_traits>
 
 namespace {
+
+using namespace avcbn;
 
 constexpr int PTILE = 128;  // rows per partial (must match gemm.hip BM)
 
@@ -23,32 +26,7 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 //   mean = sum_t s_t / n;   M2 = sum_t [ q_t + n_t (s_t / n_t - mean)^2 ]   (Chan, parallel form)
 // 256-thread blocks: a 1024-thread finalize block needs 16 free wave slots on one CU and waits
 // behind the side stream's weight-gradient GEMMs (measured 14.8 us per backward finalize in the
-// C2 step); 4 row groups x 64 channels start anywhere
-constexpr int FG = 4;  // row groups of the finalize reductions (256 threads = 64 channels x 4)
-constexpr int FU = 8;   // partial rows per thread loaded together (independent loads in flight)
-
-// sum over b = grp, grp + FG, ... < nrb of NV consecutive floats at ws[(b*ld + c)*NV + v]:
-// FU rows' loads are issued before any is added (one memory latency per FU*FG rows, not per row)
-template <int NV, bool SC1 = false, int FUN = FU>  // SC1: partials handed over within the launch
-__device__ __forceinline__ void strided_sums(const float* __restrict__ ws, int nrb, long long ld, int c, int grp,
-                                             float (&out)[NV]) {
-#pragma unroll
-  for (int v = 0; v < NV; ++v) out[v] = 0.f;
-  for (int b0 = grp; b0 < nrb; b0 += FG * FUN) {
-    float x[FUN][NV];
-#pragma unroll
-    for (int u = 0; u < FUN; ++u) {
-      const int b = b0 + u * FG;
-      const float* p = ws + ((long long)(b < nrb ? b : 0) * ld + c) * NV;
-#pragma unroll
-      for (int v = 0; v < NV; ++v) x[u][v] = b < nrb ? (SC1 ? ld_sc1(p + v) : p[v]) : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < FUN; ++u)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) out[v] += x[u][v];
-  }
-}
+// C2 step); 4 row groups x 64 channels start anywhere (FG, strided_sums: bn_internal.h)
 
 __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ partial, int M, int C,
                                                           const float* gamma, const float* beta, float* rmean,
@@ -157,69 +135,11 @@ __global__ void bn_apply1_kernel(const TY* __restrict__ y, const float* __restri
 
 // Backward finalize of one 64-channel strip by one 256-thread block (4 row groups reduce the
 // per-row-block partials in parallel): apply coefficients + dgamma / dbeta / conv-bias gradient.
-struct BwdFin {
-  const float* gamma;
-  const float* beta;
-  const float* mean;
-  const float* rstd;
-  float* coef;
-  float* dgamma;
-  float* dbeta;
-  float* dbias;
-  int acc;
-};
-
-template <bool SC1>
-__device__ __forceinline__ void bwd_finalize_strip(const float* ws, int nrb, int M, int C, int strip,
-                                                   const BwdFin& f) {
-  __shared__ float red[3][FG][64];
-  const float* gamma = f.gamma;
-  const float* beta = f.beta;
-  float* coef = f.coef;
-  float* dgamma = f.dgamma;
-  float* dbeta = f.dbeta;
-  float* dbias = f.dbias;
-  const int acc = f.acc;
-  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int c = strip * 64 + cl;
-  float sv[3] = {0.f, 0.f, 0.f};
-  if (c < C) strided_sums<3, SC1, 32>(ws, nrb, C, c, grp, sv);
-  float s0 = sv[0], s1 = sv[1], s2 = sv[2];
-  red[0][grp][cl] = s0;
-  red[1][grp][cl] = s1;
-  red[2][grp][cl] = s2;
-  __syncthreads();
-  if (grp != 0 || c >= C) return;
-  s0 = s1 = s2 = 0.f;
-#pragma unroll
-  for (int i = 0; i < FG; ++i) {
-    s0 += red[0][i][cl];
-    s1 += red[1][i][cl];
-    s2 += red[2][i][cl];
-  }
-  const float g = gamma ? gamma[c] : 1.f;
-  const float rs = f.rstd[c], mu = f.mean[c];
-  const float k1 = g * rs;
-  const float invn = 1.f / (float)M;
-  const float m1 = s0 * invn, m2 = s1 * invn;
-  // planar per-channel constants of the apply pass (one 16-B load per plane per 4 channels):
-  //   yhat = (y - mu)*rs,  z = (y - mu)*k1 + beta,  dy = k1*(dz - m1 - yhat*m2)
-  coef[c] = k1;
-  coef[C + c] = m1;
-  coef[2 * C + c] = m2;
-  coef[3 * C + c] = mu;
-  coef[4 * C + c] = rs;
-  coef[5 * C + c] = beta ? beta[c] : 0.f;
-  const float gb = -k1 * s1 * s2 * invn;
-  if (dgamma) dgamma[c] = acc ? dgamma[c] + s1 : s1;
-  if (dbeta) dbeta[c] = acc ? dbeta[c] + s0 : s0;
-  if (dbias) dbias[c] = acc ? dbias[c] + gb : gb;
-}
-
 // standalone finalize (no counter pool): one block per strip
 __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ ws, int nrb, int M, int C,
                                                               BwdFin f) {
-  bwd_finalize_strip<false>(ws, nrb, M, C, blockIdx.x, f);
+  __shared__ float red[3 * FG * 64];
+  bwd_finalize_cols<false>(ws, nrb, M, C, blockIdx.x * 64, 64, f, red);
 }
 
 // backward reduce: per (64-row block, 64 channels) partial sums of dz, dz*yhat, yhat.
@@ -304,7 +224,9 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TD* __restrict
     }
   }
   // the last row block of this channel strip merges all partials (no finalize launch)
-  if (cnt && arrive_last(cnt + blockIdx.x, gridDim.y)) bwd_finalize_strip<true>(ws, gridDim.y, M, C, blockIdx.x, fin);
+  __shared__ float fred[3 * FG * 64];
+  if (cnt && arrive_last(cnt + blockIdx.x, gridDim.y))
+    bwd_finalize_cols<true>(ws, gridDim.y, M, C, blockIdx.x * 64, 64, fin, fred);
 }
 
 // scalar variant (C % 4 != 0): 64 channels x 4 row lanes
@@ -349,7 +271,9 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const TD* __restric
       else p[q] = v[q];
     }
   }
-  if (cnt && arrive_last(cnt + blockIdx.x, gridDim.y)) bwd_finalize_strip<true>(ws, gridDim.y, M, C, blockIdx.x, fin);
+  __shared__ float fred[3 * FG * 64];
+  if (cnt && arrive_last(cnt + blockIdx.x, gridDim.y))
+    bwd_finalize_cols<true>(ws, gridDim.y, M, C, blockIdx.x * 64, 64, fin, fred);
 }
 
 
@@ -620,6 +544,59 @@ extern "C" int avc_bn_bwd(const void* dA, int dA_dtype, const float* a, const vo
     });
   });
   return avc_check_launch("avc_bn_bwd");
+}
+
+int avcbn::bn_bwd_reduce_finalize(const void* dA, int dA_dtype, const void* y, int y_dtype, int M, int C, int act,
+                                  float* ws, const BwdFin& fin, hipStream_t s) {
+  auto al = [](const void* p, int dt) { return (reinterpret_cast<uintptr_t>(p) & (dt == AVC_BF16 ? 7 : 15)) == 0; };
+  const bool v4 = C % 4 == 0 && al(dA, dA_dtype) && al(y, y_dtype) && (!fin.gamma || aligned16(fin.gamma)) &&
+                  (!fin.beta || aligned16(fin.beta));
+  const int nrb = cdiv(M, v4 ? RB * RBN : RB);
+  dim3 grid(cdiv(C, 64), nrb);
+  with_type(dA_dtype, [&](auto dtag) {
+    using TD = std::remove_const_t<std::remove_pointer_t<decltype(dtag)>>;
+    with_type(y_dtype, [&](auto ytag) {
+      using TY = std::remove_const_t<std::remove_pointer_t<decltype(ytag)>>;
+      const TD* dp = static_cast<const TD*>(dA);
+      const TY* yp = static_cast<const TY*>(y);
+      if (v4)
+        bn_bwd_reduce_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, nullptr, yp, fin.mean, fin.rstd, fin.gamma, fin.beta,
+                                                                M, C, act, ws, nullptr, fin);
+      else
+        bn_bwd_reduce1_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, nullptr, yp, fin.mean, fin.rstd, fin.gamma,
+                                                                 fin.beta, M, C, act, ws, nullptr, fin);
+      bn_bwd_finalize_kernel<<<cdiv(C, 64), 256, 0, s>>>(ws, nrb, M, C, fin);
+    });
+  });
+  return avc_check_launch("bn_bwd_reduce_finalize");
+}
+
+extern "C" int avc_bn_bwd_apply(const void* dA, int dA_dtype, const void* y, int y_dtype, const float* coef, int M,
+                                int C, int act, float* dy, void* dy_bf16, void* stream) {
+  bf16* d16 = reinterpret_cast<bf16*>(dy_bf16);
+  AVC_CHECK_ARG(dA && y && coef && (dy || d16) && M > 0 && C > 0 && (dA_dtype == AVC_F32 || dA_dtype == AVC_BF16) &&
+                    (y_dtype == AVC_F32 || y_dtype == AVC_BF16) && aligned16(coef),
+                "avc_bn_bwd_apply: bad args");
+  hipStream_t s = as_stream(stream);
+  auto al = [](const void* p, int dt) { return (reinterpret_cast<uintptr_t>(p) & (dt == AVC_BF16 ? 7 : 15)) == 0; };
+  const bool v4 = C % 4 == 0 && al(dA, dA_dtype) && al(y, y_dtype) && (!dy || aligned16(dy)) &&
+                  (!d16 || al(d16, AVC_BF16));
+  const long long total = (long long)M * C;
+  with_type(dA_dtype, [&](auto dtag) {
+    using TD = std::remove_const_t<std::remove_pointer_t<decltype(dtag)>>;
+    with_type(y_dtype, [&](auto ytag) {
+      using TY = std::remove_const_t<std::remove_pointer_t<decltype(ytag)>>;
+      const TD* dp = static_cast<const TD*>(dA);
+      const TY* yp = static_cast<const TY*>(y);
+      if (v4)
+        bn_bwd_apply_kernel<true, TD, TY><<<cdiv(total / 4, 256), 256, 0, s>>>(dp, nullptr, yp, coef, total / 4, C,
+                                                                              act, dy, d16);
+      else
+        bn_bwd_apply1_kernel<true, TD, TY><<<cdiv(total, 256), 256, 0, s>>>(dp, nullptr, yp, coef, total, C, act, dy,
+                                                                           d16);
+    });
+  });
+  return avc_check_launch("avc_bn_bwd_apply");
 }
 
 extern "C" size_t avc_colsum_ws(int M, int N) { return (size_t)cdiv(M, RB) * N; }

@@ -706,7 +706,17 @@ static int bn_finalize_after(const GemmArgs& g, const avc_bn_fin* f, void* strea
   return 0;
 }
 
-static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream) {
+// avc_gemm_bnb off the fused epilogue: the same reduction as a pass over the GEMM's output
+static int bnb_after(const avc_gemm_desc* d, const avc_bnb_args* bb, hipStream_t s) {
+  const avcbn::BwdFin fin{bb->gamma, bb->beta, bb->mean, bb->rstd, bb->coef, bb->dgamma, bb->dbeta, bb->dbias,
+                          bb->accumulate};
+  AVC_CHECK_ARG(d->ldc == d->N, "avc_gemm_bnb: the unfused fallback needs ldc == N");
+  const void* out = d->c ? (const void*)d->c : d->c_bf16;
+  return avcbn::bn_bwd_reduce_finalize(out, d->c ? AVC_F32 : AVC_BF16, bb->y, bb->y_dtype, d->M, d->N, bb->act, bb->ws,
+                                       fin, s);
+}
+
+static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, const avc_bnb_args* bb = nullptr) {
   AVC_CHECK_ARG(d != nullptr, "avc_gemm: null desc");
   AVC_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0, "avc_gemm: negative dims");
   if (d->M == 0 || d->N == 0) return 0;
@@ -738,6 +748,12 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream) 
                 "avc_gemm: cperm needs N %% taps == 0 and no bias / residual / bf16 / BN epilogue");
   g.cpd = make_fastdiv(g.cperm ? (uint32_t)(d->N / g.cperm) : 1u);
   g.bn_cnt = nullptr;
+  g.bnb_ws = nullptr;
+  g.bnb_cnt = nullptr;
+  g.bnb_y = nullptr;
+  g.bnb_ydt = AVC_F32;
+  g.bnb_act = 0;
+  g.bnb_fin = avcbn::BwdFin{};
   if (f) {
     AVC_CHECK_ARG(g.bn_partial && f->mean && f->rstd && f->scale && f->shift && f->nupd >= 1 &&
                       (!f->running_mean == !f->running_var),
@@ -778,6 +794,17 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream) 
       g.bn_cnt = avc_counter_slots(cdiv(g.N, 64), s);
       if (!g.bn_cnt) return -1;
     }
+    const bool bnb_fused = bb && !aks && !bks;  // every non-TT fast kernel runs fast_epilogue
+    if (bnb_fused) {
+      g.bnb_ws = bb->ws;
+      g.bnb_y = bb->y;
+      g.bnb_ydt = bb->y_dtype;
+      g.bnb_act = bb->act;
+      g.bnb_fin = avcbn::BwdFin{bb->gamma, bb->beta, bb->mean, bb->rstd, bb->coef, bb->dgamma, bb->dbeta, bb->dbias,
+                                bb->accumulate};
+      g.bnb_cnt = avc_counter_slots(cdiv(g.N, 32), s);  // one per column tile (tiles >= 32 columns)
+      if (!g.bnb_cnt) return -1;
+    }
     const char* what = "avc_gemm(fast)";
     if (!aks && !bks && gemm_conv_launch(g, s)) what = "avc_gemm(conv)";
     else if (!aks && !bks && gemm_nt_launch(g, s)) what = "avc_gemm(nt)";
@@ -790,6 +817,7 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream) 
       else launch_fast_layout<128>(g, aks, bks, nb, s);
     }
     if (avc_check_launch(what)) return -1;
+    if (bb && !bnb_fused) return bnb_after(d, bb, s);
     return (f && !g.bn_cnt) ? bn_finalize_after(g, f, stream) : 0;
   }
   AVC_CHECK_ARG(!g.c16, "avc_gemm: c_bf16 output needs the fast path (bf16 compute, vectorisable operands)");
@@ -814,10 +842,27 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream) 
   }
 #undef AVC_GEMM_LAUNCH
   if (avc_check_launch("avc_gemm")) return -1;
+  if (bb) return bnb_after(d, bb, s);
   return f ? bn_finalize_after(g, f, stream) : 0;  // generic kernels: finalize launch(es) after the GEMM
 }
 
 extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) { return gemm_impl(d, nullptr, stream); }
+
+extern "C" size_t avc_gemm_bnb_ws(int M, int N) {
+  // fused: cdiv(M, 128) row tiles; fallback pass: cdiv(M, 64) row blocks; 3 sums each
+  return (size_t)cdiv(M, 64) * N * 3;
+}
+
+extern "C" int avc_gemm_bnb(const avc_gemm_desc* d, const avc_bnb_args* bb, void* stream) {
+  AVC_CHECK_ARG(d != nullptr && bb != nullptr, "avc_gemm_bnb: null args");
+  AVC_CHECK_ARG(bb->y && bb->mean && bb->rstd && bb->coef && bb->ws && (bb->y_dtype == AVC_F32 || bb->y_dtype == AVC_BF16),
+                "avc_gemm_bnb: needs y, mean, rstd, coef, ws");
+  AVC_CHECK_ARG(d->batch <= 1 && d->split_k <= 1 && !d->accumulate && !d->residual && !d->cperm && !d->bias &&
+                    !d->bn_partial,
+                "avc_gemm_bnb: a plain single product (no split K, batch, accumulate, residual, bias, BN stats)");
+  AVC_CHECK_ARG((reinterpret_cast<uintptr_t>(bb->coef) & 15) == 0, "avc_gemm_bnb: coef must be 16-B aligned");
+  return gemm_impl(d, nullptr, stream, bb);
+}
 
 extern "C" int avc_gemm_bn(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream) {
   AVC_CHECK_ARG(f != nullptr, "avc_gemm_bn: null finalize args");

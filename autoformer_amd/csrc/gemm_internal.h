@@ -2,6 +2,7 @@
 // the LDS-tiled kernels in gemm.hip and gemm_nt.hip (internal to libautovc_hip.so).
 #pragma once
 #include "common.h"
+#include "bn_internal.h"
 
 namespace avcg {
 
@@ -42,6 +43,15 @@ struct GemmArgs {
   float* bn_shift;
   float bn_momentum, bn_eps;
   int bn_nupd;
+  // BatchNorm BACKWARD reduction of the layer that produced this GEMM's output gradient
+  // (bnb_ws != null, avc_gemm_bnb): per 128-row tile and column (sum dz, sum dz*yhat,
+  // sum yhat) with dz = C * act'(z), z = (y - mean)*rstd*gamma + beta recomputed from the
+  // producer's stored conv output y; the last row tile of each column tile finalizes them
+  const void* bnb_y;
+  int bnb_ydt, bnb_act;
+  float* bnb_ws;
+  unsigned* bnb_cnt;
+  avcbn::BwdFin bnb_fin;
 };
 
 // Last-arriving row tile of a column tile: merge the per-row-tile (sum, M2) partials of columns
@@ -92,7 +102,7 @@ __device__ __forceinline__ long long out_col(const GemmArgs& g, int col) {
 // rows wm*64 + i*16 + 4*(lane>>4) + e and columns wn*BN_/2 + j*16 + (lane&15) of the tile.
 // Fused epilogue: bias, residual, accumulate / atomics (split-K, batch-sum), bf16 copy, and
 // BatchNorm partial statistics (per 128-row tile: column sum and M2 about the tile mean).
-template <int BN_>
+template <int BN_, bool BNB = true>  // BNB: the BatchNorm-backward reduction compiled in
 __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4][BN_ / 32], int m0, int n0, int mt,
                                               int bz, int ks, char* smem_raw) {
   constexpr int NJ = BN_ / 32;
@@ -193,6 +203,78 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
       }
     }
     if (g.bn_cnt && arrive_last(g.bn_cnt + n0 / BN_, (g.M + BM - 1) / BM)) bn_finalize_cols<BN_>(g, n0, red);
+  }
+  if (BNB && g.bnb_ws) {
+    // BatchNorm backward reduction of the producing layer over this tile's rows (the value the
+    // apply pass will read: rounded to bf16 when C is bf16-only)
+    float* red = reinterpret_cast<float*>(smem_raw);  // [3][2 wm][BN_], then the finalize's 3*FG*64
+    const avcbn::BwdFin& f = g.bnb_fin;
+    float s0[NJ], s1[NJ], s2[NJ];
+    // y through a buffer resource: 32-bit element offsets (M*ldc < 2^30 checked by the host)
+    const bool ybf = g.bnb_ydt == AVC_BF16;
+    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(g.bnb_y), (short)0, (int)min((long long)g.M * g.ldc * (ybf ? 2 : 4), 0x7fffffffLL), 0x00020000);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = cbase + j * 16;
+      const bool cv = col < g.N;
+      const float mu = cv ? f.mean[col] : 0.f, rs = cv ? f.rstd[col] : 0.f;
+      const float gm = cv && f.gamma ? f.gamma[col] : 1.f, bt = cv && f.beta ? f.beta[col] : 0.f;
+      float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = rbase + i * 16 + e;
+          if (!cv || row >= g.M) continue;
+          float v = acc[i][j][e];
+          if (!C) v = (float)(bf16)v;
+          const int o = row * (int)g.ldc + col;
+          const float yv = ybf ? __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(yr, o * 2, 0, 0)
+                                                               << 16)
+                               : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(yr, o * 4, 0, 0));
+          const float yh = (yv - mu) * rs;
+          const float dz = act_bwd_from_pre(v, yh * gm + bt, g.bnb_act);
+          t0 += dz;
+          t1 += dz * yh;
+          t2 += yh;
+        }
+      t0 += __shfl_xor(t0, 16, 64);
+      t0 += __shfl_xor(t0, 32, 64);
+      t1 += __shfl_xor(t1, 16, 64);
+      t1 += __shfl_xor(t1, 32, 64);
+      t2 += __shfl_xor(t2, 16, 64);
+      t2 += __shfl_xor(t2, 32, 64);
+      s0[j] = t0;
+      s1[j] = t1;
+      s2[j] = t2;
+      // one column group's y loads at a time: hoisting all of them doubled the kernels' VGPRs
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int cl = wn * WN + j * 16 + lane;
+        red[(0 * 2 + wm) * BN_ + cl] = s0[j];
+        red[(1 * 2 + wm) * BN_ + cl] = s1[j];
+        red[(2 * 2 + wm) * BN_ + cl] = s2[j];
+      }
+    }
+    __syncthreads();
+    if (tid < BN_) {
+      const int col = n0 + tid;
+      if (col < g.N) {
+        float* p = g.bnb_ws + ((long long)mt * g.N + col) * 3;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) st_sc1(p + q, red[(q * 2) * BN_ + tid] + red[(q * 2 + 1) * BN_ + tid]);
+      }
+    }
+    if (arrive_last(g.bnb_cnt + n0 / BN_, (g.M + BM - 1) / BM)) {
+      const int c1 = min(n0 + BN_, g.N);
+      for (int c0 = n0; c0 < c1; c0 += 64)
+        avcbn::bwd_finalize_cols<true, 4>(g.bnb_ws, (g.M + BM - 1) / BM, g.M, g.N, c0, min(64, c1 - c0), f, red);
+    }
   }
 }
 

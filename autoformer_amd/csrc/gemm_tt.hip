@@ -202,7 +202,7 @@ __global__ void __launch_bounds__(256, 2) gemm_tt_kernel(GemmArgs g) {
     }
   }
   __syncthreads();
-  fast_epilogue<BN_>(g, acc, m0, n0, mt, bz, ks, smem_raw);
+  fast_epilogue<BN_, false>(g, acc, m0, n0, mt, bz, ks, smem_raw);  // (weight gradients: no BN-backward epilogue)
 }
 
 template <bool WINB>

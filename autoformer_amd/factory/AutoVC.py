@@ -65,8 +65,8 @@ class Encoder(nn.Module):
             raise IndexError(f"len_crop {T} is not a multiple of freq {self.freq}")
         # conv outputs feed only the next conv / the BiLSTM input projection: bf16 storage
         h = Lyr.enc_conv0(self._convs[0], mel, c_org.contiguous(), B, T, out_bf16=True)
-        for core in self._convs[1:]:
-            h = Lyr.conv_bn(core, h, B, T, out_bf16=True)
+        for core in self._convs[1:]:  # each conv output feeds the next conv alone (fuse_prev)
+            h = Lyr.conv_bn(core, h, B, T, out_bf16=True, fuse_prev=True)
         h = Lyr.lstm(self.lstm, self._lstm, h, B, T)
         return Lyr.codes(h, B, T, self.dim_neck, self.freq)
 
@@ -98,8 +98,8 @@ class Decoder(nn.Module):
         return self._after_lstm1(h, B, T)
 
     def _after_lstm1(self, h, B, T):
-        for core in self._convs:
-            h = Lyr.conv_bn(core, h, B, T, out_bf16=True)
+        for core in self._convs:  # (lstm1's output carries no BN link: fuse_prev is a no-op there)
+            h = Lyr.conv_bn(core, h, B, T, out_bf16=True, fuse_prev=True)
         h = Lyr.lstm(self.lstm2, self._lstm2, h, B, T)
         lin = self.linear_projection.linear_layer
         return Lyr.linear(h, lin.weight, lin.bias, self._lin)
@@ -125,8 +125,8 @@ class Postnet(nn.Module):
     def frames(self, mel, B, T, residual=None):
         h = mel
         for core in self._convs[:-1]:
-            h = Lyr.conv_bn(core, h, B, T, out_bf16=True)
-        return Lyr.conv_bn(self._convs[-1], h, B, T, residual=residual)
+            h = Lyr.conv_bn(core, h, B, T, out_bf16=True, fuse_prev=True)
+        return Lyr.conv_bn(self._convs[-1], h, B, T, residual=residual, fuse_prev=True)
 
     def forward(self, x):
         """Reference layout (B, 80, T) in and out."""

@@ -81,11 +81,15 @@ def operand(t: torch.Tensor, ld: int, kstrided: bool = False, window=None, batch
 
 
 def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=None, accumulate=False, split_k=1,
-         bn_partial=None, batch=1, c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0, bn_fin=None):
+         bn_partial=None, batch=1, c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0, bn_fin=None,
+         bnb=None):
     """cperm = taps > 1: C's columns are (tap, channel) pairs written in nn.Conv1d's [Co][Ci][K]
     weight layout (a conv weight gradient straight into .grad).
     bn_fin = (gamma, beta, running_mean, running_var, nbt, momentum, eps, nupd): the BatchNorm
-    finalize of bn_partial fused into the GEMM (avc_gemm_bn); returns (mean, rstd, scale, shift)."""
+    finalize of bn_partial fused into the GEMM (avc_gemm_bn); returns (mean, rstd, scale, shift).
+    bnb = (y, mean, rstd, gamma, beta, act, coef, dgamma, dbeta, dbias, accumulate): C is dL/da of
+    the conv + BN + act layer whose conv output is y; the GEMM also computes that layer's BN
+    backward statistics (avc_gemm_bnb: coef[6][N] and the parameter gradients)."""
     _dev(c, bias, bn_partial, c_bf16, residual)
     if c.dtype == torch.bfloat16:  # bf16-only output
         assert c_bf16 is None and not accumulate and split_k == 1 and not cperm
@@ -106,6 +110,17 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     d.c_bf16 = _ptr(c_bf16)
     d.residual = _ptr(residual)
     d.cperm = int(cperm)
+    if bnb is not None:
+        y, mean, rstd, gamma, beta, act, coef, dgamma, dbeta, dbias, acc = bnb
+        _dev(y, mean, rstd, coef)
+        bb = L.BnbArgs()
+        bb.y, bb.y_dtype, bb.mean, bb.rstd = y.data_ptr(), _dt(y), mean.data_ptr(), rstd.data_ptr()
+        bb.gamma, bb.beta, bb.act, bb.coef = _ptr(gamma), _ptr(beta), int(act), coef.data_ptr()
+        bb.dgamma, bb.dbeta, bb.dbias, bb.accumulate = _ptr(dgamma), _ptr(dbeta), _ptr(dbias), int(acc)
+        ws = torch.empty(int(L.lib().avc_gemm_bnb_ws(int(M), int(N))), device=y.device)
+        bb.ws = ws.data_ptr()
+        L.check(L.lib().avc_gemm_bnb(d, bb, stream()), "avc_gemm_bnb")
+        return None
     if bn_fin is None:
         L.check(L.lib().avc_gemm(d, stream()), "avc_gemm")
         return None
@@ -226,6 +241,20 @@ def bn_bwd(dA, a, y, mean, rstd, gamma, act, need_dbias=True, into=None, twin16=
            int(into is not None), ws.data_ptr(), stream())
     out = d16 if dy_bf16 else attach_twin(dy, d16)
     return out, dgamma, dbeta, dbias
+
+
+def bn_bwd_apply(dA, y, coef, act, dy_bf16=False, twin16=None):
+    """The apply half of the BN backward with avc_gemm_bnb's constants (see bn_bwd)."""
+    M, C = y.shape
+    dev = y.device
+    if dy_bf16:
+        dy, d16 = None, torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+    else:
+        dy = torch.empty(M, C, device=dev)
+        d16 = _twin_buf(dy, twin16)
+    L.call("avc_bn_bwd_apply", dA.data_ptr(), _dt(dA), y.data_ptr(), _dt(y), coef.data_ptr(), M, C, int(act),
+           _ptr(dy), _ptr(d16), stream())
+    return d16 if dy_bf16 else attach_twin(dy, d16)
 
 
 def colsum(x, M, N, ld=None, out=None, accumulate=False, out2=None):

@@ -361,7 +361,10 @@ class ConvBNCore:
         a = K.bn_apply(y, scale, shift, self.act, residual, out_bf16=out_bf16 and bf and residual is None)
         return a, (y, mean, rstd, T_out)
 
-    def backward(self, dA, x, a, saved, B, T_in, n_dx):
+    def backward(self, dA, x, a, saved, B, T_in, n_dx, self_link=None, prev_link=None):
+        """self_link: this layer's BnbLink (its BN backward statistics may already have been
+        computed by the consumer's data-gradient GEMM); prev_link: the link of the conv + BN
+        layer that produced x, whose statistics this layer's data-gradient GEMM computes."""
         y, mean, rstd, T_out = saved
         if not self.bn.training:
             raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
@@ -369,11 +372,21 @@ class ConvBNCore:
         Co, Ci, Kw = conv.weight.shape
         M = B * T_out
         sink = _SINK["on"]
-        into = (_grad_of(bn.weight), _grad_of(bn.bias), _grad_of(conv.bias)) if sink else None
-        # act' from the recomputed pre-activation: the activation output `a` is not re-read
-        # bf16 mode: dy feeds the two bf16 GEMMs below only -> stored in bf16 alone
-        dy, dgamma, dbeta, dbias = K.bn_bwd(dA, None, y, mean, rstd, bn.weight, self.act, into=into, beta=bn.bias,
-                                            dy_bf16=K.compute() == K.BF16)
+        dy_bf16 = K.compute() == K.BF16
+        if self_link is not None and self_link.coef is not None:
+            # statistics (and the parameter gradients) came from the consumer's GEMM epilogue
+            if dA.data_ptr() != self_link.dA_ptr:
+                raise RuntimeError("fused BatchNorm backward: dL/da is not the linked consumer's data gradient "
+                                   "(the output was used twice?)")
+            dy = K.bn_bwd_apply(dA, y, self_link.coef, self.act, dy_bf16=dy_bf16)
+            dgamma, dbeta, dbias = self_link.grads
+            self_link.coef = None
+        else:
+            into = (_grad_of(bn.weight), _grad_of(bn.bias), _grad_of(conv.bias)) if sink else None
+            # act' from the recomputed pre-activation: the activation output `a` is not re-read
+            # bf16 mode: dy feeds the two bf16 GEMMs below only -> stored in bf16 alone
+            dy, dgamma, dbeta, dbias = K.bn_bwd(dA, None, y, mean, rstd, bn.weight, self.act, into=into,
+                                                beta=bn.bias, dy_bf16=dy_bf16)
 
         def wgrad():
             return conv_wgrad(dy, x, B, T_in, T_out, conv.weight, self.pad,
@@ -383,8 +396,11 @@ class ConvBNCore:
         if n_dx:
             _, Wd = self.packs()
             dx = torch.empty(B * T_in, n_dx, device=x.device, dtype=x.dtype)
+            bnb = prev_link.gemm_args(B * T_in, n_dx, sink) if prev_link is not None and n_dx == Ci else None
             K.gemm(B * T_in, n_dx, Kw * Co, operand(dy, Co, window=(Kw, Kw - 1 - self.pad, T_in, T_out, Co)),
-                   operand(Wd, Kw * Co), dx)
+                   operand(Wd, Kw * Co), dx, bnb=bnb)
+            if bnb is not None:
+                prev_link.dA_ptr = dx.data_ptr()
         if sink and (n_dx or not _LAST_WGRAD_MAIN):
             with _Side(ev) as sd:
                 sd.keep(dy, x)
@@ -402,14 +418,60 @@ class ConvBNCore:
         return dx, dW, dbias, dgamma, dbeta
 
 
+class BnbLink:
+    """A conv + BN + act layer whose output feeds ONE consumer conv_bn (fuse_prev=True at the call
+    site, where the model code guarantees the single use): the consumer's data-gradient GEMM
+    computes this layer's BatchNorm backward statistics and parameter gradients in its epilogue
+    (avc_gemm_bnb), and this layer's backward runs only the apply pass -- the separate reduce
+    and finalize launches of nn.BatchNorm1d.backward's statistics (AutoVC.py:38,91,138,154,169)
+    are gone.  One-shot per forward."""
+
+    __slots__ = ("core", "saved", "coef", "dA_ptr", "grads")
+
+    def __init__(self, core, saved):
+        self.core, self.saved = core, saved
+        self.coef, self.dA_ptr, self.grads = None, None, (None, None, None)
+
+    def gemm_args(self, M, C, sink):
+        core = self.core
+        y, mean, rstd, _ = self.saved
+        if y.shape != (M, C):
+            return None
+        bn, conv = core.bn, core.conv
+        dev = y.device
+        if sink:
+            dg, db, dbi = _grad_of(bn.weight), _grad_of(bn.bias), (_grad_of(conv.bias) if conv.bias is not None else None)
+            self.grads = (None, None, None)
+        else:
+            dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
+            dbi = torch.empty(C, device=dev) if conv.bias is not None else None
+            self.grads = (dg, db, dbi)
+        self.coef = torch.empty(6 * C, device=dev)
+        return (y, mean, rstd, bn.weight, bn.bias, core.act, self.coef, dg, db, dbi, int(sink))
+
+
+def _links(ctx, x, core, a, saved, fuse_prev):
+    """Forward bookkeeping of the fused BN-backward statistics (BnbLink), bf16 training only."""
+    on = _BNB_ON and K.compute() == K.BF16 and core.bn.training
+    ctx.self_link = BnbLink(core, saved) if on else None
+    if on:
+        a._bnb_link = ctx.self_link
+    prev = getattr(x, "_bnb_link", None) if (on and fuse_prev) else None
+    ctx.prev_link = prev if (prev is not None and prev.core.bn.training) else None
+
+
+_BNB_ON = os.environ.get("AVC_BNB", "1") != "0"
+
+
 class _ConvBNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, core, B, T_in, residual, out_bf16, w, b, gamma, beta):
+    def forward(ctx, x, core, B, T_in, residual, out_bf16, fuse_prev, w, b, gamma, beta):
         a, saved = core.forward(x, B, T_in, residual, out_bf16)
         ctx.core, ctx.B, ctx.T_in, ctx.saved = core, B, T_in, saved
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, a)
         ctx.x16 = getattr(x, "_bf16", None)
+        _links(ctx, x, core, a, saved, fuse_prev)
         return a
 
     @staticmethod
@@ -418,16 +480,19 @@ class _ConvBNFn(torch.autograd.Function):
         K.attach_twin(x, ctx.x16)
         dA = dA.contiguous()
         n_dx = x.shape[1] if ctx.needs_input_grad[0] else 0
-        dx, dW, db, dg, dbe = ctx.core.backward(dA, x, a, ctx.saved, ctx.B, ctx.T_in, n_dx)
+        dx, dW, db, dg, dbe = ctx.core.backward(dA, x, a, ctx.saved, ctx.B, ctx.T_in, n_dx, self_link=ctx.self_link,
+                                                prev_link=ctx.prev_link)
         dres = dA if ctx.has_res and ctx.needs_input_grad[4] else None
-        return dx, None, None, None, dres, None, dW, db, dg, dbe
+        return dx, None, None, None, dres, None, None, dW, db, dg, dbe
 
 
-def conv_bn(core: ConvBNCore, x, B, T_in, residual=None, out_bf16=False):
+def conv_bn(core: ConvBNCore, x, B, T_in, residual=None, out_bf16=False, fuse_prev=False):
     """out_bf16: the caller feeds the result only to another conv_bn / lstm (bf16 storage in
-    bf16 compute mode, see ConvBNCore.forward)."""
+    bf16 compute mode, see ConvBNCore.forward).  fuse_prev: x is the output of a conv_bn /
+    enc_conv0 used by this layer alone -- its BatchNorm backward statistics ride on this layer's
+    data-gradient GEMM (BnbLink)."""
     c, bn = core.conv, core.bn
-    return _ConvBNFn.apply(x, core, B, T_in, residual, out_bf16, c.weight, c.bias, bn.weight, bn.bias)
+    return _ConvBNFn.apply(x, core, B, T_in, residual, out_bf16, fuse_prev, c.weight, c.bias, bn.weight, bn.bias)
 
 
 class _EncConv0Fn(torch.autograd.Function):
@@ -441,6 +506,7 @@ class _EncConv0Fn(torch.autograd.Function):
         ctx.core, ctx.B, ctx.T, ctx.saved, ctx.n_mel = core, B, T, saved, mel2d.shape[1]
         ctx.save_for_backward(x, a)
         ctx.x16 = getattr(x, "_bf16", None)
+        _links(ctx, x, core, a, saved, False)
         return a
 
     @staticmethod
@@ -452,7 +518,8 @@ class _EncConv0Fn(torch.autograd.Function):
         nm = ctx.n_mel
         demb_needed = ctx.needs_input_grad[1]
         n_dx = x.shape[1] if demb_needed else (nm if ctx.needs_input_grad[0] else 0)
-        dx, dW, db, dg, dbe = ctx.core.backward(dA.contiguous(), x, a, ctx.saved, ctx.B, ctx.T, n_dx)
+        dx, dW, db, dg, dbe = ctx.core.backward(dA.contiguous(), x, a, ctx.saved, ctx.B, ctx.T, n_dx,
+                                                self_link=ctx.self_link)
         demb = None
         if demb_needed:
             demb = K.segsum(dx[:, nm:], ctx.B, ctx.T, x.shape[1] - nm, ld=x.shape[1])

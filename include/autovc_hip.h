@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 10
+#define AVC_ABI_VERSION 11
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -84,6 +84,43 @@ const char* avc_last_error(void);
  * Discriminator.py:7-9, MLPMixer.py:53,82), nn.Linear (Norm.py:40-50, MLPMixer.py:70-76),
  * the W_ih products inside nn.LSTM (AutoVC.py:43,77,96) and all their backward GEMMs. */
 int avc_gemm(const avc_gemm_desc* d, void* stream);
+
+/* BatchNorm1d BACKWARD reduction fused into a data-gradient GEMM (avc_gemm_bnb).  The GEMM's
+ * output C is dL/da of a conv + BatchNorm + activation layer (the layer BEFORE this GEMM's own
+ * layer: e.g. the encoder's conv1 -> conv2 chain, AutoVC.py:56-58, postnet :167-170); y is that
+ * layer's stored conv output (pre-BN, [M][N] row-major like C), mean / rstd its batch
+ * statistics, gamma / beta its affine parameters, act its activation (AVC_ACT_*).  The
+ * epilogue recomputes dz = C * act'(z), z = (y - mean)*rstd*gamma + beta, sums dz, dz*yhat and
+ * yhat per column and 128-row tile, and the last row tile of each column tile writes the
+ * planar apply constants coef[6][N] (16-B aligned; k1 = gamma*rstd, mean(dz), mean(dz*yhat),
+ * mean, rstd, beta) and dgamma / dbeta / the conv-bias gradient (accumulated when accumulate
+ * != 0; nullable) -- what avc_bn_bwd's reduce + finalize passes compute; avc_bn_bwd_apply
+ * then finishes the layer.  ws: avc_gemm_bnb_ws(M, N) floats.  Replaces the statistics half
+ * of nn.BatchNorm1d.backward (AutoVC.py:38,91,138,154,169). */
+typedef struct {
+  const void* y;
+  int y_dtype;
+  const float* mean;
+  const float* rstd;
+  const float* gamma;
+  const float* beta;
+  int act;
+  float* coef;
+  float* dgamma;
+  float* dbeta;
+  float* dbias;
+  int accumulate;
+  float* ws;
+} avc_bnb_args;
+
+size_t avc_gemm_bnb_ws(int M, int N);
+int avc_gemm_bnb(const avc_gemm_desc* d, const avc_bnb_args* bnb, void* stream);
+
+/* The apply half of the BatchNorm backward with the constants of avc_gemm_bnb:
+ * dy = k1*(dz - mean(dz) - yhat*mean(dz*yhat)), dz from the pre-activation recomputed from y.
+ * dy fp32 and/or bf16 (dy_bf16), either nullable but not both. */
+int avc_bn_bwd_apply(const void* dA, int dA_dtype, const void* y, int y_dtype, const float* coef, int M, int C,
+                     int act, float* dy, void* dy_bf16, void* stream);
 
 /* BatchNorm1d training-mode statistics from avc_gemm's bn_partial: mean/rstd per
  * channel, scale = gamma*rstd, shift = beta - mean*scale, running-stat update with

@@ -716,3 +716,85 @@ def test_lstm2_wavefront_autograd_matches_layerwise():
     assert relf(dxa, dxb) < 2e-2, relf(dxa, dxb)
     for a, b in zip(ga, gb):
         assert relf(a, b) < 2e-2, relf(a, b)
+
+
+@pytest.mark.parametrize("out_bf16", [True, False])
+@pytest.mark.parametrize("act_name", ["relu", "tanh"])
+def test_gemm_bnb_matches_separate_bn_backward(out_bf16, act_name):
+    """avc_gemm_bnb (the producing layer's BatchNorm backward statistics in the GEMM epilogue,
+    last-row-tile finalize) + avc_bn_bwd_apply equal avc_bn_bwd's reduce / finalize / apply
+    passes over the same GEMM output: dy, dgamma, dbeta and the conv-bias gradient."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute("bf16")
+    act = {"relu": Kr.ACT_RELU, "tanh": Kr.ACT_TANH}[act_name]
+    M, N, Kd = 1000, 320, 256  # ragged row tiles (1000 = 7 x 128 + 104), 5 column tiles of 64
+    torch.manual_seed(9)
+    a = (torch.randn(M, Kd) * 0.5).bfloat16().to(DEV)
+    w = (torch.randn(N, Kd) * 0.05).bfloat16().to(DEV)
+    y = (torch.randn(M, N) * 1.3 + 0.2).bfloat16().to(DEV)
+    mean = y.float().mean(0)
+    rstd = 1.0 / (y.float().var(0, unbiased=False) + 1e-5).sqrt()
+    gamma = (torch.rand(N) + 0.5).to(DEV)
+    beta = (torch.randn(N) * 0.2).to(DEV)
+    dt = torch.bfloat16 if out_bf16 else torch.float32
+    c_ref = torch.empty(M, N, device=DEV, dtype=dt)
+    Kr.gemm(M, N, Kd, Kr.operand(a, Kd), Kr.operand(w, Kd), c_ref)
+    dy_ref, dg_ref, db_ref, dbi_ref = Kr.bn_bwd(c_ref, None, y, mean, rstd, gamma, act, beta=beta)
+    c = torch.empty(M, N, device=DEV, dtype=dt)
+    coef = torch.empty(6 * N, device=DEV)
+    dg, db, dbi = (torch.full((N,), 0.25, device=DEV) for _ in range(3))  # accumulate onto 0.25
+    Kr.gemm(M, N, Kd, Kr.operand(a, Kd), Kr.operand(w, Kd), c,
+            bnb=(y, mean, rstd, gamma, beta, act, coef, dg, db, dbi, 1))
+    dy = Kr.bn_bwd_apply(c, y, coef, act)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(c, c_ref, rtol=0, atol=0)
+    assert relf(dy, dy_ref) < 1e-5, relf(dy, dy_ref)
+    assert relf(dg - 0.25, dg_ref) < 1e-5
+    assert relf(db - 0.25, db_ref) < 1e-5
+    assert float((dbi - 0.25 - dbi_ref).abs().max()) < 1e-4 * max(float(dbi_ref.abs().max()), 1e-3)
+
+
+def test_conv_chain_fused_bn_backward_matches_separate():
+    """Three conv_bn layers (the encoder chain, AutoVC.py:46-58) with fuse_prev: output and every
+    parameter / input gradient equal the chain run with the fusion off (AVC_BNB=0 path)."""
+    import autoformer_amd as A
+    from autoformer_amd import layers as Ly
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute("bf16")
+    Ly.set_grad_sink(False)
+    B, T, C = 8, 64, 512
+    torch.manual_seed(10)
+    mods = []
+    for i in range(3):
+        conv = torch.nn.Conv1d(C if i else 80, C, 5, padding=2).to(DEV)
+        bn = torch.nn.BatchNorm1d(C).to(DEV).train()
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.normal_(0, 0.1)
+        mods += [conv, bn]
+    cores = [Ly.ConvBNCore(mods[2 * i], mods[2 * i + 1], Kr.ACT_RELU) for i in range(3)]
+    x0 = torch.randn(B * T, 80, device=DEV)
+    res = []
+    for on in (True, False):
+        Ly._BNB_ON = on
+        try:
+            for m in mods:
+                m.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            h = Ly.conv_bn(cores[0], x, B, T, out_bf16=True)
+            h = Ly.conv_bn(cores[1], h, B, T, out_bf16=True, fuse_prev=True)
+            h = Ly.conv_bn(cores[2], h, B, T, fuse_prev=True)
+            (h.float() * torch.linspace(-1, 1, C, device=DEV)).sum().backward()
+            torch.cuda.synchronize()
+            res.append((h.detach().float().clone(), x.grad.clone(),
+                        [p.grad.clone() for m in mods for p in m.parameters()]))
+        finally:
+            Ly._BNB_ON = True
+    (ha, dxa, ga), (hb, dxb, gb) = res
+    torch.testing.assert_close(ha, hb, rtol=0, atol=0)
+    assert relf(dxa, dxb) < 2e-3, relf(dxa, dxb)
+    for p, q in zip(ga, gb):
+        assert relf(p, q) < 2e-3 or float((p - q).abs().max()) < 1e-4, relf(p, q)
