@@ -753,7 +753,10 @@ def test_gemm_bnb_matches_separate_bn_backward(out_bf16, act_name):
     assert relf(dy, dy_ref) < 1e-5, relf(dy, dy_ref)
     assert relf(dg - 0.25, dg_ref) < 1e-5
     assert relf(db - 0.25, db_ref) < 1e-5
-    assert float((dbi - 0.25 - dbi_ref).abs().max()) < 1e-4 * max(float(dbi_ref.abs().max()), 1e-3)
+    # the conv-bias gradient of a conv feeding training-mode BN is analytically zero: both sides
+    # are cancellation residue of sums whose terms have dbeta's scale (plus 0.25's fp32 ulp)
+    tol = 1e-5 * float(db_ref.abs().max()) + 4 * 2.0 ** -25
+    assert float((dbi - 0.25 - dbi_ref).abs().max()) < tol, float((dbi - 0.25 - dbi_ref).abs().max())
 
 
 def test_conv_chain_fused_bn_backward_matches_separate():
