@@ -193,6 +193,95 @@ __global__ void loss_grad_kernel(const float* a, const float* b, long long n, co
   g[i] = sign * dloss[0] * f / (float)n;
 }
 
+// The loss block of Solver.train (train.py:84-96) in one launch: grid-stride partial sums of
+// (x - y1)^2, (x - y2)^2 over n1 and |ca - cb| over n2 (float4 loads when 16-B aligned), block
+// partials handed over with write-through stores, the last-arriving block sums them in block
+// order (deterministic, no zeroing launch) and writes the three means and the weighted total.
+constexpr int VCL_GRID = 256;
+__global__ void __launch_bounds__(256) vc_loss_kernel(const float* __restrict__ x, const float* __restrict__ y1,
+                                                      const float* __restrict__ y2, long long n1,
+                                                      const float* __restrict__ ca, const float* __restrict__ cb,
+                                                      long long n2, float lam, float* out, float* ws, unsigned* cnt,
+                                                      int vec) {
+  __shared__ float red[3][4];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (vec) {
+    const long long q1 = n1 / 4;
+    for (long long i = i0; i < q1; i += stride) {
+      const f32x4 a = reinterpret_cast<const f32x4*>(x)[i];
+      const f32x4 d1 = a - reinterpret_cast<const f32x4*>(y1)[i];
+      const f32x4 d2 = a - reinterpret_cast<const f32x4*>(y2)[i];
+      s0 += d1[0] * d1[0] + d1[1] * d1[1] + d1[2] * d1[2] + d1[3] * d1[3];
+      s1 += d2[0] * d2[0] + d2[1] * d2[1] + d2[2] * d2[2] + d2[3] * d2[3];
+    }
+    for (long long i = 4 * q1 + i0; i < n1; i += stride) {
+      const float d1 = x[i] - y1[i], d2 = x[i] - y2[i];
+      s0 += d1 * d1;
+      s1 += d2 * d2;
+    }
+  } else {
+    for (long long i = i0; i < n1; i += stride) {
+      const float d1 = x[i] - y1[i], d2 = x[i] - y2[i];
+      s0 += d1 * d1;
+      s1 += d2 * d2;
+    }
+  }
+  for (long long i = i0; i < n2; i += stride) s2 += fabsf(ca[i] - cb[i]);
+  s0 = warp_sum(s0);
+  s1 = warp_sum(s1);
+  s2 = warp_sum(s2);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = s0;
+    red[1][w] = s1;
+    red[2][w] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const float* r = red[threadIdx.x];
+    st_sc1(ws + (long long)blockIdx.x * 3 + threadIdx.x, r[0] + r[1] + r[2] + r[3]);
+  }
+  if (!arrive_last(cnt, gridDim.x)) return;
+  if (threadIdx.x < 64) {
+    // lane q < 3 sums partial q over the blocks in order
+    float t = 0.f;
+    if (threadIdx.x < 3)
+      for (int b = 0; b < (int)gridDim.x; ++b) t += ld_sc1(ws + (long long)b * 3 + threadIdx.x);
+    const float m0 = __shfl(t, 0, 64) / (float)n1, m1 = __shfl(t, 1, 64) / (float)n1;
+    const float m2 = n2 > 0 ? __shfl(t, 2, 64) / (float)n2 : 0.f;
+    if (threadIdx.x == 0) {
+      out[0] = m0;
+      out[1] = m1;
+      out[2] = m2;
+      out[3] = m0 + m1 + lam * m2;
+    }
+  }
+}
+
+__device__ __forceinline__ float dval(const float* p) { return p ? *p : 0.f; }
+
+__global__ void vc_loss_grad_kernel(const float* __restrict__ x, const float* __restrict__ y1,
+                                    const float* __restrict__ y2, long long n1, const float* __restrict__ ca,
+                                    const float* __restrict__ cb, long long n2, float lam, const float* d0,
+                                    const float* d1, const float* d2, const float* d3, float* g1, float* g2,
+                                    float* ga, float* gb) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const float t3 = dval(d3);
+  if (i < n1) {
+    const float xv = x[i];
+    if (g1) g1[i] = (t3 + dval(d0)) * 2.f * (y1[i] - xv) / (float)n1;
+    if (g2) g2[i] = (t3 + dval(d1)) * 2.f * (y2[i] - xv) / (float)n1;
+  } else if (i < n1 + n2) {
+    const long long k = i - n1;
+    const float d = ca[k] - cb[k];
+    const float v = (lam * t3 + dval(d2)) * (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) / (float)n2;
+    if (ga) ga[k] = v;
+    if (gb) gb[k] = -v;
+  }
+}
+
 // Batched weight packing (avc_pack_batch).  The launch is cut into UNITS: 1024 elements of an
 // elementwise op (copy / add / conv re-layout, walked along the source, 4 per thread), or one
 // 32 x 32 tile of a transpose (staged through LDS so both the fp32 reads and the bf16 writes are
@@ -432,6 +521,30 @@ extern "C" int avc_loss_grad(const float* a, const float* b, long long n, const 
   AVC_CHECK_ARG(a && b && dloss && g, "avc_loss_grad: null");
   loss_grad_kernel<<<GRID1(n)>>>(a, b, n, dloss, mode, g, sign);
   return avc_check_launch("avc_loss_grad");
+}
+
+extern "C" size_t avc_vc_loss_ws(void) { return (size_t)VCL_GRID * 3; }
+
+extern "C" int avc_vc_loss(const float* x, const float* y1, const float* y2, long long n1, const float* ca,
+                           const float* cb, long long n2, float lambda_cd, float* out, float* ws, void* stream) {
+  AVC_CHECK_ARG(x && y1 && y2 && out && ws && n1 > 0 && n2 >= 0 && (n2 == 0 || (ca && cb)), "avc_vc_loss: bad args");
+  hipStream_t s = as_stream(stream);
+  unsigned* cnt = avc_counter_slots(1, s);
+  if (!cnt) return -1;
+  const int vec = (((uintptr_t)x | (uintptr_t)y1 | (uintptr_t)y2) & 15) == 0;
+  const int grid = (int)std::min<long long>(VCL_GRID, std::max<long long>(1, cdiv(std::max(n1 / 4, n2), 256)));
+  vc_loss_kernel<<<grid, 256, 0, s>>>(x, y1, y2, n1, ca, cb, n2, lambda_cd, out, ws, cnt, vec);
+  return avc_check_launch("avc_vc_loss");
+}
+
+extern "C" int avc_vc_loss_grad(const float* x, const float* y1, const float* y2, long long n1, const float* ca,
+                                const float* cb, long long n2, float lambda_cd, const float* d0, const float* d1,
+                                const float* d2, const float* d3, float* g1, float* g2, float* ga, float* gb,
+                                void* stream) {
+  AVC_CHECK_ARG(x && y1 && y2 && n1 > 0 && n2 >= 0 && (n2 == 0 || (ca && cb)), "avc_vc_loss_grad: bad args");
+  const long long n = n1 + n2;
+  vc_loss_grad_kernel<<<GRID1(n)>>>(x, y1, y2, n1, ca, cb, n2, lambda_cd, d0, d1, d2, d3, g1, g2, ga, gb);
+  return avc_check_launch("avc_vc_loss_grad");
 }
 
 extern "C" int avc_pack_batch(const avc_pack_op* ops, const long long* prefix, int nops, long long total,

@@ -534,6 +534,25 @@ def loss_grad(a, b, dloss, mode, sign):
     return g
 
 
+def vc_loss(x, y1, y2, ca, cb, lambda_cd):
+    """The loss block of Solver.train in one launch (avc_vc_loss): a (4,) device tensor
+    [mse(x, y1), mse(x, y2), l1(ca, cb), total]."""
+    out = torch.empty(4, device=x.device)
+    ws = torch.empty(int(L.lib().avc_vc_loss_ws()), device=x.device)
+    L.call("avc_vc_loss", x.data_ptr(), y1.data_ptr(), y2.data_ptr(), x.numel(), ca.data_ptr(), cb.data_ptr(),
+           ca.numel(), float(lambda_cd), out.data_ptr(), ws.data_ptr(), stream())
+    return out
+
+
+def vc_loss_grad(x, y1, y2, ca, cb, lambda_cd, d, need):
+    """Gradients of vc_loss's outputs (avc_vc_loss_grad): d = 4 upstream device scalars (or
+    None), need = (y1, y2, ca, cb) flags; returns the four gradients (None where not needed)."""
+    outs = [torch.empty_like(t) if nd else None for t, nd in zip((y1, y2, ca, cb), need)]
+    L.call("avc_vc_loss_grad", x.data_ptr(), y1.data_ptr(), y2.data_ptr(), x.numel(), ca.data_ptr(), cb.data_ptr(),
+           ca.numel(), float(lambda_cd), *[_ptr(t) for t in d], *[_ptr(t) for t in outs], stream())
+    return outs
+
+
 def adam(p, g, m, v, lr, beta1, beta2, eps, state, advance=True):
     L.call("avc_adam", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), float(lr), float(beta1),
            float(beta2), float(eps), state.data_ptr(), int(advance), stream())

@@ -104,6 +104,42 @@ def gan_extra(D):
     return extra
 
 
+class _VCLossFn(torch.autograd.Function):
+    """The loss block of Solver.train (train.py:84-96) as one launch forward and one backward:
+    (total, l_id, l_id_psnt, l_cd) with total = l_id + l_id_psnt + lambda_cd * l_cd, where
+    l_id = F.mse_loss(x_real, x_identic), l_id_psnt = F.mse_loss(x_real, x_identic_psnt),
+    l_cd = F.l1_loss(code_real, code_reconst).  The separate losses' kernels, their zeroing
+    memsets and the scalar adds / multiply of the reference's expression are gone; the upstream
+    gradients of all four outputs reach the one gradient kernel as device scalars."""
+
+    @staticmethod
+    def forward(ctx, x, y1, y2, ca, cb, lambda_cd):
+        x, y1, y2 = x.contiguous(), y1.reshape(x.shape).contiguous(), y2.reshape(x.shape).contiguous()
+        ca, cb = ca.contiguous(), cb.reshape(ca.shape).contiguous()
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(x, y1, y2, ca, cb)
+        ctx.lam = float(lambda_cd)
+        out = K.vc_loss(x, y1, y2, ca, cb, ctx.lam)
+        return out[3], out[0], out[1], out[2]
+
+    @staticmethod
+    def backward(ctx, d_total, d_id, d_psnt, d_cd):
+        x, y1, y2, ca, cb = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        d = [t.contiguous() if t is not None else None for t in (d_id, d_psnt, d_cd, d_total)]
+        # x_real is data in train.py; its gradient (rare) is -(g1 + g2)
+        n1, n2 = need[1] or need[0], need[2] or need[0]
+        g1, g2, ga, gb = K.vc_loss_grad(x, y1, y2, ca, cb, ctx.lam, d, (n1, n2, need[3], need[4]))
+        gx = -(g1 + g2) if need[0] else None
+        return gx, g1 if need[1] else None, g2 if need[2] else None, ga, gb, None
+
+
+def vc_loss_block(x_real, x_id, x_id_psnt, code_real, code_re, lambda_cd=1.0):
+    """(total, (l_id, l_id_psnt, l_cd)) of train.py:84-96, fused (_VCLossFn)."""
+    total, l_id, l_psnt, l_cd = _VCLossFn.apply(x_real, x_id, x_id_psnt, code_real, code_re, lambda_cd)
+    return total, (l_id, l_psnt, l_cd)
+
+
 def mse_loss(a, b):
     return _MSEFn.apply(a, b.reshape(a.shape))
 
@@ -115,33 +151,28 @@ def l1_loss(a, b):
 def vc_losses(model, x_real, emb, lambda_cd=1.0):
     """The loss block of Solver.train (train.py:84-96)."""
     x_id, x_id_psnt, code_real = model(x_real, emb, emb)
-    l_id = mse_loss(x_real, x_id.squeeze())
-    l_id_psnt = mse_loss(x_real, x_id_psnt.squeeze())
     code_re = model(x_id_psnt, emb, None)
-    l_cd = l1_loss(code_real, code_re)
-    return l_id + l_id_psnt + lambda_cd * l_cd, (l_id, l_id_psnt, l_cd), x_id_psnt
+    total, parts = vc_loss_block(x_real, x_id.squeeze(), x_id_psnt.squeeze(), code_real, code_re, lambda_cd)
+    return total, parts, x_id_psnt
 
 
 def adain_losses(model, x_real, emb, lambda_cd=1.0):
     """train.py's loss block with isadain=True (train.py:89-92) for the AdaIN variants
     (AutoVC2 & co.), whose c_trg=None pass returns (codes, features) (AutoVC2.py:219-220)."""
     x_id, x_id_psnt, code_real = model(x_real, emb, emb)
-    l_id = mse_loss(x_real, x_id.squeeze())
-    l_id_psnt = mse_loss(x_real, x_id_psnt.squeeze())
     code_re, _ = model(x_id_psnt, emb, None)
-    l_cd = l1_loss(code_real, code_re)
-    return l_id + l_id_psnt + lambda_cd * l_cd, (l_id, l_id_psnt, l_cd), x_id_psnt
+    total, parts = vc_loss_block(x_real, x_id.squeeze(), x_id_psnt.squeeze(), code_real, code_re, lambda_cd)
+    return total, parts, x_id_psnt
 
 
 def adjust_losses(model, x_real, emb, lambda_cd=1.0, lambda_ad=1.0):
     """The loss block of train_with_adjust.py:Solver.train (train_with_adjust.py:96-124)."""
     emb_adjust, x_id, x_id_psnt, code_real = model(x_real, emb, emb)
-    l_id = mse_loss(x_real, x_id.squeeze())
-    l_id_psnt = mse_loss(x_real, x_id_psnt.squeeze())
     code_re = model(x_id_psnt, emb, None)
-    l_cd = l1_loss(code_real, code_re)
+    total, (l_id, l_id_psnt, l_cd) = vc_loss_block(x_real, x_id.squeeze(), x_id_psnt.squeeze(), code_real, code_re,
+                                                   lambda_cd)
     l_ad = l1_loss(emb_adjust, emb)
-    return (l_id + l_id_psnt + lambda_cd * l_cd + lambda_ad * l_ad, (l_id, l_id_psnt, l_cd, l_ad), x_id_psnt)
+    return (total + lambda_ad * l_ad, (l_id, l_id_psnt, l_cd, l_ad), x_id_psnt)
 
 
 def losses_for(model):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 11
+#define AVC_ABI_VERSION 12
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -301,6 +301,23 @@ int avc_l1_loss(const float* a, const float* b, long long n, float* out, void* s
 /* g = scale * dL * (mode 0: 2(a-b)/n ; mode 1: sign(a-b)/n) ; dL = *dloss (device) */
 int avc_loss_grad(const float* a, const float* b, long long n, const float* dloss, int mode, float* g,
                   float sign, void* stream);
+/* The whole loss block of Solver.train in ONE launch (train.py:84-96): with x = x_real (n1),
+ * y1 = x_identic, y2 = x_identic_psnt (n1 each), ca = code_real, cb = code_reconst (n2)
+ *   out[0] = mean((x - y1)^2), out[1] = mean((x - y2)^2), out[2] = mean|ca - cb|,
+ *   out[3] = out[0] + out[1] + lambda_cd * out[2]
+ * Block partials are handed over in-kernel and summed in a fixed order by the last-arriving
+ * block (deterministic; no zeroing launch).  Replaces 3 avc_mse_loss/avc_l1_loss + the adds.
+ * ws: avc_vc_loss_ws() floats of caller-owned scratch (not shared with a concurrent call). */
+size_t avc_vc_loss_ws(void);
+int avc_vc_loss(const float* x, const float* y1, const float* y2, long long n1, const float* ca, const float* cb,
+                long long n2, float lambda_cd, float* out, float* ws, void* stream);
+/* Its gradient, one launch: with the upstream gradients d[0..3] of out[0..3] (device scalars,
+ * each pointer may be null = 0) and c_id = d3 + d0, c_psnt = d3 + d1, c_cd = lambda_cd*d3 + d2:
+ *   g1 = c_id * 2(y1 - x)/n1, g2 = c_psnt * 2(y2 - x)/n1, ga = c_cd * sign(ca - cb)/n2, gb = -ga
+ * (any output pointer may be null: not computed). */
+int avc_vc_loss_grad(const float* x, const float* y1, const float* y2, long long n1, const float* ca,
+                     const float* cb, long long n2, float lambda_cd, const float* d0, const float* d1,
+                     const float* d2, const float* d3, float* g1, float* g2, float* ga, float* gb, void* stream);
 
 /* Activation-only passes (Discriminator's conv -> LeakyReLU -> BN order,
  * factory/Discriminator.py:18-29); the backward takes the activation OUTPUT. */

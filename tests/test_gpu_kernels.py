@@ -801,3 +801,37 @@ def test_conv_chain_fused_bn_backward_matches_separate():
     assert relf(dxa, dxb) < 2e-3, relf(dxa, dxb)
     for p, q in zip(ga, gb):
         assert relf(p, q) < 2e-3 or float((p - q).abs().max()) < 1e-4, relf(p, q)
+
+
+@pytest.mark.parametrize("n1,n2,off", [(64 * 128 * 80, 64 * 8 * 88, 0), (1001, 37, 1), (5, 0, 0)])
+def test_vc_loss_block_matches_torch(n1, n2, off):
+    """avc_vc_loss / avc_vc_loss_grad (the fused loss block of train.py:84-96) against
+    F.mse_loss / F.l1_loss in fp64: values, the weighted total, and the gradients for upstream
+    gradients on the total AND on the separate terms (off = 1: unaligned, scalar-load path)."""
+    from autoformer_amd.train import vc_loss_block
+
+    torch.manual_seed(3)
+    x = torch.randn(n1).to(DEV)
+    y1 = (torch.randn(n1) * 0.7).to(DEV)
+    y2 = (torch.randn(n1) * 1.3).to(DEV)
+    if off:  # misaligned views into a larger buffer
+        big = torch.randn(3 * n1 + 3, device=DEV)
+        x, y1, y2 = big[1:1 + n1], big[n1 + 2:2 * n1 + 2], big[2 * n1 + 3:3 * n1 + 3]
+    ca, cb = torch.randn(max(n2, 1)).to(DEV)[:n2], torch.randn(max(n2, 1)).to(DEV)[:n2]
+    lam = 0.75
+    y1r, y2r, car, cbr = (t.detach().clone().requires_grad_(True) for t in (y1, y2, ca, cb))
+    total, (l_id, l_ps, l_cd) = vc_loss_block(x, y1r, y2r, car, cbr, lam)
+    xd, y1d, y2d, cad, cbd = (t.detach().cpu().double().requires_grad_(True) for t in (x, y1, y2, ca, cb))
+    r_id = F.mse_loss(y1d, xd)
+    r_ps = F.mse_loss(y2d, xd)
+    r_cd = F.l1_loss(cad, cbd) if n2 else torch.zeros((), dtype=torch.float64)
+    r_tot = r_id + r_ps + lam * r_cd
+    for a, b in ((l_id, r_id), (l_ps, r_ps), (l_cd, r_cd), (total, r_tot)):
+        assert abs(float(a) - float(b)) <= 1e-5 * max(abs(float(b)), 1e-6), (float(a), float(b))
+    (2.0 * total + 0.5 * l_ps + 3.0 * l_cd).backward()
+    (2.0 * r_tot + 0.5 * r_ps + 3.0 * r_cd).backward()
+    assert relf(y1r.grad, y1d.grad) < 1e-5
+    assert relf(y2r.grad, y2d.grad) < 1e-5
+    if n2:
+        assert relf(car.grad, cad.grad) < 1e-5
+        assert relf(cbr.grad, cbd.grad) < 1e-5
