@@ -648,7 +648,7 @@ __global__ void __launch_bounds__(256, 2) gemm_fast_kernel(GemmArgs g) {
     __syncthreads();
   }
 
-  fast_epilogue<BN_>(g, acc, m0, n0, mt, bz, ks, smem_raw);
+  fast_epilogue<BN_, !AKS && !BKS>(g, acc, m0, n0, mt, bz, ks, smem_raw);  // bnb: non-TT layouts only
 }
 
 template <int BN_, bool AKS, bool BKS, int ADT, int BDT>

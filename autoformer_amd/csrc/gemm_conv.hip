@@ -60,7 +60,9 @@ struct ConvCfg {
   __device__ static __forceinline__ int swz(int r) { return (r >> 1) & (CPR - 1); }
 };
 
-template <int TAPS, int NST, int CBK, int CBN>
+// BNB: the BatchNorm-backward epilogue compiled in (only the instances launched with bnb: its
+// code in every conv instance cost 20 % of the conv time, measured)
+template <int TAPS, int NST, int CBK, int CBN, bool BNB>
 __global__ void __launch_bounds__(256, 2) gemm_conv_kernel(GemmArgs g) {
   using C = ConvCfg<TAPS, CBK, CBN>;
   constexpr int STAGE = C::STAGE, LPT = C::LPT, AI4 = C::AI / 4, BI4 = C::BI / 4, P = NST - 1;
@@ -192,21 +194,21 @@ __global__ void __launch_bounds__(256, 2) gemm_conv_kernel(GemmArgs g) {
     }
   }
   __syncthreads();  // last wait was vmcnt(0); every fragment read done before the epilogue reuses LDS
-  fast_epilogue<CBN>(g, acc, m0, n0, mt, 0, 0, smem_raw);
+  fast_epilogue<CBN, BNB>(g, acc, m0, n0, mt, 0, 0, smem_raw);
 }
 
-template <int NST, int CBK, int CBN>
+template <int NST, int CBK, int CBN, bool BNB = false>
 void launch(const GemmArgs& g, hipStream_t s) {
   using C = ConvCfg<5, CBK, CBN>;
   const size_t lds = (size_t)NST * C::STAGE;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_conv_kernel<5, NST, CBK, CBN>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_conv_kernel<5, NST, CBK, CBN, BNB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int nb = ((g.M + BM - 1) / BM) * ((g.N + CBN - 1) / CBN);
-  gemm_conv_kernel<5, NST, CBK, CBN><<<nb, 256, lds, s>>>(g);
+  gemm_conv_kernel<5, NST, CBK, CBN, BNB><<<nb, 256, lds, s>>>(g);
 }
 
 bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -241,6 +243,11 @@ bool gemm_conv_launch(const GemmArgs& g, hipStream_t s) {
   if (a.chans % bk) bk = 32;  // 32-channel stages for channel counts that are not 64-multiples
   if (a.chans % bk) return false;
   if (bk == 32 && bn == 32) bn = 64;
+  if (g.bnb_ws) {  // the BN-backward epilogue is instantiated for the default configuration only
+    if (bk != 32) return false;
+    launch<2, 32, 64, true>(g, s);
+    return true;
+  }
 #define CONV_CASE(NS, BK, BN)                  \
   if (ns == NS && bk == BK && bn == BN) {      \
     launch<NS, BK, BN>(g, s);                  \

@@ -100,7 +100,8 @@ struct NtLoader {
   }
 };
 
-template <int BN_, int NST, bool WIN>
+// BNB: the BatchNorm-backward epilogue compiled in (only for launches with bnb)
+template <int BN_, int NST, bool WIN, bool BNB>
 __global__ void __launch_bounds__(256, 1) gemm_nt_kernel(GemmArgs g) {
   constexpr int NJ = BN_ / 32, WN = BN_ / 2;
   constexpr int A_BYTES = BM * ROWB, STAGE = (BM + BN_) * ROWB;
@@ -185,19 +186,19 @@ __global__ void __launch_bounds__(256, 1) gemm_nt_kernel(GemmArgs g) {
     }
   }
   __syncthreads();  // every glds retired (last wait was vmcnt(0)) and every fragment read done
-  fast_epilogue<BN_>(g, acc, m0, n0, mt, bz, ks, smem_raw);
+  fast_epilogue<BN_, BNB>(g, acc, m0, n0, mt, bz, ks, smem_raw);
 }
 
-template <int BN_, int NST, bool WIN>
+template <int BN_, int NST, bool WIN, bool BNB = false>
 void launch(const GemmArgs& g, int nblocks, hipStream_t s) {
   const size_t lds = (size_t)NST * (BM + BN_) * ROWB;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<BN_, NST, WIN>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<BN_, NST, WIN, BNB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  gemm_nt_kernel<BN_, NST, WIN><<<nblocks, 256, lds, s>>>(g);
+  gemm_nt_kernel<BN_, NST, WIN, BNB><<<nblocks, 256, lds, s>>>(g);
 }
 
 bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -239,6 +240,16 @@ bool gemm_nt_launch(const GemmArgs& g, hipStream_t s) {
   if (nst < 2 || nst > 4) nst = 2;
   const int nb = ((g.M + BM - 1) / BM) * ((g.N + bn - 1) / bn) * g.batch * g.split_k;
   const bool win = g.a.win != 0;
+  if (g.bnb_ws) {  // BN-backward epilogue: two-stage instances only
+    if (bn == 128) {
+      if (win) launch<128, 2, true, true>(g, nb, s);
+      else launch<128, 2, false, true>(g, nb, s);
+    } else {
+      if (win) launch<64, 2, true, true>(g, nb, s);
+      else launch<64, 2, false, true>(g, nb, s);
+    }
+    return true;
+  }
 #define NT_CASE(BNV, NSV)                                   \
   if (bn == BNV && nst == NSV) {                            \
     if (win) launch<BNV, NSV, true>(g, nb, s);              \

@@ -835,3 +835,39 @@ def test_vc_loss_block_matches_torch(n1, n2, off):
     if n2:
         assert relf(car.grad, cad.grad) < 1e-5
         assert relf(cbr.grad, cbd.grad) < 1e-5
+
+
+@pytest.mark.parametrize("ydt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,C", [(1001, 520), (8192, 512), (37, 80), (50, 84)])
+def test_bn_apply_forms(ydt, M, C):
+    """avc_bn_apply / avc_bn_bwd_apply (8-channel row-looping forms when C % 8 == 0, 4-channel /
+    scalar otherwise; ragged row counts) against torch fp32 of the same formulas."""
+    from autoformer_amd import kernels as Kr
+
+    torch.manual_seed(5)
+    y = (torch.randn(M, C) * 2 + 0.3).to(ydt).to(DEV)
+    yf = y.float()
+    scale, shift = (torch.rand(C) + 0.5).to(DEV), torch.randn(C).to(DEV)
+    res = torch.randn(M, C, device=DEV)
+    for act, fn in ((Kr.ACT_RELU, torch.relu), (Kr.ACT_TANH, torch.tanh)):
+        ref = fn(yf * scale + shift)
+        out = Kr.bn_apply(y, scale, shift, act)
+        assert relf(out, ref) < 1e-6
+        out = Kr.bn_apply(y, scale, shift, act, residual=res)
+        assert relf(out, ref + res) < 1e-6
+        o16 = Kr.bn_apply(y, scale, shift, act, out_bf16=True)
+        assert o16.dtype == torch.bfloat16 and relf(o16, ref) < 4e-3
+    k1, m1, m2, mu, rs, bt = (torch.rand(C) + 0.5, torch.randn(C) * 0.1, torch.randn(C) * 0.1, torch.randn(C) * 0.2,
+                              torch.rand(C) + 0.5, torch.randn(C) * 0.3)
+    coef = torch.cat([k1, m1, m2, mu, rs, bt]).to(DEV)
+    k1, m1, m2, mu, rs, bt = (t.to(DEV) for t in (k1, m1, m2, mu, rs, bt))
+    dA = torch.randn(M, C).to(ydt).to(DEV)
+    for act in (Kr.ACT_RELU, Kr.ACT_TANH):
+        yc = yf - mu
+        z = yc * k1 + bt
+        der = (z > 0).float() if act == Kr.ACT_RELU else 1 - torch.tanh(z) ** 2
+        ref = k1 * (dA.float() * der - m1 - yc * rs * m2)
+        dy = Kr.bn_bwd_apply(dA, y, coef, act)
+        assert relf(dy, ref) < 1e-5, relf(dy, ref)
+        d16 = Kr.bn_bwd_apply(dA, y, coef, act, dy_bf16=True)
+        assert d16.dtype == torch.bfloat16 and relf(d16, ref) < 4e-3

@@ -6,4 +6,6 @@ cd $R
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 \
   || { tail -40 $OUT/pytest_gpu.log; exit 1; }
 tail -2 $OUT/pytest_gpu.log
-bash $R/tools/gpu_envab.sh s5ab "AVC_BNB=1" "AVC_BNB=0" "AVC_BNB=1" "AVC_BNB=0"
+timeout -k 10 200 python -u tools/aten_ops.py > $OUT/aten_ops.log 2>&1 || { tail -20 $OUT/aten_ops.log; exit 1; }
+cat $OUT/aten_ops.log | grep -v amdgpu
+bash $R/tools/gpu_envab.sh s5ab "AVC_X=1" "AVC_APPLY8=0" "AVC_BNB=0"
