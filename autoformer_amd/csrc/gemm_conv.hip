@@ -194,7 +194,7 @@ __global__ void __launch_bounds__(256, 2) gemm_conv_kernel(GemmArgs g) {
     }
   }
   __syncthreads();  // last wait was vmcnt(0); every fragment read done before the epilogue reuses LDS
-  fast_epilogue<CBN, BNB>(g, acc, m0, n0, mt, 0, 0, smem_raw);
+  fast_epilogue<CBN, BNB, true>(g, acc, m0, n0, mt, 0, 0, smem_raw);
 }
 
 template <int NST, int CBK, int CBN, bool BNB = false>

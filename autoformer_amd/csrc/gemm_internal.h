@@ -6,6 +6,8 @@
 
 namespace avcg {
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
 constexpr int BM = 128;                    // rows per workgroup tile (BN partial-stat tiles follow it)
 constexpr int FBK = 64;                    // K per LDS stage of the fast kernels
 
@@ -102,7 +104,10 @@ __device__ __forceinline__ long long out_col(const GemmArgs& g, int col) {
 // rows wm*64 + i*16 + 4*(lane>>4) + e and columns wn*BN_/2 + j*16 + (lane&15) of the tile.
 // Fused epilogue: bias, residual, accumulate / atomics (split-K, batch-sum), bf16 copy, and
 // BatchNorm partial statistics (per 128-row tile: column sum and M2 about the tile mean).
-template <int BN_, bool BNB = true>  // BNB: the BatchNorm-backward reduction compiled in
+// BNB: the BatchNorm-backward reduction compiled in.  YST: the caller's LDS holds at least
+// 8 KiB + 128 x (2*BN_ + 16) bytes, so a bf16 y tile is staged through it with 16-B coalesced
+// loads (per-element 2-B buffer loads of y made a fused conv 30 us slower than a plain one)
+template <int BN_, bool BNB = true, bool YST = false>
 __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4][BN_ / 32], int m0, int n0, int mt,
                                               int bz, int ks, char* smem_raw) {
   constexpr int NJ = BN_ / 32;
@@ -214,6 +219,33 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
     const bool ybf = g.bnb_ydt == AVC_BF16;
     const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<void*>(g.bnb_y), (short)0, (int)min((long long)g.M * g.ldc * (ybf ? 2 : 4), 0x7fffffffLL), 0x00020000);
+    constexpr int YP = 2 * BN_ + 16;  // LDS row pitch of the staged tile (bytes)
+    char* ys = smem_raw + 8192;
+    const bool yst = YST && ybf && (g.ldc % 8) == 0 && (reinterpret_cast<uintptr_t>(g.bnb_y) & 15) == 0;
+    if (yst) {
+      // rows m0.., columns n0..n0+BN_-1 as 16-B chunks (8 columns), zero outside [M) x [N)
+      constexpr int CPR = BN_ / 8;
+      const bf16* yb = reinterpret_cast<const bf16*>(g.bnb_y);
+      __syncthreads();  // the caller's last use of LDS is done
+      for (int q = tid; q < BM * CPR; q += blockDim.x) {
+        const int r = q / CPR, cc = q - r * CPR;
+        const int row = m0 + r, col = n0 + cc * 8;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (row < g.M && col < g.N) {
+          if (col + 8 <= g.N) {
+            v = *reinterpret_cast<const u32x4*>(yb + (long long)row * g.ldc + col);
+          } else {
+            unsigned short h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int k = 0; k < 8 && col + k < g.N; ++k)
+              h[k] = __builtin_bit_cast(unsigned short, yb[(long long)row * g.ldc + col + k]);
+            v = u32x4{h[0] | (unsigned)h[1] << 16, h[2] | (unsigned)h[3] << 16, h[4] | (unsigned)h[5] << 16,
+                      h[6] | (unsigned)h[7] << 16};
+          }
+        }
+        *reinterpret_cast<u32x4*>(ys + r * YP + cc * 16) = v;
+      }
+      __syncthreads();
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int col = cbase + j * 16;
@@ -230,9 +262,13 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
           float v = acc[i][j][e];
           if (!C) v = (float)(bf16)v;
           const int o = row * (int)g.ldc + col;
-          const float yv = ybf ? __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(yr, o * 2, 0, 0)
-                                                               << 16)
-                               : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(yr, o * 4, 0, 0));
+          float yv;
+          if (YST && yst)
+            yv = __builtin_bit_cast(float, (unsigned)*reinterpret_cast<const unsigned short*>(
+                                               ys + (row - m0) * YP + (col - n0) * 2) << 16);
+          else
+            yv = ybf ? __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(yr, o * 2, 0, 0) << 16)
+                     : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(yr, o * 4, 0, 0));
           const float yh = (yv - mu) * rs;
           const float dz = act_bwd_from_pre(v, yh * gm + bt, g.bnb_act);
           t0 += dz;
@@ -273,7 +309,7 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
     if (arrive_last(g.bnb_cnt + n0 / BN_, (g.M + BM - 1) / BM)) {
       const int c1 = min(n0 + BN_, g.N);
       for (int c0 = n0; c0 < c1; c0 += 64)
-        avcbn::bwd_finalize_cols<true, 4>(g.bnb_ws, (g.M + BM - 1) / BM, g.M, g.N, c0, min(64, c1 - c0), f, red);
+        avcbn::bwd_finalize_cols<true, 16>(g.bnb_ws, (g.M + BM - 1) / BM, g.M, g.N, c0, min(64, c1 - c0), f, red);
     }
   }
 }

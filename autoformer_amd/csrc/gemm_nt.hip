@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt_kernel(GemmArgs g) {
     }
   }
   __syncthreads();  // every glds retired (last wait was vmcnt(0)) and every fragment read done
-  fast_epilogue<BN_, BNB>(g, acc, m0, n0, mt, bz, ks, smem_raw);
+  fast_epilogue<BN_, BNB, true>(g, acc, m0, n0, mt, bz, ks, smem_raw);
 }
 
 template <int BN_, int NST, bool WIN, bool BNB = false>

@@ -6,4 +6,4 @@ cd $R
 timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py -x -q --timeout 120 --timeout-method thread \
   > gpurun_out/s7/pytest.log 2>&1 || { tail -40 gpurun_out/s7/pytest.log; exit 1; }
 tail -1 gpurun_out/s7/pytest.log
-bash tools/ab_head.sh "--steps 30 --warmup 5" "" 3
+bash tools/ab_head.sh "--steps 30 --warmup 5" "AVC_BNB=0" 2
