@@ -781,6 +781,7 @@ def test_conv_chain_fused_bn_backward_matches_separate():
     cores = [Ly.ConvBNCore(mods[2 * i], mods[2 * i + 1], Kr.ACT_RELU) for i in range(3)]
     x0 = torch.randn(B * T, 80, device=DEV)
     res = []
+    saved = Ly._BNB_ON
     for on in (True, False):
         Ly._BNB_ON = on
         try:
@@ -795,7 +796,7 @@ def test_conv_chain_fused_bn_backward_matches_separate():
             res.append((h.detach().float().clone(), x.grad.clone(),
                         [p.grad.clone() for m in mods for p in m.parameters()]))
         finally:
-            Ly._BNB_ON = True
+            Ly._BNB_ON = saved
     (ha, dxa, ga), (hb, dxb, gb) = res
     torch.testing.assert_close(ha, hb, rtol=0, atol=0)
     assert relf(dxa, dxb) < 2e-3, relf(dxa, dxb)
