@@ -244,19 +244,34 @@ __global__ void __launch_bounds__(256) vc_loss_kernel(const float* __restrict__ 
     st_sc1(ws + (long long)blockIdx.x * 3 + threadIdx.x, r[0] + r[1] + r[2] + r[3]);
   }
   if (!arrive_last(cnt, gridDim.x)) return;
-  if (threadIdx.x < 64) {
-    // lane q < 3 sums partial q over the blocks in order
-    float t = 0.f;
-    if (threadIdx.x < 3)
-      for (int b = 0; b < (int)gridDim.x; ++b) t += ld_sc1(ws + (long long)b * 3 + threadIdx.x);
-    const float m0 = __shfl(t, 0, 64) / (float)n1, m1 = __shfl(t, 1, 64) / (float)n1;
-    const float m2 = n2 > 0 ? __shfl(t, 2, 64) / (float)n2 : 0.f;
-    if (threadIdx.x == 0) {
-      out[0] = m0;
-      out[1] = m1;
-      out[2] = m2;
-      out[3] = m0 + m1 + lam * m2;
-    }
+  // thread t loads block t's three partials (all loads in flight at once; a serial loop of
+  // agent-scope loads cost 30 us), then a fixed-order tree: deterministic
+  float p0 = 0.f, p1 = 0.f, p2 = 0.f;
+  if (threadIdx.x < gridDim.x) {
+    const float* q = ws + (long long)threadIdx.x * 3;
+    p0 = ld_sc1(q);
+    p1 = ld_sc1(q + 1);
+    p2 = ld_sc1(q + 2);
+  }
+  p0 = warp_sum(p0);
+  p1 = warp_sum(p1);
+  p2 = warp_sum(p2);
+  __syncthreads();  // red reused
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = p0;
+    red[1][w] = p1;
+    red[2][w] = p2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t0 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    const float t1 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    const float t2 = red[2][0] + red[2][1] + red[2][2] + red[2][3];
+    const float m0 = t0 / (float)n1, m1 = t1 / (float)n1, m2 = n2 > 0 ? t2 / (float)n2 : 0.f;
+    out[0] = m0;
+    out[1] = m1;
+    out[2] = m2;
+    out[3] = m0 + m1 + lam * m2;
   }
 }
 
