@@ -68,7 +68,9 @@ def test_variant_oracle_step(name):
             assert abs(ours - gn) <= 1e-3 * gn + 1e-6, (k, ours, gn)
             head = t.grad.reshape(-1)[:64].numpy()
             ref = g["step_ghead/" + k]
-            assert np.abs(head - ref).max() <= 1e-3 * max(np.abs(ref).max(), 1e-3), k
+            # 2e-3: the fp32 CPU oracle's reduction order follows the host's thread count (measured
+            # 1.07e-3 for a MetaConv2 BN-bias head on a 16-thread box, < 1e-3 on 8 threads)
+            assert np.abs(head - ref).max() <= 2e-3 * max(np.abs(ref).max(), 1e-3), k
         elif "running" in k or "num_batches" in k:
             np.testing.assert_allclose(t.numpy(), g["step_bn/" + k], rtol=1e-5, atol=1e-6)
 
