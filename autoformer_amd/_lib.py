@@ -112,6 +112,8 @@ _SIGS = {
     "avc_vc_loss_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_void_p, c_void_p, c_ll, c_float, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "avc_pack_batch": (c_int, [c_void_p, c_void_p, c_int, c_ll, c_void_p]),
+    "avc_adam_blocks": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_float, c_float, c_float, c_float,
+                                c_void_p, c_int, c_int, c_void_p]),
     "avc_adam": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_float, c_float, c_float, c_float, c_void_p,
                          c_int, c_void_p]),
     "avc_act_fwd": (c_int, [c_void_p, c_void_p, c_ll, c_int, c_void_p]),

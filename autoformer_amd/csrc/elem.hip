@@ -571,15 +571,20 @@ extern "C" int avc_pack_batch(const avc_pack_op* ops, const long long* prefix, i
   return avc_check_launch("avc_pack_batch");
 }
 
-extern "C" int avc_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
-                        float eps, float* state, int advance, void* stream) {
-  AVC_CHECK_ARG(p && g && m && v && state, "avc_adam: null");
+extern "C" int avc_adam_blocks(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
+                               float beta2, float eps, float* state, int advance, int max_blocks, void* stream) {
+  AVC_CHECK_ARG(p && g && m && v && state && max_blocks >= 0, "avc_adam: bad args");
   hipStream_t s = as_stream(stream);
   if (advance) adam_prep_kernel<<<1, 1, 0, s>>>(state, lr, beta1, beta2);
   if (n == 0) return avc_check_launch("avc_adam");
-  int grid = (int)std::min<long long>(4096, cdiv(n, 256));
+  int grid = (int)std::min<long long>(max_blocks > 0 ? max_blocks : 4096, cdiv(n, 256));
   adam_kernel<<<grid, 256, 0, s>>>(p, g, m, v, n, beta1, beta2, eps, state);
   return avc_check_launch("avc_adam");
+}
+
+extern "C" int avc_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
+                        float eps, float* state, int advance, void* stream) {
+  return avc_adam_blocks(p, g, m, v, n, lr, beta1, beta2, eps, state, advance, 0, stream);
 }
 
 extern "C" int avc_act_fwd(const float* x, float* y, long long n, int act, void* stream) {

@@ -553,9 +553,9 @@ def vc_loss_grad(x, y1, y2, ca, cb, lambda_cd, d, need):
     return outs
 
 
-def adam(p, g, m, v, lr, beta1, beta2, eps, state, advance=True):
-    L.call("avc_adam", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), float(lr), float(beta1),
-           float(beta2), float(eps), state.data_ptr(), int(advance), stream())
+def adam(p, g, m, v, lr, beta1, beta2, eps, state, advance=True, max_blocks=0):
+    L.call("avc_adam_blocks", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), float(lr),
+           float(beta1), float(beta2), float(eps), state.data_ptr(), int(advance), int(max_blocks), stream())
 
 
 def act_fwd(x, act, out=None):

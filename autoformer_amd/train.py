@@ -204,16 +204,20 @@ class FusedAdam:
         K.adam(self.flat, self.gflat, self.m, self.v, self.lr, self.betas[0], self.betas[1], self.eps, self.state)
         weights_changed()
 
-    def step_slice(self, lo, hi, advance):
+    def step_slice(self, lo, hi, advance, max_blocks=0):
         """Adam over flat[lo:hi] only; `advance` on the step's first slice (the step count and
-        bias corrections live in self.state; later slices must be stream-ordered after it)."""
+        bias corrections live in self.state; later slices must be stream-ordered after it).
+        max_blocks: workgroup cap for a slice that runs beside other kernels."""
         sl = slice(lo, hi)
         K.adam(self.flat[sl], self.gflat[sl], self.m[sl], self.v[sl], self.lr, self.betas[0], self.betas[1],
-               self.eps, self.state, advance=advance)
+               self.eps, self.state, advance=advance, max_blocks=max_blocks)
 
 
 # ------------------------------------------------------------------------- bench step
 _MAIN_PRIO = os.environ.get("AVC_MAIN_PRIO", "0") == "1"
+# workgroup cap of the decoder-slice Adam that runs beside the encoder backward (0 = full grid;
+# 256 measured best: the full 4096-block grid slowed the latency-bound BiLSTM backward beside it)
+_SIDE_ADAM_BLOCKS = int(os.environ.get("AVC_SIDE_ADAM_BLOCKS", "256"))
 
 
 class TrainStep:
@@ -284,7 +288,7 @@ class TrainStep:
                 # RCCL: the comm stream waits for the collective; the Adam slice follows it
                 self._early = D.allreduce_mean_async_(self.gflat[self.split:])
                 D.finish_allreduce_(self._early)
-            self.opt.step_slice(self.split, self.flat.numel(), advance=True)
+            self.opt.step_slice(self.split, self.flat.numel(), advance=True, max_blocks=_SIDE_ADAM_BLOCKS)
         self._early_adam = True
 
     def _fwd_bwd(self, x, emb, overlap=False):

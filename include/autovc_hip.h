@@ -383,6 +383,11 @@ int avc_pack_batch(const avc_pack_op* ops, const long long* prefix, int nops, lo
  * first slice only; the later slices run on a stream ordered after it. */
 int avc_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
              float beta2, float eps, float* state, int advance, void* stream);
+/* avc_adam with at most max_blocks 256-thread workgroups (0 = as avc_adam): a slice that runs
+ * BESIDE latency-bound kernels (the decoder-slice Adam next to the encoder backward) takes a
+ * smaller share of the memory system. */
+int avc_adam_blocks(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
+                    float beta2, float eps, float* state, int advance, int max_blocks, void* stream);
 
 /* AdaIN / speaker-embedding-adjust variants (variants.hip).
  * Whole-tensor moments of x.mean(), x.std() (unbiased) — factory/AutoVC2.py:58-60,
