@@ -6,7 +6,7 @@ OUT=$R/gpurun_out/${1:-envab}
 shift
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-for rep in 1 2; do
+for rep in $(seq 1 ${AB_REPS:-2}); do
   i=0
   for spec in "$@"; do
     i=$((i+1))
