@@ -127,10 +127,18 @@ class _VCLossFn(torch.autograd.Function):
         x, y1, y2, ca, cb = ctx.saved_tensors
         need = ctx.needs_input_grad
         d = [t.contiguous() if t is not None else None for t in (d_id, d_psnt, d_cd, d_total)]
-        # x_real is data in train.py; its gradient (rare) is -(g1 + g2)
-        n1, n2 = need[1] or need[0], need[2] or need[0]
-        g1, g2, ga, gb = K.vc_loss_grad(x, y1, y2, ca, cb, ctx.lam, d, (n1, n2, need[3], need[4]))
-        gx = -(g1 + g2) if need[0] else None
+        # a term whose upstream gradients are all None contributes nothing (None, not zeros);
+        # x_real is data in train.py, its gradient (rare) is -(g1 + g2)
+        t = d_total is not None
+        h1, h2, hc = t or d_id is not None, t or d_psnt is not None, t or d_cd is not None
+        n1, n2 = h1 and (need[1] or need[0]), h2 and (need[2] or need[0])
+        want = (n1, n2, hc and need[3], hc and need[4])
+        if not any(want):
+            return None, None, None, None, None, None
+        g1, g2, ga, gb = K.vc_loss_grad(x, y1, y2, ca, cb, ctx.lam, d, want)
+        gx = None
+        if need[0] and (g1 is not None or g2 is not None):
+            gx = -(g1 + g2) if g1 is not None and g2 is not None else -(g1 if g1 is not None else g2)
         return gx, g1 if need[1] else None, g2 if need[2] else None, ga, gb, None
 
 
