@@ -16,8 +16,8 @@ import torch  # noqa: F401  (must precede the HIP library)
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip"]
-ABI_VERSION = 12
+SOURCES = ["gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "graph.hip"]
+ABI_VERSION = 13
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -86,6 +86,11 @@ _SIGS = {
                              c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "avc_lstm_bwd_scratch_bytes": (c_size, [c_int, c_int, c_int]),
     "avc_lstm_set_bwd_form": (c_int, [c_int]),
+    "avc_capture_deps": (c_int, [c_void_p, ctypes.POINTER(c_void_p), c_int]),
+    "avc_graph_split": (c_int, [c_void_p, ctypes.POINTER(c_void_p), c_int, ctypes.POINTER(c_void_p), c_int, c_int,
+                                ctypes.POINTER(c_void_p), ctypes.POINTER(c_int)]),
+    "avc_graph_launch2": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "avc_graph_split_destroy": (c_int, [c_void_p]),
     "avc_lstm2_persistent": (c_int, [c_int, c_int, c_int, c_int]),
     "avc_lstm2_scratch_bytes": (c_size, [c_int, c_int]),
     "avc_lstm2_fwd": (c_int, [c_void_p] * 5 + [c_int] * 3 + [c_void_p] * 10),

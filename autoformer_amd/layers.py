@@ -93,9 +93,25 @@ class _Side:
 
 
 def join_side() -> None:
-    if _SINK["side"] is not None:
-        torch.cuda.current_stream().wait_stream(_SINK["side"])
+    side = _SINK["side"]
+    if side is not None:
+        cur = torch.cuda.current_stream()
+        if _SINK.get("tails") == [] and torch.cuda.is_current_stream_capturing():
+            # a capture that TrainStep will split into a main and a side graph: each stream's
+            # capture dependencies at the join (graph.hip, avc_graph_split)
+            _SINK["tails"] = [K.capture_deps(cur), K.capture_deps(side)]
+        cur.wait_stream(side)
     _SINK["keep"].clear()
+
+
+def record_join_tails(on: bool):
+    """Arm (on) / take (off: returns [main tails, side tails] or None) the capture dependencies
+    that join_side() records while a graph capture is running."""
+    if on:
+        _SINK["tails"] = []
+        return None
+    t = _SINK.pop("tails", None)
+    return t if t else None
 
 
 def _grad_of(p):

@@ -25,7 +25,7 @@ import torch
 
 from . import dist as D
 from . import kernels as K
-from .layers import join_side, prefetch_packs, set_grad_sink, side_stream, weights_changed
+from .layers import join_side, prefetch_packs, record_join_tails, set_grad_sink, side_stream, weights_changed
 
 
 def _load_state(model, path, device):
@@ -226,6 +226,8 @@ _MAIN_PRIO = os.environ.get("AVC_MAIN_PRIO", "0") == "1"
 # workgroup cap of the decoder-slice Adam that runs beside the encoder backward (0 = full grid;
 # 256 measured best: the full 4096-block grid slowed the latency-bound BiLSTM backward beside it)
 _SIDE_ADAM_BLOCKS = int(os.environ.get("AVC_SIDE_ADAM_BLOCKS", "256"))
+# capture(): split the captured step into concurrent main / side graphs (0 = one graph, A/B)
+_GRAPH_SPLIT = os.environ.get("AVC_GRAPH_SPLIT", "1") == "1"
 
 
 class TrainStep:
@@ -239,13 +241,17 @@ class TrainStep:
         self.lambda_cd = lambda_cd
         self.extra = extra  # optional callable(x, emb, x_psnt) -> extra loss (GAN step)
         # one flat buffer (and one fused Adam) over every module: Adam is elementwise, so this
-        # equals the reference's separate g_optimizer / d_optimizer with the same settings
-        owner = torch.nn.ModuleList([model, *extra_modules]) if extra_modules else model
+        # equals the reference's separate g_optimizer / d_optimizer with the same settings.  The
+        # extra modules (the GAN step's discriminator) go FIRST, below the split offset: their
+        # gradients (the real-data branch D(x) included) are complete only at the end of the
+        # backward, not when the decoder hook fires, so they are stepped with the encoder slice
+        owner = torch.nn.ModuleList([*extra_modules, model]) if extra_modules else model
         self.params, self.flat, self.gflat = D.flatten_params_(owner)
         D.broadcast_(self.flat)
         set_grad_sink(True)  # kernels accumulate straight into the flat gradient buffer
         self.opt = FusedAdam(self.flat, self.gflat, lr)
         self.graph_fb = None
+        self.graph_split = None
         self.world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
         self.loss = None
         # The decoder / postnet (/ discriminator) gradients are final once the backward reaches
@@ -356,7 +362,10 @@ class TrainStep:
 
     def _step(self, x, emb):
         if self.graph_fb is not None:
-            self.graph_fb.replay()
+            if self.graph_split is not None:
+                self.graph_split.launch(torch.cuda.current_stream(), side_stream())
+            else:
+                self.graph_fb.replay()
             loss = self.loss
         else:
             loss = self._fwd_bwd(x, emb, overlap=self.split is not None)
@@ -380,9 +389,21 @@ class TrainStep:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         weights_changed()  # the captured forward must contain the weight repacks
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.loss = self._fwd_bwd(x, emb)
+        # keep_graph: the raw graph is split into a main-stream and a side-stream graph that
+        # replay concurrently (graph.hip): one graph would run the weight-gradient branch
+        # serially after the main chain (the runtime executes a graph in one queue)
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        record_join_tails(True)
+        try:
+            with torch.cuda.graph(g):
+                self.loss = self._fwd_bwd(x, emb)
+        finally:
+            tails = record_join_tails(False)
+        self.graph_split = None
+        if tails is not None and all(tails) and _GRAPH_SPLIT:
+            self.graph_split = K.GraphSplit(g.raw_cuda_graph(), tails[0], tails[1])
+        else:
+            g.instantiate()
         self.graph_fb = g  # capture only records: the next step() replays it
 
 

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 12
+#define AVC_ABI_VERSION 13
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -448,6 +448,25 @@ int avc_mg_wn_pack(const float* v, const float* g, const float* bias, int d0, in
  * out[b*L + t] = tanh(bias + sum_k,c w[k][c] act(x[b][reflect(t + k - 3)][c])). */
 int avc_mg_conv_out(const float* x, int B, int L, int C, int taps, const float* w, const float* bias, float slope,
                     float* out, void* stream);
+
+/* ---- the training step as two concurrent hipGraphs (graph.hip).  Not a reference operation:
+ * host plumbing of train.py's step loop (train.py:82-99) when the step is replayed from a capture.
+ * avc_capture_deps: the current capture dependencies (graph nodes, as void*) of a capturing stream;
+ * returns their count (<= max_out) or -1.
+ * avc_graph_split: rebuild a captured graph whose side-stream branch forked from the main stream
+ * and joins it only at the end as up to max_segments (main graph, side graph) pairs: the main
+ * chain is cut after main nodes that side nodes wait for, side segment k holds the side nodes whose
+ * latest main dependency is in main segment k; main_tails / side_tails = each stream's capture
+ * dependencies at the join.  counts (nullable, 4 ints): [main nodes, side nodes, cross edges,
+ * segments].
+ * avc_graph_launch2: per segment, main graph on main_stream, event, side_stream waits for it,
+ * side graph on side_stream; finally main_stream waits for side_stream.
+ * avc_graph_split_destroy: frees the two graphs, their executables and events. */
+int avc_capture_deps(void* stream, void** out, int max_out);
+int avc_graph_split(void* graph, void* const* main_tails, int n_main, void* const* side_tails, int n_side,
+                    int max_segments, void** handle, int* counts);
+int avc_graph_launch2(void* handle, void* main_stream, void* side_stream);
+int avc_graph_split_destroy(void* handle);
 
 #ifdef __cplusplus
 }

@@ -123,3 +123,88 @@ def test_gan_solver_matches_reference_solver(golden):
     det_init_(s.D)
     hist = s.train()
     np.testing.assert_allclose([h[3] for h in hist], g["d_step_losses"], rtol=2e-3)
+
+
+def _split_vs_whole(make, extra=None, steps=2):
+    """Two identical TrainSteps, one with the overlapped early slice (decoder / postnet Adam
+    from the backward hook), one with split=None (one Adam over the whole buffer after the
+    backward): after `steps` fp32 steps the Adam moments of every parameter tensor agree, and
+    the parameters agree up to isolated elements.  (Split-K weight gradients add in a
+    run-dependent order, and Adam's first updates turn the sign of a ~0 gradient's rounding noise
+    into a whole-lr move, so a few elements may differ by up to 2 lr; an Adam run on an
+    incomplete gradient would move whole tensors and their first moments by O(1).)"""
+    from autoformer_amd.detinit import det_inputs
+    from autoformer_amd.dist import param_offsets
+    from autoformer_amd.layers import set_grad_sink
+    from autoformer_amd.train import TrainStep
+
+    lr = 1e-3
+    x, e = det_inputs(4, 176, seed=11)
+    x, e = torch.from_numpy(x).to(DEV), torch.from_numpy(e).to(DEV)
+    out = []
+    for split in (True, False):
+        mods = make()
+        G, rest = mods[0], mods[1:]
+        ts = TrainStep(G, lr=lr, extra=extra(*rest) if extra else None, extra_modules=list(rest))
+        assert ts.split is not None
+        if not split:
+            ts.split = None
+        try:
+            for _ in range(steps):
+                ts.step(x, e)
+            torch.cuda.synchronize()
+        finally:
+            set_grad_sink(False)
+        out.append((ts.flat.clone(), ts.opt.m.clone(), ts.opt.v.clone(), ts.opt.state.clone(), ts.params))
+    (fa, ma, va, sa, params), (fb, mb, vb, sb, _) = out
+    assert torch.equal(sa, sb)
+    offs, _ = param_offsets(params)
+    # absolute floor per tensor: 1e-4 of the buffer's rms moment (the conv biases that feed a
+    # training-mode BatchNorm have an analytically zero gradient: pure rounding noise)
+    rms = {"adam m": mb.double().pow(2).mean().sqrt().item(), "adam v": vb.double().pow(2).mean().sqrt().item()}
+    for p, off in zip(params, offs):
+        sl = slice(off, off + p.numel())
+        for name, a, b in (("adam m", ma[sl], mb[sl]), ("adam v", va[sl], vb[sl])):
+            a, b = a.double(), b.double()
+            assert (a - b).norm() <= 1e-3 * b.norm() + 1e-4 * rms[name] * p.numel() ** 0.5, (name, p.shape, off)
+    d = (fa.double() - fb.double()).abs()
+    assert d.max().item() <= 2.5 * lr, d.max().item()
+    assert (d > 0.05 * lr).sum().item() <= 1e-4 * d.numel(), (d > 0.05 * lr).sum().item()
+
+
+def test_trainstep_early_slice_equals_whole_adam_autovc():
+    """the decoder-slice Adam run from the backward hook equals one Adam over the
+    whole buffer (AutoVC)."""
+    import autoformer_amd as A
+    from autoformer_amd.detinit import det_init_
+    from factory.AutoVC import AutoVC
+
+    def make():
+        A.set_compute("fp32")
+        m = AutoVC(44, 256, 512, 22)
+        det_init_(m)
+        return (m.to(DEV).train(),)
+    _split_vs_whole(make)
+
+
+def test_trainstep_early_slice_equals_whole_adam_gan():
+    """The same for the GAN step: the discriminator's gradients (its real-data branch does not
+    feed the decoder) complete only at the end of the backward, so its parameters must sit in
+    the late slice -- they do (extra modules first in the flat buffer)."""
+    from autoformer_amd.train import gan_extra
+
+    _split_vs_whole(lambda: _models("fp32"), extra=gan_extra)
+
+
+def test_trainstep_early_slice_equals_whole_adam_autovc2():
+    """The same for the AdaIN variant AutoVC2 (its own loss function, same split)."""
+    import autoformer_amd as A
+    from autoformer_amd.detinit import det_init_
+    from factory.AutoVC2 import AutoVC2
+
+    def make():
+        A.set_compute("fp32")
+        m = AutoVC2(44, 256, 512, 22)
+        det_init_(m)
+        return (m.to(DEV).train(),)
+    _split_vs_whole(make)

@@ -479,13 +479,14 @@ def test_gemm_nt_conv_window_and_bn_stats(B, T, Cin, Cout, Kw, pad):
     assert rinf(1.0 / rstd.double() ** 2 - 1e-5, refv) < 1e-3
 
 
-@pytest.mark.parametrize("form", [1, 0])
+@pytest.mark.parametrize("form", [2, 3, 1, 0])
 @pytest.mark.parametrize("B,H", [(64, 1024), (20, 1024), (64, 512), (3, 512), (64, 768), (2, 768)])
 def test_lstm_persistent_backward(B, H, form):
     """The one-launch backward recurrence (bf16 products, fp32 cell math) against an fp32
     CPU loop that rounds dG_{t+1} to bf16 for the recurrent product, as the kernel does;
     its bf16 dG twin equals the fp32 output rounded; the spin-timeout flag stays clear.
-    Both hand-off forms: partial-sum exchange (1, default) and dG gather (0)."""
+    Every hand-off form: sentinel (2, default; 3 = with the XCD-verified L2-resident stores),
+    partial-sum exchange (1) and dG gather (0)."""
     import autoformer_amd as A
     from autoformer_amd import kernels as Kr
 
@@ -493,6 +494,50 @@ def test_lstm_persistent_backward(B, H, form):
     Kr.lstm_set_bwd_form(form)
     try:
         _persistent_backward_case(B, H)
+    finally:
+        Kr.lstm_set_bwd_form(-1)
+
+
+@pytest.mark.parametrize("form", [2, 3])
+def test_lstm_persistent_backward_under_load(form):
+    """The sentinel hand-off under uneven load: the same backward run alone and beside a stream
+    of large GEMMs on another stream (so members start and run at different times, and the
+    payload lines compete with streaming traffic) is bit-identical -- the recurrence's arithmetic
+    order is fixed, so any stale or torn payload read would show as a difference."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute("bf16")
+    B, H, T = 64, 1024, 48
+    G = 4 * H
+    torch.manual_seed(5)
+    dh = (torch.randn(B * T, H) * 0.1).to(DEV)
+    c = (torch.randn(B * T, H) * 0.7).to(DEV)
+    gates = torch.rand(B * T, G) * 0.9 + 0.05
+    gates[:, 2 * H:3 * H] = gates[:, 2 * H:3 * H] * 2 - 1
+    gates = gates.to(DEV)
+    wt = ((torch.randn(G, H) * (1.0 / H ** 0.5)).bfloat16().t().contiguous()).to(DEV)
+    gbuf = Kr.lstm_bwd_scratch(B, H, 1, DEV)
+    Kr.lstm_set_bwd_form(form)
+    try:
+        quiet = Kr.lstm_bwd(dh, dh, c, gates, None, wt, B, T, H, 1, gbuf=gbuf)
+        torch.cuda.synchronize()
+        assert Kr.lstm_bwd_timeout_flag(gbuf, B, H) == 0
+        side = torch.cuda.Stream()
+        x = torch.randn(4096, 4096, device=DEV, dtype=torch.bfloat16)
+        for lead in (0, 1, 3):
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(lead):
+                    x = (x @ x).clamp_(-1, 1)
+            loaded = Kr.lstm_bwd(dh, dh, c, gates, None, wt, B, T, H, 1, gbuf=gbuf)
+            with torch.cuda.stream(side):
+                for _ in range(4):
+                    x = (x @ x).clamp_(-1, 1)
+            torch.cuda.synchronize()
+            assert Kr.lstm_bwd_timeout_flag(gbuf, B, H) == 0
+            assert torch.equal(loaded, quiet), (lead, (loaded - quiet).abs().max().item())
+            assert torch.equal(loaded._bf16, quiet._bf16), lead
     finally:
         Kr.lstm_set_bwd_form(-1)
 
