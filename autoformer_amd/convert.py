@@ -42,14 +42,16 @@ class Converter:
         self.vocoder = vocoder  # autoformer_amd.melgan.MelVocoder (evaluate.py:24) or None
 
     @torch.no_grad()
-    def get_wavs(self, mel):
-        """evaluate.py:96-98: (1, 80, T) mel -> (1, T*256) waveform.  A frame-major (1, T, 80)
-        mel, the layout get_trans_mel returns, goes straight in without the transpose."""
+    def get_wavs(self, mel, frames: bool = False):
+        """evaluate.py:96-98: (1, 80, T) mel -> (1, T*256) waveform (the reference contract).
+        frames=True: a frame-major (1, T, 80) mel, the layout get_trans_mel returns, goes straight
+        in without the transpose.  The layout is stated, never guessed from the shape (T may be 80)."""
         if self.vocoder is None:
             raise RuntimeError("Converter was built without a vocoder (pass vocoder=MelVocoder(...))")
-        if mel.dim() == 3 and mel.shape[-1] == 80 and mel.shape[1] != 80:
-            return self.vocoder.inverse_frames(mel)
-        return self.vocoder.inverse(mel)
+        if mel.dim() != 3 or mel.shape[2 if frames else 1] != 80:
+            raise ValueError(f"get_wavs: expected a {'(1, T, 80)' if frames else '(1, 80, T)'} mel, got "
+                             f"{tuple(mel.shape)}")
+        return self.vocoder.inverse_frames(mel) if frames else self.vocoder.inverse(mel)
 
     def _dev(self, a):
         return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).unsqueeze(0).to(self.device)

@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TD* __restrict
                                                             const float* __restrict__ rstd,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta, int M, int C, int act,
-                                                            float* ws, unsigned* cnt, BwdFin fin) {
+                                                            float* ws) {
   __shared__ float red[3][16][65];
   const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
   const int c = blockIdx.x * 64 + cq * 4;
@@ -219,14 +219,9 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TD* __restrict
       float t = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) t += red[q][i][cl];
-      if (cnt) st_sc1(ws + ((long long)blockIdx.y * C + cc) * 3 + q, t);
-      else ws[((long long)blockIdx.y * C + cc) * 3 + q] = t;
+      ws[((long long)blockIdx.y * C + cc) * 3 + q] = t;
     }
   }
-  // the last row block of this channel strip merges all partials (no finalize launch)
-  __shared__ float fred[3 * FG * 64];
-  if (cnt && arrive_last(cnt + blockIdx.x, gridDim.y))
-    bwd_finalize_cols<true>(ws, gridDim.y, M, C, blockIdx.x * 64, 64, fin, fred);
 }
 
 // scalar variant (C % 4 != 0): 64 channels x 4 row lanes
@@ -237,7 +232,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const TD* __restric
                                                              const float* __restrict__ rstd,
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, int M, int C, int act,
-                                                             float* ws, unsigned* cnt, BwdFin fin) {
+                                                             float* ws) {
   __shared__ float red[3][4][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -266,14 +261,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const TD* __restric
 #pragma unroll
     for (int q = 0; q < 3; ++q) v[q] = red[q][0][cl] + red[q][1][cl] + red[q][2][cl] + red[q][3][cl];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      if (cnt) st_sc1(p + q, v[q]);
-      else p[q] = v[q];
-    }
+    for (int q = 0; q < 3; ++q) p[q] = v[q];
   }
-  __shared__ float fred[3 * FG * 64];
-  if (cnt && arrive_last(cnt + blockIdx.x, gridDim.y))
-    bwd_finalize_cols<true>(ws, gridDim.y, M, C, blockIdx.x * 64, 64, fin, fred);
 }
 
 
@@ -416,17 +405,6 @@ extern "C" int avc_bn_stats(const float* y, long long ld, int M, int C, float* p
   return avc_check_launch("avc_bn_stats");
 }
 
-// AVC_LAST_BLOCK=1: the backward finalize by the reduce's last-arriving row block instead of its
-// own launch.  Off by default: measured 22.8 us per BN backward reduce+finalize vs 11.6 + 8.5 us
-// as two launches in the C2 step (the single last block's serial merge sits on the critical path).
-static bool last_block_finalize() {
-  static const bool on = [] {
-    const char* e = getenv("AVC_LAST_BLOCK");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 unsigned* avc_counter_slots(int n, hipStream_t s) {
   constexpr unsigned POOL = 1u << 16;
   constexpr int MAXD = 64;
@@ -513,9 +491,6 @@ extern "C" int avc_bn_bwd(const void* dA, int dA_dtype, const float* a, const vo
   float* coef = ws + coff;
   const long long total = (long long)M * C;
   const BwdFin fin{gamma, beta, mean, rstd, coef, dgamma, dbeta, dbias, accumulate};
-  // one arrival counter per channel strip: the reduce's last row block finalizes the strip
-  unsigned* cnt = last_block_finalize() ? avc_counter_slots(cdiv(C, 64), s) : nullptr;
-  if (last_block_finalize() && !cnt) return -1;
   with_type(dA_dtype, [&](auto dtag) {
     using TD = std::remove_const_t<std::remove_pointer_t<decltype(dtag)>>;
     with_type(y_dtype, [&](auto ytag) {
@@ -523,13 +498,13 @@ extern "C" int avc_bn_bwd(const void* dA, int dA_dtype, const float* a, const vo
       const TD* dp = static_cast<const TD*>(dA);
       const TY* yp = static_cast<const TY*>(y);
       if (v4) {
-        if (pre) bn_bwd_reduce_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws, cnt, fin);
-        else bn_bwd_reduce_kernel<false, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws, cnt, fin);
+        if (pre) bn_bwd_reduce_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws);
+        else bn_bwd_reduce_kernel<false, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws);
       } else {
-        if (pre) bn_bwd_reduce1_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws, cnt, fin);
-        else bn_bwd_reduce1_kernel<false, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws, cnt, fin);
+        if (pre) bn_bwd_reduce1_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws);
+        else bn_bwd_reduce1_kernel<false, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws);
       }
-      if (!cnt) bn_bwd_finalize_kernel<<<cdiv(C, 64), 256, 0, s>>>(ws, nrb, M, C, fin);
+      bn_bwd_finalize_kernel<<<cdiv(C, 64), 256, 0, s>>>(ws, nrb, M, C, fin);
       if (v4) {
         if (pre)
           bn_bwd_apply_kernel<true, TD, TY><<<cdiv(total / 4, 256), 256, 0, s>>>(dp, a, yp, coef, total / 4, C, act, dy, d16);
@@ -561,10 +536,10 @@ int avcbn::bn_bwd_reduce_finalize(const void* dA, int dA_dtype, const void* y, i
       const TY* yp = static_cast<const TY*>(y);
       if (v4)
         bn_bwd_reduce_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, nullptr, yp, fin.mean, fin.rstd, fin.gamma, fin.beta,
-                                                                M, C, act, ws, nullptr, fin);
+                                                                M, C, act, ws);
       else
         bn_bwd_reduce1_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, nullptr, yp, fin.mean, fin.rstd, fin.gamma,
-                                                                 fin.beta, M, C, act, ws, nullptr, fin);
+                                                                 fin.beta, M, C, act, ws);
       bn_bwd_finalize_kernel<<<cdiv(C, 64), 256, 0, s>>>(ws, nrb, M, C, fin);
     });
   });

@@ -791,7 +791,7 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
     g.klen = ((klf + FBK - 1) / FBK) * FBK;
     if (g.klen <= 0) g.klen = FBK;
     if (f && gemm_bnfin()) {  // the BN finalize rides on the fast kernels' epilogue (one counter per 64 columns)
-      g.bn_cnt = avc_counter_slots(cdiv(g.N, 64), s);
+      g.bn_cnt = avc_counter_slots(cdiv(g.N, 32), s);  // one per column tile (tiles >= 32 columns)
       if (!g.bn_cnt) return -1;
     }
     const bool bnb_fused = bb && !aks && !bks;  // every non-TT fast kernel runs fast_epilogue

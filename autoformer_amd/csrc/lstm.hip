@@ -1506,168 +1506,6 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd_sg(PersistBwdArgs a) 
   }
 }
 
-// Backward with the NARROW side handed over (partial-sum exchange).  The recurrent product
-// dh_rec[b][j] = sum_q dG_{t+1}[b][q] W_hh[q][j] contracts over the 4H gate rows, and member r
-// already holds 128 of them (its own dG columns: 4 gates x 32 units).  So instead of gathering
-// the group's whole dG_{t+1} (8 x 4H bf16 = 64 KB per consumer per step at H = 1024) before a
-// K = 4H product, each member multiplies its OWN dG tile (in LDS, no wait) by
-// W_hh[own 128 rows][all H columns] and publishes the fp32 partial dh (8 x H); consumer r then
-// reads, from each of the H/32 producers, only the 8 x 32 block of its own units (1 KB) and sums
-// them: 32 KB per consumer per step at H = 1024, half the bytes, and the product's LDS operand
-// is the 8 x 128 own tile (4 KB per wave) instead of the group tile (16 KB per wave).
-//   product:   wave w owns dh columns [w*H/8, (w+1)*H/8) as H/128 16-row MFMA tiles (A = W_hh^T
-//              rows in VGPRs for the whole sequence, K = the 4 gate k-blocks of the member's
-//              units); B = the dG tile (utterances as the 16 columns, 8 valid); each lane ends
-//              with 4 consecutive dh columns of one utterance = one 16-B sc1 store.
-//   partials:  fp32 [2 parities][NG][NR producers][NR consumers][8][32] (1 KB blocks).
-//   hand-off:  every wave drains its stores, workgroup barrier, wave 0 raises the member's
-//              flag (write-through form as above); consumers poll the group's flags with
-//              wave 0, then wave w sums producers w, w+8, ... with 16-B sc1 loads and the eight
-//              waves' sums meet in LDS.
-// The parity argument of the forward holds unchanged (a member publishes step s+2 into the
-// slot of step s only after every member published step s+1, i.e. consumed step s).
-constexpr size_t ps_bytes(int ng, int H) { return (size_t)2 * ng * (H / PJU) * (H / PJU) * PRG * PJU * 4; }
-
-template <int H>
-__global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd_ps(PersistBwdArgs a) {
-  constexpr int G = 4 * H, NR = H / PJU, NT = H / 128, NPW = NR / 8, DP = 4 * PJU + 8, CW = H / 8;
-  static_assert(NR % 8 == 0 && PRG * PJU == 256 && PNT == 512, "partial-sum layout");
-  __shared__ __attribute__((aligned(16))) bf16 ds16[(PRG + 1) * DP];  // dG_t tile, row PRG = zeros
-  __shared__ __attribute__((aligned(16))) float red[8 * PRG * PJU];   // per-wave producer sums
-  __shared__ float outs[4 * PRG * PJU];                               // dG of the step (HBM copy)
-  __shared__ int quit;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
-  const int j0 = r * PJU, b0 = g * PRG;
-  const int T = a.T, B = a.B, rows = min(PRG, B - b0);
-  const __amdgpu_buffer_rsrc_t prs = rsrc_of(a.pay, (long long)ps_bytes(a.ng, H));
-  unsigned* flags = a.ctl + 4 + g * PFL;
-
-  // A fragments: W_hh^T[j][q*H + j0 + 8*(lane>>4) .. +8], j = w*CW + 16m + (lane & 15)
-  bf16x8 wf[NT][4];
-#pragma unroll
-  for (int m = 0; m < NT; ++m) {
-    const bf16* row = a.wt + (long long)(w * CW + 16 * m + (lane & 15)) * G + j0 + 8 * (lane >> 4);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) wf[m][q] = *reinterpret_cast<const bf16x8*>(row + q * H);
-  }
-  for (int i = tid; i < (PRG + 1) * DP / 2; i += PNT) reinterpret_cast<unsigned*>(ds16)[i] = 0u;
-  if (tid == 0) quit = 0;
-  const int pr = (tid >> 5) & (PRG - 1), pu = tid & 31, pb = b0 + pr, pj = j0 + pu;
-  const bool pv = tid < PRG * PJU && pb < B;
-  const int bcol = lane & 15, brow = bcol < PRG ? bcol : PRG;  // B operand: utterance columns
-  // float offset of this member's outgoing partial block for consumer rd, utterance bcol
-  const long long pbase = ((long long)g * NR + r) * NR * (PRG * PJU);
-  const long long pslot = (long long)a.ng * NR * NR * (PRG * PJU);
-  float dc = 0.f;
-  __syncthreads();
-
-  for (int s = 0; s < T; ++s) {
-    const int t = T - 1 - s;
-    stamp(a.trace, T, s, 0);
-    float dh = 0.f, ct = 0.f, cp = 0.f, gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f;
-    if (pv) {
-      const long long oh = ((long long)pb * T + t) * H + pj;
-      dh = a.dhout[oh];
-      ct = a.call[oh];
-      cp = t > 0 ? a.call[oh - H] : 0.f;
-      const float* gp = a.gall + ((long long)pb * T + t) * G + pj;
-      gi = gp[0];
-      gf = gp[H];
-      gg = gp[2 * H];
-      go = gp[3 * H];
-    }
-    if (s > 0) {
-      if (w == 0 && !poll_flags(flags, NR, (unsigned)s, a.ctl, a.fault, a.spin)) quit = 1;
-      __syncthreads();
-      if (quit) return;  // block-uniform exit after a spin timeout
-      // wave w: producers w, w + 8, ...; lane = one 16-B chunk of the 8 x 32 block
-      const long long src = ((s - 1) & 1) * pslot + ((long long)g * NR * NR + r) * (PRG * PJU) + 4 * lane;
-      f32x4 v[NPW];
-#pragma unroll
-      for (int i = 0; i < NPW; ++i)
-        v[i] = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)((src + (long long)(w + 8 * i) * NR * (PRG * PJU)) * 4),
-                                                         0, AUX_SC1));
-      f32x4 sum = v[0];
-#pragma unroll
-      for (int i = 1; i < NPW; ++i) sum += v[i];
-      *reinterpret_cast<f32x4*>(red + w * (PRG * PJU) + 4 * lane) = sum;
-      __syncthreads();
-      stamp(a.trace, T, s, 1);
-      if (pv) {
-#pragma unroll
-        for (int ww = 0; ww < 8; ++ww) dh += red[ww * (PRG * PJU) + pr * PJU + pu];
-      }
-    }
-    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
-    if (pv) {
-      const float tc = ftanh(ct);
-      const float dcs = dc + dh * go * (1.f - tc * tc);
-      v0 = dcs * gg * gi * (1.f - gi);  // d(pre i)
-      v1 = dcs * cp * gf * (1.f - gf);  // d(pre f)
-      v2 = dcs * gi * (1.f - gg * gg);  // d(pre g)
-      v3 = dh * tc * go * (1.f - go);   // d(pre o)
-      dc = dcs * gf;
-    }
-    if (tid < PRG * PJU) {
-      bf16* dsr = ds16 + pr * DP + pu;
-      dsr[0] = (bf16)v0;
-      dsr[PJU] = (bf16)v1;
-      dsr[2 * PJU] = (bf16)v2;
-      dsr[3 * PJU] = (bf16)v3;
-      float* o = outs + tid;
-      o[0] = v0;
-      o[PRG * PJU] = v1;
-      o[2 * PRG * PJU] = v2;
-      o[3 * PRG * PJU] = v3;
-    }
-    __syncthreads();
-    stamp(a.trace, T, s, 2);
-    if (s + 1 < T) {
-      // ---- partial dh of the next step from the own dG tile, published to every consumer
-      bf16x8 bfr[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) bfr[q] = *reinterpret_cast<const bf16x8*>(ds16 + brow * DP + q * PJU + 8 * (lane >> 4));
-      f32x4 acc[NT];
-#pragma unroll
-      for (int m = 0; m < NT; ++m) {
-        acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[m][q], bfr[q], acc[m], 0, 0, 0);
-      }
-      if (bcol < rows) {
-        const long long dst = (s & 1) * pslot + pbase + bcol * PJU;
-#pragma unroll
-        for (int m = 0; m < NT; ++m) {
-          const int jj = w * CW + 16 * m + 4 * (lane >> 4);  // 4 consecutive dh columns
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[m]), prs,
-                                                 (int)((dst + (long long)(jj >> 5) * (PRG * PJU) + (jj & 31)) * 4), 0,
-                                                 AUX_SC1);
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (w == 0) raise_flag(flags, r, (unsigned)(s + 1));
-    }
-    // ---- dG of the step to HBM (after the hand-off: its stores never delay the drain)
-    if (w >= 4) {
-      const int cell = tid - PRG * PJU, ob = b0 + (cell >> 5), oj = j0 + (cell & 31);
-      if (ob < B) {
-        const float* o = outs + cell;
-        const long long og = ((long long)ob * T + t) * G + oj;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) a.dg[og + q * H] = o[q * PRG * PJU];
-        if (a.dg16) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) a.dg16[og + q * H] = (bf16)o[q * PRG * PJU];
-        }
-      }
-    }
-    stamp(a.trace, T, s, 3);
-  }
-}
-
 // =============================================================== two stacked layers, one launch
 // Decoder lstm2 (nn.LSTM(512 -> 1024, num_layers=2), AutoVC.py:96,110) forward as a layer
 // WAVEFRONT: tick k runs layer 0 at step k and layer 1 at step k - 1, so both layers share one
@@ -1934,14 +1772,6 @@ unsigned spin_bound() {
   return s ? s : env ? env : PSPIN;
 }
 
-// AVC_LSTM_EXCL=1 (A/B): persistent recurrences claim the whole LDS of their CU, so no
-// side-stream GEMM workgroup can share the CU with them (they wait for the recurrence instead).
-constexpr size_t LDS_ALL = 160 * 1024;
-size_t excl_lds(size_t need) {
-  static const bool ex = getenv("AVC_LSTM_EXCL") && atoi(getenv("AVC_LSTM_EXCL")) == 1;
-  return ex ? LDS_ALL : need;
-}
-
 // Dynamic-LDS attribute of the persistent backward kernels, set once per (kernel, device).
 template <int H, bool GR>
 void set_bwd_lds_attr() {
@@ -1950,7 +1780,7 @@ void set_bwd_lds_attr() {
   static std::once_flag once[MAXDEV];
   std::call_once(once[dev & (MAXDEV - 1)], [] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_persist_bwd<H, GR>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)excl_lds(persist_bwd_lds<H>()));
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_bwd_lds<H>());
   });
 }
 
@@ -1976,17 +1806,17 @@ int nap() {
   return v;
 }
 
-// Backward form: 2 = sentinel hand-off (lstm_persist_bwd_sg, default), 3 = the same with the
-// L2-resident (XCD-verified plain-store) request, 1 = partial-sum exchange (lstm_persist_bwd_ps),
-// 0 = flag / granule gather (lstm_persist_bwd).  avc_lstm_set_bwd_form or AVC_LSTM_BWD_FORM
-// override the default; AVC_LSTM_L2=1 adds the L2-resident request to form 2.
+// Backward form: 0 = flag / granule gather (lstm_persist_bwd, default), 2 = sentinel hand-off
+// (lstm_persist_bwd_sg), 3 = the same with the L2-resident (XCD-verified plain-store) request.
+// avc_lstm_set_bwd_form or AVC_LSTM_BWD_FORM override the default; AVC_LSTM_L2=1 adds the
+// L2-resident request to form 2.  (Form 1, the partial-sum exchange, measured slower at H = 1024
+// -- 5.56 vs 4.06 us/step, profiles/r2_lstm_handoff_forms.txt -- and was removed.)
 std::atomic<int> g_bwd_form{-1};  // avc_lstm_set_bwd_form; -1 = environment / default
 int bwd_form() {
   static const int env = getenv("AVC_LSTM_BWD_FORM") ? atoi(getenv("AVC_LSTM_BWD_FORM")) : 0;
   const int f = g_bwd_form.load(std::memory_order_relaxed);
   return f < 0 ? env : f;
 }
-bool ps_bwd() { return bwd_form() == 1; }
 bool sg_bwd() { return bwd_form() >= 2; }
 int l2_mode() {
   static const int v = getenv("AVC_LSTM_L2") ? atoi(getenv("AVC_LSTM_L2")) : 0;
@@ -1996,7 +1826,6 @@ int l2_mode() {
 template <int H>
 const void* persist_fn(bool bwd) {
   if (bwd && sg_bwd()) return reinterpret_cast<const void*>(&lstm_persist_bwd_sg<H>);
-  if (bwd && ps_bwd()) return reinterpret_cast<const void*>(&lstm_persist_bwd_ps<H>);
   if (bwd) {
     if (gran(true, H)) {
       set_bwd_lds_attr<H, true>();
@@ -2050,19 +1879,18 @@ bool persistent_path(int B, int H, int dirs, bool bf, bool bwd) {
   const int ng = (B + PRG - 1) / PRG, grid = ng * (H / PJU);
   if (grid > num_cus()) return false;
   const void* fn = H == 1024 ? persist_fn<1024>(bwd) : H == 768 ? persist_fn<768>(bwd) : persist_fn<512>(bwd);
-  const size_t lds = !bwd || ps_bwd() || sg_bwd() ? 0
-                     : H == 1024 ? excl_lds(persist_bwd_lds<1024>())
-                     : H == 768  ? excl_lds(persist_bwd_lds<768>())
-                                 : excl_lds(persist_bwd_lds<512>());
+  const size_t lds = !bwd || sg_bwd() ? 0
+                     : H == 1024 ? persist_bwd_lds<1024>()
+                     : H == 768  ? persist_bwd_lds<768>()
+                                 : persist_bwd_lds<512>();
   return fits_resident(fn, PNT, lds, grid);
 }
 
 template <int H>
 void launch_persist_bwd(dim3 grid, hipStream_t s, bool gr, const PersistBwdArgs& p) {
   if (sg_bwd()) lstm_persist_bwd_sg<H><<<grid, PNT, 0, s>>>(p);
-  else if (ps_bwd()) lstm_persist_bwd_ps<H><<<grid, PNT, 0, s>>>(p);
-  else if (gr) lstm_persist_bwd<H, true><<<grid, PNT, excl_lds(persist_bwd_lds<H>()), s>>>(p);
-  else lstm_persist_bwd<H, false><<<grid, PNT, excl_lds(persist_bwd_lds<H>()), s>>>(p);
+  else if (gr) lstm_persist_bwd<H, true><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
+  else lstm_persist_bwd<H, false><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
 }
 
 template <int HM>
@@ -2110,9 +1938,9 @@ bool persist2_path(int B, int H, int In1, bool bf) {
   (void)hipGetDevice(&dev);
   std::call_once(once[dev & (MAXDEV - 1)], [] {
     for (const void* f : {L2FN(1, false), L2FN(2, false), L2FN(1, true), L2FN(2, true)})
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)excl_lds(persist2_lds<1024>()));
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist2_lds<1024>());
   });
-  return fits_resident(L2FN(2, false), PNT, excl_lds(persist2_lds<1024>()), grid);
+  return fits_resident(L2FN(2, false), PNT, persist2_lds<1024>(), grid);
 }
 
 extern "C" int avc_lstm2_persistent(int B, int H, int in1, int compute) {
@@ -2164,7 +1992,7 @@ extern "C" int avc_lstm2_fwd(const float* xproj0, const void* w_hh0, const void*
   // instead of after the products
   static const int cfg = getenv("AVC_LSTM2_CFG") ? atoi(getenv("AVC_LSTM2_CFG")) : 20;
   const dim3 grid(ng * (H / QJU));
-  const size_t lds = excl_lds(persist2_lds<1024>());
+  const size_t lds = persist2_lds<1024>();
   switch (cfg) {
     case 10: lstm2_persist_fwd<1024, 2, 1, false><<<grid, PNT, lds, s>>>(p); break;
     case 11: lstm2_persist_fwd<1024, 2, 1, true><<<grid, PNT, lds, s>>>(p); break;
@@ -2175,17 +2003,16 @@ extern "C" int avc_lstm2_fwd(const float* xproj0, const void* w_hh0, const void*
 }
 
 extern "C" int avc_lstm_set_bwd_form(int form) {
-  AVC_CHECK_ARG(form >= -1 && form <= 3, "avc_lstm_set_bwd_form: form must be -1 .. 3");
+  AVC_CHECK_ARG(form == -1 || form == 0 || form == 2 || form == 3,
+                "avc_lstm_set_bwd_form: form must be -1, 0, 2 or 3");
   g_bwd_form.store(form, std::memory_order_relaxed);
   return 0;
 }
 
 extern "C" size_t avc_lstm_bwd_scratch_bytes(int B, int H, int dirs) {
   if (B <= 0 || H <= 0 || dirs <= 0) return 0;
-  const int ng = (B + PRG - 1) / PRG;
-  size_t n = std::max((size_t)16 * dirs * B * H, (size_t)32 * B * H + 8192);
-  if (H % PJU == 0) n = std::max(n, px_payload_off(ng) + ps_bytes(ng, H));
-  return n;
+  // per-step ping-pong (16 dirs B H) or control words + the [2][B][4H] granule payload (32 B H)
+  return std::max((size_t)16 * dirs * B * H, (size_t)32 * B * H + 8192);
 }
 
 extern "C" int avc_lstm_persistent(int B, int H, int dirs, int compute, int backward) {
@@ -2322,7 +2149,7 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
     const bool sg = sg_bwd();
     AVC_CHECK_ARG(!sg || (dgates_bf16 && (long long)B * T * 8 * H < (1ll << 31)),
                   "avc_lstm_bwd: the sentinel form needs the bf16 dG twin and B*T*4H*2 < 2^31 bytes");
-    const bool gr = gran(true, H) && !ps_bwd() && !sg;
+    const bool gr = gran(true, H) && !sg;
     (void)hipMemsetAsync(gbuf, 0, gr ? px_payload_off(ng) + (size_t)32 * B * H : px_ctl_bytes(ng), s);
     // the twin starts as the sentinel everywhere (re-initialised every call)
     if (sg) (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dgates_bf16), (int)DG_SENT, (size_t)B * T * 2 * H, s);

@@ -392,7 +392,8 @@ def lstm_bwd_scratch(B, H, dirs, device):
 
 
 def lstm_set_bwd_form(form: int) -> None:
-    """Debug / A-B: persistent backward form (1 partial-sum exchange, 0 dG gather, -1 default)."""
+    """Debug / A-B: persistent backward form (0 dG gather + flags, 2 sentinel hand-off, 3 sentinel +
+    XCD-verified L2-resident stores, -1 default)."""
     L.call("avc_lstm_set_bwd_form", int(form))
 
 

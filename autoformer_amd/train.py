@@ -222,7 +222,6 @@ class FusedAdam:
 
 
 # ------------------------------------------------------------------------- bench step
-_MAIN_PRIO = os.environ.get("AVC_MAIN_PRIO", "0") == "1"
 # workgroup cap of the decoder-slice Adam that runs beside the encoder backward (0 = full grid;
 # 256 measured best: the full 4096-block grid slowed the latency-bound BiLSTM backward beside it)
 _SIDE_ADAM_BLOCKS = int(os.environ.get("AVC_SIDE_ADAM_BLOCKS", "256"))
@@ -274,7 +273,6 @@ class TrainStep:
         self._fault = K.fault_word(self.flat.device)
         self._fault_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         self._fault_ev = None
-        self._hp = None
         # optional exposed all-reduce time: a list of (start, end) HIP event pairs recorded on
         # the main stream around its wait for the collective (bench.py's allreduce_ms)
         self.comm_timing = None
@@ -346,18 +344,6 @@ class TrainStep:
             self.comm_timing.append(ev)
 
     def step(self, x, emb):
-        if _MAIN_PRIO and self.graph_fb is None:
-            # the critical path (recurrences, data gradients) on a high-priority queue: when
-            # both have workgroups waiting, the dispatcher serves it before the weight-gradient
-            # side stream (same-priority queues are served round-robin)
-            if self._hp is None:
-                self._hp = torch.cuda.Stream(priority=-1)
-            cur = torch.cuda.current_stream()
-            self._hp.wait_stream(cur)
-            with torch.cuda.stream(self._hp):
-                loss = self._step(x, emb)
-            cur.wait_stream(self._hp)
-            return loss
         return self._step(x, emb)
 
     def _step(self, x, emb):

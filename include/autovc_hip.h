@@ -204,17 +204,17 @@ int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T,
  * (small H, pass the same layout as avc_lstm_fwd). dcbuf: B*H*dirs fp32.  gbuf (large H,
  * bf16 compute): at least avc_lstm_bwd_scratch_bytes(B, H, dirs) bytes.  For dirs == 1, H in
  * {512, 768, 1024} and enough CUs the whole sequence is ONE persistent launch (W_hh^T slices
- * register-resident; each workgroup multiplies its own dG_{t+1} columns by its W_hh rows and
- * hands the fp32 partial dh over as write-through payload + flags, bounded spins;
- * timeout flag = u32 at byte 0 of gbuf).  The small-H and persistent launches can also write a
- * bf16 copy of dgates (dgates_bf16, else null); the per-step path needs null. */
-/* Bytes of the backward scratch gbuf for (B, H, dirs) -- the persistent partial-sum form needs
- * 2*ceil(B/8)*(H/32)^2 KB of fp32 partials besides the control words (16.8 MB at B=64, H=1024). */
+ * register-resident; each workgroup gathers the group's bf16 dG_{t+1}, handed over as
+ * write-through payload + per-workgroup flags, bounded spins; timeout flag = u32 at byte 0 of
+ * gbuf).  The small-H and persistent launches can also write a bf16 copy of dgates (dgates_bf16,
+ * else null; the sentinel forms 2/3 need it: it is their payload); the per-step path needs null. */
+/* Bytes of the backward scratch gbuf for (B, H, dirs). */
 size_t avc_lstm_bwd_scratch_bytes(int B, int H, int dirs);
 
-/* Debug / A-B: form of the persistent backward recurrence.  1 = partial-sum exchange (each
- * workgroup publishes its fp32 partial dh; the default), 0 = dG gather (each workgroup gathers
- * the group's bf16 dG_{t+1}), -1 = back to the default (AVC_LSTM_BWD_PS=0 selects 0). */
+/* Debug / A-B: form of the persistent backward recurrence.  0 = dG gather with per-workgroup flags
+ * (the default), 2 = sentinel hand-off (the bf16 dG twin is filled with a signalling-NaN pattern
+ * and is itself the payload; no flags), 3 = form 2 with plain (L2-resident) payload stores where a
+ * group's workgroups verify one shared XCD, -1 = back to the default (AVC_LSTM_BWD_FORM). */
 int avc_lstm_set_bwd_form(int form);
 
 int avc_lstm_bwd(const float* dh_out, const float* h, const float* c, const float* gates,

@@ -111,7 +111,7 @@ def test_converter_get_wavs_end_to_end():
         g.load_state_dict(sd)
         conv = Converter(m.cuda().train(), T, vocoder=MelVocoder(generator=g))
         _, _, mel = conv.get_trans_mel(x[0][: T - 6], None, e[0], e[1], isPlay=True)  # (1, T-6, 80)
-        wav = conv.get_wavs(mel)
+        wav = conv.get_wavs(mel, frames=True)
         wav2 = conv.get_wavs(mel.transpose(1, 2).contiguous())
         torch.cuda.synchronize()
         assert wav.shape == (1, (T - 6) * 256)
@@ -120,3 +120,27 @@ def test_converter_get_wavs_end_to_end():
         assert torch.equal(wav, wav2)
     finally:
         A.set_compute("bf16")
+
+
+def test_get_wavs_layout_is_stated_not_guessed():
+    """a frame-major mel with T == 80 is vocoded frame-major only when the caller says
+    so (frames=True); the default is the reference's (1, 80, T) contract; a wrong layout raises."""
+    from autoformer_amd.convert import Converter
+
+    class Voc:
+        def inverse(self, m):
+            return ("inverse", tuple(m.shape))
+
+        def inverse_frames(self, m):
+            return ("frames", tuple(m.shape))
+
+    c = Converter(None, 80, device="cpu", vocoder=Voc())
+    sq = torch.zeros(1, 80, 80)
+    assert c.get_wavs(sq) == ("inverse", (1, 80, 80))
+    assert c.get_wavs(sq, frames=True) == ("frames", (1, 80, 80))
+    assert c.get_wavs(torch.zeros(1, 80, 64)) == ("inverse", (1, 80, 64))
+    assert c.get_wavs(torch.zeros(1, 64, 80), frames=True) == ("frames", (1, 64, 80))
+    with pytest.raises(ValueError):
+        c.get_wavs(torch.zeros(1, 64, 80))
+    with pytest.raises(ValueError):
+        c.get_wavs(torch.zeros(1, 80, 64), frames=True)
