@@ -85,7 +85,6 @@ _SIGS = {
     "avc_lstm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                              c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "avc_lstm_bwd_scratch_bytes": (c_size, [c_int, c_int, c_int]),
-    "avc_lstm_set_bwd_form": (c_int, [c_int]),
     "avc_capture_deps": (c_int, [c_void_p, ctypes.POINTER(c_void_p), c_int]),
     "avc_graph_split": (c_int, [c_void_p, ctypes.POINTER(c_void_p), c_int, ctypes.POINTER(c_void_p), c_int, c_int,
                                 ctypes.POINTER(c_void_p), ctypes.POINTER(c_int)]),

@@ -408,9 +408,22 @@ __global__ void __launch_bounds__(256, 2) gemm_tt_halo_kernel(GemmArgs g) {
   const int rem = lid - ks * nC * nM;
   const int mt = rem / nC, ct = rem - mt * nC;
   const int m0 = mt * BM, c0 = ct * CW;
-  const int kbeg = ks * g.klen;
-  const int kend = min(g.K, kbeg + g.klen);
-  const int nkt = kend > kbeg ? (kend - kbeg + FBK - 1) / FBK : 0;
+  // K-tiles follow the utterance grid: utterance u has tpu tiles of FBK frames, the last one
+  // partial when T % FBK != 0 (its dy rows past the utterance load as zeros), so a tile never
+  // spans two utterances and one halo copy serves all five taps.  Split ks takes tiles
+  // [tb, te) of the (K / T) * tpu.
+  const int tpu = (T + FBK - 1) / FBK;
+  const int ntiles = (g.K / T) * tpu;
+  const int tps = (ntiles + g.split_k - 1) / g.split_k;
+  const int tb = min(ntiles, ks * tps), te = min(ntiles, tb + tps);
+  const int nkt = te - tb;
+  auto tile = [&](int j, int& fend, int& u0) {
+    const int u = j / tpu;
+    u0 = u * T;
+    const int f0 = u0 + (j - u * tpu) * FBK;
+    fend = min(f0 + FBK, u0 + T);
+    return f0;
+  };
 
   TtLoader<false> la;
   la.init(g.a, m0, 0);
@@ -423,15 +436,21 @@ __global__ void __launch_bounds__(256, 2) gemm_tt_halo_kernel(GemmArgs g) {
     hrow[i] = 16 * (2 * wid + i) + (lane >> 2);
     hchk[i] = 8 * ((lane & 3) ^ hswz(hrow[i]));
   }
-  auto issue_halo = [&](char* tile, int f0) {
-    const int u0 = (f0 / T) * T;  // the K-tile's utterance: frames [u0, u0 + T)
+  // the K-tile at frame f0 of the utterance [u0, u0 + T); halo rows outside it load as zeros
+  auto issue_halo = [&](char* st, int f0, int u0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int f = f0 - pad + hrow[i];
-      const bool ok = hrow[i] < FBK + TAPS - 1 && f >= u0 && f < u0 + T && f < g.K;
+      const bool ok = hrow[i] < FBK + TAPS - 1 && f >= u0 && f < u0 + T;
       const void* src = ok ? (const void*)(xb + (long long)f * ldx + c0 + hchk[i]) : (const void*)g_zero16_tt;
-      glds16(src, tile + (2 * wid + i) * 1024);
+      glds16(src, st + (2 * wid + i) * 1024);
     }
+  };
+  auto issue_tile = [&](char* st, int j) {
+    int fend, u0;
+    const int f0 = tile(j, fend, u0);
+    la.issue(st, f0, fend);
+    issue_halo(st + TSTAGE_OP, f0, u0);
   };
 
   f32x4 acc[4][TAPS];
@@ -446,10 +465,7 @@ __global__ void __launch_bounds__(256, 2) gemm_tt_halo_kernel(GemmArgs g) {
 
 #pragma unroll
   for (int p = 0; p < P; ++p)
-    if (p < nkt) {
-      la.issue(smem_raw + p * HSTAGE, kbeg + p * FBK, kend);
-      issue_halo(smem_raw + p * HSTAGE + TSTAGE_OP, kbeg + p * FBK);
-    }
+    if (p < nkt) issue_tile(smem_raw + p * HSTAGE, tb + p);
   for (int kt = 0; kt < nkt; ++kt) {
     const int ahead = min(P - 1, nkt - 1 - kt);  // K-tiles allowed to stay in flight
     if constexpr (P >= 2) {
@@ -459,11 +475,7 @@ __global__ void __launch_bounds__(256, 2) gemm_tt_halo_kernel(GemmArgs g) {
       wait_vm<0>();
     }
     raw_barrier();
-    if (kt + P < nkt) {
-      char* st = smem_raw + ((kt + P) % NST) * HSTAGE;
-      la.issue(st, kbeg + (kt + P) * FBK, kend);
-      issue_halo(st + TSTAGE_OP, kbeg + (kt + P) * FBK);
-    }
+    if (kt + P < nkt) issue_tile(smem_raw + ((kt + P) % NST) * HSTAGE, tb + kt + P);
     const char* As = smem_raw + (kt % NST) * HSTAGE;
     const char* Hs = As + TSTAGE_OP;
 #pragma unroll
@@ -529,7 +541,7 @@ bool gemm_tt_launch(const GemmArgs& g, hipStream_t s) {
   const bool halo_off = halo == 0;
   const OpDev& x = g.b;
   if (!halo_off && x.win && x.taps == 5 && x.t_in == x.t_out && 2 * x.pad == x.taps - 1 && x.chans % 32 == 0 &&
-      x.t_out % FBK == 0 && g.batch == 1 && g.N == x.taps * x.chans && !g.res && !g.c16 && !g.bias && !g.bn_partial) {
+      g.K % x.t_out == 0 && g.batch == 1 && g.N == x.taps * x.chans && !g.res && !g.c16 && !g.bias && !g.bn_partial) {
     if (halo == 2) launch_halo<2>(g, s);
     else launch_halo<3>(g, s);
     return true;

@@ -1088,8 +1088,6 @@ struct PersistBwdArgs {
   unsigned spin;
   int nap;
   int B, T, ng;
-  int l2;      // sentinel form: request the L2-resident (XCD-verified plain-store) hand-off
-  int sample;  // sentinel form: poll one sample chunk per producer wave before re-loading
 };
 
 template <int H, bool GR>
@@ -1244,265 +1242,6 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
       }
     }
     stamp(a.trace, T, s, 3);
-  }
-}
-
-// ---------------------------------------------------------------- backward, sentinel hand-off
-// The default backward.  The bf16 twin of dG that the recurrence writes for the later GEMMs IS
-// the hand-off payload: before the launch the host fills the twin with the sentinel dword DG_SENT
-// (two signalling-NaN bf16; v_cvt_pk_bf16_f32 quiets every NaN, so no computed dG pair has this bit
-// pattern), and a consumer re-reads a payload chunk until none of its four dwords is the sentinel.
-// So the data is its own flag (MI355X_MICROARCH.md "Valid forms", R2: no drain, no flag word, no
-// second round trip for the payload after the flag) at the bf16 payload size (no tags), with no
-// parity slots and no separate twin store.  A consumer needs 4-byte atomicity only: a dword is
-// either still the sentinel or final.
-//   consumer: wave w owns K blocks kb = w + 8i (i < H/64) of the 4H contraction; lane (row, kq)
-//             of the 16x16x32 MFMA A fragment loads its 16-B chunk of dG_{t+1} straight into
-//             registers with an sc1 buffer load (L1 bypassed), re-loads only the chunks still
-//             holding the sentinel, and runs its 2 x H/64 MFMAs once the wave's chunks are all in
-//             -- no LDS staging of the payload, no workgroup barrier between the wait and the
-//             product; a wave's K blocks come from 4 producers (H = 1024).
-//   reduce:    the eight waves' 8 x 32 partial products meet in LDS (double-buffered by step
-//             parity: waves 4-7 may enter the next step's product while waves 0-3 still read this
-//             one's), ONE workgroup barrier per step.
-//   producer:  waves 0-3 own the 8 x 32 (utterance, unit) cells; each wave transposes its two
-//             rows' 4 gates x 32 units through a wave-private LDS tile and stores 16-B chunks of
-//             the bf16 twin (sc1 write-through; plain stores when the group is verified
-//             XCD-local, below), then the fp32 dG.
-//   inputs:   dh, c_t, c_{t-1} and the 4 activated gates of step s+1 are loaded during step s
-//             (after the wait), two register sets alternating by step parity, so the HBM latency
-//             of the step inputs never sits between a consumer's wait and its product.
-// L2-resident mode (a.l2, opt-in AVC_LSTM_L2=1): every member reads its XCC id
-// (s_getreg HW_REG_XCC_ID) and publishes it; if all members of the group report the same XCD
-// the group's payload stores are plain (the line stays in that XCD's L2, which every member
-// reads through, instead of being written through and re-fetched from the fabric), otherwise the
-// group keeps sc1 stores.  The placement is checked, never assumed.
-constexpr unsigned DG_SENT = 0x7F817F81u;
-
-__device__ __forceinline__ bool sent_free(u32x4_t v) {
-  return (v[0] != DG_SENT) & (v[1] != DG_SENT) & (v[2] != DG_SENT) & (v[3] != DG_SENT);
-}
-
-__device__ __forceinline__ unsigned xcc_id() {
-  unsigned x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
-  return x;
-}
-
-struct BwdIn {
-  float dh, ct, cp, gi, gf, gg, go;
-};
-
-template <int H>
-__global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd_sg(PersistBwdArgs a) {
-  constexpr int G = 4 * H, NW = PNT / 64, NKB = G / 32 / NW, NR = H / PJU;
-  static_assert(G % (32 * NW) == 0 && NR <= PFL, "K blocks per wave / members per group");
-  __shared__ float red[2][NW][PRG][PJU + 1];
-  __shared__ __attribute__((aligned(16))) bf16 pub[4][2 * 4 * PJU];
-  __shared__ int quit, local;
-  __shared__ unsigned long long xlast[2];  // trace: the last wave's exchange-complete time
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
-  const int j0 = r * PJU, b0 = g * PRG;
-  const int T = a.T, B = a.B, rows = min(PRG, B - b0);
-  const __amdgpu_buffer_rsrc_t dgr = rsrc_of(a.dg16, (long long)B * T * G * 2);
-
-  // W_hh^T fragments (B operand): unit j0 + 16n + (lane & 15), gate rows 32 kb + 8 (lane >> 4) ..
-  bf16x8 wf[2][NKB];
-#pragma unroll
-  for (int n = 0; n < 2; ++n) {
-    const bf16* row = a.wt + (long long)(j0 + n * 16 + (lane & 15)) * G + 8 * (lane >> 4);
-#pragma unroll
-    for (int i = 0; i < NKB; ++i) wf[n][i] = *reinterpret_cast<const bf16x8*>(row + 32 * (w + NW * i));
-  }
-  // A fragment lane: utterance row b0 + arow (rows >= 8 are the zero padding), K offset 8 akq
-  const int arow = lane & 15, akq = lane >> 4;
-  const bool aact = arow < rows;
-  const int abase = (b0 + (aact ? arow : 0)) * T;  // frame row of utterance b0 + arow at t = 0
-  // cell (utterance, unit) of threads 0..255; a cell past the batch reads row b0 (clamped, unused)
-  const int pr = (tid >> 5) & (PRG - 1), pu = tid & 31, pb = b0 + pr, pj = j0 + pu;
-  const bool pv = tid < PRG * PJU && pb < B;
-  const long long cbase = (long long)(pb < B ? pb : b0) * T;
-  if (tid == 0) {
-    quit = 0;
-    local = 0;
-    xlast[0] = xlast[1] = 0ull;
-  }
-  // ---- XCD check of the L2-resident mode: member r publishes XCC id + 1 in the group's flag row
-  unsigned* flags = a.ctl + 4 + g * PFL;
-  if (a.l2 && w == 0) {
-    const unsigned me = xcc_id() + 1u;
-    if (lane == 0) __hip_atomic_store((gu32*)flags + r, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned spins = 0;
-    bool same = true;
-    while (true) {
-      const unsigned v =
-          lane < NR ? __hip_atomic_load((gu32*)flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : me;
-      if (__all(v != 0u)) {
-        same = __all(v == me);
-        break;
-      }
-      if (++spins > a.spin) {
-        if (lane == 0) {
-          atomicOr(a.ctl, 1u);
-          if (a.fault) atomicOr(a.fault, 1u);
-          quit = 1;
-        }
-        same = false;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (lane == 0) local = same ? 1 : 0;
-  }
-
-  // Step inputs of time t (waves 0-3): unconditional loads from clamped addresses, so no branch
-  // merges a loaded register with a constant (a merge would make the compiler copy -- and wait
-  // for -- the value right after its load); c_{t-1} at t = 0 is masked where it is used.
-  auto prefetch = [&](int t, BwdIn& o) {
-    if (w < 4) {
-      const int tc = max(t, 0);
-      const long long oh = (cbase + tc) * H + pj;
-      o.dh = a.dhout[oh];
-      o.ct = a.call[oh];
-      o.cp = a.call[tc > 0 ? oh - H : oh];
-      const float* gp = a.gall + (cbase + tc) * G + pj;
-      o.gi = gp[0];
-      o.gf = gp[H];
-      o.gg = gp[2 * H];
-      o.go = gp[3 * H];
-    }
-  };
-  float dc = 0.f;
-  // Cell update of (pb, pj) at time t (waves 0-3) and publication of dG_t.
-  auto tail = [&](int t, const BwdIn& cur, float dhr, bool plain) {
-    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
-    if (pv) {
-      const float dh = cur.dh + dhr, cp = t > 0 ? cur.cp : 0.f;
-      const float tc = ftanh(cur.ct);
-      const float dcs = dc + dh * cur.go * (1.f - tc * tc);
-      v0 = dcs * cur.gg * cur.gi * (1.f - cur.gi);  // d(pre i)
-      v1 = dcs * cp * cur.gf * (1.f - cur.gf);      // d(pre f)
-      v2 = dcs * cur.gi * (1.f - cur.gg * cur.gg);  // d(pre g)
-      v3 = dh * tc * cur.go * (1.f - cur.go);       // d(pre o)
-      dc = dcs * cur.gf;
-    }
-    // wave-private transpose: [2 rows][4 gates][32 units] bf16, then 16-B chunks (8 units)
-    bf16* pw = pub[w] + ((tid >> 5) & 1) * (4 * PJU) + pu;
-    pw[0] = (bf16)v0;
-    pw[PJU] = (bf16)v1;
-    pw[2 * PJU] = (bf16)v2;
-    pw[3 * PJU] = (bf16)v3;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane < 32) {
-      const int row = lane >> 4, q = (lane >> 2) & 3, c8 = lane & 3, ob = b0 + 2 * w + row;
-      if (ob < B) {
-        const u32x4_t x = *reinterpret_cast<const u32x4_t*>(pub[w] + row * (4 * PJU) + q * PJU + c8 * 8);
-        const int off = (((ob * T + t) * G) + q * H + j0 + c8 * 8) * 2;
-        if (plain) __builtin_amdgcn_raw_buffer_store_b128(x, dgr, off, 0, 0);
-        else __builtin_amdgcn_raw_buffer_store_b128(x, dgr, off, 0, AUX_SC1);
-      }
-    }
-    if (pv) {
-      float* o = a.dg + ((long long)pb * T + t) * G + pj;
-      o[0] = v0;
-      o[H] = v1;
-      o[2 * H] = v2;
-      o[3 * H] = v3;
-    }
-  };
-
-  BwdIn in0, in1;  // step inputs, even / odd steps (static register sets: the loop is unrolled by 2)
-  prefetch(T - 1, in0);
-  __syncthreads();
-  if (quit) return;
-  const bool plain = local != 0;
-
-  // step s >= 1; returns false on a spin timeout (block-uniform)
-  auto step = [&](int s, const BwdIn& cur, BwdIn& nxt) -> bool {
-    const int t = T - 1 - s;
-    stamp(a.trace, T, s, 0);
-    // ---- dG_{t+1} chunks of this wave's K blocks -> registers, and the product, pipelined: all
-    // NKB chunk loads are issued at once (branch-free: padding lanes load from an offset past the
-    // buffer -- no access, zeros; one address VGPR, chunk i adds the constant i * 512 B as the
-    // instruction's soffset); chunk i's two MFMAs issue as soon as chunk i holds no sentinel
-    // (accumulation order fixed: the result is bit-reproducible), so the product overlaps the
-    // arrival of the later chunks.  A chunk still holding the sentinel re-loads every chunk not
-    // yet consumed (the producers run in step: the ones behind it are most likely stale too).
-    u32x4_t v[NKB];
-    const int off0 = aact ? ((abase + t + 1) * G + 8 * akq + 32 * w) * 2 : OOB;
-#pragma unroll
-    for (int i = 0; i < NKB; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(dgr, off0, 64 * NW * i, AUX_SC1);
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    unsigned spins = 0;
-    constexpr int NP = NR / NW;  // producers of this wave's K blocks: w + 8m, m < NP
-    const int sm = lane >> 2, spw = lane & 3;
-    const int soff = (lane < 4 * NP && 2 * spw < rows)
-                         ? (((b0 + 2 * spw) * T + t + 1) * G + 32 * (w + NW * sm)) * 2 : OOB;
-#pragma unroll
-    for (int i = 0; i < NKB; ++i) {
-      while (!__all(sent_free(v[i]))) {
-        if (++spins > a.spin) {  // timeout: raise, finish with garbage, exit after the barrier
-          if (lane == 0) {
-            atomicOr(a.ctl, 1u);
-            if (a.fault) atomicOr(a.fault, 1u);
-            quit = 1;
-          }
-          break;
-        }
-        for (int k = 0; k < a.nap; ++k) __builtin_amdgcn_s_sleep(1);
-        asm volatile("" ::: "memory");  // the re-reads are real loads, never hoisted
-        if (a.sample) {
-          // poll one sample chunk per producer wave (lane 0's chunk of each store instruction)
-          while (!__all(sent_free(__builtin_amdgcn_raw_buffer_load_b128(dgr, soff, 0, AUX_SC1))) &&
-                 ++spins <= a.spin)
-            for (int k = 0; k < a.nap; ++k) __builtin_amdgcn_s_sleep(1);
-        }
-#pragma unroll
-        for (int j = i; j < NKB; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b128(dgr, off0, 64 * NW * j, AUX_SC1);
-      }
-      const bf16x8 af = __builtin_bit_cast(bf16x8, v[i]);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[0][i], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[1][i], acc1, 0, 0, 0);
-    }
-    if (a.trace && lane == 0) atomicMax(&xlast[s & 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    // the next step's inputs: issued once the payload is in, landed long before they are used
-    // (the empty asm keeps the compiler from sinking the loads into the tail below the barrier)
-    prefetch(t - 1, nxt);
-    asm volatile("" ::: "memory");
-    // rows 4*(lane>>4)+e < 8 only for lanes 0..31
-    if (lane < 32) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        red[s & 1][w][4 * (lane >> 4) + e][lane & 15] = acc0[e];
-        red[s & 1][w][4 * (lane >> 4) + e][16 + (lane & 15)] = acc1[e];
-      }
-    }
-    if (a.trace && tid == 0) xlast[(s + 1) & 1] = 0ull;  // last read at step s - 1, by this thread
-    __syncthreads();
-    if (quit) return false;  // block-uniform exit after a spin timeout
-    if (a.trace && tid == 0) a.trace[((long long)blockIdx.x * T + s) * 4 + 1] = xlast[s & 1];
-    stamp(a.trace, T, s, 2);
-    if (w < 4) {
-      float dhr = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < NW; ++ww) dhr += red[s & 1][ww][pr][pu];
-      tail(t, cur, dhr, plain);
-    }
-    if (w == 0) stamp(a.trace, T, s, 3);
-    return true;
-  };
-
-  // step 0 (t = T - 1): no recurrent term
-  stamp(a.trace, T, 0, 0);
-  prefetch(T - 2, in1);
-  if (w < 4) tail(T - 1, in0, 0.f, plain);
-  if (w == 0) stamp(a.trace, T, 0, 3);
-  for (int s = 1; s < T; s += 2) {
-    if (!step(s, in1, in0)) return;
-    if (s + 1 < T && !step(s + 1, in0, in1)) return;
   }
 }
 
@@ -1806,26 +1545,8 @@ int nap() {
   return v;
 }
 
-// Backward form: 0 = flag / granule gather (lstm_persist_bwd, default), 2 = sentinel hand-off
-// (lstm_persist_bwd_sg), 3 = the same with the L2-resident (XCD-verified plain-store) request.
-// avc_lstm_set_bwd_form or AVC_LSTM_BWD_FORM override the default; AVC_LSTM_L2=1 adds the
-// L2-resident request to form 2.  (Form 1, the partial-sum exchange, measured slower at H = 1024
-// -- 5.56 vs 4.06 us/step, profiles/r2_lstm_handoff_forms.txt -- and was removed.)
-std::atomic<int> g_bwd_form{-1};  // avc_lstm_set_bwd_form; -1 = environment / default
-int bwd_form() {
-  static const int env = getenv("AVC_LSTM_BWD_FORM") ? atoi(getenv("AVC_LSTM_BWD_FORM")) : 0;
-  const int f = g_bwd_form.load(std::memory_order_relaxed);
-  return f < 0 ? env : f;
-}
-bool sg_bwd() { return bwd_form() >= 2; }
-int l2_mode() {
-  static const int v = getenv("AVC_LSTM_L2") ? atoi(getenv("AVC_LSTM_L2")) : 0;
-  return bwd_form() == 3 || v == 1;
-}
-
 template <int H>
 const void* persist_fn(bool bwd) {
-  if (bwd && sg_bwd()) return reinterpret_cast<const void*>(&lstm_persist_bwd_sg<H>);
   if (bwd) {
     if (gran(true, H)) {
       set_bwd_lds_attr<H, true>();
@@ -1879,7 +1600,7 @@ bool persistent_path(int B, int H, int dirs, bool bf, bool bwd) {
   const int ng = (B + PRG - 1) / PRG, grid = ng * (H / PJU);
   if (grid > num_cus()) return false;
   const void* fn = H == 1024 ? persist_fn<1024>(bwd) : H == 768 ? persist_fn<768>(bwd) : persist_fn<512>(bwd);
-  const size_t lds = !bwd || sg_bwd() ? 0
+  const size_t lds = !bwd ? 0
                      : H == 1024 ? persist_bwd_lds<1024>()
                      : H == 768  ? persist_bwd_lds<768>()
                                  : persist_bwd_lds<512>();
@@ -1888,8 +1609,7 @@ bool persistent_path(int B, int H, int dirs, bool bf, bool bwd) {
 
 template <int H>
 void launch_persist_bwd(dim3 grid, hipStream_t s, bool gr, const PersistBwdArgs& p) {
-  if (sg_bwd()) lstm_persist_bwd_sg<H><<<grid, PNT, 0, s>>>(p);
-  else if (gr) lstm_persist_bwd<H, true><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
+  if (gr) lstm_persist_bwd<H, true><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
   else lstm_persist_bwd<H, false><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
 }
 
@@ -2000,13 +1720,6 @@ extern "C" int avc_lstm2_fwd(const float* xproj0, const void* w_hh0, const void*
     default: lstm2_persist_fwd<1024, 2, 2, false><<<grid, PNT, lds, s>>>(p); break;
   }
   return avc_check_launch("avc_lstm2_fwd");
-}
-
-extern "C" int avc_lstm_set_bwd_form(int form) {
-  AVC_CHECK_ARG(form == -1 || form == 0 || form == 2 || form == 3,
-                "avc_lstm_set_bwd_form: form must be -1, 0, 2 or 3");
-  g_bwd_form.store(form, std::memory_order_relaxed);
-  return 0;
 }
 
 extern "C" size_t avc_lstm_bwd_scratch_bytes(int B, int H, int dirs) {
@@ -2143,16 +1856,8 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
     p.B = B;
     p.T = T;
     p.ng = ng;
-    p.l2 = l2_mode();
-    static const int sample = getenv("AVC_LSTM_SAMPLE") ? atoi(getenv("AVC_LSTM_SAMPLE")) : 1;
-    p.sample = sample;
-    const bool sg = sg_bwd();
-    AVC_CHECK_ARG(!sg || (dgates_bf16 && (long long)B * T * 8 * H < (1ll << 31)),
-                  "avc_lstm_bwd: the sentinel form needs the bf16 dG twin and B*T*4H*2 < 2^31 bytes");
-    const bool gr = gran(true, H) && !sg;
+    const bool gr = gran(true, H);
     (void)hipMemsetAsync(gbuf, 0, gr ? px_payload_off(ng) + (size_t)32 * B * H : px_ctl_bytes(ng), s);
-    // the twin starts as the sentinel everywhere (re-initialised every call)
-    if (sg) (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dgates_bf16), (int)DG_SENT, (size_t)B * T * 2 * H, s);
     // (persistent_path above set the dynamic-LDS attributes)
     const dim3 grid(ng * (H / PJU));
     if (H == 1024) launch_persist_bwd<1024>(grid, s, gr, p);

@@ -391,12 +391,6 @@ def lstm_bwd_scratch(B, H, dirs, device):
     return torch.empty((nbytes + 1) // 2, device=device, dtype=torch.bfloat16)
 
 
-def lstm_set_bwd_form(form: int) -> None:
-    """Debug / A-B: persistent backward form (0 dG gather + flags, 2 sentinel hand-off, 3 sentinel +
-    XCD-verified L2-resident stores, -1 default)."""
-    L.call("avc_lstm_set_bwd_form", int(form))
-
-
 def lstm_bwd_timeout_flag(gbuf, B, H):
     return int(gbuf.view(torch.int32)[0].item())
 

@@ -207,15 +207,9 @@ int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, int B, int T,
  * register-resident; each workgroup gathers the group's bf16 dG_{t+1}, handed over as
  * write-through payload + per-workgroup flags, bounded spins; timeout flag = u32 at byte 0 of
  * gbuf).  The small-H and persistent launches can also write a bf16 copy of dgates (dgates_bf16,
- * else null; the sentinel forms 2/3 need it: it is their payload); the per-step path needs null. */
+ * else null); the per-step path needs null. */
 /* Bytes of the backward scratch gbuf for (B, H, dirs). */
 size_t avc_lstm_bwd_scratch_bytes(int B, int H, int dirs);
-
-/* Debug / A-B: form of the persistent backward recurrence.  0 = dG gather with per-workgroup flags
- * (the default), 2 = sentinel hand-off (the bf16 dG twin is filled with a signalling-NaN pattern
- * and is itself the payload; no flags), 3 = form 2 with plain (L2-resident) payload stores where a
- * group's workgroups verify one shared XCD, -1 = back to the default (AVC_LSTM_BWD_FORM). */
-int avc_lstm_set_bwd_form(int form);
 
 int avc_lstm_bwd(const float* dh_out, const float* h, const float* c, const float* gates,
                  const void* w_hh, const void* w_hh_t, int wdtype, int B, int T, int H, int dirs,

@@ -479,31 +479,22 @@ def test_gemm_nt_conv_window_and_bn_stats(B, T, Cin, Cout, Kw, pad):
     assert rinf(1.0 / rstd.double() ** 2 - 1e-5, refv) < 1e-3
 
 
-@pytest.mark.parametrize("form", [0, 2, 3])
 @pytest.mark.parametrize("B,H", [(64, 1024), (20, 1024), (64, 512), (3, 512), (64, 768), (2, 768)])
-def test_lstm_persistent_backward(B, H, form):
+def test_lstm_persistent_backward(B, H):
     """The one-launch backward recurrence (bf16 products, fp32 cell math) against an fp32
     CPU loop that rounds dG_{t+1} to bf16 for the recurrent product, as the kernel does;
-    its bf16 dG twin equals the fp32 output rounded; the spin-timeout flag stays clear.
-    Every hand-off form: dG gather with flags (0, default) and the sentinel hand-off (2; 3 = with
-    the XCD-verified L2-resident stores)."""
+    its bf16 dG twin equals the fp32 output rounded; the spin-timeout flag stays clear."""
     import autoformer_amd as A
-    from autoformer_amd import kernels as Kr
 
     A.set_compute("bf16")
-    Kr.lstm_set_bwd_form(form)
-    try:
-        _persistent_backward_case(B, H)
-    finally:
-        Kr.lstm_set_bwd_form(-1)
+    _persistent_backward_case(B, H)
 
 
-@pytest.mark.parametrize("form", [2, 3])
-def test_lstm_persistent_backward_under_load(form):
-    """The sentinel hand-off under uneven load: the same backward run alone and beside a stream
-    of large GEMMs on another stream (so members start and run at different times, and the
-    payload lines compete with streaming traffic) is bit-identical -- the recurrence's arithmetic
-    order is fixed, so any stale or torn payload read would show as a difference."""
+def test_lstm_persistent_backward_under_load():
+    """The hand-off under uneven load: the same backward run alone and beside a stream of large
+    GEMMs on another stream (so members start and run at different times, and the payload lines
+    compete with streaming traffic) is bit-identical -- the recurrence's arithmetic order is
+    fixed, so any stale or torn payload read would show as a difference."""
     import autoformer_amd as A
     from autoformer_amd import kernels as Kr
 
@@ -518,28 +509,24 @@ def test_lstm_persistent_backward_under_load(form):
     gates = gates.to(DEV)
     wt = ((torch.randn(G, H) * (1.0 / H ** 0.5)).bfloat16().t().contiguous()).to(DEV)
     gbuf = Kr.lstm_bwd_scratch(B, H, 1, DEV)
-    Kr.lstm_set_bwd_form(form)
-    try:
-        quiet = Kr.lstm_bwd(dh, dh, c, gates, None, wt, B, T, H, 1, gbuf=gbuf)
+    quiet = Kr.lstm_bwd(dh, dh, c, gates, None, wt, B, T, H, 1, gbuf=gbuf)
+    torch.cuda.synchronize()
+    assert Kr.lstm_bwd_timeout_flag(gbuf, B, H) == 0
+    side = torch.cuda.Stream()
+    x = torch.randn(4096, 4096, device=DEV, dtype=torch.bfloat16)
+    for lead in (0, 1, 3):
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(lead):
+                x = (x @ x).clamp_(-1, 1)
+        loaded = Kr.lstm_bwd(dh, dh, c, gates, None, wt, B, T, H, 1, gbuf=gbuf)
+        with torch.cuda.stream(side):
+            for _ in range(4):
+                x = (x @ x).clamp_(-1, 1)
         torch.cuda.synchronize()
         assert Kr.lstm_bwd_timeout_flag(gbuf, B, H) == 0
-        side = torch.cuda.Stream()
-        x = torch.randn(4096, 4096, device=DEV, dtype=torch.bfloat16)
-        for lead in (0, 1, 3):
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                for _ in range(lead):
-                    x = (x @ x).clamp_(-1, 1)
-            loaded = Kr.lstm_bwd(dh, dh, c, gates, None, wt, B, T, H, 1, gbuf=gbuf)
-            with torch.cuda.stream(side):
-                for _ in range(4):
-                    x = (x @ x).clamp_(-1, 1)
-            torch.cuda.synchronize()
-            assert Kr.lstm_bwd_timeout_flag(gbuf, B, H) == 0
-            assert torch.equal(loaded, quiet), (lead, (loaded - quiet).abs().max().item())
-            assert torch.equal(loaded._bf16, quiet._bf16), lead
-    finally:
-        Kr.lstm_set_bwd_form(-1)
+        assert torch.equal(loaded, quiet), (lead, (loaded - quiet).abs().max().item())
+        assert torch.equal(loaded._bf16, quiet._bf16), lead
 
 
 def _persistent_backward_case(B, H):
@@ -608,11 +595,13 @@ def test_gemm_tt_lds_transposed_reads(M, N, K, split):
 
 
 @pytest.mark.parametrize("B,T,Cin,Cout,Kw,pad", [(4, 37, 64, 96, 5, 2), (64, 128, 512, 512, 5, 2), (3, 20, 88, 176, 3, 1),
-                                                 (3, 64, 96, 80, 5, 2), (2, 192, 32, 200, 5, 2)])
+                                                 (3, 64, 96, 80, 5, 2), (2, 192, 32, 200, 5, 2),
+                                                 (64, 176, 512, 512, 5, 2), (3, 100, 32, 80, 5, 2)])
 @pytest.mark.parametrize("split", ["auto", 1])
 def test_gemm_tt_conv_weight_gradient_window(B, T, Cin, Cout, Kw, pad, split):
-    """Conv dW through the TT kernel.  5-tap 'same' convs with T % 64 == 0 and Cin % 32 == 0 take
-    the halo form (one x tile for all taps; utterance edges zero-filled at load), the others the
+    """Conv dW through the TT kernel.  5-tap 'same' convs with Cin % 32 == 0 take the halo form
+    (one x tile for all taps; utterance edges zero-filled at load; K-tiles on the utterance grid,
+    the last one of an utterance partial when T % 64 != 0: T = 37, 100, 176), the others the
     window stream; split-K (atomics) and single-pass (plain stores) epilogues."""
     import autoformer_amd as A
     from autoformer_amd import kernels as Kr
