@@ -16,8 +16,8 @@ import torch  # noqa: F401  (must precede the HIP library)
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "graph.hip"]
-ABI_VERSION = 13
+SOURCES = ["gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "graph.hip", "fold.hip"]
+ABI_VERSION = 14
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -34,7 +34,8 @@ class GemmDesc(ctypes.Structure):
     _fields_ = [("M", c_int), ("N", c_int), ("K", c_int), ("batch", c_int), ("a", Operand), ("b", Operand),
                 ("c", c_void_p), ("ldc", c_ll), ("c_batch_stride", c_ll), ("bias", c_void_p),
                 ("accumulate", c_int), ("split_k", c_int), ("bn_partial", c_void_p), ("compute", c_int),
-                ("c_bf16", c_void_p), ("residual", c_void_p), ("cperm", c_int)]
+                ("c_bf16", c_void_p), ("residual", c_void_p), ("cperm", c_int), ("row_bias", c_void_p),
+                ("rb_t", c_int), ("rb_pad", c_int)]
 
 
 class BnFin(ctypes.Structure):
@@ -104,6 +105,12 @@ _SIGS = {
     "avc_dec_concat_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_conv_pack": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_conv_grad_unpack": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "avc_conv_pack_slice": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                    c_void_p]),
+    "avc_conv_edge_table": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "avc_conv_edge_colsum": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "avc_conv_grad_unpack_slice": (c_int, [c_void_p, c_ll, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                                           c_void_p]),
     "avc_convert": (c_int, [c_void_p, c_void_p, c_int, c_ll, c_void_p]),
     "avc_transpose": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_ll, c_void_p]),
     "avc_add": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_void_p]),

@@ -295,6 +295,7 @@ __global__ void __launch_bounds__(NT) gemm_generic_kernel(GemmArgs g) {
       for (int i = 0; i < 4; ++i) acc[i][j] += bv;
     }
   }
+  if (g.rbias && ks == 0) add_row_bias<4>(g, acc, rbase, cbase);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -747,6 +748,13 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
   AVC_CHECK_ARG(!g.cperm || (d->N % g.cperm == 0 && !g.bias && !g.res && !g.c16 && !g.bn_partial),
                 "avc_gemm: cperm needs N %% taps == 0 and no bias / residual / bf16 / BN epilogue");
   g.cpd = make_fastdiv(g.cperm ? (uint32_t)(d->N / g.cperm) : 1u);
+  g.rbias = d->row_bias;
+  g.rb_t = d->rb_t;
+  g.rb_pad = d->rb_pad;
+  g.rb_div = make_fastdiv(d->row_bias && d->rb_t > 0 ? (uint32_t)d->rb_t : 1u);
+  AVC_CHECK_ARG(!g.rbias || (d->rb_t > 2 * d->rb_pad && d->rb_pad >= 0 && d->M % d->rb_t == 0 && !g.cperm &&
+                             g.batch == 1 && !d->a.kstrided && !d->b.kstrided),
+                "avc_gemm: row_bias needs rb_t > 2 rb_pad, M %% rb_t == 0, batch 1, no cperm, non-K-strided operands");
   g.bn_cnt = nullptr;
   g.bnb_ws = nullptr;
   g.bnb_cnt = nullptr;

@@ -31,6 +31,9 @@ struct GemmArgs {
   float* bn_partial;
   int cperm;     // 0, or taps: column n = tap*chans + ch is stored at ch*taps + tap (conv weight layout)
   FastDiv cpd;   // divide a column by chans = N / cperm
+  const float* rbias;  // per-(utterance, edge class) row bias (avc_gemm_desc.row_bias), nullable
+  int rb_t, rb_pad;
+  FastDiv rb_div;      // divide a row by rb_t
   // BatchNorm finalize by the last row tile of each column tile (bn_cnt != null, bn_partial set):
   // mean / rstd / scale / shift and the running statistics of the tile's columns (avc_gemm_bn)
   unsigned* bn_cnt;
@@ -100,6 +103,27 @@ __device__ __forceinline__ long long out_col(const GemmArgs& g, int col) {
 }
 
 
+// Row bias of the conv0 fold (avc_gemm_desc.row_bias): rows rbase + 16 i + e, columns cbase + 16 j.
+template <int NJ>
+__device__ __forceinline__ void add_row_bias(const GemmArgs& g, f32x4 (&acc)[4][NJ], int rbase, int cbase) {
+  const int T = g.rb_t, pad = g.rb_pad, ncls = 2 * pad + 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = rbase + i * 16 + e;
+      if (row >= g.M) continue;
+      const int b = (int)fdiv((uint32_t)row, g.rb_div), t = row - b * T;
+      const int cls = t < pad ? t : (t >= T - pad ? 2 * pad - (T - 1 - t) : pad);
+      const float* rp = g.rbias + (long long)(b * ncls + cls) * g.N;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int col = cbase + j * 16;
+        if (col < g.N) acc[i][j][e] += rp[col];
+      }
+    }
+}
+
 // Accumulator layout shared by the fast kernels: 4 waves as 2 (M) x 2 (N); wave (wm, wn) owns
 // rows wm*64 + i*16 + 4*(lane>>4) + e and columns wn*BN_/2 + j*16 + (lane&15) of the tile.
 // Fused epilogue: bias, residual, accumulate / atomics (split-K, batch-sum), bf16 copy, and
@@ -127,6 +151,7 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
       for (int i = 0; i < 4; ++i) acc[i][j] += bv;
     }
   }
+  if (g.rbias && ks == 0) add_row_bias<NJ>(g, acc, rbase, cbase);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll

@@ -82,14 +82,15 @@ def operand(t: torch.Tensor, ld: int, kstrided: bool = False, window=None, batch
 
 def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=None, accumulate=False, split_k=1,
          bn_partial=None, batch=1, c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0, bn_fin=None,
-         bnb=None):
+         bnb=None, row_bias=None):
     """cperm = taps > 1: C's columns are (tap, channel) pairs written in nn.Conv1d's [Co][Ci][K]
     weight layout (a conv weight gradient straight into .grad).
     bn_fin = (gamma, beta, running_mean, running_var, nbt, momentum, eps, nupd): the BatchNorm
     finalize of bn_partial fused into the GEMM (avc_gemm_bn); returns (mean, rstd, scale, shift).
     bnb = (y, mean, rstd, gamma, beta, act, coef, dgamma, dbeta, dbias, accumulate): C is dL/da of
     the conv + BN + act layer whose conv output is y; the GEMM also computes that layer's BN
-    backward statistics (avc_gemm_bnb: coef[6][N] and the parameter gradients)."""
+    backward statistics (avc_gemm_bnb: coef[6][N] and the parameter gradients).
+    row_bias = (S, T, pad): S[(b*(2 pad + 1) + edge class)][N] added to row b*T + t (the conv0 fold)."""
     _dev(c, bias, bn_partial, c_bf16, residual)
     if c.dtype == torch.bfloat16:  # bf16-only output
         assert c_bf16 is None and not accumulate and split_k == 1 and not cperm
@@ -110,6 +111,10 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     d.c_bf16 = _ptr(c_bf16)
     d.residual = _ptr(residual)
     d.cperm = int(cperm)
+    if row_bias is not None:
+        rb, rb_t, rb_pad = row_bias
+        _dev(rb)
+        d.row_bias, d.rb_t, d.rb_pad = rb.data_ptr(), int(rb_t), int(rb_pad)
     if bnb is not None:
         y, mean, rstd, gamma, beta, act, coef, dgamma, dbeta, dbias, acc = bnb
         _dev(y, mean, rstd, coef)
@@ -479,6 +484,40 @@ def conv_pack(w, mode, dtype):
     out = torch.empty(Co * Ci * K, device=w.device, dtype=tdt)
     L.call("avc_conv_pack", w.data_ptr(), out.data_ptr(), dtype, Co, Ci, K, int(mode), stream())
     return out.view(Co, K * Ci) if mode == 0 else out.view(Ci, K * Co)
+
+
+def conv_pack_slice(w, ci0, cn, cpad, mode, dtype):
+    """Pack input channels [ci0, ci0+cn) of conv weight w (Co, Ci, K), channel axis zero-padded to
+    cpad: mode 0 -> (Co, K*cpad), 1 -> (cpad, K*Co) (flipped taps), 2 -> (K*Co, cpad)."""
+    Co, Ci, Kw = w.shape
+    tdt = torch.bfloat16 if dtype == BF16 else torch.float32
+    out = torch.empty(Co * cpad * Kw, device=w.device, dtype=tdt)
+    L.call("avc_conv_pack_slice", w.data_ptr(), out.data_ptr(), dtype, Co, Ci, Kw, ci0, cn, cpad, mode, stream())
+    return out.view(*((Co, Kw * cpad) if mode == 0 else (cpad, Kw * Co) if mode == 1 else (Kw * Co, cpad)))
+
+
+def conv_edge_table(E, B, Co, Kw, T, pad):
+    """S[b][cls][co]: the sum of E[b][k][co] over the taps valid at each edge class (fold.hip)."""
+    _dev(E)
+    S = torch.empty(B * (2 * pad + 1), Co, device=E.device)
+    L.call("avc_conv_edge_table", E.data_ptr(), B, Co, Kw, T, pad, S.data_ptr(), stream())
+    return S
+
+
+def conv_edge_colsum(dy, B, T, C, Kw, pad):
+    """(B*Kw, C): per utterance and tap, the column sums of dy over the frames the tap reads."""
+    _dev(dy)
+    out = torch.empty(B * Kw, C, device=dy.device)
+    L.call("avc_conv_edge_colsum", dy.data_ptr(), _dt(dy), B, T, C, Kw, pad, out.data_ptr(), stream())
+    return out
+
+
+def conv_grad_unpack_slice(dwf, ld, kstride, dw, ci0, cn, accumulate=True):
+    """dw[co][ci0+ci][k] (+)= dwf[co*ld + k*kstride + ci], ci < cn."""
+    Co, Ci, Kw = dw.shape
+    L.call("avc_conv_grad_unpack_slice", dwf.data_ptr(), int(ld), int(kstride), dw.data_ptr(), Co, Ci, Kw, ci0, cn,
+           int(accumulate), stream())
+    return dw
 
 
 def conv_grad_unpack(dwf, Co, Ci, K, into=None):

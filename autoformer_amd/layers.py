@@ -352,42 +352,42 @@ class ConvBNCore:
         projection); its gradient then arrives in bf16 too.  In bf16 mode the conv output y
         (kept for the BN backward) is stored in bf16; the BN statistics come from the fp32
         accumulators in the GEMM epilogue."""
-        conv, bn = self.conv, self.bn
-        Co, Ci, Kw = conv.weight.shape
+        Co, Ci, Kw = self.conv.weight.shape
         T_out = T_in + 2 * self.pad - Kw + 1
-        M = B * T_out
         Wf, _ = self.packs()
         x = K.twin(x)
-        bf = K.compute() == K.BF16
-        y = torch.empty(M, Co, device=x.device, dtype=torch.bfloat16 if bf else torch.float32)
         xop, wop = operand(x, Ci, window=(Kw, self.pad, T_out, T_in, Ci)), operand(Wf, Kw * Ci)
+        return self.conv_bn_act(xop, wop, Kw * Ci, B * T_out, T_out, x.device, residual, out_bf16)
+
+    def conv_bn_act(self, xop, wop, Kdim, M, T_out, dev, residual=None, out_bf16=False, row_bias=None):
+        """The conv GEMM (operands given) + BatchNorm (statistics from the epilogue) + activation."""
+        conv, bn = self.conv, self.bn
+        Co = conv.weight.shape[0]
+        bf = K.compute() == K.BF16
+        y = torch.empty(M, Co, device=dev, dtype=torch.bfloat16 if bf else torch.float32)
         if bn.training:
             # batch statistics from the epilogue, finalized by the GEMM's last row tiles; the
             # running statistics take stat_updates updates (the *_Adjust double pass)
-            partial = K.bn_partial_buffer(M, Co, x.device)
+            partial = K.bn_partial_buffer(M, Co, dev)
             nbt = bn.num_batches_tracked if bn.track_running_stats else None
             mom = bn.momentum if bn.momentum is not None else 0.1
-            stats = K.gemm(M, Co, Kw * Ci, xop, wop, y, bias=conv.bias, bn_partial=partial,
+            stats = K.gemm(M, Co, Kdim, xop, wop, y, bias=conv.bias, bn_partial=partial,
                            bn_fin=(bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, mom, bn.eps,
-                                   self.stat_updates))
+                                   self.stat_updates), row_bias=row_bias)
         else:
-            K.gemm(M, Co, Kw * Ci, xop, wop, y, bias=conv.bias)
+            K.gemm(M, Co, Kdim, xop, wop, y, bias=conv.bias, row_bias=row_bias)
             stats = K.bn_eval(bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.eps)
         mean, rstd, scale, shift = stats
         a = K.bn_apply(y, scale, shift, self.act, residual, out_bf16=out_bf16 and bf and residual is None)
         return a, (y, mean, rstd, T_out)
 
-    def backward(self, dA, x, a, saved, B, T_in, n_dx, self_link=None, prev_link=None):
-        """self_link: this layer's BnbLink (its BN backward statistics may already have been
-        computed by the consumer's data-gradient GEMM); prev_link: the link of the conv + BN
-        layer that produced x, whose statistics this layer's data-gradient GEMM computes."""
-        y, mean, rstd, T_out = saved
+    def bn_grad(self, dA, saved, self_link=None):
+        """BatchNorm + activation backward: dy (bf16 in bf16 mode) and, outside sink mode, the
+        (dgamma, dbeta, conv-bias) gradients (sink mode: accumulated into .grad)."""
+        y, mean, rstd, _ = saved
         if not self.bn.training:
             raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
         conv, bn = self.conv, self.bn
-        Co, Ci, Kw = conv.weight.shape
-        M = B * T_out
-        sink = _SINK["on"]
         dy_bf16 = K.compute() == K.BF16
         if self_link is not None and self_link.coef is not None:
             # statistics (and the parameter gradients) came from the consumer's GEMM epilogue
@@ -397,12 +397,38 @@ class ConvBNCore:
             dy = K.bn_bwd_apply(dA, y, self_link.coef, self.act, dy_bf16=dy_bf16)
             dgamma, dbeta, dbias = self_link.grads
             self_link.coef = None
-        else:
-            into = (_grad_of(bn.weight), _grad_of(bn.bias), _grad_of(conv.bias)) if sink else None
-            # act' from the recomputed pre-activation: the activation output `a` is not re-read
-            # bf16 mode: dy feeds the two bf16 GEMMs below only -> stored in bf16 alone
-            dy, dgamma, dbeta, dbias = K.bn_bwd(dA, None, y, mean, rstd, bn.weight, self.act, into=into,
-                                                beta=bn.bias, dy_bf16=dy_bf16)
+            return dy, dgamma, dbeta, dbias
+        into = (_grad_of(bn.weight), _grad_of(bn.bias), _grad_of(conv.bias)) if _SINK["on"] else None
+        # act' from the recomputed pre-activation: the activation output `a` is not re-read
+        # bf16 mode: dy feeds the two bf16 GEMMs below only -> stored in bf16 alone
+        dy, dgamma, dbeta, dbias = K.bn_bwd(dA, None, y, mean, rstd, bn.weight, self.act, into=into,
+                                            beta=bn.bias, dy_bf16=dy_bf16)
+        return dy, dgamma, dbeta, dbias
+
+    def fold_packs(self, nm, cp):
+        """Packs of the conv0 fold (fold.hip): the first nm input channels as Wf [Co][K*cp] and
+        Wd [nm][K*Co], the rest (the broadcast speaker embedding) as We [K*Co][Ci - nm]."""
+        w = self.conv.weight
+        if not hasattr(self, "fold_cache"):
+            self.fold_cache = PackCache()
+
+        def build():
+            dt = K.compute()
+            Ci = w.shape[1]
+            return (K.conv_pack_slice(w, 0, nm, cp, 0, dt), K.conv_pack_slice(w, 0, nm, nm, 1, dt),
+                    K.conv_pack_slice(w, nm, Ci - nm, Ci - nm, 2, dt))
+        return self.fold_cache.get([w], build)
+
+    def backward(self, dA, x, a, saved, B, T_in, n_dx, self_link=None, prev_link=None):
+        """self_link: this layer's BnbLink (its BN backward statistics may already have been
+        computed by the consumer's data-gradient GEMM); prev_link: the link of the conv + BN
+        layer that produced x, whose statistics this layer's data-gradient GEMM computes."""
+        T_out = saved[3]
+        conv = self.conv
+        Co, Ci, Kw = conv.weight.shape
+        M = B * T_out
+        sink = _SINK["on"]
+        dy, dgamma, dbeta, dbias = self.bn_grad(dA, saved, self_link)
 
         def wgrad():
             return conv_wgrad(dy, x, B, T_in, T_out, conv.weight, self.pad,
@@ -543,8 +569,93 @@ class _EncConv0Fn(torch.autograd.Function):
         return dx, demb, None, None, None, None, dW, db, dg, dbe
 
 
+class _EncConv0FoldFn(torch.autograd.Function):
+    """The same layer with the speaker half folded out of the frames (fold.hip,
+    AutoVC.py:46-51): conv0 runs on the mel channels (zero-padded to a multiple of 32) and the
+    broadcast embedding's contribution E = c_org . We (B x K*Co) enters as a per-(utterance,
+    edge class) row bias of the GEMM epilogue, before the BatchNorm statistics.  Backward: dy's
+    per-utterance column sums over each tap's valid frames (Sdy) give the embedding half of
+    dW (a K = B product per tap) and, for a trained embedding, dc_org = Sdy . We; the mel half
+    of dW and dL/dmel are the usual halo-conv products over the padded mel channels."""
+
+    @staticmethod
+    def forward(ctx, mel2d, emb, core, B, T, out_bf16, w, b, gamma, beta):
+        Co, Ci, Kw = core.conv.weight.shape
+        nm, pad = mel2d.shape[1], core.pad
+        de, cp = Ci - nm, -(-nm // 32) * 32
+        Wmf, _, We = core.fold_packs(nm, cp)
+        dev = mel2d.device
+        xm = K.pad_cols(mel2d, cp, dtype=K.compute())
+        # a fresh compute-dtype copy, never attached to emb: the caller may refill emb in place
+        # (a captured step fed through the same input tensors), and a cached twin would go stale
+        e = K.convert(emb, K.BF16) if K.compute() == K.BF16 else emb
+        E = torch.empty(B, Kw * Co, device=dev)
+        K.gemm(B, Kw * Co, de, operand(e, de), operand(We, de), E)
+        S = K.conv_edge_table(E, B, Co, Kw, T, pad)
+        a, saved = core.conv_bn_act(operand(xm, cp, window=(Kw, pad, T, T, cp)), operand(Wmf, Kw * cp), Kw * cp,
+                                    B * T, T, dev, None, out_bf16, row_bias=(S, T, pad))
+        ctx.core, ctx.B, ctx.T, ctx.saved, ctx.dims = core, B, T, saved, (nm, de, cp)
+        ctx.save_for_backward(xm, emb, a)
+        _links(ctx, xm, core, a, saved, False)
+        return a
+
+    @staticmethod
+    def backward(ctx, dA):
+        xm, emb, a = ctx.saved_tensors
+        core, B, T = ctx.core, ctx.B, ctx.T
+        nm, de, cp = ctx.dims
+        conv = core.conv
+        Co, Ci, Kw = conv.weight.shape
+        pad, M = core.pad, B * T
+        sink = _SINK["on"]
+        dy, dgamma, dbeta, dbias = core.bn_grad(dA.contiguous(), ctx.saved, ctx.self_link)
+        _, Wmd, We = core.fold_packs(nm, cp)
+        Sdy = K.conv_edge_colsum(dy, B, T, Co, Kw, pad)  # (B*Kw, Co): dy summed over each tap's valid frames
+        ev = mark()
+        dmel = demb = None
+        if ctx.needs_input_grad[0]:  # the encoder re-pass: dL/d(mel_postnet)
+            dmel = torch.empty(M, nm, device=dy.device)
+            K.gemm(M, nm, Kw * Co, operand(dy, Co, window=(Kw, Kw - 1 - pad, T, T, Co)), operand(Wmd, Kw * Co), dmel)
+        if ctx.needs_input_grad[1]:  # a trained embedding (the *_Adjust variants)
+            demb = torch.empty(B, de, device=dy.device)
+            K.gemm(B, de, Kw * Co, operand(Sdy, Kw * Co), operand(We, de, kstrided=True), demb)
+
+        def wgrad():
+            gw = _grad_of(conv.weight) if sink else torch.zeros_like(conv.weight)
+            dWm = torch.empty(Co, Kw * cp, device=dy.device)
+            K.gemm(Co, Kw * cp, M, operand(dy, Co, kstrided=True),
+                   operand(xm, cp, kstrided=True, window=(Kw, pad, T, T, cp)), dWm,
+                   split_k=K.auto_split_k(Co, Kw * cp, M))
+            K.conv_grad_unpack_slice(dWm, Kw * cp, cp, gw, 0, nm)
+            # embedding half, one K = B product per tap: dWe[co][k][ci] = sum_b Sdy[b][k][co] emb[b][ci]
+            dWe = torch.empty(Co, Kw * de, device=dy.device)
+            K.gemm(Co, de, B, operand(Sdy, Kw * Co, kstrided=True, batch_stride=Co),
+                   operand(emb, de, kstrided=True), dWe, ldc=Kw * de, batch=Kw, c_batch_stride=de)
+            K.conv_grad_unpack_slice(dWe, Kw * de, de, gw, nm, de)
+            return gw
+        if sink and (dmel is not None or demb is not None or not _LAST_WGRAD_MAIN):
+            with _Side(ev) as sd:
+                sd.keep(dy, xm, Sdy, emb)
+                if not _ABLATE_WGRAD:
+                    wgrad()
+            dW = dgamma = dbeta = dbias = None
+        elif sink:
+            wgrad()  # the last layer of the backward: on the main stream (see ConvBNCore.backward)
+            dW = dgamma = dbeta = dbias = None
+        else:
+            dW = wgrad()
+        return dmel, demb, None, None, None, None, dW, dbias, dgamma, dbeta
+
+
+# the speaker-half fold of the encoder's first conv (AVC_CONV0_FOLD=0: the concat form, A/B)
+_FOLD = os.environ.get("AVC_CONV0_FOLD", "1") == "1"
+
+
 def enc_conv0(core, mel2d, emb, B, T, out_bf16=False):
     c, bn = core.conv, core.bn
+    Kw = c.weight.shape[2]
+    if _FOLD and Kw == 2 * core.pad + 1 and T > 2 * core.pad and c.weight.shape[1] > mel2d.shape[1]:
+        return _EncConv0FoldFn.apply(mel2d, emb, core, B, T, out_bf16, c.weight, c.bias, bn.weight, bn.bias)
     return _EncConv0Fn.apply(mel2d, emb, core, B, T, out_bf16, c.weight, c.bias, bn.weight, bn.bias)
 
 

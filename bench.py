@@ -159,24 +159,32 @@ def pmc_mfma(kernel):
     return None
 
 
-def cpu_baseline(B, T, freq, steps=3):
+def cpu_baseline(B, T, freq, steps=5):
     """The CPU oracle (oracle/autovc_cpu.py, the pinned restatement of the reference) timed on
-    this box's host cores: same step, fp32, bounded sample of 1 warm-up + `steps` steps
-    (SURVEY.md §8(d)).  `cores` = the intra-op threads torch ran the oracle with."""
+    this box's host cores: same step, fp32, bounded sample of 1 warm-up + `steps` steps, the
+    MEDIAN step reported.  `cores` = the intra-op threads torch ran the oracle
+    with: the CPU share the GPU pool grants one GPU's process (OMP_NUM_THREADS, 16 on the box),
+    not the host's physical core count (128) -- that many threads would run on CPUs other jobs of
+    the host own."""
     from oracle import autovc_cpu as O
 
     x, e = synthetic_batch(B, T, 0, "cpu")
     s = O.OracleSolver(freq=freq)
     s.step(x, e)
-    t0 = time.perf_counter()
+    times = []
     for _ in range(steps):
+        t0 = time.perf_counter()
         s.step(x, e)
-    dt = (time.perf_counter() - t0) / steps
+        times.append(time.perf_counter() - t0)
+    dt = sorted(times)[len(times) // 2]
     phys, aff = host_cores()
     return {"value": round(B * T / dt, 1), "unit": "mel-frames/s", "cores": torch.get_num_threads(),
             "kind": "port", "host_physical_cores": phys, "host_cpus_allowed": aff,
-            "sample": f"oracle train step B={B} T={T} freq={freq} fp32, 1 warm-up + {steps} timed "
-                      f"steps ({dt * 1e3:.0f} ms/step), {torch.get_num_threads()} intra-op threads"}
+            "cores_note": "intra-op threads = the per-GPU CPU share of the pool (OMP_NUM_THREADS), not the host's "
+                          "physical cores",
+            "sample": f"oracle train step B={B} T={T} freq={freq} fp32, 1 warm-up + {steps} timed steps, median "
+                      f"{dt * 1e3:.0f} ms/step (min {min(times) * 1e3:.0f}, max {max(times) * 1e3:.0f}), "
+                      f"{torch.get_num_threads()} intra-op threads"}
 
 
 def launch_ranks(n):

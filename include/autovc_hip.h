@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 13
+#define AVC_ABI_VERSION 14
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -74,6 +74,12 @@ typedef struct {
   int cperm;             /* 0, or taps > 1: columns are (tap, channel) pairs, n = tap*(N/taps) + ch, and
                             land at C[m*ldc + ch*taps + tap] -- a Conv1d weight gradient written straight
                             into nn.Conv1d's [Co][Ci][K] layout (no bias / residual / bf16 / BN epilogue) */
+  const float* row_bias; /* nullable: per-(utterance, edge class) bias added with `bias` (before the BN
+                            statistics): row m = b*rb_t + t adds row_bias[(b*(2 rb_pad + 1) + cls)*N + n],
+                            cls = t (t < rb_pad), 2 rb_pad - (rb_t - 1 - t) (t >= rb_t - rb_pad), else
+                            rb_pad -- the speaker half of the encoder's first conv folded out of the
+                            frames (factory/AutoVC.py:46-51, fold.hip); non-K-strided operands only */
+  int rb_t, rb_pad;
 } avc_gemm_desc;
 
 int avc_abi_version(void);
@@ -280,6 +286,22 @@ int avc_expand_codes(const float* pc, const float* pe, float* out, int B, int T,
  * grad_unpack: dWf[co][k][ci] -> dW[co][ci][k] (accumulate optional). */
 int avc_conv_pack(const float* w, void* out, int dtype, int Cout, int Cin, int Kw, int mode, void* stream);
 int avc_conv_grad_unpack(const float* dwf, float* dw, int Cout, int Cin, int Kw, int accumulate, void* stream);
+
+/* The encoder conv0 fold (fold.hip; factory/AutoVC.py:46-51: cat(mel, c_org broadcast) -> ConvNorm(336,
+ * 512, 5)).  pack_slice packs the input channels [ci0, ci0 + cn) of W [Co][Ci][K] (fp32) into `out`
+ * (dtype), the channel axis zero-padded to cpad: mode 0 Wf[co][k][cpad] (forward), 1 Wd[cpad][K-1-k][co]
+ * (data gradient), 2 We[k][co][cpad] (the speaker term E = c . We^T).
+ * edge_table: S[b][cls][co] = sum over the taps k valid at edge class cls (see avc_gemm_desc.row_bias)
+ * of E[b][k*Co + co]; T > 2 pad.
+ * edge_colsum: out[b][k][c] = sum over the frames t of utterance b with 0 <= t + k - pad < T of
+ * dy[b*T + t][c] (dy fp32 or bf16, C % 4 == 0, K <= 16): the speaker half's weight / embedding gradients.
+ * grad_unpack_slice: dw[co][ci0 + ci][k] (+)= dwf[co*ld + k*kstride + ci] for ci < cn (dw has Ci channels). */
+int avc_conv_pack_slice(const float* w, void* out, int dtype, int Co, int Ci, int K, int ci0, int cn, int cpad,
+                        int mode, void* stream);
+int avc_conv_edge_table(const float* E, int B, int Co, int K, int T, int pad, float* S, void* stream);
+int avc_conv_edge_colsum(const void* dy, int dy_dtype, int B, int T, int C, int K, int pad, float* out, void* stream);
+int avc_conv_grad_unpack_slice(const float* dwf, long long ld, int kstride, float* dw, int Co, int Ci, int K, int ci0,
+                               int cn, int accumulate, void* stream);
 /* dst = convert(src) (n elements). */
 int avc_convert(const float* src, void* dst, int dtype, long long n, void* stream);
 /* dst[c * ld_dst + r] = convert(src[r][c]) for a row-major [R][C] fp32 matrix (ld_dst = 0:

@@ -105,6 +105,20 @@ def _act_grad_from_pre(pre, act, slope=0.2):
     raise ValueError(act)
 
 
+def edge_class(T, pad, device=None):
+    """Edge class of every frame t of an utterance (avc_gemm_desc.row_bias)."""
+    t = torch.arange(T, device=device)
+    return torch.where(t < pad, t, torch.where(t >= T - pad, 2 * pad - (T - 1 - t), torch.full_like(t, pad)))
+
+
+def row_bias_rows(S, M, T, pad):
+    """The (M, N) float64 matrix the row bias adds: row b*T + t takes S[b*(2 pad + 1) + class(t)]."""
+    ncls = 2 * pad + 1
+    rows = torch.arange(M, device=S.device)
+    idx = (rows // T) * ncls + edge_class(T, pad, S.device)[rows % T]
+    return S.double()[idx]
+
+
 # ----------------------------------------------------------------------------- LSTM fp64
 def lstm_fwd_ref(xproj, whh, B, T, H, dirs):
     """nn.LSTM forward of `dirs` directions from the input projections (B*T, dirs*4H) and W_hh
@@ -166,11 +180,11 @@ class Capture:
 
     # ---------------------------------------------------------------- wrappers
     def _gemm(self, M, N, Kd, a, b, c, ldc=None, bias=None, accumulate=False, split_k=1, bn_partial=None, batch=1,
-              c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0, bn_fin=None, bnb=None):
+              c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0, bn_fin=None, bnb=None, row_bias=None):
         f = self._orig["gemm"]
         kw = dict(ldc=ldc, bias=bias, accumulate=accumulate, split_k=split_k, bn_partial=bn_partial, batch=batch,
                   c_batch_stride=c_batch_stride, comp=comp, c_bf16=c_bf16, residual=residual, cperm=cperm,
-                  bn_fin=bn_fin, bnb=bnb)
+                  bn_fin=bn_fin, bnb=bnb, row_bias=row_bias)
         if bnb is not None and self.skip_bnb:
             return f(M, N, Kd, a, b, c, **kw)
         torch.cuda.synchronize()
@@ -190,13 +204,15 @@ class Capture:
             P = P + bias.double()[None, None, :N]
         if residual is not None:
             P = P + _c_view(residual, M, N, ldc_, batch, c_batch_stride, 0).double()
+        if row_bias is not None:
+            P = P + row_bias_rows(row_bias[0], M, row_bias[1], row_bias[2])[None]
         stats = f(M, N, Kd, a, b, c, **kw)
         torch.cuda.synchronize()
         got = _c_view(c, M, N, ldc_, batch, c_batch_stride, cperm).double()
         ref = P if before is None else before + P
         tag = (f"gemm M{M} N{N} K{Kd}" + (f" b{batch}" if batch > 1 else "") + (f" sk{split_k}" if split_k > 1 else "")
                + (" acc" if accumulate else "") + (" win" if a.taps or b.taps else "") + (" cperm" if cperm else "")
-               + (" bf16out" if only16 else ""))
+               + (" bf16out" if only16 else "") + (" rowbias" if row_bias is not None else ""))
         res = {"C": _rel(got, ref, before)}
         if c_bf16 is not None and not only16:
             res["C_bf16"] = _rel(_c_view(c_bf16, M, N, ldc_, batch, c_batch_stride, 0), ref, before)
@@ -310,9 +326,33 @@ class Capture:
         self.records.append(("expand_codes", f"expand_codes B{B} T{T} nc{nc}", {"out": _rel(out, ref.reshape(B * T, G))}))
         return out
 
+    def _conv_edge_table(self, E, B, Co, Kw, T, pad):
+        torch.cuda.synchronize()
+        S = self._orig["conv_edge_table"](E, B, Co, Kw, T, pad)
+        torch.cuda.synchronize()
+        Ev = E.double().view(B, Kw, Co)
+        ref = torch.zeros(B, 2 * pad + 1, Co, dtype=torch.float64, device=E.device)
+        for cls in range(2 * pad + 1):
+            t = cls if cls < pad else (pad if cls == pad else T - 1 - (2 * pad - cls))
+            for k in range(Kw):
+                if 0 <= t + k - pad < T:
+                    ref[:, cls] += Ev[:, k]
+        self.records.append(("conv_edge_table", f"conv_edge_table B{B} Co{Co}", {"S": _rel(S, ref.view_as(S))}))
+        return S
+
+    def _conv_edge_colsum(self, dy, B, T, C, Kw, pad):
+        torch.cuda.synchronize()
+        out = self._orig["conv_edge_colsum"](dy, B, T, C, Kw, pad)
+        torch.cuda.synchronize()
+        d = dy.double().view(B, T, C)
+        ref = torch.stack([d[:, max(0, pad - k):min(T, T + pad - k)].sum(1) for k in range(Kw)], 1)
+        self.records.append(("conv_edge_colsum", f"conv_edge_colsum B{B} T{T} C{C}", {"Sdy": _rel(out, ref.view_as(out))}))
+        return out
+
     # ---------------------------------------------------------------- context
     def __enter__(self):
-        for name in ("gemm", "lstm_fwd", "lstm2_fwd", "lstm_bwd", "bn_apply", "bn_bwd", "expand_codes"):
+        for name in ("gemm", "lstm_fwd", "lstm2_fwd", "lstm_bwd", "bn_apply", "bn_bwd", "expand_codes",
+                     "conv_edge_table", "conv_edge_colsum"):
             self._orig[name] = getattr(K, name)
             setattr(K, name, getattr(self, "_" + name))
         return self

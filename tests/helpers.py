@@ -12,9 +12,12 @@ def rel_inf(a, b):
 def grad_mismatches(model, g, tol=1e-2, head_tol=1e-2,
                     bn_fed_bias=lambda n: "conv.bias" in n and "postnet.convolutions.4" not in n):
     """Per-parameter check against the golden gradient norm (rel <= tol) and first-64-element
-    head (max abs error <= head_tol * max|head|).  Parameters whose true gradient is
-    analytically zero (conv biases feeding a training-mode BatchNorm; `bn_fed_bias`) get an
-    absolute floor only: their golden values are fp32 rounding noise."""
+    head (max abs error <= head_tol * max(max|head|, rms of the whole golden tensor)): a head
+    whose 64 elements happen to be far below the tensor's typical magnitude is held to the
+    tensor's scale, not to its own (fp32 reassociation moves every element by ~1e-7 x rms).
+    Parameters whose true gradient is analytically zero (conv biases feeding a training-mode
+    BatchNorm; `bn_fed_bias`) get an absolute floor only: their golden values are fp32
+    rounding noise."""
     bad = {}
     for name, p in model.named_parameters():
         ref_n = float(g["gnorm/" + name])
@@ -24,7 +27,8 @@ def grad_mismatches(model, g, tol=1e-2, head_tol=1e-2,
         if bn_fed_bias(name):
             ok = err < 1e-6 + head_tol * np.abs(head).max()
         else:
-            ok = abs(got.norm().item() - ref_n) <= tol * ref_n + 1e-6 and err <= head_tol * max(np.abs(head).max(), 1e-6)
+            scale = max(np.abs(head).max(), ref_n / np.sqrt(max(p.numel(), 1)), 1e-6)
+            ok = abs(got.norm().item() - ref_n) <= tol * ref_n + 1e-6 and err <= head_tol * scale
         if not ok:
             bad[name] = (got.norm().item(), ref_n, err)
     return bad

@@ -68,10 +68,11 @@ def _assert(cap, must):
 @pytest.mark.timeout(600)
 def test_c2_ops_vs_fp64():
     cap = _run("AutoVC", 16, 64, 128)
-    _assert(cap, ["gemm", "lstm_fwd", "lstm2_fwd", "lstm_bwd", "bn_apply", "bn_bwd", "expand_codes"])
+    _assert(cap, ["gemm", "lstm_fwd", "lstm2_fwd", "lstm_bwd", "bn_apply", "bn_bwd", "expand_codes",
+                  "conv_edge_table", "conv_edge_colsum"])
     tags = " | ".join(t for _, t, _ in cap.records)
     assert "lstm_bwd B64 T128 H1024" in tags and "lstm_bwd B64 T128 H512" in tags
-    assert " sk" in tags and " win" in tags and " acc" in tags
+    assert " sk" in tags and " win" in tags and " acc" in tags and " rowbias" in tags
 
 
 @pytest.mark.timeout(600)

@@ -906,3 +906,98 @@ def test_bn_apply_forms(ydt, M, C):
         assert relf(dy, ref) < 1e-5, relf(dy, ref)
         d16 = Kr.bn_bwd_apply(dA, y, coef, act, dy_bf16=True)
         assert d16.dtype == torch.bfloat16 and relf(d16, ref) < 4e-3
+
+
+# ------------------------------------------------------------------ encoder conv0 fold (fold.hip)
+@pytest.mark.parametrize("comp", ["fp32", "bf16"])
+def test_fold_kernels(comp):
+    """avc_conv_pack_slice (3 modes), avc_conv_edge_table, avc_conv_edge_colsum (fp32 / bf16 dy),
+    avc_conv_grad_unpack_slice and the GEMM row-bias epilogue against torch restatements."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+    from tests.capture_ref import row_bias_rows
+
+    A.set_compute(comp)
+    dt = Kr.compute()
+    tdt = torch.bfloat16 if comp == "bf16" else torch.float32
+    torch.manual_seed(3)
+    Co, Ci, Kw, nm, cp = 48, 40, 5, 10, 32
+    w = torch.randn(Co, Ci, Kw, device=DEV)
+    f = Kr.conv_pack_slice(w, 0, nm, cp, 0, dt)
+    ref = torch.zeros(Co, Kw, cp, device=DEV)
+    ref[:, :, :nm] = w[:, :nm].permute(0, 2, 1)
+    assert torch.equal(f.float(), ref.reshape(Co, Kw * cp).to(tdt).float())
+    d = Kr.conv_pack_slice(w, 0, nm, nm, 1, dt)
+    refd = w[:, :nm].flip(2).permute(1, 2, 0).reshape(nm, Kw * Co)
+    assert torch.equal(d.float(), refd.to(tdt).float())
+    e = Kr.conv_pack_slice(w, nm, Ci - nm, Ci - nm, 2, dt)
+    refe = w[:, nm:].permute(2, 0, 1).reshape(Kw * Co, Ci - nm)
+    assert torch.equal(e.float(), refe.to(tdt).float())
+    B, T, pad = 3, 13, 2
+    E = torch.randn(B, Kw * Co, device=DEV)
+    S = Kr.conv_edge_table(E, B, Co, Kw, T, pad)
+    Ev = E.view(B, Kw, Co)
+    for cls, t in enumerate([0, 1, 2, T - 2, T - 1]):
+        want = sum(Ev[:, k] for k in range(Kw) if 0 <= t + k - pad < T)
+        assert (S.view(B, 5, Co)[:, cls] - want).abs().max() < 1e-5
+    dy = torch.randn(B * T, Co, device=DEV).to(tdt)
+    Sdy = Kr.conv_edge_colsum(dy, B, T, Co, Kw, pad).view(B, Kw, Co)
+    dv = dy.float().view(B, T, Co)
+    for k in range(Kw):
+        assert (Sdy[:, k] - dv[:, max(0, pad - k):min(T, T + pad - k)].sum(1)).abs().max() < 1e-3
+    g = torch.randn(Co, Ci, Kw, device=DEV)
+    g0 = g.clone()
+    dwf = torch.randn(Co, Kw * 16, device=DEV)
+    Kr.conv_grad_unpack_slice(dwf, Kw * 16, 16, g, 12, 9)
+    want = g0.clone()
+    want[:, 12:21] += dwf.view(Co, Kw, 16)[:, :, :9].permute(0, 2, 1)
+    assert (g - want).abs().max() < 1e-6
+    # row bias on a 5-tap window GEMM (the conv kernel in bf16 mode: 32-multiple channels)
+    C2, N2 = 64, 96
+    x = torch.randn(B * T, C2, device=DEV).to(tdt)
+    W2 = (torch.randn(N2, Kw * C2, device=DEV) * 0.1).to(tdt)
+    S2 = torch.randn(B * 5, N2, device=DEV)
+    y = torch.empty(B * T, N2, device=DEV)
+    Kr.gemm(B * T, N2, Kw * C2, Kr.operand(x, C2, window=(Kw, pad, T, T, C2)), Kr.operand(W2, Kw * C2), y,
+            row_bias=(S2, T, pad))
+    xs = torch.nn.functional.pad(x.double().view(B, T, C2), (0, 0, pad, pad))
+    im = torch.cat([xs[:, k:k + T] for k in range(Kw)], 2).reshape(B * T, Kw * C2)
+    refy = im @ W2.double().t() + row_bias_rows(S2, B * T, T, pad)
+    assert relf(y, refy) < 1e-5, relf(y, refy)
+
+
+@pytest.mark.parametrize("comp", ["fp32", "bf16"])
+def test_enc_conv0_fold_matches_concat(comp):
+    """The folded encoder conv0 (layers._EncConv0FoldFn) against the concat form
+    (_EncConv0Fn) on the same weights and inputs: activation, BN running statistics, dL/dmel,
+    dL/demb and every parameter gradient (fp32: 1e-5; bf16: the bf16 bar of the layer)."""
+    import autoformer_amd as A
+    from autoformer_amd import layers as Lyr
+    from autoformer_amd.factory.Norm import ConvNorm
+
+    A.set_compute(comp)
+    torch.manual_seed(4)
+    B, T, nm, de, Co = 4, 32, 80, 256, 512
+    res = []
+    for fold in (True, False):
+        torch.manual_seed(4)
+        conv = ConvNorm(nm + de, Co, kernel_size=5, stride=1, padding=2, dilation=1, w_init_gain="relu").conv.to(DEV)
+        bn = torch.nn.BatchNorm1d(Co).to(DEV)
+        core = Lyr.ConvBNCore(conv, bn, Kr_act_relu())
+        mel = torch.randn(B * T, nm, device=DEV, requires_grad=True)
+        emb = torch.nn.functional.normalize(torch.randn(B, de, device=DEV), dim=1).requires_grad_(True)
+        fn = Lyr._EncConv0FoldFn if fold else Lyr._EncConv0Fn
+        a = fn.apply(mel, emb, core, B, T, False, conv.weight, conv.bias, bn.weight, bn.bias)
+        (a.float() * torch.linspace(-1, 1, Co, device=DEV)).sum().backward()
+        torch.cuda.synchronize()
+        res.append((a.float(), mel.grad, emb.grad, conv.weight.grad, bn.weight.grad, bn.bias.grad, bn.running_mean,
+                    bn.running_var))
+    bar = 1e-5 if comp == "fp32" else 2e-2
+    names = ("a", "dmel", "demb", "dW", "dgamma", "dbeta", "running_mean", "running_var")
+    for n, u, v in zip(names, res[0], res[1]):
+        assert relf(u, v.double()) < bar, (n, relf(u, v.double()))
+
+
+def Kr_act_relu():
+    from autoformer_amd import kernels as Kr
+    return Kr.ACT_RELU

@@ -32,7 +32,13 @@ def main():
     tb.step(xb, eb)
     tb.capture(xb, eb, warmup=0)
     print("split:", None if tb.graph_split is None else tb.graph_split.counts, flush=True)
+    from autoformer_amd import kernels as K
     for i, (x, e) in enumerate(batches):
+        pre = [n for n, p in mb.named_parameters() if not torch.isfinite(p).all()]
+        st = tb.opt.state.tolist()
+        mv = bool(torch.isfinite(tb.opt.m).all() and torch.isfinite(tb.opt.v).all())
+        print(f"before replay {i}: non-finite params {len(pre)}, adam state {st}, m/v finite {mv}, "
+              f"fault word {int(K.fault_word().item())}", flush=True)
         la = ta.step(x, e)
         xb.copy_(x)
         eb.copy_(e)
