@@ -127,13 +127,13 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
 // its hand-off stores, which must be st_sc1 stores: they are waited for (vmcnt(0)), one lane
 // increments the counter (agent-scope relaxed atomic), and the block that arrives last resets it
 // and returns true; it then reads the hand-off data with ld_sc1.
-__device__ __forceinline__ bool arrive_last(unsigned* cnt, unsigned arrivals) {
+__device__ __forceinline__ bool arrive_last(unsigned* cnt, unsigned arrivals, unsigned mine = 1) {
   __shared__ unsigned s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = old == arrivals - 1;
+    const unsigned old = __hip_atomic_fetch_add(cnt, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old + mine == arrivals;
     if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = last ? 1u : 0u;
   }

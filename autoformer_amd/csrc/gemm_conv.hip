@@ -41,20 +41,25 @@ __device__ __forceinline__ void wait_vm() {
 }
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
-// CBK channels per stage (LDS rows of 2*CBK bytes), CBN output columns per tile.
-template <int TAPS, int CBK, int CBN>
+// CBK channels per stage (LDS rows of 2*CBK bytes), CBN output columns per tile, NWM waves along
+// M (tile rows 64*NWM; NWM*2 waves per workgroup).  Every wave issues the same number of glds per
+// stage (the counted vmcnt waits assume it), so the halo and weight instruction counts are
+// rounded up to a multiple of the wave count; the extra rows load zeros.
+template <int TAPS, int CBK, int CBN, int NWM = 2>
 struct ConvCfg {
+  static constexpr int NW = 2 * NWM;              // waves per workgroup
+  static constexpr int TM = 64 * NWM;             // tile rows
   static constexpr int ROW = 2 * CBK;             // bytes per LDS row
   static constexpr int CPR = ROW / 16;            // 16-B chunks per row
   static constexpr int RPI = 1024 / ROW;          // rows per glds wave-instruction
-  static constexpr int AI = ((BM + TAPS - 1 + RPI - 1) / RPI + 3) / 4 * 4;  // halo instructions (x4 waves)
+  static constexpr int AI = ((TM + TAPS - 1 + RPI - 1) / RPI + NW - 1) / NW * NW;  // halo instructions
   static constexpr int A_BYTES = AI * 1024;
-  static constexpr int BI = TAPS * CBN / RPI;     // weight instructions
+  static constexpr int BROWS = TAPS * CBN;        // weight rows actually used
+  static constexpr int BI = ((BROWS + RPI - 1) / RPI + NW - 1) / NW * NW;           // weight instructions
   static constexpr int B_BYTES = BI * 1024;
   static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int LPT = AI / 4 + BI / 4;     // glds per thread per stage
+  static constexpr int LPT = AI / NW + BI / NW;   // glds per thread per stage
   static constexpr int NJ = CBN / 32;
-  static_assert(BI % 4 == 0, "weight rows must split over four waves");
   static_assert(CBN % 32 == 0 && (CBK == 32 || CBK == 64), "tile shape");
   // slot of chunk c in row r (XOR swizzle on the 16-B chunk index)
   __device__ static __forceinline__ int swz(int r) { return (r >> 1) & (CPR - 1); }
@@ -62,10 +67,11 @@ struct ConvCfg {
 
 // BNB: the BatchNorm-backward epilogue compiled in (only the instances launched with bnb: its
 // code in every conv instance cost 20 % of the conv time, measured)
-template <int TAPS, int NST, int CBK, int CBN, bool BNB>
-__global__ void __launch_bounds__(256, 2) gemm_conv_kernel(GemmArgs g) {
-  using C = ConvCfg<TAPS, CBK, CBN>;
-  constexpr int STAGE = C::STAGE, LPT = C::LPT, AI4 = C::AI / 4, BI4 = C::BI / 4, P = NST - 1;
+template <int TAPS, int NST, int CBK, int CBN, bool BNB, int NWM = 2>
+__global__ void __launch_bounds__(128 * NWM, 4 / NWM) gemm_conv_kernel(GemmArgs g) {
+  using C = ConvCfg<TAPS, CBK, CBN, NWM>;
+  constexpr int NW = C::NW, TM = C::TM;
+  constexpr int STAGE = C::STAGE, LPT = C::LPT, AI4 = C::AI / NW, BI4 = C::BI / NW, P = NST - 1;
   constexpr int ROW = C::ROW, CPR = C::CPR, RPI = C::RPI, NJ = C::NJ, KB = CBK / 32;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -77,7 +83,7 @@ __global__ void __launch_bounds__(256, 2) gemm_conv_kernel(GemmArgs g) {
   const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
   const int nN = (g.N + CBN - 1) / CBN;
   const int mt = lid / nN, nt = lid - mt * nN;
-  const int m0 = mt * BM, n0 = nt * CBN;
+  const int m0 = mt * TM, n0 = nt * CBN;
 
   const OpDev& A = g.a;
   const OpDev& Bo = g.b;
@@ -96,7 +102,7 @@ __global__ void __launch_bounds__(256, 2) gemm_conv_kernel(GemmArgs g) {
   for (int i = 0; i < AI4; ++i) {
     const int hr = RPI * (AI4 * wid + i) + lrow;
     const int f = m0 - pad + hr;
-    aok[i] = hr < BM + TAPS - 1 && f >= 0 && f < g.M;
+    aok[i] = hr < TM + TAPS - 1 && f >= 0 && f < g.M;
     aoff[i] = (long long)(aok[i] ? f : 0) * lda + 8 * (lslot ^ C::swz(hr));
   }
   long long boff[BI4];
@@ -104,7 +110,7 @@ __global__ void __launch_bounds__(256, 2) gemm_conv_kernel(GemmArgs g) {
 #pragma unroll
   for (int i = 0; i < BI4; ++i) {
     const int ins = wid * BI4 + i, wr = RPI * ins + lrow, tap = wr / CBN, n = n0 + (wr - tap * CBN);
-    bok[i] = n < g.N;
+    bok[i] = n < g.N && wr < C::BROWS;
     boff[i] = (long long)(bok[i] ? n : 0) * ldb + (long long)tap * chans + 8 * (lslot ^ C::swz(wr));
   }
   auto issue = [&](int st, int cs) {
@@ -194,21 +200,21 @@ __global__ void __launch_bounds__(256, 2) gemm_conv_kernel(GemmArgs g) {
     }
   }
   __syncthreads();  // last wait was vmcnt(0); every fragment read done before the epilogue reuses LDS
-  fast_epilogue<CBN, BNB, true>(g, acc, m0, n0, mt, 0, 0, smem_raw);
+  fast_epilogue<CBN, BNB, true, NWM>(g, acc, m0, n0, mt * (TM / BM), 0, 0, smem_raw);
 }
 
-template <int NST, int CBK, int CBN, bool BNB = false>
+template <int NST, int CBK, int CBN, bool BNB = false, int NWM = 2>
 void launch(const GemmArgs& g, hipStream_t s) {
-  using C = ConvCfg<5, CBK, CBN>;
+  using C = ConvCfg<5, CBK, CBN, NWM>;
   const size_t lds = (size_t)NST * C::STAGE;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_conv_kernel<5, NST, CBK, CBN, BNB>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_conv_kernel<5, NST, CBK, CBN, BNB, NWM>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  const int nb = ((g.M + BM - 1) / BM) * ((g.N + CBN - 1) / CBN);
-  gemm_conv_kernel<5, NST, CBK, CBN, BNB><<<nb, 256, lds, s>>>(g);
+  const int nb = ((g.M + C::TM - 1) / C::TM) * ((g.N + CBN - 1) / CBN);
+  gemm_conv_kernel<5, NST, CBK, CBN, BNB, NWM><<<nb, 64 * C::NW, lds, s>>>(g);
 }
 
 bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -248,6 +254,9 @@ bool gemm_conv_launch(const GemmArgs& g, hipStream_t s) {
     launch<2, 32, 64, true>(g, s);
     return true;
   }
+  // (256-row tiles -- eight waves, one workgroup per CU, three 48-KiB stages, NWM = 4 -- measured no
+  // faster: 44.4 / 36.6 us vs 42.5 / 35.2 us with / without the BN epilogue on 8192x512x2560,
+  // profiles/r3_conv_tile_ab.txt; not dispatched)
 #define CONV_CASE(NS, BK, BN)                  \
   if (ns == NS && bk == BK && bn == BN) {      \
     launch<NS, BK, BN>(g, s);                  \

@@ -219,8 +219,18 @@ int build(hipGraph_t g, hipGraphNode_t const* main_tails, int n_main, hipGraphNo
     }
     S = r + 1;
   }
-  static const bool whole = getenv("AVC_GRAPH_CLONE_ONLY") && getenv("AVC_GRAPH_CLONE_ONLY")[0] == '1';  // debug
-  if (whole) {  // one clone of the whole graph as "main segment 0", no side graphs
+  // debug: AVC_GRAPH_CLONE_ONLY=1 one copy of the whole graph as "main segment 0", no side graphs;
+  // =2 the same single graph with every main node created before every side node
+  static const int whole = getenv("AVC_GRAPH_CLONE_ONLY") ? atoi(getenv("AVC_GRAPH_CLONE_ONLY")) : 0;
+  if (whole == 2) {
+    std::vector<int> mfirst;
+    for (int x : order)
+      if (pos[x] >= 0) mfirst.push_back(x);
+    for (int x : order)
+      if (pos[x] < 0) mfirst.push_back(x);
+    order.swap(mfirst);
+  }
+  if (whole) {
     s->gm.assign(1, nullptr);
     s->gs.assign(1, nullptr);
     s->em.assign(1, nullptr);

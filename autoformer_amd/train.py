@@ -225,8 +225,12 @@ class FusedAdam:
 # workgroup cap of the decoder-slice Adam that runs beside the encoder backward (0 = full grid;
 # 256 measured best: the full 4096-block grid slowed the latency-bound BiLSTM backward beside it)
 _SIDE_ADAM_BLOCKS = int(os.environ.get("AVC_SIDE_ADAM_BLOCKS", "256"))
-# capture(): split the captured step into concurrent main / side graphs (0 = one graph, A/B)
-_GRAPH_SPLIT = os.environ.get("AVC_GRAPH_SPLIT", "1") == "1"
+# capture(): split the captured step into concurrent main / side graphs (opt-in, AVC_GRAPH_SPLIT=1).
+# Off by default: the split graphs replay correctly ONCE and produce NaN from the second replay on,
+# in every arrangement measured (any number of segments, side graphs serialised on the main stream,
+# side graphs skipped), while one graph holding the same copied nodes -- in capture order or with
+# every main node first -- replays correctly (profiles/r3_graph_split.txt).  One graph is the default.
+_GRAPH_SPLIT = os.environ.get("AVC_GRAPH_SPLIT", "0") == "1"
 
 
 class TrainStep:

@@ -1,5 +1,6 @@
-"""The step replayed as two concurrent hipGraphs (main stream + weight-gradient stream,
-graph.hip / TrainStep.capture) against the eager step.
+"""The step replayed as a captured hipGraph (TrainStep.capture: one graph by default; the
+opt-in main / side split of graph.hip is not replay-safe, see train._GRAPH_SPLIT) against the
+eager step.
 
 Each replay gets a NEW batch (copied into the captured input tensors) and lr = 0, so a side-graph
 kernel that ran before the main-graph node it depends on would read the previous batch's
@@ -36,10 +37,7 @@ def _compare(comp, B, T, freq, gtol, steps=4):
     try:
         tb.step(xb, eb)
         tb.capture(xb, eb, warmup=0)
-        assert tb.graph_split is not None, "the capture was not split into main / side graphs"
-        n_main, n_side, n_cross, n_seg = tb.graph_split.counts
-        assert n_seg > 1
-        assert n_side > 0 and n_cross > 0
+        assert tb.graph_split is None and tb.graph_fb is not None
         for i, (x, e) in enumerate(batches):
             la = ta.step(x, e)
             ga = ta.gflat.clone()
@@ -55,14 +53,13 @@ def _compare(comp, B, T, freq, gtol, steps=4):
         tb.check()
     finally:
         set_grad_sink(False)
-    return n_main, n_side, n_cross, n_seg
 
 
-def test_split_graph_replay_matches_eager_fp32():
+def test_graph_replay_matches_eager_fp32():
     _compare("fp32", 4, 64, 16, 1e-4)
 
 
-def test_split_graph_replay_matches_eager_bf16_c2():
+def test_graph_replay_matches_eager_bf16_c2():
     """At the C2 shape (B=64, T=128, bf16: the persistent recurrences, split-K weight gradients,
     halo conv kernels).  bf16 run-to-run spread of a gradient tensor is ~1e-3 (split-K order)."""
     _compare("bf16", 64, 128, 16, 1e-2)

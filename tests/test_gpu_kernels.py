@@ -992,7 +992,9 @@ def test_enc_conv0_fold_matches_concat(comp):
         torch.cuda.synchronize()
         res.append((a.float(), mel.grad, emb.grad, conv.weight.grad, bn.weight.grad, bn.bias.grad, bn.running_mean,
                     bn.running_var))
-    bar = 1e-5 if comp == "fp32" else 2e-2
+    # bf16: two bf16 computations of the same layer whose fp32 sums run in different orders; the
+    # ReLU after BN flips units with a near-zero pre-activation, which moves dL/dmel by ~3 %
+    bar = 1e-5 if comp == "fp32" else 5e-2
     names = ("a", "dmel", "demb", "dW", "dgamma", "dbeta", "running_mean", "running_var")
     for n, u, v in zip(names, res[0], res[1]):
         assert relf(u, v.double()) < bar, (n, relf(u, v.double()))
@@ -1001,3 +1003,46 @@ def test_enc_conv0_fold_matches_concat(comp):
 def Kr_act_relu():
     from autoformer_amd import kernels as Kr
     return Kr.ACT_RELU
+
+
+@pytest.mark.parametrize("B,T,Cin,Cout", [(64, 128, 512, 512), (3, 37, 64, 96), (5, 50, 96, 136), (8, 176, 512, 80),
+                                          (2, 300, 32, 64)])
+def test_conv_bn_fused_finalize(B, T, Cin, Cout):
+    """The halo conv kernel with the BN finalize in its epilogue (the forward conv + BN of every
+    ConvNorm layer) against the same conv with the separate finalize, under whatever conv tile
+    configuration the process runs (AVC_CONV_CFG: 128-row tiles by default, 256-row tiles =
+    two statistics tiles per workgroup with 13,32,64): y, partials, mean / rstd / scale / shift
+    and the running statistics."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute("bf16")
+    torch.manual_seed(11)
+    M = B * T
+    x = torch.randn(M, Cin, device=DEV).bfloat16()
+    Wf = (torch.randn(Cout, 5 * Cin, device=DEV) * 0.1).bfloat16()
+    bias = torch.randn(Cout, device=DEV)
+    gamma, beta = (torch.rand(Cout) + 0.5).to(DEV), torch.randn(Cout).to(DEV)
+    rm0, rv0 = torch.randn(Cout).to(DEV), (torch.rand(Cout) + 0.5).to(DEV)
+    outs = []
+    for fused in (True, False):
+        y = torch.empty(M, Cout, device=DEV)
+        p = Kr.bn_partial_buffer(M, Cout, DEV)
+        rm, rv, n = rm0.clone(), rv0.clone(), torch.zeros((), dtype=torch.long, device=DEV)
+        xo, wo = Kr.operand(x, Cin, window=(5, 2, T, T, Cin)), Kr.operand(Wf, 5 * Cin)
+        if fused:
+            st = Kr.gemm(M, Cout, 5 * Cin, xo, wo, y, bias=bias, bn_partial=p,
+                         bn_fin=(gamma, beta, rm, rv, n, 0.1, 1e-5, 1))
+        else:
+            Kr.gemm(M, Cout, 5 * Cin, xo, wo, y, bias=bias, bn_partial=p)
+            st = Kr.bn_finalize(p, M, Cout, gamma, beta, rm, rv, n, 0.1, 1e-5)
+        torch.cuda.synchronize()
+        outs.append((y, p, st, rm, rv))
+    (y1, p1, s1, rm1, rv1), (y2, p2, s2, rm2, rv2) = outs
+    assert torch.equal(y1, y2) and torch.equal(p1, p2)
+    for a, b in zip(s1, s2):
+        assert rinf(a, b) < 1e-6
+    assert rinf(rm1, rm2) < 1e-6 and rinf(rv1, rv2) < 1e-6
+    yf = y1.double()
+    assert rinf(s1[0], yf.mean(0)) < 1e-5
+    assert rinf(s1[1], 1 / torch.sqrt(yf.var(0, unbiased=False) + 1e-5)) < 1e-4

@@ -18,5 +18,8 @@ for fname in ("autovc_T128.npz", "autovc_T176.npz"):
     outs, losses, total = _step(m, x, e)
     torch.cuda.synchronize()
     r = [rel_inf(o.detach().cpu(), g[k]) for o, k in zip(outs[:2], ("mel", "mel_psnt"))]
+    rf = [float(np.linalg.norm(o.detach().cpu().numpy().ravel() - g[k].ravel()) / np.linalg.norm(g[k].ravel()))
+          for o, k in zip(outs[:2], ("mel", "mel_psnt"))]
     lr = np.abs(np.array([l.item() for l in losses]) / g["losses"] - 1).max()
-    print(f"{fname} bf16: mel rel-inf {r[0]:.3e}, mel_psnt {r[1]:.3e}, losses rel {lr:.2e}", flush=True)
+    print(f"{fname} bf16: mel rel-inf {r[0]:.3e} rel-frob {rf[0]:.3e}, mel_psnt rel-inf {r[1]:.3e} rel-frob "
+          f"{rf[1]:.3e}, losses rel {lr:.2e}", flush=True)
