@@ -330,3 +330,28 @@ extern "C" int avc_graph_split_destroy(void* handle) {
   destroy(reinterpret_cast<Split*>(handle));
   return 0;
 }
+
+// ---------------------------------------------------------------- host-side event helpers
+// Cross-stream ordering of the step (weight-gradient side stream, pack prefetch) with raw HIP
+// events on raw stream handles: torch.cuda.Event / current_stream() cost ~10-15 us of Python
+// per use, ~1 ms per AutoVC step at ~90 uses.  Events are created once (a ring on the Python
+// side) and re-recorded; hipStreamWaitEvent waits for the record current at the time of the call.
+extern "C" int avc_event_create(void** out) {
+  AVC_CHECK_ARG(out, "avc_event_create: null");
+  hipEvent_t e = nullptr;
+  GCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming), "avc_event_create");
+  *out = e;
+  return 0;
+}
+
+extern "C" int avc_event_record(void* ev, void* stream) {
+  AVC_CHECK_ARG(ev, "avc_event_record: null event");
+  GCHK(hipEventRecord(reinterpret_cast<hipEvent_t>(ev), as_stream(stream)), "avc_event_record");
+  return 0;
+}
+
+extern "C" int avc_stream_wait_event(void* stream, void* ev) {
+  AVC_CHECK_ARG(ev, "avc_stream_wait_event: null event");
+  GCHK(hipStreamWaitEvent(as_stream(stream), reinterpret_cast<hipEvent_t>(ev), 0), "avc_stream_wait_event");
+  return 0;
+}

@@ -45,6 +45,65 @@ def set_grad_sink(on: bool) -> None:
         _SINK["side"] = torch.cuda.Stream()
 
 
+# ---- cheap cross-stream ordering: raw HIP events on raw stream handles (graph.hip helpers) and
+# torch's current stream switched through its C bindings.  torch.cuda.Event() / .record() /
+# current_stream() / torch.cuda.stream() cost 10-15 us of Python each (measured ~1 ms per AutoVC
+# step at ~90 uses, tools/host_profile2.py); these cost a ctypes call.
+_EV = {"ring": [], "i": 0}
+_EV_RING = 512  # events in flight per step are < 100; a handle is re-recorded 5+ steps later
+
+
+def ev_record(stream_raw=None):
+    """Record a ring event on the raw stream (default: torch's current stream); returns its handle."""
+    ring = _EV["ring"]
+    if not ring:
+        import ctypes
+
+        for _ in range(_EV_RING):
+            h = ctypes.c_void_p()
+            K.L.call("avc_event_create", ctypes.byref(h))
+            ring.append(h.value)
+    i = _EV["i"]
+    _EV["i"] = (i + 1) % len(ring)
+    h = ring[i]
+    K.L.call("avc_event_record", h, K.stream() if stream_raw is None else stream_raw)
+    return h
+
+
+def stream_wait(stream_raw, ev):
+    """The raw stream waits for the event's current record."""
+    K.L.call("avc_stream_wait_event", stream_raw, ev)
+
+
+_get_cur = torch._C._cuda_getCurrentStream
+_set_cur = torch._C._cuda_setStream
+
+
+def on_stream(stream):
+    return _OnStream(stream)
+
+
+class _OnStream:
+    """torch's current stream switched to `stream` (allocations and launches go there) through
+    the C bindings -- what torch.cuda.stream(stream) does for a single-device process."""
+
+    __slots__ = ("stream", "prev")
+
+    def __init__(self, stream):
+        self.stream = stream
+
+    def __enter__(self):
+        self.prev = _get_cur(K._cur_device())
+        st = self.stream
+        _set_cur(stream_id=st.stream_id, device_index=st.device_index, device_type=st.device_type)
+        return self
+
+    def __exit__(self, *exc):
+        sid, dev, dt = self.prev
+        _set_cur(stream_id=sid, device_index=dev, device_type=dt)
+        return False
+
+
 def sink_on() -> bool:
     return _SINK["on"]
 
@@ -60,9 +119,7 @@ def mark():
     the host work of queueing the weight-gradient branch."""
     if not _SINK["on"]:
         return None
-    ev = torch.cuda.Event()
-    ev.record()
-    return ev
+    return ev_record()
 
 
 class _Side:
@@ -74,13 +131,9 @@ class _Side:
         self.after = after
 
     def __enter__(self):
-        self.main = torch.cuda.current_stream()
         side = _SINK["side"]
-        if self.after is not None:
-            side.wait_event(self.after)
-        else:
-            side.wait_stream(self.main)
-        self.ctx = torch.cuda.stream(side)
+        stream_wait(side.cuda_stream, self.after if self.after is not None else ev_record())
+        self.ctx = _OnStream(side)
         self.ctx.__enter__()
         return self
 
@@ -95,12 +148,11 @@ class _Side:
 def join_side() -> None:
     side = _SINK["side"]
     if side is not None:
-        cur = torch.cuda.current_stream()
         if _SINK.get("tails") == [] and torch.cuda.is_current_stream_capturing():
             # a capture that TrainStep will split into a main and a side graph: each stream's
             # capture dependencies at the join (graph.hip, avc_graph_split)
-            _SINK["tails"] = [K.capture_deps(cur), K.capture_deps(side)]
-        cur.wait_stream(side)
+            _SINK["tails"] = [K.capture_deps(torch.cuda.current_stream()), K.capture_deps(side)]
+        stream_wait(K.stream(), ev_record(side.cuda_stream))
     _SINK["keep"].clear()
 
 
@@ -153,7 +205,7 @@ class PackCache:
         if key != self.key:
             pend, self.pending = self.pending, None
             if pend is not None and pend[0] == key:
-                torch.cuda.current_stream().wait_event(pend[2])
+                stream_wait(K.stream(), pend[2])
                 self.val = pend[1]
             else:
                 with torch.no_grad():
@@ -232,8 +284,9 @@ def prefetch_packs() -> None:
     side = _SINK["side"]
     if side is None or not _PLAN:
         return
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side), torch.no_grad():
+    side_raw = side.cuda_stream
+    stream_wait(side_raw, ev_record())
+    with _OnStream(side), torch.no_grad():
         batched = []
         for ref in list(_PLAN):
             c = ref()
@@ -247,9 +300,7 @@ def prefetch_packs() -> None:
                 batched.append((c, key))
                 continue
             val = c.build()
-            ev = torch.cuda.Event()
-            ev.record(side)
-            c.pending = (key, val, ev)
+            c.pending = (key, val, ev_record(side_raw))
         # a few launches in first-use order, each with its own event: the next forward waits for
         # the encoder's packs only, not for the whole batch
         for gi in range(0, len(batched), _PACK_GROUP):
@@ -257,8 +308,7 @@ def prefetch_packs() -> None:
             plan = _batch_plan([c for c, _ in grp], gi)
             K.L.call("avc_pack_batch", plan["ops"].data_ptr(), plan["prefix"].data_ptr(), plan["n"], plan["total"],
                      K.stream())
-            ev = torch.cuda.Event()
-            ev.record(side)
+            ev = ev_record(side_raw)
             for c, key in grp:
                 c.pending = (key, c.val, ev)
 
@@ -1074,11 +1124,9 @@ def dec_concat(codes, emb, B, T, nc, cd):
 
 # =============================================================================== layout
 def _transpose_batched(x, B, R, C):
-    """x viewed as B x [R][C] -> B x [C][R] (fp32)."""
-    out = torch.empty(B * C * R, device=x.device)
-    for b in range(B):
-        K.transpose(x.reshape(B, R, C)[b], K.F32, out=out[b * C * R:(b + 1) * C * R].view(C, R))
-    return out
+    """x viewed as B x [R][C] -> B x [C][R] (fp32), one launch (a per-utterance loop of transposes
+    had cost the discriminator step 196 launches and 0.8 ms of GPU time)."""
+    return K.transpose_batched(x, B, R, C)
 
 
 class _BCTToFramesFn(torch.autograd.Function):

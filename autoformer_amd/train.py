@@ -25,7 +25,8 @@ import torch
 
 from . import dist as D
 from . import kernels as K
-from .layers import join_side, prefetch_packs, record_join_tails, set_grad_sink, side_stream, weights_changed
+from .layers import (ev_record, join_side, on_stream, prefetch_packs, record_join_tails, set_grad_sink, side_stream,
+                     stream_wait, weights_changed)
 
 
 def _load_state(model, path, device):
@@ -294,12 +295,12 @@ class TrainStep:
         K.raise_on_fault(self._fault.item())
 
     def _decoder_done(self):
-        main = torch.cuda.current_stream()
-        self.comm.wait_stream(main)
+        comm = self.comm.cuda_stream
+        stream_wait(comm, ev_record())
         side = side_stream()
         if side is not None:
-            self.comm.wait_stream(side)
-        with torch.cuda.stream(self.comm):
+            stream_wait(comm, ev_record(side.cuda_stream))
+        with on_stream(self.comm):
             if self.world > 1:
                 # RCCL: the comm stream waits for the collective; the Adam slice follows it
                 self._early = D.allreduce_mean_async_(self.gflat[self.split:])
@@ -326,7 +327,6 @@ class TrainStep:
         if timed:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        main = torch.cuda.current_stream()
         if not self._early_adam:  # no overlapped part (graph replay, or no hook fired)
             if self.world > 1:
                 D.allreduce_mean_(self.gflat)
@@ -335,10 +335,10 @@ class TrainStep:
             self.opt.step()
         else:
             if self.world > 1:
-                self.comm.wait_stream(main)
+                self.comm.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(self.comm):
                     D.finish_allreduce_(D.allreduce_mean_async_(self.gflat[:self.split]))
-            main.wait_stream(self.comm)  # the early slice's Adam (and its step-count advance)
+            stream_wait(K.stream(), ev_record(self.comm.cuda_stream))  # the early slice's Adam (and its step count)
             if timed:
                 ev[1].record()
             self.opt.step_slice(0, self.split, advance=False)

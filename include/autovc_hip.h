@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 14
+#define AVC_ABI_VERSION 15
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -464,6 +464,14 @@ int avc_mg_wn_pack(const float* v, const float* g, const float* bias, int d0, in
  * out[b*L + t] = tanh(bias + sum_k,c w[k][c] act(x[b][reflect(t + k - 3)][c])). */
 int avc_mg_conv_out(const float* x, int B, int L, int C, int taps, const float* w, const float* bias, float slope,
                     float* out, void* stream);
+
+/* Host-side event helpers (graph.hip): one reusable event (hipEventDisableTiming), recorded on a
+ * raw stream handle, and a stream made to wait for the record current at the time of the call --
+ * the step's cross-stream ordering (weight-gradient side stream, pack prefetch) without
+ * torch.cuda.Event / current_stream() Python costs.  Work inside a stream capture as well. */
+int avc_event_create(void** out);
+int avc_event_record(void* ev, void* stream);
+int avc_stream_wait_event(void* stream, void* ev);
 
 /* ---- the training step as two concurrent hipGraphs (graph.hip).  Not a reference operation:
  * host plumbing of train.py's step loop (train.py:82-99) when the step is replayed from a capture.
