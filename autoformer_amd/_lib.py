@@ -16,8 +16,8 @@ import torch  # noqa: F401  (must precede the HIP library)
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "graph.hip", "fold.hip"]
-ABI_VERSION = 15
+SOURCES = ["gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "graph.hip", "fold.hip", "disc.hip"]
+ABI_VERSION = 16
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -114,6 +114,9 @@ _SIGS = {
     "avc_conv_edge_colsum": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "avc_conv_grad_unpack_slice": (c_int, [c_void_p, c_ll, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                            c_void_p]),
+    "avc_disc_dense_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "avc_disc_dense_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                   c_void_p, c_void_p]),
     "avc_convert": (c_int, [c_void_p, c_void_p, c_int, c_ll, c_void_p]),
     "avc_transpose": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_ll, c_void_p]),
     "avc_add": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_void_p]),

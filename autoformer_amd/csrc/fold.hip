@@ -26,9 +26,16 @@ __device__ __forceinline__ void put(void* dst, long long i, float v, int dtype) 
 __global__ void conv_pack_slice_kernel(const float* __restrict__ w, void* __restrict__ out, int dtype, int Co, int Ci,
                                        int K, int ci0, int cn, int cpad, int mode) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)Co * cpad * K;
+  const long long total = (long long)(mode == 3 ? cn : Co) * cpad * K;
   if (i >= total) return;
   int co, ci, k;
+  if (mode == 3) {  // out[cn][k'][cpad], k' = K-1-k: the OUTPUT channel axis padded (data-gradient pack)
+    co = (int)(i % cpad);
+    k = K - 1 - (int)((i / cpad) % K);
+    ci = (int)(i / ((long long)cpad * K));
+    put(out, i, co < Co ? w[((long long)co * Ci + ci0 + ci) * K + k] : 0.f, dtype);
+    return;
+  }
   if (mode == 0) {  // out[co][k][cpad]
     ci = (int)(i % cpad);
     k = (int)((i / cpad) % K);
@@ -120,10 +127,10 @@ __global__ void conv_grad_unpack_slice_kernel(const float* __restrict__ dwf, lon
 
 extern "C" int avc_conv_pack_slice(const float* w, void* out, int dtype, int Co, int Ci, int K, int ci0, int cn,
                                    int cpad, int mode, void* stream) {
-  AVC_CHECK_ARG(w && out && Co > 0 && Ci > 0 && K > 0 && ci0 >= 0 && cn > 0 && ci0 + cn <= Ci && cpad >= cn &&
-                    (mode == 0 || mode == 1 || mode == 2) && (dtype == AVC_F32 || dtype == AVC_BF16),
+  AVC_CHECK_ARG(w && out && Co > 0 && Ci > 0 && K > 0 && ci0 >= 0 && cn > 0 && ci0 + cn <= Ci &&
+                    cpad >= (mode == 3 ? Co : cn) && mode >= 0 && mode <= 3 && (dtype == AVC_F32 || dtype == AVC_BF16),
                 "avc_conv_pack_slice: bad args");
-  const long long n = (long long)Co * cpad * K;
+  const long long n = (long long)(mode == 3 ? cn : Co) * cpad * K;
   conv_pack_slice_kernel<<<cdiv(n, 256), 256, 0, as_stream(stream)>>>(w, out, dtype, Co, Ci, K, ci0, cn, cpad, mode);
   return avc_check_launch("avc_conv_pack_slice");
 }

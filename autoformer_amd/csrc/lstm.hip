@@ -1090,11 +1090,7 @@ struct PersistBwdArgs {
   int B, T, ng;
 };
 
-// WL (flag form only): after the flag poll each wave stages ONLY its own K range of dG_{t+1}
-// (gate gq, K half kh: 8 rows x H/2, coalesced 1-KiB row segments) into its part of the LDS tile
-// and reads only that part, so the workgroup barrier between the payload load and the product
-// is gone -- a wave starts its MFMAs as soon as its own 8 KB have landed.
-template <int H, bool GR, bool WL = false>
+template <int H, bool GR>
 __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
   constexpr int G = 4 * H, NKH = H / 64, AP = G + 8, KH = H / 2, NW = PNT / 64;
   constexpr int NCH = (PRG * G / 8 + PNT - 1) / PNT;  // 16-B payload chunks per thread per step
@@ -1158,27 +1154,6 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
           *quit = 1;
         __syncthreads();
         if (*quit) return;
-      } else if constexpr (WL) {
-        if (w == 0 && !poll_flags(flags, H / PJU, (unsigned)s, a.ctl, a.fault, a.spin)) *quit = 1;
-        __syncthreads();
-        if (*quit) return;  // block-uniform exit after a spin timeout
-        // this wave's K range: columns [gq*H + kh*KH, +KH) of the PRG payload rows, KH/8 chunks per row
-        constexpr int CPRW = KH / 8, NCW = PRG * CPRW / 64;
-        static_assert(NCW * 64 == PRG * CPRW, "wave chunks must tile its payload slice");
-        const int row0 = ((s - 1) & 1) * B + b0, c0 = gq * H + kh * KH;
-        u32x4_t v[NCW];
-#pragma unroll
-        for (int i = 0; i < NCW; ++i) {
-          const int ch = lane + 64 * i, row = ch / CPRW, col = ch - row * CPRW;
-          v[i] = row < rows ? __builtin_amdgcn_raw_buffer_load_b128(pay, ((row0 + row) * G + c0 + col * 8) * 2, 0, AUX_SC1)
-                            : u32x4_t{0u, 0u, 0u, 0u};
-        }
-#pragma unroll
-        for (int i = 0; i < NCW; ++i) {
-          const int ch = lane + 64 * i, row = ch / CPRW, col = ch - row * CPRW;
-          *reinterpret_cast<u32x4_t*>(As + row * AP + c0 + col * 8) = v[i];
-        }
-        // the wave reads only what it wrote: its own LDS writes are ordered before its reads
       } else {
         if (w == 0 && !poll_flags(flags, H / PJU, (unsigned)s, a.ctl, a.fault, a.spin)) *quit = 1;
         __syncthreads();
@@ -1537,24 +1512,15 @@ unsigned spin_bound() {
 }
 
 // Dynamic-LDS attribute of the persistent backward kernels, set once per (kernel, device).
-template <int H, bool GR, bool WL = false>
+template <int H, bool GR>
 void set_bwd_lds_attr() {
   int dev = 0;
   (void)hipGetDevice(&dev);
   static std::once_flag once[MAXDEV];
   std::call_once(once[dev & (MAXDEV - 1)], [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_persist_bwd<H, GR, WL>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_persist_bwd<H, GR>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_bwd_lds<H>());
   });
-}
-
-// AVC_LSTM_BWD_WL=1: the wave-local payload staging of lstm_persist_bwd (WL, A/B)
-bool bwd_wl() {
-  static const bool v = [] {
-    const char* e = getenv("AVC_LSTM_BWD_WL");
-    return e && e[0] == '1';
-  }();
-  return v;
 }
 
 // Hand-off form.  Default (measured): granules where a consumer's granule
@@ -1585,10 +1551,6 @@ const void* persist_fn(bool bwd) {
     if (gran(true, H)) {
       set_bwd_lds_attr<H, true>();
       return reinterpret_cast<const void*>(&lstm_persist_bwd<H, true>);
-    }
-    if (bwd_wl()) {
-      set_bwd_lds_attr<H, false, true>();
-      return reinterpret_cast<const void*>(&lstm_persist_bwd<H, false, true>);
     }
     set_bwd_lds_attr<H, false>();
     return reinterpret_cast<const void*>(&lstm_persist_bwd<H, false>);
@@ -1648,7 +1610,6 @@ bool persistent_path(int B, int H, int dirs, bool bf, bool bwd) {
 template <int H>
 void launch_persist_bwd(dim3 grid, hipStream_t s, bool gr, const PersistBwdArgs& p) {
   if (gr) lstm_persist_bwd<H, true><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
-  else if (bwd_wl()) lstm_persist_bwd<H, false, true><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
   else lstm_persist_bwd<H, false><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
 }
 

@@ -43,43 +43,46 @@ class _DiscFn(torch.autograd.Function):
         st2 = mod._bn(bn2, z3)
         a3 = K.bn_apply(z3, st2[2], st2[3], K.ACT_NONE)
         C3 = c3.weight.shape[0]
-        # dense1 weight is (1, C3*L3) channel-major; our a3 rows are (l, c) bin-major
-        wperm = K.transpose(dense.weight.reshape(C3, L3), K.F32).reshape(1, L3 * C3).contiguous()
-        logit = torch.empty(B, 1, device=x.device)
-        K.gemm(B, 1, L3 * C3, K.operand(a3, L3 * C3), K.operand(wperm, L3 * C3), logit, bias=dense.bias, comp=K.F32)
-        p = K.act_fwd(logit, K.ACT_SIGMOID)
+        # dense1 + sigmoid: dense1.weight is (1, C3*L3) channel-major, a3's rows are (l, c)
+        # bin-major; the kernel indexes the weight through that permutation (disc.hip)
+        wd = dense.weight.detach()
+        p = K.disc_dense_fwd(a3, wd, dense.bias, B, L3, C3)
         ctx.mod = mod
         ctx.dims = (B, C0, L0, L1, L2, L3, C3)
         ctx.stats = (st1, st2)
-        ctx.save_for_backward(xt, a1, z2, a2, z3, a3, wperm, p)
+        ctx.save_for_backward(xt, a1, z2, a2, z3, a3, wd, p)
         ctx.twins = tuple(getattr(t, "_bf16", None) for t in (xt, a1, a2))
         return p
 
     @staticmethod
     def backward(ctx, dp):
-        xt, a1, z2, a2, z3, a3, wperm, p = ctx.saved_tensors
+        xt, a1, z2, a2, z3, a3, wd, p = ctx.saved_tensors
         for t, tw in zip((xt, a1, a2), ctx.twins):
             K.attach_twin(t, tw)
         mod = ctx.mod
         B, C0, L0, L1, L2, L3, C3 = ctx.dims
         (m1, r1, _, _), (m2, r2, _, _) = ctx.stats
         c1, c2, c3, bn1, bn2, dense = mod.conv1, mod.conv2, mod.conv3, mod.bn1, mod.bn2, mod.dense1
-        dlogit = K.act_bwd(dp.contiguous(), p, K.ACT_SIGMOID)
-        F = L3 * C3
-        dwp = torch.empty(1, F, device=p.device)
-        K.gemm(1, F, B, K.operand(dlogit, 1, kstrided=True), K.operand(a3, F, kstrided=True), dwp, comp=K.F32)
-        d_dense_w = K.transpose(dwp.view(L3, C3), K.F32).reshape(1, F)
-        d_dense_b = K.colsum(dlogit, B, 1)
-        da3 = torch.empty(B, F, device=p.device)
-        K.gemm(B, F, 1, K.operand(dlogit, 1), K.operand(wperm, F, kstrided=True), da3, comp=K.F32)
+        da3, d_dense_w, d_dense_b = K.disc_dense_bwd(dp.contiguous(), p, a3, wd, B, L3, C3)
         dz3, dg2, db2, _ = K.bn_bwd(da3.view(B * L3, C3), a3, z3, m2, r2, bn2.weight, K.ACT_NONE, need_dbias=False)
-        dy3 = K.twin(K.act_bwd(dz3, z3, K.ACT_LEAKY))
-        _, Wd3 = Lyr.conv_packs(mod._c[2], c3.weight)
+        dy3 = K.act_bwd(dz3, z3, K.ACT_LEAKY)
         _, Wd2 = Lyr.conv_packs(mod._c[1], c2.weight)
         _, Wd1 = Lyr.conv_packs(mod._c[0], c1.weight)
-        dW3 = Lyr.conv_wgrad(dy3, a2, B, L2, L3, c3.weight, 0)
+        # conv3's 22 output channels: dy3 and the data-gradient pack zero-padded to a multiple of 4,
+        # so both conv3 gradient products take the vectorised GEMM kernels (22-wide rows ran on the
+        # generic kernel: 2 x 85 us per C5 step)
+        C2, C3p = c3.weight.shape[1], -(-C3 // 4) * 4
+        w3 = c3.weight
+        dy3p = K.pad_cols(dy3, C3p, K.compute())
+        Wd3 = mod._c3d.get([w3], lambda: K.conv_pack_slice(w3.detach(), 0, C2, C3p, 3, K.compute()))
+        dWf3 = torch.empty(C3p, 3 * C2, device=p.device)
+        K.gemm(C3p, 3 * C2, B * L3, Lyr.operand(dy3p, C3p, kstrided=True),
+               Lyr.operand(a2, C2, kstrided=True, window=(3, 0, L3, L2, C2)), dWf3,
+               split_k=K.auto_split_k(C3p, 3 * C2, B * L3))
+        dW3 = K.conv_grad_unpack(dWf3[:C3], C3, C2, 3)
         db3 = K.colsum(dy3, B * L3, C3)
-        da2 = Lyr.conv_dgrad(dy3, B, L2, L3, c3.weight, 0, Wd3)
+        da2 = torch.empty(B * L2, C2, device=p.device)
+        K.gemm(B * L2, C2, 3 * C3p, Lyr.operand(dy3p, C3p, window=(3, 2, L2, L3, C3p)), Lyr.operand(Wd3, 3 * C3p), da2)
         dz2, dg1, db1, _ = K.bn_bwd(da2, a2, z2, m1, r1, bn1.weight, K.ACT_NONE, need_dbias=False)
         dy2 = K.twin(K.act_bwd(dz2, z2, K.ACT_LEAKY))
         dW2 = Lyr.conv_wgrad(dy2, a1, B, L1, L2, c2.weight, 0)
@@ -108,6 +111,7 @@ class Discriminator(nn.Module):
         self.dense1 = nn.Linear(1628, 1)
         self.sigmoid = nn.Sigmoid()
         self._c = [Lyr.PackCache() for _ in range(3)]
+        self._c3d = Lyr.PackCache()  # conv3 data-gradient pack, output channels padded
 
     def _bn(self, bn, z):
         M, C = z.shape

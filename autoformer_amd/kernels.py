@@ -488,11 +488,15 @@ def conv_pack(w, mode, dtype):
 
 def conv_pack_slice(w, ci0, cn, cpad, mode, dtype):
     """Pack input channels [ci0, ci0+cn) of conv weight w (Co, Ci, K), channel axis zero-padded to
-    cpad: mode 0 -> (Co, K*cpad), 1 -> (cpad, K*Co) (flipped taps), 2 -> (K*Co, cpad)."""
+    cpad: mode 0 -> (Co, K*cpad), 1 -> (cpad, K*Co) (flipped taps), 2 -> (K*Co, cpad); mode 3 pads
+    the OUTPUT channel axis instead: (cn, K*cpad), flipped taps, cpad >= Co (a data-gradient pack
+    whose dy operand has cpad columns)."""
     Co, Ci, Kw = w.shape
     tdt = torch.bfloat16 if dtype == BF16 else torch.float32
-    out = torch.empty(Co * cpad * Kw, device=w.device, dtype=tdt)
+    out = torch.empty((cn if mode == 3 else Co) * cpad * Kw, device=w.device, dtype=tdt)
     L.call("avc_conv_pack_slice", w.data_ptr(), out.data_ptr(), dtype, Co, Ci, Kw, ci0, cn, cpad, mode, stream())
+    if mode == 3:
+        return out.view(cn, Kw * cpad)
     return out.view(*((Co, Kw * cpad) if mode == 0 else (cpad, Kw * Co) if mode == 1 else (Kw * Co, cpad)))
 
 
@@ -510,6 +514,25 @@ def conv_edge_colsum(dy, B, T, C, Kw, pad):
     out = torch.empty(B * Kw, C, device=dy.device)
     L.call("avc_conv_edge_colsum", dy.data_ptr(), _dt(dy), B, T, C, Kw, pad, out.data_ptr(), stream())
     return out
+
+
+def disc_dense_fwd(a, w, bias, B, nl, nc):
+    """Discriminator head: sigmoid(bias + a . w) per utterance with a bin-major [B][nl*nc] and w
+    the channel-major dense1.weight (nc*nl).  Returns p (B, 1)."""
+    _dev(a)
+    p = torch.empty(B, 1, device=a.device)
+    L.call("avc_disc_dense_fwd", a.data_ptr(), w.data_ptr(), _ptr(bias), B, nl, nc, None, p.data_ptr(), stream())
+    return p
+
+
+def disc_dense_bwd(dp, p, a, w, B, nl, nc):
+    """(da [B][nl*nc], dw (1, nc*nl), dbias (1,)) from dL/dp through the sigmoid."""
+    da = torch.empty(B, nl * nc, device=a.device)
+    dw = torch.empty(1, nc * nl, device=a.device)
+    db = torch.empty(1, device=a.device)
+    L.call("avc_disc_dense_bwd", dp.data_ptr(), p.data_ptr(), a.data_ptr(), w.data_ptr(), B, nl, nc, da.data_ptr(),
+           dw.data_ptr(), db.data_ptr(), stream())
+    return da, dw, db
 
 
 def conv_grad_unpack_slice(dwf, ld, kstride, dw, ci0, cn, accumulate=True):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 15
+#define AVC_ABI_VERSION 16
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -290,7 +290,8 @@ int avc_conv_grad_unpack(const float* dwf, float* dw, int Cout, int Cin, int Kw,
 /* The encoder conv0 fold (fold.hip; factory/AutoVC.py:46-51: cat(mel, c_org broadcast) -> ConvNorm(336,
  * 512, 5)).  pack_slice packs the input channels [ci0, ci0 + cn) of W [Co][Ci][K] (fp32) into `out`
  * (dtype), the channel axis zero-padded to cpad: mode 0 Wf[co][k][cpad] (forward), 1 Wd[cpad][K-1-k][co]
- * (data gradient), 2 We[k][co][cpad] (the speaker term E = c . We^T).
+ * (data gradient), 2 We[k][co][cpad] (the speaker term E = c . We^T); mode 3 Wd[cn][K-1-k][cpad] with
+ * the OUTPUT channel axis padded (cpad >= Co; the Discriminator's 22-channel conv3 data gradient).
  * edge_table: S[b][cls][co] = sum over the taps k valid at edge class cls (see avc_gemm_desc.row_bias)
  * of E[b][k*Co + co]; T > 2 pad.
  * edge_colsum: out[b][k][c] = sum over the frames t of utterance b with 0 <= t + k - pad < T of
@@ -302,6 +303,14 @@ int avc_conv_edge_table(const float* E, int B, int Co, int K, int T, int pad, fl
 int avc_conv_edge_colsum(const void* dy, int dy_dtype, int B, int T, int C, int K, int pad, float* out, void* stream);
 int avc_conv_grad_unpack_slice(const float* dwf, long long ld, int kstride, float* dw, int Co, int Ci, int K, int ci0,
                                int cn, int accumulate, void* stream);
+/* Discriminator head (factory/Discriminator.py:28-29, dense1 + sigmoid over the flattened C x L
+ * channel-major features) on the bin-major activation a [B][L][C]: p[b] = sigmoid(bias +
+ * sum a[b][l*C + c] w[c*L + l]) (logit optional); backward through the sigmoid from dL/dp:
+ * da [B][L*C], dw [C*L] (dense1.weight layout), dbias [1] (each optional), B <= 1024. */
+int avc_disc_dense_fwd(const float* a, const float* w, const float* bias, int B, int L, int C, float* logit, float* p,
+                       void* stream);
+int avc_disc_dense_bwd(const float* dp, const float* p, const float* a, const float* w, int B, int L, int C, float* da,
+                       float* dw, float* dbias, void* stream);
 /* dst = convert(src) (n elements). */
 int avc_convert(const float* src, void* dst, int dtype, long long n, void* stream);
 /* dst[c * ld_dst + r] = convert(src[r][c]) for a row-major [R][C] fp32 matrix (ld_dst = 0:

@@ -166,6 +166,21 @@ def test_bn_stats_epilogue_and_finalize(M, C):
     assert int(nbt.item()) == 1
 
 
+@pytest.mark.parametrize("M,C,ld", [(4864, 44, 44), (4736, 22, 22), (300, 70, 80), (77, 5, 8), (128, 512, 512)])
+def test_bn_stats_plain(M, C, ld):
+    """avc_bn_stats (the stats pass for activations no GEMM produced: the Discriminator's BNs)
+    + finalize against fp64 batch statistics, ragged row tiles and a row stride > C."""
+    from autoformer_amd import kernels as Kr
+
+    y = torch.randn(M, ld) * 2 + 3.0
+    yd = y.to(DEV)
+    part = Kr.bn_stats(yd, M, C, ld=ld)
+    mean, rstd, _, _ = Kr.bn_finalize(part, M, C, None, None, None, None, None, 0.1, 1e-5)
+    ref = y[:, :C].double()
+    assert rinf(mean, ref.mean(0)) < 1e-5
+    assert rinf(rstd, 1 / torch.sqrt(ref.var(0, unbiased=False) + 1e-5)) < 1e-4
+
+
 @pytest.mark.parametrize("M,C,Kd", [(8192, 512, 2560), (352, 80, 64), (300, 176, 64), (1000, 1024, 128)])
 @pytest.mark.parametrize("comp,nupd", [("bf16", 1), ("bf16", 2), ("fp32", 2)])
 def test_gemm_bn_fused_finalize(M, C, Kd, comp, nupd):
@@ -1046,3 +1061,41 @@ def test_conv_bn_fused_finalize(B, T, Cin, Cout):
     yf = y1.double()
     assert rinf(s1[0], yf.mean(0)) < 1e-5
     assert rinf(s1[1], 1 / torch.sqrt(yf.var(0, unbiased=False) + 1e-5)) < 1e-4
+
+
+# ------------------------------------------------------------------ Discriminator head (disc.hip)
+@pytest.mark.parametrize("B,nl,nc", [(64, 74, 22), (5, 9, 7), (300, 3, 130)])
+def test_disc_dense_head(B, nl, nc):
+    """sigmoid(dense1(flatten(a))) with the channel-major flatten of Discriminator.py:28-29 on a
+    bin-major activation, and its backward from dL/dp, against fp64 autograd."""
+    from autoformer_amd import kernels as K
+
+    a = torch.randn(B, nl, nc)
+    w = torch.randn(1, nc * nl) * 0.1
+    bias = torch.randn(1)
+    dp = torch.randn(B, 1)
+    a64, w64, b64 = (t.double().requires_grad_() for t in (a, w, bias))
+    # reference flatten: (B, C, L) channel-major
+    p64 = torch.sigmoid(a64.transpose(1, 2).reshape(B, nc * nl) @ w64.t() + b64)
+    p64.backward(dp.double())
+    ad, wd, bd = a.to(DEV).reshape(B, nl * nc), w.to(DEV), bias.to(DEV)
+    p = K.disc_dense_fwd(ad, wd, bd, B, nl, nc)
+    da, dw, db = K.disc_dense_bwd(dp.to(DEV), p, ad, wd, B, nl, nc)
+    assert rinf(p, p64.detach()) < 1e-5
+    assert relf(da.view(B, nl, nc), a64.grad) < 1e-5
+    assert relf(dw, w64.grad) < 1e-5
+    assert relf(db, b64.grad) < 1e-5
+
+
+def test_conv_pack_slice_output_padded():
+    """conv_pack_slice mode 3 (data-gradient pack with the output-channel axis zero-padded):
+    Wd[ci][k'][co] = w[co][ci][K-1-k'] for co < Co, 0 in the pad -- conv_pack mode 1 widened."""
+    from autoformer_amd import kernels as Kr
+
+    w = torch.randn(22, 44, 3)
+    got = Kr.conv_pack_slice(w.to(DEV), 0, 44, 24, 3, Kr.F32).cpu().view(44, 3, 24)
+    ref = torch.zeros(44, 3, 24)
+    ref[:, :, :22] = w.flip(2).permute(1, 2, 0)
+    assert torch.equal(got, ref)
+    base = Kr.conv_pack(w.to(DEV), 1, Kr.F32).cpu().view(44, 3, 22)
+    assert torch.equal(got[:, :, :22], base)

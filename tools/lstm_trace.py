@@ -109,3 +109,40 @@ h, c, g = K.lstm_fwd(xproj, whh, B, T, H, 2)
 dh = torch.randn_like(h) * 0.1
 usb = ev_time(lambda: K.lstm_bwd(dh, h, c, g, whh, None, B, T, H, 2))
 print(f"BiLSTM H=44 fwd {us:7.1f} us ({us / T:4.2f}/step)  bwd {usb:7.1f} us ({usb / T:4.2f}/step)", flush=True)
+
+# BiLSTM per-step phases (TRACE build of the small-H kernels: stamps of wave 0 at j = 0..3, the
+# other compute waves' pre-barrier stamps at j = 5..7 forward; backward j = 0..3 wave 0, 4 / 5
+# the flush wave's step start / pre-barrier).  The stamps' own s_waitcnt lgkmcnt(0) serialises
+# LDS traffic, so the traced step is slower than the untraced one; the split is what counts.
+Tp = (T + 15) // 16 * 16
+
+
+def small_traced(fn):
+    buf = torch.zeros(B * 2 * Tp * 8, dtype=torch.int64, device=dev)
+    _lib.call("avc_lstm_trace", buf.data_ptr())
+    try:
+        fn()
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("avc_lstm_trace", None)
+    return buf.cpu().numpy().reshape(B * 2, Tp, 8).astype(np.float64) * 1e-2
+
+
+s = slice(1, T - 1)
+st = small_traced(lambda: K.lstm_fwd(xproj, whh, B, T, H, 2))
+per = np.diff(st[:, :T, 0], axis=1)[:, 1:].mean()
+dot = (st[:, s, 1] - st[:, s, 0]).mean()
+cell = (st[:, s, 2] - st[:, s, 1]).mean()
+wr = (st[:, s, 3] - st[:, s, 2]).mean()
+last = np.maximum(st[:, s, 3], st[:, s, 5:8].max(axis=2))
+bar = (st[:, 2:T, 0] - last).mean()
+print(f"BiLSTM fwd traced: period {per:5.3f} | dot {dot:5.3f} cell {cell:5.3f} write {wr:5.3f} "
+      f"last-wave -> next step {bar:5.3f} us", flush=True)
+st = small_traced(lambda: K.lstm_bwd(dh, h, c, g, whh, None, B, T, H, 2))
+per = np.diff(st[:, :T, 0], axis=1)[:, 1:].mean()
+dot = (st[:, s, 1] - st[:, s, 0]).mean()
+cell = (st[:, s, 2] - st[:, s, 1]).mean()
+wr = (st[:, s, 3] - st[:, s, 2]).mean()
+bar = (st[:, 2:T, 0] - np.maximum(st[:, s, 3], st[:, s, 5])).mean()
+print(f"BiLSTM bwd traced: period {per:5.3f} | dot {dot:5.3f} cell {cell:5.3f} write {wr:5.3f} "
+      f"last-wave -> next step {bar:5.3f} us", flush=True)
