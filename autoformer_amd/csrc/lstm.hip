@@ -805,6 +805,13 @@ __device__ __forceinline__ bool poll_flags(unsigned* flags, int NR, unsigned tag
   const int lane = threadIdx.x & 63;
   gu32* f = (gu32*)flags;
   unsigned spins = 0;
+  if (spin == 0) {  // injected timeout (avc_lstm_set_spin(~0u)): fail without polling
+    if (lane == 0) {
+      atomicOr(ctl, 1u);
+      if (fault) atomicOr(fault, 1u);
+    }
+    return false;
+  }
   while (true) {
     bool ok = true;
     if (lane < NR) ok = __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= tag;
@@ -869,6 +876,13 @@ __device__ __forceinline__ bool sweep_group(__amdgpu_buffer_rsrc_t pay, int row0
   bool ok[NCH];
 #pragma unroll
   for (int i = 0; i < NCH; ++i) ok[i] = (tid + NT * (I0 + i)) / CPR >= rows;
+  if (spin == 0) {  // injected timeout (avc_lstm_set_spin(~0u)): fail without reading
+    if ((threadIdx.x & 63) == 0) {
+      atomicOr(ctl, 1u);
+      if (fault) atomicOr(fault, 1u);
+    }
+    return false;
+  }
   for (unsigned spins = 0;; ++spins) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
@@ -1508,6 +1522,7 @@ unsigned spin_bound() {
     return v ? (unsigned)strtoul(v, nullptr, 10) : 0u;
   }();
   const unsigned s = g_spin.load(std::memory_order_relaxed);
+  if (s == ~0u) return 0;  // injected timeout: every wait fails at once (fault-path tests)
   return s ? s : env ? env : PSPIN;
 }
 

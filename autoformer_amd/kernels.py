@@ -334,8 +334,9 @@ def clear_faults(device=None):
 
 
 def lstm_set_spin(spins: int) -> None:
-    """Debug: spin bound of the persistent recurrences (0 restores the default)."""
-    L.call("avc_lstm_set_spin", int(spins))
+    """Debug: spin bound of the persistent recurrences (0 restores the default; -1 injects a
+    timeout at every wait, deterministically)."""
+    L.call("avc_lstm_set_spin", int(spins) & 0xFFFFFFFF)
 
 
 def lstm_fwd(xproj, w_hh, B, T, H, dirs, hbuf=None):

@@ -252,7 +252,9 @@ int avc_lstm_trace(void* buf);
 int avc_set_fault_word(void* word);
 
 /* Debug: spin bound of the persistent recurrences' waits (0 = the built-in bound, or the
- * AVC_LSTM_SPIN environment variable when set).  A tiny bound forces the timeout path. */
+ * AVC_LSTM_SPIN environment variable when set).  ~0u injects a timeout: every wait fails at
+ * once, deterministically (the fault-path tests); a small bound only times out the waits that
+ * do not succeed within it. */
 int avc_lstm_set_spin(unsigned spins);
 
 /* 1 when avc_lstm_fwd (backward = 0) / avc_lstm_bwd (backward = 1) take the one-launch

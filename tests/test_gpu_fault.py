@@ -47,7 +47,7 @@ def test_forced_spin_timeout_raises_at_loss_read():
         K.clear_faults()
         ts.step(x, e)
         ts.check()  # healthy step: no fault
-        K.lstm_set_spin(1)  # every wait that does not succeed at once times out
+        K.lstm_set_spin(-1)  # injected: every wait of the persistent recurrences times out
         ts.step(x, e)
         with pytest.raises(K.DeviceFault, match="spin timeout"):
             ts.check()
@@ -81,7 +81,7 @@ def test_solver_raises_on_fault():
     s = Solver([(torch.from_numpy(x), torch.from_numpy(e))], Cfg())
     try:
         K.clear_faults()
-        K.lstm_set_spin(1)
+        K.lstm_set_spin(-1)
         with pytest.raises(K.DeviceFault):
             s.train()
     finally:
