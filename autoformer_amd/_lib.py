@@ -236,8 +236,16 @@ def check(rc: int, what: str = "") -> None:
         raise RuntimeError(f"libautovc_hip {what} failed ({rc}): {msg}")
 
 
+_FNS = {}  # name -> bound ctypes function (one dict lookup per launch instead of lib() + getattr)
+
+
 def call(name: str, *args) -> None:
-    check(getattr(lib(), name)(*args), name)
+    fn = _FNS.get(name)
+    if fn is None:
+        fn = _FNS[name] = getattr(lib(), name)
+    rc = fn(*args)
+    if rc != 0:
+        check(rc, name)
 
 
 def exported_symbols():
