@@ -141,6 +141,7 @@ __global__ void bn_apply_kernel(const TY* __restrict__ y, const float* __restric
   st4(out, out16, e, o);
 }
 
+
 template <typename TY>
 __global__ void bn_apply1_kernel(const TY* __restrict__ y, const float* __restrict__ scale,
                                  const float* __restrict__ shift, const float* __restrict__ res, float* __restrict__ out,
@@ -156,11 +157,50 @@ __global__ void bn_apply1_kernel(const TY* __restrict__ y, const float* __restri
 
 // Backward finalize of one 64-channel strip by one 256-thread block (4 row groups reduce the
 // per-row-block partials in parallel): apply coefficients + dgamma / dbeta / conv-bias gradient.
-// standalone finalize (no counter pool): one block per strip
-__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ ws, int nrb, int M, int C,
-                                                              BwdFin f) {
-  __shared__ float red[3 * FG * 64];
-  bwd_finalize_cols<false>(ws, nrb, M, C, blockIdx.x * 64, 64, f, red);
+// Backward finalize, stand-alone: 16 channels x 16 row groups per block (32 blocks at C = 512, 8
+// partial rows per thread at 128 row blocks).  The 64-channel x 4-group form of the GEMM epilogue
+// (bwd_finalize_cols) as its own launch ran 8 blocks x 32 rows per thread in 9.9 us per call
+// beside the side stream's GEMMs, this one 6.0 us (profiles/r3_bn_bwd_forms_ab.txt)
+__global__ void __launch_bounds__(256) bn_bwd_finalize16_kernel(const float* __restrict__ ws, int nrb, int M, int C,
+                                                                BwdFin f) {
+  __shared__ float red[3][16][17];
+  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+  if (c < C)
+    for (int b0 = grp; b0 < nrb; b0 += 16 * 8) {
+      float x[8][3];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = b0 + 16 * u;
+        const float* p = ws + ((long long)(b < nrb ? b : 0) * C + c) * 3;
+#pragma unroll
+        for (int v = 0; v < 3; ++v) x[u][v] = b < nrb ? p[v] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s0 += x[u][0];
+        s1 += x[u][1];
+        s2 += x[u][2];
+      }
+    }
+  red[0][grp][cl] = s0;
+  red[1][grp][cl] = s1;
+  red[2][grp][cl] = s2;
+  __syncthreads();
+  if (threadIdx.x >= 16 || c >= C) return;
+  float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    t0 += red[0][i][cl];
+    t1 += red[1][i][cl];
+    t2 += red[2][i][cl];
+  }
+  bwd_finalize_store(c, t0, t1, t2, M, C, f);
+}
+
+void launch_bwd_finalize(const float* ws, int nrb, int M, int C, const BwdFin& f, hipStream_t s) {
+  bn_bwd_finalize16_kernel<<<cdiv(C, 16), 256, 0, s>>>(ws, nrb, M, C, f);
 }
 
 // backward reduce: per (64-row block, 64 channels) partial sums of dz, dz*yhat, yhat.
@@ -287,18 +327,22 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce1_kernel(const TD* __restric
 }
 
 
-template <bool FROM_PRE, typename TD, typename TY>
-__global__ void bn_bwd_apply_kernel(const TD* __restrict__ dA, const float* __restrict__ a,
-                                    const TY* __restrict__ y, const float* __restrict__ coef, long long total4,
-                                    int C, int act, float* __restrict__ dy, bf16* __restrict__ dy16) {
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total4) return;
-  long long e = i * 4;
-  int c = (int)(e % C);
-  f32x4 g = ld4(dA + e);
-  f32x4 av = {0.f, 0.f, 0.f, 0.f};
-  if (!FROM_PRE) av = ld4(a + e);
-  f32x4 yv = ld4(y + e);
+// Row-strip form of the backward apply pass: a 256-thread block = 64 channel quads (a 256-channel
+// strip) x 4 row lanes, each lane RPT rows, so the six planar per-channel constants are loaded
+// once per RPT rows instead of once per 4 elements (the one-quad-per-thread form spends six 16-B
+// constant loads per 8-B element load).  All RPT rows' loads are issued before any is used.
+// RPT 4 measured best (10.9-11.1 us per 8192 x 512 bf16 call against 13.6 for the one-quad form;
+// RPT 8 no better in the step, profiles/r3_bn_bwd_forms_ab.txt).  The forward apply, two
+// constants per quad, measured slower in this form (8.6 vs 6.1 us at RPT 8: fewer waves in
+// flight) and keeps the one-quad form.
+template <int RPT, bool FROM_PRE, typename TD, typename TY>
+__global__ void __launch_bounds__(256) bn_bwd_apply_rows_kernel(const TD* __restrict__ dA, const float* __restrict__ a,
+                                                                const TY* __restrict__ y,
+                                                                const float* __restrict__ coef, int M, int C, int act,
+                                                                float* __restrict__ dy, bf16* __restrict__ dy16) {
+  const int c = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
+  if (c >= C) return;
+  const int r0 = blockIdx.y * 4 * RPT + (threadIdx.x >> 6);
   const f32x4 k1 = *reinterpret_cast<const f32x4*>(coef + c);
   const f32x4 m1 = *reinterpret_cast<const f32x4*>(coef + C + c);
   const f32x4 m2 = *reinterpret_cast<const f32x4*>(coef + 2 * C + c);
@@ -306,14 +350,36 @@ __global__ void bn_bwd_apply_kernel(const TD* __restrict__ dA, const float* __re
   const f32x4 rs = *reinterpret_cast<const f32x4*>(coef + 4 * C + c);
   f32x4 bt = {0.f, 0.f, 0.f, 0.f};
   if (FROM_PRE) bt = *reinterpret_cast<const f32x4*>(coef + 5 * C + c);
-  f32x4 o;
+  f32x4 g[RPT], yv[RPT], av[RPT];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float yc = yv[k] - mu[k];
-    const float dz = FROM_PRE ? act_bwd_from_pre(g[k], yc * k1[k] + bt[k], act) : act_bwd_from_out(g[k], av[k], act);
-    o[k] = k1[k] * (dz - m1[k] - yc * rs[k] * m2[k]);
+  for (int i = 0; i < RPT; ++i) {
+    const int r = r0 + 4 * i;
+    const long long e = (long long)(r < M ? r : 0) * C + c;
+    g[i] = ld4(dA + e);
+    yv[i] = ld4(y + e);
+    if (!FROM_PRE) av[i] = ld4(a + e);
   }
-  st4(dy, dy16, e, o);
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = r0 + 4 * i;
+    if (r >= M) break;
+    f32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float yc = yv[i][k] - mu[k];
+      const float dz = FROM_PRE ? act_bwd_from_pre(g[i][k], yc * k1[k] + bt[k], act)
+                                : act_bwd_from_out(g[i][k], av[i][k], act);
+      o[k] = k1[k] * (dz - m1[k] - yc * rs[k] * m2[k]);
+    }
+    st4(dy, dy16, (long long)r * C + c, o);
+  }
+}
+
+template <bool FROM_PRE, typename TD, typename TY>
+void launch_bwd_apply_rows(const TD* dp, const float* a, const TY* yp, const float* coef, int M, int C, int act,
+                           float* dy, bf16* d16, hipStream_t s) {
+  bn_bwd_apply_rows_kernel<4, FROM_PRE, TD, TY><<<dim3(cdiv(C / 4, 64), cdiv(M, 16)), 256, 0, s>>>(dp, a, yp, coef, M,
+                                                                                                C, act, dy, d16);
 }
 
 template <bool FROM_PRE, typename TD, typename TY>
@@ -525,12 +591,10 @@ extern "C" int avc_bn_bwd(const void* dA, int dA_dtype, const float* a, const vo
         if (pre) bn_bwd_reduce1_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws);
         else bn_bwd_reduce1_kernel<false, TD, TY><<<grid, 256, 0, s>>>(dp, a, yp, mean, rstd, gamma, beta, M, C, act, ws);
       }
-      bn_bwd_finalize_kernel<<<cdiv(C, 64), 256, 0, s>>>(ws, nrb, M, C, fin);
+      launch_bwd_finalize(ws, nrb, M, C, fin, s);
       if (v4) {
-        if (pre)
-          bn_bwd_apply_kernel<true, TD, TY><<<cdiv(total / 4, 256), 256, 0, s>>>(dp, a, yp, coef, total / 4, C, act, dy, d16);
-        else
-          bn_bwd_apply_kernel<false, TD, TY><<<cdiv(total / 4, 256), 256, 0, s>>>(dp, a, yp, coef, total / 4, C, act, dy, d16);
+        if (pre) launch_bwd_apply_rows<true>(dp, a, yp, coef, M, C, act, dy, d16, s);
+        else launch_bwd_apply_rows<false>(dp, a, yp, coef, M, C, act, dy, d16, s);
       } else {
         if (pre)
           bn_bwd_apply1_kernel<true, TD, TY><<<cdiv(total, 256), 256, 0, s>>>(dp, a, yp, coef, total, C, act, dy, d16);
@@ -561,7 +625,7 @@ int avcbn::bn_bwd_reduce_finalize(const void* dA, int dA_dtype, const void* y, i
       else
         bn_bwd_reduce1_kernel<true, TD, TY><<<grid, 256, 0, s>>>(dp, nullptr, yp, fin.mean, fin.rstd, fin.gamma,
                                                                  fin.beta, M, C, act, ws);
-      bn_bwd_finalize_kernel<<<cdiv(C, 64), 256, 0, s>>>(ws, nrb, M, C, fin);
+      launch_bwd_finalize(ws, nrb, M, C, fin, s);
     });
   });
   return avc_check_launch("bn_bwd_reduce_finalize");
@@ -585,8 +649,7 @@ extern "C" int avc_bn_bwd_apply(const void* dA, int dA_dtype, const void* y, int
       const TD* dp = static_cast<const TD*>(dA);
       const TY* yp = static_cast<const TY*>(y);
       if (v4)
-        bn_bwd_apply_kernel<true, TD, TY><<<cdiv(total / 4, 256), 256, 0, s>>>(dp, nullptr, yp, coef, total / 4, C,
-                                                                              act, dy, d16);
+        launch_bwd_apply_rows<true>(dp, static_cast<const float*>(nullptr), yp, coef, M, C, act, dy, d16, s);
       else
         bn_bwd_apply1_kernel<true, TD, TY><<<cdiv(total, 256), 256, 0, s>>>(dp, nullptr, yp, coef, total, C, act, dy,
                                                                            d16);

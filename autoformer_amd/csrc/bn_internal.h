@@ -44,6 +44,28 @@ struct BwdFin {
   int acc;
 };
 
+// Channel c's apply constants (planar coef[6][C]) and parameter gradients from its three column
+// sums over all rows: s0 = sum dz, s1 = sum dz*yhat, s2 = sum yhat.
+__device__ __forceinline__ void bwd_finalize_store(int c, float s0, float s1, float s2, int M, int C, const BwdFin& f) {
+  const float g = f.gamma ? f.gamma[c] : 1.f;
+  const float rs = f.rstd[c], mu = f.mean[c];
+  const float k1 = g * rs;
+  const float invn = 1.f / (float)M;
+  const float m1 = s0 * invn, m2 = s1 * invn;
+  // planar per-channel constants of the apply pass (one 16-B load per plane per 4 channels):
+  //   yhat = (y - mu)*rs,  z = (y - mu)*k1 + beta,  dy = k1*(dz - m1 - yhat*m2)
+  f.coef[c] = k1;
+  f.coef[C + c] = m1;
+  f.coef[2 * C + c] = m2;
+  f.coef[3 * C + c] = mu;
+  f.coef[4 * C + c] = rs;
+  f.coef[5 * C + c] = f.beta ? f.beta[c] : 0.f;
+  const float gb = -k1 * s1 * s2 * invn;
+  if (f.dgamma) f.dgamma[c] = f.acc ? f.dgamma[c] + s1 : s1;
+  if (f.dbeta) f.dbeta[c] = f.acc ? f.dbeta[c] + s0 : s0;
+  if (f.dbias) f.dbias[c] = f.acc ? f.dbias[c] + gb : gb;
+}
+
 // BatchNorm backward finalize of channels c0 .. c0+nc-1 (nc <= 64) from per-row-block partials
 // ws[(b*C + c)*3 + {0,1,2}] = (sum dz, sum dz*yhat, sum yhat), b < nrb: the planar apply
 // constants coef[6][C] and the parameter gradients.  256 threads (64 channels x FG row
@@ -69,23 +91,7 @@ __device__ __forceinline__ void bwd_finalize_cols(const float* ws, int nrb, int 
     s1 += red[(1 * FG + i) * 64 + cl];
     s2 += red[(2 * FG + i) * 64 + cl];
   }
-  const float g = f.gamma ? f.gamma[c] : 1.f;
-  const float rs = f.rstd[c], mu = f.mean[c];
-  const float k1 = g * rs;
-  const float invn = 1.f / (float)M;
-  const float m1 = s0 * invn, m2 = s1 * invn;
-  // planar per-channel constants of the apply pass (one 16-B load per plane per 4 channels):
-  //   yhat = (y - mu)*rs,  z = (y - mu)*k1 + beta,  dy = k1*(dz - m1 - yhat*m2)
-  f.coef[c] = k1;
-  f.coef[C + c] = m1;
-  f.coef[2 * C + c] = m2;
-  f.coef[3 * C + c] = mu;
-  f.coef[4 * C + c] = rs;
-  f.coef[5 * C + c] = f.beta ? f.beta[c] : 0.f;
-  const float gb = -k1 * s1 * s2 * invn;
-  if (f.dgamma) f.dgamma[c] = f.acc ? f.dgamma[c] + s1 : s1;
-  if (f.dbeta) f.dbeta[c] = f.acc ? f.dbeta[c] + s0 : s0;
-  if (f.dbias) f.dbias[c] = f.acc ? f.dbias[c] + gb : gb;
+  bwd_finalize_store(c, s0, s1, s2, M, C, f);
 }
 
 // The same reduction as a stand-alone pass over (dA, y) (bn.hip reduce kernels + finalize):
