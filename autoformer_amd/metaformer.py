@@ -13,11 +13,31 @@ References:
 """
 from __future__ import annotations
 
+import contextlib
+import os
+
 import torch
 
 from . import kernels as K
 from . import layers as Lyr
 from .kernels import operand
+
+
+# gradient-sink mode: the mixer's weight-gradient products (both operands K-strided, compute-bound)
+# run on the side stream beside the memory-bound data-gradient chain (LayerNorm, GELU, transposes,
+# pads) instead of in line with it (AVC_MIX_SIDE=0: in line, A/B)
+_MIX_SIDE = os.environ.get("AVC_MIX_SIDE", "1") != "0"
+
+
+def _wside(on, *keep):
+    """Context for a weight-gradient product: the side stream (after everything queued so far,
+    `keep` alive until join_side) when `on`, else the current stream.  Operand twins must exist
+    before entering: a twin made inside would be written on the side stream and read on this one."""
+    if not on:
+        return contextlib.nullcontext()
+    sd = Lyr._Side()
+    sd.keep(*keep)
+    return sd
 
 
 def _sink(p):
@@ -182,24 +202,25 @@ def _pad8(n):
 
 
 def _token_mix_weights(mix, w1, w2, NP):
-    """(W1^T, W2) as (NPp x 4NPp) zero-padded matrices in the compute dtype, NPp = NP rounded
-    up to a multiple of 8 (121 -> 128, 1849 -> 1856 patches), rebuilt when w1 / w2 change.
-    The padding makes every token-mixing operand 8-aligned in K and in its row stride, which
-    the bf16 LDS-DMA GEMM kernels need; padded rows / columns are zero, so the products over
-    them add nothing."""
+    """(W1^T, W2) as (NPp x 4NPp) and (W1, W2^T) as (4NPp x NPp) zero-padded matrices in the
+    compute dtype, NPp = NP rounded up to a multiple of 8 (121 -> 128, 1849 -> 1856 patches),
+    rebuilt when w1 / w2 change.  The padding makes every token-mixing operand 8-aligned in K and
+    in its row stride, which the bf16 LDS-DMA GEMM kernels need; padded rows / columns are zero,
+    so the products over them add nothing.  The (4NPp x NPp) forms are the K-contiguous B
+    operands of the per-utterance products UT_b = Y1T_b W1^T (forward) and dUT_b = dRT_b W2
+    (backward), so both run on the NT kernel against the transposed activations the step
+    already holds, instead of the TT kernel over two K-strided operands."""
     def build():
         dt = K.compute()
         NPp = _pad8(NP)
         w1t = K.pad_cols(K.transpose(w1.view(4 * NP, NP), K.F32), 4 * NPp)   # (NP, 4NPp)
         w2p = K.pad_cols(w2.view(NP, 4 * NP), 4 * NPp)                         # (NP, 4NPp)
         rows = lambda t: K.pad_cols(t.view(1, NP * 4 * NPp), NPp * 4 * NPp, dtype=dt).view(NPp, 4 * NPp)  # noqa: E731
-        return rows(w1t), rows(w2p)
+        w1n = K.pad_cols(w1.view(4 * NP, NP), NPp)                             # (4NP, NPp)
+        w2t = K.pad_cols(K.transpose(w2.view(NP, 4 * NP), K.F32), NPp)        # (4NP, NPp)
+        rows4 = lambda t: K.pad_cols(t.view(1, 4 * NP * NPp), 4 * NPp * NPp, dtype=dt).view(4 * NPp, NPp)  # noqa: E731
+        return rows(w1t), rows(w2p), rows4(w1n), rows4(w2t)
     return mix.tm_cache.get([w1, w2], build)
-
-
-def _pad_rows(x, B, NP, D, NPp):
-    """Frame-major (B*NP, D) -> (B*NPp, D) in the compute dtype, zero rows appended per utterance."""
-    return K.pad_cols(x.view(B, NP * D), NPp * D, dtype=K.compute()).view(B * NPp, D)
 
 
 def _cf_weights(mix, we, w3, w4):
@@ -272,19 +293,18 @@ class _MLPMixerFn(torch.autograd.Function):
         weC, w3C, w4C = _cf_weights(mix, we, w3, w4)
         Z = _lin(P, B * NP, D, ps * ps, weC, be)                # (B*NP, D)
         Y1, m1, r1 = K.layer_norm_fwd(Z, g1, b1n, mix.ln_eps[0])
-        # token mixing: UT_b (D x 4NP) = Y1_b^T . W1^T + b1   (Conv1d(NP -> 4NP, k1) on (B, NP, D)).
-        # NP (121 / 1849 patches) is never the contiguous dimension of a GEMM operand: W1 is
-        # used as its transpose W1T (NP x 4NP), so every product takes the vectorised kernels.
+        # token mixing: UT_b (D x 4NP) = Y1_b^T . W1^T + b1   (Conv1d(NP -> 4NP, k1) on (B, NP, D)),
+        # as an NT product of the per-utterance transpose Y1T_b (D x NPp) and W1 (4NPp x NPp).
         # Patch counts are zero-padded to NPp (_token_mix_weights): UT / V carry 4NPp columns
-        # (padded ones stay 0: zero weights, zero bias, GELU(0) = 0), Y1 gets NPp rows.
-        W1T, W2c = _token_mix_weights(mix, w1, w2, NP)
+        # (padded ones stay 0: zero weights, zero bias, GELU(0) = 0).
+        W1T, W2c, W1n, _ = _token_mix_weights(mix, w1, w2, NP)
         NPp = W1T.shape[0]
-        # Y1^T per utterance, (B*D, NPp): the K = B*D operand of the dW1 product (backward)
+        # Y1^T per utterance, (B*D, NPp): the K-contiguous A operand of UT_b = Y1T_b W1^T here and
+        # the K = B*D operand of the dW1 product (backward)
         Y1T = K.pad_cols(K.transpose_batched(Y1, B, NP, D).view(B * D, NP), NPp, dtype=K.compute())
-        Y1 = _pad_rows(Y1, B, NP, D, NPp)
         bb1p = K.pad_cols(bb1.view(1, 4 * NP), 4 * NPp).view(-1)
-        UT, V = _gelu_gemm(D, 4 * NPp, NPp, operand(Y1, D, kstrided=True, batch_stride=NPp * D),
-                           operand(W1T, 4 * NPp, kstrided=True), bb1p, dev, batch=B)
+        UT, V = _gelu_gemm(D, 4 * NPp, NPp, operand(Y1T, NPp, batch_stride=D * NPp), operand(W1n, NPp), bb1p, dev,
+                           batch=B)
         RT = torch.empty(B * D, NP, device=dev)
         K.gemm(D, NP, 4 * NPp, operand(V, 4 * NPp, batch_stride=D * 4 * NPp), operand(W2c, 4 * NPp), RT, bias=bb2,
                batch=B, c_batch_stride=D * NP)
@@ -324,25 +344,30 @@ class _MLPMixerFn(torch.autograd.Function):
         # zero-padded products) and the function returns None for the parameters -- no autograd
         # accumulation pass per parameter
         sink = Lyr.sink_on()
-        if NPp != NP:
-            dwc = Lyr.conv_wgrad(K.twin(dout), Z2T, B, D, D, wp, pad)
-            dwc = (K.crop_add(dwc.view(O, NPp * Kw), _sink(wc).view(O, NP * Kw)) if sink
-                   else K.pad_cols(dwc.view(O, NPp * Kw), NP * Kw).view(O, NP, Kw))
-        else:
-            dwc = Lyr.conv_wgrad(K.twin(dout), Z2T, B, D, D, wp, pad, into=_sink(wc))
+        side = sink and _MIX_SIDE and Lyr.side_stream() is not None
+        dout16 = K.twin(dout)
+        with _wside(side, dout, dout16, Z2T, wp):
+            if NPp != NP:
+                dwc = Lyr.conv_wgrad(dout16, Z2T, B, D, D, wp, pad)
+                dwc = (K.crop_add(dwc.view(O, NPp * Kw), _sink(wc).view(O, NP * Kw)) if sink
+                       else K.pad_cols(dwc.view(O, NPp * Kw), NP * Kw).view(O, NP, Kw))
+            else:
+                dwc = Lyr.conv_wgrad(dout16, Z2T, B, D, D, wp, pad, into=_sink(wc))
         dbc = K.colsum(dout, B * D, wc.shape[0], out=_sink(bc), accumulate=sink)
         dZ2T = Lyr.conv_dgrad(dout, B, D, D, wp, pad, Wd, n_dx=NP)
         dZ2 = K.twin(K.transpose_batched(dZ2T, B, D, NP).view(B * NP, D))
         M = B * NP
         # channel FF: Z2 = GELU(LN2(Z1) W3^T + b3) W4^T + b4 + Z1
         dw4 = _sink(w4) if sink else torch.empty_like(w4)
-        K.gemm(D, 4 * D, M, operand(dZ2, D, kstrided=True), operand(V2, 4 * D, kstrided=True), dw4,
-               split_k=K.auto_split_k(D, 4 * D, M), accumulate=sink)
+        with _wside(side, dZ2, V2):
+            K.gemm(D, 4 * D, M, operand(dZ2, D, kstrided=True), operand(V2, 4 * D, kstrided=True), dw4,
+                   split_k=K.auto_split_k(D, 4 * D, M), accumulate=sink)
         dbb4 = K.colsum(dZ2, M, D, out=_sink(bb4), accumulate=sink)
         dU2 = _dgelu_gemm(M, 4 * D, D, operand(dZ2, D), operand(w4C, 4 * D, kstrided=True), U2, dev)
         dw3 = _sink(w3) if sink else torch.empty_like(w3)
-        K.gemm(4 * D, D, M, operand(dU2, 4 * D, kstrided=True), operand(Y2, D, kstrided=True), dw3,
-               split_k=K.auto_split_k(4 * D, D, M), accumulate=sink)
+        with _wside(side, dU2, Y2):
+            K.gemm(4 * D, D, M, operand(dU2, 4 * D, kstrided=True), operand(Y2, D, kstrided=True), dw3,
+                   split_k=K.auto_split_k(4 * D, D, M), accumulate=sink)
         dbb3 = K.colsum(dU2, M, 4 * D, out=_sink(bb3), accumulate=sink)
         dY2 = torch.empty(M, D, device=dev)
         K.gemm(M, D, 4 * D, operand(dU2, 4 * D), operand(w3C, D, kstrided=True), dY2)
@@ -350,25 +375,26 @@ class _MLPMixerFn(torch.autograd.Function):
         dZ1 = K.add(dZ2, K.layer_norm_bwd(dY2, Z1, g2, m2, r2, dg2, db2n, accumulate=sink))
         # token FF: Z1 = Z + (GELU(Y1^T W1^T + b1) W2^T + b2)^T   per utterance.  dRT_b = dZ1_b^T is
         # read in place from dZ1 (as the transposed operand), so NP is never a contiguous dimension.
-        W1T, W2c = _token_mix_weights(mix, w1, w2, NP)
+        W1T, W2c, _, W2t = _token_mix_weights(mix, w1, w2, NP)
         NPp = W1T.shape[0]
-        dZ1p = _pad_rows(dZ1, B, NP, D, NPp)
         # Token-mixing weight gradients sum over utterances AND the D positions: with the
         # per-utterance transposes (B*D rows) that sum is the K dimension of ONE product
         # (K = B*D, both operands K-strided), with no per-utterance slabs to reduce.
         dRT = K.transpose_batched(dZ1, B, NP, D).view(B * D, NP)
         dbb2 = K.colsum(dRT, B * D, NP, out=_sink(bb2), accumulate=sink)
         dRTp = K.pad_cols(dRT, NPp, dtype=K.compute())
-        dW2p = torch.empty(NPp, 4 * NPp, device=dev)
-        K.gemm(NPp, 4 * NPp, B * D, operand(dRTp, NPp, kstrided=True), operand(V, 4 * NPp, kstrided=True), dW2p,
-               split_k=K.auto_split_k(NPp, 4 * NPp, B * D))
-        dW2 = K.crop_add(dW2p[:NP], _sink(w2).view(NP, 4 * NP)) if sink else K.pad_cols(dW2p, 4 * NP)[:NP]
-        dUT = _dgelu_gemm(D, 4 * NPp, NPp, operand(dZ1p, D, kstrided=True, batch_stride=NPp * D),
-                          operand(W2c, 4 * NPp, kstrided=True), UT, dev, batch=B)
-        dW1p = torch.empty(4 * NPp, NPp, device=dev)
-        K.gemm(4 * NPp, NPp, B * D, operand(dUT, 4 * NPp, kstrided=True), operand(Y1T, NPp, kstrided=True), dW1p,
-               split_k=K.auto_split_k(4 * NPp, NPp, B * D))
-        dW1 = K.crop_add(dW1p[:4 * NP], _sink(w1).view(4 * NP, NP)) if sink else K.pad_cols(dW1p, NP)[:4 * NP]
+        with _wside(side, dRTp, V):
+            dW2p = torch.empty(NPp, 4 * NPp, device=dev)
+            K.gemm(NPp, 4 * NPp, B * D, operand(dRTp, NPp, kstrided=True), operand(V, 4 * NPp, kstrided=True), dW2p,
+                   split_k=K.auto_split_k(NPp, 4 * NPp, B * D))
+            dW2 = K.crop_add(dW2p[:NP], _sink(w2).view(NP, 4 * NP)) if sink else K.pad_cols(dW2p, 4 * NP)[:NP]
+        dUT = _dgelu_gemm(D, 4 * NPp, NPp, operand(dRTp, NPp, batch_stride=D * NPp), operand(W2t, NPp), UT, dev,
+                          batch=B)
+        with _wside(side, dUT, Y1T):
+            dW1p = torch.empty(4 * NPp, NPp, device=dev)
+            K.gemm(4 * NPp, NPp, B * D, operand(dUT, 4 * NPp, kstrided=True), operand(Y1T, NPp, kstrided=True),
+                   dW1p, split_k=K.auto_split_k(4 * NPp, NPp, B * D))
+            dW1 = K.crop_add(dW1p[:4 * NP], _sink(w1).view(4 * NP, NP)) if sink else K.pad_cols(dW1p, NP)[:4 * NP]
         dbb1 = K.colsum(dUT, B * D, 4 * NP, ld=4 * NPp, out=_sink(bb1), accumulate=sink)
         dY1T = torch.empty(B * D, NP, device=dev)
         K.gemm(B * D, NP, 4 * NPp, operand(dUT, 4 * NPp), operand(W1T, 4 * NPp), dY1T)
@@ -378,8 +404,9 @@ class _MLPMixerFn(torch.autograd.Function):
         # patch embedding
         pp = ps * ps
         dwe = _sink(we) if sink else torch.empty_like(we)
-        K.gemm(D, pp, M, operand(dZ, D, kstrided=True), operand(P, pp, kstrided=True), dwe,
-               split_k=K.auto_split_k(D, pp, M), accumulate=sink)
+        with _wside(side, dZ, P):
+            K.gemm(D, pp, M, operand(dZ, D, kstrided=True), operand(P, pp, kstrided=True), dwe,
+                   split_k=K.auto_split_k(D, pp, M), accumulate=sink)
         dbe = K.colsum(dZ, M, D, out=_sink(be), accumulate=sink)
         dnf = None
         if ctx.needs_input_grad[0]:
