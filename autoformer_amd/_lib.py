@@ -16,8 +16,8 @@ import torch  # noqa: F401  (must precede the HIP library)
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "graph.hip", "fold.hip", "disc.hip"]
-ABI_VERSION = 16
+SOURCES = ["gemm_ring.hip", "gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "graph.hip", "fold.hip", "disc.hip"]
+ABI_VERSION = 17
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -86,17 +86,13 @@ _SIGS = {
     "avc_lstm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                              c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "avc_lstm_bwd_scratch_bytes": (c_size, [c_int, c_int, c_int]),
-    "avc_capture_deps": (c_int, [c_void_p, ctypes.POINTER(c_void_p), c_int]),
-    "avc_graph_split": (c_int, [c_void_p, ctypes.POINTER(c_void_p), c_int, ctypes.POINTER(c_void_p), c_int, c_int,
-                                ctypes.POINTER(c_void_p), ctypes.POINTER(c_int)]),
-    "avc_graph_launch2": (c_int, [c_void_p, c_void_p, c_void_p]),
-    "avc_graph_split_destroy": (c_int, [c_void_p]),
     "avc_lstm2_persistent": (c_int, [c_int, c_int, c_int, c_int]),
     "avc_lstm2_scratch_bytes": (c_size, [c_int, c_int]),
     "avc_lstm2_fwd": (c_int, [c_void_p] * 5 + [c_int] * 3 + [c_void_p] * 10),
     "avc_lstm_trace": (c_int, [c_void_p]),
     "avc_set_fault_word": (c_int, [c_void_p]),
     "avc_lstm_set_spin": (c_int, [ctypes.c_uint]),
+    "avc_gemm_set_ring": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "avc_lstm_persistent": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "avc_enc_concat": (c_int, [c_void_p, c_ll, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_codes_gather": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),

@@ -730,6 +730,17 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
   g.split_k = d->split_k > 1 ? d->split_k : 1;
   if (make_op(d->a, d->M, d->K, g.a, "A")) return -1;
   if (make_op(d->b, d->N, d->K, g.b, "B")) return -1;
+  // A batch of products that share B (no B batch stride) with contiguous A and C batches is ONE
+  // product of batch*M rows: one tile grid without a per-batch row-tile remainder (the MetaConv
+  // token-mixing products, 64 x 344 rows: 3 x 128-row tiles per utterance -> 172 for all)
+  if (g.batch > 1 && g.split_k == 1 && !d->a.kstrided && !g.a.win && d->b.batch_stride == 0 && d->ldc > 0 &&
+      d->a.batch_stride == (long long)d->M * d->a.ld && d->c_batch_stride == (long long)d->M * d->ldc &&
+      (long long)d->M * g.batch < (1ll << 30)) {
+    g.M = d->M * g.batch;
+    g.a.rows = g.M;
+    g.a.bstride = 0;
+    g.batch = 1;
+  }
   int kl = (d->K + g.split_k - 1) / g.split_k;
   kl = ((kl + BK - 1) / BK) * BK;
   g.klen = kl > 0 ? kl : BK;
@@ -814,7 +825,8 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
       if (!g.bnb_cnt) return -1;
     }
     const char* what = "avc_gemm(fast)";
-    if (!aks && !bks && gemm_conv_launch(g, s)) what = "avc_gemm(conv)";
+    if (!aks && !bks && gemm_ring_launch(g, s)) what = "avc_gemm(ring)";
+    else if (!aks && !bks && gemm_conv_launch(g, s)) what = "avc_gemm(conv)";
     else if (!aks && !bks && gemm_nt_launch(g, s)) what = "avc_gemm(nt)";
     else if (aks && bks && gemm_tt_launch(g, s)) what = "avc_gemm(tt)";
     else {

@@ -358,5 +358,8 @@ bool gemm_nt_launch(const GemmArgs& g, hipStream_t s);
 bool gemm_conv_launch(const GemmArgs& g, hipStream_t s);
 // Entry of the TT (both operands K-strided, bf16) weight-gradient kernel (gemm_tt.hip).
 bool gemm_tt_launch(const GemmArgs& g, hipStream_t s);
+// Entry of the 8-wave deep-ring NT kernel (gemm_ring.hip); false when the shape / operands do
+// not qualify or AVC_RING=0.
+bool gemm_ring_launch(const GemmArgs& g, hipStream_t s);
 
 }  // namespace avcg

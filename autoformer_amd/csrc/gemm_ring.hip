@@ -1,0 +1,466 @@
+// gemm_ring.hip — bf16 NT GEMM with a deep LDS-DMA ring, eight waves, one workgroup per CU.
+//
+// C[M][N] = A[M][K] . B[N][K]^T (fp32 accumulate) for the products whose operands are both
+// K-contiguous: the MetaConv MLP-Mixer token / channel mixing (factory/MLPMixer.py:58-92,
+// factory/MetaConv.py:23-76), the decoder LSTM input projections and data gradients
+// (factory/AutoVC.py:96,103,110), and the Conv1d window stream (factory/Norm.py:21-28: A is the
+// frame window of the conv input, K = tap x channel, zero outside the utterance).
+//
+// Why a new kernel: the 4-wave, two-stage kernels of gemm_nt.hip /
+// gemm_conv.hip keep ONE LDS-DMA fill in flight per workgroup and two workgroups per CU; their
+// times match the ≈25 GB/s-per-CU fill rate of that regime (MI355X_MICROARCH.md
+// "ldsdma-fill"), not the MFMA rate.  Here:
+//   * one 512-thread workgroup per CU, 8 waves as 2 (M) x 4 (N), so every SIMD holds two waves
+//     that cover each other's LDS-read latency (MI355X_MICROARCH.md "Two waves per SIMD");
+//   * a ring of NST K-steps (BK = 64, 128-B LDS rows) with NST-1 K-steps of fills in flight
+//     ACROSS the barrier: a counted `s_waitcnt vmcnt` + raw `s_barrier` per K-step, never
+//     vmcnt(0) inside the loop (cdna_hip_programming.md §5 "Pipelining across barriers");
+//     every wave issues the same number of `global_load_lds_dwordx4` per K-step (the counts
+//     assume it), rows beyond the operand read a 16-B zero granule;
+//   * 128 x 128 (4 slots, 3 in flight), 256 x 128 (3 slots) or 256 x 256 tiles (2 slots; half
+//     the operand bytes per FLOP of a 128 x 128 tile);
+//   * XOR-swizzled 16-B chunks (chunk ^ ((row >> 1) & 7), applied on the SOURCE address, the
+//     LDS image stays lane-linear), conflict-free ds_read_b128 fragment reads;
+//   * XCD-aware bijective block remap, then grouped tile order (GM row tiles per group) so the
+//     workgroups an XCD runs together share A row panels and B column panels in its L2;
+//   * all LDS in ONE __shared__ array (a second __shared__ object can make hipcc drain vmcnt
+//     before every K-step's first ds_read: cdna_hip_programming.md §5 item 4(a)); the
+//     last-arriver flag of the BN finalize lives in that array too.
+// Epilogue: bias, conv0-fold row bias, residual, accumulate / split-K atomics, fp32 C and / or
+// bf16 twin, conv weight-layout permutation, BatchNorm partial statistics per 128-row tile and
+// the finalize by the last-arriving row tile (the semantics of gemm_internal.h:fast_epilogue).
+#include "gemm_internal.h"
+
+namespace avcg {
+namespace {
+
+__device__ __attribute__((aligned(16))) unsigned int g_zero16_rg[4] = {0u, 0u, 0u, 0u};
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
+
+constexpr int RROW = 128;  // bytes per LDS row (64 bf16 of K)
+constexpr int RBK = 64;    // K per ring slot
+constexpr int RNT = 512;   // threads per workgroup
+
+__device__ __forceinline__ void glds16(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)lds, 16, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// R rows x 64 K of one operand per slot: R/64 glds per thread.  Instruction i of wave w covers
+// slot rows (8i + w)*8 .. +8; lane L writes row +(L>>3), 16-B slot L&7, which holds global K
+// chunk (L&7) ^ ((row>>1)&7) = (L&7) ^ ((4*(w&1) + (L>>4)) & 7) for every i.
+template <int R, bool WIN>
+struct RingLoader {
+  static constexpr int NI = R / 64;
+  const bf16* base;
+  long long roff[NI];  // element offset of the row (plain) / of the row's frame (window)
+  int tt[NI];          // window: frame within the utterance
+  bool rok[NI];
+  int kc;              // this lane's K offset inside the 64-wide slot
+  int ld, pad, t_in, chans;
+
+  __device__ __forceinline__ void init(const OpDev& o, int row0, int bz) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    base = reinterpret_cast<const bf16*>(o.ptr) + (long long)bz * o.bstride;
+    kc = 8 * ((lane & 7) ^ ((4 * (w & 1) + (lane >> 4)) & 7));
+    ld = (int)o.ld;
+    pad = o.pad;
+    t_in = o.t_in;
+    chans = o.chans;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int r = row0 + (8 * i + w) * 8 + (lane >> 3);
+      rok[i] = r < o.rows;
+      const int rr = rok[i] ? r : 0;
+      if (WIN) {
+        const int b = (int)fdiv((uint32_t)rr, o.tdiv);
+        tt[i] = rr - b * o.t_out;
+        roff[i] = (long long)(b * o.t_in + tt[i]) * o.ld;
+      } else {
+        tt[i] = 0;
+        roff[i] = (long long)rr * o.ld;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void issue(char* lds, int kbase, int kend, const FastDiv& cdv) {
+    const int w = threadIdx.x >> 6;
+    const int k = kbase + kc;
+    const bool kok = k < kend;
+    int tap = 0, cc = k;
+    if (WIN) {
+      tap = (int)fdiv((uint32_t)k, cdv);
+      cc = k - tap * chans;
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      bool ok = kok && rok[i];
+      long long off;
+      if (WIN) {
+        const int t2 = tt[i] + tap - pad;
+        ok = ok && t2 >= 0 && t2 < t_in;
+        off = roff[i] + (long long)(tap - pad) * ld + cc;
+      } else {
+        off = roff[i] + k;
+      }
+      glds16(ok ? (const void*)(base + off) : (const void*)g_zero16_rg, lds + (8 * i + w) * 8 * RROW);
+    }
+  }
+};
+
+// "last arrival" on a counter with the flag in the kernel's one LDS array (see header)
+__device__ __forceinline__ bool ring_arrive_last(unsigned* cnt, unsigned arrivals, unsigned mine, unsigned* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(cnt, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old + mine == arrivals;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last ? 1u : 0u;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// Epilogue for the 2 x 4 wave layout: wave (wm, wn) owns rows m0 + wm*TWM + i*16 + 4*(lane>>4) + e
+// and columns n0 + wn*TWN + j*16 + (lane&15).
+template <int BM_, int BN_>
+__device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM_ / 32][BN_ / 64], int m0, int n0,
+                                              int bz, int ks, char* smem_raw) {
+  constexpr int TWM = BM_ / 2, TWN = BN_ / 4, MI = TWM / 16, NJ = TWN / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int rbase = m0 + wm * TWM + 4 * (lane >> 4);
+  const int cbase = n0 + wn * TWN + (lane & 15);
+  float* C = g.c ? g.c + (long long)bz * g.cbs : nullptr;
+  bf16* C16 = g.c16 ? g.c16 + (long long)bz * g.cbs : nullptr;
+  if (g.bias && ks == 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = cbase + j * 16;
+      const float bv = col < g.N ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) acc[i][j] += bv;
+    }
+  }
+  if (g.rbias && ks == 0) {
+    const int T = g.rb_t, pad = g.rb_pad, ncls = 2 * pad + 1;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = rbase + i * 16 + e;
+        if (row >= g.M) continue;
+        const int b = (int)fdiv((uint32_t)row, g.rb_div), t = row - b * T;
+        const int cls = t < pad ? t : (t >= T - pad ? 2 * pad - (T - 1 - t) : pad);
+        const float* rp = g.rbias + (long long)(b * ncls + cls) * g.N;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int col = cbase + j * 16;
+          if (col < g.N) acc[i][j][e] += rp[col];
+        }
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = rbase + i * 16 + e;
+      if (row >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int col = cbase + j * 16;
+        if (col >= g.N) continue;
+        const long long o = (long long)row * g.ldc + out_col(g, col);
+        float v = acc[i][j][e];
+        if (g.res && ks == 0) v += g.res[(long long)bz * g.cbs + o];
+        if (g.atomic) {
+          atomicAdd(C + o, v);
+        } else {
+          if (g.accumulate) v += C[o];
+          if (C) C[o] = v;
+          if (C16) C16[o] = (bf16)v;
+        }
+      }
+    }
+  if (g.bn_partial) {
+    // per 128-row statistics tile: column sum and M2 about the tile mean (Chan's form, merged by
+    // the finalize).  Waves w with (w's rows)/128 == h contribute to tile h of this workgroup.
+    constexpr int NH = BM_ / 128;       // statistics tiles per workgroup tile
+    constexpr int WPT = 128 / TWM;      // waves (along M) per statistics tile
+    float* red = reinterpret_cast<float*>(smem_raw);  // [2][BN_] sums, then [2][BN_] M2
+    float* red2 = red + 2 * BN_;
+    unsigned* flag = reinterpret_cast<unsigned*>(red2 + 2 * BN_);
+    const int h = wm / WPT;
+    const int cnt = max(1, min(128, g.M - (m0 + 128 * h)));
+    float s[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t += (rbase + i * 16 + e < g.M) ? acc[i][j][e] : 0.f;
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      s[j] = t;
+    }
+    __syncthreads();  // the main loop's last fragment reads of LDS are done
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) red[wm * BN_ + wn * TWN + j * 16 + lane] = s[j];
+    }
+    __syncthreads();
+    float qv[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int cl = wn * TWN + j * 16 + (lane & 15);
+      float tot = 0.f;
+#pragma unroll
+      for (int w = 0; w < WPT; ++w) tot += red[(h * WPT + w) * BN_ + cl];
+      const float mean = tot / (float)cnt;
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = acc[i][j][e] - mean;
+          t += (rbase + i * 16 + e < g.M) ? d * d : 0.f;
+        }
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      qv[j] = t;
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) red2[wm * BN_ + wn * TWN + j * 16 + lane] = qv[j];
+    }
+    __syncthreads();
+    const int mt0 = m0 / 128;
+    if (tid < NH * BN_) {
+      const int hh = tid / BN_, cl = tid - hh * BN_;
+      const int col = n0 + cl;
+      if (col < g.N && m0 + 128 * hh < g.M) {
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int w = 0; w < WPT; ++w) {
+          s0 += red[(hh * WPT + w) * BN_ + cl];
+          s1 += red2[(hh * WPT + w) * BN_ + cl];
+        }
+        float* p = g.bn_partial + ((long long)(mt0 + hh) * g.N + col) * 2;
+        if (g.bn_cnt) {
+          st_sc1(p, s0);
+          st_sc1(p + 1, s1);
+        } else {
+          p[0] = s0;
+          p[1] = s1;
+        }
+      }
+    }
+    if (g.bn_cnt) {
+      const int ntile = (g.M + 127) / 128;
+      const int mine = min(NH, ntile - mt0);
+      if (ring_arrive_last(g.bn_cnt + n0 / BN_, (unsigned)ntile, (unsigned)mine, flag))
+        bn_finalize_cols<BN_>(g, n0, red);
+    }
+  }
+}
+
+template <int BM_, int BN_, int NST, bool WIN>
+__global__ void __launch_bounds__(RNT, 2) gemm_ring_kernel(GemmArgs g, int gm) {
+  constexpr int TWM = BM_ / 2, TWN = BN_ / 4, MI = TWM / 16, NJ = TWN / 16;
+  constexpr int A_BYTES = BM_ * RROW, STAGE = (BM_ + BN_) * RROW;
+  constexpr int LPT = BM_ / 64 + BN_ / 64;  // glds per thread per K-step
+  constexpr int P = NST - 1;                // K-steps in flight
+  static_assert(NST >= 2 && NST <= 4, "ring depth");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+
+  // XCD-aware bijective remap (blocks b, b+8, ... share an XCD) ...
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  // ... then grouped order: gm row tiles x all column tiles per group, row tile fastest
+  const int nN = (g.N + BN_ - 1) / BN_, nM = (g.M + BM_ - 1) / BM_;
+  const int z = lid / (nN * nM);
+  const int rem = lid - z * nN * nM;
+  const int grp = rem / (gm * nN);
+  const int fm = grp * gm;
+  const int gsz = min(nM - fm, gm);
+  const int wi = rem - grp * gm * nN;
+  const int mt = fm + wi % gsz, nt = wi / gsz;
+  const int m0 = mt * BM_, n0 = nt * BN_;
+  const int bz = z / g.split_k, ks = z - bz * g.split_k;
+  const int kbeg = ks * g.klen;
+  const int kend = min(g.K, kbeg + g.klen);
+  const int nkt = kend > kbeg ? (kend - kbeg + RBK - 1) / RBK : 0;
+
+  RingLoader<BM_, WIN> la;
+  RingLoader<BN_, false> lb;
+  la.init(g.a, m0, bz);
+  lb.init(g.b, n0, bz);
+  const FastDiv cdv = g.a.cdv;
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment reads: row (lane&15) of each 16-row block, logical chunk 4h + (lane>>4) stored at
+  // chunk ^ ((row>>1)&7) = chunk ^ ((lane&15)>>1) (block bases are multiples of 16 rows)
+  const int frow = lane & 15, sw = frow >> 1;
+  const int ch0 = ((lane >> 4) ^ sw) << 4, ch1 = ((4 + (lane >> 4)) ^ sw) << 4;
+  const int aoff = (wm * TWM + frow) * RROW, boff = A_BYTES + (wn * TWN + frow) * RROW;
+
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+    if (p < nkt) {
+      char* st = smem_raw + p * STAGE;
+      la.issue(st, kbeg + p * RBK, kend, cdv);
+      lb.issue(st + A_BYTES, kbeg + p * RBK, kend, cdv);
+    }
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int ahead = min(P - 1, nkt - 1 - kt);  // K-steps allowed to stay in flight
+    if constexpr (P >= 3) {
+      if (ahead >= 2) wait_vm<2 * LPT>();
+      else if (ahead == 1) wait_vm<LPT>();
+      else wait_vm<0>();
+    } else if constexpr (P == 2) {
+      if (ahead >= 1) wait_vm<LPT>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    raw_barrier();
+    if (kt + P < nkt) {
+      char* st = smem_raw + ((kt + P) % NST) * STAGE;
+      la.issue(st, kbeg + (kt + P) * RBK, kend, cdv);
+      lb.issue(st + A_BYTES, kbeg + (kt + P) * RBK, kend, cdv);
+    }
+    const char* st = smem_raw + (kt % NST) * STAGE;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int co = h ? ch1 : ch0;
+      bf16x8 af[MI], bfr[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(st + boff + j * 16 * RROW + co);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(st + aoff + i * 16 * RROW + co);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // every glds retired (the last wait was vmcnt(0)) and every fragment read done
+  ring_epilogue<BM_, BN_>(g, acc, m0, n0, bz, ks, smem_raw);
+}
+
+template <int BM_, int BN_, int NST, bool WIN>
+void launch(const GemmArgs& g, int gm, hipStream_t s) {
+  const size_t lds = (size_t)NST * (BM_ + BN_) * RROW;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ring_kernel<BM_, BN_, NST, WIN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const int nb = ((g.M + BM_ - 1) / BM_) * ((g.N + BN_ - 1) / BN_) * g.batch * g.split_k;
+  gemm_ring_kernel<BM_, BN_, NST, WIN><<<nb, RNT, lds, s>>>(g, gm);
+}
+
+bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+bool operand_ok(const OpDev& o, bool allow_win) {
+  if (o.dtype != AVC_BF16 || !ok16(o.ptr) || o.ld % 8 || o.bstride % 8) return false;
+  if (o.win && (!allow_win || o.chans % 8)) return false;
+  return true;
+}
+
+// AVC_RING = "BM,BN,NST[,GM]" forces a configuration (benchmarking), "0" disables the kernel;
+// AVC_RING_WIN=0 leaves the conv window operands to gemm_conv.hip.  avc_gemm_set_ring() sets the
+// same at run time (A/B tools in one process).
+struct RingCfg {
+  int mode = 0;  // -1 auto, 0 off, 1 forced (off until measured: AVC_RING=-1 turns it on)
+  int bm = 0, bn = 0, nst = 0, gm = 8, win = 1;
+};
+RingCfg init_cfg() {
+  RingCfg r;
+  if (const char* e = getenv("AVC_RING")) {
+    int a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    const int n = sscanf(e, "%d,%d,%d,%d", &a0, &a1, &a2, &a3);
+    if (n >= 1 && a0 <= 0) r.mode = a0 < 0 ? -1 : 0;
+    if (n >= 3) {
+      r.mode = 1;
+      r.bm = a0;
+      r.bn = a1;
+      r.nst = a2;
+    }
+    if (n >= 4 && a3 > 0) r.gm = a3;
+  }
+  if (const char* e = getenv("AVC_RING_WIN")) r.win = e[0] != '0';
+  return r;
+}
+RingCfg g_ring = init_cfg();
+
+}  // namespace
+
+bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
+  const RingCfg& c = g_ring;
+  if (c.mode == 0 || (g.a.win && !c.win)) return false;
+  if (g.K % 8 || g.klen % RBK || g.bnb_ws) return false;
+  if (!operand_ok(g.a, true) || !operand_ok(g.b, false)) return false;
+  const long long units = (long long)g.batch * g.split_k;
+  int bm, bn, nst;
+  if (c.mode == 1) {
+    bm = c.bm;
+    bn = c.bn;
+    nst = c.nst;
+  } else {
+    // one workgroup per CU: the largest tile that still gives every CU a tile
+    const long long t22 = (long long)((g.M + 255) / 256) * ((g.N + 255) / 256) * units;
+    const long long t21 = (long long)((g.M + 255) / 256) * ((g.N + 127) / 128) * units;
+    if (g.N > 128 && t22 >= 256) {
+      bm = 256; bn = 256; nst = 2;
+    } else if (t21 >= 256) {
+      bm = 256; bn = 128; nst = 3;
+    } else {
+      bm = 128; bn = 128; nst = 4;
+    }
+  }
+  const bool win = g.a.win != 0;
+#define RING_CASE(BMV, BNV, NSV)                       \
+  if (bm == BMV && bn == BNV && nst == NSV) {          \
+    if (win) launch<BMV, BNV, NSV, true>(g, c.gm, s);  \
+    else launch<BMV, BNV, NSV, false>(g, c.gm, s);     \
+    return true;                                       \
+  }
+  RING_CASE(256, 256, 2) RING_CASE(256, 128, 3) RING_CASE(128, 128, 4) RING_CASE(128, 128, 3)
+  RING_CASE(128, 256, 3) RING_CASE(256, 128, 2)
+#undef RING_CASE
+  return false;
+}
+
+}  // namespace avcg
+
+// Benchmarking hook (tools/ring_ab.py): mode -1 auto, 0 off, 1 forced (bm, bn, nst); gm row
+// tiles per group (<= 0 keeps it); win 0/1: whether conv window operands take this kernel.
+extern "C" int avc_gemm_set_ring(int mode, int bm, int bn, int nst, int gm, int win) {
+  avcg::g_ring.mode = mode;
+  avcg::g_ring.bm = bm;
+  avcg::g_ring.bn = bn;
+  avcg::g_ring.nst = nst;
+  if (gm > 0) avcg::g_ring.gm = gm;
+  avcg::g_ring.win = win;
+  return 0;
+}

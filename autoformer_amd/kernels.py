@@ -817,40 +817,3 @@ def gelu_bwd_twin(g, x):
     L.call("avc_gelu_twin", g.data_ptr(), x.data_ptr(), dx.data_ptr(), _ptr(d16), x.numel(), 1, stream())
     return attach_twin(dx, d16)
 
-# ------------------------------------------------------------------------- two-graph replay
-def capture_deps(stream):
-    """Capture dependencies (graph node handles) of a capturing stream; [] if it is not capturing."""
-    import ctypes
-
-    arr = (ctypes.c_void_p * 64)()
-    n = L.lib().avc_capture_deps(ctypes.c_void_p(stream.cuda_stream), arr, 64)
-    return [arr[i] for i in range(n)] if n > 0 else []
-
-
-class GraphSplit:
-    """A captured step rebuilt as a main-stream graph and a side-stream graph (graph.hip)."""
-
-    def __init__(self, raw_graph, main_tails, side_tails, max_segments=None):
-        import ctypes
-
-        if max_segments is None:
-            max_segments = int(os.environ.get("AVC_GRAPH_SEGMENTS", "16"))
-        mt = (ctypes.c_void_p * len(main_tails))(*main_tails)
-        st = (ctypes.c_void_p * len(side_tails))(*side_tails)
-        h = ctypes.c_void_p()
-        counts = (ctypes.c_int * 4)()
-        L.call("avc_graph_split", ctypes.c_void_p(raw_graph), mt, len(main_tails), st, len(side_tails),
-               int(max_segments), ctypes.byref(h), counts)
-        self.handle = h
-        self.counts = tuple(counts)
-
-    def launch(self, main, side):
-        L.call("avc_graph_launch2", self.handle, main.cuda_stream, side.cuda_stream)
-
-    def __del__(self):
-        if getattr(self, "handle", None):
-            try:
-                L.lib().avc_graph_split_destroy(self.handle)
-            except Exception:
-                pass
-            self.handle = None

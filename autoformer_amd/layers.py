@@ -148,22 +148,8 @@ class _Side:
 def join_side() -> None:
     side = _SINK["side"]
     if side is not None:
-        if _SINK.get("tails") == [] and torch.cuda.is_current_stream_capturing():
-            # a capture that TrainStep will split into a main and a side graph: each stream's
-            # capture dependencies at the join (graph.hip, avc_graph_split)
-            _SINK["tails"] = [K.capture_deps(torch.cuda.current_stream()), K.capture_deps(side)]
         stream_wait(K.stream(), ev_record(side.cuda_stream))
     _SINK["keep"].clear()
-
-
-def record_join_tails(on: bool):
-    """Arm (on) / take (off: returns [main tails, side tails] or None) the capture dependencies
-    that join_side() records while a graph capture is running."""
-    if on:
-        _SINK["tails"] = []
-        return None
-    t = _SINK.pop("tails", None)
-    return t if t else None
 
 
 def _grad_of(p):

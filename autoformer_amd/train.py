@@ -25,7 +25,7 @@ import torch
 
 from . import dist as D
 from . import kernels as K
-from .layers import (ev_record, join_side, on_stream, prefetch_packs, record_join_tails, set_grad_sink, side_stream,
+from .layers import (ev_record, join_side, on_stream, prefetch_packs, set_grad_sink, side_stream,
                      stream_wait, weights_changed)
 
 
@@ -226,12 +226,6 @@ class FusedAdam:
 # workgroup cap of the decoder-slice Adam that runs beside the encoder backward (0 = full grid;
 # 256 measured best: the full 4096-block grid slowed the latency-bound BiLSTM backward beside it)
 _SIDE_ADAM_BLOCKS = int(os.environ.get("AVC_SIDE_ADAM_BLOCKS", "256"))
-# capture(): split the captured step into concurrent main / side graphs (opt-in, AVC_GRAPH_SPLIT=1).
-# Off by default: the split graphs replay correctly ONCE and produce NaN from the second replay on,
-# in every arrangement measured (any number of segments, side graphs serialised on the main stream,
-# side graphs skipped), while one graph holding the same copied nodes -- in capture order or with
-# every main node first -- replays correctly (profiles/r3_graph_split.txt).  One graph is the default.
-_GRAPH_SPLIT = os.environ.get("AVC_GRAPH_SPLIT", "0") == "1"
 
 
 class TrainStep:
@@ -255,7 +249,6 @@ class TrainStep:
         set_grad_sink(True)  # kernels accumulate straight into the flat gradient buffer
         self.opt = FusedAdam(self.flat, self.gflat, lr)
         self.graph_fb = None
-        self.graph_split = None
         self.world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
         self.loss = None
         # The decoder / postnet (/ discriminator) gradients are final once the backward reaches
@@ -352,10 +345,7 @@ class TrainStep:
 
     def _step(self, x, emb):
         if self.graph_fb is not None:
-            if self.graph_split is not None:
-                self.graph_split.launch(torch.cuda.current_stream(), side_stream())
-            else:
-                self.graph_fb.replay()
+            self.graph_fb.replay()
             loss = self.loss
         else:
             loss = self._fwd_bwd(x, emb, overlap=self.split is not None)
@@ -379,21 +369,12 @@ class TrainStep:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         weights_changed()  # the captured forward must contain the weight repacks
-        # keep_graph: the raw graph is split into a main-stream and a side-stream graph that
-        # replay concurrently (graph.hip): one graph would run the weight-gradient branch
-        # serially after the main chain (the runtime executes a graph in one queue)
-        g = torch.cuda.CUDAGraph(keep_graph=True)
-        record_join_tails(True)
-        try:
-            with torch.cuda.graph(g):
-                self.loss = self._fwd_bwd(x, emb)
-        finally:
-            tails = record_join_tails(False)
-        self.graph_split = None
-        if tails is not None and all(tails) and _GRAPH_SPLIT:
-            self.graph_split = K.GraphSplit(g.raw_cuda_graph(), tails[0], tails[1])
-        else:
-            g.instantiate()
+        # One graph: the runtime executes it in one queue, so the weight-gradient branch captured
+        # from the side stream runs after the main chain instead of beside it (the
+        # round-3 main / side split replayed NaN from its second replay and was removed).
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.loss = self._fwd_bwd(x, emb)
         self.graph_fb = g  # capture only records: the next step() replays it
 
 

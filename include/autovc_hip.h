@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 16
+#define AVC_ABI_VERSION 17
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -257,6 +257,13 @@ int avc_set_fault_word(void* word);
  * do not succeed within it. */
 int avc_lstm_set_spin(unsigned spins);
 
+/* Benchmarking: configuration of the 8-wave deep-ring NT GEMM (gemm_ring.hip) that avc_gemm
+ * dispatches bf16 products with K-contiguous operands to.  mode -1 = automatic tile choice,
+ * 0 = off (the older kernels), 1 = forced bm x bn tile with nst ring slots; gm = row tiles per
+ * tile group (<= 0 keeps the current value); win = 1 lets conv window operands take it.  Same as
+ * the AVC_RING / AVC_RING_WIN environment variables.  Returns 0. */
+int avc_gemm_set_ring(int mode, int bm, int bn, int nst, int gm, int win);
+
 /* 1 when avc_lstm_fwd (backward = 0) / avc_lstm_bwd (backward = 1) take the one-launch
  * persistent path for this shape on the current device: bf16 compute, dirs == 1, H in
  * {512, 768, 1024}, and the occupancy API admits the whole grid (ceil(B/8) * H/32
@@ -484,24 +491,6 @@ int avc_event_create(void** out);
 int avc_event_record(void* ev, void* stream);
 int avc_stream_wait_event(void* stream, void* ev);
 
-/* ---- the training step as two concurrent hipGraphs (graph.hip).  Not a reference operation:
- * host plumbing of train.py's step loop (train.py:82-99) when the step is replayed from a capture.
- * avc_capture_deps: the current capture dependencies (graph nodes, as void*) of a capturing stream;
- * returns their count (<= max_out) or -1.
- * avc_graph_split: rebuild a captured graph whose side-stream branch forked from the main stream
- * and joins it only at the end as up to max_segments (main graph, side graph) pairs: the main
- * chain is cut after main nodes that side nodes wait for, side segment k holds the side nodes whose
- * latest main dependency is in main segment k; main_tails / side_tails = each stream's capture
- * dependencies at the join.  counts (nullable, 4 ints): [main nodes, side nodes, cross edges,
- * segments].
- * avc_graph_launch2: per segment, main graph on main_stream, event, side_stream waits for it,
- * side graph on side_stream; finally main_stream waits for side_stream.
- * avc_graph_split_destroy: frees the two graphs, their executables and events. */
-int avc_capture_deps(void* stream, void** out, int max_out);
-int avc_graph_split(void* graph, void* const* main_tails, int n_main, void* const* side_tails, int n_side,
-                    int max_segments, void** handle, int* counts);
-int avc_graph_launch2(void* handle, void* main_stream, void* side_stream);
-int avc_graph_split_destroy(void* handle);
 
 #ifdef __cplusplus
 }

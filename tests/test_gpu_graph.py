@@ -1,9 +1,8 @@
-"""The step replayed as a captured hipGraph (TrainStep.capture: one graph by default; the
-opt-in main / side split of graph.hip is not replay-safe, see train._GRAPH_SPLIT) against the
-eager step.
+"""The step replayed as a captured hipGraph (TrainStep.capture: one graph) against the eager
+step.
 
-Each replay gets a NEW batch (copied into the captured input tensors) and lr = 0, so a side-graph
-kernel that ran before the main-graph node it depends on would read the previous batch's
+Each replay gets a NEW batch (copied into the captured input tensors) and lr = 0, so a weight-gradient
+kernel that ran before the node it depends on would read the previous batch's
 activations / data gradients and show as an O(1) gradient error, while rounding differences stay
 tiny (fp32: the split-K weight gradients add in a run-dependent order)."""
 import numpy as np
@@ -37,7 +36,7 @@ def _compare(comp, B, T, freq, gtol, steps=4):
     try:
         tb.step(xb, eb)
         tb.capture(xb, eb, warmup=0)
-        assert tb.graph_split is None and tb.graph_fb is not None
+        assert tb.graph_fb is not None
         for i, (x, e) in enumerate(batches):
             la = ta.step(x, e)
             ga = ta.gflat.clone()

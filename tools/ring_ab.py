@@ -1,0 +1,120 @@
+"""A/B of the deep-ring NT GEMM (gemm_ring.hip) against the older kernels on the C2 / C4 product
+shapes, interleaved in one process (cdna_hip_programming.md §5.4 rule 24), random operands, with
+an fp32 reference check of every configuration.
+
+  python tools/ring_ab.py [--reps 20] [--rounds 3] [--only c2|c4]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import autoformer_amd as A  # noqa: E402
+from autoformer_amd import _lib  # noqa: E402
+from autoformer_amd import kernels as K  # noqa: E402
+
+A.set_compute("bf16")
+dev = "cuda:0"
+
+
+def ring(mode, bm=0, bn=0, nst=0, gm=0, win=1):
+    _lib.call("avc_gemm_set_ring", mode, bm, bn, nst, gm, win)
+
+
+def ev(fn, n):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n * 1e3
+
+
+def shapes(only):
+    out = []
+    if only in (None, "c2"):
+        out += [
+            ("conv 8192x512x2560 w5", 8192, 512, 2560, dict(win=(64, 128, 512)), False),
+            ("conv 8192x512x2560 w5 bn", 8192, 512, 2560, dict(win=(64, 128, 512)), True),
+            ("conv 8192x80x2560 w5", 8192, 80, 2560, dict(win=(64, 128, 512)), False),
+            ("xproj 8192x4096x512", 8192, 4096, 512, {}, False),
+            ("dx 8192x1024x4096", 8192, 1024, 4096, {}, False),
+            ("dx 8192x512x4096", 8192, 512, 4096, {}, False),
+            ("xproj1 8192x2048x344", 8192, 2048, 344, {}, False),
+        ]
+    if only in (None, "c4"):
+        out += [
+            ("tok1 22016x7424x1856", 22016, 7424, 1856, {}, False),
+            ("tok2 22016x1849x7424", 22016, 1849, 7424, {}, False),
+            ("cf1 118336x1376x344", 118336, 1376, 344, {}, False),
+            ("cf2 118336x344x1376", 118336, 344, 1376, {}, False),
+            ("conv T176 11264x512x2560 w5", 11264, 512, 2560, dict(win=(64, 176, 512)), False),
+        ]
+    return out
+
+
+CONFIGS = [("old", (0,)), ("auto", (-1,)), ("128x128x4", (1, 128, 128, 4)), ("256x128x3", (1, 256, 128, 3)),
+           ("256x256x2", (1, 256, 256, 2)), ("128x256x3", (1, 128, 256, 3))]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--only", default=None)
+    args = ap.parse_args()
+    torch.manual_seed(0)
+    for name, M, N, Kd, kw, bn in shapes(args.only):
+        if "win" in kw:
+            B, T, Ci = kw["win"]
+            x = torch.randn(B * T, Ci, device=dev).bfloat16()
+            opa = K.operand(x, Ci, window=(5, 2, T, T, Ci))
+            # reference: explicit im2col
+            xp = torch.nn.functional.pad(x.float().view(B, T, Ci), (0, 0, 2, 2))
+            aref = torch.cat([xp[:, k:k + T] for k in range(5)], dim=2).reshape(B * T, 5 * Ci)
+        else:
+            a = torch.randn(M, Kd, device=dev).bfloat16()
+            opa = K.operand(a, Kd)
+            aref = a.float()
+        b = (torch.randn(N, Kd, device=dev) * 0.05).bfloat16()
+        c = torch.empty(M, N, device=dev)
+        ref = aref @ b.float().t()
+        kwb = {}
+        if bn:
+            part = K.bn_partial_buffer(M, N, dev)
+            g_, b_ = torch.ones(N, device=dev), torch.zeros(N, device=dev)
+            rm, rv = torch.zeros(N, device=dev), torch.ones(N, device=dev)
+            kwb = dict(bn_partial=part, bn_fin=(g_, b_, rm, rv, None, 0.1, 1e-5, 1))
+
+        def run():
+            K.gemm(M, N, Kd, opa, K.operand(b, Kd), c, **kwb)
+
+        res = {}
+        for cname, cfg in CONFIGS:
+            ring(*cfg)
+            c.zero_()
+            run()
+            torch.cuda.synchronize()
+            err = ((c - ref).abs().max() / ref.abs().max()).item()
+            res[cname] = ([], err)
+        for _ in range(args.rounds):
+            for cname, cfg in CONFIGS:
+                ring(*cfg)
+                run()
+                torch.cuda.synchronize()
+                res[cname][0].append(ev(run, args.reps))
+        fl = 2.0 * M * N * Kd
+        for cname, (ts, err) in res.items():
+            t = min(ts)
+            print(f"{name:30s} {cname:10s} {t:8.1f} us (med {sorted(ts)[len(ts) // 2]:8.1f})  "
+                  f"{fl / t / 1e6:7.1f} TF  err {err:.2e}", flush=True)
+        del c, ref, aref
+        torch.cuda.empty_cache()
+    ring(-1)
+
+
+if __name__ == "__main__":
+    main()
