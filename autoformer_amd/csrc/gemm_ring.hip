@@ -379,6 +379,184 @@ void launch(const GemmArgs& g, int gm, hipStream_t s) {
   gemm_ring_kernel<BM_, BN_, NST, WIN><<<nb, RNT, lds, s>>>(g, gm);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Conv1d (5 taps, stride 1, 'same' padding) with the input tile staged ONCE for all taps, in the
+// ring form: 128 frames x 128 output columns per workgroup (the one tile that gives each of the
+// 256 CUs a tile of the AutoVC 8192 x 512 convs), 8 waves as 2 x 4 (64 x 32 each), stages of
+// CBK = 32 channels: the 132-row halo (128 frames + 4, 64-B rows) and the five 128-column weight
+// slices (640 rows x 64 B) = 49 KiB per stage, three stages (147 KiB), two in flight.  Tap k
+// reads the halo k rows down.  The 49 glds wave-instructions of a stage are dealt over the 8
+// waves (wave 0 issues 7, the others 6: the counted waits use each wave's own count).
+// ALIGNED (T % 128 == 0): a tile never spans two utterances, so the loader zero-fills the halo
+// rows of other utterances and the fragments need no per-lane predicate; otherwise a per-lane,
+// per-tap mask zeroes the A fragment rows whose shifted frame leaves the utterance.
+// X = activation, W = Wf[co][tap][ci] (forward) or dy and Wd[ci][tap'][co] (data gradient).
+constexpr int CV_TM = 128, CV_TN = 128, CV_TAPS = 5, CV_CBK = 32, CV_NST = 3;
+constexpr int CV_AI = (CV_TM + CV_TAPS - 1 + 15) / 16;  // 9 halo instructions (16 rows of 64 B)
+constexpr int CV_BI = CV_TAPS * CV_TN / 16;             // 40 weight instructions
+constexpr int CV_TOT = CV_AI + CV_BI;                   // 49
+constexpr int CV_LW = (CV_TOT + 7) / 8;                 // 7: instructions of waves < CV_TOT % 8
+constexpr int CV_ABYTES = CV_AI * 1024;
+constexpr int CV_STAGE = CV_TOT * 1024;
+
+template <int N>
+__device__ __forceinline__ void wait_cv(bool full) {
+  if (full) wait_vm<N * CV_LW>();
+  else wait_vm<N * (CV_LW - 1)>();
+}
+
+// ABL (timing diagnostics only, wrong results; tools/ring_ab.py --ablate): 1 = no fragment reads /
+// MFMAs (the ring's loads alone), 2 = no loads after the prologue (fragment reads + MFMAs alone)
+template <bool ALIGNED, int ABL = 0>
+__global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
+  constexpr int MI = 4, NJ = 2, P = CV_NST - 1;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const bool full = wid < (CV_TOT % 8 ? CV_TOT % 8 : 8);  // this wave issues CV_LW per stage
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int nN = (g.N + CV_TN - 1) / CV_TN, nM = (g.M + CV_TM - 1) / CV_TM;
+  const int grp = lid / (gm * nN), fm = grp * gm, gsz = min(nM - fm, gm);
+  const int wi = lid - grp * gm * nN;
+  const int mt = fm + wi % gsz, nt = wi / gsz;
+  const int m0 = mt * CV_TM, n0 = nt * CV_TN;
+
+  const OpDev& A = g.a;
+  const OpDev& Bo = g.b;
+  const bf16* xa = reinterpret_cast<const bf16*>(A.ptr);
+  const bf16* wb = reinterpret_cast<const bf16*>(Bo.ptr);
+  const int pad = A.pad, T = A.t_out, chans = A.chans;
+  const int nst = chans / CV_CBK;
+
+  // ---- loader: instruction qi = i*8 + wid (i < CV_LW, qi < CV_TOT) writes stage bytes
+  // [qi KiB, +1 KiB) = rows 16*qi + (lane>>2) of 64 B, 16-B slot lane&3 holding the global chunk
+  // (lane&3) ^ ((row>>1)&3)
+  const int b0 = (int)fdiv((uint32_t)m0, A.tdiv);  // utterance of the tile's first row
+  const bf16* src[CV_LW];
+  bool sok[CV_LW];
+#pragma unroll
+  for (int i = 0; i < CV_LW; ++i) {
+    const int qi = i * 8 + wid;
+    const int lrow = lane >> 2, slot = lane & 3;
+    src[i] = reinterpret_cast<const bf16*>(g_zero16_rg);
+    sok[i] = false;
+    if (qi < CV_AI) {
+      const int hr = 16 * qi + lrow;  // halo row
+      const int f = m0 - pad + hr;
+      bool ok = hr < CV_TM + CV_TAPS - 1 && f >= 0 && f < g.M;
+      if (ALIGNED && ok) ok = (int)fdiv((uint32_t)f, A.tdiv) == b0;
+      if (ok) {
+        src[i] = xa + (long long)f * A.ld + 8 * (slot ^ ((hr >> 1) & 3));
+        sok[i] = true;
+      }
+    } else if (qi < CV_TOT) {
+      const int wr = 16 * (qi - CV_AI) + lrow;  // weight row = tap * 128 + column
+      const int tap = wr / CV_TN, n = n0 + (wr - tap * CV_TN);
+      if (n < g.N) {
+        src[i] = wb + (long long)n * Bo.ld + (long long)tap * chans + 8 * (slot ^ ((wr >> 1) & 3));
+        sok[i] = true;
+      }
+    }
+  }
+  auto issue = [&](int stg, int cs) {
+    char* base = smem_raw + stg * CV_STAGE;
+    const int c0 = cs * CV_CBK;
+#pragma unroll
+    for (int i = 0; i < CV_LW; ++i) {
+      const int qi = i * 8 + wid;
+      if (qi < CV_TOT) glds16(sok[i] ? (const void*)(src[i] + c0) : (const void*)g_zero16_rg, base + qi * 1024);
+    }
+  };
+
+  // ---- fragments: A row (halo) wm*64 + i*16 + frow + k, chunk (lane>>4) ^ ((row>>1)&3); rows
+  // 16 apart share the swizzle, so i is an immediate offset of 1 KiB.  B row k*128 + wn*32 + j*16 +
+  // frow: its swizzle is ((frow>>1)&3), the (k, j) part an immediate offset.
+  const int frow = lane & 15, kq = lane >> 4;
+  int aaddr[CV_TAPS];
+#pragma unroll
+  for (int k = 0; k < CV_TAPS; ++k) {
+    const int r = wm * 64 + frow + k;
+    aaddr[k] = r * 64 + 16 * (kq ^ ((r >> 1) & 3));
+  }
+  const int baddr = CV_ABYTES + (wn * 32 + frow) * 64 + 16 * (kq ^ ((frow >> 1) & 3));
+  unsigned vmask = 0xFFFFFFFFu;
+  if (!ALIGNED) {
+    vmask = 0;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = min(m0 + wm * 64 + i * 16 + frow, g.M - 1);
+      const int b = (int)fdiv((uint32_t)m, A.tdiv);
+      const int t = m - b * T;
+#pragma unroll
+      for (int k = 0; k < CV_TAPS; ++k) {
+        const int t2 = t + k - pad;
+        if (t2 >= 0 && t2 < T) vmask |= 1u << (i * 8 + k);
+      }
+    }
+  }
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+    if (p < nst) issue(p, p);
+
+  for (int cs = 0; cs < nst; ++cs) {
+    const int ahead = min(P - 1, nst - 1 - cs);
+    if (ahead >= 1) wait_cv<1>(full);
+    else wait_vm<0>();
+    raw_barrier();
+    if (ABL != 2 && cs + P < nst) issue((cs + P) % CV_NST, cs + P);
+    if (ABL == 1) continue;
+    const char* st = smem_raw + (cs % CV_NST) * CV_STAGE;
+    bf16x8 af[2][MI], bfr[2][NJ];
+    auto read_tap = [&](int k, int slot) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(st + aaddr[k] + i * 1024);
+        af[slot][i] = (ALIGNED || ((vmask >> (i * 8 + k)) & 1u)) ? v : bf16x8{};
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        bfr[slot][j] = *reinterpret_cast<const bf16x8*>(st + baddr + (k * CV_TN + j * 16) * 64);
+    };
+    read_tap(0, 0);
+#pragma unroll
+    for (int k = 0; k < CV_TAPS; ++k) {
+      const int slot = k & 1;
+      if (k + 1 < CV_TAPS) read_tap(k + 1, slot ^ 1);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[slot][i], bfr[slot][j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  ring_epilogue<CV_TM, CV_TN>(g, acc, m0, n0, 0, 0, smem_raw);
+}
+
+template <bool ALIGNED, int ABL = 0>
+void launch_conv(const GemmArgs& g, int gm, hipStream_t s) {
+  const size_t lds = (size_t)CV_NST * CV_STAGE;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<ALIGNED, ABL>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const int nb = ((g.M + CV_TM - 1) / CV_TM) * ((g.N + CV_TN - 1) / CV_TN);
+  conv_ring_kernel<ALIGNED, ABL><<<nb, RNT, lds, s>>>(g, gm);
+}
+
 bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 bool operand_ok(const OpDev& o, bool allow_win) {
@@ -388,11 +566,13 @@ bool operand_ok(const OpDev& o, bool allow_win) {
 }
 
 // AVC_RING = "BM,BN,NST[,GM]" forces a configuration (benchmarking), "0" disables the kernel;
-// AVC_RING_WIN=0 leaves the conv window operands to gemm_conv.hip.  avc_gemm_set_ring() sets the
+// AVC_RING_WIN = 0 leaves the conv window operands to gemm_conv.hip, 1 lets forced configurations
+// stream them as im2col windows, 2 (default) puts aligned 5-tap convs on the halo ring kernel.  avc_gemm_set_ring() sets the
 // same at run time (A/B tools in one process).
 struct RingCfg {
-  int mode = 0;  // -1 auto, 0 off, 1 forced (off until measured: AVC_RING=-1 turns it on)
-  int bm = 0, bn = 0, nst = 0, gm = 8, win = 1;
+  int mode = -1;  // -1 auto, 0 off, 1 forced
+  int bm = 0, bn = 0, nst = 0, gm = 8, win = 2;
+  int abl = 0;  // timing ablations of the halo conv (win 3 / 4 through avc_gemm_set_ring)
 };
 RingCfg init_cfg() {
   RingCfg r;
@@ -408,7 +588,7 @@ RingCfg init_cfg() {
     }
     if (n >= 4 && a3 > 0) r.gm = a3;
   }
-  if (const char* e = getenv("AVC_RING_WIN")) r.win = e[0] != '0';
+  if (const char* e = getenv("AVC_RING_WIN")) r.win = atoi(e);
   return r;
 }
 RingCfg g_ring = init_cfg();
@@ -421,24 +601,36 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
   if (g.K % 8 || g.klen % RBK || g.bnb_ws) return false;
   if (!operand_ok(g.a, true) || !operand_ok(g.b, false)) return false;
   const long long units = (long long)g.batch * g.split_k;
+  const bool win = g.a.win != 0;
+  // 5-tap 'same' convs on 32-channel stages: the halo form (win == 2), utterance-aligned tiles only
+  // unless forced (T % 128 != 0 leaves 1.4 tiles per CU at B=64 T=176, where the 128 x 64 tiles of
+  // gemm_conv.hip spread better -- tools/ring_ab.py, profiles/r4_ring_ab.txt)
+  const OpDev& a = g.a;
+  if (win && c.win == 2 && a.taps == CV_TAPS && a.t_in == a.t_out && 2 * a.pad == a.taps - 1 &&
+      g.K == a.taps * a.chans && a.chans % CV_CBK == 0 && g.batch == 1 && g.split_k == 1 && !g.b.win &&
+      (c.mode == 1 || a.t_out % CV_TM == 0)) {
+    if (c.abl == 1) launch_conv<true, 1>(g, c.gm, s);
+    else if (c.abl == 2) launch_conv<true, 2>(g, c.gm, s);
+    else if (a.t_out % CV_TM == 0) launch_conv<true>(g, c.gm, s);
+    else launch_conv<false>(g, c.gm, s);
+    return true;
+  }
   int bm, bn, nst;
   if (c.mode == 1) {
     bm = c.bm;
     bn = c.bn;
     nst = c.nst;
   } else {
-    // one workgroup per CU: the largest tile that still gives every CU a tile
+    // measured (tools/ring_ab.py): the 256 x 256 ring beats the older kernels by 20-45 % on wide
+    // products with at least one tile per CU (MLP-Mixer token / channel mixing, the decoder LSTM
+    // input projections); narrower products (N < 1024) and conv window streams stay on
+    // gemm_nt.hip / gemm_conv.hip, as fast or faster there
     const long long t22 = (long long)((g.M + 255) / 256) * ((g.N + 255) / 256) * units;
-    const long long t21 = (long long)((g.M + 255) / 256) * ((g.N + 127) / 128) * units;
-    if (g.N > 128 && t22 >= 256) {
-      bm = 256; bn = 256; nst = 2;
-    } else if (t21 >= 256) {
-      bm = 256; bn = 128; nst = 3;
-    } else {
-      bm = 128; bn = 128; nst = 4;
-    }
+    if (win || g.N < 1024 || t22 < 256) return false;
+    bm = 256;
+    bn = 256;
+    nst = 2;
   }
-  const bool win = g.a.win != 0;
 #define RING_CASE(BMV, BNV, NSV)                       \
   if (bm == BMV && bn == BNV && nst == NSV) {          \
     if (win) launch<BMV, BNV, NSV, true>(g, c.gm, s);  \
@@ -454,13 +646,14 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
 }  // namespace avcg
 
 // Benchmarking hook (tools/ring_ab.py): mode -1 auto, 0 off, 1 forced (bm, bn, nst); gm row
-// tiles per group (<= 0 keeps it); win 0/1: whether conv window operands take this kernel.
+// tiles per group (<= 0 keeps it); win: as AVC_RING_WIN.
 extern "C" int avc_gemm_set_ring(int mode, int bm, int bn, int nst, int gm, int win) {
   avcg::g_ring.mode = mode;
   avcg::g_ring.bm = bm;
   avcg::g_ring.bn = bn;
   avcg::g_ring.nst = nst;
   if (gm > 0) avcg::g_ring.gm = gm;
-  avcg::g_ring.win = win;
+  avcg::g_ring.win = win >= 3 ? 2 : win;
+  avcg::g_ring.abl = win >= 3 ? win - 2 : 0;  // 3: loads only, 4: reads + MFMAs only (wrong results)
   return 0;
 }

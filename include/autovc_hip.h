@@ -257,11 +257,13 @@ int avc_set_fault_word(void* word);
  * do not succeed within it. */
 int avc_lstm_set_spin(unsigned spins);
 
-/* Benchmarking: configuration of the 8-wave deep-ring NT GEMM (gemm_ring.hip) that avc_gemm
- * dispatches bf16 products with K-contiguous operands to.  mode -1 = automatic tile choice,
- * 0 = off (the older kernels), 1 = forced bm x bn tile with nst ring slots; gm = row tiles per
- * tile group (<= 0 keeps the current value); win = 1 lets conv window operands take it.  Same as
- * the AVC_RING / AVC_RING_WIN environment variables.  Returns 0. */
+/* Benchmarking: configuration of the 8-wave deep-ring GEMMs (gemm_ring.hip) that avc_gemm
+ * dispatches bf16 products with K-contiguous operands to.  mode -1 = the measured default policy
+ * (256 x 256 tiles for N >= 1024 with a tile per CU, the halo ring for utterance-aligned 5-tap
+ * convs), 0 = off (the older kernels), 1 = forced bm x bn tile with nst ring slots; gm = row tiles
+ * per tile group (<= 0 keeps the current value); win: 0 = conv window operands never take it,
+ * 1 = forced configurations stream them as im2col windows, 2 = 5-tap convs take the halo ring.
+ * Same as the AVC_RING / AVC_RING_WIN environment variables.  Returns 0. */
 int avc_gemm_set_ring(int mode, int bm, int bn, int nst, int gm, int win);
 
 /* 1 when avc_lstm_fwd (backward = 0) / avc_lstm_bwd (backward = 1) take the one-launch

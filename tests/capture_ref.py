@@ -3,8 +3,9 @@
 `Capture` wraps the kernels-module entry points that carry the step's arithmetic -- every GEMM
 (conv windows, halo conv / halo dW, split-K weight gradients, the lstm1 fold products, fused
 bias / residual / BN-statistics / BN-finalize / bf16-twin / cperm epilogues), the persistent and
-wavefront LSTM recurrences, the small-H BiLSTM, the BN apply / backward passes and the code
-expansion.  For each call it synchronises, snapshots what the op accumulates into, runs the
+wavefront LSTM recurrences, the small-H BiLSTM, the BN apply / backward passes, the code
+expansion, the MetaFormer blocks (GroupNorm, LayerNorm, GELU twins, pooling mixer, patchify,
+batched transposes), the discriminator head, the loss block, BCE and the fused Adam.  For each call it synchronises, snapshots what the op accumulates into, runs the
 production kernel, and computes the same op in float64 from the very tensors the kernel read
 (bf16 operands are exact in fp64).  The deviation recorded per output is the relative
 Frobenius norm  ||got - ref|| / ||ref||  (of the increment for accumulating outputs).
@@ -349,10 +350,229 @@ class Capture:
         self.records.append(("conv_edge_colsum", f"conv_edge_colsum B{B} T{T} C{C}", {"Sdy": _rel(out, ref.view_as(out))}))
         return out
 
+    # ---------------------------------------------------------------- MetaFormer (C4) blocks
+    def _group_norm_fwd(self, x, B, C, gamma, beta, eps):
+        torch.cuda.synchronize()
+        y, mean, rstd = self._orig["group_norm_fwd"](x, B, C, gamma, beta, eps)
+        torch.cuda.synchronize()
+        xv = x.double().reshape(B, -1)
+        mu, var = xv.mean(1), xv.var(1, unbiased=False)
+        rs = 1.0 / torch.sqrt(var + eps)
+        ref = ((xv - mu[:, None]) * rs[:, None]).view(B, -1, C)
+        if gamma is not None:
+            ref = ref * gamma.double() + (beta.double() if beta is not None else 0.0)
+        res = {"y": _rel(y, ref.view_as(y)), "mean": _rel(mean, mu), "rstd": _rel(rstd, rs)}
+        self.records.append(("group_norm_fwd", f"group_norm_fwd B{B} S{xv.shape[1]} C{C}", res))
+        return y, mean, rstd
+
+    def _group_norm_bwd(self, dy, x, gamma, mean, rstd, B, C, dgamma=None, dbeta=None, accumulate=False):
+        torch.cuda.synchronize()
+        b0 = dgamma.double().clone() if (dgamma is not None and accumulate) else None
+        b1 = dbeta.double().clone() if (dbeta is not None and accumulate) else None
+        dx = self._orig["group_norm_bwd"](dy, x, gamma, mean, rstd, B, C, dgamma, dbeta, accumulate)
+        torch.cuda.synchronize()
+        xh = (x.double().reshape(B, -1) - mean.double()[:, None]) * rstd.double()[:, None]
+        g = dy.double().reshape(B, -1)
+        gm = gamma.double() if gamma is not None else torch.ones(C, dtype=torch.float64, device=x.device)
+        dxh = (g.view(B, -1, C) * gm).reshape(B, -1)
+        rdx = rstd.double()[:, None] * (dxh - dxh.mean(1, keepdim=True) - xh * (dxh * xh).mean(1, keepdim=True))
+        res = {"dx": _rel(dx, rdx.view_as(dx))}
+        if dgamma is not None:
+            rg = (g * xh).view(-1, C).sum(0)
+            res["dgamma"] = _rel(dgamma, rg + (b0 if b0 is not None else 0), b0)
+        if dbeta is not None:
+            rb = g.view(-1, C).sum(0)
+            res["dbeta"] = _rel(dbeta, rb + (b1 if b1 is not None else 0), b1)
+        self.records.append(("group_norm_bwd", f"group_norm_bwd B{B} C{C}", res))
+        return dx
+
+    def _layer_norm_fwd(self, x, gamma, beta, eps):
+        torch.cuda.synchronize()
+        y, mean, rstd = self._orig["layer_norm_fwd"](x, gamma, beta, eps)
+        torch.cuda.synchronize()
+        xv = x.double()
+        mu, var = xv.mean(1), xv.var(1, unbiased=False)
+        rs = 1.0 / torch.sqrt(var + eps)
+        ref = (xv - mu[:, None]) * rs[:, None]
+        if gamma is not None:
+            ref = ref * gamma.double()[None] + (beta.double()[None] if beta is not None else 0.0)
+        res = {"y": _rel(y, ref), "mean": _rel(mean, mu), "rstd": _rel(rstd, rs)}
+        self.records.append(("layer_norm_fwd", f"layer_norm_fwd R{x.shape[0]} D{x.shape[1]}", res))
+        return y, mean, rstd
+
+    def _layer_norm_bwd(self, dy, x, gamma, mean, rstd, dgamma=None, dbeta=None, accumulate=False):
+        torch.cuda.synchronize()
+        b0 = dgamma.double().clone() if (dgamma is not None and accumulate) else None
+        b1 = dbeta.double().clone() if (dbeta is not None and accumulate) else None
+        dx = self._orig["layer_norm_bwd"](dy, x, gamma, mean, rstd, dgamma, dbeta, accumulate)
+        torch.cuda.synchronize()
+        xh = (x.double() - mean.double()[:, None]) * rstd.double()[:, None]
+        g = dy.double()
+        dxh = g * (gamma.double()[None] if gamma is not None else 1.0)
+        rdx = rstd.double()[:, None] * (dxh - dxh.mean(1, keepdim=True) - xh * (dxh * xh).mean(1, keepdim=True))
+        res = {"dx": _rel(dx, rdx)}
+        if dgamma is not None:
+            res["dgamma"] = _rel(dgamma, (g * xh).sum(0) + (b0 if b0 is not None else 0), b0)
+        if dbeta is not None:
+            res["dbeta"] = _rel(dbeta, g.sum(0) + (b1 if b1 is not None else 0), b1)
+        self.records.append(("layer_norm_bwd", f"layer_norm_bwd R{x.shape[0]} D{x.shape[1]}", res))
+        return dx
+
+    def _gelu_fwd_operand(self, x):
+        torch.cuda.synchronize()
+        y = self._orig["gelu_fwd_operand"](x)
+        torch.cuda.synchronize()
+        self.records.append(("gelu_fwd", f"gelu_fwd n{x.numel()}",
+                             {"y": _rel(y, torch.nn.functional.gelu(x.double()))}))
+        return y
+
+    def _gelu_bwd_twin(self, g, x):
+        torch.cuda.synchronize()
+        dx = self._orig["gelu_bwd_twin"](g, x)
+        torch.cuda.synchronize()
+        xd = x.double()
+        cdf = 0.5 * (1.0 + torch.erf(xd / 2 ** 0.5))
+        pdf = torch.exp(-0.5 * xd * xd) / (2 * torch.pi) ** 0.5
+        ref = g.double() * (cdf + xd * pdf)
+        res = {"dx": _rel(dx, ref)}
+        if getattr(dx, "_bf16", None) is not None:
+            res["dx_bf16"] = _rel(dx._bf16, ref)
+        self.records.append(("gelu_bwd", f"gelu_bwd n{x.numel()}", res))
+        return dx
+
+    def _pool3_mixer(self, x, B, Lf, C, backward=False):
+        torch.cuda.synchronize()
+        y = self._orig["pool3_mixer"](x, B, Lf, C, backward)
+        torch.cuda.synchronize()
+        xin = x.double().view(B, Lf, C).permute(0, 2, 1)  # (B, C, L)
+
+        def fwd(t):
+            return torch.nn.functional.avg_pool1d(t, 3, 1, 1, count_include_pad=False) - t
+
+        if not backward:
+            ref = fwd(xin)
+        else:  # the adjoint of the forward map applied to dy
+            z = torch.zeros_like(xin, requires_grad=True)
+            ref = torch.autograd.grad(fwd(z), z, grad_outputs=xin)[0]
+        ref = ref.permute(0, 2, 1).reshape_as(y)
+        self.records.append(("pool3", f"pool3 B{B} L{Lf} C{C}" + (" bwd" if backward else ""), {"y": _rel(y, ref)}))
+        return y
+
+    def _patchify(self, src, B, Lf, C, ps, backward=False):
+        torch.cuda.synchronize()
+        dst = self._orig["patchify"](src, B, Lf, C, ps, backward)
+        torch.cuda.synchronize()
+        H, W = C // ps, Lf // ps
+        if not backward:  # P[b][h*W + w][p1*ps + p2] = nf[b][w*ps + p2][h*ps + p1]
+            ref = src.double().view(B, W, ps, H, ps).permute(0, 3, 1, 4, 2).reshape_as(dst)
+        else:
+            ref = src.double().view(B, H, W, ps, ps).permute(0, 2, 4, 1, 3).reshape_as(dst)
+        self.records.append(("patchify", f"patchify B{B} L{Lf} C{C}" + (" bwd" if backward else ""),
+                             {"out": _rel(dst, ref)}))
+        return dst
+
+    def _transpose_batched(self, src, B, R, C, out=None, accumulate=False):
+        torch.cuda.synchronize()
+        before = out.double().clone() if (out is not None and accumulate) else None
+        dst = self._orig["transpose_batched"](src, B, R, C, out, accumulate)
+        torch.cuda.synchronize()
+        ref = src.double().reshape(B, R, C).transpose(1, 2).reshape(-1)
+        if before is not None:
+            ref = ref + before.reshape(-1)
+        self.records.append(("btranspose", f"btranspose B{B} R{R} C{C}" + (" acc" if accumulate else ""),
+                             {"out": _rel(dst.reshape(-1), ref, None if before is None else before.reshape(-1))}))
+        return dst
+
+    # ---------------------------------------------------------------- discriminator head (C5)
+    def _disc_dense_fwd(self, a, w, bias, B, nl, nc):
+        torch.cuda.synchronize()
+        p = self._orig["disc_dense_fwd"](a, w, bias, B, nl, nc)
+        torch.cuda.synchronize()
+        wb = w.double().reshape(nc, nl).t().reshape(-1)  # bin-major order of the channel-major weight
+        z = a.double().reshape(B, nl * nc) @ wb + (bias.double().reshape(-1) if bias is not None else 0.0)
+        self.records.append(("disc_dense_fwd", f"disc_dense_fwd B{B} L{nl} C{nc}",
+                             {"p": _rel(p.reshape(-1), torch.sigmoid(z))}))
+        return p
+
+    def _disc_dense_bwd(self, dp, p, a, w, B, nl, nc):
+        torch.cuda.synchronize()
+        da, dw, db = self._orig["disc_dense_bwd"](dp, p, a, w, B, nl, nc)
+        torch.cuda.synchronize()
+        pd = p.double().reshape(-1)
+        dz = dp.double().reshape(-1) * pd * (1 - pd)
+        wb = w.double().reshape(nc, nl).t().reshape(-1)
+        rda = dz[:, None] * wb[None]
+        rdw = (dz[:, None] * a.double().reshape(B, nl * nc)).sum(0).reshape(nl, nc).t().reshape(-1)
+        res = {"da": _rel(da, rda.view_as(da)), "dw": _rel(dw.reshape(-1), rdw), "db": _rel(db.reshape(-1), dz.sum()[None])}
+        self.records.append(("disc_dense_bwd", f"disc_dense_bwd B{B} L{nl} C{nc}", res))
+        return da, dw, db
+
+    # ---------------------------------------------------------------- losses and the optimizer
+    def _vc_loss(self, x, y1, y2, ca, cb, lambda_cd):
+        torch.cuda.synchronize()
+        out = self._orig["vc_loss"](x, y1, y2, ca, cb, lambda_cd)
+        torch.cuda.synchronize()
+        m1 = ((x.double() - y1.double()) ** 2).mean()
+        m2 = ((x.double() - y2.double()) ** 2).mean()
+        l1 = (ca.double() - cb.double()).abs().mean()
+        ref = torch.stack([m1, m2, l1, m1 + m2 + lambda_cd * l1])
+        self.records.append(("vc_loss", f"vc_loss n{x.numel()} nc{ca.numel()}", {"out": _rel(out, ref)}))
+        return out
+
+    def _vc_loss_grad(self, x, y1, y2, ca, cb, lambda_cd, d, need):
+        torch.cuda.synchronize()
+        outs = self._orig["vc_loss_grad"](x, y1, y2, ca, cb, lambda_cd, d, need)
+        torch.cuda.synchronize()
+        dv = [float(t.item()) if t is not None else 0.0 for t in d]
+        n1, n2 = x.numel(), ca.numel()
+        c_id, c_ps, c_cd = dv[3] + dv[0], dv[3] + dv[1], lambda_cd * dv[3] + dv[2]
+        ga = c_cd * torch.sign(ca.double() - cb.double()) / n2
+        refs = (c_id * 2 * (y1.double() - x.double()) / n1, c_ps * 2 * (y2.double() - x.double()) / n1, ga, -ga)
+        res = {n: _rel(o, r) for n, o, r in zip(("g1", "g2", "ga", "gb"), outs, refs) if o is not None}
+        self.records.append(("vc_loss_grad", f"vc_loss_grad n{n1}", res))
+        return outs
+
+    def _bce_loss(self, p, target):
+        torch.cuda.synchronize()
+        out = self._orig["bce_loss"](p, target)
+        torch.cuda.synchronize()
+        pd = p.double()
+        ref = -(target * torch.clamp(torch.log(pd), min=-100) + (1 - target) * torch.clamp(torch.log(1 - pd), min=-100))
+        self.records.append(("bce_loss", f"bce_loss n{p.numel()} t{target}", {"out": _rel(out, ref.mean())}))
+        return out
+
+    def _bce_grad(self, p, target, dloss, through_sigmoid=False):
+        torch.cuda.synchronize()
+        g = self._orig["bce_grad"](p, target, dloss, through_sigmoid)
+        torch.cuda.synchronize()
+        pd = p.double()
+        ref = dloss.double().reshape(()) * (pd - target) / torch.clamp((1 - pd) * pd, min=1e-12) / p.numel()
+        if through_sigmoid:
+            ref = ref * pd * (1 - pd)
+        self.records.append(("bce_grad", f"bce_grad n{p.numel()}", {"g": _rel(g, ref)}))
+        return g
+
+    def _adam(self, p, g, m, v, lr, beta1, beta2, eps, state, advance=True, max_blocks=0):
+        torch.cuda.synchronize()
+        p0, m0, v0, st0 = p.double().clone(), m.double().clone(), v.double().clone(), state.double().clone()
+        self._orig["adam"](p, g, m, v, lr, beta1, beta2, eps, state, advance, max_blocks)
+        torch.cuda.synchronize()
+        step = float(st0[0].item()) + (1.0 if advance else 0.0)
+        gd = g.double()
+        rm = beta1 * m0 + (1 - beta1) * gd
+        rv = beta2 * v0 + (1 - beta2) * gd * gd
+        bc1, bc2 = 1 - beta1 ** step, 1 - beta2 ** step
+        rp = p0 - (lr / bc1) * rm / (torch.sqrt(rv) / bc2 ** 0.5 + eps)
+        res = {"dp": _rel(p, rp, p0), "m": _rel(m, rm), "v": _rel(v, rv)}
+        self.records.append(("adam", f"adam n{p.numel()}" + ("" if advance else " slice"), res))
+
     # ---------------------------------------------------------------- context
     def __enter__(self):
         for name in ("gemm", "lstm_fwd", "lstm2_fwd", "lstm_bwd", "bn_apply", "bn_bwd", "expand_codes",
-                     "conv_edge_table", "conv_edge_colsum"):
+                     "conv_edge_table", "conv_edge_colsum", "group_norm_fwd", "group_norm_bwd", "layer_norm_fwd",
+                     "layer_norm_bwd", "gelu_fwd_operand", "gelu_bwd_twin", "pool3_mixer", "patchify",
+                     "transpose_batched", "disc_dense_fwd", "disc_dense_bwd", "vc_loss", "vc_loss_grad", "bce_loss",
+                     "bce_grad", "adam"):
             self._orig[name] = getattr(K, name)
             setattr(K, name, getattr(self, "_" + name))
         return self

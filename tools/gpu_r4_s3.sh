@@ -1,0 +1,25 @@
+# round 4: full GPU suite, then C2 / C4 / C5 bench with the ring GEMMs on and off (interleaved), and
+# a kernel-trace profile of the C2 step -> gpurun_out/$1
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/$1
+mkdir -p $OUT
+cd $R
+if [ "$2" != "skip-tests" ]; then
+  timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -rA \
+      > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }
+  tail -3 $OUT/pytest_gpu.log
+fi
+for rep in 1 2; do
+  for ring in -1 0; do
+    AVC_RING=$ring timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/c2_ring$ring.$rep.json 2>/dev/null || exit 1
+    AVC_RING=$ring timeout -k 10 200 python -u bench.py --model MetaConv --steps 10 --warmup 3 --no-cpu-baseline > $OUT/c4_ring$ring.$rep.json 2>/dev/null || exit 1
+  done
+done
+timeout -k 10 200 python -u bench.py --disc --steps 20 --warmup 3 --no-cpu-baseline > $OUT/c5.json 2>/dev/null || exit 1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
+    python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-kernel-timing > $OUT/prof.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c4 -o run -- \
+    python3 $R/bench.py --model MetaConv --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing > $OUT/prof_c4.log 2>&1 || exit 1
+grep -o '"ms_per_step": [0-9.]*' $OUT/*.json

@@ -19,7 +19,7 @@ A.set_compute("bf16")
 dev = "cuda:0"
 
 
-def ring(mode, bm=0, bn=0, nst=0, gm=0, win=1):
+def ring(mode, bm=0, bn=0, nst=0, gm=8, win=1):
     _lib.call("avc_gemm_set_ring", mode, bm, bn, nst, gm, win)
 
 
@@ -35,6 +35,9 @@ def ev(fn, n):
 
 def shapes(only):
     out = []
+    if only == "conv":
+        return [("conv 8192x512x2560 w5", 8192, 512, 2560, dict(win=(64, 128, 512)), False),
+                ("xproj 8192x4096x512", 8192, 4096, 512, {}, False)]
     if only in (None, "c2"):
         out += [
             ("conv 8192x512x2560 w5", 8192, 512, 2560, dict(win=(64, 128, 512)), False),
@@ -56,8 +59,13 @@ def shapes(only):
     return out
 
 
-CONFIGS = [("old", (0,)), ("auto", (-1,)), ("128x128x4", (1, 128, 128, 4)), ("256x128x3", (1, 256, 128, 3)),
-           ("256x256x2", (1, 256, 256, 2)), ("128x256x3", (1, 128, 256, 3))]
+# (mode, bm, bn, nst, gm, win): win 2 = 5-tap convs on the halo ring kernel
+CONFIGS = [("old", (0, 0, 0, 0, 0, 1)), ("auto", (-1, 0, 0, 0, 8, 1)), ("halo", (-1, 0, 0, 0, 8, 2)),
+           ("128x128x4", (1, 128, 128, 4, 8, 1)), ("256x128x3", (1, 256, 128, 3, 8, 1)),
+           ("256x256x2", (1, 256, 256, 2, 8, 1)), ("128x256x3", (1, 128, 256, 3, 8, 1)),
+           ("auto-gm4", (-1, 0, 0, 0, 4, 1)), ("auto-gm16", (-1, 0, 0, 0, 16, 1)),
+           # timing ablations of the halo conv (wrong results): its loads alone / its reads + MFMAs alone
+           ("halo-loads", (-1, 0, 0, 0, 8, 3)), ("halo-math", (-1, 0, 0, 0, 8, 4))]
 
 
 def main():
@@ -65,7 +73,10 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--configs", default=None, help="comma-separated subset of the CONFIGS names")
     args = ap.parse_args()
+    configs = [c for c in CONFIGS if (args.configs is None and not c[0].startswith("halo-"))
+               or (args.configs is not None and c[0] in args.configs.split(","))]
     torch.manual_seed(0)
     for name, M, N, Kd, kw, bn in shapes(args.only):
         if "win" in kw:
@@ -93,7 +104,7 @@ def main():
             K.gemm(M, N, Kd, opa, K.operand(b, Kd), c, **kwb)
 
         res = {}
-        for cname, cfg in CONFIGS:
+        for cname, cfg in configs:
             ring(*cfg)
             c.zero_()
             run()
@@ -101,7 +112,7 @@ def main():
             err = ((c - ref).abs().max() / ref.abs().max()).item()
             res[cname] = ([], err)
         for _ in range(args.rounds):
-            for cname, cfg in CONFIGS:
+            for cname, cfg in configs:
                 ring(*cfg)
                 run()
                 torch.cuda.synchronize()
@@ -113,7 +124,7 @@ def main():
                   f"{fl / t / 1e6:7.1f} TF  err {err:.2e}", flush=True)
         del c, ref, aref
         torch.cuda.empty_cache()
-    ring(-1)
+    ring(0)
 
 
 if __name__ == "__main__":
