@@ -41,14 +41,14 @@ __device__ __forceinline__ void wait_vm() {
 }
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
-// CBK channels per stage (LDS rows of 2*CBK bytes), CBN output columns per tile, NWM waves along
-// M (tile rows 64*NWM; NWM*2 waves per workgroup).  Every wave issues the same number of glds per
+// CBK channels per stage (LDS rows of 2*CBK bytes), CBN output columns per tile, 128-row tiles,
+// 4 waves (2 along M, 2 along N).  Every wave issues the same number of glds per
 // stage (the counted vmcnt waits assume it), so the halo and weight instruction counts are
 // rounded up to a multiple of the wave count; the extra rows load zeros.
-template <int TAPS, int CBK, int CBN, int NWM = 2>
+template <int TAPS, int CBK, int CBN>
 struct ConvCfg {
-  static constexpr int NW = 2 * NWM;              // waves per workgroup
-  static constexpr int TM = 64 * NWM;             // tile rows
+  static constexpr int NW = 4;                    // waves per workgroup
+  static constexpr int TM = 128;                  // tile rows
   static constexpr int ROW = 2 * CBK;             // bytes per LDS row
   static constexpr int CPR = ROW / 16;            // 16-B chunks per row
   static constexpr int RPI = 1024 / ROW;          // rows per glds wave-instruction
@@ -67,9 +67,9 @@ struct ConvCfg {
 
 // BNB: the BatchNorm-backward epilogue compiled in (only the instances launched with bnb: its
 // code in every conv instance cost 20 % of the conv time, measured)
-template <int TAPS, int NST, int CBK, int CBN, bool BNB, int NWM = 2>
-__global__ void __launch_bounds__(128 * NWM, 4 / NWM) gemm_conv_kernel(GemmArgs g) {
-  using C = ConvCfg<TAPS, CBK, CBN, NWM>;
+template <int TAPS, int NST, int CBK, int CBN, bool BNB>
+__global__ void __launch_bounds__(256, 2) gemm_conv_kernel(GemmArgs g) {
+  using C = ConvCfg<TAPS, CBK, CBN>;
   constexpr int NW = C::NW, TM = C::TM;
   constexpr int STAGE = C::STAGE, LPT = C::LPT, AI4 = C::AI / NW, BI4 = C::BI / NW, P = NST - 1;
   constexpr int ROW = C::ROW, CPR = C::CPR, RPI = C::RPI, NJ = C::NJ, KB = CBK / 32;
@@ -200,21 +200,21 @@ __global__ void __launch_bounds__(128 * NWM, 4 / NWM) gemm_conv_kernel(GemmArgs 
     }
   }
   __syncthreads();  // last wait was vmcnt(0); every fragment read done before the epilogue reuses LDS
-  fast_epilogue<CBN, BNB, true, NWM>(g, acc, m0, n0, mt * (TM / BM), 0, 0, smem_raw);
+  fast_epilogue<CBN, BNB, true>(g, acc, m0, n0, mt, 0, 0, smem_raw);
 }
 
-template <int NST, int CBK, int CBN, bool BNB = false, int NWM = 2>
+template <int NST, int CBK, int CBN, bool BNB = false>
 void launch(const GemmArgs& g, hipStream_t s) {
-  using C = ConvCfg<5, CBK, CBN, NWM>;
+  using C = ConvCfg<5, CBK, CBN>;
   const size_t lds = (size_t)NST * C::STAGE;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_conv_kernel<5, NST, CBK, CBN, BNB, NWM>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_conv_kernel<5, NST, CBK, CBN, BNB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int nb = ((g.M + C::TM - 1) / C::TM) * ((g.N + CBN - 1) / CBN);
-  gemm_conv_kernel<5, NST, CBK, CBN, BNB, NWM><<<nb, 64 * C::NW, lds, s>>>(g);
+  gemm_conv_kernel<5, NST, CBK, CBN, BNB><<<nb, 64 * C::NW, lds, s>>>(g);
 }
 
 bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -254,9 +254,9 @@ bool gemm_conv_launch(const GemmArgs& g, hipStream_t s) {
     launch<2, 32, 64, true>(g, s);
     return true;
   }
-  // (256-row tiles -- eight waves, one workgroup per CU, three 48-KiB stages, NWM = 4 -- measured no
-  // faster: 44.4 / 36.6 us vs 42.5 / 35.2 us with / without the BN epilogue on 8192x512x2560,
-  // profiles/r3_conv_tile_ab.txt; not dispatched)
+  // (round 3 measured 256-row tiles of this kernel -- eight waves, one workgroup per CU, three
+  // 48-KiB stages -- no faster, profiles/r3_conv_tile_ab.txt; round 4 removed that form: the
+  // eight-wave halo conv is gemm_ring.hip's conv_ring_kernel)
 #define CONV_CASE(NS, BK, BN)                  \
   if (ns == NS && bk == BK && bn == BN) {      \
     launch<NS, BK, BN>(g, s);                  \

@@ -131,15 +131,11 @@ __device__ __forceinline__ void add_row_bias(const GemmArgs& g, f32x4 (&acc)[4][
 // BNB: the BatchNorm-backward reduction compiled in.  YST: the caller's LDS holds at least
 // 8 KiB + 128 x (2*BN_ + 16) bytes, so a bf16 y tile is staged through it with 16-B coalesced
 // loads (per-element 2-B buffer loads of y made a fused conv 30 us slower than a plain one)
-// NWM = 4: eight waves as 4 (M) x 2 (N), a 256-row tile = two 128-row BN statistics tiles mt, mt+1
-// (no BN-backward epilogue in that form).
-template <int BN_, bool BNB = true, bool YST = false, int NWM = 2>
+template <int BN_, bool BNB = true, bool YST = false>
 __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4][BN_ / 32], int m0, int n0, int mt,
                                               int bz, int ks, char* smem_raw) {
-  static_assert(NWM == 2 || (NWM == 4 && !BNB), "the 256-row form has no BN-backward epilogue");
   constexpr int NJ = BN_ / 32;
   constexpr int WN = BN_ / 2;
-  constexpr int NH = NWM / 2;  // 128-row statistics tiles per workgroup tile
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int rbase = m0 + wm * 64 + 4 * (lane >> 4);
@@ -179,9 +175,8 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
       }
     }
   if (g.bn_partial) {
-    float* red = reinterpret_cast<float*>(smem_raw);  // [NWM][BN_] sums, then [NWM][BN_] M2
-    const int hh = wm >> 1;                           // this wave's 128-row statistics tile
-    const int cnt = max(1, min(BM, g.M - (m0 + BM * hh)));
+    float* red = reinterpret_cast<float*>(smem_raw);  // [2][BN_] sums, then [2][BN_] M2
+    const int cnt = max(1, min(BM, g.M - m0));
     float s[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -204,7 +199,7 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int cl = wn * WN + j * 16 + (lane & 15);
-      const float mean = (red[(2 * hh) * BN_ + cl] + red[(2 * hh + 1) * BN_ + cl]) / (float)cnt;
+      const float mean = (red[cl] + red[BN_ + cl]) / (float)cnt;
       float t = 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -217,19 +212,19 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
       t += __shfl_xor(t, 32, 64);
       qv[j] = t;
     }
-    float* red2 = red + NWM * BN_;
+    float* red2 = red + 2 * BN_;
     if (lane < 16) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) red2[wm * BN_ + wn * WN + j * 16 + lane] = qv[j];
     }
     __syncthreads();
-    if (tid < NH * BN_) {
-      const int h = tid / BN_, cl = tid - h * BN_;
+    if (tid < BN_) {
+      const int cl = tid;
       const int col = n0 + cl;
-      if (col < g.N && m0 + BM * h < g.M) {
-        float* p = g.bn_partial + ((long long)(mt + h) * g.N + col) * 2;
-        const float s0 = red[(2 * h) * BN_ + cl] + red[(2 * h + 1) * BN_ + cl];
-        const float s1 = red2[(2 * h) * BN_ + cl] + red2[(2 * h + 1) * BN_ + cl];
+      if (col < g.N) {
+        float* p = g.bn_partial + ((long long)mt * g.N + col) * 2;
+        const float s0 = red[cl] + red[BN_ + cl];
+        const float s1 = red2[cl] + red2[BN_ + cl];
         // sc1 when another block merges them (bn_cnt): no L2-wide release fence needed
         if (g.bn_cnt) {
           st_sc1(p, s0);
@@ -242,8 +237,7 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
     }
     if (g.bn_cnt) {
       const int ntile = (g.M + BM - 1) / BM;
-      const int mine = min(NH, ntile - mt);  // statistics tiles this workgroup delivers
-      if (arrive_last(g.bn_cnt + n0 / BN_, (unsigned)ntile, (unsigned)mine)) bn_finalize_cols<BN_>(g, n0, red);
+      if (arrive_last(g.bn_cnt + n0 / BN_, (unsigned)ntile)) bn_finalize_cols<BN_>(g, n0, red);
     }
   }
   if (BNB && g.bnb_ws) {

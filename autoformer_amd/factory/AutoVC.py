@@ -7,10 +7,14 @@ codes (B, T/freq*2*dim_neck))``, or only ``codes`` when ``c_trg is None``) and t
 unchanged through their ``importlib`` plugin lookup (train.py:45-47).
 
 Every op runs as a HIP kernel from libautovc_hip.so:
-  Encoder  AutoVC.py:18-68  -> enc_conv0 (concat + conv + BN-stats epilogue) , 2x conv_bn,
-                               2 BiLSTM layers (persistent small-H recurrence), code gather
-  Decoder  AutoVC.py:71-114 -> lstm1 (per-step fused MFMA recurrence), 3x conv_bn,
-                               lstm2 (2 layers), linear
+  Encoder  AutoVC.py:18-68  -> enc_conv0 (the speaker half of cat(mel, c_org) folded into a
+                               per-(utterance, edge class) GEMM row bias; the conv runs on the 80
+                               mel channels, fold.hip), 2x conv_bn (BN statistics + finalize in the
+                               conv epilogue), 2 BiLSTM layers (persistent small-H recurrence),
+                               code gather
+  Decoder  AutoVC.py:71-114 -> lstm1 (input projection folded per code / utterance, persistent
+                               recurrence), 3x conv_bn, lstm2 (2 layers: one-launch wavefront
+                               forward, persistent backward per layer), linear
   Postnet  AutoVC.py:117-179-> 5x conv_bn (tanh x4, none x1 with the residual add fused)
 Activations are frame-major (B*T, C); the reference's (B, C, T) transposes disappear.
 """

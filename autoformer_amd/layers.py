@@ -49,12 +49,11 @@ def set_grad_sink(on: bool) -> None:
 # torch's current stream switched through its C bindings.  torch.cuda.Event() / .record() /
 # current_stream() / torch.cuda.stream() cost 10-15 us of Python each (measured ~1 ms per AutoVC
 # step at ~90 uses, tools/host_profile2.py); these cost a ctypes call.
-_EV = {"ring": [], "i": 0}
+_EV = {"ring": [], "i": 0, "gen": 0, "slot": []}
 _EV_RING = 512  # events in flight per step are < 100; a handle is re-recorded 5+ steps later
 
 
-def ev_record(stream_raw=None):
-    """Record a ring event on the raw stream (default: torch's current stream); returns its handle."""
+def _ev_next(stream_raw):
     ring = _EV["ring"]
     if not ring:
         import ctypes
@@ -63,16 +62,40 @@ def ev_record(stream_raw=None):
             h = ctypes.c_void_p()
             K.L.call("avc_event_create", ctypes.byref(h))
             ring.append(h.value)
+        _EV["slot"] = [0] * len(ring)
     i = _EV["i"]
     _EV["i"] = (i + 1) % len(ring)
-    h = ring[i]
-    K.L.call("avc_event_record", h, K.stream() if stream_raw is None else stream_raw)
-    return h
+    _EV["gen"] += 1
+    _EV["slot"][i] = _EV["gen"]
+    K.L.call("avc_event_record", ring[i], K.stream() if stream_raw is None else stream_raw)
+    return i
+
+
+def ev_record(stream_raw=None):
+    """Record a ring event on the raw stream (default: torch's current stream); returns its handle.
+    For waits issued right away (within the same step); a wait that may come much later takes
+    ev_token / wait_token, which check that the ring slot was not re-recorded meanwhile."""
+    return _EV["ring"][_ev_next(stream_raw)]
+
+
+def ev_token(stream_raw=None):
+    """Record a ring event and return (slot, generation) for a later wait_token."""
+    i = _ev_next(stream_raw)
+    return (i, _EV["slot"][i])
 
 
 def stream_wait(stream_raw, ev):
     """The raw stream waits for the event's current record."""
     K.L.call("avc_stream_wait_event", stream_raw, ev)
+
+
+def wait_token(stream_raw, tok):
+    """stream_wait on an ev_token's record; raises if the ring slot has been re-recorded since (the
+    dependency would silently move to the newer record -- ADVICE r3)."""
+    i, gen = tok
+    if _EV["slot"][i] != gen:
+        raise RuntimeError(f"event ring slot {i} was re-recorded before its wait (> {_EV_RING} records in between)")
+    K.L.call("avc_stream_wait_event", stream_raw, _EV["ring"][i])
 
 
 _get_cur = torch._C._cuda_getCurrentStream
@@ -191,7 +214,7 @@ class PackCache:
         if key != self.key:
             pend, self.pending = self.pending, None
             if pend is not None and pend[0] == key:
-                stream_wait(K.stream(), pend[2])
+                wait_token(K.stream(), pend[2])
                 self.val = pend[1]
             else:
                 with torch.no_grad():
@@ -286,7 +309,7 @@ def prefetch_packs() -> None:
                 batched.append((c, key))
                 continue
             val = c.build()
-            c.pending = (key, val, ev_record(side_raw))
+            c.pending = (key, val, ev_token(side_raw))
         # a few launches in first-use order, each with its own event: the next forward waits for
         # the encoder's packs only, not for the whole batch
         for gi in range(0, len(batched), _PACK_GROUP):
@@ -294,7 +317,7 @@ def prefetch_packs() -> None:
             plan = _batch_plan([c for c, _ in grp], gi)
             K.L.call("avc_pack_batch", plan["ops"].data_ptr(), plan["prefix"].data_ptr(), plan["n"], plan["total"],
                      K.stream())
-            ev = ev_record(side_raw)
+            ev = ev_token(side_raw)
             for c, key in grp:
                 c.pending = (key, c.val, ev)
 

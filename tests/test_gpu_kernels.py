@@ -1023,11 +1023,10 @@ def Kr_act_relu():
 @pytest.mark.parametrize("B,T,Cin,Cout", [(64, 128, 512, 512), (3, 37, 64, 96), (5, 50, 96, 136), (8, 176, 512, 80),
                                           (2, 300, 32, 64)])
 def test_conv_bn_fused_finalize(B, T, Cin, Cout):
-    """The halo conv kernel with the BN finalize in its epilogue (the forward conv + BN of every
-    ConvNorm layer) against the same conv with the separate finalize, under whatever conv tile
-    configuration the process runs (AVC_CONV_CFG: 128-row tiles by default, 256-row tiles =
-    two statistics tiles per workgroup with 13,32,64): y, partials, mean / rstd / scale / shift
-    and the running statistics."""
+    """The halo conv kernels with the BN finalize in their epilogue (the forward conv + BN of every
+    ConvNorm layer) against the same conv with the separate finalize: y, partials, mean / rstd /
+    scale / shift and the running statistics.  Utterance-aligned shapes (T % 128 == 0) take the
+    eight-wave ring kernel (gemm_ring.hip conv_ring_kernel), the others gemm_conv.hip."""
     import autoformer_amd as A
     from autoformer_amd import kernels as Kr
 
