@@ -717,6 +717,32 @@ static int bnb_after(const avc_gemm_desc* d, const avc_bnb_args* bb, hipStream_t
                                        fin, s);
 }
 
+// The fused GELU epilogues (avc_gemm_desc.c_bf16_act / act_grad_of) exist in the ring kernels
+// only; for the other kernels the GEMM writes plain fp32 C and one avc_gelu_twin pass follows.
+extern "C" int avc_gelu_twin(const float* g, const float* x, float* y, void* y16, long long n, int bwd, void* stream);
+struct GeluPost {
+  int act = 0;
+  const float* agrad = nullptr;
+  bf16* c16 = nullptr;
+};
+static GeluPost strip_gelu(GemmArgs& g) {
+  GeluPost p;
+  if (!g.c16_act && !g.agrad) return p;
+  p.act = g.c16_act;
+  p.agrad = g.agrad;
+  p.c16 = g.c16;
+  g.c16_act = 0;
+  g.agrad = nullptr;
+  g.c16 = nullptr;
+  return p;
+}
+static int gelu_after(const GemmArgs& g, const GeluPost& p, hipStream_t s) {
+  const long long n = (long long)g.M * g.N * g.batch;
+  if (p.agrad) return avc_gelu_twin(g.c, p.agrad, g.c, p.c16, n, 1, s);  // C *= GELU'(x), twin
+  if (p.act) return avc_gelu_twin(nullptr, g.c, nullptr, p.c16, n, 0, s);  // twin = GELU(C)
+  return 0;
+}
+
 static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, const avc_bnb_args* bb = nullptr) {
   AVC_CHECK_ARG(d != nullptr, "avc_gemm: null desc");
   AVC_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0, "avc_gemm: negative dims");
@@ -759,6 +785,16 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
   AVC_CHECK_ARG(!g.cperm || (d->N % g.cperm == 0 && !g.bias && !g.res && !g.c16 && !g.bn_partial),
                 "avc_gemm: cperm needs N %% taps == 0 and no bias / residual / bf16 / BN epilogue");
   g.cpd = make_fastdiv(g.cperm ? (uint32_t)(d->N / g.cperm) : 1u);
+  g.c16_act = d->c_bf16_act;
+  g.agrad = d->act_grad_of;
+  AVC_CHECK_ARG(g.c16_act == 0 || g.c16_act == AVC_ACT_GELU, "avc_gemm: c_bf16_act must be 0 or AVC_ACT_GELU");
+  AVC_CHECK_ARG(!(g.c16_act || g.agrad) ||
+                    (d->c && d->ldc == d->N && (g.batch == 1 || d->c_batch_stride == (long long)d->M * d->N) &&
+                     !d->accumulate && g.split_k == 1 &&
+                     !d->cperm && !d->bn_partial && !bb && (!g.agrad || !d->residual) &&
+                     (!g.c16_act || d->c_bf16)),
+                "avc_gemm: the fused GELU epilogues need an fp32 C with ldc == N, no accumulate / split-K / batch "
+                "sum / cperm / BN epilogues (act_grad_of: no residual; c_bf16_act: c_bf16 set)");
   g.rbias = d->row_bias;
   g.rb_t = d->rb_t;
   g.rb_pad = d->rb_pad;
@@ -825,8 +861,12 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
       if (!g.bnb_cnt) return -1;
     }
     const char* what = "avc_gemm(fast)";
-    if (!aks && !bks && gemm_ring_launch(g, s)) what = "avc_gemm(ring)";
-    else if (!aks && !bks && gemm_conv_launch(g, s)) what = "avc_gemm(conv)";
+    GeluPost post;
+    const bool ring = !aks && !bks && gemm_ring_launch(g, s);
+    if (ring) what = "avc_gemm(ring)";
+    else post = strip_gelu(g);  // the other kernels have no GELU epilogue: a pass after them
+    if (ring) {
+    } else if (!aks && !bks && gemm_conv_launch(g, s)) what = "avc_gemm(conv)";
     else if (!aks && !bks && gemm_nt_launch(g, s)) what = "avc_gemm(nt)";
     else if (aks && bks && gemm_tt_launch(g, s)) what = "avc_gemm(tt)";
     else {
@@ -837,10 +877,12 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
       else launch_fast_layout<128>(g, aks, bks, nb, s);
     }
     if (avc_check_launch(what)) return -1;
+    if (gelu_after(g, post, s)) return -1;
     if (bb && !bnb_fused) return bnb_after(d, bb, s);
     return (f && !g.bn_cnt) ? bn_finalize_after(g, f, stream) : 0;
   }
-  AVC_CHECK_ARG(!g.c16, "avc_gemm: c_bf16 output needs the fast path (bf16 compute, vectorisable operands)");
+  const GeluPost post = strip_gelu(g);
+  AVC_CHECK_ARG(!g.c16 || post.c16, "avc_gemm: c_bf16 output needs the fast path (bf16 compute, vectorisable operands)");
   static const bool trace_generic = getenv("AVC_GEMM_TRACE") != nullptr;
   if (trace_generic && bf)
     fprintf(stderr, "avc_gemm generic: M=%d N=%d K=%d batch=%d split=%d aks=%d bks=%d avec=%d bvec=%d awin=%d chans=%d\n",
@@ -862,6 +904,7 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
   }
 #undef AVC_GEMM_LAUNCH
   if (avc_check_launch("avc_gemm")) return -1;
+  if (gelu_after(g, post, s)) return -1;
   if (bb) return bnb_after(d, bb, s);
   return f ? bn_finalize_after(g, f, stream) : 0;  // generic kernels: finalize launch(es) after the GEMM
 }

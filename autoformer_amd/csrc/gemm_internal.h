@@ -31,6 +31,8 @@ struct GemmArgs {
   float* bn_partial;
   int cperm;     // 0, or taps: column n = tap*chans + ch is stored at ch*taps + tap (conv weight layout)
   FastDiv cpd;   // divide a column by chans = N / cperm
+  int c16_act;         // avc_gemm_desc.c_bf16_act: C16 holds GELU(C) (ring kernels only)
+  const float* agrad;  // avc_gemm_desc.act_grad_of: C *= GELU'(agrad[o]) (ring kernels only)
   const float* rbias;  // per-(utterance, edge class) row bias (avc_gemm_desc.row_bias), nullable
   int rb_t, rb_pad;
   FastDiv rb_div;      // divide a row by rb_t
@@ -93,6 +95,12 @@ __device__ __forceinline__ void bn_finalize_cols(const GemmArgs& g, int n0, floa
     }
   }
   if (tid == 0 && n0 == 0 && g.bn_nbt) *g.bn_nbt += g.bn_nupd;
+}
+
+// GELU (erf form, nn.GELU) and its derivative for the fused epilogues
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143267794f * __expf(-0.5f * x * x);
 }
 
 // Column offset of output column `col` (cperm: the Conv1d [Co][Ci][K] layout).

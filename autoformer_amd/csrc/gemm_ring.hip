@@ -184,8 +184,9 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
           atomicAdd(C + o, v);
         } else {
           if (g.accumulate) v += C[o];
+          if (g.agrad) v *= gelu_grad_f(g.agrad[(long long)bz * g.cbs + o]);
           if (C) C[o] = v;
-          if (C16) C16[o] = (bf16)v;
+          if (C16) C16[o] = (bf16)(g.c16_act ? gelu_f(v) : v);
         }
       }
     }

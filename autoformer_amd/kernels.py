@@ -82,7 +82,7 @@ def operand(t: torch.Tensor, ld: int, kstrided: bool = False, window=None, batch
 
 def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=None, accumulate=False, split_k=1,
          bn_partial=None, batch=1, c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0, bn_fin=None,
-         bnb=None, row_bias=None):
+         bnb=None, row_bias=None, c_bf16_act=0, act_grad_of=None):
     """cperm = taps > 1: C's columns are (tap, channel) pairs written in nn.Conv1d's [Co][Ci][K]
     weight layout (a conv weight gradient straight into .grad).
     bn_fin = (gamma, beta, running_mean, running_var, nbt, momentum, eps, nupd): the BatchNorm
@@ -90,7 +90,9 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     bnb = (y, mean, rstd, gamma, beta, act, coef, dgamma, dbeta, dbias, accumulate): C is dL/da of
     the conv + BN + act layer whose conv output is y; the GEMM also computes that layer's BN
     backward statistics (avc_gemm_bnb: coef[6][N] and the parameter gradients).
-    row_bias = (S, T, pad): S[(b*(2 pad + 1) + edge class)][N] added to row b*T + t (the conv0 fold)."""
+    row_bias = (S, T, pad): S[(b*(2 pad + 1) + edge class)][N] added to row b*T + t (the conv0 fold).
+    c_bf16_act = ACT_GELU: c_bf16 receives GELU(C); act_grad_of = x: C *= GELU'(x) (and its twin) --
+    the MLP-Mixer GELU forward / backward folded into the GEMM epilogue (avc_gemm_desc)."""
     _dev(c, bias, bn_partial, c_bf16, residual)
     if c.dtype == torch.bfloat16:  # bf16-only output
         assert c_bf16 is None and not accumulate and split_k == 1 and not cperm
@@ -111,6 +113,10 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     d.c_bf16 = _ptr(c_bf16)
     d.residual = _ptr(residual)
     d.cperm = int(cperm)
+    d.c_bf16_act = int(c_bf16_act)
+    if act_grad_of is not None:
+        _dev(act_grad_of)
+        d.act_grad_of = act_grad_of.data_ptr()
     if row_bias is not None:
         rb, rb_t, rb_pad = row_bias
         _dev(rb)

@@ -263,18 +263,28 @@ def _lin(x, M, N, Kd, w, b=None, residual=None, out=None):
 
 def _gelu_gemm(M, N, Kd, a, b, bias, dev, batch=1):
     """(U, V): U = a . b^T + bias (the pre-activation the backward needs), V = GELU(U) as the next
-    GEMM's operand (bf16 only in bf16 mode).  GELU in the GEMM epilogue was measured slower
-    (DESIGN.md section 8): the per-element epilogue stalls the GEMM tail."""
+    GEMM's operand (bf16 only in bf16 mode).  bf16 mode: V comes out of the GEMM's epilogue
+    (avc_gemm_desc.c_bf16_act; the ring kernels compute it in the epilogue, other kernels run one
+    GELU pass after the GEMM), instead of a separate pass that re-reads U."""
     U = torch.empty(batch * M, N, device=dev)
-    K.gemm(M, N, Kd, a, b, U, bias=bias, batch=batch, c_batch_stride=M * N)
-    return U, K.gelu_fwd_operand(U)
+    if K.compute() != K.BF16:
+        K.gemm(M, N, Kd, a, b, U, bias=bias, batch=batch, c_batch_stride=M * N)
+        return U, K.gelu_fwd_operand(U)
+    V = torch.empty(batch * M, N, device=dev, dtype=torch.bfloat16)
+    K.gemm(M, N, Kd, a, b, U, bias=bias, batch=batch, c_batch_stride=M * N, c_bf16=V, c_bf16_act=K.ACT_GELU)
+    return U, V
 
 
 def _dgelu_gemm(M, N, Kd, a, b, U, dev, batch=1):
-    """dU = (a . b^T) * GELU'(U), fp32 with its bf16 operand twin."""
+    """dU = (a . b^T) * GELU'(U), fp32 with its bf16 operand twin (bf16 mode: in the GEMM epilogue,
+    avc_gemm_desc.act_grad_of)."""
     dU = torch.empty(batch * M, N, device=dev)
-    K.gemm(M, N, Kd, a, b, dU, batch=batch, c_batch_stride=M * N)
-    return K.gelu_bwd_twin(dU, U)
+    if K.compute() != K.BF16:
+        K.gemm(M, N, Kd, a, b, dU, batch=batch, c_batch_stride=M * N)
+        return K.gelu_bwd_twin(dU, U)
+    d16 = torch.empty(batch * M, N, device=dev, dtype=torch.bfloat16)
+    K.gemm(M, N, Kd, a, b, dU, batch=batch, c_batch_stride=M * N, c_bf16=d16, act_grad_of=U)
+    return K.attach_twin(dU, d16)
 
 
 class _MLPMixerFn(torch.autograd.Function):

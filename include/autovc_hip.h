@@ -80,6 +80,11 @@ typedef struct {
                             rb_pad -- the speaker half of the encoder's first conv folded out of the
                             frames (factory/AutoVC.py:46-51, fold.hip); non-K-strided operands only */
   int rb_t, rb_pad;
+  int c_bf16_act;        /* 0, or AVC_ACT_GELU: c_bf16 receives GELU(C) (erf form) instead of C rounded -- the
+                            next GEMM's operand (MLPMixer.py:16-23 FeedForward); fp32 C is the pre-activation.
+                            Needs c and c_bf16, ldc == N, no accumulate / split-K / batch sum / cperm */
+  const float* act_grad_of; /* nullable: C = (A.B + bias) * GELU'(act_grad_of[m*ldc + n]) and its bf16 twin -- the
+                            GELU backward folded into the data-gradient GEMM.  Same restrictions, no residual */
 } avc_gemm_desc;
 
 int avc_abi_version(void);

@@ -181,11 +181,12 @@ class Capture:
 
     # ---------------------------------------------------------------- wrappers
     def _gemm(self, M, N, Kd, a, b, c, ldc=None, bias=None, accumulate=False, split_k=1, bn_partial=None, batch=1,
-              c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0, bn_fin=None, bnb=None, row_bias=None):
+              c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0, bn_fin=None, bnb=None, row_bias=None,
+              c_bf16_act=0, act_grad_of=None):
         f = self._orig["gemm"]
         kw = dict(ldc=ldc, bias=bias, accumulate=accumulate, split_k=split_k, bn_partial=bn_partial, batch=batch,
                   c_batch_stride=c_batch_stride, comp=comp, c_bf16=c_bf16, residual=residual, cperm=cperm,
-                  bn_fin=bn_fin, bnb=bnb, row_bias=row_bias)
+                  bn_fin=bn_fin, bnb=bnb, row_bias=row_bias, c_bf16_act=c_bf16_act, act_grad_of=act_grad_of)
         if bnb is not None and self.skip_bnb:
             return f(M, N, Kd, a, b, c, **kw)
         torch.cuda.synchronize()
@@ -207,16 +208,21 @@ class Capture:
             P = P + _c_view(residual, M, N, ldc_, batch, c_batch_stride, 0).double()
         if row_bias is not None:
             P = P + row_bias_rows(row_bias[0], M, row_bias[1], row_bias[2])[None]
+        if act_grad_of is not None:  # the GELU backward folded into the epilogue
+            xg = _c_view(act_grad_of, M, N, ldc_, batch, c_batch_stride, 0).double()
+            P = P * (0.5 * (1.0 + torch.erf(xg / 2 ** 0.5)) + xg * torch.exp(-0.5 * xg * xg) / (2 * torch.pi) ** 0.5)
         stats = f(M, N, Kd, a, b, c, **kw)
         torch.cuda.synchronize()
         got = _c_view(c, M, N, ldc_, batch, c_batch_stride, cperm).double()
         ref = P if before is None else before + P
         tag = (f"gemm M{M} N{N} K{Kd}" + (f" b{batch}" if batch > 1 else "") + (f" sk{split_k}" if split_k > 1 else "")
                + (" acc" if accumulate else "") + (" win" if a.taps or b.taps else "") + (" cperm" if cperm else "")
-               + (" bf16out" if only16 else "") + (" rowbias" if row_bias is not None else ""))
+               + (" bf16out" if only16 else "") + (" rowbias" if row_bias is not None else "")
+               + (" gelu" if c_bf16_act else "") + (" dgelu" if act_grad_of is not None else ""))
         res = {"C": _rel(got, ref, before)}
         if c_bf16 is not None and not only16:
-            res["C_bf16"] = _rel(_c_view(c_bf16, M, N, ldc_, batch, c_batch_stride, 0), ref, before)
+            r16 = torch.nn.functional.gelu(ref) if c_bf16_act else ref
+            res["C_bf16"] = _rel(_c_view(c_bf16, M, N, ldc_, batch, c_batch_stride, 0), r16, before)
         if bn_partial is not None:
             # per 128-row tile (sum, M2) of the stored values -> column mean / variance
             nt = (M + 127) // 128

@@ -1,0 +1,145 @@
+"""The deep-ring GEMM kernels (gemm_ring.hip) against fp32 references of the same op:
+
+  * gemm_ring_kernel at every tile configuration, with ragged M / N / K (zero-granule tails), bias,
+    residual, accumulate, bf16 twin and the batch fold of shared-B products
+    (reference: the nn.Linear / Conv1d(k=1) products of factory/MLPMixer.py:16-33,58-92);
+  * conv_ring_kernel (5-tap 'same' Conv1d, factory/Norm.py:21-28) on utterance-aligned and
+    straddling tiles, with the BatchNorm statistics + finalize epilogue;
+  * the fused GELU epilogues (avc_gemm_desc.c_bf16_act / act_grad_of, MLPMixer.py:9-23), on the
+    ring kernel and on the fallback pass after the older kernels.
+Operands are bf16 (exact in fp32), so the references are fp32 products of the same values.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _ring(mode, bm=0, bn=0, nst=0, gm=8, win=2):
+    from autoformer_amd import _lib
+
+    _lib.call("avc_gemm_set_ring", mode, bm, bn, nst, gm, win)
+
+
+@pytest.fixture(autouse=True)
+def _bf16_and_reset():
+    import autoformer_amd as A
+
+    A.set_compute("bf16")
+    yield
+    _ring(-1)
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
+
+
+CFGS = [(256, 256, 2), (256, 128, 3), (128, 128, 4), (128, 128, 3), (128, 256, 3), (256, 128, 2)]
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+@pytest.mark.parametrize("M,N,Kd", [(1000, 300, 200), (513, 1100, 72), (256, 256, 64)])
+def test_ring_gemm_configs(cfg, M, N, Kd):
+    from autoformer_amd import kernels as K
+
+    torch.manual_seed(M + N + Kd)
+    a = torch.randn(M, Kd, device=DEV).bfloat16()
+    b = torch.randn(N, Kd, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    res = torch.randn(M, N, device=DEV)
+    ref = a.float() @ b.float().t() + bias + res
+    _ring(1, *cfg)
+    c = torch.empty(M, N, device=DEV)
+    c16 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    K.gemm(M, N, Kd, K.operand(a, Kd), K.operand(b, Kd), c, bias=bias, residual=res, c_bf16=c16)
+    torch.cuda.synchronize()
+    assert _rel(c, ref) < 1e-5
+    assert _rel(c16.float(), ref) < 1e-2
+    # accumulate on top
+    c2 = c.clone()
+    K.gemm(M, N, Kd, K.operand(a, Kd), K.operand(b, Kd), c2, accumulate=True)
+    torch.cuda.synchronize()
+    assert _rel(c2, c + a.float() @ b.float().t()) < 1e-5
+
+
+def test_ring_default_policy_and_batch_fold():
+    """The MetaConv token-mixing shape at reduced batch: a batch of per-utterance products sharing B
+    is folded into one product (344-row utterances, no per-batch row-tile remainder)."""
+    from autoformer_amd import kernels as K
+
+    torch.manual_seed(3)
+    B, D, NPp, N4 = 6, 344, 1856, 4 * 1856
+    a = torch.randn(B * D, NPp, device=DEV).bfloat16()
+    w = (torch.randn(N4, NPp, device=DEV) * 0.05).bfloat16()
+    bias = torch.randn(N4, device=DEV)
+    c = torch.empty(B * D, N4, device=DEV)
+    K.gemm(D, N4, NPp, K.operand(a, NPp, batch_stride=D * NPp), K.operand(w, NPp), c, bias=bias, batch=B,
+           c_batch_stride=D * N4)
+    torch.cuda.synchronize()
+    assert _rel(c, a.float() @ w.float().t() + bias) < 1e-5
+
+
+@pytest.mark.parametrize("B,T,Cin,Cout,forced", [(8, 128, 512, 512, False), (4, 256, 64, 136, False),
+                                                  (3, 176, 96, 200, True), (2, 50, 32, 64, True)])
+@pytest.mark.parametrize("bn", [False, True])
+def test_conv_ring(B, T, Cin, Cout, forced, bn):
+    from autoformer_amd import kernels as K
+
+    torch.manual_seed(B * T + Cin)
+    M = B * T
+    x = torch.randn(M, Cin, device=DEV).bfloat16()
+    Wf = (torch.randn(Cout, 5 * Cin, device=DEV) * 0.1).bfloat16()
+    bias = torch.randn(Cout, device=DEV)
+    xp = torch.nn.functional.pad(x.float().view(B, T, Cin), (0, 0, 2, 2))
+    win = torch.cat([xp[:, k:k + T] for k in range(5)], dim=2).reshape(M, 5 * Cin)
+    ref = win @ Wf.float().t() + bias
+    outs = []
+    for mode in ((1, 128, 128, 4) if forced else (-1,), (0,)):  # ring (forced for straddling tiles), old
+        _ring(*mode)
+        y = torch.empty(M, Cout, device=DEV)
+        xo, wo = K.operand(x, Cin, window=(5, 2, T, T, Cin)), K.operand(Wf, 5 * Cin)
+        if bn:
+            p = K.bn_partial_buffer(M, Cout, DEV)
+            g_, b_ = torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV)
+            rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+            st = K.gemm(M, Cout, 5 * Cin, xo, wo, y, bias=bias, bn_partial=p, bn_fin=(g_, b_, rm, rv, None, 0.1, 1e-5, 1))
+        else:
+            st = None
+            K.gemm(M, Cout, 5 * Cin, xo, wo, y, bias=bias)
+        torch.cuda.synchronize()
+        outs.append((y, st))
+        assert _rel(y, ref) < 1e-5, mode
+        if bn:
+            assert _rel(st[0], ref.mean(0)) < 1e-5
+            assert _rel(st[1], 1 / torch.sqrt(ref.var(0, unbiased=False) + 1e-5)) < 1e-4
+
+
+@pytest.mark.parametrize("ring", [-1, 0])
+def test_gelu_epilogues(ring):
+    """c_bf16_act = GELU and act_grad_of on the ring kernel (-1: N >= 1024) and on the pass after
+    the older kernels (0)."""
+    from autoformer_amd import kernels as K
+
+    torch.manual_seed(5)
+    M, N, Kd = 1024, 1376, 344
+    a = torch.randn(M, Kd, device=DEV).bfloat16()
+    b = (torch.randn(N, Kd, device=DEV) * 0.1).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    x = torch.randn(M, N, device=DEV)
+    _ring(ring)
+    u = torch.empty(M, N, device=DEV)
+    v = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    K.gemm(M, N, Kd, K.operand(a, Kd), K.operand(b, Kd), u, bias=bias, c_bf16=v, c_bf16_act=K.ACT_GELU)
+    d = torch.empty(M, N, device=DEV)
+    d16 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    K.gemm(M, N, Kd, K.operand(a, Kd), K.operand(b, Kd), d, c_bf16=d16, act_grad_of=x)
+    torch.cuda.synchronize()
+    uref = a.float() @ b.float().t() + bias
+    assert _rel(u, uref) < 1e-5
+    assert _rel(v.float(), torch.nn.functional.gelu(uref.double())) < 1e-2
+    xd = x.double()
+    gp = 0.5 * (1 + torch.erf(xd / 2 ** 0.5)) + xd * torch.exp(-0.5 * xd * xd) / (2 * torch.pi) ** 0.5
+    dref = (a.float() @ b.float().t()).double() * gp
+    assert _rel(d, dref) < 1e-5
+    assert _rel(d16.float(), dref) < 1e-2
