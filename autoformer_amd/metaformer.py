@@ -225,10 +225,14 @@ def _token_mix_weights(mix, w1, w2, NP):
 
 def _cf_weights(mix, we, w3, w4):
     """Patch-embedding and channel-FF weights in the compute dtype (bf16 in bf16 mode, so the
-    products take the LDS-DMA bf16 kernels instead of the fp32-operand path)."""
+    products take the LDS-DMA bf16 kernels instead of the fp32-operand path), and their transposes:
+    the K-contiguous B operands of the data gradients dP = dZ we, dY2 = dU2 w3, dV2 = dZ2 w4
+    (MLPMixer.py:16-23,70-76), which as K-strided operands of the untransposed weights took the
+    register-staged kernel (3.3 ms per C4 step, profiles/r3_c4_step_breakdown.txt)."""
     def build():
         dt = K.compute()
-        return K.convert(we, dt), K.convert(w3, dt), K.convert(w4, dt)
+        return (K.convert(we, dt), K.convert(w3, dt), K.convert(w4, dt), K.transpose(we, dt), K.transpose(w3, dt),
+                K.transpose(w4, dt))
     return mix.cf_cache.get([we, w3, w4], build)
 
 
@@ -300,7 +304,7 @@ class _MLPMixerFn(torch.autograd.Function):
         D = we.shape[0]
         dev = nf.device
         P = K.twin(K.patchify(nf, B, Lf, C, ps))               # (B*NP, ps^2)
-        weC, w3C, w4C = _cf_weights(mix, we, w3, w4)
+        weC, w3C, w4C, _, _, _ = _cf_weights(mix, we, w3, w4)
         Z = _lin(P, B * NP, D, ps * ps, weC, be)                # (B*NP, D)
         Y1, m1, r1 = K.layer_norm_fwd(Z, g1, b1n, mix.ln_eps[0])
         # token mixing: UT_b (D x 4NP) = Y1_b^T . W1^T + b1   (Conv1d(NP -> 4NP, k1) on (B, NP, D)),
@@ -342,7 +346,7 @@ class _MLPMixerFn(torch.autograd.Function):
         m1, r1, m2, r2 = ctx.stats
         for t, t16 in zip((P, Y2, V2, V), ctx.twins):
             K.attach_twin(t, t16)
-        weC, w3C, w4C = _cf_weights(mix, we, w3, w4)
+        weC, w3C, w4C, weT, w3T, w4T = _cf_weights(mix, we, w3, w4)
         dev = dout.device
         dout = dout.contiguous()
         pad = wc.shape[-1] // 2
@@ -373,14 +377,14 @@ class _MLPMixerFn(torch.autograd.Function):
             K.gemm(D, 4 * D, M, operand(dZ2, D, kstrided=True), operand(V2, 4 * D, kstrided=True), dw4,
                    split_k=K.auto_split_k(D, 4 * D, M), accumulate=sink)
         dbb4 = K.colsum(dZ2, M, D, out=_sink(bb4), accumulate=sink)
-        dU2 = _dgelu_gemm(M, 4 * D, D, operand(dZ2, D), operand(w4C, 4 * D, kstrided=True), U2, dev)
+        dU2 = _dgelu_gemm(M, 4 * D, D, operand(dZ2, D), operand(w4T, D), U2, dev)
         dw3 = _sink(w3) if sink else torch.empty_like(w3)
         with _wside(side, dU2, Y2):
             K.gemm(4 * D, D, M, operand(dU2, 4 * D, kstrided=True), operand(Y2, D, kstrided=True), dw3,
                    split_k=K.auto_split_k(4 * D, D, M), accumulate=sink)
         dbb3 = K.colsum(dU2, M, 4 * D, out=_sink(bb3), accumulate=sink)
         dY2 = torch.empty(M, D, device=dev)
-        K.gemm(M, D, 4 * D, operand(dU2, 4 * D), operand(w3C, D, kstrided=True), dY2)
+        K.gemm(M, D, 4 * D, operand(dU2, 4 * D), operand(w3T, 4 * D), dY2)
         dg2, db2n = (_sink(g2), _sink(b2n)) if sink else (torch.empty(D, device=dev), torch.empty(D, device=dev))
         dZ1 = K.add(dZ2, K.layer_norm_bwd(dY2, Z1, g2, m2, r2, dg2, db2n, accumulate=sink))
         # token FF: Z1 = Z + (GELU(Y1^T W1^T + b1) W2^T + b2)^T   per utterance.  dRT_b = dZ1_b^T is
@@ -421,7 +425,7 @@ class _MLPMixerFn(torch.autograd.Function):
         dnf = None
         if ctx.needs_input_grad[0]:
             dP = torch.empty(M, pp, device=dev)
-            K.gemm(M, pp, D, operand(dZ, D), operand(weC, pp, kstrided=True), dP)
+            K.gemm(M, pp, D, operand(dZ, D), operand(weT, D), dP)
             dnf = K.patchify(dP, B, Lf, C, ps, backward=True)
         if sink:
             return (dnf, None, None, None) + (None,) * 16
