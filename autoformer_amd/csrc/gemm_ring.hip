@@ -406,8 +406,10 @@ __device__ __forceinline__ void wait_cv(bool full) {
   else wait_vm<N * (CV_LW - 1)>();
 }
 
-// ABL (timing diagnostics only, wrong results; tools/ring_ab.py --ablate): 1 = no fragment reads /
-// MFMAs (the ring's loads alone), 2 = no loads after the prologue (fragment reads + MFMAs alone)
+// ABL (timing diagnostics only, wrong results; tools/ring_ab.py): 1 = no fragment reads / MFMAs
+// (the ring's loads alone), 2 = no loads after the prologue (fragment reads + MFMAs alone),
+// 3 = the weight slices fetched as 1-KiB contiguous pieces ([Ci/32][K][Co][32] addressing applied
+// to the [Co][K][Ci] buffer: the timing of a repacked weight layout)
 template <bool ALIGNED, int ABL = 0>
 __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
   constexpr int MI = 4, NJ = 2, P = CV_NST - 1;
@@ -439,12 +441,14 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
   const int b0 = (int)fdiv((uint32_t)m0, A.tdiv);  // utterance of the tile's first row
   const bf16* src[CV_LW];
   bool sok[CV_LW];
+  long long sst[CV_LW];  // elements per stage
 #pragma unroll
   for (int i = 0; i < CV_LW; ++i) {
     const int qi = i * 8 + wid;
     const int lrow = lane >> 2, slot = lane & 3;
     src[i] = reinterpret_cast<const bf16*>(g_zero16_rg);
     sok[i] = false;
+    sst[i] = CV_CBK;
     if (qi < CV_AI) {
       const int hr = 16 * qi + lrow;  // halo row
       const int f = m0 - pad + hr;
@@ -458,18 +462,23 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
       const int wr = 16 * (qi - CV_AI) + lrow;  // weight row = tap * 128 + column
       const int tap = wr / CV_TN, n = n0 + (wr - tap * CV_TN);
       if (n < g.N) {
-        src[i] = wb + (long long)n * Bo.ld + (long long)tap * chans + 8 * (slot ^ ((wr >> 1) & 3));
+        if (ABL == 3) {
+          src[i] = wb + ((long long)tap * g.N + n) * CV_CBK + 8 * (slot ^ ((wr >> 1) & 3));
+          sst[i] = (long long)CV_TAPS * g.N * CV_CBK;
+        } else {
+          src[i] = wb + (long long)n * Bo.ld + (long long)tap * chans + 8 * (slot ^ ((wr >> 1) & 3));
+        }
         sok[i] = true;
       }
     }
   }
   auto issue = [&](int stg, int cs) {
     char* base = smem_raw + stg * CV_STAGE;
-    const int c0 = cs * CV_CBK;
 #pragma unroll
     for (int i = 0; i < CV_LW; ++i) {
       const int qi = i * 8 + wid;
-      if (qi < CV_TOT) glds16(sok[i] ? (const void*)(src[i] + c0) : (const void*)g_zero16_rg, base + qi * 1024);
+      if (qi < CV_TOT)
+        glds16(sok[i] ? (const void*)(src[i] + cs * sst[i]) : (const void*)g_zero16_rg, base + qi * 1024);
     }
   };
 
@@ -612,6 +621,7 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
       (c.mode == 1 || a.t_out % CV_TM == 0)) {
     if (c.abl == 1) launch_conv<true, 1>(g, c.gm, s);
     else if (c.abl == 2) launch_conv<true, 2>(g, c.gm, s);
+    else if (c.abl == 3) launch_conv<true, 3>(g, c.gm, s);
     else if (a.t_out % CV_TM == 0) launch_conv<true>(g, c.gm, s);
     else launch_conv<false>(g, c.gm, s);
     return true;
@@ -655,6 +665,6 @@ extern "C" int avc_gemm_set_ring(int mode, int bm, int bn, int nst, int gm, int 
   avcg::g_ring.nst = nst;
   if (gm > 0) avcg::g_ring.gm = gm;
   avcg::g_ring.win = win >= 3 ? 2 : win;
-  avcg::g_ring.abl = win >= 3 ? win - 2 : 0;  // 3: loads only, 4: reads + MFMAs only (wrong results)
+  avcg::g_ring.abl = win >= 3 ? win - 2 : 0;  // 3: loads only, 4: reads + MFMAs only, 5: contiguous weight pieces
   return 0;
 }

@@ -5,6 +5,8 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/$1
 mkdir -p $OUT
 cd $R
+timeout -k 10 200 python -u tools/ring_ab.py --only conv --reps 10 --rounds 3 \
+    --configs old,halo,auto,halo-loads,halo-math,halo-contig > $OUT/conv_abl.log 2>&1 || exit 1
 if [ "$2" != "skip-tests" ]; then
   timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -rA \
       > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }

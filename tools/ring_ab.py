@@ -65,7 +65,8 @@ CONFIGS = [("old", (0, 0, 0, 0, 0, 1)), ("auto", (-1, 0, 0, 0, 8, 1)), ("halo", 
            ("256x256x2", (1, 256, 256, 2, 8, 1)), ("128x256x3", (1, 128, 256, 3, 8, 1)),
            ("auto-gm4", (-1, 0, 0, 0, 4, 1)), ("auto-gm16", (-1, 0, 0, 0, 16, 1)),
            # timing ablations of the halo conv (wrong results): its loads alone / its reads + MFMAs alone
-           ("halo-loads", (-1, 0, 0, 0, 8, 3)), ("halo-math", (-1, 0, 0, 0, 8, 4))]
+           ("halo-loads", (-1, 0, 0, 0, 8, 3)), ("halo-math", (-1, 0, 0, 0, 8, 4)),
+           ("halo-contig", (-1, 0, 0, 0, 8, 5))]
 
 
 def main():
