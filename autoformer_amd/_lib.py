@@ -146,6 +146,7 @@ _SIGS = {
     "avc_pool3_mixer": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_patchify": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_transpose_batched": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "avc_transpose_batched2": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_moments_ws": (c_size, []),
     "avc_moments": (c_int, [c_void_p, c_ll, c_void_p, c_void_p, c_void_p]),
     "avc_moments_bwd": (c_int, [c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -275,9 +275,12 @@ __global__ void patchify_kernel(const float* nf, float* P, int L, int C, int ps,
 }
 
 // ---------------------------------------------------------------- batched transpose (+accumulate)
-__global__ void btranspose_kernel(const float* src, float* dst, int R, int C, int acc) {
+// dst[b][c][r] (+)= src[b][r][c] for r < R; dst rows are ld (>= R) long and r in [R, ld) is written
+// 0 (the zero-padded patch count of the MLP-Mixer operands).  dst (fp32) and / or dst16 (bf16,
+// the GEMM operand) -- one pass instead of a transpose followed by a pad / convert pass.
+__global__ void btranspose_kernel(const float* src, float* dst, bf16* dst16, int R, int C, int ld, int acc) {
   __shared__ float tile[32][33];
-  const long long off = (long long)blockIdx.z * R * C;
+  const long long off = (long long)blockIdx.z * R * C, doff = (long long)blockIdx.z * C * ld;
   const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   for (int y = ty; y < 32; y += 8) {
@@ -287,9 +290,14 @@ __global__ void btranspose_kernel(const float* src, float* dst, int R, int C, in
   __syncthreads();
   for (int y = ty; y < 32; y += 8) {
     const int c = c0 + y, r = r0 + tx;
-    if (c < C && r < R) {
-      float* d = dst + off + (long long)c * R + r;
-      *d = acc ? *d + tile[tx][y] : tile[tx][y];
+    if (c < C && r < ld) {
+      const long long o = doff + (long long)c * ld + r;
+      float v = tile[tx][y];
+      if (dst) {
+        if (acc) v += dst[o];
+        dst[o] = v;
+      }
+      if (dst16) dst16[o] = (bf16)v;
     }
   }
 }
@@ -372,6 +380,15 @@ extern "C" int avc_patchify(const float* src, float* dst, int B, int L, int C, i
 extern "C" int avc_transpose_batched(const float* src, float* dst, int B, int R, int C, int accumulate, void* stream) {
   AVC_CHECK_ARG(src && dst && src != dst, "avc_transpose_batched: bad args");
   dim3 g(cdiv(C, 32), cdiv(R, 32), B);
-  btranspose_kernel<<<g, 256, 0, as_stream(stream)>>>(src, dst, R, C, accumulate);
+  btranspose_kernel<<<g, 256, 0, as_stream(stream)>>>(src, dst, nullptr, R, C, R, accumulate);
   return avc_check_launch("avc_transpose_batched");
+}
+
+extern "C" int avc_transpose_batched2(const float* src, float* dst, void* dst16, int B, int R, int C, int ld,
+                                      int accumulate, void* stream) {
+  AVC_CHECK_ARG(src && (dst || dst16) && (const void*)src != (const void*)dst && ld >= R && (!accumulate || dst),
+                "avc_transpose_batched2: bad args");
+  dim3 g(cdiv(C, 32), cdiv(ld, 32), B);
+  btranspose_kernel<<<g, 256, 0, as_stream(stream)>>>(src, dst, reinterpret_cast<bf16*>(dst16), R, C, ld, accumulate);
+  return avc_check_launch("avc_transpose_batched2");
 }

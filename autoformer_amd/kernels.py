@@ -714,6 +714,20 @@ def transpose_batched(src, B, R, C, out=None, accumulate=False):
     return dst
 
 
+def transpose_pad(src, B, R, C, ld, dtype=F32, twin=False):
+    """(B*C, ld) per-utterance transpose of src (B, R, C), rows zero-padded from R to ld, in dtype;
+    twin (fp32 dtype only): the bf16 operand twin written in the same pass (avc_transpose_batched2)."""
+    if dtype == BF16:
+        out, o16 = None, torch.empty(B * C, ld, device=src.device, dtype=torch.bfloat16)
+    else:
+        out = torch.empty(B * C, ld, device=src.device)
+        o16 = _twin_buf(out, None) if twin else None
+    L.call("avc_transpose_batched2", src.data_ptr(), _ptr(out), _ptr(o16), B, R, C, int(ld), 0, stream())
+    if dtype == BF16:
+        return o16
+    return attach_twin(out, o16) if o16 is not None else out
+
+
 # ------------------------------------------------------------------------- AdaIN / Adjust variants
 def moments(x, out=None):
     """[x.mean(), x.std()] (unbiased) of the whole tensor, on device (variants.hip)."""

@@ -315,7 +315,7 @@ class _MLPMixerFn(torch.autograd.Function):
         NPp = W1T.shape[0]
         # Y1^T per utterance, (B*D, NPp): the K-contiguous A operand of UT_b = Y1T_b W1^T here and
         # the K = B*D operand of the dW1 product (backward)
-        Y1T = K.pad_cols(K.transpose_batched(Y1, B, NP, D).view(B * D, NP), NPp, dtype=K.compute())
+        Y1T = K.transpose_pad(Y1, B, NP, D, NPp, dtype=K.compute())
         bb1p = K.pad_cols(bb1.view(1, 4 * NP), 4 * NPp).view(-1)
         UT, V = _gelu_gemm(D, 4 * NPp, NPp, operand(Y1T, NPp, batch_stride=D * NPp), operand(W1n, NPp), bb1p, dev,
                            batch=B)
@@ -326,10 +326,11 @@ class _MLPMixerFn(torch.autograd.Function):
         Y2, m2, r2 = K.layer_norm_fwd(Z1, g2, b2n, mix.ln_eps[1])
         U2, V2 = _gelu_gemm(B * NP, 4 * D, D, operand(K.twin(Y2), D), operand(w3C, D), bb3, dev)
         Z2 = _lin(V2, B * NP, D, 4 * D, w4C, bb4, residual=Z1)
-        Z2T = K.transpose_batched(Z2, B, NP, D).view(B * D, NP)
         (Wf, _), wp = _out_conv_packs(mix, wc)
         if wp.shape[1] != NP:  # padded patch channels, written once in the compute dtype
-            Z2T = K.pad_cols(Z2T, wp.shape[1], dtype=K.compute())
+            Z2T = K.transpose_pad(Z2, B, NP, D, wp.shape[1], dtype=K.compute())
+        else:
+            Z2T = K.transpose_batched(Z2, B, NP, D).view(B * D, NP)
         out, _ = Lyr.conv_fwd(Z2T, B, D, wp, bc, wc.shape[-1] // 2, Wf)
         ctx.mix, ctx.dims = mix, (B, Lf, C, ps, NP, D)
         ctx.stats = (m1, r1, m2, r2)
@@ -369,7 +370,7 @@ class _MLPMixerFn(torch.autograd.Function):
                 dwc = Lyr.conv_wgrad(dout16, Z2T, B, D, D, wp, pad, into=_sink(wc))
         dbc = K.colsum(dout, B * D, wc.shape[0], out=_sink(bc), accumulate=sink)
         dZ2T = Lyr.conv_dgrad(dout, B, D, D, wp, pad, Wd, n_dx=NP)
-        dZ2 = K.twin(K.transpose_batched(dZ2T, B, D, NP).view(B * NP, D))
+        dZ2 = K.transpose_pad(dZ2T, B, D, NP, D, twin=True)
         M = B * NP
         # channel FF: Z2 = GELU(LN2(Z1) W3^T + b3) W4^T + b4 + Z1
         dw4 = _sink(w4) if sink else torch.empty_like(w4)

@@ -395,6 +395,11 @@ int avc_pool3_mixer(const float* x, float* y, int B, int L, int C, int backward,
 int avc_patchify(const float* src, float* dst, int B, int L, int C, int ps, int backward, void* stream);
 /* dst[b] (+)= src[b]^T for B row-major R x C matrices. */
 int avc_transpose_batched(const float* src, float* dst, int B, int R, int C, int accumulate, void* stream);
+/* The same transpose into rows of ld >= R elements (r in [R, ld) written 0), writing dst (fp32, nullable) and / or
+ * dst16 (bf16 GEMM operand, nullable) in one pass; accumulate needs dst (MLPMixer.py:58-92 operands with the patch
+ * count zero-padded to a multiple of 8). */
+int avc_transpose_batched2(const float* src, float* dst, void* dst16, int B, int R, int C, int ld, int accumulate,
+                           void* stream);
 
 /* Batched weight packing: every bf16 / re-laid-out copy of the parameters the kernels read
  * (conv Wf / Wd, LSTM W_ih / W_hh / W_hh^T / W_ih^T, b_ih + b_hh, linear W) rebuilt after the

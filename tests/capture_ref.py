@@ -489,6 +489,19 @@ class Capture:
                              {"out": _rel(dst.reshape(-1), ref, None if before is None else before.reshape(-1))}))
         return dst
 
+    def _transpose_pad(self, src, B, R, C, ld, dtype=K.F32, twin=False):
+        torch.cuda.synchronize()
+        out = self._orig["transpose_pad"](src, B, R, C, ld, dtype, twin)
+        torch.cuda.synchronize()
+        ref = torch.zeros(B, C, ld, dtype=torch.float64, device=src.device)
+        ref[:, :, :R] = src.double().reshape(B, R, C).transpose(1, 2)
+        ref = ref.reshape(B * C, ld)
+        res = {"out": _rel(out, ref)}
+        if getattr(out, "_bf16", None) is not None:
+            res["out_bf16"] = _rel(out._bf16, ref)
+        self.records.append(("btranspose", f"transpose_pad B{B} R{R} C{C} ld{ld}", res))
+        return out
+
     # ---------------------------------------------------------------- discriminator head (C5)
     def _disc_dense_fwd(self, a, w, bias, B, nl, nc):
         torch.cuda.synchronize()
@@ -577,7 +590,7 @@ class Capture:
         for name in ("gemm", "lstm_fwd", "lstm2_fwd", "lstm_bwd", "bn_apply", "bn_bwd", "expand_codes",
                      "conv_edge_table", "conv_edge_colsum", "group_norm_fwd", "group_norm_bwd", "layer_norm_fwd",
                      "layer_norm_bwd", "gelu_fwd_operand", "gelu_bwd_twin", "pool3_mixer", "patchify",
-                     "transpose_batched", "disc_dense_fwd", "disc_dense_bwd", "vc_loss", "vc_loss_grad", "bce_loss",
+                     "transpose_batched", "transpose_pad", "disc_dense_fwd", "disc_dense_bwd", "vc_loss", "vc_loss_grad", "bce_loss",
                      "bce_grad", "adam"):
             self._orig[name] = getattr(K, name)
             setattr(K, name, getattr(self, "_" + name))
