@@ -29,6 +29,8 @@
 // Epilogue: bias, conv0-fold row bias, residual, accumulate / split-K atomics, fp32 C and / or
 // bf16 twin, conv weight-layout permutation, BatchNorm partial statistics per 128-row tile and
 // the finalize by the last-arriving row tile (the semantics of gemm_internal.h:fast_epilogue).
+#include <algorithm>
+
 #include "gemm_internal.h"
 
 namespace avcg {
@@ -128,8 +130,83 @@ __device__ __forceinline__ bool ring_arrive_last(unsigned* cnt, unsigned arrival
   return *flag != 0;
 }
 
-// Epilogue for the 2 x 4 wave layout: wave (wm, wn) owns rows m0 + wm*TWM + i*16 + 4*(lane>>4) + e
-// and columns n0 + wn*TWN + j*16 + (lane&15).
+// LDS bytes the staged stores need (ring_store_tile): per wave 64 rows x (TWN + 4) fp32
+template <int BM_, int BN_>
+constexpr size_t ring_epi_lds() {
+  return (size_t)8 * 64 * (BN_ / 4 + 4) * 4;
+}
+
+// Stores of the 2 x 4 wave layout's accumulators (wave (wm, wn) owns rows m0 + wm*TWM + i*16 +
+// 4*(lane>>4) + e and columns n0 + wn*TWN + j*16 + (lane&15)): each wave stages 64-row chunks of
+// its tile in its own LDS region and stores them row-contiguous, 16 B per lane (fp32 C) / 8 B
+// (bf16), with the residual, accumulate and GELU epilogues applied per 4-column vector and their
+// uniform conditions tested once per vector, not per element (the per-element form carried ~1,800
+// uniform branches per 256 x 256 tile: 60 -> 90 us on the 8192 x 4096 x 512 projection).
+// Column tails and row strides that are not 16-B multiples take the per-element path.
+template <int BM_, int BN_>
+__device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[BM_ / 32][BN_ / 64], int m0, int n0,
+                                                int bz, int ks, char* smem_raw) {
+  constexpr int TWM = BM_ / 2, TWN = BN_ / 4, NJ = TWN / 16, RP = TWN + 4, NIT = TWN / 4;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  float* reg = reinterpret_cast<float*>(smem_raw) + wid * 64 * RP;
+  float* C = g.c ? g.c + (long long)bz * g.cbs : nullptr;
+  bf16* C16 = g.c16 ? g.c16 + (long long)bz * g.cbs : nullptr;
+  const float* res = (g.res && ks == 0) ? g.res + (long long)bz * g.cbs : nullptr;
+  const float* agr = g.agrad ? g.agrad + (long long)bz * g.cbs : nullptr;
+  const bool vec = (g.ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(C16) & 7) == 0 && (reinterpret_cast<uintptr_t>(res) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(agr) & 15) == 0;
+  const bool acc_c = g.accumulate != 0, gelu16 = g.c16_act != 0;
+#pragma unroll
+  for (int ch = 0; ch < TWM / 64; ++ch) {
+    // this wave's rows ch*64 .. +64 -> its LDS region (the region is the wave's own: the read below
+    // only needs the wave's LDS writes retired, which the barrier also guarantees)
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          reg[(ii * 16 + 4 * (lane >> 4) + e) * RP + j * 16 + (lane & 15)] = acc[ch * 4 + ii][j][e];
+    __syncthreads();
+#pragma unroll 4
+    for (int it = 0; it < NIT; ++it) {
+      const int q = it * 64 + lane, lr = q / (TWN / 4), c4 = q - lr * (TWN / 4);
+      const int row = m0 + wm * TWM + ch * 64 + lr, col = n0 + wn * TWN + 4 * c4;
+      if (row >= g.M || col >= g.N) continue;
+      f32x4 v = *reinterpret_cast<const f32x4*>(reg + lr * RP + 4 * c4);
+      const long long o = (long long)row * g.ldc + col;
+      if (vec && col + 3 < g.N) {
+        if (res) v += *reinterpret_cast<const f32x4*>(res + o);
+        if (acc_c) v += *reinterpret_cast<const f32x4*>(C + o);
+        if (agr) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(agr + o);
+          v = f32x4{v[0] * gelu_grad_f(x[0]), v[1] * gelu_grad_f(x[1]), v[2] * gelu_grad_f(x[2]),
+                    v[3] * gelu_grad_f(x[3])};
+        }
+        if (C) *reinterpret_cast<f32x4*>(C + o) = v;
+        if (C16) {
+          const f32x4 w = gelu16 ? f32x4{gelu_f(v[0]), gelu_f(v[1]), gelu_f(v[2]), gelu_f(v[3])} : v;
+          *reinterpret_cast<bf16x4*>(C16 + o) = bf16x4{(bf16)w[0], (bf16)w[1], (bf16)w[2], (bf16)w[3]};
+        }
+      } else {
+        for (int k = 0; k < 4 && col + k < g.N; ++k) {
+          float x = v[k];
+          if (res) x += res[o + k];
+          if (acc_c) x += C[o + k];
+          if (agr) x *= gelu_grad_f(agr[o + k]);
+          if (C) C[o + k] = x;
+          if (C16) C16[o + k] = (bf16)(gelu16 ? gelu_f(x) : x);
+        }
+      }
+    }
+    __syncthreads();  // the region is rewritten by the next chunk / reused by the BN epilogue
+  }
+}
+
+// Epilogue for the 2 x 4 wave layout (see ring_store_tile): bias and conv0-fold row bias in the
+// accumulators, the staged stores, then the BatchNorm partial statistics / finalize.
 template <int BM_, int BN_>
 __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM_ / 32][BN_ / 64], int m0, int n0,
                                               int bz, int ks, char* smem_raw) {
@@ -138,8 +215,6 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
   const int wm = wid >> 2, wn = wid & 3;
   const int rbase = m0 + wm * TWM + 4 * (lane >> 4);
   const int cbase = n0 + wn * TWN + (lane & 15);
-  float* C = g.c ? g.c + (long long)bz * g.cbs : nullptr;
-  bf16* C16 = g.c16 ? g.c16 + (long long)bz * g.cbs : nullptr;
   if (g.bias && ks == 0) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -167,29 +242,7 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
         }
       }
   }
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = rbase + i * 16 + e;
-      if (row >= g.M) continue;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int col = cbase + j * 16;
-        if (col >= g.N) continue;
-        const long long o = (long long)row * g.ldc + out_col(g, col);
-        float v = acc[i][j][e];
-        if (g.res && ks == 0) v += g.res[(long long)bz * g.cbs + o];
-        if (g.atomic) {
-          atomicAdd(C + o, v);
-        } else {
-          if (g.accumulate) v += C[o];
-          if (g.agrad) v *= gelu_grad_f(g.agrad[(long long)bz * g.cbs + o]);
-          if (C) C[o] = v;
-          if (C16) C16[o] = (bf16)(g.c16_act ? gelu_f(v) : v);
-        }
-      }
-    }
+  ring_store_tile<BM_, BN_>(g, acc, m0, n0, bz, ks, smem_raw);
   if (g.bn_partial) {
     // per 128-row statistics tile: column sum and M2 about the tile mean (Chan's form, merged by
     // the finalize).  Waves w with (w's rows)/128 == h contribute to tile h of this workgroup.
@@ -369,7 +422,7 @@ __global__ void __launch_bounds__(RNT, 2) gemm_ring_kernel(GemmArgs g, int gm) {
 
 template <int BM_, int BN_, int NST, bool WIN>
 void launch(const GemmArgs& g, int gm, hipStream_t s) {
-  const size_t lds = (size_t)NST * (BM_ + BN_) * RROW;
+  const size_t lds = std::max((size_t)NST * (BM_ + BN_) * RROW, ring_epi_lds<BM_, BN_>());
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ring_kernel<BM_, BN_, NST, WIN>),
@@ -556,7 +609,7 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
 
 template <bool ALIGNED, int ABL = 0>
 void launch_conv(const GemmArgs& g, int gm, hipStream_t s) {
-  const size_t lds = (size_t)CV_NST * CV_STAGE;
+  const size_t lds = std::max((size_t)CV_NST * CV_STAGE, ring_epi_lds<CV_TM, CV_TN>());
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<ALIGNED, ABL>),
@@ -608,7 +661,7 @@ RingCfg g_ring = init_cfg();
 bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
   const RingCfg& c = g_ring;
   if (c.mode == 0 || (g.a.win && !c.win)) return false;
-  if (g.K % 8 || g.klen % RBK || g.bnb_ws) return false;
+  if (g.K % 8 || g.klen % RBK || g.bnb_ws || g.atomic || g.cperm) return false;  // (no atomic / cperm stores)
   if (!operand_ok(g.a, true) || !operand_ok(g.b, false)) return false;
   const long long units = (long long)g.batch * g.split_k;
   const bool win = g.a.win != 0;

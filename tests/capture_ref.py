@@ -457,9 +457,10 @@ class Capture:
 
         if not backward:
             ref = fwd(xin)
-        else:  # the adjoint of the forward map applied to dy
-            z = torch.zeros_like(xin, requires_grad=True)
-            ref = torch.autograd.grad(fwd(z), z, grad_outputs=xin)[0]
+        else:  # the adjoint of the forward map applied to dy (this runs inside autograd's backward)
+            with torch.enable_grad():
+                z = torch.zeros_like(xin, requires_grad=True)
+                ref = torch.autograd.grad(fwd(z), z, grad_outputs=xin)[0]
         ref = ref.permute(0, 2, 1).reshape_as(y)
         self.records.append(("pool3", f"pool3 B{B} L{Lf} C{C}" + (" bwd" if backward else ""), {"y": _rel(y, ref)}))
         return y
