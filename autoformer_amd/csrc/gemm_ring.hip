@@ -30,6 +30,7 @@
 // bf16 twin, conv weight-layout permutation, BatchNorm partial statistics per 128-row tile and
 // the finalize by the last-arriving row tile (the semantics of gemm_internal.h:fast_epilogue).
 #include <algorithm>
+#include <type_traits>
 
 #include "gemm_internal.h"
 
@@ -53,6 +54,32 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// LDS byte address of a pointer into the kernel's dynamic LDS array
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+// 16-B fragment read issued as inline asm: hipcc's waitcnt pass does not track it, so the caller
+// places counted `s_waitcnt lgkmcnt` (+ sched_barrier, cdna_hip_programming.md §5.4 rule 18)
+template <int OFF>
+__device__ __forceinline__ bf16x8 ds_read16(unsigned addr) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+  return __builtin_bit_cast(bf16x8, v);
+}
+// N reads at BASE, BASE + STRIDE, ... bytes from addr into d[0..N)
+template <int N, int STRIDE, int BASE = 0>
+__device__ __forceinline__ void ds_read_n(bf16x8* d, unsigned addr) {
+  if constexpr (N > 0) {
+    d[0] = ds_read16<BASE>(addr);
+    ds_read_n<N - 1, STRIDE, BASE + STRIDE>(d + 1, addr);
+  }
+}
+template <int N>
+__device__ __forceinline__ void wait_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 // R rows x 64 K of one operand per slot: R/64 glds per thread.  Instruction i of wave w covers
 // slot rows (8i + w)*8 .. +8; lane L writes row +(L>>3), 16-B slot L&7, which holds global K
@@ -400,21 +427,42 @@ __global__ void __launch_bounds__(RNT, 2) gemm_ring_kernel(GemmArgs g, int gm) {
       la.issue(st, kbeg + (kt + P) * RBK, kend, cdv);
       lb.issue(st + A_BYTES, kbeg + (kt + P) * RBK, kend, cdv);
     }
-    const char* st = smem_raw + (kt % NST) * STAGE;
+    // One K-step = two 32-deep halves h; fragments read by inline asm with counted waits so that
+    // the next group's reads are in flight while the current group's MFMAs issue (hipcc's own
+    // schedule re-used one register set and drained lgkmcnt(0) before every MFMA group):
+    //   read B(h0), A(h0) rows 0..MI/2, A(h0) rows MI/2..MI | MFMA h0 first half
+    //   read B(h1), A(h1) first half                       | MFMA h0 second half
+    //   read A(h1) second half                             | MFMA h1 first half | MFMA h1 second half
+    constexpr int MH = MI / 2;
+    const unsigned st = lds_addr(smem_raw + (kt % NST) * STAGE);
+    const unsigned a0 = st + aoff + ch0, a1 = st + aoff + ch1, b0 = st + boff + ch0, b1 = st + boff + ch1;
+    bf16x8 af0[MI], bf0[NJ], af1[MI], bf1[NJ];
+    auto mfma_rows = [&](const bf16x8* af, const bf16x8* bfr, auto i0c) {
+      constexpr int I0 = decltype(i0c)::value;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int co = h ? ch1 : ch0;
-      bf16x8 af[MI], bfr[NJ];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(st + boff + j * 16 * RROW + co);
-#pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(st + aoff + i * 16 * RROW + co);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
+      for (int i = 0; i < MH; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
+          acc[I0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[I0 + i], bfr[j], acc[I0 + i][j], 0, 0, 0);
+    };
+    using Z0 = std::integral_constant<int, 0>;
+    using ZH = std::integral_constant<int, MH>;
+    ds_read_n<NJ, 16 * RROW>(bf0, b0);
+    ds_read_n<MH, 16 * RROW>(af0, a0);
+    ds_read_n<MH, 16 * RROW, MH * 16 * RROW>(af0 + MH, a0);
+    wait_lgkm<MH>();
+    mfma_rows(af0, bf0, Z0{});
+    __builtin_amdgcn_sched_barrier(0);
+    ds_read_n<NJ, 16 * RROW>(bf1, b1);
+    ds_read_n<MH, 16 * RROW>(af1, a1);
+    wait_lgkm<NJ + MH>();
+    mfma_rows(af0, bf0, ZH{});
+    __builtin_amdgcn_sched_barrier(0);
+    ds_read_n<MH, 16 * RROW, MH * 16 * RROW>(af1 + MH, a1);
+    wait_lgkm<MH>();
+    mfma_rows(af1, bf1, Z0{});
+    wait_lgkm<0>();
+    mfma_rows(af1, bf1, ZH{});
   }
   __syncthreads();  // every glds retired (the last wait was vmcnt(0)) and every fragment read done
   ring_epilogue<BM_, BN_>(g, acc, m0, n0, bz, ks, smem_raw);
@@ -579,29 +627,54 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
     raw_barrier();
     if (ABL != 2 && cs + P < nst) issue((cs + P) % CV_NST, cs + P);
     if (ABL == 1) continue;
-    const char* st = smem_raw + (cs % CV_NST) * CV_STAGE;
+    const unsigned st = lds_addr(smem_raw + (cs % CV_NST) * CV_STAGE);
     bf16x8 af[2][MI], bfr[2][NJ];
-    auto read_tap = [&](int k, int slot) {
+    auto read_tap = [&](auto kc, int slot) {
+      constexpr int k = decltype(kc)::value;
+      const unsigned a0 = st + aaddr[k], b0 = st + baddr;
+      af[slot][0] = ds_read16<0>(a0);
+      af[slot][1] = ds_read16<1024>(a0);
+      af[slot][2] = ds_read16<2048>(a0);
+      af[slot][3] = ds_read16<3072>(a0);
+      bfr[slot][0] = ds_read16<(k * CV_TN) * 64>(b0);
+      bfr[slot][1] = ds_read16<(k * CV_TN + 16) * 64>(b0);
+    };
+    auto mfma_tap = [&](auto kc, int slot) {
+      constexpr int k = decltype(kc)::value;
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(st + aaddr[k] + i * 1024);
-        af[slot][i] = (ALIGNED || ((vmask >> (i * 8 + k)) & 1u)) ? v : bf16x8{};
+        const bf16x8 av = (ALIGNED || ((vmask >> (i * 8 + k)) & 1u)) ? af[slot][i] : bf16x8{};
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bfr[slot][j], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        bfr[slot][j] = *reinterpret_cast<const bf16x8*>(st + baddr + (k * CV_TN + j * 16) * 64);
     };
-    read_tap(0, 0);
-#pragma unroll
-    for (int k = 0; k < CV_TAPS; ++k) {
-      const int slot = k & 1;
-      if (k + 1 < CV_TAPS) read_tap(k + 1, slot ^ 1);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[slot][i], bfr[slot][j], acc[i][j], 0, 0, 0);
-    }
+    // Software pipeline with inline-asm fragment reads and counted waits: tap k+1's six reads are
+    // in flight while tap k's eight MFMAs issue (the wave waits only for tap k's reads).  Left to
+    // itself hipcc re-used one register set and waited lgkmcnt(0) twice per tap -- two exposed
+    // LDS round trips per tap, 23.5 us of the conv in its reads + MFMAs alone (tools/ring_ab.py).
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    read_tap(I0{}, 0);
+    read_tap(I1{}, 1);
+    wait_lgkm<6>();
+    mfma_tap(I0{}, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_tap(I2{}, 0);
+    wait_lgkm<6>();
+    mfma_tap(I1{}, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    read_tap(I3{}, 1);
+    wait_lgkm<6>();
+    mfma_tap(I2{}, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_tap(I4{}, 0);
+    wait_lgkm<6>();
+    mfma_tap(I3{}, 1);
+    wait_lgkm<0>();
+    mfma_tap(I4{}, 0);
   }
   __syncthreads();
   ring_epilogue<CV_TM, CV_TN>(g, acc, m0, n0, 0, 0, smem_raw);

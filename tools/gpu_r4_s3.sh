@@ -7,6 +7,8 @@ mkdir -p $OUT
 cd $R
 timeout -k 10 200 python -u tools/ring_ab.py --only conv --reps 10 --rounds 3 \
     --configs old,halo,auto,halo-loads,halo-math,halo-contig > $OUT/conv_abl.log 2>&1 || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ring.py -x -q --timeout 120 --timeout-method thread \
+    > $OUT/ring_tests.log 2>&1 || { tail -30 $OUT/ring_tests.log; exit 1; }
 if [ "$2" != "skip-tests" ]; then
   timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -rA \
       > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }
