@@ -26,4 +26,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
     python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-kernel-timing > $OUT/prof.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c4 -o run -- \
     python3 $R/bench.py --model MetaConv --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing > $OUT/prof_c4.log 2>&1 || exit 1
+for d in prof prof_c4; do
+  python3 $R/tools/step_breakdown.py $OUT/$d/run_kernel_trace.csv 40 > $OUT/${d}_breakdown.txt 2>&1
+  cp $OUT/$d/run_kernel_stats.csv $OUT/${d}_kernel_stats.csv 2>/dev/null
+  rm -rf $OUT/$d
+done
 grep -o '"ms_per_step": [0-9.]*' $OUT/*.json
