@@ -23,6 +23,16 @@ def set_compute(name: str) -> None:
     _COMPUTE = {"bf16": BF16, "fp32": F32}[name]
 
 
+_DETERMINISTIC = False
+
+
+def set_deterministic(on: bool) -> None:
+    """Run-to-run bitwise reproducible gradients (tests): every GEMM without split-K, so no output
+    is a sum of float atomics in arrival order.  Slower weight-gradient products; off by default."""
+    global _DETERMINISTIC
+    _DETERMINISTIC = bool(on)
+
+
 def compute() -> int:
     return _COMPUTE
 
@@ -94,6 +104,8 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     c_bf16_act = ACT_GELU: c_bf16 receives GELU(C); act_grad_of = x: C *= GELU'(x) (and its twin) --
     the MLP-Mixer GELU forward / backward folded into the GEMM epilogue (avc_gemm_desc)."""
     _dev(c, bias, bn_partial, c_bf16, residual)
+    if _DETERMINISTIC:
+        split_k = 1
     if c.dtype == torch.bfloat16:  # bf16-only output
         assert c_bf16 is None and not accumulate and split_k == 1 and not cperm
         c, c_bf16 = None, c
