@@ -35,7 +35,8 @@ class GemmDesc(ctypes.Structure):
                 ("c", c_void_p), ("ldc", c_ll), ("c_batch_stride", c_ll), ("bias", c_void_p),
                 ("accumulate", c_int), ("split_k", c_int), ("bn_partial", c_void_p), ("compute", c_int),
                 ("c_bf16", c_void_p), ("residual", c_void_p), ("cperm", c_int), ("row_bias", c_void_p),
-                ("rb_t", c_int), ("rb_pad", c_int), ("c_bf16_act", c_int), ("act_grad_of", c_void_p)]
+                ("rb_t", c_int), ("rb_pad", c_int), ("c_bf16_act", c_int), ("act_grad_of", c_void_p),
+                ("col_sum", c_void_p), ("col_sum_n", c_int)]
 
 
 class BnFin(ctypes.Structure):

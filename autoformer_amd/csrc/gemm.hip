@@ -724,9 +724,14 @@ struct GeluPost {
   int act = 0;
   const float* agrad = nullptr;
   bf16* c16 = nullptr;
+  float* csum = nullptr;
+  int csum_n = 0;
 };
 static GeluPost strip_gelu(GemmArgs& g) {
   GeluPost p;
+  p.csum = g.csum;
+  p.csum_n = g.csum_n;
+  g.csum = nullptr;
   if (!g.c16_act && !g.agrad) return p;
   p.act = g.c16_act;
   p.agrad = g.agrad;
@@ -736,10 +741,25 @@ static GeluPost strip_gelu(GemmArgs& g) {
   g.c16 = nullptr;
   return p;
 }
+// column sums of C (rows ldc apart) added into out[n], n < nc: 256 columns x 64 rows per block
+__global__ void colsum_atomic_kernel(const float* c, long long ldc, int M, int nc, float* out) {
+  const int col = blockIdx.x * 256 + threadIdx.x, r0 = blockIdx.y * 64;
+  if (col >= nc) return;
+  float s = 0.f;
+  for (int r = r0; r < min(M, r0 + 64); ++r) s += c[(long long)r * ldc + col];
+  atomicAdd(out + col, s);
+}
 static int gelu_after(const GemmArgs& g, const GeluPost& p, hipStream_t s) {
   const long long n = (long long)g.M * g.N * g.batch;
-  if (p.agrad) return avc_gelu_twin(g.c, p.agrad, g.c, p.c16, n, 1, s);  // C *= GELU'(x), twin
-  if (p.act) return avc_gelu_twin(nullptr, g.c, nullptr, p.c16, n, 0, s);  // twin = GELU(C)
+  int rc = 0;
+  if (p.agrad) rc = avc_gelu_twin(g.c, p.agrad, g.c, p.c16, n, 1, s);  // C *= GELU'(x), twin
+  else if (p.act) rc = avc_gelu_twin(nullptr, g.c, nullptr, p.c16, n, 0, s);  // twin = GELU(C)
+  if (rc) return rc;
+  if (p.csum) {
+    const int nc = p.csum_n > 0 ? p.csum_n : g.N, rows = g.M * g.batch;
+    colsum_atomic_kernel<<<dim3(cdiv(nc, 256), cdiv(rows, 64)), 256, 0, s>>>(g.c, g.ldc, rows, nc, p.csum);
+    return avc_check_launch("avc_gemm(col_sum)");
+  }
   return 0;
 }
 
@@ -787,6 +807,12 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
   g.cpd = make_fastdiv(g.cperm ? (uint32_t)(d->N / g.cperm) : 1u);
   g.c16_act = d->c_bf16_act;
   g.agrad = d->act_grad_of;
+  g.csum = d->col_sum;
+  g.csum_n = d->col_sum_n;
+  AVC_CHECK_ARG(!g.csum || (d->c && !d->accumulate && g.split_k == 1 && !d->cperm &&
+                            (g.batch == 1 || d->c_batch_stride == (long long)d->M * d->ldc) &&
+                            d->col_sum_n >= 0 && d->col_sum_n <= d->N),
+                "avc_gemm: col_sum needs an fp32 C, no accumulate / split-K / batch sum / cperm, col_sum_n <= N");
   AVC_CHECK_ARG(g.c16_act == 0 || g.c16_act == AVC_ACT_GELU, "avc_gemm: c_bf16_act must be 0 or AVC_ACT_GELU");
   AVC_CHECK_ARG(!(g.c16_act || g.agrad) ||
                     (d->c && d->ldc == d->N && (g.batch == 1 || d->c_batch_stride == (long long)d->M * d->N) &&

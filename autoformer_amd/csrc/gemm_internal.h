@@ -33,6 +33,8 @@ struct GemmArgs {
   FastDiv cpd;   // divide a column by chans = N / cperm
   int c16_act;         // avc_gemm_desc.c_bf16_act: C16 holds GELU(C) (ring kernels only)
   const float* agrad;  // avc_gemm_desc.act_grad_of: C *= GELU'(agrad[o]) (ring kernels only)
+  float* csum;         // avc_gemm_desc.col_sum: csum[n] += column sums of the stored C (ring kernels only)
+  int csum_n;
   const float* rbias;  // per-(utterance, edge class) row bias (avc_gemm_desc.row_bias), nullable
   int rb_t, rb_pad;
   FastDiv rb_div;      // divide a row by rb_t

@@ -185,6 +185,9 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
                    (reinterpret_cast<uintptr_t>(C16) & 7) == 0 && (reinterpret_cast<uintptr_t>(res) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(agr) & 15) == 0;
   const bool acc_c = g.accumulate != 0, gelu16 = g.c16_act != 0;
+  float* csum = g.csum;
+  // column-sum epilogue: lane's 4 columns are the same for every iteration (64 % (TWN/4) == 0)
+  f32x4 cs = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ch = 0; ch < TWM / 64; ++ch) {
     // this wave's rows ch*64 .. +64 -> its LDS region (the region is the wave's own: the read below
@@ -213,6 +216,7 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
                     v[3] * gelu_grad_f(x[3])};
         }
         if (C) *reinterpret_cast<f32x4*>(C + o) = v;
+        if (csum) cs += v;
         if (C16) {
           const f32x4 w = gelu16 ? f32x4{gelu_f(v[0]), gelu_f(v[1]), gelu_f(v[2]), gelu_f(v[3])} : v;
           *reinterpret_cast<bf16x4*>(C16 + o) = bf16x4{(bf16)w[0], (bf16)w[1], (bf16)w[2], (bf16)w[3]};
@@ -224,11 +228,26 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
           if (acc_c) x += C[o + k];
           if (agr) x *= gelu_grad_f(agr[o + k]);
           if (C) C[o + k] = x;
+          if (csum) cs[k] += x;
           if (C16) C16[o + k] = (bf16)(gelu16 ? gelu_f(x) : x);
         }
       }
     }
     __syncthreads();  // the region is rewritten by the next chunk / reused by the BN epilogue
+  }
+  if (csum) {
+    // lanes sharing this lane's 4 columns: lane + k * (TWN/4)
+#pragma unroll
+    for (int sh = TWN / 4; sh < 64; sh *= 2)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cs[k] += __shfl_xor(cs[k], sh, 64);
+    if (lane < TWN / 4) {
+      const int col = n0 + wn * TWN + 4 * lane;
+      const int lim = g.csum_n > 0 ? g.csum_n : g.N;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (col + k < lim) atomicAdd(csum + col + k, cs[k]);
+    }
   }
 }
 

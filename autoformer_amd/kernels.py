@@ -92,7 +92,7 @@ def operand(t: torch.Tensor, ld: int, kstrided: bool = False, window=None, batch
 
 def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=None, accumulate=False, split_k=1,
          bn_partial=None, batch=1, c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0, bn_fin=None,
-         bnb=None, row_bias=None, c_bf16_act=0, act_grad_of=None):
+         bnb=None, row_bias=None, c_bf16_act=0, act_grad_of=None, col_sum=None, col_sum_n=0):
     """cperm = taps > 1: C's columns are (tap, channel) pairs written in nn.Conv1d's [Co][Ci][K]
     weight layout (a conv weight gradient straight into .grad).
     bn_fin = (gamma, beta, running_mean, running_var, nbt, momentum, eps, nupd): the BatchNorm
@@ -102,7 +102,8 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     backward statistics (avc_gemm_bnb: coef[6][N] and the parameter gradients).
     row_bias = (S, T, pad): S[(b*(2 pad + 1) + edge class)][N] added to row b*T + t (the conv0 fold).
     c_bf16_act = ACT_GELU: c_bf16 receives GELU(C); act_grad_of = x: C *= GELU'(x) (and its twin) --
-    the MLP-Mixer GELU forward / backward folded into the GEMM epilogue (avc_gemm_desc)."""
+    the MLP-Mixer GELU forward / backward folded into the GEMM epilogue (avc_gemm_desc).
+    col_sum: col_sum[:col_sum_n or N] += column sums of C (a bias gradient, float atomics)."""
     _dev(c, bias, bn_partial, c_bf16, residual)
     if _DETERMINISTIC:
         split_k = 1
@@ -126,6 +127,9 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     d.residual = _ptr(residual)
     d.cperm = int(cperm)
     d.c_bf16_act = int(c_bf16_act)
+    if col_sum is not None:
+        _dev(col_sum)
+        d.col_sum, d.col_sum_n = col_sum.data_ptr(), int(col_sum_n)
     if act_grad_of is not None:
         _dev(act_grad_of)
         d.act_grad_of = act_grad_of.data_ptr()

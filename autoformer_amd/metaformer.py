@@ -279,15 +279,27 @@ def _gelu_gemm(M, N, Kd, a, b, bias, dev, batch=1):
     return U, V
 
 
-def _dgelu_gemm(M, N, Kd, a, b, U, dev, batch=1):
+def _dgelu_gemm(M, N, Kd, a, b, U, dev, batch=1, bias_grad=None):
     """dU = (a . b^T) * GELU'(U), fp32 with its bf16 operand twin (bf16 mode: in the GEMM epilogue,
-    avc_gemm_desc.act_grad_of)."""
+    avc_gemm_desc.act_grad_of).  bias_grad = (out, n, accumulate): out[:n] (+)= the column sums of
+    dU, the bias gradient of the GELU's linear layer -- in bf16 mode in the same epilogue
+    (avc_gemm_desc.col_sum) instead of a colsum pass that re-reads dU."""
     dU = torch.empty(batch * M, N, device=dev)
     if K.compute() != K.BF16:
         K.gemm(M, N, Kd, a, b, dU, batch=batch, c_batch_stride=M * N)
-        return K.gelu_bwd_twin(dU, U)
+        dU = K.gelu_bwd_twin(dU, U)
+        if bias_grad is not None:
+            out, n, acc = bias_grad
+            K.colsum(dU, batch * M, n, ld=N, out=out, accumulate=acc)
+        return dU
     d16 = torch.empty(batch * M, N, device=dev, dtype=torch.bfloat16)
-    K.gemm(M, N, Kd, a, b, dU, batch=batch, c_batch_stride=M * N, c_bf16=d16, act_grad_of=U)
+    kw = {}
+    if bias_grad is not None:
+        out, n, acc = bias_grad
+        if not acc:
+            out.zero_()
+        kw = dict(col_sum=out, col_sum_n=n)
+    K.gemm(M, N, Kd, a, b, dU, batch=batch, c_batch_stride=M * N, c_bf16=d16, act_grad_of=U, **kw)
     return K.attach_twin(dU, d16)
 
 
@@ -378,12 +390,12 @@ class _MLPMixerFn(torch.autograd.Function):
             K.gemm(D, 4 * D, M, operand(dZ2, D, kstrided=True), operand(V2, 4 * D, kstrided=True), dw4,
                    split_k=K.auto_split_k(D, 4 * D, M), accumulate=sink)
         dbb4 = K.colsum(dZ2, M, D, out=_sink(bb4), accumulate=sink)
-        dU2 = _dgelu_gemm(M, 4 * D, D, operand(dZ2, D), operand(w4T, D), U2, dev)
+        dbb3 = _sink(bb3) if sink else torch.empty(4 * D, device=dev)
+        dU2 = _dgelu_gemm(M, 4 * D, D, operand(dZ2, D), operand(w4T, D), U2, dev, bias_grad=(dbb3, 4 * D, sink))
         dw3 = _sink(w3) if sink else torch.empty_like(w3)
         with _wside(side, dU2, Y2):
             K.gemm(4 * D, D, M, operand(dU2, 4 * D, kstrided=True), operand(Y2, D, kstrided=True), dw3,
                    split_k=K.auto_split_k(4 * D, D, M), accumulate=sink)
-        dbb3 = K.colsum(dU2, M, 4 * D, out=_sink(bb3), accumulate=sink)
         dY2 = torch.empty(M, D, device=dev)
         K.gemm(M, D, 4 * D, operand(dU2, 4 * D), operand(w3T, 4 * D), dY2)
         dg2, db2n = (_sink(g2), _sink(b2n)) if sink else (torch.empty(D, device=dev), torch.empty(D, device=dev))
@@ -403,14 +415,14 @@ class _MLPMixerFn(torch.autograd.Function):
             K.gemm(NPp, 4 * NPp, B * D, operand(dRTp, NPp, kstrided=True), operand(V, 4 * NPp, kstrided=True), dW2p,
                    split_k=K.auto_split_k(NPp, 4 * NPp, B * D))
             dW2 = K.crop_add(dW2p[:NP], _sink(w2).view(NP, 4 * NP)) if sink else K.pad_cols(dW2p, 4 * NP)[:NP]
+        dbb1 = _sink(bb1) if sink else torch.empty(4 * NP, device=dev)
         dUT = _dgelu_gemm(D, 4 * NPp, NPp, operand(dRTp, NPp, batch_stride=D * NPp), operand(W2t, NPp), UT, dev,
-                          batch=B)
+                          batch=B, bias_grad=(dbb1, 4 * NP, sink))
         with _wside(side, dUT, Y1T):
             dW1p = torch.empty(4 * NPp, NPp, device=dev)
             K.gemm(4 * NPp, NPp, B * D, operand(dUT, 4 * NPp, kstrided=True), operand(Y1T, NPp, kstrided=True),
                    dW1p, split_k=K.auto_split_k(4 * NPp, NPp, B * D))
             dW1 = K.crop_add(dW1p[:4 * NP], _sink(w1).view(4 * NP, NP)) if sink else K.pad_cols(dW1p, NP)[:4 * NP]
-        dbb1 = K.colsum(dUT, B * D, 4 * NP, ld=4 * NPp, out=_sink(bb1), accumulate=sink)
         dY1T = torch.empty(B * D, NP, device=dev)
         K.gemm(B * D, NP, 4 * NPp, operand(dUT, 4 * NPp), operand(W1T, 4 * NPp), dY1T)
         dY1 = K.transpose_batched(dY1T, B, D, NP).view(M, D)

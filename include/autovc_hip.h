@@ -85,6 +85,11 @@ typedef struct {
                             Needs c and c_bf16, ldc == N, no accumulate / split-K / batch sum / cperm */
   const float* act_grad_of; /* nullable: C = (A.B + bias) * GELU'(act_grad_of[m*ldc + n]) and its bf16 twin -- the
                             GELU backward folded into the data-gradient GEMM.  Same restrictions, no residual */
+  float* col_sum;        /* nullable: col_sum[n] += sum over m of the stored C[m][n], n < col_sum_n (0 = N) -- the
+                            bias gradient of the layer whose output gradient C is (MLPMixer.py:16-23), without a
+                            second pass over C.  Float atomics (order-dependent rounding); needs an fp32 C, no
+                            accumulate / split-K / batch sum / cperm */
+  int col_sum_n;
 } avc_gemm_desc;
 
 int avc_abi_version(void);

@@ -186,11 +186,12 @@ class Capture:
     # ---------------------------------------------------------------- wrappers
     def _gemm(self, M, N, Kd, a, b, c, ldc=None, bias=None, accumulate=False, split_k=1, bn_partial=None, batch=1,
               c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0, bn_fin=None, bnb=None, row_bias=None,
-              c_bf16_act=0, act_grad_of=None):
+              c_bf16_act=0, act_grad_of=None, col_sum=None, col_sum_n=0):
         f = self._orig["gemm"]
         kw = dict(ldc=ldc, bias=bias, accumulate=accumulate, split_k=split_k, bn_partial=bn_partial, batch=batch,
                   c_batch_stride=c_batch_stride, comp=comp, c_bf16=c_bf16, residual=residual, cperm=cperm,
-                  bn_fin=bn_fin, bnb=bnb, row_bias=row_bias, c_bf16_act=c_bf16_act, act_grad_of=act_grad_of)
+                  bn_fin=bn_fin, bnb=bnb, row_bias=row_bias, c_bf16_act=c_bf16_act, act_grad_of=act_grad_of,
+                  col_sum=col_sum, col_sum_n=col_sum_n)
         if bnb is not None and self.skip_bnb:
             return f(M, N, Kd, a, b, c, **kw)
         torch.cuda.synchronize()
@@ -198,6 +199,8 @@ class Capture:
         only16 = c.dtype == torch.bfloat16
         cv = _c_view(c, M, N, ldc_, batch, c_batch_stride, cperm)
         before = cv.double().clone() if accumulate else None
+        ncs = (col_sum_n or N) if col_sum is not None else 0
+        cs_before = col_sum[:ncs].double().clone() if ncs else None
         # product in fp64 from the operands the kernel reads (bf16 twins in bf16 mode)
         P = None
         for z in range(batch):
@@ -222,8 +225,12 @@ class Capture:
         tag = (f"gemm M{M} N{N} K{Kd}" + (f" b{batch}" if batch > 1 else "") + (f" sk{split_k}" if split_k > 1 else "")
                + (" acc" if accumulate else "") + (" win" if a.taps or b.taps else "") + (" cperm" if cperm else "")
                + (" bf16out" if only16 else "") + (" rowbias" if row_bias is not None else "")
-               + (" gelu" if c_bf16_act else "") + (" dgelu" if act_grad_of is not None else ""))
+               + (" gelu" if c_bf16_act else "") + (" dgelu" if act_grad_of is not None else "")
+               + (" colsum" if ncs else ""))
         res = {"C": _rel(got, ref, before)}
+        if ncs:  # the bias gradient accumulated in the epilogue: column sums of the stored values
+            cs_ref = cs_before + ref.reshape(-1, N)[:, :ncs].sum(0)
+            res["col_sum"] = _rel(col_sum[:ncs].double(), cs_ref, cs_before)
         if c_bf16 is not None and not only16:
             r16 = torch.nn.functional.gelu(ref) if c_bf16_act else ref
             res["C_bf16"] = _rel(_c_view(c_bf16, M, N, ldc_, batch, c_batch_stride, 0), r16, before)

@@ -97,6 +97,7 @@ def test_c4_ops_vs_fp64():
                   "layer_norm_bwd", "patchify", "btranspose"] + STEP_OPS)
     tags = " | ".join(t for _, t, _ in cap.records)
     assert " gelu" in tags and " dgelu" in tags  # the GELU forward / backward epilogues of the mixer
+    assert " colsum" in tags  # the mixer's bias gradients in the dgelu epilogue
 
 
 @pytest.mark.timeout(600)

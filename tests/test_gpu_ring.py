@@ -5,8 +5,9 @@
     (reference: the nn.Linear / Conv1d(k=1) products of factory/MLPMixer.py:16-33,58-92);
   * conv_ring_kernel (5-tap 'same' Conv1d, factory/Norm.py:21-28) on utterance-aligned and
     straddling tiles, with the BatchNorm statistics + finalize epilogue;
-  * the fused GELU epilogues (avc_gemm_desc.c_bf16_act / act_grad_of, MLPMixer.py:9-23), on the
-    ring kernel and on the fallback pass after the older kernels.
+  * the fused GELU epilogues (avc_gemm_desc.c_bf16_act / act_grad_of, MLPMixer.py:9-23) and the
+    bias-gradient column sums (col_sum), on the ring kernel and on the fallback pass after the
+    older kernels.
 Operands are bf16 (exact in fp32), so the references are fp32 products of the same values.
 """
 import pytest
@@ -143,3 +144,31 @@ def test_gelu_epilogues(ring):
     dref = (a.float() @ b.float().t()).double() * gp
     assert _rel(d, dref) < 1e-5
     assert _rel(d16.float(), dref) < 1e-2
+
+
+@pytest.mark.parametrize("ring", [-1, 0])
+@pytest.mark.parametrize("batch", [1, 3])
+def test_col_sum_epilogue(ring, batch):
+    """col_sum[:n] += column sums of the stored (GELU-backward) values, over every row of every
+    folded batch, with a padded leading dimension (n < N: the token mixer's 4*NP of 4*NPp)."""
+    from autoformer_amd import kernels as K
+
+    torch.manual_seed(7 + batch)
+    M, N, Kd, n = 344, 1408, 192, 1300
+    a = torch.randn(batch * M, Kd, device=DEV).bfloat16()
+    b = (torch.randn(N, Kd, device=DEV) * 0.1).bfloat16()
+    x = torch.randn(batch * M, N, device=DEV)
+    _ring(ring)
+    d = torch.empty(batch * M, N, device=DEV)
+    d16 = torch.empty(batch * M, N, device=DEV, dtype=torch.bfloat16)
+    cs = torch.randn(n + 5, device=DEV)
+    cs0 = cs.clone()
+    K.gemm(M, N, Kd, K.operand(a, Kd, batch_stride=M * Kd), K.operand(b, Kd), d, c_bf16=d16, act_grad_of=x,
+           batch=batch, c_batch_stride=M * N, col_sum=cs, col_sum_n=n)
+    torch.cuda.synchronize()
+    xd = x.double()
+    gp = 0.5 * (1 + torch.erf(xd / 2 ** 0.5)) + xd * torch.exp(-0.5 * xd * xd) / (2 * torch.pi) ** 0.5
+    dref = (a.float() @ b.float().t()).double() * gp
+    assert _rel(d, dref) < 1e-5
+    assert _rel(cs[:n] - cs0[:n], dref[:, :n].sum(0)) < 1e-5
+    assert torch.equal(cs[n:], cs0[n:])
