@@ -717,13 +717,15 @@ static int bnb_after(const avc_gemm_desc* d, const avc_bnb_args* bb, hipStream_t
                                        fin, s);
 }
 
-// The fused GELU epilogues (avc_gemm_desc.c_bf16_act / act_grad_of) exist in the ring kernels
-// only; for the other kernels the GEMM writes plain fp32 C and one avc_gelu_twin pass follows.
-extern "C" int avc_gelu_twin(const float* g, const float* x, float* y, void* y16, long long n, int bwd, void* stream);
+// The fused GELU / column-sum epilogues (avc_gemm_desc.c_bf16_act / act_grad_of / col_sum) exist in
+// the ring kernels only; the other kernels store the plain product (fp32 C and / or bf16: the
+// pre-activation slot, or the bf16 C itself when there is no fp32 C) and one pass follows.
 struct GeluPost {
   int act = 0;
-  const float* agrad = nullptr;
+  const void* agrad = nullptr;
+  int agrad16 = 0;
   bf16* c16 = nullptr;
+  bf16* pre16 = nullptr;
   float* csum = nullptr;
   int csum_n = 0;
 };
@@ -732,32 +734,61 @@ static GeluPost strip_gelu(GemmArgs& g) {
   p.csum = g.csum;
   p.csum_n = g.csum_n;
   g.csum = nullptr;
-  if (!g.c16_act && !g.agrad) return p;
-  p.act = g.c16_act;
-  p.agrad = g.agrad;
-  p.c16 = g.c16;
+  if (g.c16_act) {  // product -> c (fp32) and the bf16 pre-activation slot; c16 = GELU(that) after
+    p.act = g.c16_act;
+    p.c16 = g.c16;
+    p.pre16 = g.c16pre;
+    g.c16 = g.c16pre;
+  } else if (g.agrad) {  // product -> c, or (no fp32 C) the bf16 C; scaled by GELU' after
+    p.agrad = g.agrad;
+    p.agrad16 = g.agrad16;
+    p.c16 = g.c16;
+    if (g.c) g.c16 = nullptr;
+  }
   g.c16_act = 0;
   g.agrad = nullptr;
-  g.c16 = nullptr;
+  g.c16pre = nullptr;
   return p;
 }
+// act: c16[i] = GELU(src[i]); else c[i] / c16[i] = src[i] * GELU'(agr[i]) (src may alias either)
+template <typename TS>
+__global__ void gelu_post_kernel(const TS* src, const void* agr, int agr16, float* c, bf16* c16, long long n,
+                                 int act) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    float x = (float)src[i];
+    if (act) {
+      c16[i] = (bf16)gelu_f(x);
+      continue;
+    }
+    x *= gelu_grad_f(agr16 ? (float)static_cast<const bf16*>(agr)[i] : static_cast<const float*>(agr)[i]);
+    if (c) c[i] = x;
+    if (c16) c16[i] = (bf16)x;
+  }
+}
 // column sums of C (rows ldc apart) added into out[n], n < nc: 256 columns x 64 rows per block
-__global__ void colsum_atomic_kernel(const float* c, long long ldc, int M, int nc, float* out) {
+template <typename T>
+__global__ void colsum_atomic_kernel(const T* c, long long ldc, int M, int nc, float* out) {
   const int col = blockIdx.x * 256 + threadIdx.x, r0 = blockIdx.y * 64;
   if (col >= nc) return;
   float s = 0.f;
-  for (int r = r0; r < min(M, r0 + 64); ++r) s += c[(long long)r * ldc + col];
+  for (int r = r0; r < min(M, r0 + 64); ++r) s += (float)c[(long long)r * ldc + col];
   atomicAdd(out + col, s);
 }
 static int gelu_after(const GemmArgs& g, const GeluPost& p, hipStream_t s) {
   const long long n = (long long)g.M * g.N * g.batch;
-  int rc = 0;
-  if (p.agrad) rc = avc_gelu_twin(g.c, p.agrad, g.c, p.c16, n, 1, s);  // C *= GELU'(x), twin
-  else if (p.act) rc = avc_gelu_twin(nullptr, g.c, nullptr, p.c16, n, 0, s);  // twin = GELU(C)
-  if (rc) return rc;
+  const int blocks = (int)(n / 256 + 1 < 8192 ? n / 256 + 1 : 8192);
+  if (p.act || p.agrad) {
+    if (g.c) gelu_post_kernel<float><<<blocks, 256, 0, s>>>(g.c, p.agrad, p.agrad16, p.agrad ? g.c : nullptr, p.c16, n,
+                                                           p.act);
+    else gelu_post_kernel<bf16><<<blocks, 256, 0, s>>>(p.act ? p.pre16 : p.c16, p.agrad, p.agrad16, nullptr, p.c16, n,
+                                                       p.act);
+    if (avc_check_launch("avc_gemm(gelu)")) return -1;
+  }
   if (p.csum) {
     const int nc = p.csum_n > 0 ? p.csum_n : g.N, rows = g.M * g.batch;
-    colsum_atomic_kernel<<<dim3(cdiv(nc, 256), cdiv(rows, 64)), 256, 0, s>>>(g.c, g.ldc, rows, nc, p.csum);
+    const dim3 grid(cdiv(nc, 256), cdiv(rows, 64));
+    if (g.c) colsum_atomic_kernel<float><<<grid, 256, 0, s>>>(g.c, g.ldc, rows, nc, p.csum);
+    else colsum_atomic_kernel<bf16><<<grid, 256, 0, s>>>(p.c16 ? p.c16 : g.c16, g.ldc, rows, nc, p.csum);
     return avc_check_launch("avc_gemm(col_sum)");
   }
   return 0;
@@ -807,20 +838,26 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
   g.cpd = make_fastdiv(g.cperm ? (uint32_t)(d->N / g.cperm) : 1u);
   g.c16_act = d->c_bf16_act;
   g.agrad = d->act_grad_of;
+  g.agrad16 = d->act_grad_dtype == AVC_BF16;
+  g.c16pre = reinterpret_cast<bf16*>(d->c_pre_bf16);
   g.csum = d->col_sum;
   g.csum_n = d->col_sum_n;
-  AVC_CHECK_ARG(!g.csum || (d->c && !d->accumulate && g.split_k == 1 && !d->cperm &&
+  AVC_CHECK_ARG(d->act_grad_dtype == AVC_F32 || d->act_grad_dtype == AVC_BF16, "avc_gemm: bad act_grad_dtype");
+  AVC_CHECK_ARG(!g.csum || (!d->accumulate && g.split_k == 1 && !d->cperm &&
                             (g.batch == 1 || d->c_batch_stride == (long long)d->M * d->ldc) &&
-                            d->col_sum_n >= 0 && d->col_sum_n <= d->N),
-                "avc_gemm: col_sum needs an fp32 C, no accumulate / split-K / batch sum / cperm, col_sum_n <= N");
+                            d->col_sum_n >= 0 && d->col_sum_n <= d->N && !(g.c16_act && !d->c)),
+                "avc_gemm: col_sum needs no accumulate / split-K / batch sum / cperm, col_sum_n <= N (and an fp32 "
+                "C with c_bf16_act)");
   AVC_CHECK_ARG(g.c16_act == 0 || g.c16_act == AVC_ACT_GELU, "avc_gemm: c_bf16_act must be 0 or AVC_ACT_GELU");
+  AVC_CHECK_ARG(!g.c16pre || g.c16_act, "avc_gemm: c_pre_bf16 needs c_bf16_act");
+  AVC_CHECK_ARG(!(g.c16_act && g.agrad), "avc_gemm: c_bf16_act and act_grad_of are exclusive");
   AVC_CHECK_ARG(!(g.c16_act || g.agrad) ||
-                    (d->c && d->ldc == d->N && (g.batch == 1 || d->c_batch_stride == (long long)d->M * d->N) &&
+                    (d->ldc == d->N && (g.batch == 1 || d->c_batch_stride == (long long)d->M * d->N) &&
                      !d->accumulate && g.split_k == 1 &&
                      !d->cperm && !d->bn_partial && !bb && (!g.agrad || !d->residual) &&
-                     (!g.c16_act || d->c_bf16)),
-                "avc_gemm: the fused GELU epilogues need an fp32 C with ldc == N, no accumulate / split-K / batch "
-                "sum / cperm / BN epilogues (act_grad_of: no residual; c_bf16_act: c_bf16 set)");
+                     (!g.c16_act || (d->c_bf16 && (d->c || g.c16pre)))),
+                "avc_gemm: the fused GELU epilogues need ldc == N, no accumulate / split-K / batch sum / cperm / BN "
+                "epilogues (act_grad_of: no residual; c_bf16_act: c_bf16 and c or c_pre_bf16 set)");
   g.rbias = d->row_bias;
   g.rb_t = d->rb_t;
   g.rb_pad = d->rb_pad;

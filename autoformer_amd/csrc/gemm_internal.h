@@ -32,7 +32,9 @@ struct GemmArgs {
   int cperm;     // 0, or taps: column n = tap*chans + ch is stored at ch*taps + tap (conv weight layout)
   FastDiv cpd;   // divide a column by chans = N / cperm
   int c16_act;         // avc_gemm_desc.c_bf16_act: C16 holds GELU(C) (ring kernels only)
-  const float* agrad;  // avc_gemm_desc.act_grad_of: C *= GELU'(agrad[o]) (ring kernels only)
+  const void* agrad;   // avc_gemm_desc.act_grad_of: C *= GELU'(agrad[o]) (ring kernels only)
+  int agrad16;         // agrad is bf16
+  bf16* c16pre;        // avc_gemm_desc.c_pre_bf16: pre-activation C in bf16 (ring kernels only)
   float* csum;         // avc_gemm_desc.col_sum: csum[n] += column sums of the stored C (ring kernels only)
   int csum_n;
   const float* rbias;  // per-(utterance, edge class) row bias (avc_gemm_desc.row_bias), nullable

@@ -180,10 +180,14 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
   float* C = g.c ? g.c + (long long)bz * g.cbs : nullptr;
   bf16* C16 = g.c16 ? g.c16 + (long long)bz * g.cbs : nullptr;
   const float* res = (g.res && ks == 0) ? g.res + (long long)bz * g.cbs : nullptr;
-  const float* agr = g.agrad ? g.agrad + (long long)bz * g.cbs : nullptr;
+  // GELU-backward input, fp32 or bf16 (avc_gemm_desc.act_grad_dtype)
+  const float* agr = (g.agrad && !g.agrad16) ? static_cast<const float*>(g.agrad) + (long long)bz * g.cbs : nullptr;
+  const bf16* agr16 = (g.agrad && g.agrad16) ? static_cast<const bf16*>(g.agrad) + (long long)bz * g.cbs : nullptr;
+  bf16* P16 = g.c16pre ? g.c16pre + (long long)bz * g.cbs : nullptr;  // bf16 pre-activation
   const bool vec = (g.ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(C16) & 7) == 0 && (reinterpret_cast<uintptr_t>(res) & 15) == 0 &&
-                   (reinterpret_cast<uintptr_t>(agr) & 15) == 0;
+                   (reinterpret_cast<uintptr_t>(agr) & 15) == 0 && (reinterpret_cast<uintptr_t>(agr16) & 7) == 0 &&
+                   (reinterpret_cast<uintptr_t>(P16) & 7) == 0;
   const bool acc_c = g.accumulate != 0, gelu16 = g.c16_act != 0;
   float* csum = g.csum;
   // column-sum epilogue: lane's 4 columns are the same for every iteration (64 % (TWN/4) == 0)
@@ -210,12 +214,19 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
       if (vec && col + 3 < g.N) {
         if (res) v += *reinterpret_cast<const f32x4*>(res + o);
         if (acc_c) v += *reinterpret_cast<const f32x4*>(C + o);
-        if (agr) {
-          const f32x4 x = *reinterpret_cast<const f32x4*>(agr + o);
+        if (agr || agr16) {
+          f32x4 x;
+          if (agr) {
+            x = *reinterpret_cast<const f32x4*>(agr + o);
+          } else {
+            const bf16x4 h = *reinterpret_cast<const bf16x4*>(agr16 + o);
+            x = f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+          }
           v = f32x4{v[0] * gelu_grad_f(x[0]), v[1] * gelu_grad_f(x[1]), v[2] * gelu_grad_f(x[2]),
                     v[3] * gelu_grad_f(x[3])};
         }
         if (C) *reinterpret_cast<f32x4*>(C + o) = v;
+        if (P16) *reinterpret_cast<bf16x4*>(P16 + o) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
         if (csum) cs += v;
         if (C16) {
           const f32x4 w = gelu16 ? f32x4{gelu_f(v[0]), gelu_f(v[1]), gelu_f(v[2]), gelu_f(v[3])} : v;
@@ -227,7 +238,9 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
           if (res) x += res[o + k];
           if (acc_c) x += C[o + k];
           if (agr) x *= gelu_grad_f(agr[o + k]);
+          if (agr16) x *= gelu_grad_f((float)agr16[o + k]);
           if (C) C[o + k] = x;
+          if (P16) P16[o + k] = (bf16)x;
           if (csum) cs[k] += x;
           if (C16) C16[o + k] = (bf16)(gelu16 ? gelu_f(x) : x);
         }
@@ -763,7 +776,7 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
   const OpDev& a = g.a;
   if (win && c.win == 2 && a.taps == CV_TAPS && a.t_in == a.t_out && 2 * a.pad == a.taps - 1 &&
       g.K == a.taps * a.chans && a.chans % CV_CBK == 0 && g.batch == 1 && g.split_k == 1 && !g.b.win &&
-      (c.mode == 1 || a.t_out % CV_TM == 0)) {
+      (c.mode == 1 || (a.t_out % CV_TM == 0 && g.N >= 128))) {
     if (c.abl == 1) launch_conv<true, 1>(g, c.gm, s);
     else if (c.abl == 2) launch_conv<true, 2>(g, c.gm, s);
     else if (c.abl == 3) launch_conv<true, 3>(g, c.gm, s);
@@ -777,15 +790,34 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
     bn = c.bn;
     nst = c.nst;
   } else {
-    // measured (tools/ring_ab.py): the 256 x 256 ring beats the older kernels by 20-45 % on wide
-    // products with at least one tile per CU (MLP-Mixer token / channel mixing, the decoder LSTM
-    // input projections); narrower products (N < 1024) and conv window streams stay on
-    // gemm_nt.hip / gemm_conv.hip, as fast or faster there
-    const long long t22 = (long long)((g.M + 255) / 256) * ((g.N + 255) / 256) * units;
-    if (win || g.N < 1024 || t22 < 256) return false;
-    bm = 256;
-    bn = 256;
-    nst = 2;
+    // Tile choice by a wave-quantised cost model: each configuration runs one workgroup per CU, so
+    // a product costs ceil(tiles / 256) rounds of BM*BN*K work at the configuration's per-flop
+    // efficiency (1 : 0.85 : 0.75 for 256x256 / 256x128 / 128x128, fitted to the per-call census
+    // of the C2 / C4 steps, tools/gemm_census.py --ring-ab, profiles/r4_gemm_census_*.txt).  Every
+    // plain bf16 NN product of those steps ran as fast or faster on the chosen ring tile than on
+    // gemm_nt.hip.  Conv windows: the generic window stream only for channel counts the halo form
+    // cannot take (344 / 88 / 80 channels) and N <= 512, where it measured faster than
+    // gemm_conv.hip; the rest stay on gemm_conv.hip.
+    if (win && (g.N > 512 || a.chans % CV_CBK == 0)) return false;
+    struct Opt {
+      int bm, bn, nst;
+      double eff;
+    };
+    const Opt opts[3] = {{256, 256, 2, 1.0}, {256, 128, 3, 0.85}, {128, 128, 4, 0.75}};
+    double best = 0;
+    bm = 0;
+    bn = 0;
+    nst = 0;
+    for (const Opt& o : opts) {
+      const long long tiles = (long long)((g.M + o.bm - 1) / o.bm) * ((g.N + o.bn - 1) / o.bn) * units;
+      const double cost = (double)((tiles + 255) / 256) * o.bm * o.bn / o.eff;
+      if (!bm || cost < best * 0.999) {
+        best = cost;
+        bm = o.bm;
+        bn = o.bn;
+        nst = o.nst;
+      }
+    }
   }
 #define RING_CASE(BMV, BNV, NSV)                       \
   if (bm == BMV && bn == BNV && nst == NSV) {          \

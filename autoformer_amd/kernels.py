@@ -101,13 +101,18 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     the conv + BN + act layer whose conv output is y; the GEMM also computes that layer's BN
     backward statistics (avc_gemm_bnb: coef[6][N] and the parameter gradients).
     row_bias = (S, T, pad): S[(b*(2 pad + 1) + edge class)][N] added to row b*T + t (the conv0 fold).
-    c_bf16_act = ACT_GELU: c_bf16 receives GELU(C); act_grad_of = x: C *= GELU'(x) (and its twin) --
-    the MLP-Mixer GELU forward / backward folded into the GEMM epilogue (avc_gemm_desc).
+    c_bf16_act = ACT_GELU: c_bf16 receives GELU(C), C itself (the pre-activation) is stored to c --
+    fp32, or bf16 (avc_gemm_desc.c_pre_bf16) when c is a bf16 tensor; act_grad_of = x (fp32 or
+    bf16): C *= GELU'(x) -- the MLP-Mixer GELU forward / backward folded into the GEMM epilogue.
     col_sum: col_sum[:col_sum_n or N] += column sums of C (a bias gradient, float atomics)."""
     _dev(c, bias, bn_partial, c_bf16, residual)
     if _DETERMINISTIC:
         split_k = 1
-    if c.dtype == torch.bfloat16:  # bf16-only output
+    pre16 = None
+    if c.dtype == torch.bfloat16 and c_bf16_act:  # bf16 pre-activation + bf16 activation
+        assert c_bf16 is not None
+        c, pre16 = None, c
+    elif c.dtype == torch.bfloat16:  # bf16-only output
         assert c_bf16 is None and not accumulate and split_k == 1 and not cperm
         c, c_bf16 = None, c
     else:
@@ -132,7 +137,10 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
         d.col_sum, d.col_sum_n = col_sum.data_ptr(), int(col_sum_n)
     if act_grad_of is not None:
         _dev(act_grad_of)
+        assert act_grad_of.dtype in (torch.float32, torch.bfloat16)
         d.act_grad_of = act_grad_of.data_ptr()
+        d.act_grad_dtype = _dt(act_grad_of)
+    d.c_pre_bf16 = _ptr(pre16)
     if row_bias is not None:
         rb, rb_t, rb_pad = row_bias
         _dev(rb)

@@ -270,22 +270,24 @@ def _gelu_gemm(M, N, Kd, a, b, bias, dev, batch=1):
     GEMM's operand (bf16 only in bf16 mode).  bf16 mode: V comes out of the GEMM's epilogue
     (avc_gemm_desc.c_bf16_act; the ring kernels compute it in the epilogue, other kernels run one
     GELU pass after the GEMM), instead of a separate pass that re-reads U."""
-    U = torch.empty(batch * M, N, device=dev)
     if K.compute() != K.BF16:
+        U = torch.empty(batch * M, N, device=dev)
         K.gemm(M, N, Kd, a, b, U, bias=bias, batch=batch, c_batch_stride=M * N)
         return U, K.gelu_fwd_operand(U)
+    # bf16 mode: U is only the backward's GELU' input -- stored in bf16 (avc_gemm_desc.c_pre_bf16)
+    U = torch.empty(batch * M, N, device=dev, dtype=torch.bfloat16)
     V = torch.empty(batch * M, N, device=dev, dtype=torch.bfloat16)
     K.gemm(M, N, Kd, a, b, U, bias=bias, batch=batch, c_batch_stride=M * N, c_bf16=V, c_bf16_act=K.ACT_GELU)
     return U, V
 
 
 def _dgelu_gemm(M, N, Kd, a, b, U, dev, batch=1, bias_grad=None):
-    """dU = (a . b^T) * GELU'(U), fp32 with its bf16 operand twin (bf16 mode: in the GEMM epilogue,
-    avc_gemm_desc.act_grad_of).  bias_grad = (out, n, accumulate): out[:n] (+)= the column sums of
+    """dU = (a . b^T) * GELU'(U): fp32 (fp32 mode), or bf16 only -- it is read only as the next
+    GEMMs' operand -- from the GEMM epilogue (bf16 mode, avc_gemm_desc.act_grad_of).  bias_grad = (out, n, accumulate): out[:n] (+)= the column sums of
     dU, the bias gradient of the GELU's linear layer -- in bf16 mode in the same epilogue
     (avc_gemm_desc.col_sum) instead of a colsum pass that re-reads dU."""
-    dU = torch.empty(batch * M, N, device=dev)
     if K.compute() != K.BF16:
+        dU = torch.empty(batch * M, N, device=dev)
         K.gemm(M, N, Kd, a, b, dU, batch=batch, c_batch_stride=M * N)
         dU = K.gelu_bwd_twin(dU, U)
         if bias_grad is not None:
@@ -299,8 +301,8 @@ def _dgelu_gemm(M, N, Kd, a, b, U, dev, batch=1, bias_grad=None):
         if not acc:
             out.zero_()
         kw = dict(col_sum=out, col_sum_n=n)
-    K.gemm(M, N, Kd, a, b, dU, batch=batch, c_batch_stride=M * N, c_bf16=d16, act_grad_of=U, **kw)
-    return K.attach_twin(dU, d16)
+    K.gemm(M, N, Kd, a, b, d16, batch=batch, c_batch_stride=M * N, act_grad_of=U, **kw)
+    return d16
 
 
 class _MLPMixerFn(torch.autograd.Function):

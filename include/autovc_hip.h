@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 17
+#define AVC_ABI_VERSION 18
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -81,15 +81,20 @@ typedef struct {
                             frames (factory/AutoVC.py:46-51, fold.hip); non-K-strided operands only */
   int rb_t, rb_pad;
   int c_bf16_act;        /* 0, or AVC_ACT_GELU: c_bf16 receives GELU(C) (erf form) instead of C rounded -- the
-                            next GEMM's operand (MLPMixer.py:16-23 FeedForward); fp32 C is the pre-activation.
-                            Needs c and c_bf16, ldc == N, no accumulate / split-K / batch sum / cperm */
-  const float* act_grad_of; /* nullable: C = (A.B + bias) * GELU'(act_grad_of[m*ldc + n]) and its bf16 twin -- the
-                            GELU backward folded into the data-gradient GEMM.  Same restrictions, no residual */
+                            next GEMM's operand (MLPMixer.py:16-23 FeedForward); the pre-activation C goes to
+                            c (fp32) and / or c_pre_bf16.  Needs c_bf16 and one of those, ldc == N, no
+                            accumulate / split-K / batch sum / cperm */
+  const void* act_grad_of; /* nullable: C = (A.B + bias) * GELU'(act_grad_of[m*ldc + n]) (fp32 or bf16 per
+                            act_grad_dtype) stored to c and / or c_bf16 -- the GELU backward folded into the
+                            data-gradient GEMM.  Same restrictions, no residual */
   float* col_sum;        /* nullable: col_sum[n] += sum over m of the stored C[m][n], n < col_sum_n (0 = N) -- the
                             bias gradient of the layer whose output gradient C is (MLPMixer.py:16-23), without a
-                            second pass over C.  Float atomics (order-dependent rounding); needs an fp32 C, no
-                            accumulate / split-K / batch sum / cperm */
+                            second pass over C.  Float atomics (order-dependent rounding); no accumulate /
+                            split-K / batch sum / cperm */
   int col_sum_n;
+  void* c_pre_bf16;      /* nullable, with c_bf16_act: the pre-activation C rounded to bf16 (same ldc) -- the
+                            backward's act_grad_of at half the bytes of an fp32 C */
+  int act_grad_dtype;    /* AVC_F32 / AVC_BF16: element type of act_grad_of */
 } avc_gemm_desc;
 
 int avc_abi_version(void);

@@ -196,7 +196,7 @@ class Capture:
             return f(M, N, Kd, a, b, c, **kw)
         torch.cuda.synchronize()
         ldc_ = N if ldc is None else ldc
-        only16 = c.dtype == torch.bfloat16
+        only16 = c.dtype == torch.bfloat16 and not c_bf16_act  # (with c_bf16_act: a bf16 pre-activation)
         cv = _c_view(c, M, N, ldc_, batch, c_batch_stride, cperm)
         before = cv.double().clone() if accumulate else None
         ncs = (col_sum_n or N) if col_sum is not None else 0

@@ -1,7 +1,8 @@
 """Every avc_gemm call of one AutoVC train step (B=64, T=128, bf16), replayed in isolation with
-HIP events: per-call time, TFLOP/s and the stream it ran on, largest first.
+HIP events: per-call time, TFLOP/s and the stream it ran on, largest first.  --ring-ab also times
+each call with the ring kernels off (avc_gemm_set_ring(0)) next to the default policy.
 
-  python tools/gemm_census.py [--model AutoVC|MetaConv] [--reps 10]
+  python tools/gemm_census.py [--model AutoVC|MetaConv] [--reps 10] [--ring-ab]
 """
 import argparse
 import os
@@ -19,10 +20,13 @@ def main():
     ap.add_argument("--model", default="AutoVC")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--sweep", action="store_true", help="also time split-K 1..64 for the K-strided (TT) calls")
+    ap.add_argument("--ring-ab", action="store_true")
+    ap.add_argument("--force", default="", help="also time forced ring configs, e.g. '256,128,3;128,128,4'")
     args = ap.parse_args()
     import importlib
 
     import autoformer_amd as A
+    from autoformer_amd import _lib
     from autoformer_amd import kernels as K
     from autoformer_amd.detinit import det_init_, det_inputs
     from autoformer_amd.layers import side_stream
@@ -70,13 +74,37 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / args.reps * 1e3
+        off = ""
+        if args.ring_ab:
+            _lib.call("avc_gemm_set_ring", 0, 0, 0, 0, 0, 2)
+            run()
+            e0.record()
+            for _ in range(args.reps):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            _lib.call("avc_gemm_set_ring", -1, 0, 0, 0, 0, 2)
+            off = f" | ring off {e0.elapsed_time(e1) / args.reps * 1e3:.1f} us"
+        for cfg in filter(None, args.force.split(";")):
+            bm, bn, nst = map(int, cfg.split(","))
+            _lib.call("avc_gemm_set_ring", 1, bm, bn, nst, 0, 2)
+            run()
+            e0.record()
+            for _ in range(args.reps):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            _lib.call("avc_gemm_set_ring", -1, 0, 0, 0, 0, 2)
+            off += f" | {bm}x{bn}x{nst} {e0.elapsed_time(e1) / args.reps * 1e3:.1f}"
         batch = kw.get("batch", 1)
         fl = 2.0 * M * N * Kd * batch
         lay = ("T" if a.kstrided else "N") + ("T" if b.kstrided else "N")
         win = "w%d" % a.taps if a.taps > 1 else ("w%d" % b.taps if b.taps > 1 else "")
         desc = (f"{M}x{N}x{Kd}" + (f" b{batch}" if batch > 1 else "") + f" {lay} {DT[a.dtype]}/{DT[b.dtype]} {win}"
                 + (f" sk{kw['split_k']}" if kw.get("split_k", 1) > 1 else "")
-                + (" bn" if kw.get("bn_partial") is not None else "") + (" acc" if kw.get("accumulate") else ""))
+                + (" bn" if kw.get("bn_partial") is not None else "") + (" acc" if kw.get("accumulate") else "")
+                + (" gelu" if kw.get("c_bf16_act") else "") + (" dgelu" if kw.get("act_grad_of") is not None else "")
+                + (" colsum" if kw.get("col_sum") is not None else "") + off)
         if args.sweep and a.kstrided and b.kstrided:
             best = []
             for sk in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64):
