@@ -397,27 +397,31 @@ __global__ void bn_bwd_apply1_kernel(const TD* __restrict__ dA, const float* __r
   if (dy16) dy16[i] = (bf16)o;
 }
 
-// column sums: partial per 64-row block (vectorised like bn_bwd_reduce when N % 4 == 0 and
-// ld % 4 == 0, scalar otherwise), then a parallel finalize.
+// column sums: partial per strip of rpb rows (a multiple of 64; vectorised like bn_bwd_reduce when
+// N % 4 == 0 and ld % 4 == 0, scalar otherwise), then a parallel finalize over the strips.  The
+// strips are sized for ~2048 partial blocks, so the finalize reads at most a few hundred rows
+// (64-row strips had left it a serial 1849-row loop per column on the mixer's 118336-row sums).
 template <bool V4>
 __global__ void __launch_bounds__(256) colsum_partial_kernel(const float* __restrict__ x, long long ld, int M, int N,
-                                                             float* ws) {
+                                                             int rpb, float* ws) {
   __shared__ float red[16][65];
   const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
-  const int r0 = blockIdx.y * RB;
+  const int r0 = blockIdx.y * rpb, r1 = min(M, r0 + rpb);
   if constexpr (V4) {
     const int c = blockIdx.x * 64 + cq * 4;
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
     if (c < N) {
-      f32x4 v[4];
+      for (int rb = r0; rb < r1; rb += 64) {
+        f32x4 v[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = r0 + rl + 16 * i;
-        v[i] = *reinterpret_cast<const f32x4*>(x + (long long)(r < M ? r : 0) * ld + c);
+        for (int i = 0; i < 4; ++i) {
+          const int r = rb + rl + 16 * i;
+          v[i] = *reinterpret_cast<const f32x4*>(x + (long long)(r < r1 ? r : r0) * ld + c);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (rb + rl + 16 * i < r1) s += v[i];
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (r0 + rl + 16 * i < M) s += v[i];
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) red[rl][cq * 4 + k] = s[k];
@@ -428,10 +432,7 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const float* __rest
       const int c = blockIdx.x * 64 + cq + 16 * k;
       float s = 0.f;
       if (c < N)
-        for (int i = 0; i < 4; ++i) {
-          const int r = r0 + rl + 16 * i;
-          if (r < M) s += x[(long long)r * ld + c];
-        }
+        for (int r = r0 + rl; r < r1; r += 16) s += x[(long long)r * ld + c];
       red[rl][cq + 16 * k] = s;
     }
   }
@@ -664,11 +665,13 @@ extern "C" int avc_colsum(const float* x, long long ld, int M, int N, float* out
                           float* ws, void* stream) {
   AVC_CHECK_ARG(x && out && ws && ld >= N, "avc_colsum: bad args");
   hipStream_t s = as_stream(stream);
-  const int nrb = cdiv(M, RB);
+  // row strips of rpb rows: ~2048 partial blocks in all (nrb <= cdiv(M, RB), the workspace bound)
+  const int ncb = cdiv(N, 64), target = 2048 / ncb > 1 ? 2048 / ncb : 1;
+  const int rpb = M > 0 ? RB * cdiv(cdiv(M, RB), target) : RB, nrb = cdiv(M, rpb);
   if (N % 4 == 0 && ld % 4 == 0 && aligned16(x))
-    colsum_partial_kernel<true><<<dim3(cdiv(N, 64), nrb), 256, 0, s>>>(x, ld, M, N, ws);
+    colsum_partial_kernel<true><<<dim3(ncb, nrb), 256, 0, s>>>(x, ld, M, N, rpb, ws);
   else
-    colsum_partial_kernel<false><<<dim3(cdiv(N, 64), nrb), 256, 0, s>>>(x, ld, M, N, ws);
+    colsum_partial_kernel<false><<<dim3(ncb, nrb), 256, 0, s>>>(x, ld, M, N, rpb, ws);
   colsum_final_kernel<<<cdiv(N, 64), 256, 0, s>>>(ws, nrb, N, out, out2, accumulate);
   return avc_check_launch("avc_colsum");
 }

@@ -1102,6 +1102,8 @@ struct PersistBwdArgs {
   unsigned spin;
   int nap;
   int B, T, ng;
+  int abl;  // diagnostic (AVC_LSTM_BWD_ABL=1): gather the group's payload twice per step -- the
+            // 128 KB per consumer a 16-utterance group would read
 };
 
 template <int H, bool GR>
@@ -1173,6 +1175,10 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
         __syncthreads();
         if (*quit) return;  // block-uniform exit after a spin timeout
         load_group<G, NCH, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
+        if (a.abl & 1) {
+          __syncthreads();
+          load_group<G, NCH, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
+        }
         __syncthreads();
       }
       stamp(a.trace, T, s, 1);
@@ -1871,6 +1877,8 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
     p.B = B;
     p.T = T;
     p.ng = ng;
+    static const int abl = getenv("AVC_LSTM_BWD_ABL") ? atoi(getenv("AVC_LSTM_BWD_ABL")) : 0;
+    p.abl = abl;
     const bool gr = gran(true, H);
     (void)hipMemsetAsync(gbuf, 0, gr ? px_payload_off(ng) + (size_t)32 * B * H : px_ctl_bytes(ng), s);
     // (persistent_path above set the dynamic-LDS attributes)

@@ -214,6 +214,134 @@ __global__ void ln_bwd_param_kernel(const float* dy, const float* x, const float
   }
 }
 
+// Vectorised forms (D % 4 == 0, 16-B aligned rows, D <= 256 * NV): one wave per row holds the
+// row in registers (NV float4 per lane), so x is read from HBM once; outputs fp32 and / or bf16.
+template <int NV>
+__global__ void __launch_bounds__(256) ln_fwd_v_kernel(const float* x, int R, int D, const float* gamma,
+                                                       const float* beta, float eps, float* y, bf16* y16, float* mean,
+                                                       float* rstd) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63, D4 = D >> 2;
+  if (row >= R) return;
+  const f32x4* xr = reinterpret_cast<const f32x4*>(x + (long long)row * D);
+  f32x4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c4 = l + 64 * i;
+    v[i] = c4 < D4 ? xr[c4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+  const float mu = warp_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    if (l + 64 * i < D4) {
+      const f32x4 d = v[i] - mu;
+      q += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+    }
+  const float rs = 1.f / sqrtf(warp_sum(q) / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c4 = l + 64 * i;
+    if (c4 >= D4) continue;
+    const f32x4 g = gamma ? reinterpret_cast<const f32x4*>(gamma)[c4] : f32x4{1.f, 1.f, 1.f, 1.f};
+    const f32x4 b = beta ? reinterpret_cast<const f32x4*>(beta)[c4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 o = (v[i] - mu) * rs * g + b;
+    const long long off = (long long)row * D + 4 * c4;
+    if (y) *reinterpret_cast<f32x4*>(y + off) = o;
+    if (y16) *reinterpret_cast<bf16x4*>(y16 + off) = bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+  }
+  if (l == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+}
+
+// LayerNorm backward, dx and the parameter partials in one pass: 16 waves x LRB rows per block,
+// each wave one row at a time (dy and x rows in registers); dx = rs (g - mean g - xh mean(g xh))
+// (+ dres, the residual branch's gradient: the add after the norm folded in) to fp32 and / or
+// bf16; per-lane column partials of dy*xh and dy summed over the block's rows, reduced through
+// LDS into one (a, b) partial row per block for pair_final_kernel.
+constexpr int LRB = 64;
+template <int NV>
+__global__ void __launch_bounds__(1024) ln_bwd_v_kernel(const float* dy, const float* x, const float* gamma,
+                                                        const float* mean, const float* rstd, int R, int D,
+                                                        const float* dres, float* dx, bf16* dx16, float* ws) {
+  __shared__ f32x4 red[2][16][64 * NV];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, D4 = D >> 2;
+  f32x4 pa[NV], pb[NV], gm[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    pa[i] = pb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int c4 = l + 64 * i;
+    gm[i] = (gamma && c4 < D4) ? reinterpret_cast<const f32x4*>(gamma)[c4] : f32x4{1.f, 1.f, 1.f, 1.f};
+  }
+  const int r1 = min(R, (int)blockIdx.x * LRB + LRB);
+  for (int row = blockIdx.x * LRB + w; row < r1; row += 16) {
+    const long long o = (long long)row * D;
+    const float mu = mean[row], rs = rstd[row];
+    f32x4 dv[NV], xh[NV];
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = l + 64 * i;
+      if (c4 < D4) {
+        dv[i] = reinterpret_cast<const f32x4*>(dy + o)[c4];
+        xh[i] = (reinterpret_cast<const f32x4*>(x + o)[c4] - mu) * rs;
+      } else {
+        dv[i] = xh[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      const f32x4 g = dv[i] * gm[i], gx = g * xh[i];
+      s0 += g[0] + g[1] + g[2] + g[3];
+      s1 += gx[0] + gx[1] + gx[2] + gx[3];
+      pa[i] += dv[i] * xh[i];
+      pb[i] += dv[i];
+    }
+    const float m0 = warp_sum(s0) / (float)D, m1 = warp_sum(s1) / (float)D;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = l + 64 * i;
+      if (c4 >= D4) continue;
+      f32x4 d = rs * (dv[i] * gm[i] - m0 - xh[i] * m1);
+      if (dres) d += reinterpret_cast<const f32x4*>(dres + o)[c4];
+      if (dx) reinterpret_cast<f32x4*>(dx + o)[c4] = d;
+      if (dx16) *reinterpret_cast<bf16x4*>(dx16 + o + 4 * c4) = bf16x4{(bf16)d[0], (bf16)d[1], (bf16)d[2], (bf16)d[3]};
+    }
+  }
+  if (!ws) return;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    red[0][w][l + 64 * i] = pa[i];
+    red[1][w][l + 64 * i] = pb[i];
+  }
+  __syncthreads();
+  // thread t: column quad c4 = t % (64 NV), quantity t / (64 NV)
+  for (int t = threadIdx.x; t < 2 * 64 * NV; t += 1024) {
+    const int qn = t / (64 * NV), c4 = t - qn * 64 * NV;
+    if (c4 >= D4) continue;
+    f32x4 a = red[qn][0][c4];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) a += red[qn][k][c4];
+    float* p = ws + ((long long)blockIdx.x * D + 4 * c4) * 2 + qn;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) p[2 * e] = a[e];
+  }
+}
+
+// GroupNorm apply, 4 channels per thread (C % 4 == 0): fp32 and / or the bf16 operand twin
+__global__ void gn_apply_v_kernel(const float* x, long long S, int C, const float* gamma, const float* beta,
+                                  const float* mean, const float* rstd, float* y, bf16* y16, long long total4) {
+  const long long i4 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i4 >= total4) return;
+  const long long i = 4 * i4;
+  const int b = (int)(i / S), c = (int)(i % C);
+  const f32x4 g = gamma ? *reinterpret_cast<const f32x4*>(gamma + c) : f32x4{1.f, 1.f, 1.f, 1.f};
+  const f32x4 bt = beta ? *reinterpret_cast<const f32x4*>(beta + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 o = (*reinterpret_cast<const f32x4*>(x + i) - mean[b]) * rstd[b] * g + bt;
+  if (y) *reinterpret_cast<f32x4*>(y + i) = o;
+  if (y16) *reinterpret_cast<bf16x4*>(y16 + i) = bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+}
+
 // ---------------------------------------------------------------- GELU (exact, erf) backward
 __global__ void gelu_bwd_kernel(const float* g, const float* x, float* dx, long long n) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -278,14 +406,15 @@ __global__ void patchify_kernel(const float* nf, float* P, int L, int C, int ps,
 // dst[b][c][r] (+)= src[b][r][c] for r < R; dst rows are ld (>= R) long and r in [R, ld) is written
 // 0 (the zero-padded patch count of the MLP-Mixer operands).  dst (fp32) and / or dst16 (bf16,
 // the GEMM operand) -- one pass instead of a transpose followed by a pad / convert pass.
-__global__ void btranspose_kernel(const float* src, float* dst, bf16* dst16, int R, int C, int ld, int acc) {
+template <typename TS>
+__global__ void btranspose_kernel(const TS* src, float* dst, bf16* dst16, int R, int C, int ld, int acc) {
   __shared__ float tile[32][33];
   const long long off = (long long)blockIdx.z * R * C, doff = (long long)blockIdx.z * C * ld;
   const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   for (int y = ty; y < 32; y += 8) {
     const int r = r0 + y, c = c0 + tx;
-    tile[y][tx] = (r < R && c < C) ? src[off + (long long)r * C + c] : 0.f;
+    tile[y][tx] = (r < R && c < C) ? (float)src[off + (long long)r * C + c] : 0.f;
   }
   __syncthreads();
   for (int y = ty; y < 32; y += 8) {
@@ -306,15 +435,31 @@ __global__ void btranspose_kernel(const float* src, float* dst, bf16* dst16, int
 
 #define GRID1(n) dim3(cdiv((n), 256)), dim3(256), 0, as_stream(stream)
 
-extern "C" size_t avc_norm_ws(int rows, int C) { return (size_t)cdiv(rows, 128) * C * 2 + 1024; }
+static bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+static bool a8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
+
+
+extern "C" size_t avc_norm_ws(int rows, int C) { return (size_t)cdiv(rows, 64) * C * 2 + 1024; }
+
+extern "C" int avc_group_norm_fwd2(const float* x, int B, long long S, int C, const float* gamma, const float* beta,
+                                   float eps, float* y, void* y16, float* mean, float* rstd, void* stream) {
+  AVC_CHECK_ARG(x && (y || y16) && mean && rstd && B > 0 && S > 0 && C > 0 && S % C == 0,
+                "avc_group_norm_fwd: bad args");
+  gn_stats_kernel<<<B, 1024, 0, as_stream(stream)>>>(x, S, eps, mean, rstd);
+  const long long total = (long long)B * S;
+  bf16* o16 = static_cast<bf16*>(y16);
+  if (C % 4 == 0 && a16(x) && a16(y) && a8(o16) && a16(gamma) && a16(beta)) {
+    gn_apply_v_kernel<<<GRID1(total / 4)>>>(x, S, C, gamma, beta, mean, rstd, y, o16, total / 4);
+  } else {
+    AVC_CHECK_ARG(y && !y16, "avc_group_norm_fwd: the bf16 twin needs C %% 4 == 0 and aligned data");
+    gn_apply_kernel<<<GRID1(total)>>>(x, S, C, gamma, beta, mean, rstd, y, total);
+  }
+  return avc_check_launch("avc_group_norm_fwd");
+}
 
 extern "C" int avc_group_norm_fwd(const float* x, int B, long long S, int C, const float* gamma, const float* beta,
                                   float eps, float* y, float* mean, float* rstd, void* stream) {
-  AVC_CHECK_ARG(x && y && mean && rstd && B > 0 && S > 0 && C > 0 && S % C == 0, "avc_group_norm_fwd: bad args");
-  gn_stats_kernel<<<B, 1024, 0, as_stream(stream)>>>(x, S, eps, mean, rstd);
-  const long long total = (long long)B * S;
-  gn_apply_kernel<<<GRID1(total)>>>(x, S, C, gamma, beta, mean, rstd, y, total);
-  return avc_check_launch("avc_group_norm_fwd");
+  return avc_group_norm_fwd2(x, B, S, C, gamma, beta, eps, y, nullptr, mean, rstd, stream);
 }
 
 extern "C" int avc_group_norm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
@@ -335,11 +480,45 @@ extern "C" int avc_group_norm_bwd(const float* dy, const float* x, const float* 
   return avc_check_launch("avc_group_norm_bwd");
 }
 
+extern "C" int avc_layer_norm_fwd2(const float* x, int R, int D, const float* gamma, const float* beta, float eps,
+                                   float* y, void* y16, float* mean, float* rstd, void* stream) {
+  AVC_CHECK_ARG(x && (y || y16) && mean && rstd && R > 0 && D > 0, "avc_layer_norm_fwd: bad args");
+  hipStream_t s = as_stream(stream);
+  bf16* o16 = static_cast<bf16*>(y16);
+  const bool v = D % 4 == 0 && D <= 512 && a16(x) && a16(y) && a8(o16) && a16(gamma) && a16(beta);
+  if (v && D <= 256) ln_fwd_v_kernel<1><<<cdiv(R, 4), 256, 0, s>>>(x, R, D, gamma, beta, eps, y, o16, mean, rstd);
+  else if (v) ln_fwd_v_kernel<2><<<cdiv(R, 4), 256, 0, s>>>(x, R, D, gamma, beta, eps, y, o16, mean, rstd);
+  else {
+    AVC_CHECK_ARG(y && !y16, "avc_layer_norm_fwd: the bf16 output needs D %% 4 == 0, D <= 512, aligned rows");
+    ln_fwd_kernel<<<cdiv(R, 4), 256, 0, s>>>(x, R, D, gamma, beta, eps, y, mean, rstd);
+  }
+  return avc_check_launch("avc_layer_norm_fwd");
+}
+
 extern "C" int avc_layer_norm_fwd(const float* x, int R, int D, const float* gamma, const float* beta, float eps,
                                   float* y, float* mean, float* rstd, void* stream) {
-  AVC_CHECK_ARG(x && y && mean && rstd && R > 0 && D > 0, "avc_layer_norm_fwd: bad args");
-  ln_fwd_kernel<<<cdiv(R, 4), 256, 0, as_stream(stream)>>>(x, R, D, gamma, beta, eps, y, mean, rstd);
-  return avc_check_launch("avc_layer_norm_fwd");
+  return avc_layer_norm_fwd2(x, R, D, gamma, beta, eps, y, nullptr, mean, rstd, stream);
+}
+
+extern "C" int avc_layer_norm_bwd2(const float* dy, const float* x, const float* gamma, const float* mean,
+                                   const float* rstd, int R, int D, const float* dres, float* dx, void* dx16,
+                                   float* dgamma, float* dbeta, int accumulate, float* ws, void* stream) {
+  AVC_CHECK_ARG(dy && x && mean && rstd && (dx || dx16) && ws && R > 0 && D > 0, "avc_layer_norm_bwd: bad args");
+  hipStream_t s = as_stream(stream);
+  bf16* o16 = static_cast<bf16*>(dx16);
+  const bool v = D % 4 == 0 && D <= 512 && a16(dy) && a16(x) && a16(dx) && a8(o16) && a16(gamma) && a16(dres);
+  if (v) {
+    const bool par = dgamma || dbeta;
+    const int nrb = cdiv(R, LRB);
+    if (D <= 256)
+      ln_bwd_v_kernel<1><<<nrb, 1024, 0, s>>>(dy, x, gamma, mean, rstd, R, D, dres, dx, o16, par ? ws : nullptr);
+    else
+      ln_bwd_v_kernel<2><<<nrb, 1024, 0, s>>>(dy, x, gamma, mean, rstd, R, D, dres, dx, o16, par ? ws : nullptr);
+    if (par) pair_final_kernel<<<cdiv(D, 64), 1024, 0, s>>>(ws, nrb, D, dgamma, dbeta, accumulate);
+    return avc_check_launch("avc_layer_norm_bwd");
+  }
+  AVC_CHECK_ARG(dx && !dx16 && !dres, "avc_layer_norm_bwd: dres / bf16 output need D %% 4 == 0, D <= 512, aligned rows");
+  return avc_layer_norm_bwd(dy, x, gamma, mean, rstd, R, D, dx, dgamma, dbeta, accumulate, ws, stream);
 }
 
 extern "C" int avc_layer_norm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
@@ -380,15 +559,21 @@ extern "C" int avc_patchify(const float* src, float* dst, int B, int L, int C, i
 extern "C" int avc_transpose_batched(const float* src, float* dst, int B, int R, int C, int accumulate, void* stream) {
   AVC_CHECK_ARG(src && dst && src != dst, "avc_transpose_batched: bad args");
   dim3 g(cdiv(C, 32), cdiv(R, 32), B);
-  btranspose_kernel<<<g, 256, 0, as_stream(stream)>>>(src, dst, nullptr, R, C, R, accumulate);
+  btranspose_kernel<float><<<g, 256, 0, as_stream(stream)>>>(src, dst, nullptr, R, C, R, accumulate);
   return avc_check_launch("avc_transpose_batched");
 }
 
-extern "C" int avc_transpose_batched2(const float* src, float* dst, void* dst16, int B, int R, int C, int ld,
-                                      int accumulate, void* stream) {
-  AVC_CHECK_ARG(src && (dst || dst16) && (const void*)src != (const void*)dst && ld >= R && (!accumulate || dst),
+extern "C" int avc_transpose_batched2(const void* src, int src_dtype, float* dst, void* dst16, int B, int R, int C,
+                                      int ld, int accumulate, void* stream) {
+  AVC_CHECK_ARG(src && (dst || dst16) && (const void*)src != (const void*)dst && ld >= R && (!accumulate || dst) &&
+                    (src_dtype == AVC_F32 || src_dtype == AVC_BF16),
                 "avc_transpose_batched2: bad args");
   dim3 g(cdiv(C, 32), cdiv(ld, 32), B);
-  btranspose_kernel<<<g, 256, 0, as_stream(stream)>>>(src, dst, reinterpret_cast<bf16*>(dst16), R, C, ld, accumulate);
+  if (src_dtype == AVC_BF16)
+    btranspose_kernel<bf16><<<g, 256, 0, as_stream(stream)>>>(static_cast<const bf16*>(src), dst,
+                                                              reinterpret_cast<bf16*>(dst16), R, C, ld, accumulate);
+  else
+    btranspose_kernel<float><<<g, 256, 0, as_stream(stream)>>>(static_cast<const float*>(src), dst,
+                                                               reinterpret_cast<bf16*>(dst16), R, C, ld, accumulate);
   return avc_check_launch("avc_transpose_batched2");
 }

@@ -55,7 +55,7 @@ class MetaBlock(nn.Module):
         """MetaConv.py:64-76 on frame-major x (B*L, 512); L must equal crop_len."""
         if L != self.crop_len:
             raise RuntimeError(f"MetaBlock needs L == crop_len ({self.crop_len}), got {L}")
-        y = MF.group_norm(x, B, self.norm1)
+        y = MF.group_norm(x, B, self.norm1, twin=not self.pool)  # the conv mixer reads it as a bf16 operand
         mix = MF.pool_mixer(y, B, L) if self.pool else Lyr.conv_bn(self._mix, y, B, L)
         x = MF.add(x, mix)
         a = Lyr.conv_bn(self._c1, x, B, L)

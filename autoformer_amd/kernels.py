@@ -676,13 +676,15 @@ def _ws(rows, C, dev):
     return torch.empty(int(L.lib().avc_norm_ws(rows, C)), device=dev)
 
 
-def group_norm_fwd(x, B, C, gamma, beta, eps):
+def group_norm_fwd(x, B, C, gamma, beta, eps, twin=False):
+    """twin (C % 4 == 0): the bf16 operand twin of y written in the same pass."""
     S = x.numel() // B
     y = torch.empty_like(x)
+    y16 = _twin_buf(y, None) if twin else None
     mean, rstd = torch.empty(B, device=x.device), torch.empty(B, device=x.device)
-    L.call("avc_group_norm_fwd", x.data_ptr(), B, S, C, _ptr(gamma), _ptr(beta), float(eps), y.data_ptr(),
+    L.call("avc_group_norm_fwd2", x.data_ptr(), B, S, C, _ptr(gamma), _ptr(beta), float(eps), y.data_ptr(), _ptr(y16),
            mean.data_ptr(), rstd.data_ptr(), stream())
-    return y, mean, rstd
+    return (attach_twin(y, y16) if y16 is not None else y), mean, rstd
 
 
 def group_norm_bwd(dy, x, gamma, mean, rstd, B, C, dgamma=None, dbeta=None, accumulate=False):
@@ -694,21 +696,27 @@ def group_norm_bwd(dy, x, gamma, mean, rstd, B, C, dgamma=None, dbeta=None, accu
     return dx
 
 
-def layer_norm_fwd(x, gamma, beta, eps):
+def layer_norm_fwd(x, gamma, beta, eps, out_bf16=False):
+    """out_bf16: y as a bf16 tensor only (an operand read only by bf16 GEMMs / transposes)."""
     R, D = x.shape
-    y = torch.empty_like(x)
+    y = torch.empty(R, D, device=x.device, dtype=torch.bfloat16 if out_bf16 else torch.float32)
     mean, rstd = torch.empty(R, device=x.device), torch.empty(R, device=x.device)
-    L.call("avc_layer_norm_fwd", x.data_ptr(), R, D, _ptr(gamma), _ptr(beta), float(eps), y.data_ptr(),
-           mean.data_ptr(), rstd.data_ptr(), stream())
+    L.call("avc_layer_norm_fwd2", x.data_ptr(), R, D, _ptr(gamma), _ptr(beta), float(eps),
+           None if out_bf16 else y.data_ptr(), y.data_ptr() if out_bf16 else None, mean.data_ptr(), rstd.data_ptr(),
+           stream())
     return y, mean, rstd
 
 
-def layer_norm_bwd(dy, x, gamma, mean, rstd, dgamma=None, dbeta=None, accumulate=False):
+def layer_norm_bwd(dy, x, gamma, mean, rstd, dgamma=None, dbeta=None, accumulate=False, residual=None, twin=False):
+    """dx (+ residual: the gradient of a residual branch around the norm, added in the same pass;
+    twin: its bf16 operand twin written beside it)."""
     R, D = x.shape
     dx = torch.empty_like(x)
-    L.call("avc_layer_norm_bwd", dy.data_ptr(), x.data_ptr(), _ptr(gamma), mean.data_ptr(), rstd.data_ptr(), R, D,
-           dx.data_ptr(), _ptr(dgamma), _ptr(dbeta), int(accumulate), _ws(R, D, x.device).data_ptr(), stream())
-    return dx
+    dx16 = _twin_buf(dx, None) if twin else None
+    L.call("avc_layer_norm_bwd2", dy.data_ptr(), x.data_ptr(), _ptr(gamma), mean.data_ptr(), rstd.data_ptr(), R, D,
+           _ptr(residual), dx.data_ptr(), _ptr(dx16), _ptr(dgamma), _ptr(dbeta), int(accumulate),
+           _ws(R, D, x.device).data_ptr(), stream())
+    return attach_twin(dx, dx16) if dx16 is not None else dx
 
 
 def gelu_bwd(g, x):
@@ -746,7 +754,7 @@ def transpose_pad(src, B, R, C, ld, dtype=F32, twin=False):
     else:
         out = torch.empty(B * C, ld, device=src.device)
         o16 = _twin_buf(out, None) if twin else None
-    L.call("avc_transpose_batched2", src.data_ptr(), _ptr(out), _ptr(o16), B, R, C, int(ld), 0, stream())
+    L.call("avc_transpose_batched2", src.data_ptr(), _dt(src), _ptr(out), _ptr(o16), B, R, C, int(ld), 0, stream())
     if dtype == BF16:
         return o16
     return attach_twin(out, o16) if o16 is not None else out

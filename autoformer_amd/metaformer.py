@@ -83,9 +83,9 @@ class _GroupNormFn(torch.autograd.Function):
     """GroupNorm(1, C) on frame-major (B*L, C): per-sample statistics over all L*C values."""
 
     @staticmethod
-    def forward(ctx, x, B, gamma, beta, eps):
+    def forward(ctx, x, B, gamma, beta, eps, twin):
         C = x.shape[1]
-        y, mean, rstd = K.group_norm_fwd(x, B, C, gamma, beta, eps)
+        y, mean, rstd = K.group_norm_fwd(x, B, C, gamma, beta, eps, twin=twin)
         ctx.save_for_backward(x, gamma, mean, rstd)
         ctx.B, ctx.beta = B, beta
         return y
@@ -97,15 +97,16 @@ class _GroupNormFn(torch.autograd.Function):
         if Lyr.sink_on():
             dx = K.group_norm_bwd(g.contiguous(), x, gamma, mean, rstd, ctx.B, C, _sink(gamma), _sink(ctx.beta),
                                   accumulate=True)
-            return dx, None, None, None, None
+            return dx, None, None, None, None, None
         dgamma = torch.empty(C, device=x.device)
         dbeta = torch.empty(C, device=x.device)
         dx = K.group_norm_bwd(g.contiguous(), x, gamma, mean, rstd, ctx.B, C, dgamma, dbeta)
-        return dx, None, dgamma, dbeta, None
+        return dx, None, dgamma, dbeta, None, None
 
 
-def group_norm(x, B, gn):
-    return _GroupNormFn.apply(x, B, gn.weight, gn.bias, gn.eps)
+def group_norm(x, B, gn, twin=False):
+    """twin: the output's bf16 operand twin in the same pass (a GEMM reads it next)."""
+    return _GroupNormFn.apply(x, B, gn.weight, gn.bias, gn.eps, twin)
 
 
 class _PoolMixerFn(torch.autograd.Function):
@@ -320,7 +321,8 @@ class _MLPMixerFn(torch.autograd.Function):
         P = K.twin(K.patchify(nf, B, Lf, C, ps))               # (B*NP, ps^2)
         weC, w3C, w4C, _, _, _ = _cf_weights(mix, we, w3, w4)
         Z = _lin(P, B * NP, D, ps * ps, weC, be)                # (B*NP, D)
-        Y1, m1, r1 = K.layer_norm_fwd(Z, g1, b1n, mix.ln_eps[0])
+        bf = K.compute() == K.BF16  # Y1 / Y2 are read only as bf16 operands: no fp32 copies
+        Y1, m1, r1 = K.layer_norm_fwd(Z, g1, b1n, mix.ln_eps[0], out_bf16=bf)
         # token mixing: UT_b (D x 4NP) = Y1_b^T . W1^T + b1   (Conv1d(NP -> 4NP, k1) on (B, NP, D)),
         # as an NT product of the per-utterance transpose Y1T_b (D x NPp) and W1 (4NPp x NPp).
         # Patch counts are zero-padded to NPp (_token_mix_weights): UT / V carry 4NPp columns
@@ -337,7 +339,7 @@ class _MLPMixerFn(torch.autograd.Function):
         K.gemm(D, NP, 4 * NPp, operand(V, 4 * NPp, batch_stride=D * 4 * NPp), operand(W2c, 4 * NPp), RT, bias=bb2,
                batch=B, c_batch_stride=D * NP)
         Z1 = K.transpose_batched(RT, B, D, NP, out=K.convert(Z, K.F32), accumulate=True).view(B * NP, D)
-        Y2, m2, r2 = K.layer_norm_fwd(Z1, g2, b2n, mix.ln_eps[1])
+        Y2, m2, r2 = K.layer_norm_fwd(Z1, g2, b2n, mix.ln_eps[1], out_bf16=bf)
         U2, V2 = _gelu_gemm(B * NP, 4 * D, D, operand(K.twin(Y2), D), operand(w3C, D), bb3, dev)
         Z2 = _lin(V2, B * NP, D, 4 * D, w4C, bb4, residual=Z1)
         (Wf, _), wp = _out_conv_packs(mix, wc)
@@ -401,7 +403,7 @@ class _MLPMixerFn(torch.autograd.Function):
         dY2 = torch.empty(M, D, device=dev)
         K.gemm(M, D, 4 * D, operand(dU2, 4 * D), operand(w3T, 4 * D), dY2)
         dg2, db2n = (_sink(g2), _sink(b2n)) if sink else (torch.empty(D, device=dev), torch.empty(D, device=dev))
-        dZ1 = K.add(dZ2, K.layer_norm_bwd(dY2, Z1, g2, m2, r2, dg2, db2n, accumulate=sink))
+        dZ1 = K.layer_norm_bwd(dY2, Z1, g2, m2, r2, dg2, db2n, accumulate=sink, residual=dZ2)
         # token FF: Z1 = Z + (GELU(Y1^T W1^T + b1) W2^T + b2)^T   per utterance.  dRT_b = dZ1_b^T is
         # read in place from dZ1 (as the transposed operand), so NP is never a contiguous dimension.
         W1T, W2c, _, W2t = _token_mix_weights(mix, w1, w2, NP)
@@ -429,7 +431,7 @@ class _MLPMixerFn(torch.autograd.Function):
         K.gemm(B * D, NP, 4 * NPp, operand(dUT, 4 * NPp), operand(W1T, 4 * NPp), dY1T)
         dY1 = K.transpose_batched(dY1T, B, D, NP).view(M, D)
         dg1, db1n = (_sink(g1), _sink(b1n)) if sink else (torch.empty(D, device=dev), torch.empty(D, device=dev))
-        dZ = K.twin(K.add(dZ1, K.layer_norm_bwd(dY1, Z, g1, m1, r1, dg1, db1n, accumulate=sink)))
+        dZ = K.twin(K.layer_norm_bwd(dY1, Z, g1, m1, r1, dg1, db1n, accumulate=sink, residual=dZ1, twin=True))
         # patch embedding
         pp = ps * ps
         dwe = _sink(we) if sink else torch.empty_like(we)

@@ -250,7 +250,7 @@ def main():
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     # diagnostic ablations skip work inside the step: a number measured under them is not the metric
-    skipped = [k for k in ("AVC_ABLATE_WGRAD", "AVC_LSTM_DEBUG") if os.environ.get(k, "0") not in ("", "0")]
+    skipped = [k for k in ("AVC_ABLATE_WGRAD", "AVC_LSTM_DEBUG", "AVC_LSTM_BWD_ABL") if os.environ.get(k, "0") not in ("", "0")]
     if skipped:
         raise SystemExit(f"bench.py: diagnostic ablation(s) {skipped} set; they skip work in the timed step")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:

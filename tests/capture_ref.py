@@ -368,9 +368,9 @@ class Capture:
         return out
 
     # ---------------------------------------------------------------- MetaFormer (C4) blocks
-    def _group_norm_fwd(self, x, B, C, gamma, beta, eps):
+    def _group_norm_fwd(self, x, B, C, gamma, beta, eps, twin=False):
         torch.cuda.synchronize()
-        y, mean, rstd = self._orig["group_norm_fwd"](x, B, C, gamma, beta, eps)
+        y, mean, rstd = self._orig["group_norm_fwd"](x, B, C, gamma, beta, eps, twin=twin)
         torch.cuda.synchronize()
         xv = x.double().reshape(B, -1)
         mu, var = xv.mean(1), xv.var(1, unbiased=False)
@@ -379,7 +379,10 @@ class Capture:
         if gamma is not None:
             ref = ref * gamma.double() + (beta.double() if beta is not None else 0.0)
         res = {"y": _rel(y, ref.view_as(y)), "mean": _rel(mean, mu), "rstd": _rel(rstd, rs)}
-        self.records.append(("group_norm_fwd", f"group_norm_fwd B{B} S{xv.shape[1]} C{C}", res))
+        if getattr(y, "_bf16", None) is not None:
+            res["y_bf16"] = _rel(y._bf16, ref.view_as(y))
+        self.records.append(("group_norm_fwd", f"group_norm_fwd B{B} S{xv.shape[1]} C{C}" + (" twin" if twin else ""),
+                             res))
         return y, mean, rstd
 
     def _group_norm_bwd(self, dy, x, gamma, mean, rstd, B, C, dgamma=None, dbeta=None, accumulate=False):
@@ -404,9 +407,9 @@ class Capture:
         self.records.append(("group_norm_bwd", f"group_norm_bwd B{B} C{C}", res))
         return dx
 
-    def _layer_norm_fwd(self, x, gamma, beta, eps):
+    def _layer_norm_fwd(self, x, gamma, beta, eps, out_bf16=False):
         torch.cuda.synchronize()
-        y, mean, rstd = self._orig["layer_norm_fwd"](x, gamma, beta, eps)
+        y, mean, rstd = self._orig["layer_norm_fwd"](x, gamma, beta, eps, out_bf16=out_bf16)
         torch.cuda.synchronize()
         xv = x.double()
         mu, var = xv.mean(1), xv.var(1, unbiased=False)
@@ -415,26 +418,34 @@ class Capture:
         if gamma is not None:
             ref = ref * gamma.double()[None] + (beta.double()[None] if beta is not None else 0.0)
         res = {"y": _rel(y, ref), "mean": _rel(mean, mu), "rstd": _rel(rstd, rs)}
-        self.records.append(("layer_norm_fwd", f"layer_norm_fwd R{x.shape[0]} D{x.shape[1]}", res))
+        self.records.append(("layer_norm_fwd", f"layer_norm_fwd R{x.shape[0]} D{x.shape[1]}" + (" bf16out" if out_bf16
+                                                                                               else ""), res))
         return y, mean, rstd
 
-    def _layer_norm_bwd(self, dy, x, gamma, mean, rstd, dgamma=None, dbeta=None, accumulate=False):
+    def _layer_norm_bwd(self, dy, x, gamma, mean, rstd, dgamma=None, dbeta=None, accumulate=False, residual=None,
+                        twin=False):
         torch.cuda.synchronize()
         b0 = dgamma.double().clone() if (dgamma is not None and accumulate) else None
         b1 = dbeta.double().clone() if (dbeta is not None and accumulate) else None
-        dx = self._orig["layer_norm_bwd"](dy, x, gamma, mean, rstd, dgamma, dbeta, accumulate)
+        dx = self._orig["layer_norm_bwd"](dy, x, gamma, mean, rstd, dgamma, dbeta, accumulate, residual=residual,
+                                          twin=twin)
         torch.cuda.synchronize()
         xh = (x.double() - mean.double()[:, None]) * rstd.double()[:, None]
         g = dy.double()
         dxh = g * (gamma.double()[None] if gamma is not None else 1.0)
         rdx = rstd.double()[:, None] * (dxh - dxh.mean(1, keepdim=True) - xh * (dxh * xh).mean(1, keepdim=True))
+        if residual is not None:
+            rdx = rdx + residual.double()
         res = {"dx": _rel(dx, rdx)}
+        if getattr(dx, "_bf16", None) is not None:
+            res["dx_bf16"] = _rel(dx._bf16, rdx)
         fl = 1e-3 * g.norm().item()
         if dgamma is not None:
             res["dgamma"] = _rel(dgamma, (g * xh).sum(0) + (b0 if b0 is not None else 0), b0, fl)
         if dbeta is not None:
             res["dbeta"] = _rel(dbeta, g.sum(0) + (b1 if b1 is not None else 0), b1, fl)
-        self.records.append(("layer_norm_bwd", f"layer_norm_bwd R{x.shape[0]} D{x.shape[1]}", res))
+        self.records.append(("layer_norm_bwd", f"layer_norm_bwd R{x.shape[0]} D{x.shape[1]}"
+                             + (" res" if residual is not None else "") + (" twin" if twin else ""), res))
         return dx
 
     def _gelu_fwd_operand(self, x):

@@ -76,6 +76,55 @@ def test_layer_norm_fwd_bwd(R, D):
     torch.testing.assert_close(db, br.grad, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("R,D", [(242, 176), (3698, 344), (130, 512), (67, 12)])
+def test_layer_norm_bf16_and_residual_forms(R, D):
+    """avc_layer_norm_fwd2 with a bf16-only output and avc_layer_norm_bwd2 with the residual branch's
+    gradient added and the bf16 twin written (the mixer's LN -> add chains, MLPMixer.py:80-86),
+    dx and the parameter sums from the one-pass kernel, accumulate on."""
+    from autoformer_amd import kernels as K
+
+    w, b = _t(D, seed=1) * 0.3 + 1, _t(D, seed=2) * 0.1
+    x = _t(R, D, seed=3, scale=3.0)
+    dy, res = _t(R, D, seed=4), _t(R, D, seed=5)
+    y16, mean, rstd = K.layer_norm_fwd(x, w, b, 1e-5, out_bf16=True)
+    assert y16.dtype == torch.bfloat16
+    dg, db = _t(D, seed=6), _t(D, seed=7)
+    dg0, db0 = dg.clone(), db.clone()
+    dx = K.layer_norm_bwd(dy, x, w, mean, rstd, dg, db, accumulate=True, residual=res, twin=True)
+    xr, wr, br = (t.clone().requires_grad_() for t in (x, w, b))
+    yr = F.layer_norm(xr, (D,), wr, br, 1e-5)
+    yr.backward(dy)
+    torch.testing.assert_close(y16.float(), yr, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(dx, xr.grad + res, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(dx._bf16.float(), xr.grad + res, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(dg, dg0 + wr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(db, db0 + br.grad, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("B,L,C", [(2, 176, 512), (3, 344, 344)])
+def test_group_norm_twin(B, L, C):
+    from autoformer_amd import kernels as K
+
+    x = _t(B * L, C, seed=3, scale=2.0)
+    w, b = _t(C, seed=1) * 0.5 + 1, _t(C, seed=2) * 0.1
+    y, _, _ = K.group_norm_fwd(x, B, C, w, b, 1e-5, twin=True)
+    yr = F.group_norm(_frames_to_bcl(x, B, L), 1, w, b, 1e-5).transpose(1, 2).reshape(B * L, C)
+    torch.testing.assert_close(y, yr, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(y._bf16.float(), yr, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("B,R,C,ld", [(2, 1849, 344, 1856), (3, 121, 176, 128), (1, 7, 5, 8)])
+def test_transpose_pad_bf16_source(B, R, C, ld):
+    """avc_transpose_batched2 from a bf16 source (the LayerNorm's bf16 output) into padded rows."""
+    from autoformer_amd import kernels as K
+
+    x = _t(B * R, C, seed=12).bfloat16()
+    y = K.transpose_pad(x, B, R, C, ld, dtype=K.BF16)
+    ref = torch.zeros(B, C, ld, device=DEV, dtype=torch.bfloat16)
+    ref[:, :, :R] = x.view(B, R, C).transpose(1, 2)
+    torch.testing.assert_close(y.view(B, C, ld), ref, rtol=0, atol=0)
+
+
 def test_gelu_fwd_bwd():
     from autoformer_amd import kernels as K
 

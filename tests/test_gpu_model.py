@@ -101,13 +101,12 @@ def test_autovc_three_adam_steps_match_reference_solver(golden, fname):
 
 @pytest.mark.parametrize("fname", ["autovc_T128.npz", "autovc_T176.npz"])
 def test_autovc_bf16_loose(golden, fname):
-    """The bf16 production model against the reference's fp32 goldens (B=2).  mel_postnet is held
-    to the SURVEY §8(c) bf16 bar of 5e-2 as a relative Frobenius norm, and to 1e-1 in the max
-    norm: on 2 utterances the max-norm error is set by one element and moves by +-1.3e-2 when
-    only the fp32 summation order of one layer changes, while the Frobenius error does not
-    (tools/bf16_margin.py, T128 / T176, encoder conv0 folded or concatenated: rel-inf
-    6.7e-2 / 4.1e-2 vs 4.2e-2 / 4.8e-2; rel-Frobenius 3.27e-2 in all four).  Every production op
-    is held to 1e-2 against fp64 on its own inputs by tests/test_gpu_capture.py."""
+    """The bf16 production model against the reference's fp32 goldens (B=2), held to the SURVEY
+    §8(c) bf16 bar of 5e-2 as a relative Frobenius norm.  No max-norm bar at B=2: there it is set
+    by one element and moves by +-1.3e-2 when only the fp32 summation order of one layer changes
+    (tools/bf16_margin.py); the max-norm bars are measured at the bench batch against the oracle
+    (test_autovc_bf16_b64_vs_oracle).  Every production op is held to 1e-2 against fp64 on its own
+    inputs by tests/test_gpu_capture.py."""
     g = golden(fname)
     m = _model(int(g["freq"]), "bf16")
     x, e = torch.from_numpy(g["x"]).to(DEV), torch.from_numpy(g["emb"]).to(DEV)
@@ -116,8 +115,8 @@ def test_autovc_bf16_loose(golden, fname):
     torch.cuda.synchronize()
     got, ref = outs[1].detach().cpu().double().numpy().ravel(), g["mel_psnt"].astype(np.float64).ravel()
     assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 5e-2
-    assert rel_inf(outs[1].detach().cpu(), g["mel_psnt"]) < 1e-1
-    assert rel_inf(outs[0].detach().cpu(), g["mel"]) < 5e-2
+    mel = outs[0].detach().cpu().double().numpy().ravel()
+    assert np.linalg.norm(mel - g["mel"].ravel()) / np.linalg.norm(g["mel"]) < 5e-2
     np.testing.assert_allclose([l.item() for l in losses], g["losses"], rtol=5e-2)
     for p in m.parameters():
         assert torch.isfinite(p.grad).all()
@@ -137,6 +136,66 @@ def test_autovc_vs_oracle_batch8():
     outs, losses, total = _step(m, xt.to(DEV), et.to(DEV))
     assert rel_inf(outs[1].detach().cpu(), outs_ref[1].detach()) < 1e-3
     np.testing.assert_allclose([l.item() for l in losses], [l.item() for l in losses_ref], rtol=1e-4)
+
+
+def _rel_frob(a, b):
+    a = np.asarray(a, np.float64).ravel()
+    b = np.asarray(b, np.float64).ravel()
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+# bf16 bars at the bench configuration (B=64, T=128, freq=16), measured in round 4 against the fp32
+# oracle on identical weights and inputs (profiles/r4_bf16_b64_vs_oracle.txt) with ~2x headroom
+B64_BARS = {"mel_psnt_frob": 5e-2, "mel_psnt_inf": 1e-1, "mel_frob": 5e-2, "mel_inf": 1e-1, "loss_rtol": 5e-2,
+            "grad_frob": 1e-1, "zero_grad_abs": 1e-3}
+
+
+@pytest.mark.timeout(900)
+def test_autovc_bf16_b64_vs_oracle():
+    """The bf16 production model at the bench batch (B=64, T=128: 8192 frames, so the max-norm
+    error is an extreme over 655k mel values, not one element) against the CPU oracle's fp32
+    step on identical weights and inputs: outputs in the relative Frobenius and max norms, the
+    three losses, and every parameter gradient (relative Frobenius)."""
+    from autoformer_amd.detinit import det_inputs
+    from oracle import autovc_cpu as O
+
+    B, T, freq = 64, 128, 16
+    x, e = det_inputs(B, T, seed=21)
+    xt, et = torch.from_numpy(x), torch.from_numpy(e)
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    sd = O.make_state(O.autovc_spec())
+    losses_ref, total_ref, outs_ref = O.step_losses(lambda a, b, c: O.autovc_forward(sd, a, b, c, freq=freq), xt, et)
+    total_ref.backward()
+    m = _model(freq, "bf16")
+    outs, losses, total = _step(m, xt.to(DEV), et.to(DEV))
+    total.backward()
+    torch.cuda.synchronize()
+    got = {
+        "mel_psnt_frob": _rel_frob(outs[1].detach().cpu(), outs_ref[1].detach()),
+        "mel_psnt_inf": rel_inf(outs[1].detach().cpu(), outs_ref[1].detach()),
+        "mel_frob": _rel_frob(outs[0].detach().cpu(), outs_ref[0].detach()),
+        "mel_inf": rel_inf(outs[0].detach().cpu(), outs_ref[0].detach()),
+        "loss_rtol": max(abs(a.item() - b.item()) / abs(b.item()) for a, b in zip(losses, losses_ref)),
+    }
+    gref = {k: v.grad for k, v in sd.items() if v.requires_grad and v.grad is not None}
+    gmax = max(float(g.norm()) for g in gref.values())
+    rels, zeros = [], []
+    for name, p in m.named_parameters():
+        if name in gref and p.grad is not None:
+            if float(gref[name].norm()) < 1e-6 * gmax:
+                # analytically zero (a conv bias feeding a training-mode BatchNorm): absolute, scaled
+                # by the largest gradient norm of the step
+                zeros.append((float(p.grad.norm()) / gmax, name))
+            else:
+                rels.append((_rel_frob(p.grad.detach().cpu(), gref[name]), name))
+    assert len(rels) + len(zeros) >= 70, f"only {len(rels) + len(zeros)} parameter gradients matched the oracle's names"
+    rels.sort(reverse=True)
+    got["grad_frob"] = rels[0][0]
+    got["zero_grad_abs"] = max(zeros)[0] if zeros else 0.0
+    print("\nbf16 B=64 vs oracle: " + " ".join(f"{k} {v:.3e}" for k, v in got.items()) + f" | worst grads "
+          + ", ".join(f"{nm} {r:.2e}" for r, nm in rels[:5]) + f" | {len(zeros)} analytically-zero grads")
+    bad = {k: (v, B64_BARS[k]) for k, v in got.items() if not v < B64_BARS[k]}
+    assert not bad, bad
 
 
 def test_encoder_list_api_and_eval_mode(golden):
