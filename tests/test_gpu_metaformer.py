@@ -81,8 +81,18 @@ def test_layer_norm_bf16_and_residual_forms(R, D):
     """avc_layer_norm_fwd2 with a bf16-only output and avc_layer_norm_bwd2 with the residual branch's
     gradient added and the bf16 twin written (the mixer's LN -> add chains, MLPMixer.py:80-86),
     dx and the parameter sums from the one-pass kernel, accumulate on."""
+    import autoformer_amd as A
     from autoformer_amd import kernels as K
 
+    prev = "bf16" if K.compute() == K.BF16 else "fp32"
+    A.set_compute("bf16")  # the bf16 twins exist in bf16 compute mode only
+    try:
+        _ln_forms(K, R, D)
+    finally:
+        A.set_compute(prev)
+
+
+def _ln_forms(K, R, D):
     w, b = _t(D, seed=1) * 0.3 + 1, _t(D, seed=2) * 0.1
     x = _t(R, D, seed=3, scale=3.0)
     dy, res = _t(R, D, seed=4), _t(R, D, seed=5)
@@ -103,11 +113,17 @@ def test_layer_norm_bf16_and_residual_forms(R, D):
 
 @pytest.mark.parametrize("B,L,C", [(2, 176, 512), (3, 344, 344)])
 def test_group_norm_twin(B, L, C):
+    import autoformer_amd as A
     from autoformer_amd import kernels as K
 
     x = _t(B * L, C, seed=3, scale=2.0)
     w, b = _t(C, seed=1) * 0.5 + 1, _t(C, seed=2) * 0.1
-    y, _, _ = K.group_norm_fwd(x, B, C, w, b, 1e-5, twin=True)
+    prev = "bf16" if K.compute() == K.BF16 else "fp32"
+    A.set_compute("bf16")
+    try:
+        y, _, _ = K.group_norm_fwd(x, B, C, w, b, 1e-5, twin=True)
+    finally:
+        A.set_compute(prev)
     yr = F.group_norm(_frames_to_bcl(x, B, L), 1, w, b, 1e-5).transpose(1, 2).reshape(B * L, C)
     torch.testing.assert_close(y, yr, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(y._bf16.float(), yr, rtol=1e-2, atol=1e-2)
