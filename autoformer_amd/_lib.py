@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["gemm_ring.hip", "gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "graph.hip", "fold.hip", "disc.hip"]
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -36,7 +36,8 @@ class GemmDesc(ctypes.Structure):
                 ("accumulate", c_int), ("split_k", c_int), ("bn_partial", c_void_p), ("compute", c_int),
                 ("c_bf16", c_void_p), ("residual", c_void_p), ("cperm", c_int), ("row_bias", c_void_p),
                 ("rb_t", c_int), ("rb_pad", c_int), ("c_bf16_act", c_int), ("act_grad_of", c_void_p),
-                ("col_sum", c_void_p), ("col_sum_n", c_int), ("c_pre_bf16", c_void_p), ("act_grad_dtype", c_int)]
+                ("col_sum", c_void_p), ("col_sum_n", c_int), ("c_pre_bf16", c_void_p), ("act_grad_dtype", c_int),
+                ("c_trans_rows", c_int)]
 
 
 class BnFin(ctypes.Structure):

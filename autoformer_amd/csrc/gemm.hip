@@ -306,9 +306,9 @@ __global__ void __launch_bounds__(NT) gemm_generic_kernel(GemmArgs g) {
       for (int j = 0; j < 4; ++j) {
         int col = cbase + j * 16;
         if (col >= g.N) continue;
-        float* p = C + (long long)row * g.ldc + out_col(g, col);
+        float* p = C + out_off(g, row, col);
         float v = acc[i][j][e];
-        if (g.res && ks == 0) v += g.res[(long long)bz * g.cbs + (long long)row * g.ldc + col];
+        if (g.res && ks == 0) v += g.res[(long long)bz * g.cbs + out_off(g, row, col)];
         if (g.atomic) atomicAdd(p, v);
         else if (g.accumulate) *p += v;
         else *p = v;
@@ -842,6 +842,14 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
   g.c16pre = reinterpret_cast<bf16*>(d->c_pre_bf16);
   g.csum = d->col_sum;
   g.csum_n = d->col_sum_n;
+  g.ctr = d->c_trans_rows;
+  AVC_CHECK_ARG(g.ctr == 0 || (g.ctr > 0 && g.ctr % 4 == 0 && d->M % g.ctr == 0 && d->ldc == d->N && d->c &&
+                               !d->a.kstrided && !d->b.kstrided &&
+                               !d->c_bf16 && !d->cperm && !d->bn_partial && !bb &&
+                               !g.c16_act && !g.agrad && !g.csum && !d->row_bias && g.split_k == 1 &&
+                               (g.batch == 1 || d->c_batch_stride == (long long)d->M * d->N)),
+                "avc_gemm: c_trans_rows needs rows %% 4 == 0 dividing M, an fp32 C with ldc == N and no bf16 / BN / "
+                "GELU / col_sum / row-bias / cperm / split-K / batch-sum epilogue");
   AVC_CHECK_ARG(d->act_grad_dtype == AVC_F32 || d->act_grad_dtype == AVC_BF16, "avc_gemm: bad act_grad_dtype");
   AVC_CHECK_ARG(!g.csum || (!d->accumulate && g.split_k == 1 && !d->cperm &&
                             (g.batch == 1 || d->c_batch_stride == (long long)d->M * d->ldc) &&

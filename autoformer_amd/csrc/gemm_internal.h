@@ -35,6 +35,7 @@ struct GemmArgs {
   const void* agrad;   // avc_gemm_desc.act_grad_of: C *= GELU'(agrad[o]) (ring kernels only)
   int agrad16;         // agrad is bf16
   bf16* c16pre;        // avc_gemm_desc.c_pre_bf16: pre-activation C in bf16 (ring kernels only)
+  int ctr;             // avc_gemm_desc.c_trans_rows: C(m, n) stored at ((m / ctr) * N + n) * ctr + m % ctr
   float* csum;         // avc_gemm_desc.col_sum: csum[n] += column sums of the stored C (ring kernels only)
   int csum_n;
   const float* rbias;  // per-(utterance, edge class) row bias (avc_gemm_desc.row_bias), nullable
@@ -114,6 +115,15 @@ __device__ __forceinline__ long long out_col(const GemmArgs& g, int col) {
   return (long long)ch * g.cperm + tap;
 }
 
+// Element offset of C(row, col): row-major with the cperm column map, or the transposed blocks of
+// avc_gemm_desc.c_trans_rows (C(m, n) at ((m / ctr) * N + n) * ctr + m % ctr)
+__device__ __forceinline__ long long out_off(const GemmArgs& g, int row, int col) {
+  if (g.ctr) {
+    const int b = row / g.ctr;
+    return ((long long)b * g.N + col) * g.ctr + (row - b * g.ctr);
+  }
+  return (long long)row * g.ldc + out_col(g, col);
+}
 
 // Row bias of the conv0 fold (avc_gemm_desc.row_bias): rows rbase + 16 i + e, columns cbase + 16 j.
 template <int NJ>
@@ -174,7 +184,7 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
       for (int j = 0; j < NJ; ++j) {
         const int col = cbase + j * 16;
         if (col >= g.N) continue;
-        const long long o = (long long)row * g.ldc + out_col(g, col);
+        const long long o = out_off(g, row, col);
         float v = acc[i][j][e];
         if (g.res && ks == 0) v += g.res[(long long)bz * g.cbs + o];
         if (g.atomic) {

@@ -190,6 +190,35 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
                    (reinterpret_cast<uintptr_t>(P16) & 7) == 0;
   const bool acc_c = g.accumulate != 0, gelu16 = g.c16_act != 0;
   float* csum = g.csum;
+  if (g.ctr) {
+    // transposed blocks (avc_gemm_desc.c_trans_rows): a lane stores 4 consecutive ROWS of one
+    // column (contiguous in C, ctr % 4 == 0), consecutive lanes consecutive row quads
+#pragma unroll
+    for (int ch = 0; ch < TWM / 64; ++ch) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            reg[(ii * 16 + 4 * (lane >> 4) + e) * RP + j * 16 + (lane & 15)] = acc[ch * 4 + ii][j][e];
+      __syncthreads();
+#pragma unroll 4
+      for (int it = 0; it < NIT; ++it) {
+        const int q = it * 64 + lane, r4 = q & 15, cl = q >> 4;
+        const int row = m0 + wm * TWM + ch * 64 + 4 * r4, col = n0 + wn * TWN + cl;
+        if (row >= g.M || col >= g.N) continue;
+        f32x4 v = {reg[(4 * r4) * RP + cl], reg[(4 * r4 + 1) * RP + cl], reg[(4 * r4 + 2) * RP + cl],
+                   reg[(4 * r4 + 3) * RP + cl]};
+        const long long o = out_off(g, row, col);
+        if (res) v += *reinterpret_cast<const f32x4*>(res + o);
+        if (acc_c) v += *reinterpret_cast<const f32x4*>(C + o);
+        *reinterpret_cast<f32x4*>(C + o) = v;
+      }
+      __syncthreads();
+    }
+    return;
+  }
   // column-sum epilogue: lane's 4 columns are the same for every iteration (64 % (TWN/4) == 0)
   f32x4 cs = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -767,6 +796,9 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
   const RingCfg& c = g_ring;
   if (c.mode == 0 || (g.a.win && !c.win)) return false;
   if (g.K % 8 || g.klen % RBK || g.bnb_ws || g.atomic || g.cperm) return false;  // (no atomic / cperm stores)
+  if (g.ctr && ((reinterpret_cast<uintptr_t>(g.c) & 15) || (reinterpret_cast<uintptr_t>(g.res) & 15) ||
+                (g.cbs & 3)))
+    return false;  // the transposed stores are 16-B vectors
   if (!operand_ok(g.a, true) || !operand_ok(g.b, false)) return false;
   const long long units = (long long)g.batch * g.split_k;
   const bool win = g.a.win != 0;

@@ -92,7 +92,7 @@ def operand(t: torch.Tensor, ld: int, kstrided: bool = False, window=None, batch
 
 def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=None, accumulate=False, split_k=1,
          bn_partial=None, batch=1, c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0, bn_fin=None,
-         bnb=None, row_bias=None, c_bf16_act=0, act_grad_of=None, col_sum=None, col_sum_n=0):
+         bnb=None, row_bias=None, c_bf16_act=0, act_grad_of=None, col_sum=None, col_sum_n=0, c_trans_rows=0):
     """cperm = taps > 1: C's columns are (tap, channel) pairs written in nn.Conv1d's [Co][Ci][K]
     weight layout (a conv weight gradient straight into .grad).
     bn_fin = (gamma, beta, running_mean, running_var, nbt, momentum, eps, nupd): the BatchNorm
@@ -104,7 +104,8 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     c_bf16_act = ACT_GELU: c_bf16 receives GELU(C), C itself (the pre-activation) is stored to c --
     fp32, or bf16 (avc_gemm_desc.c_pre_bf16) when c is a bf16 tensor; act_grad_of = x (fp32 or
     bf16): C *= GELU'(x) -- the MLP-Mixer GELU forward / backward folded into the GEMM epilogue.
-    col_sum: col_sum[:col_sum_n or N] += column sums of C (a bias gradient, float atomics)."""
+    col_sum: col_sum[:col_sum_n or N] += column sums of C (a bias gradient, float atomics).
+    c_trans_rows = R: every R-row block of C stored transposed (avc_gemm_desc.c_trans_rows)."""
     _dev(c, bias, bn_partial, c_bf16, residual)
     if _DETERMINISTIC:
         split_k = 1
@@ -141,6 +142,7 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
         d.act_grad_of = act_grad_of.data_ptr()
         d.act_grad_dtype = _dt(act_grad_of)
     d.c_pre_bf16 = _ptr(pre16)
+    d.c_trans_rows = int(c_trans_rows)
     if row_bias is not None:
         rb, rb_t, rb_pad = row_bias
         _dev(rb)

@@ -335,10 +335,18 @@ class _MLPMixerFn(torch.autograd.Function):
         bb1p = K.pad_cols(bb1.view(1, 4 * NP), 4 * NPp).view(-1)
         UT, V = _gelu_gemm(D, 4 * NPp, NPp, operand(Y1T, NPp, batch_stride=D * NPp), operand(W1n, NPp), bb1p, dev,
                            batch=B)
-        RT = torch.empty(B * D, NP, device=dev)
-        K.gemm(D, NP, 4 * NPp, operand(V, 4 * NPp, batch_stride=D * 4 * NPp), operand(W2c, 4 * NPp), RT, bias=bb2,
-               batch=B, c_batch_stride=D * NP)
-        Z1 = K.transpose_batched(RT, B, D, NP, out=K.convert(Z, K.F32), accumulate=True).view(B * NP, D)
+        if bf and D % 4 == 0:
+            # Z1 = Z + RT^T per utterance straight from the GEMM epilogue: each D-row block of the
+            # (B*D x NP) product stored transposed into the frame-major layout, Z read there as the
+            # residual (avc_gemm_desc.c_trans_rows; no RT tensor, no copy of Z, no transpose pass)
+            Z1 = torch.empty(B * NP, D, device=dev)
+            K.gemm(D, NP, 4 * NPp, operand(V, 4 * NPp, batch_stride=D * 4 * NPp), operand(W2c, 4 * NPp), Z1, bias=bb2,
+                   batch=B, c_batch_stride=D * NP, residual=Z, c_trans_rows=D)
+        else:
+            RT = torch.empty(B * D, NP, device=dev)
+            K.gemm(D, NP, 4 * NPp, operand(V, 4 * NPp, batch_stride=D * 4 * NPp), operand(W2c, 4 * NPp), RT,
+                   bias=bb2, batch=B, c_batch_stride=D * NP)
+            Z1 = K.transpose_batched(RT, B, D, NP, out=K.convert(Z, K.F32), accumulate=True).view(B * NP, D)
         Y2, m2, r2 = K.layer_norm_fwd(Z1, g2, b2n, mix.ln_eps[1], out_bf16=bf)
         U2, V2 = _gelu_gemm(B * NP, 4 * D, D, operand(K.twin(Y2), D), operand(w3C, D), bb3, dev)
         Z2 = _lin(V2, B * NP, D, 4 * D, w4C, bb4, residual=Z1)

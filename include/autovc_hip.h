@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 19
+#define AVC_ABI_VERSION 20
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -95,6 +95,11 @@ typedef struct {
   void* c_pre_bf16;      /* nullable, with c_bf16_act: the pre-activation C rounded to bf16 (same ldc) -- the
                             backward's act_grad_of at half the bytes of an fp32 C */
   int act_grad_dtype;    /* AVC_F32 / AVC_BF16: element type of act_grad_of */
+  int c_trans_rows;      /* 0, or R > 0 (R % 4 == 0, dividing M of the folded batch): C(m, n) is stored at
+                            ((m / R) * N + n) * R + m % R -- each R-row block of C transposed, the per-utterance
+                            (D x NP) token-mixing output written straight into the frame-major (NP x D) layout
+                            with the residual read in the same layout (MLPMixer.py:80-86).  fp32 C only, ldc == N,
+                            bias / residual / accumulate; no bf16 / BN / GELU / col_sum / row-bias epilogue */
 } avc_gemm_desc;
 
 int avc_abi_version(void);

@@ -69,8 +69,12 @@ def _rel(got, ref, base=None, floor=0.0):
     return num / den if den > 0 else num
 
 
-def _c_view(c, M, N, ldc, batch, cbs, cperm):
+def _c_view(c, M, N, ldc, batch, cbs, cperm, ctr=0):
     base, off = _storage_view(c)
+    if ctr:  # avc_gemm_desc.c_trans_rows: every ctr-row block of C stored transposed
+        nb = batch if cbs else 1
+        v = base.as_strided((nb * M // ctr, N, ctr), (N * ctr, ctr, 1), off)
+        return v.transpose(1, 2).reshape(nb, M, N)
     if cperm:
         taps = cperm
         v = base.as_strided((M, taps, N // taps), (ldc, 1, taps), off)
@@ -186,18 +190,19 @@ class Capture:
     # ---------------------------------------------------------------- wrappers
     def _gemm(self, M, N, Kd, a, b, c, ldc=None, bias=None, accumulate=False, split_k=1, bn_partial=None, batch=1,
               c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0, bn_fin=None, bnb=None, row_bias=None,
-              c_bf16_act=0, act_grad_of=None, col_sum=None, col_sum_n=0):
+              c_bf16_act=0, act_grad_of=None, col_sum=None, col_sum_n=0, c_trans_rows=0):
         f = self._orig["gemm"]
         kw = dict(ldc=ldc, bias=bias, accumulate=accumulate, split_k=split_k, bn_partial=bn_partial, batch=batch,
                   c_batch_stride=c_batch_stride, comp=comp, c_bf16=c_bf16, residual=residual, cperm=cperm,
                   bn_fin=bn_fin, bnb=bnb, row_bias=row_bias, c_bf16_act=c_bf16_act, act_grad_of=act_grad_of,
-                  col_sum=col_sum, col_sum_n=col_sum_n)
+                  col_sum=col_sum, col_sum_n=col_sum_n, c_trans_rows=c_trans_rows)
         if bnb is not None and self.skip_bnb:
             return f(M, N, Kd, a, b, c, **kw)
         torch.cuda.synchronize()
         ldc_ = N if ldc is None else ldc
         only16 = c.dtype == torch.bfloat16 and not c_bf16_act  # (with c_bf16_act: a bf16 pre-activation)
-        cv = _c_view(c, M, N, ldc_, batch, c_batch_stride, cperm)
+        ctr = c_trans_rows
+        cv = _c_view(c, M, N, ldc_, batch, c_batch_stride, cperm, ctr)
         before = cv.double().clone() if accumulate else None
         ncs = (col_sum_n or N) if col_sum is not None else 0
         cs_before = col_sum[:ncs].double().clone() if ncs else None
@@ -212,7 +217,7 @@ class Capture:
         if bias is not None:
             P = P + bias.double()[None, None, :N]
         if residual is not None:
-            P = P + _c_view(residual, M, N, ldc_, batch, c_batch_stride, 0).double()
+            P = P + _c_view(residual, M, N, ldc_, batch, c_batch_stride, 0, ctr).double()
         if row_bias is not None:
             P = P + row_bias_rows(row_bias[0], M, row_bias[1], row_bias[2])[None]
         if act_grad_of is not None:  # the GELU backward folded into the epilogue
@@ -220,13 +225,13 @@ class Capture:
             P = P * (0.5 * (1.0 + torch.erf(xg / 2 ** 0.5)) + xg * torch.exp(-0.5 * xg * xg) / (2 * torch.pi) ** 0.5)
         stats = f(M, N, Kd, a, b, c, **kw)
         torch.cuda.synchronize()
-        got = _c_view(c, M, N, ldc_, batch, c_batch_stride, cperm).double()
+        got = _c_view(c, M, N, ldc_, batch, c_batch_stride, cperm, ctr).double()
         ref = P if before is None else before + P
         tag = (f"gemm M{M} N{N} K{Kd}" + (f" b{batch}" if batch > 1 else "") + (f" sk{split_k}" if split_k > 1 else "")
                + (" acc" if accumulate else "") + (" win" if a.taps or b.taps else "") + (" cperm" if cperm else "")
                + (" bf16out" if only16 else "") + (" rowbias" if row_bias is not None else "")
                + (" gelu" if c_bf16_act else "") + (" dgelu" if act_grad_of is not None else "")
-               + (" colsum" if ncs else ""))
+               + (" colsum" if ncs else "") + (" trans" if ctr else ""))
         res = {"C": _rel(got, ref, before)}
         if ncs:  # the bias gradient accumulated in the epilogue: column sums of the stored values
             cs_ref = cs_before + ref.reshape(-1, N)[:, :ncs].sum(0)

@@ -188,3 +188,26 @@ def test_col_sum_epilogue(ring, batch, store):
     assert _rel(d.float(), dref) < tol
     assert _rel(cs[:n] - cs0[:n], dref[:, :n].sum(0)) < tol
     assert torch.equal(cs[n:], cs0[n:])
+
+
+@pytest.mark.parametrize("ring", [-1, 0])
+@pytest.mark.parametrize("B,D,NP,Kd", [(5, 344, 1849, 512), (3, 176, 121, 512), (2, 8, 37, 64)])
+def test_transposed_store(ring, B, D, NP, Kd):
+    """c_trans_rows = D: the per-utterance (D x NP) products Z1_b = Z_b + (V_b W^T + b)^T written
+    straight into the frame-major (NP x D) layout with the residual read there (the MLP-Mixer
+    token FF output, MLPMixer.py:80-86), on the ring kernel and on the older kernels' epilogue."""
+    from autoformer_amd import kernels as K
+
+    torch.manual_seed(B + D)
+    v = torch.randn(B * D, Kd, device=DEV).bfloat16()
+    w = (torch.randn(NP, Kd, device=DEV) * 0.1).bfloat16()
+    bias = torch.randn(NP, device=DEV)
+    z = torch.randn(B * NP, D, device=DEV)
+    _ring(ring)
+    z1 = torch.empty(B * NP, D, device=DEV)
+    K.gemm(D, NP, Kd, K.operand(v, Kd, batch_stride=D * Kd), K.operand(w, Kd), z1, bias=bias, batch=B,
+           c_batch_stride=D * NP, residual=z, c_trans_rows=D)
+    torch.cuda.synchronize()
+    rt = (v.float() @ w.float().t() + bias).view(B, D, NP)
+    ref = z + rt.transpose(1, 2).reshape(B * NP, D)
+    assert _rel(z1, ref) < 1e-5

@@ -24,3 +24,5 @@ timeout -k 10 200 python -u tools/lstm_trace.py > $OUT/lstm_trace.txt 2>&1 || ex
 AVC_LSTM_BWD_ABL=1 timeout -k 10 200 python -u tools/lstm_trace.py > $OUT/lstm_trace_abl.txt 2>&1 || exit 1
 grep -a "bwd" $OUT/lstm_trace.txt $OUT/lstm_trace_abl.txt
 grep -o '"ms_per_step": [0-9.]*' $OUT/*.json
+timeout -k 10 200 python -u tools/blas_probe2.py > $OUT/blas_probe2.txt 2>&1 || exit 1
+cat $OUT/blas_probe2.txt
