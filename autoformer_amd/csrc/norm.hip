@@ -266,7 +266,8 @@ constexpr int LRB = 64;
 template <int NV>
 __global__ void __launch_bounds__(1024) ln_bwd_v_kernel(const float* dy, const float* x, const float* gamma,
                                                         const float* mean, const float* rstd, int R, int D,
-                                                        const float* dres, float* dx, bf16* dx16, float* ws) {
+                                                        const float* dres, float* dx, bf16* dx16, float* ws,
+                                                        float* rsum) {
   __shared__ f32x4 red[2][16][64 * NV];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, D4 = D >> 2;
   f32x4 pa[NV], pb[NV], gm[NV];
@@ -298,6 +299,7 @@ __global__ void __launch_bounds__(1024) ln_bwd_v_kernel(const float* dy, const f
       pb[i] += dv[i];
     }
     const float m0 = warp_sum(s0) / (float)D, m1 = warp_sum(s1) / (float)D;
+    float rsv = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c4 = l + 64 * i;
@@ -306,6 +308,11 @@ __global__ void __launch_bounds__(1024) ln_bwd_v_kernel(const float* dy, const f
       if (dres) d += reinterpret_cast<const f32x4*>(dres + o)[c4];
       if (dx) reinterpret_cast<f32x4*>(dx + o)[c4] = d;
       if (dx16) *reinterpret_cast<bf16x4*>(dx16 + o + 4 * c4) = bf16x4{(bf16)d[0], (bf16)d[1], (bf16)d[2], (bf16)d[3]};
+      rsv += d[0] + d[1] + d[2] + d[3];
+    }
+    if (rsum) {  // the row's sum of dx (a later bias gradient over the transposed layout)
+      rsv = warp_sum(rsv);
+      if (l == 0) rsum[row] = rsv;
     }
   }
   if (!ws) return;
@@ -502,7 +509,8 @@ extern "C" int avc_layer_norm_fwd(const float* x, int R, int D, const float* gam
 
 extern "C" int avc_layer_norm_bwd2(const float* dy, const float* x, const float* gamma, const float* mean,
                                    const float* rstd, int R, int D, const float* dres, float* dx, void* dx16,
-                                   float* dgamma, float* dbeta, int accumulate, float* ws, void* stream) {
+                                   float* row_sum, float* dgamma, float* dbeta, int accumulate, float* ws,
+                                   void* stream) {
   AVC_CHECK_ARG(dy && x && mean && rstd && (dx || dx16) && ws && R > 0 && D > 0, "avc_layer_norm_bwd: bad args");
   hipStream_t s = as_stream(stream);
   bf16* o16 = static_cast<bf16*>(dx16);
@@ -511,13 +519,16 @@ extern "C" int avc_layer_norm_bwd2(const float* dy, const float* x, const float*
     const bool par = dgamma || dbeta;
     const int nrb = cdiv(R, LRB);
     if (D <= 256)
-      ln_bwd_v_kernel<1><<<nrb, 1024, 0, s>>>(dy, x, gamma, mean, rstd, R, D, dres, dx, o16, par ? ws : nullptr);
+      ln_bwd_v_kernel<1><<<nrb, 1024, 0, s>>>(dy, x, gamma, mean, rstd, R, D, dres, dx, o16, par ? ws : nullptr,
+                                              row_sum);
     else
-      ln_bwd_v_kernel<2><<<nrb, 1024, 0, s>>>(dy, x, gamma, mean, rstd, R, D, dres, dx, o16, par ? ws : nullptr);
+      ln_bwd_v_kernel<2><<<nrb, 1024, 0, s>>>(dy, x, gamma, mean, rstd, R, D, dres, dx, o16, par ? ws : nullptr,
+                                              row_sum);
     if (par) pair_final_kernel<<<cdiv(D, 64), 1024, 0, s>>>(ws, nrb, D, dgamma, dbeta, accumulate);
     return avc_check_launch("avc_layer_norm_bwd");
   }
-  AVC_CHECK_ARG(dx && !dx16 && !dres, "avc_layer_norm_bwd: dres / bf16 output need D %% 4 == 0, D <= 512, aligned rows");
+  AVC_CHECK_ARG(dx && !dx16 && !dres && !row_sum,
+                "avc_layer_norm_bwd: dres / bf16 output / row sums need D %% 4 == 0, D <= 512, aligned rows");
   return avc_layer_norm_bwd(dy, x, gamma, mean, rstd, R, D, dx, dgamma, dbeta, accumulate, ws, stream);
 }
 

@@ -709,14 +709,15 @@ def layer_norm_fwd(x, gamma, beta, eps, out_bf16=False):
     return y, mean, rstd
 
 
-def layer_norm_bwd(dy, x, gamma, mean, rstd, dgamma=None, dbeta=None, accumulate=False, residual=None, twin=False):
+def layer_norm_bwd(dy, x, gamma, mean, rstd, dgamma=None, dbeta=None, accumulate=False, residual=None, twin=False,
+                   row_sum=None):
     """dx (+ residual: the gradient of a residual branch around the norm, added in the same pass;
-    twin: its bf16 operand twin written beside it)."""
+    twin: its bf16 operand twin written beside it; row_sum: a (R,) tensor receiving each row's sum of dx)."""
     R, D = x.shape
     dx = torch.empty_like(x)
     dx16 = _twin_buf(dx, None) if twin else None
     L.call("avc_layer_norm_bwd2", dy.data_ptr(), x.data_ptr(), _ptr(gamma), mean.data_ptr(), rstd.data_ptr(), R, D,
-           _ptr(residual), dx.data_ptr(), _ptr(dx16), _ptr(dgamma), _ptr(dbeta), int(accumulate),
+           _ptr(residual), dx.data_ptr(), _ptr(dx16), _ptr(row_sum), _ptr(dgamma), _ptr(dbeta), int(accumulate),
            _ws(R, D, x.device).data_ptr(), stream())
     return attach_twin(dx, dx16) if dx16 is not None else dx
 

@@ -411,7 +411,12 @@ class _MLPMixerFn(torch.autograd.Function):
         dY2 = torch.empty(M, D, device=dev)
         K.gemm(M, D, 4 * D, operand(dU2, 4 * D), operand(w3T, 4 * D), dY2)
         dg2, db2n = (_sink(g2), _sink(b2n)) if sink else (torch.empty(D, device=dev), torch.empty(D, device=dev))
-        dZ1 = K.layer_norm_bwd(dY2, Z1, g2, m2, r2, dg2, db2n, accumulate=sink, residual=dZ2)
+        # bf16 mode: dZ1's row sums come out of the same pass -- dbb2[p] = sum over (b, d) of
+        # dRT_b[d][p] = sum over b of rowsum(dZ1)[b*NP + p] -- and the padded bf16 dRT operand is
+        # ONE transpose of dZ1 (no fp32 dRT, no colsum / pad passes over it)
+        tr = K.compute() == K.BF16 and D % 4 == 0
+        rs1 = torch.empty(B * NP, device=dev) if tr else None
+        dZ1 = K.layer_norm_bwd(dY2, Z1, g2, m2, r2, dg2, db2n, accumulate=sink, residual=dZ2, row_sum=rs1)
         # token FF: Z1 = Z + (GELU(Y1^T W1^T + b1) W2^T + b2)^T   per utterance.  dRT_b = dZ1_b^T is
         # read in place from dZ1 (as the transposed operand), so NP is never a contiguous dimension.
         W1T, W2c, _, W2t = _token_mix_weights(mix, w1, w2, NP)
@@ -419,9 +424,13 @@ class _MLPMixerFn(torch.autograd.Function):
         # Token-mixing weight gradients sum over utterances AND the D positions: with the
         # per-utterance transposes (B*D rows) that sum is the K dimension of ONE product
         # (K = B*D, both operands K-strided), with no per-utterance slabs to reduce.
-        dRT = K.transpose_batched(dZ1, B, NP, D).view(B * D, NP)
-        dbb2 = K.colsum(dRT, B * D, NP, out=_sink(bb2), accumulate=sink)
-        dRTp = K.pad_cols(dRT, NPp, dtype=K.compute())
+        if tr:
+            dbb2 = K.colsum(rs1, B, NP, out=_sink(bb2), accumulate=sink)
+            dRTp = K.transpose_pad(dZ1, B, NP, D, NPp, dtype=K.BF16)
+        else:
+            dRT = K.transpose_batched(dZ1, B, NP, D).view(B * D, NP)
+            dbb2 = K.colsum(dRT, B * D, NP, out=_sink(bb2), accumulate=sink)
+            dRTp = K.pad_cols(dRT, NPp, dtype=K.compute())
         with _wside(side, dRTp, V):
             dW2p = torch.empty(NPp, 4 * NPp, device=dev)
             K.gemm(NPp, 4 * NPp, B * D, operand(dRTp, NPp, kstrided=True), operand(V, 4 * NPp, kstrided=True), dW2p,
@@ -435,9 +444,13 @@ class _MLPMixerFn(torch.autograd.Function):
             K.gemm(4 * NPp, NPp, B * D, operand(dUT, 4 * NPp, kstrided=True), operand(Y1T, NPp, kstrided=True),
                    dW1p, split_k=K.auto_split_k(4 * NPp, NPp, B * D))
             dW1 = K.crop_add(dW1p[:4 * NP], _sink(w1).view(4 * NP, NP)) if sink else K.pad_cols(dW1p, NP)[:4 * NP]
-        dY1T = torch.empty(B * D, NP, device=dev)
-        K.gemm(B * D, NP, 4 * NPp, operand(dUT, 4 * NPp), operand(W1T, 4 * NPp), dY1T)
-        dY1 = K.transpose_batched(dY1T, B, D, NP).view(M, D)
+        if tr:  # dY1 straight into the frame-major layout (avc_gemm_desc.c_trans_rows)
+            dY1 = torch.empty(M, D, device=dev)
+            K.gemm(B * D, NP, 4 * NPp, operand(dUT, 4 * NPp), operand(W1T, 4 * NPp), dY1, c_trans_rows=D)
+        else:
+            dY1T = torch.empty(B * D, NP, device=dev)
+            K.gemm(B * D, NP, 4 * NPp, operand(dUT, 4 * NPp), operand(W1T, 4 * NPp), dY1T)
+            dY1 = K.transpose_batched(dY1T, B, D, NP).view(M, D)
         dg1, db1n = (_sink(g1), _sink(b1n)) if sink else (torch.empty(D, device=dev), torch.empty(D, device=dev))
         dZ = K.twin(K.layer_norm_bwd(dY1, Z, g1, m1, r1, dg1, db1n, accumulate=sink, residual=dZ1, twin=True))
         # patch embedding

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 20
+#define AVC_ABI_VERSION 21
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -402,15 +402,16 @@ int avc_layer_norm_bwd(const float* dy, const float* x, const float* gamma, cons
                        int R, int D, float* dx, float* dgamma, float* dbeta, int accumulate, float* ws, void* stream);
 /* The same passes with bf16 outputs: y16 / dx16 (nullable) beside or instead of the fp32 y / dx (GEMM operands
  * only ever read in bf16), and for the LayerNorm backward dres (nullable): dx = dres + the norm's gradient -- the
- * residual add after the norm (MLPMixer.py:80-86) folded into the pass.  The bf16 / dres forms need C (D) % 4 == 0,
+ * residual add after the norm (MLPMixer.py:80-86) folded into the pass, and row_sum (nullable): each row's sum of dx
+ * (the token-mixing bias gradient of the transposed layout, summed per patch).  The bf16 / dres forms need C (D) % 4 == 0,
  * D <= 512 and 16-B aligned rows; the LayerNorm backward then computes dx and the parameter sums in ONE pass. */
 int avc_group_norm_fwd2(const float* x, int B, long long S, int C, const float* gamma, const float* beta, float eps,
                         float* y, void* y16, float* mean, float* rstd, void* stream);
 int avc_layer_norm_fwd2(const float* x, int R, int D, const float* gamma, const float* beta, float eps, float* y,
                         void* y16, float* mean, float* rstd, void* stream);
 int avc_layer_norm_bwd2(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
-                        int R, int D, const float* dres, float* dx, void* dx16, float* dgamma, float* dbeta,
-                        int accumulate, float* ws, void* stream);
+                        int R, int D, const float* dres, float* dx, void* dx16, float* row_sum, float* dgamma,
+                        float* dbeta, int accumulate, float* ws, void* stream);
 /* exact (erf) GELU backward from the GELU input x; the forward is avc_act_fwd(AVC_ACT_GELU). */
 int avc_gelu_bwd(const float* g, const float* x, float* dx, long long n, void* stream);
 /* y = AvgPool1d(3,1,1,count_include_pad=False)(x) - x along the frames of (B, L, C);

@@ -428,12 +428,12 @@ class Capture:
         return y, mean, rstd
 
     def _layer_norm_bwd(self, dy, x, gamma, mean, rstd, dgamma=None, dbeta=None, accumulate=False, residual=None,
-                        twin=False):
+                        twin=False, row_sum=None):
         torch.cuda.synchronize()
         b0 = dgamma.double().clone() if (dgamma is not None and accumulate) else None
         b1 = dbeta.double().clone() if (dbeta is not None and accumulate) else None
         dx = self._orig["layer_norm_bwd"](dy, x, gamma, mean, rstd, dgamma, dbeta, accumulate, residual=residual,
-                                          twin=twin)
+                                          twin=twin, row_sum=row_sum)
         torch.cuda.synchronize()
         xh = (x.double() - mean.double()[:, None]) * rstd.double()[:, None]
         g = dy.double()
@@ -444,6 +444,8 @@ class Capture:
         res = {"dx": _rel(dx, rdx)}
         if getattr(dx, "_bf16", None) is not None:
             res["dx_bf16"] = _rel(dx._bf16, rdx)
+        if row_sum is not None:
+            res["row_sum"] = _rel(row_sum, rdx.sum(1), None, 1e-3 * rdx.norm().item())
         fl = 1e-3 * g.norm().item()
         if dgamma is not None:
             res["dgamma"] = _rel(dgamma, (g * xh).sum(0) + (b0 if b0 is not None else 0), b0, fl)

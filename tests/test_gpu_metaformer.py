@@ -100,13 +100,15 @@ def _ln_forms(K, R, D):
     assert y16.dtype == torch.bfloat16
     dg, db = _t(D, seed=6), _t(D, seed=7)
     dg0, db0 = dg.clone(), db.clone()
-    dx = K.layer_norm_bwd(dy, x, w, mean, rstd, dg, db, accumulate=True, residual=res, twin=True)
+    rsum = torch.empty(R, device=DEV)
+    dx = K.layer_norm_bwd(dy, x, w, mean, rstd, dg, db, accumulate=True, residual=res, twin=True, row_sum=rsum)
     xr, wr, br = (t.clone().requires_grad_() for t in (x, w, b))
     yr = F.layer_norm(xr, (D,), wr, br, 1e-5)
     yr.backward(dy)
     torch.testing.assert_close(y16.float(), yr, rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(dx, xr.grad + res, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(dx._bf16.float(), xr.grad + res, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(rsum, (xr.grad + res).sum(1), rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dg, dg0 + wr.grad, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(db, db0 + br.grad, rtol=1e-4, atol=1e-4)
 
