@@ -145,9 +145,12 @@ def _rel_frob(a, b):
 
 
 # bf16 bars at the bench configuration (B=64, T=128, freq=16), measured in round 4 against the fp32
-# oracle on identical weights and inputs (profiles/r4_bf16_b64_vs_oracle.txt) with ~2x headroom
-B64_BARS = {"mel_psnt_frob": 5e-2, "mel_psnt_inf": 1e-1, "mel_frob": 5e-2, "mel_inf": 1e-1, "loss_rtol": 5e-2,
-            "grad_frob": 1e-1, "zero_grad_abs": 1e-3}
+# oracle on identical weights and inputs with ~1.6-1.8x headroom (profiles/r4_bf16_b64_vs_oracle.txt:
+# mel_psnt rel-Frobenius 1.81e-2 / rel-inf 2.51e-2, mel 8.8e-3 / 1.07e-2, losses 2.8e-5, worst
+# parameter gradient 0.138 (encoder conv BN bias, through the code loss and the BiLSTM), gradients
+# that are analytically zero 2.1e-5 of the largest gradient norm)
+B64_BARS = {"mel_psnt_frob": 3e-2, "mel_psnt_inf": 4e-2, "mel_frob": 1.5e-2, "mel_inf": 2e-2, "loss_rtol": 1e-3,
+            "grad_frob": 0.25, "zero_grad_abs": 1e-4}
 
 
 @pytest.mark.timeout(900)
