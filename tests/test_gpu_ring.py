@@ -57,6 +57,11 @@ def test_ring_gemm_configs(cfg, M, N, Kd):
     torch.cuda.synchronize()
     assert _rel(c, ref) < 1e-5
     assert _rel(c16.float(), ref) < 1e-2
+    # bf16-only output (the 16-B bf16 store path of the ring epilogue), no residual
+    o16 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    K.gemm(M, N, Kd, K.operand(a, Kd), K.operand(b, Kd), o16, bias=bias)
+    torch.cuda.synchronize()
+    assert _rel(o16.float(), ref - res) < 1e-2
     # accumulate on top
     c2 = c.clone()
     K.gemm(M, N, Kd, K.operand(a, Kd), K.operand(b, Kd), c2, accumulate=True)
