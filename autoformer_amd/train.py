@@ -249,6 +249,7 @@ class TrainStep:
         set_grad_sink(True)  # kernels accumulate straight into the flat gradient buffer
         self.opt = FusedAdam(self.flat, self.gflat, lr)
         self.graph_fb = None
+        self.graph_f = None  # forward-only graph (capture(forward_only=True)); the backward stays eager
         self.world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
         self.loss = None
         # The decoder / postnet (/ discriminator) gradients are final once the backward reaches
@@ -347,17 +348,29 @@ class TrainStep:
         if self.graph_fb is not None:
             self.graph_fb.replay()
             loss = self.loss
+        elif self.graph_f is not None:
+            # the captured forward replays into its static activations; the eager backward walks
+            # the autograd graph recorded at capture (retained) over those same tensors
+            self.gflat.zero_()
+            self.graph_f.replay()
+            self.loss.backward(retain_graph=True)
+            join_side()
+            loss = self.loss
         else:
             loss = self._fwd_bwd(x, emb, overlap=self.split is not None)
         self._finish()
         if self.graph_fb is None:
-            prefetch_packs()  # next step's weight packs, on the side stream
+            prefetch_packs()  # next step's weight packs (the backward's, with a forward graph), on the side stream
         self._probe_fault()
         return loss
 
-    def capture(self, x, emb, warmup=2):
+    def capture(self, x, emb, warmup=2, forward_only=False):
         """Capture zero_grad + forward + re-pass + losses + backward into one hipGraph
-        (x, emb must stay the same tensors: the synthetic batch is resident in HBM)."""
+        (x, emb must stay the same tensors: the synthetic batch is resident in HBM).
+        forward_only: capture the forward + re-pass + losses only and keep their autograd graph;
+        every step replays the forward (no host work for its ~half of the step's launches) and
+        runs the backward eagerly over the retained graph, so the weight-gradient side stream
+        still overlaps the data-gradient chain (one graph replays it serially)."""
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -373,6 +386,20 @@ class TrainStep:
         # from the side stream runs after the main chain instead of beside it (the
         # round-3 main / side split replayed NaN from its second replay and was removed).
         g = torch.cuda.CUDAGraph()
+        if forward_only:
+            # the decoder hook (early decoder-slice Adam) is registered on the captured tensors and
+            # fires in every eager backward
+            self.model._decoder_bwd_done = self._decoder_done if self.split is not None else None
+            try:
+                with torch.cuda.graph(g):
+                    loss, _, x_psnt = self.loss_fn(self.model, x, emb, self.lambda_cd)
+                    if self.extra is not None:
+                        loss = loss + self.extra(x, emb, x_psnt)
+            finally:
+                self.model._decoder_bwd_done = None
+            self.loss = loss
+            self.graph_f = g
+            return
         with torch.cuda.graph(g):
             self.loss = self._fwd_bwd(x, emb)
         self.graph_fb = g  # capture only records: the next step() replays it

@@ -244,6 +244,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--graph", action="store_true",
                     help="replay the fwd+bwd as one hipGraph (serialises the side-stream wgrad branch on ROCm 7)")
+    ap.add_argument("--graph-fwd", action="store_true",
+                    help="replay the forward + losses as a hipGraph, backward eager over the retained autograd graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
@@ -303,8 +305,8 @@ def main():
 
     for _ in range(args.warmup):
         trainer.step(x, e)
-    if args.graph:
-        trainer.capture(x, e)
+    if args.graph or args.graph_fwd:
+        trainer.capture(x, e, forward_only=args.graph_fwd)
         trainer.step(x, e)
     torch.cuda.synchronize()
     if world > 1:
@@ -356,7 +358,7 @@ def main():
            "config": {"workload": f"{name} {step}, B={B}/GPU, T={T}, freq={freq}, dim_neck=44, dim_emb=256, "
                                   f"dim_pre=512",
                       "global_batch": B * world, "seq_len": T, "freq": freq, "parallelism": f"dp{world}",
-                      "graph": bool(args.graph)},
+                      "graph": "fwd+bwd" if args.graph else ("fwd" if args.graph_fwd else False)},
            "step_mfma_frac": round(value * fpf / (world * peak * 1e12), 5) if fpf else None,
            "final_loss": loss_v}
     if world > 1:

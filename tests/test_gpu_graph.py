@@ -24,7 +24,7 @@ def _model(comp, freq):
     return m.to(DEV).train()
 
 
-def _compare(comp, B, T, freq, gtol, steps=4):
+def _compare(comp, B, T, freq, gtol, steps=4, forward_only=False):
     from autoformer_amd.detinit import det_inputs
     from autoformer_amd.layers import set_grad_sink
     from autoformer_amd.train import TrainStep
@@ -35,8 +35,8 @@ def _compare(comp, B, T, freq, gtol, steps=4):
     xb, eb = batches[0][0].clone(), batches[0][1].clone()
     try:
         tb.step(xb, eb)
-        tb.capture(xb, eb, warmup=0)
-        assert tb.graph_fb is not None
+        tb.capture(xb, eb, warmup=0, forward_only=forward_only)
+        assert (tb.graph_f if forward_only else tb.graph_fb) is not None
         for i, (x, e) in enumerate(batches):
             la = ta.step(x, e)
             ga = ta.gflat.clone()
@@ -62,3 +62,12 @@ def test_graph_replay_matches_eager_bf16_c2():
     """At the C2 shape (B=64, T=128, bf16: the persistent recurrences, split-K weight gradients,
     halo conv kernels).  bf16 run-to-run spread of a gradient tensor is ~1e-3 (split-K order)."""
     _compare("bf16", 64, 128, 16, 1e-2)
+
+
+def test_forward_graph_matches_eager_fp32():
+    """capture(forward_only=True): forward replayed, backward eager over the retained graph."""
+    _compare("fp32", 4, 64, 16, 1e-4, forward_only=True)
+
+
+def test_forward_graph_matches_eager_bf16_c2():
+    _compare("bf16", 64, 128, 16, 1e-2, forward_only=True)

@@ -1,0 +1,24 @@
+# round 4: ring tests, host phase split, C2 / C4 benches, C4 kernel-trace breakdown, BLAS probe -> gpurun_out/$1
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/$1
+mkdir -p $OUT
+cd $R
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ring.py tests/test_gpu_capture.py -x -q --timeout 600 --timeout-method thread \
+    > $OUT/ring_tests.log 2>&1 || { tail -30 $OUT/ring_tests.log; exit 1; }
+tail -1 $OUT/ring_tests.log
+timeout -k 10 200 python -u tools/host_split.py --steps 20 > $OUT/host_split.txt 2>&1 || { tail -20 $OUT/host_split.txt; exit 1; }
+head -4 $OUT/host_split.txt
+timeout -k 10 200 python -u tools/host_time.py --steps 30 > $OUT/host_time.txt 2>&1 || exit 1
+tail -1 $OUT/host_time.txt
+for rep in 1 2; do
+  timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/c2.$rep.json 2>/dev/null || exit 1
+  timeout -k 10 200 python -u bench.py --model MetaConv --steps 10 --warmup 3 --no-cpu-baseline > $OUT/c4.$rep.json 2>/dev/null || exit 1
+done
+timeout -k 10 200 python -u tools/blas_probe2.py > $OUT/blas_probe2.txt 2>&1 || exit 1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c4 -o run -- \
+    python3 $R/bench.py --model MetaConv --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing > $OUT/prof_c4.log 2>&1 || exit 1
+python3 $R/tools/step_breakdown.py $OUT/prof_c4/run_kernel_trace.csv 45 > $OUT/prof_c4_breakdown.txt 2>&1
+rm -rf $OUT/prof_c4
+grep -o '"ms_per_step": [0-9.]*' $OUT/*.json
