@@ -197,9 +197,10 @@ class PackCache:
     """Derived copy of some parameters (packed / transposed / bf16 weights), rebuilt when
     they change.  prefetch_packs() builds the next step's copies on the side stream right
     after the optimizer step; get() then only orders the current stream after that build."""
-    __slots__ = ("key", "val", "pending", "params", "build", "ops", "__weakref__")
+    __slots__ = ("key", "val", "pending", "params", "build", "ops", "used", "__weakref__")
 
     def __init__(self):
+        self.used = True  # get() since the last prefetch (a forward-graph replay asks for none of its packs)
         self.key = None
         self.val = None
         self.pending = None
@@ -208,6 +209,7 @@ class PackCache:
         self.ops = None  # optional: val -> list of pack ops rebuilding val in place (batched prefetch)
 
     def get(self, params, build, ops=None):
+        self.used = True
         if ops is not None:
             self.ops = ops
         key = _pack_key(params)
@@ -302,6 +304,9 @@ def prefetch_packs() -> None:
             if c is None:
                 _PLAN.remove(ref)
                 continue
+            if not c.used:  # only built inside a captured forward graph, which rebuilds it itself
+                continue
+            c.used = False
             key = _pack_key(c.params)
             if key == c.key:
                 continue
