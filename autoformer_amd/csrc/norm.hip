@@ -438,6 +438,46 @@ __global__ void btranspose_kernel(const TS* src, float* dst, bf16* dst16, int R,
   }
 }
 
+// 64 x 64 tiles with 16-B loads (4 source columns) and 16-B fp32 / 8-B bf16 stores (4 output
+// columns = 4 source rows): interior tiles of sources with C % 4 == 0 and outputs with ld % 4 == 0
+// (16-B aligned bases); other tiles take the 32 x 32 element form above
+template <typename TS>
+__global__ void __launch_bounds__(256) btranspose64_kernel(const TS* src, float* dst, bf16* dst16, int R, int C,
+                                                           int ld, int acc) {
+  __shared__ float tile[64][65];
+  const long long off = (long long)blockIdx.z * R * C, doff = (long long)blockIdx.z * C * ld;
+  const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+  const int t = threadIdx.x, q = t & 15, rr = t >> 4;  // 16 quads per row, 16 rows per pass
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int r = r0 + rr + 16 * p, c = c0 + 4 * q;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (r < R && c < C) {
+      if constexpr (sizeof(TS) == 4) {
+        v = *reinterpret_cast<const f32x4*>(src + off + (long long)r * C + c);
+      } else {
+        const bf16x4 h = *reinterpret_cast<const bf16x4*>(src + off + (long long)r * C + c);
+        v = f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tile[rr + 16 * p][4 * q + k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int cl = rr + 16 * p, c = c0 + cl, r = r0 + 4 * q;  // output row c, columns r .. r+3
+    if (c >= C || r >= ld) continue;
+    f32x4 v = {tile[4 * q][cl], tile[4 * q + 1][cl], tile[4 * q + 2][cl], tile[4 * q + 3][cl]};
+    const long long o = doff + (long long)c * ld + r;
+    if (dst) {
+      if (acc) v += *reinterpret_cast<const f32x4*>(dst + o);
+      *reinterpret_cast<f32x4*>(dst + o) = v;
+    }
+    if (dst16) *reinterpret_cast<bf16x4*>(dst16 + o) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  }
+}
+
 }  // namespace
 
 #define GRID1(n) dim3(cdiv((n), 256)), dim3(256), 0, as_stream(stream)
@@ -569,6 +609,11 @@ extern "C" int avc_patchify(const float* src, float* dst, int B, int L, int C, i
 
 extern "C" int avc_transpose_batched(const float* src, float* dst, int B, int R, int C, int accumulate, void* stream) {
   AVC_CHECK_ARG(src && dst && src != dst, "avc_transpose_batched: bad args");
+  if (C % 4 == 0 && R % 4 == 0 && a16(src) && a16(dst)) {
+    dim3 g64(cdiv(C, 64), cdiv(R, 64), B);
+    btranspose64_kernel<float><<<g64, 256, 0, as_stream(stream)>>>(src, dst, nullptr, R, C, R, accumulate);
+    return avc_check_launch("avc_transpose_batched");
+  }
   dim3 g(cdiv(C, 32), cdiv(R, 32), B);
   btranspose_kernel<float><<<g, 256, 0, as_stream(stream)>>>(src, dst, nullptr, R, C, R, accumulate);
   return avc_check_launch("avc_transpose_batched");
@@ -579,6 +624,21 @@ extern "C" int avc_transpose_batched2(const void* src, int src_dtype, float* dst
   AVC_CHECK_ARG(src && (dst || dst16) && (const void*)src != (const void*)dst && ld >= R && (!accumulate || dst) &&
                     (src_dtype == AVC_F32 || src_dtype == AVC_BF16),
                 "avc_transpose_batched2: bad args");
+  // rows r in [R, ld) of the output are zero: the 64-row tiles read zeros past R, so ld % 4 == 0 keeps
+  // every 4-column output group inside one tile and the vector path applies
+  const bool v64 = C % 4 == 0 && ld % 4 == 0 && a16(src) && a16(dst) && a8(dst16);
+  if (v64) {
+    dim3 g64(cdiv(C, 64), cdiv(ld, 64), B);
+    if (src_dtype == AVC_BF16)
+      btranspose64_kernel<bf16><<<g64, 256, 0, as_stream(stream)>>>(static_cast<const bf16*>(src), dst,
+                                                                    reinterpret_cast<bf16*>(dst16), R, C, ld,
+                                                                    accumulate);
+    else
+      btranspose64_kernel<float><<<g64, 256, 0, as_stream(stream)>>>(static_cast<const float*>(src), dst,
+                                                                     reinterpret_cast<bf16*>(dst16), R, C, ld,
+                                                                     accumulate);
+    return avc_check_launch("avc_transpose_batched2");
+  }
   dim3 g(cdiv(C, 32), cdiv(ld, 32), B);
   if (src_dtype == AVC_BF16)
     btranspose_kernel<bf16><<<g, 256, 0, as_stream(stream)>>>(static_cast<const bf16*>(src), dst,
