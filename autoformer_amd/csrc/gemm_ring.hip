@@ -614,6 +614,196 @@ __global__ void __launch_bounds__(RNT, 2) gemm_ring_kernel(GemmArgs g, int gm) {
   ring_epilogue<BM_, BN_>(g, acc, m0, n0, bz, ks, smem_raw);
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same tile with 32-deep K slots of 64-B rows (K32): a slot of the 256 x 256 tile is 32 KB, so
+// four slots fit the LDS of the two-slot 64-deep form and THREE K-steps of fills are in flight
+// during a step's MFMAs instead of one (the K loop is bound by LDS-DMA latency: fills in flight /
+// latency = the per-CU operand rate, MI355X_MICROARCH.md "ldsdma-fill").  Row chunk swizzle:
+// logical 16-B chunk c of row r is stored at c ^ ((r >> 2) & 3), so the 16 rows of a fragment read
+// spread over all four chunk positions (64-B rows repeat the bank pattern every 4 rows).
+constexpr int R32 = 64;  // bytes per LDS row (32 bf16 of K)
+
+// R rows x 32 K per slot: R/128 glds per thread.  Instruction i of wave w covers slot rows
+// (8i + w)*16 .. +16; lane L writes row +(L>>2), 16-B position L&3, which holds global K chunk
+// (L&3) ^ ((L>>4)&3) for every i and w (the row's (r >> 2) & 3).
+template <int R, bool WIN>
+struct RingLoader32 {
+  static constexpr int NI = R / 128;
+  const bf16* base;
+  long long roff[NI];
+  int tt[NI];
+  bool rok[NI];
+  int kc;
+  int ld, pad, t_in, chans;
+
+  __device__ __forceinline__ void init(const OpDev& o, int row0, int bz) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    base = reinterpret_cast<const bf16*>(o.ptr) + (long long)bz * o.bstride;
+    kc = 8 * ((lane & 3) ^ ((lane >> 4) & 3));
+    ld = (int)o.ld;
+    pad = o.pad;
+    t_in = o.t_in;
+    chans = o.chans;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int r = row0 + (8 * i + w) * 16 + (lane >> 2);
+      rok[i] = r < o.rows;
+      const int rr = rok[i] ? r : 0;
+      if (WIN) {
+        const int b = (int)fdiv((uint32_t)rr, o.tdiv);
+        tt[i] = rr - b * o.t_out;
+        roff[i] = (long long)(b * o.t_in + tt[i]) * o.ld;
+      } else {
+        tt[i] = 0;
+        roff[i] = (long long)rr * o.ld;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void issue(char* lds, int kbase, int kend, const FastDiv& cdv) {
+    const int w = threadIdx.x >> 6;
+    const int k = kbase + kc;
+    const bool kok = k < kend;
+    int tap = 0, cc = k;
+    if (WIN) {
+      tap = (int)fdiv((uint32_t)k, cdv);
+      cc = k - tap * chans;
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      bool ok = kok && rok[i];
+      long long off;
+      if (WIN) {
+        const int t2 = tt[i] + tap - pad;
+        ok = ok && t2 >= 0 && t2 < t_in;
+        off = roff[i] + (long long)(tap - pad) * ld + cc;
+      } else {
+        off = roff[i] + k;
+      }
+      glds16(ok ? (const void*)(base + off) : (const void*)g_zero16_rg, lds + (8 * i + w) * 16 * R32);
+    }
+  }
+};
+
+template <int BM_, int BN_, int NST, bool WIN>
+__global__ void __launch_bounds__(RNT, 2) gemm_ring32_kernel(GemmArgs g, int gm) {
+  constexpr int TWM = BM_ / 2, TWN = BN_ / 4, MI = TWM / 16, NJ = TWN / 16;
+  constexpr int A_BYTES = BM_ * R32, STAGE = (BM_ + BN_) * R32;
+  constexpr int LPT = BM_ / 128 + BN_ / 128;  // glds per thread per K-step
+  constexpr int P = NST - 1;                  // K-steps in flight
+  constexpr int KS = 32;
+  static_assert(NST >= 2 && NST <= 6 && BM_ % 128 == 0 && BN_ % 128 == 0, "ring32 shape");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int nN = (g.N + BN_ - 1) / BN_, nM = (g.M + BM_ - 1) / BM_;
+  const int z = lid / (nN * nM);
+  const int rem = lid - z * nN * nM;
+  const int grp = rem / (gm * nN);
+  const int fm = grp * gm;
+  const int gsz = min(nM - fm, gm);
+  const int wi = rem - grp * gm * nN;
+  const int mt = fm + wi % gsz, nt = wi / gsz;
+  const int m0 = mt * BM_, n0 = nt * BN_;
+  const int bz = z / g.split_k, ks = z - bz * g.split_k;
+  const int kbeg = ks * g.klen;
+  const int kend = min(g.K, kbeg + g.klen);
+  const int nkt = kend > kbeg ? (kend - kbeg + KS - 1) / KS : 0;
+
+  RingLoader32<BM_, WIN> la;
+  RingLoader32<BN_, false> lb;
+  la.init(g.a, m0, bz);
+  lb.init(g.b, n0, bz);
+  const FastDiv cdv = g.a.cdv;
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment reads: row (lane&15) of each 16-row block, logical chunk lane>>4 stored at
+  // (lane>>4) ^ ((row>>2)&3) (block bases are multiples of 16 rows)
+  const int frow = lane & 15;
+  const int chk = ((lane >> 4) ^ ((frow >> 2) & 3)) << 4;
+  const int aoff = (wm * TWM + frow) * R32 + chk, boff = A_BYTES + (wn * TWN + frow) * R32 + chk;
+
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+    if (p < nkt) {
+      char* st = smem_raw + p * STAGE;
+      la.issue(st, kbeg + p * KS, kend, cdv);
+      lb.issue(st + A_BYTES, kbeg + p * KS, kend, cdv);
+    }
+
+  constexpr int MH = MI / 2;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int ahead = min(P - 1, nkt - 1 - kt);  // K-steps allowed to stay in flight
+    if constexpr (P >= 5) {
+      if (ahead >= 4) wait_vm<4 * LPT>();
+      else if (ahead == 3) wait_vm<3 * LPT>();
+      else if (ahead == 2) wait_vm<2 * LPT>();
+      else if (ahead == 1) wait_vm<LPT>();
+      else wait_vm<0>();
+    } else if constexpr (P >= 3) {
+      if (ahead >= 2) wait_vm<2 * LPT>();
+      else if (ahead == 1) wait_vm<LPT>();
+      else wait_vm<0>();
+    } else if constexpr (P == 2) {
+      if (ahead >= 1) wait_vm<LPT>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    raw_barrier();
+    if (kt + P < nkt) {
+      char* st = smem_raw + ((kt + P) % NST) * STAGE;
+      la.issue(st, kbeg + (kt + P) * KS, kend, cdv);
+      lb.issue(st + A_BYTES, kbeg + (kt + P) * KS, kend, cdv);
+    }
+    // one 32-deep K-step: read B and the first half of A, MFMAs on it while the second half of A
+    // is read (inline-asm reads, counted lgkmcnt waits)
+    const unsigned st = lds_addr(smem_raw + (kt % NST) * STAGE);
+    const unsigned a0 = st + aoff, b0 = st + boff;
+    bf16x8 af[MI], bfr[NJ];
+    ds_read_n<NJ, 16 * R32>(bfr, b0);
+    ds_read_n<MH, 16 * R32>(af, a0);
+    ds_read_n<MH, 16 * R32, MH * 16 * R32>(af + MH, a0);
+    wait_lgkm<MH>();
+#pragma unroll
+    for (int i = 0; i < MH; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    wait_lgkm<0>();
+#pragma unroll
+    for (int i = MH; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+  __syncthreads();
+  ring_epilogue<BM_, BN_>(g, acc, m0, n0, bz, ks, smem_raw);
+}
+
+template <int BM_, int BN_, int NST, bool WIN>
+void launch32(const GemmArgs& g, int gm, hipStream_t s) {
+  const size_t lds = std::max((size_t)NST * (BM_ + BN_) * R32, ring_epi_lds<BM_, BN_>());
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ring32_kernel<BM_, BN_, NST, WIN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const int nb = ((g.M + BM_ - 1) / BM_) * ((g.N + BN_ - 1) / BN_) * g.batch * g.split_k;
+  gemm_ring32_kernel<BM_, BN_, NST, WIN><<<nb, RNT, lds, s>>>(g, gm);
+}
+
 template <int BM_, int BN_, int NST, bool WIN>
 void launch(const GemmArgs& g, int gm, hipStream_t s) {
   const size_t lds = std::max((size_t)NST * (BM_ + BN_) * RROW, ring_epi_lds<BM_, BN_>());
@@ -945,6 +1135,15 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
   RING_CASE(256, 256, 2) RING_CASE(256, 128, 3) RING_CASE(128, 128, 4) RING_CASE(128, 128, 3)
   RING_CASE(128, 256, 3) RING_CASE(256, 128, 2)
 #undef RING_CASE
+  // 32-deep slots (nst = 10 + stages in the forced form)
+#define RING32_CASE(BMV, BNV, NSV)                        \
+  if (bm == BMV && bn == BNV && nst == 10 + NSV) {        \
+    if (win) launch32<BMV, BNV, NSV, true>(g, c.gm, s);   \
+    else launch32<BMV, BNV, NSV, false>(g, c.gm, s);      \
+    return true;                                          \
+  }
+  RING32_CASE(256, 256, 4) RING32_CASE(256, 128, 5) RING32_CASE(128, 128, 6)
+#undef RING32_CASE
   return false;
 }
 

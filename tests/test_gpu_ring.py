@@ -36,7 +36,8 @@ def _rel(a, b):
     return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
 
 
-CFGS = [(256, 256, 2), (256, 128, 3), (128, 128, 4), (128, 128, 3), (128, 256, 3), (256, 128, 2)]
+CFGS = [(256, 256, 2), (256, 128, 3), (128, 128, 4), (128, 128, 3), (128, 256, 3), (256, 128, 2),
+        (256, 256, 14), (256, 128, 15), (128, 128, 16)]  # nst 10 + n: 32-deep slots (gemm_ring32_kernel)
 
 
 @pytest.mark.parametrize("cfg", CFGS)
