@@ -148,6 +148,119 @@ __global__ void __launch_bounds__(1024) pair_final_kernel(const float* ws, int n
   }
 }
 
+// Multi-block per-sample reductions (S % 4 == 0, 16-B aligned): a sample is split over NS blocks
+// (B x NS ~ 1024 blocks instead of B = 64 blocks of one sample each), each writing a partial that a
+// one-block finalize merges.  Statistics: (count, sum, M2 about the chunk mean), merged by Chan's
+// formula; backward: the chunk sums of g = dy * gamma and g * xhat.
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  v = warp_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void __launch_bounds__(256) gn_stats_part_kernel(const float* x, long long S, int chunk, float* part) {
+  __shared__ float red[4];
+  const int b = blockIdx.y, k = blockIdx.x;
+  const long long c0 = (long long)k * chunk, c1 = min(S, c0 + chunk);
+  const f32x4* xs = reinterpret_cast<const f32x4*>(x + (long long)b * S);
+  float s = 0.f;
+  for (long long i = c0 / 4 + threadIdx.x; i < c1 / 4; i += 256) {
+    const f32x4 v = xs[i];
+    s += v[0] + v[1] + v[2] + v[3];
+  }
+  const float n = (float)(c1 > c0 ? c1 - c0 : 0);
+  const float sum = block_sum256(s, red);
+  const float mu = n > 0.f ? sum / n : 0.f;
+  float q = 0.f;
+  for (long long i = c0 / 4 + threadIdx.x; i < c1 / 4; i += 256) {
+    const f32x4 d = xs[i] - mu;
+    q += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+  }
+  const float m2 = block_sum256(q, red);
+  if (threadIdx.x == 0) {
+    float* p = part + ((long long)b * gridDim.x + k) * 3;
+    p[0] = n;
+    p[1] = sum;
+    p[2] = m2;
+  }
+}
+
+__global__ void gn_stats_final_kernel(const float* part, int B, int NS, long long S, float eps, float* mean,
+                                      float* rstd) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* p = part + (long long)b * NS * 3;
+  double tot = 0.0;
+  for (int k = 0; k < NS; ++k) tot += p[3 * k + 1];
+  const double mu = tot / (double)S;
+  double m2 = 0.0;
+  for (int k = 0; k < NS; ++k) {
+    const double n = p[3 * k];
+    if (n > 0.0) {
+      const double d = p[3 * k + 1] / n - mu;
+      m2 += p[3 * k + 2] + n * d * d;
+    }
+  }
+  mean[b] = (float)mu;
+  rstd[b] = (float)(1.0 / sqrt(m2 / (double)S + (double)eps));
+}
+
+__global__ void __launch_bounds__(256) gn_bwd_sample_part_kernel(const float* dy, const float* x, const float* gamma,
+                                                                 const float* mean, const float* rstd, long long S,
+                                                                 int C, int chunk, float* part) {
+  __shared__ float red[4];
+  const int b = blockIdx.y, k = blockIdx.x;
+  const long long c0 = (long long)k * chunk, c1 = min(S, c0 + chunk);
+  const long long o = (long long)b * S;
+  const float mu = mean[b], rs = rstd[b];
+  float s0 = 0.f, s1 = 0.f;
+  for (long long i4 = c0 / 4 + threadIdx.x; i4 < c1 / 4; i4 += 256) {
+    const long long i = 4 * i4;
+    const int c = (int)(i % C);
+    f32x4 g = *reinterpret_cast<const f32x4*>(dy + o + i);
+    if (gamma) g *= *reinterpret_cast<const f32x4*>(gamma + c);
+    const f32x4 xh = (*reinterpret_cast<const f32x4*>(x + o + i) - mu) * rs;
+    s0 += g[0] + g[1] + g[2] + g[3];
+    s1 += g[0] * xh[0] + g[1] * xh[1] + g[2] * xh[2] + g[3] * xh[3];
+  }
+  const float t0 = block_sum256(s0, red);
+  const float t1 = block_sum256(s1, red);
+  if (threadIdx.x == 0) {
+    float* p = part + ((long long)b * gridDim.x + k) * 2;
+    p[0] = t0;
+    p[1] = t1;
+  }
+}
+
+__global__ void gn_bwd_sample_final_kernel(const float* part, int B, int NS, long long S, float* ws) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float t0 = 0.f, t1 = 0.f;
+  for (int k = 0; k < NS; ++k) {
+    t0 += part[((long long)b * NS + k) * 2];
+    t1 += part[((long long)b * NS + k) * 2 + 1];
+  }
+  ws[2 * b] = t0 / (float)S;
+  ws[2 * b + 1] = t1 / (float)S;
+}
+
+__global__ void gn_bwd_dx_v_kernel(const float* dy, const float* x, const float* gamma, const float* mean,
+                                   const float* rstd, const float* ws, long long S, int C, float* dx,
+                                   long long total4) {
+  const long long i4 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i4 >= total4) return;
+  const long long i = 4 * i4;
+  const int b = (int)(i / S), c = (int)(i % C);
+  const float rs = rstd[b];
+  f32x4 g = *reinterpret_cast<const f32x4*>(dy + i);
+  if (gamma) g *= *reinterpret_cast<const f32x4*>(gamma + c);
+  const f32x4 xh = (*reinterpret_cast<const f32x4*>(x + i) - mean[b]) * rs;
+  *reinterpret_cast<f32x4*>(dx + i) = rs * (g - ws[2 * b] - xh * ws[2 * b + 1]);
+}
+
 // ---------------------------------------------------------------- LayerNorm over rows of D
 // one wave per row
 __global__ void ln_fwd_kernel(const float* x, int R, int D, const float* gamma, const float* beta, float eps, float* y,
@@ -488,11 +601,29 @@ static bool a8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0
 
 extern "C" size_t avc_norm_ws(int rows, int C) { return (size_t)cdiv(rows, 64) * C * 2 + 1024; }
 
+// samples split into NS chunks of >= 4096 elements, ~1024 blocks in all
+static int gn_splits(int B, long long S) {
+  long long ns = 1024 / B;
+  if (ns < 1) ns = 1;
+  const long long cap = S / 4096;
+  if (ns > cap) ns = cap > 0 ? cap : 1;
+  return (int)ns;
+}
+
 extern "C" int avc_group_norm_fwd2(const float* x, int B, long long S, int C, const float* gamma, const float* beta,
-                                   float eps, float* y, void* y16, float* mean, float* rstd, void* stream) {
+                                   float eps, float* y, void* y16, float* mean, float* rstd, float* ws,
+                                   void* stream) {
   AVC_CHECK_ARG(x && (y || y16) && mean && rstd && B > 0 && S > 0 && C > 0 && S % C == 0,
                 "avc_group_norm_fwd: bad args");
-  gn_stats_kernel<<<B, 1024, 0, as_stream(stream)>>>(x, S, eps, mean, rstd);
+  hipStream_t s = as_stream(stream);
+  const int ns = gn_splits(B, S);
+  if (ws && S % 4 == 0 && a16(x) && ns > 1) {
+    const int chunk = (int)(((S + ns - 1) / ns + 3) / 4 * 4);
+    gn_stats_part_kernel<<<dim3(ns, B), 256, 0, s>>>(x, S, chunk, ws);
+    gn_stats_final_kernel<<<cdiv(B, 64), 64, 0, s>>>(ws, B, ns, S, eps, mean, rstd);
+  } else {
+    gn_stats_kernel<<<B, 1024, 0, s>>>(x, S, eps, mean, rstd);
+  }
   const long long total = (long long)B * S;
   bf16* o16 = static_cast<bf16*>(y16);
   if (C % 4 == 0 && a16(x) && a16(y) && a8(o16) && a16(gamma) && a16(beta)) {
@@ -506,7 +637,7 @@ extern "C" int avc_group_norm_fwd2(const float* x, int B, long long S, int C, co
 
 extern "C" int avc_group_norm_fwd(const float* x, int B, long long S, int C, const float* gamma, const float* beta,
                                   float eps, float* y, float* mean, float* rstd, void* stream) {
-  return avc_group_norm_fwd2(x, B, S, C, gamma, beta, eps, y, nullptr, mean, rstd, stream);
+  return avc_group_norm_fwd2(x, B, S, C, gamma, beta, eps, y, nullptr, mean, rstd, nullptr, stream);
 }
 
 extern "C" int avc_group_norm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
@@ -517,9 +648,18 @@ extern "C" int avc_group_norm_bwd(const float* dy, const float* x, const float* 
   const int L = (int)(S / C), M = B * L;
   const int nrb = cdiv(M, 128);
   float* wsamp = ws + (size_t)nrb * C * 2;
-  gn_bwd_sample_kernel<<<B, 1024, 0, s>>>(dy, x, gamma, mean, rstd, S, C, wsamp);
   const long long total = (long long)B * S;
-  gn_bwd_dx_kernel<<<cdiv(total, 256), 256, 0, s>>>(dy, x, gamma, mean, rstd, wsamp, S, C, dx, total);
+  const int ns = gn_splits(B, S);
+  if (C % 4 == 0 && a16(dy) && a16(x) && a16(dx) && a16(gamma)) {
+    float* part = wsamp + 2 * B;  // avc_norm_ws leaves room: nrb*C*2 + 2B + 2*B*ns << rows/64*C*2
+    const int chunk = (int)(((S + ns - 1) / ns + 3) / 4 * 4);
+    gn_bwd_sample_part_kernel<<<dim3(ns, B), 256, 0, s>>>(dy, x, gamma, mean, rstd, S, C, chunk, part);
+    gn_bwd_sample_final_kernel<<<cdiv(B, 64), 64, 0, s>>>(part, B, ns, S, wsamp);
+    gn_bwd_dx_v_kernel<<<cdiv(total / 4, 256), 256, 0, s>>>(dy, x, gamma, mean, rstd, wsamp, S, C, dx, total / 4);
+  } else {
+    gn_bwd_sample_kernel<<<B, 1024, 0, s>>>(dy, x, gamma, mean, rstd, S, C, wsamp);
+    gn_bwd_dx_kernel<<<cdiv(total, 256), 256, 0, s>>>(dy, x, gamma, mean, rstd, wsamp, S, C, dx, total);
+  }
   if (dgamma || dbeta) {
     gn_bwd_param_kernel<<<dim3(cdiv(C, 64), nrb), 256, 0, s>>>(dy, x, mean, rstd, L, M, C, ws);
     pair_final_kernel<<<cdiv(C, 64), 1024, 0, s>>>(ws, nrb, C, dgamma, dbeta, accumulate);

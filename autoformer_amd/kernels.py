@@ -698,7 +698,7 @@ def group_norm_fwd(x, B, C, gamma, beta, eps, twin=False):
     y16 = _twin_buf(y, None) if twin else None
     mean, rstd = torch.empty(B, device=x.device), torch.empty(B, device=x.device)
     L.call("avc_group_norm_fwd2", x.data_ptr(), B, S, C, _ptr(gamma), _ptr(beta), float(eps), y.data_ptr(), _ptr(y16),
-           mean.data_ptr(), rstd.data_ptr(), stream())
+           mean.data_ptr(), rstd.data_ptr(), _ws(x.numel() // C, C, x.device).data_ptr(), stream())
     return (attach_twin(y, y16) if y16 is not None else y), mean, rstd
 
 

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 21
+#define AVC_ABI_VERSION 22
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -404,9 +404,11 @@ int avc_layer_norm_bwd(const float* dy, const float* x, const float* gamma, cons
  * only ever read in bf16), and for the LayerNorm backward dres (nullable): dx = dres + the norm's gradient -- the
  * residual add after the norm (MLPMixer.py:80-86) folded into the pass, and row_sum (nullable): each row's sum of dx
  * (the token-mixing bias gradient of the transposed layout, summed per patch).  The bf16 / dres forms need C (D) % 4 == 0,
- * D <= 512 and 16-B aligned rows; the LayerNorm backward then computes dx and the parameter sums in ONE pass. */
+ * D <= 512 and 16-B aligned rows; the LayerNorm backward then computes dx and the parameter sums in ONE pass.
+ * avc_group_norm_fwd2's ws (nullable, >= avc_norm_ws(rows, C) floats) lets the per-sample statistics be split over
+ * ~1024 blocks (partials merged by Chan's formula) instead of one block per sample. */
 int avc_group_norm_fwd2(const float* x, int B, long long S, int C, const float* gamma, const float* beta, float eps,
-                        float* y, void* y16, float* mean, float* rstd, void* stream);
+                        float* y, void* y16, float* mean, float* rstd, float* ws, void* stream);
 int avc_layer_norm_fwd2(const float* x, int R, int D, const float* gamma, const float* beta, float eps, float* y,
                         void* y16, float* mean, float* rstd, void* stream);
 int avc_layer_norm_bwd2(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
