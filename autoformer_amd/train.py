@@ -351,6 +351,13 @@ class TrainStep:
         elif self.graph_f is not None:
             # the captured forward replays into its static activations; the eager backward walks
             # the autograd graph recorded at capture (retained) over those same tensors
+            # the forward reads the capture-time inputs: a new batch is copied into them through
+            # .data (the retained autograd graph saved them; a tracked in-place copy would bump their
+            # version and the backward would refuse them)
+            if x is not self._gx:
+                self._gx.data.copy_(x)
+            if emb is not self._ge:
+                self._ge.data.copy_(emb)
             self.gflat.zero_()
             self.graph_f.replay()
             self.loss.backward(retain_graph=True)
@@ -399,6 +406,7 @@ class TrainStep:
                 self.model._decoder_bwd_done = None
             self.loss = loss
             self.graph_f = g
+            self._gx, self._ge = x, emb
             return
         with torch.cuda.graph(g):
             self.loss = self._fwd_bwd(x, emb)
