@@ -359,6 +359,11 @@ class TrainStep:
             if emb is not self._ge:
                 self._ge.data.copy_(emb)
             self.gflat.zero_()
+            # the replay does not ask PackCache.get for its packs (it rebuilds its own), so it would
+            # not wait for the previous step's side-stream prefetch: order it explicitly
+            side = side_stream()
+            if side is not None:
+                stream_wait(K.stream(), ev_record(side.cuda_stream))
             self.graph_f.replay()
             self.loss.backward(retain_graph=True)
             join_side()
