@@ -1,0 +1,6 @@
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/$1
+mkdir -p $OUT
+cd $R
+timeout -k 10 300 python -u tools/graph_fwd_probe.py > $OUT/probe.txt 2>&1; tail -8 $OUT/probe.txt
