@@ -40,11 +40,16 @@ def run(variant):
             if variant >= 3:
                 TR.prefetch_packs()
             torch.cuda.synchronize()
-        print(f"variant {variant}: losses {out}", flush=True)
+        fault = ""
+        try:
+            ts.check()
+        except Exception as ex:  # noqa: BLE001
+            fault = f" FAULT {type(ex).__name__}: {ex}"
+        print(f"variant {variant}: losses {out}{fault}", flush=True)
     finally:
         set_grad_sink(False)
 
 
 if __name__ == "__main__":
-    for v in (0, 1, 2, 3):
+    for v in (map(int, sys.argv[1].split(",")) if len(sys.argv) > 1 else (0, 1, 2, 3)):
         run(v)
