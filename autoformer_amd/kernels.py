@@ -415,7 +415,10 @@ def lstm2_fwd(xproj0, w_hh0, w_ih1, w_hh1, bias1, B, T, H):
     for _ in range(2):
         outs += [torch.empty(B * T, H, device=dev), torch.empty(B * T, H, device=dev, dtype=torch.bfloat16),
                  torch.empty(B * T, H, device=dev), torch.empty(B * T, 4 * H, device=dev)]
-    buf = torch.empty(int(L.lib().avc_lstm2_scratch_bytes(int(B), int(H))), device=dev, dtype=torch.uint8)
+    # zeroed by a fill KERNEL on this stream as well as by the library's memset of the flag words:
+    # replayed inside a hipGraph after eager work, the memset node alone left stale flags visible
+    # to the wavefront (second replay read the previous replay's payload; tools/graph_fwd_probe.py)
+    buf = torch.zeros(int(L.lib().avc_lstm2_scratch_bytes(int(B), int(H))), device=dev, dtype=torch.uint8)
     L.call("avc_lstm2_fwd", xproj0.data_ptr(), w_hh0.data_ptr(), w_ih1.data_ptr(), w_hh1.data_ptr(),
            bias1.data_ptr(), B, T, H, *[o.data_ptr() for o in outs], buf.data_ptr(), stream())
     h0, h0b, c0, g0, h1, h1b, c1, g1 = outs
