@@ -22,6 +22,11 @@ void avc_set_error(const char* fmt, ...);
     }                                     \
   } while (0)
 int avc_check_launch(const char* what);
+// Zero `bytes` (a multiple of 4) at p with a KERNEL on stream s.  Used instead of hipMemsetAsync for
+// everything a later kernel of the same stream depends on: replayed inside a hipGraph after eager
+// work, a captured memset node was not reliably complete / visible when the next kernel node ran
+// (the persistent recurrences then read the previous replay's flags; tools/graph_fwd_probe.py).
+int avc_zero_async(void* p, size_t bytes, hipStream_t s);
 
 // ------------------------------------------------------------------ conversions
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }

@@ -514,9 +514,20 @@ extern "C" int avc_add(const float* a, const float* b, float* o, long long n, vo
   return avc_check_launch("avc_add");
 }
 
+__global__ void zero_words_kernel(unsigned* p, long long n) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) p[i] = 0u;
+}
+
+int avc_zero_async(void* p, size_t bytes, hipStream_t s) {
+  const long long n = (long long)(bytes / 4);
+  if (n == 0) return 0;
+  zero_words_kernel<<<(int)std::min<long long>(1024, cdiv(n, 256)), 256, 0, s>>>(static_cast<unsigned*>(p), n);
+  return avc_check_launch("avc_zero_async");
+}
+
 static int loss_launch(const float* a, const float* b, long long n, float* out, int mode, void* stream) {
   AVC_CHECK_ARG(a && b && out && n > 0, "avc loss: bad args");
-  (void)hipMemsetAsync(out, 0, sizeof(float), as_stream(stream));
+  if (avc_zero_async(out, sizeof(float), as_stream(stream))) return -1;
   // 256 blocks: enough loads in flight for the 655 K mel values, and 256 same-word atomicAdds
   // (≈12 ns each at the L2) instead of 1024
   int grid = (int)std::min<long long>(256, cdiv(n, 1024));
@@ -603,7 +614,7 @@ extern "C" int avc_act_bwd(const float* g, const float* yout, float* dx, long lo
 
 extern "C" int avc_bce_loss(const float* p, long long n, float target, float* out, void* stream) {
   AVC_CHECK_ARG(p && out && n > 0, "avc_bce_loss: bad args");
-  (void)hipMemsetAsync(out, 0, sizeof(float), as_stream(stream));
+  if (avc_zero_async(out, sizeof(float), as_stream(stream))) return -1;
   bce_kernel<<<(int)std::min<long long>(1024, cdiv(n, 256)), 256, 0, as_stream(stream)>>>(p, n, target, out);
   return avc_check_launch("avc_bce_loss");
 }

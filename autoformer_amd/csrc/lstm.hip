@@ -1726,7 +1726,7 @@ extern "C" int avc_lstm2_fwd(const float* xproj0, const void* w_hh0, const void*
   p.B = B;
   p.T = T;
   p.ng = ng;
-  (void)hipMemsetAsync(buf, 0, px_ctl_bytes(ng), s);
+  if (avc_zero_async(buf, px_ctl_bytes(ng), s)) return -1;
   // scheduling fence every 2 k-blocks of the product (without one the compiler hoists the A
   // fragment reads and spills weight fragments).  AVC_LSTM2_CFG = LB*10 + OS (A/B): payload loads
   // in LB batches (1 or 2); OS = 1 stores the previous tick's outputs under the payload loads
@@ -1807,7 +1807,7 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
     p.ng = ng;
     const bool gr = gran(false, H);
     // flag form: only ctl + flags are polled; granule form: every tag of the payload too
-    (void)hipMemsetAsync(hbuf, 0, gr ? px_payload_off(ng) + (size_t)8 * B * H : px_ctl_bytes(ng), s);
+    if (avc_zero_async(hbuf, gr ? px_payload_off(ng) + (size_t)8 * B * H : px_ctl_bytes(ng), s)) return -1;
     const dim3 grid(ng * (H / PJU));
     if (H == 1024) gr ? lstm_persist_fwd<1024, true><<<grid, PNT, 0, s>>>(p) : lstm_persist_fwd<1024, false><<<grid, PNT, 0, s>>>(p);
     else if (H == 768) gr ? lstm_persist_fwd<768, true><<<grid, PNT, 0, s>>>(p) : lstm_persist_fwd<768, false><<<grid, PNT, 0, s>>>(p);  // Adjust.py:30
@@ -1880,7 +1880,7 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
     static const int abl = getenv("AVC_LSTM_BWD_ABL") ? atoi(getenv("AVC_LSTM_BWD_ABL")) : 0;
     p.abl = abl;
     const bool gr = gran(true, H);
-    (void)hipMemsetAsync(gbuf, 0, gr ? px_payload_off(ng) + (size_t)32 * B * H : px_ctl_bytes(ng), s);
+    if (avc_zero_async(gbuf, gr ? px_payload_off(ng) + (size_t)32 * B * H : px_ctl_bytes(ng), s)) return -1;
     // (persistent_path above set the dynamic-LDS attributes)
     const dim3 grid(ng * (H / PJU));
     if (H == 1024) launch_persist_bwd<1024>(grid, s, gr, p);
