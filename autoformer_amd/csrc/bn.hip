@@ -399,7 +399,7 @@ __global__ void bn_bwd_apply1_kernel(const TD* __restrict__ dA, const float* __r
 
 // column sums: partial per strip of rpb rows (a multiple of 64; vectorised like bn_bwd_reduce when
 // N % 4 == 0 and ld % 4 == 0, scalar otherwise), then a parallel finalize over the strips.  The
-// strips are sized for ~2048 partial blocks, so the finalize reads at most a few hundred rows
+// strips are sized for ~1024 partial blocks, so the finalize reads at most a few hundred rows
 // (64-row strips had left it a serial 1849-row loop per column on the mixer's 118336-row sums).
 template <bool V4>
 __global__ void __launch_bounds__(256) colsum_partial_kernel(const float* __restrict__ x, long long ld, int M, int N,
@@ -665,8 +665,8 @@ extern "C" int avc_colsum(const float* x, long long ld, int M, int N, float* out
                           float* ws, void* stream) {
   AVC_CHECK_ARG(x && out && ws && ld >= N, "avc_colsum: bad args");
   hipStream_t s = as_stream(stream);
-  // row strips of rpb rows: ~2048 partial blocks in all (nrb <= cdiv(M, RB), the workspace bound)
-  const int ncb = cdiv(N, 64), target = 2048 / ncb > 1 ? 2048 / ncb : 1;
+  // row strips of rpb rows: ~1024 partial blocks in all (nrb <= cdiv(M, RB), the workspace bound)
+  const int ncb = cdiv(N, 64), target = 1024 / ncb > 1 ? 1024 / ncb : 1;
   const int rpb = M > 0 ? RB * cdiv(cdiv(M, RB), target) : RB, nrb = cdiv(M, rpb);
   if (N % 4 == 0 && ld % 4 == 0 && aligned16(x))
     colsum_partial_kernel<true><<<dim3(ncb, nrb), 256, 0, s>>>(x, ld, M, N, rpb, ws);

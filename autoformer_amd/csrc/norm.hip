@@ -6,6 +6,8 @@
 // Rearrange('b c (h p1) (w p2) -> b (h w) (p1 p2 c)') (MLPMixer.py:73-75).
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int NT = 256;
@@ -370,17 +372,17 @@ __global__ void __launch_bounds__(256) ln_fwd_v_kernel(const float* x, int R, in
   }
 }
 
-// LayerNorm backward, dx and the parameter partials in one pass: 16 waves x LRB rows per block,
+// LayerNorm backward, dx and the parameter partials in one pass: 16 waves x lrb rows per block,
 // each wave one row at a time (dy and x rows in registers); dx = rs (g - mean g - xh mean(g xh))
 // (+ dres, the residual branch's gradient: the add after the norm folded in) to fp32 and / or
 // bf16; per-lane column partials of dy*xh and dy summed over the block's rows, reduced through
 // LDS into one (a, b) partial row per block for pair_final_kernel.
-constexpr int LRB = 64;
+constexpr int LRB = 64;  // minimum rows per block (lrb grows with R so that pair_final sums <= ~512 rows)
 template <int NV>
 __global__ void __launch_bounds__(1024) ln_bwd_v_kernel(const float* dy, const float* x, const float* gamma,
                                                         const float* mean, const float* rstd, int R, int D,
                                                         const float* dres, float* dx, bf16* dx16, float* ws,
-                                                        float* rsum) {
+                                                        float* rsum, int lrb) {
   __shared__ f32x4 red[2][16][64 * NV];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, D4 = D >> 2;
   f32x4 pa[NV], pb[NV], gm[NV];
@@ -390,8 +392,8 @@ __global__ void __launch_bounds__(1024) ln_bwd_v_kernel(const float* dy, const f
     const int c4 = l + 64 * i;
     gm[i] = (gamma && c4 < D4) ? reinterpret_cast<const f32x4*>(gamma)[c4] : f32x4{1.f, 1.f, 1.f, 1.f};
   }
-  const int r1 = min(R, (int)blockIdx.x * LRB + LRB);
-  for (int row = blockIdx.x * LRB + w; row < r1; row += 16) {
+  const int r1 = min(R, (int)blockIdx.x * lrb + lrb);
+  for (int row = blockIdx.x * lrb + w; row < r1; row += 16) {
     const long long o = (long long)row * D;
     const float mu = mean[row], rs = rstd[row];
     f32x4 dv[NV], xh[NV];
@@ -697,13 +699,14 @@ extern "C" int avc_layer_norm_bwd2(const float* dy, const float* x, const float*
   const bool v = D % 4 == 0 && D <= 512 && a16(dy) && a16(x) && a16(dx) && a8(o16) && a16(gamma) && a16(dres);
   if (v) {
     const bool par = dgamma || dbeta;
-    const int nrb = cdiv(R, LRB);
+    // enough blocks for the chip, few enough partial rows for one pair_final pass
+    const int lrb = std::max(LRB, (cdiv(R, 512) + 15) / 16 * 16), nrb = cdiv(R, lrb);
     if (D <= 256)
       ln_bwd_v_kernel<1><<<nrb, 1024, 0, s>>>(dy, x, gamma, mean, rstd, R, D, dres, dx, o16, par ? ws : nullptr,
-                                              row_sum);
+                                              row_sum, lrb);
     else
       ln_bwd_v_kernel<2><<<nrb, 1024, 0, s>>>(dy, x, gamma, mean, rstd, R, D, dres, dx, o16, par ? ws : nullptr,
-                                              row_sum);
+                                              row_sum, lrb);
     if (par) pair_final_kernel<<<cdiv(D, 64), 1024, 0, s>>>(ws, nrb, D, dgamma, dbeta, accumulate);
     return avc_check_launch("avc_layer_norm_bwd");
   }

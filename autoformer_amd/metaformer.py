@@ -134,16 +134,19 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, cache, B, T_in, pad, w, b):
         Wf, _ = Lyr.conv_packs(cache, w)
+        x = K.twin(x)  # bf16 mode: the conv streams its bf16 twin (an fp32 window took the fp32-operand kernel)
         y, T_out = Lyr.conv_fwd(x, B, T_in, w, b, pad, Wf)
         ctx.cache, ctx.args, ctx.bias = cache, (B, T_in, T_out, pad), b
         ctx.save_for_backward(x, w)
+        ctx.x16 = getattr(x, "_bf16", None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
+        K.attach_twin(x, ctx.x16)
         B, T_in, T_out, pad = ctx.args
-        dy = dy.contiguous()
+        dy = K.twin(dy.contiguous())  # both gradient products read dy as a bf16 operand
         sink = Lyr.sink_on()
         dW = Lyr.conv_wgrad(dy, x, B, T_in, T_out, w, pad, into=_sink(w))
         db = K.colsum(dy, B * T_out, w.shape[0], out=_sink(ctx.bias), accumulate=sink)
@@ -163,19 +166,21 @@ class _EncEmbedFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, mel2d, emb, cache, B, T, w, b):
-        x = K.enc_concat(mel2d, emb, B, T)
+        x = K.twin(K.enc_concat(mel2d, emb, B, T))
         Wf, _ = Lyr.conv_packs(cache, w)
         y, _ = Lyr.conv_fwd(x, B, T, w, b, w.shape[-1] // 2, Wf)
         ctx.cache, ctx.args, ctx.n_mel, ctx.bias = cache, (B, T), mel2d.shape[1], b
         ctx.save_for_backward(x, w)
+        ctx.x16 = getattr(x, "_bf16", None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
+        K.attach_twin(x, ctx.x16)
         B, T = ctx.args
         pad = w.shape[-1] // 2
-        dy = dy.contiguous()
+        dy = K.twin(dy.contiguous())
         sink = Lyr.sink_on()
         dW = Lyr.conv_wgrad(dy, x, B, T, T, w, pad, into=_sink(w))
         db = K.colsum(dy, B * T, w.shape[0], out=_sink(ctx.bias), accumulate=sink)
