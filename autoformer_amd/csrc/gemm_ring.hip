@@ -1133,7 +1133,7 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
     return true;                                       \
   }
   RING_CASE(256, 256, 2) RING_CASE(256, 128, 3) RING_CASE(128, 128, 4) RING_CASE(128, 128, 3)
-  RING_CASE(128, 256, 3) RING_CASE(256, 128, 2)
+  RING_CASE(128, 256, 3) RING_CASE(256, 128, 2) RING_CASE(128, 128, 2)  // (128x128x2: 64 KB, two per CU)
 #undef RING_CASE
   // 32-deep slots (nst = 10 + stages in the forced form)
 #define RING32_CASE(BMV, BNV, NSV)                        \

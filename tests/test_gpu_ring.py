@@ -37,7 +37,7 @@ def _rel(a, b):
 
 
 CFGS = [(256, 256, 2), (256, 128, 3), (128, 128, 4), (128, 128, 3), (128, 256, 3), (256, 128, 2),
-        (256, 256, 14), (256, 128, 15), (128, 128, 16)]  # nst 10 + n: 32-deep slots (gemm_ring32_kernel)
+        (256, 256, 14), (256, 128, 15), (128, 128, 16), (128, 128, 2)]  # nst 10 + n: 32-deep slots (gemm_ring32_kernel)
 
 
 @pytest.mark.parametrize("cfg", CFGS)
