@@ -1097,8 +1097,8 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
     bn = c.bn;
     nst = c.nst;
   } else {
-    // Tile choice by a wave-quantised cost model: each configuration runs one workgroup per CU, so
-    // a product costs ceil(tiles / 256) rounds of BM*BN*K work at the configuration's per-flop
+    // Tile choice by a wave-quantised cost model: a configuration runs occ workgroups per CU, so
+    // a product costs ceil(tiles / (256 occ)) rounds of BM*BN*K work at the configuration's per-flop
     // efficiency (1 : 0.85 : 0.75 for 256x256 / 256x128 / 128x128, fitted to the per-call census
     // of the C2 / C4 steps, tools/gemm_census.py --ring-ab, profiles/r4_gemm_census_*.txt).  Every
     // plain bf16 NN product of those steps ran as fast or faster on the chosen ring tile than on
@@ -1106,18 +1106,23 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
     // cannot take (344 / 88 / 80 channels) and N <= 512, where it measured faster than
     // gemm_conv.hip; the rest stay on gemm_conv.hip.
     if (win && (g.N > 512 || a.chans % CV_CBK == 0)) return false;
+    // 128x128x2 (64 KB of LDS) runs TWO workgroups per CU, one's epilogue under the other's K loop:
+    // 512 concurrent tiles at efficiency 0.47, 0.38 under the GELU-backward epilogue (its extra
+    // operand stream) -- fitted to the same census with that tile forced (profiles/r4_gemm_census_x2_c*.txt)
     struct Opt {
-      int bm, bn, nst;
+      int bm, bn, nst, occ;
       double eff;
     };
-    const Opt opts[3] = {{256, 256, 2, 1.0}, {256, 128, 3, 0.85}, {128, 128, 4, 0.75}};
+    const Opt opts[4] = {{256, 256, 2, 1, 1.0}, {256, 128, 3, 1, 0.85}, {128, 128, 4, 1, 0.75},
+                         {128, 128, 2, 2, g.agrad ? 0.38 : 0.47}};
     double best = 0;
     bm = 0;
     bn = 0;
     nst = 0;
     for (const Opt& o : opts) {
       const long long tiles = (long long)((g.M + o.bm - 1) / o.bm) * ((g.N + o.bn - 1) / o.bn) * units;
-      const double cost = (double)((tiles + 255) / 256) * o.bm * o.bn / o.eff;
+      const long long slots = 256ll * o.occ;
+      const double cost = (double)((tiles + slots - 1) / slots) * o.bm * o.bn / o.eff;
       if (!bm || cost < best * 0.999) {
         best = cost;
         bm = o.bm;
