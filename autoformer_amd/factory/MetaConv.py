@@ -56,11 +56,11 @@ class MetaBlock(nn.Module):
         if L != self.crop_len:
             raise RuntimeError(f"MetaBlock needs L == crop_len ({self.crop_len}), got {L}")
         y = MF.group_norm(x, B, self.norm1, twin=not self.pool)  # the conv mixer reads it as a bf16 operand
-        mix = MF.pool_mixer(y, B, L) if self.pool else Lyr.conv_bn(self._mix, y, B, L)
-        x = MF.add(x, mix)
+        # the residual adds ride on the BN-apply pass of the conv branch (x + relu(bn(conv(.))))
+        x = MF.add(x, MF.pool_mixer(y, B, L)) if self.pool else Lyr.conv_bn(self._mix, y, B, L, residual=x)
         a = Lyr.conv_bn(self._c1, x, B, L)
         m = MF.mlp_mixer(MF.group_norm(a, B, self.norm2), self.mlp, B, L)
-        return MF.add(x, Lyr.conv_bn(self._c2, m, B, L))
+        return Lyr.conv_bn(self._c2, m, B, L, residual=x)
 
 
 class Encoder(nn.Module):
