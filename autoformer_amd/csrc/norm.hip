@@ -510,7 +510,8 @@ __global__ void pool3_kernel(const float* x, float* y, int L, int C, long long t
 // ---------------------------------------------------------------- MLP-Mixer patchify
 // image rows = channel axis (C = H*ps), cols = frame axis (L = W*ps) of frame-major nf (B, L, C):
 // P[b][h*W + w][p1*ps + p2] = nf[b][w*ps + p2][h*ps + p1]
-__global__ void patchify_kernel(const float* nf, float* P, int L, int C, int ps, long long total, int backward) {
+template <typename TO>
+__global__ void patchify_kernel(const float* nf, TO* P, int L, int C, int ps, long long total, int backward) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int W = L / ps, pp = ps * ps;
@@ -520,8 +521,8 @@ __global__ void patchify_kernel(const float* nf, float* P, int L, int C, int ps,
   const int b = (int)(pt / np), patch = (int)(pt % np);
   const int h = patch / W, w = patch % W, p1 = e / ps, p2 = e % ps;
   const long long src = ((long long)b * L + (w * ps + p2)) * C + (h * ps + p1);
-  if (!backward) P[i] = nf[src];
-  else P[src] = nf[i];  // scatter back: P is the frame-major gradient, nf the patch gradient
+  if (!backward) P[i] = (TO)nf[src];
+  else P[src] = (TO)nf[i];  // scatter back: P is the frame-major gradient, nf the patch gradient
 }
 
 // ---------------------------------------------------------------- batched transpose (+accumulate)
@@ -746,8 +747,15 @@ extern "C" int avc_pool3_mixer(const float* x, float* y, int B, int L, int C, in
 extern "C" int avc_patchify(const float* src, float* dst, int B, int L, int C, int ps, int backward, void* stream) {
   AVC_CHECK_ARG(src && dst && ps > 0 && L % ps == 0 && C % ps == 0, "avc_patchify: L and C must divide by patch");
   const long long total = (long long)B * L * C;
-  patchify_kernel<<<GRID1(total)>>>(src, dst, L, C, ps, total, backward);
+  patchify_kernel<float><<<GRID1(total)>>>(src, dst, L, C, ps, total, backward);
   return avc_check_launch("avc_patchify");
+}
+
+extern "C" int avc_patchify16(const float* src, void* dst, int B, int L, int C, int ps, void* stream) {
+  AVC_CHECK_ARG(src && dst && ps > 0 && L % ps == 0 && C % ps == 0, "avc_patchify16: L and C must divide by patch");
+  const long long total = (long long)B * L * C;
+  patchify_kernel<bf16><<<GRID1(total)>>>(src, static_cast<bf16*>(dst), L, C, ps, total, 0);
+  return avc_check_launch("avc_patchify16");
 }
 
 extern "C" int avc_transpose_batched(const float* src, float* dst, int B, int R, int C, int accumulate, void* stream) {

@@ -751,7 +751,12 @@ def pool3_mixer(x, B, Lf, C, backward=False):
     return y
 
 
-def patchify(src, B, Lf, C, ps, backward=False):
+def patchify(src, B, Lf, C, ps, backward=False, out_bf16=False):
+    """out_bf16 (forward only): the patches as a bf16 tensor (a GEMM operand alone)."""
+    if out_bf16 and not backward:
+        dst = torch.empty(B * (C // ps) * (Lf // ps), ps * ps, device=src.device, dtype=torch.bfloat16)
+        L.call("avc_patchify16", src.data_ptr(), dst.data_ptr(), B, Lf, C, int(ps), stream())
+        return dst
     if backward:
         dst = torch.empty(B * Lf, C, device=src.device)
     else:

@@ -323,7 +323,8 @@ class _MLPMixerFn(torch.autograd.Function):
         NP = (C // ps) * (Lf // ps)
         D = we.shape[0]
         dev = nf.device
-        P = K.twin(K.patchify(nf, B, Lf, C, ps))               # (B*NP, ps^2)
+        # (B*NP, ps^2): bf16 mode writes the patches in bf16 directly (read only as GEMM operands)
+        P = K.twin(K.patchify(nf, B, Lf, C, ps, out_bf16=K.compute() == K.BF16))
         weC, w3C, w4C, _, _, _ = _cf_weights(mix, we, w3, w4)
         Z = _lin(P, B * NP, D, ps * ps, weC, be)                # (B*NP, D)
         bf = K.compute() == K.BF16  # Y1 / Y2 are read only as bf16 operands: no fp32 copies

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 22
+#define AVC_ABI_VERSION 23
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -422,6 +422,8 @@ int avc_pool3_mixer(const float* x, float* y, int B, int L, int C, int backward,
 /* Rearrange('b c (h p1) (w p2) -> b (h w) (p1 p2 c)') of the (C x L) image held frame-major
  * as (B, L, C) (image rows = channels); backward != 0 scatters a patch gradient back. */
 int avc_patchify(const float* src, float* dst, int B, int L, int C, int ps, int backward, void* stream);
+/* The forward rearrangement written in bf16 (the patches are read only as the embedding GEMM's operand). */
+int avc_patchify16(const float* src, void* dst, int B, int L, int C, int ps, void* stream);
 /* dst[b] (+)= src[b]^T for B row-major R x C matrices. */
 int avc_transpose_batched(const float* src, float* dst, int B, int R, int C, int accumulate, void* stream);
 /* The same transpose of an fp32 or bf16 (src_dtype) source into rows of ld >= R elements (r in [R, ld) written 0),

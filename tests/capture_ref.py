@@ -494,16 +494,19 @@ class Capture:
                              {"y": _rel(y, ref.reshape_as(y))}))
         return y
 
-    def _patchify(self, src, B, Lf, C, ps, backward=False):
+    def _patchify(self, src, B, Lf, C, ps, backward=False, out_bf16=False):
         torch.cuda.synchronize()
-        dst = self._orig["patchify"](src, B, Lf, C, ps, backward)
+        dst = self._orig["patchify"](src, B, Lf, C, ps, backward, out_bf16)
         torch.cuda.synchronize()
         H, W = C // ps, Lf // ps
         if not backward:  # P[b][h*W + w][p1*ps + p2] = nf[b][w*ps + p2][h*ps + p1]
             ref = src.double().view(B, W, ps, H, ps).permute(0, 3, 1, 4, 2).reshape_as(dst)
         else:
             ref = src.double().view(B, H, W, ps, ps).permute(0, 2, 4, 1, 3).reshape_as(dst)
-        self.records.append(("patchify", f"patchify B{B} L{Lf} C{C}" + (" bwd" if backward else ""),
+        if dst.dtype == torch.bfloat16:
+            ref = ref.to(torch.bfloat16)  # the bf16 form is the rounding of the same rearrangement
+        self.records.append(("patchify", f"patchify B{B} L{Lf} C{C}" + (" bwd" if backward else "")
+                             + (" bf16" if dst.dtype == torch.bfloat16 else ""),
                              {"out": _rel(dst, ref)}))
         return dst
 

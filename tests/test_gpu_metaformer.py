@@ -183,6 +183,9 @@ def test_patchify_roundtrip(B, L, C, ps):
     torch.testing.assert_close(P, ref, rtol=0, atol=0)
     back = K.patchify(P, B, L, C, ps, backward=True)
     torch.testing.assert_close(back, x, rtol=0, atol=0)
+    P16 = K.patchify(x, B, L, C, ps, out_bf16=True)  # the bf16 form: the rounding of the same rearrangement
+    assert P16.dtype == torch.bfloat16
+    torch.testing.assert_close(P16, ref.to(torch.bfloat16), rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("B,R,C", [(2, 176, 344), (3, 7, 5), (1, 344, 88)])
