@@ -525,6 +525,35 @@ unsigned* avc_counter_slots(int n, hipStream_t s) {
   return base + b;
 }
 
+float* avc_zero_slots(int n, hipStream_t s) {
+  constexpr unsigned POOL = 1u << 23;  // 32 MB of floats per device
+  constexpr int MAXD = 64;
+  static std::mutex mu;
+  static std::atomic<float*> pool[MAXD];
+  static std::atomic<unsigned> next[MAXD];
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXD || n <= 0 || (unsigned)n > POOL) {
+    avc_set_error("avc_zero_slots: no device / bad size");
+    return nullptr;
+  }
+  if (!pool[dev].load(std::memory_order_acquire)) {
+    std::lock_guard<std::mutex> lk(mu);
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (!pool[dev].load() && hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusNone) {
+      float* p = nullptr;
+      if (hipMalloc(&p, POOL * sizeof(float)) == hipSuccess && hipMemset(p, 0, POOL * sizeof(float)) == hipSuccess &&
+          hipDeviceSynchronize() == hipSuccess)
+        pool[dev].store(p, std::memory_order_release);
+    }
+  }
+  float* base = pool[dev].load(std::memory_order_acquire);
+  if (!base) return nullptr;  // (the caller falls back to its direct form)
+  const unsigned n64 = ((unsigned)n + 63u) & ~63u;  // 256-B aligned regions
+  unsigned b = next[dev].fetch_add(n64) % POOL;
+  if (b + n64 > POOL) b = 0;
+  return base + b;
+}
+
 namespace {
 // dtype dispatch of the typed BN kernels: F(TY) / F(TD, TY) with float or bf16 pointers
 template <typename Fn>

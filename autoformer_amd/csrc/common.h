@@ -116,6 +116,9 @@ static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b)
 // use inside a stream capture, allocation failure).  The last arrival of a launch resets its
 // slot to 0, so slots are reused without a reset pass.
 unsigned* avc_counter_slots(int n, hipStream_t s);
+// n floats of a device pool that is all zero between uses: the user leaves its region zeroed
+// (a ring like avc_counter_slots; created on first use outside a stream capture)
+float* avc_zero_slots(int n, hipStream_t s);
 
 // Agent-coherent (sc1) scalar store / load: the data handed from block to block through an
 // arrival counter bypasses the per-XCD L2 on both sides, so no fence (an agent-scope release

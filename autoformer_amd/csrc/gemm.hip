@@ -774,6 +774,17 @@ __global__ void colsum_atomic_kernel(const T* c, long long ldc, int M, int nc, f
   for (int r = r0; r < min(M, r0 + 64); ++r) s += (float)c[(long long)r * ldc + col];
   atomicAdd(out + col, s);
 }
+// the slotted column sums (GemmArgs::csum_ws) into csum, leaving the slots zeroed for the next user
+__global__ void colsum_slots_kernel(float* ws, int slots, int nc, float* csum) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= nc) return;
+  float s = 0.f;
+  for (int k = 0; k < slots; ++k) {
+    s += ws[(long long)k * nc + col];
+    ws[(long long)k * nc + col] = 0.f;
+  }
+  csum[col] += s;
+}
 static int gelu_after(const GemmArgs& g, const GeluPost& p, hipStream_t s) {
   const long long n = (long long)g.M * g.N * g.batch;
   const int blocks = (int)(n / 256 + 1 < 8192 ? n / 256 + 1 : 8192);
@@ -842,6 +853,8 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
   g.c16pre = reinterpret_cast<bf16*>(d->c_pre_bf16);
   g.csum = d->col_sum;
   g.csum_n = d->col_sum_n;
+  g.csum_ws = nullptr;
+  g.csum_slots = 1;
   g.ctr = d->c_trans_rows;
   AVC_CHECK_ARG(g.ctr == 0 || (g.ctr > 0 && g.ctr % 4 == 0 && d->M % g.ctr == 0 && d->ldc == d->N && d->c &&
                                !d->a.kstrided && !d->b.kstrided &&
@@ -933,6 +946,15 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
     }
     const char* what = "avc_gemm(fast)";
     GeluPost post;
+    static const bool slots_on = [] {
+      const char* e = getenv("AVC_COLSUM_SLOTS");
+      return !(e && e[0] == '0');
+    }();
+    if (g.csum && slots_on && (long long)g.M * g.batch >= 4096) {
+      const int nc = g.csum_n > 0 ? g.csum_n : g.N;
+      g.csum_slots = 32;
+      g.csum_ws = avc_zero_slots(g.csum_slots * nc, s);  // null: the direct atomics
+    }
     const bool ring = !aks && !bks && gemm_ring_launch(g, s);
     if (ring) what = "avc_gemm(ring)";
     else post = strip_gelu(g);  // the other kernels have no GELU epilogue: a pass after them
@@ -948,6 +970,11 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
       else launch_fast_layout<128>(g, aks, bks, nb, s);
     }
     if (avc_check_launch(what)) return -1;
+    if (ring && g.csum_ws) {
+      const int nc = g.csum_n > 0 ? g.csum_n : g.N;
+      colsum_slots_kernel<<<cdiv(nc, 256), 256, 0, s>>>(g.csum_ws, g.csum_slots, nc, g.csum);
+      if (avc_check_launch("avc_gemm(col_sum slots)")) return -1;
+    }
     if (gelu_after(g, post, s)) return -1;
     if (bb && !bnb_fused) return bnb_after(d, bb, s);
     return (f && !g.bn_cnt) ? bn_finalize_after(g, f, stream) : 0;

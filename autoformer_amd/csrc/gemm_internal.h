@@ -38,6 +38,11 @@ struct GemmArgs {
   int ctr;             // avc_gemm_desc.c_trans_rows: C(m, n) stored at ((m / ctr) * N + n) * ctr + m % ctr
   float* csum;         // avc_gemm_desc.col_sum: csum[n] += column sums of the stored C (ring kernels only)
   int csum_n;
+  // csum_ws != null: the ring kernels add their tile sums into csum_ws[slot][n] (slot = row tile %
+  // csum_slots, self-zeroing pool memory) and one reduce pass adds the slots into csum -- the same
+  // column's atomics from every row tile had serialised at one address (up to 924 per column)
+  float* csum_ws;
+  int csum_slots;
   const float* rbias;  // per-(utterance, edge class) row bias (avc_gemm_desc.row_bias), nullable
   int rb_t, rb_pad;
   FastDiv rb_div;      // divide a row by rb_t

@@ -163,6 +163,11 @@ constexpr size_t ring_epi_lds() {
   return (size_t)8 * 64 * (BN_ / 4 + 4) * 4;
 }
 
+// where a row tile's column sums go: its slot of the self-zeroing workspace, or csum itself
+__device__ __forceinline__ float* csum_dst(const GemmArgs& g, int row_tile, int lim) {
+  return g.csum_ws ? g.csum_ws + (long long)(row_tile % g.csum_slots) * lim : g.csum;
+}
+
 // Stores of the 2 x 4 wave layout's accumulators (wave (wm, wn) owns rows m0 + wm*TWM + i*16 +
 // 4*(lane>>4) + e and columns n0 + wn*TWN + j*16 + (lane&15)): each wave stages 64-row chunks of
 // its tile in its own LDS region and stores them row-contiguous, 16 B per lane (fp32 C) / 8 B
@@ -297,9 +302,10 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
       if (lane < L8) {
         const int col = n0 + wn * TWN + 8 * lane;
         const int lim = g.csum_n > 0 ? g.csum_n : g.N;
+        float* dst = csum_dst(g, m0 / BM_ + bz, lim);
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-          if (col + k < lim) atomicAdd(csum + col + k, k < 4 ? cs0[k] : cs1[k - 4]);
+          if (col + k < lim) atomicAdd(dst + col + k, k < 4 ? cs0[k] : cs1[k - 4]);
       }
     }
     return;
@@ -371,9 +377,10 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
     if (lane < TWN / 4) {
       const int col = n0 + wn * TWN + 4 * lane;
       const int lim = g.csum_n > 0 ? g.csum_n : g.N;
+      float* dst = csum_dst(g, m0 / BM_ + bz, lim);
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if (col + k < lim) atomicAdd(csum + col + k, cs[k]);
+        if (col + k < lim) atomicAdd(dst + col + k, cs[k]);
     }
   }
 }

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--sweep", action="store_true", help="also time split-K 1..64 for the K-strided (TT) calls")
     ap.add_argument("--ring-ab", action="store_true")
     ap.add_argument("--force", default="", help="also time forced ring configs, e.g. '256,128,3;128,128,4'")
+    ap.add_argument("--strip", default="", help="also time each call with these keyword arguments removed, "
+                    "e.g. 'col_sum' or 'col_sum,act_grad_of' (an epilogue ablation; results not checked)")
     args = ap.parse_args()
     import importlib
 
@@ -96,6 +98,18 @@ def main():
             torch.cuda.synchronize()
             _lib.call("avc_gemm_set_ring", -1, 0, 0, 0, 0, 2)
             off += f" | {bm}x{bn}x{nst} {e0.elapsed_time(e1) / args.reps * 1e3:.1f}"
+        for group in filter(None, args.strip.split(";")):
+            drop = set(group.split(","))
+            if not drop & set(k for k, v in kw.items() if v is not None):
+                continue
+            kw2 = {k: v for k, v in kw.items() if k not in drop}
+            real(M, N, Kd, a, b, c, **kw2)
+            e0.record()
+            for _ in range(args.reps):
+                real(M, N, Kd, a, b, c, **kw2)
+            e1.record()
+            torch.cuda.synchronize()
+            off += f" | -{group} {e0.elapsed_time(e1) / args.reps * 1e3:.1f}"
         batch = kw.get("batch", 1)
         fl = 2.0 * M * N * Kd * batch
         lay = ("T" if a.kstrided else "N") + ("T" if b.kstrided else "N")
