@@ -163,12 +163,14 @@ def test_gelu_epilogues(ring, store):
 
 
 @pytest.mark.parametrize("ring", [-1, 0])
-@pytest.mark.parametrize("batch", [1, 3])
+@pytest.mark.parametrize("batch", [1, 3, 12])
 @pytest.mark.parametrize("store", ["f32", "bf16"])
 def test_col_sum_epilogue(ring, batch, store):
     """col_sum[:n] += column sums of the stored (GELU-backward) values, over every row of every
     folded batch, with a padded leading dimension (n < N: the token mixer's 4*NP of 4*NPp); with
-    a bf16-only store the sums are of the fp32 values (ring) or of the stored bf16 (fallback)."""
+    a bf16-only store the sums are of the fp32 values (ring) or of the stored bf16 (fallback).
+    batch 12 (4128 rows) takes the slotted form (32 row-tile slots + a reduce pass that leaves the
+    slots zeroed): the product runs twice and the second call must add the same sums again."""
     from autoformer_amd import kernels as K
 
     torch.manual_seed(7 + batch)
@@ -193,6 +195,12 @@ def test_col_sum_epilogue(ring, batch, store):
     tol = 1e-5 if store == "f32" else 5e-3
     assert _rel(d.float(), dref) < tol
     assert _rel(cs[:n] - cs0[:n], dref[:, :n].sum(0)) < tol
+    assert torch.equal(cs[n:], cs0[n:])
+    cs1 = cs.clone()
+    K.gemm(M, N, Kd, K.operand(a, Kd, batch_stride=M * Kd), K.operand(b, Kd), d, c_bf16=d16, act_grad_of=x,
+           batch=batch, c_batch_stride=M * N, col_sum=cs, col_sum_n=n)
+    torch.cuda.synchronize()
+    assert _rel(cs[:n] - cs1[:n], dref[:, :n].sum(0)) < tol
     assert torch.equal(cs[n:], cs0[n:])
 
 
