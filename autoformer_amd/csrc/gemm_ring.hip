@@ -240,51 +240,68 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
           for (int e = 0; e < 4; ++e)
             reg[(ii * 16 + 4 * (lane >> 4) + e) * RP + j * 16 + (lane & 15)] = acc[ch * 4 + ii][j][e];
       __syncthreads();
-#pragma unroll 4
-      for (int it = 0; it < 64 / R8; ++it) {
-        const int lr = it * R8 + lane / L8, c8 = lane % L8;
-        const int row = m0 + wm * TWM + ch * 64 + lr, col = n0 + wn * TWN + 8 * c8;
-        if (row >= g.M || col >= g.N) continue;
-        f32x4 v0 = *reinterpret_cast<const f32x4*>(reg + lr * RP + 8 * c8);
-        f32x4 v1 = *reinterpret_cast<const f32x4*>(reg + lr * RP + 8 * c8 + 4);
-        const long long o = (long long)row * g.ldc + col;
-        if (col + 7 < g.N) {
-          if (agr16) {
-            const bf16x8 h = *reinterpret_cast<const bf16x8*>(agr16 + o);
+      // the GELU-backward input is read G4 iterations at a time by UNCONDITIONAL loads (row and
+      // column clamped into the tensor: ldc == N, N % 8 == 0 on this path), so the G4 loads are in
+      // flight together; a load inside the bounds branch had been waited for at the branch join,
+      // one 16-B load per wave in flight at a time (+180-220 us on the 327 MB pre-activations)
+      constexpr int G4 = 64 / R8 < 4 ? 64 / R8 : 4;
+      for (int it0 = 0; it0 < 64 / R8; it0 += G4) {
+        bf16x8 hv[G4];
+        if (agr16) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              v0[k] *= gelu_grad_f((float)h[k]);
-              v1[k] *= gelu_grad_f((float)h[4 + k]);
-            }
+          for (int k = 0; k < G4; ++k) {
+            const int r = min(m0 + wm * TWM + ch * 64 + (it0 + k) * R8 + lane / L8, g.M - 1);
+            const int cc = min(n0 + wn * TWN + 8 * (lane % L8), g.N - 8);
+            hv[k] = *reinterpret_cast<const bf16x8*>(agr16 + (long long)r * g.ldc + cc);
           }
-          if (csum) {
-            cs0 += v0;
-            cs1 += v1;
-          }
-          if (P16)
-            *reinterpret_cast<bf16x8*>(P16 + o) = bf16x8{(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3],
-                                                         (bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
-          if (C16) {
-            if (gelu16) {
+        }
+#pragma unroll
+        for (int k4 = 0; k4 < G4; ++k4) {
+          const int it = it0 + k4;
+          const int lr = it * R8 + lane / L8, c8 = lane % L8;
+          const int row = m0 + wm * TWM + ch * 64 + lr, col = n0 + wn * TWN + 8 * c8;
+          if (row >= g.M || col >= g.N) continue;
+          f32x4 v0 = *reinterpret_cast<const f32x4*>(reg + lr * RP + 8 * c8);
+          f32x4 v1 = *reinterpret_cast<const f32x4*>(reg + lr * RP + 8 * c8 + 4);
+          const long long o = (long long)row * g.ldc + col;
+          if (col + 7 < g.N) {
+            if (agr16) {
+              const bf16x8 h = hv[k4];
 #pragma unroll
               for (int k = 0; k < 4; ++k) {
-                v0[k] = gelu_f(v0[k]);
-                v1[k] = gelu_f(v1[k]);
+                v0[k] *= gelu_grad_f((float)h[k]);
+                v1[k] *= gelu_grad_f((float)h[4 + k]);
               }
             }
-            *reinterpret_cast<bf16x8*>(C16 + o) = bf16x8{(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3],
-                                                         (bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
-          }
-        } else {
-          for (int k = 0; k < 8 && col + k < g.N; ++k) {
-            float x = k < 4 ? v0[k] : v1[k - 4];
-            if (agr16) x *= gelu_grad_f((float)agr16[o + k]);
-            if (P16) P16[o + k] = (bf16)x;
             if (csum) {
-              if (k < 4) cs0[k] += x;
-              else cs1[k - 4] += x;
+              cs0 += v0;
+              cs1 += v1;
             }
-            if (C16) C16[o + k] = (bf16)(gelu16 ? gelu_f(x) : x);
+            if (P16)
+              *reinterpret_cast<bf16x8*>(P16 + o) = bf16x8{(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3],
+                                                           (bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
+            if (C16) {
+              if (gelu16) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                  v0[k] = gelu_f(v0[k]);
+                  v1[k] = gelu_f(v1[k]);
+                }
+              }
+              *reinterpret_cast<bf16x8*>(C16 + o) = bf16x8{(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3],
+                                                           (bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
+            }
+          } else {
+            for (int k = 0; k < 8 && col + k < g.N; ++k) {
+              float x = k < 4 ? v0[k] : v1[k - 4];
+              if (agr16) x *= gelu_grad_f((float)agr16[o + k]);
+              if (P16) P16[o + k] = (bf16)x;
+              if (csum) {
+                if (k < 4) cs0[k] += x;
+                else cs1[k - 4] += x;
+              }
+              if (C16) C16[o + k] = (bf16)(gelu16 ? gelu_f(x) : x);
+            }
           }
         }
       }
