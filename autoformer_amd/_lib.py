@@ -14,7 +14,8 @@ import threading
 import torch  # noqa: F401  (must precede the HIP library)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libautovc_hip.so")
+# AVC_LIB_PATH: another build of the same ABI (same-box A/B timing of two builds, tools/ only)
+LIB_PATH = os.environ.get("AVC_LIB_PATH") or os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["gemm_ring.hip", "gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "graph.hip", "fold.hip", "disc.hip"]
 ABI_VERSION = 23

@@ -9,6 +9,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_ring.py tests/test_gpu_capt
 tail -1 $OUT/tests.log
 timeout -k 10 300 python -u tools/gemm_census.py --model MetaConv --reps 5 --strip 'col_sum;act_grad_of' > $OUT/census_c4_strip.txt 2>&1 || { tail -20 $OUT/census_c4_strip.txt; exit 1; }
 grep gelu $OUT/census_c4_strip.txt | head -16
+timeout -k 10 300 python -u tools/gemm_census.py --model AutoVC --reps 10 > $OUT/census_c2.txt 2>&1 || { tail -20 $OUT/census_c2.txt; exit 1; }
 for rep in 1 2; do
   timeout -k 10 200 python -u bench.py --model MetaConv --steps 10 --warmup 3 --no-cpu-baseline > $OUT/c4.$rep.json 2>/dev/null || exit 1
 done
