@@ -108,9 +108,10 @@ __device__ __forceinline__ void bn_finalize_cols(const GemmArgs& g, int n0, floa
 }
 
 // GELU (erf form, nn.GELU) and its derivative for the fused epilogues
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erf_nb(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float gelu_grad_f(float x) {
-  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143267794f * __expf(-0.5f * x * x);
+  return 0.5f * (1.f + erf_nb(x * 0.70710678118654752f)) +
+         x * 0.39894228040143267794f * __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);
 }
 
 // Column offset of output column `col` (cperm: the Conv1d [Co][Ci][K] layout).

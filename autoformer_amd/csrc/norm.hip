@@ -469,7 +469,7 @@ __global__ void gelu_bwd_kernel(const float* g, const float* x, float* dx, long 
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float v = x[i];
-  const float cdf = 0.5f * (1.f + erff(v * 0.70710678118654752f));
+  const float cdf = 0.5f * (1.f + erf_nb(v * 0.70710678118654752f));
   const float pdf = 0.39894228040143267794f * expf(-0.5f * v * v);
   dx[i] = g[i] * (cdf + v * pdf);
 }

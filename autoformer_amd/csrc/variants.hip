@@ -264,7 +264,7 @@ __global__ void gelu_twin_kernel(const float* __restrict__ g, const float* __res
     if (bwd) gv = *reinterpret_cast<const f32x4*>(g + i0);
     for (int k = 0; k < 4; ++k) {
       const float a = xv[k];
-      const float cdf = 0.5f * (1.f + erff(a * 0.70710678118654752f));
+      const float cdf = 0.5f * (1.f + erf_nb(a * 0.70710678118654752f));
       v[k] = bwd ? gv[k] * (cdf + a * 0.39894228040143267794f * expf(-0.5f * a * a)) : a * cdf;
     }
     if (y) *reinterpret_cast<f32x4*>(y + i0) = f32x4{v[0], v[1], v[2], v[3]};
@@ -272,7 +272,7 @@ __global__ void gelu_twin_kernel(const float* __restrict__ g, const float* __res
   } else {
     for (long long i = i0; i < n; ++i) {
       const float a = x[i];
-      const float cdf = 0.5f * (1.f + erff(a * 0.70710678118654752f));
+      const float cdf = 0.5f * (1.f + erf_nb(a * 0.70710678118654752f));
       const float r = bwd ? g[i] * (cdf + a * 0.39894228040143267794f * expf(-0.5f * a * a)) : a * cdf;
       if (y) y[i] = r;
       if (y16) y16[i] = (bf16)r;

@@ -4,7 +4,7 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/$1
 mkdir -p $OUT
 cd $R
-timeout -k 10 600 python -u -m pytest tests/test_gpu_ring.py tests/test_gpu_capture.py tests/test_gpu_metaformer.py -x -q --timeout 600 --timeout-method thread \
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread \
     > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 tail -1 $OUT/tests.log
 timeout -k 10 300 python -u tools/gemm_census.py --model MetaConv --reps 5 --strip 'col_sum;act_grad_of' > $OUT/census_c4_strip.txt 2>&1 || { tail -20 $OUT/census_c4_strip.txt; exit 1; }
