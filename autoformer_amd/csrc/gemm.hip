@@ -750,14 +750,16 @@ static GeluPost strip_gelu(GemmArgs& g) {
   g.c16pre = nullptr;
   return p;
 }
-// act: c16[i] = GELU(src[i]); else c[i] / c16[i] = src[i] * GELU'(agr[i]) (src may alias either)
+// act: c16[i] = GELU(src[i]) (and pre16[i] = src[i] in bf16 when given); else c[i] / c16[i] =
+// src[i] * GELU'(agr[i]) (src may alias either)
 template <typename TS>
 __global__ void gelu_post_kernel(const TS* src, const void* agr, int agr16, float* c, bf16* c16, long long n,
-                                 int act) {
+                                 int act, bf16* pre16) {
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     float x = (float)src[i];
     if (act) {
       c16[i] = (bf16)gelu_f(x);
+      if (pre16) pre16[i] = (bf16)x;
       continue;
     }
     x *= gelu_grad_f(agr16 ? (float)static_cast<const bf16*>(agr)[i] : static_cast<const float*>(agr)[i]);
@@ -785,14 +787,16 @@ __global__ void colsum_slots_kernel(float* ws, int slots, int nc, float* csum) {
   }
   csum[col] += s;
 }
-static int gelu_after(const GemmArgs& g, const GeluPost& p, hipStream_t s) {
+// write_pre: the product kernel wrote fp32 C only (generic kernel): the bf16 pre-activation slot of a
+// fused GELU is filled here from C
+static int gelu_after(const GemmArgs& g, const GeluPost& p, hipStream_t s, bool write_pre = false) {
   const long long n = (long long)g.M * g.N * g.batch;
   const int blocks = (int)(n / 256 + 1 < 8192 ? n / 256 + 1 : 8192);
   if (p.act || p.agrad) {
     if (g.c) gelu_post_kernel<float><<<blocks, 256, 0, s>>>(g.c, p.agrad, p.agrad16, p.agrad ? g.c : nullptr, p.c16, n,
-                                                           p.act);
+                                                           p.act, write_pre ? p.pre16 : nullptr);
     else gelu_post_kernel<bf16><<<blocks, 256, 0, s>>>(p.act ? p.pre16 : p.c16, p.agrad, p.agrad16, nullptr, p.c16, n,
-                                                       p.act);
+                                                       p.act, nullptr);
     if (avc_check_launch("avc_gemm(gelu)")) return -1;
   }
   if (p.csum) {
@@ -980,7 +984,12 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
     return (f && !g.bn_cnt) ? bn_finalize_after(g, f, stream) : 0;
   }
   const GeluPost post = strip_gelu(g);
+  // the generic kernel writes fp32 C only: a bf16 output is produced afterwards from C by the GELU
+  // pass (fused GELU / GELU' epilogues), so C must exist and a plain bf16 twin is refused
   AVC_CHECK_ARG(!g.c16 || post.c16, "avc_gemm: c_bf16 output needs the fast path (bf16 compute, vectorisable operands)");
+  AVC_CHECK_ARG(g.c != nullptr,
+                "avc_gemm: a bf16-only output (no fp32 c) needs the fast path (bf16 compute, vectorisable operands)");
+  g.c16 = nullptr;  // written by gelu_after from C
   static const bool trace_generic = getenv("AVC_GEMM_TRACE") != nullptr;
   if (trace_generic && bf)
     fprintf(stderr, "avc_gemm generic: M=%d N=%d K=%d batch=%d split=%d aks=%d bks=%d avec=%d bvec=%d awin=%d chans=%d\n",
@@ -1002,7 +1011,7 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
   }
 #undef AVC_GEMM_LAUNCH
   if (avc_check_launch("avc_gemm")) return -1;
-  if (gelu_after(g, post, s)) return -1;
+  if (gelu_after(g, post, s, true)) return -1;
   if (bb) return bnb_after(d, bb, s);
   return f ? bn_finalize_after(g, f, stream) : 0;  // generic kernels: finalize launch(es) after the GEMM
 }

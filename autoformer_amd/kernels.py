@@ -106,8 +106,9 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     bf16): C *= GELU'(x) -- the MLP-Mixer GELU forward / backward folded into the GEMM epilogue.
     col_sum: col_sum[:col_sum_n or N] += column sums of C (a bias gradient, float atomics).
     c_trans_rows = R: every R-row block of C stored transposed (avc_gemm_desc.c_trans_rows)."""
-    if not c.is_cuda:  # (operands are checked by operand(); C's device decides the launch)
-        _dev(c)
+    # every pointer argument must be device memory (operands are checked by operand()); a CPU
+    # tensor would reach the kernel as a host pointer and fault the GPU instead of raising here
+    _dev(c, bias, residual, c_bf16, bn_partial)
     if _DETERMINISTIC:
         split_k = 1
     pre16 = None
@@ -360,7 +361,9 @@ class DeviceFault(RuntimeError):
 
 
 FAULT_BITS = {1: "persistent LSTM recurrence spin timeout (a workgroup of the grid was not resident or stalled; "
-                 "the step's outputs are invalid)"}
+                 "the step's outputs are invalid)",
+              2: "graph replay: a side-stream wait for the main stream timed out (the step's weight gradients are "
+                 "invalid)"}
 
 
 def raise_on_fault(value):
@@ -715,11 +718,23 @@ def group_norm_bwd(dy, x, gamma, mean, rstd, B, C, dgamma=None, dbeta=None, accu
     return dx
 
 
+def ln_vec(D):
+    """Whether the one-pass register-row LayerNorm forms apply (norm.hip ln_*_v_kernel)."""
+    return D % 4 == 0 and D <= 512
+
+
 def layer_norm_fwd(x, gamma, beta, eps, out_bf16=False):
     """out_bf16: y as a bf16 tensor only (an operand read only by bf16 GEMMs / transposes)."""
     R, D = x.shape
-    y = torch.empty(R, D, device=x.device, dtype=torch.bfloat16 if out_bf16 else torch.float32)
     mean, rstd = torch.empty(R, device=x.device), torch.empty(R, device=x.device)
+    if out_bf16 and not ln_vec(D):
+        # the one-pass bf16 form holds a row in registers (D % 4 == 0, D <= 512): otherwise the
+        # fp32 LayerNorm, then a convert pass
+        y = torch.empty(R, D, device=x.device)
+        L.call("avc_layer_norm_fwd2", x.data_ptr(), R, D, _ptr(gamma), _ptr(beta), float(eps), y.data_ptr(), None,
+               mean.data_ptr(), rstd.data_ptr(), stream())
+        return convert(y, BF16), mean, rstd
+    y = torch.empty(R, D, device=x.device, dtype=torch.bfloat16 if out_bf16 else torch.float32)
     L.call("avc_layer_norm_fwd2", x.data_ptr(), R, D, _ptr(gamma), _ptr(beta), float(eps),
            None if out_bf16 else y.data_ptr(), y.data_ptr() if out_bf16 else None, mean.data_ptr(), rstd.data_ptr(),
            stream())
@@ -733,6 +748,19 @@ def layer_norm_bwd(dy, x, gamma, mean, rstd, dgamma=None, dbeta=None, accumulate
     R, D = x.shape
     dx = torch.empty_like(x)
     dx16 = _twin_buf(dx, None) if twin else None
+    if not ln_vec(D) and (residual is not None or twin or row_sum is not None):
+        # the one-pass form (residual add, bf16 twin, row sums in the same pass) needs D % 4 == 0 and
+        # D <= 512: otherwise the plain backward, then the add / convert passes
+        if row_sum is not None:
+            raise RuntimeError("layer_norm_bwd: row sums need D % 4 == 0 and D <= 512")
+        L.call("avc_layer_norm_bwd", dy.data_ptr(), x.data_ptr(), _ptr(gamma), mean.data_ptr(), rstd.data_ptr(), R, D,
+               dx.data_ptr(), _ptr(dgamma), _ptr(dbeta), int(accumulate), _ws(R, D, x.device).data_ptr(), stream())
+        if residual is not None:
+            add(dx, residual, out=dx)
+        if dx16 is not None:
+            convert(dx, BF16, out=dx16)
+            return attach_twin(dx, dx16)
+        return dx
     L.call("avc_layer_norm_bwd2", dy.data_ptr(), x.data_ptr(), _ptr(gamma), mean.data_ptr(), rstd.data_ptr(), R, D,
            _ptr(residual), dx.data_ptr(), _ptr(dx16), _ptr(row_sum), _ptr(dgamma), _ptr(dbeta), int(accumulate),
            _ws(R, D, x.device).data_ptr(), stream())
@@ -894,3 +922,54 @@ def gelu_bwd_twin(g, x):
     L.call("avc_gelu_twin", g.data_ptr(), x.data_ptr(), dx.data_ptr(), _ptr(d16), x.numel(), 1, stream())
     return attach_twin(dx, d16)
 
+
+
+# ------------------------------------------------------------------------- segmented graph replay
+def capture_deps(stream_raw):
+    """Capture dependencies (graph node handles) of a capturing raw stream."""
+    import ctypes
+
+    arr = (ctypes.c_void_p * 256)()
+    n = L.lib().avc_capture_deps(ctypes.c_void_p(stream_raw), arr, 256)
+    if n < 0:
+        L.check(n, "avc_capture_deps")
+    return [arr[i] for i in range(n)]
+
+
+class GraphSplit:
+    """A captured step rebuilt as main-stream / side-stream graph segments (graph.hip): the
+    weight-gradient branch replays beside the main chain instead of after it."""
+
+    FIELDS = ("main_nodes", "side_nodes", "cross_edges", "segments", "kernel_nodes", "memset_nodes",
+              "memcpy_nodes", "empty_nodes", "post_nodes", "wait_nodes", "signal_nodes")
+
+    def __init__(self, raw_graph, main_tails, side_tails, max_segments=None, mode=None):
+        """mode 1 (default): one main and one side graph ordered on the device by signal / wait
+        kernel nodes; mode 0: up to max_segments main / side graph pairs ordered by events."""
+        import ctypes
+
+        if max_segments is None:
+            max_segments = int(os.environ.get("AVC_GRAPH_SEGMENTS", "64"))
+        if mode is None:
+            mode = int(os.environ.get("AVC_GRAPH_MODE", "1"))
+        self.mode = mode
+        mt = (ctypes.c_void_p * len(main_tails))(*main_tails)
+        st = (ctypes.c_void_p * len(side_tails))(*side_tails)
+        h = ctypes.c_void_p()
+        counts = (ctypes.c_int * len(self.FIELDS))()
+        fw = fault_word().data_ptr()
+        L.call("avc_graph_split", ctypes.c_void_p(raw_graph), mt, len(main_tails), st, len(side_tails),
+               int(max_segments), int(mode), ctypes.c_void_p(fw), ctypes.byref(h), counts)
+        self.handle = h
+        self.counts = dict(zip(self.FIELDS, tuple(counts)))
+
+    def launch(self, main_raw, side_raw):
+        L.call("avc_graph_launch2", self.handle, main_raw, side_raw)
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            try:
+                L.lib().avc_graph_split_destroy(self.handle)
+            except Exception:
+                pass
+            self.handle = None

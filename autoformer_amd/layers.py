@@ -171,8 +171,22 @@ class _Side:
 def join_side() -> None:
     side = _SINK["side"]
     if side is not None:
+        if _SINK.get("tails") == []:
+            # a capture that TrainStep splits into main / side graph segments (graph.hip): each
+            # stream's capture dependencies at the join
+            _SINK["tails"] = [K.capture_deps(K.stream()), K.capture_deps(side.cuda_stream)]
         stream_wait(K.stream(), ev_record(side.cuda_stream))
     _SINK["keep"].clear()
+
+
+def record_join_tails(on: bool):
+    """Arm (on) / take (off: returns [main tails, side tails] or None) the capture dependencies
+    that join_side() records while a graph capture is running."""
+    if on:
+        _SINK["tails"] = []
+        return None
+    t = _SINK.pop("tails", None)
+    return t if t else None
 
 
 def _grad_of(p):
@@ -212,6 +226,10 @@ class PackCache:
         self.used = True
         if ops is not None:
             self.ops = ops
+        if _FROZEN[0] and self.ops is not None and self.val is not None:
+            # graph capture (TrainStep.capture): the captured step rewrites this pack in place
+            # after its optimizer step (repack_in_place), so the forward just reads the buffers
+            return self.val
         key = _pack_key(params)
         if key != self.key:
             pend, self.pending = self.pending, None
@@ -226,6 +244,57 @@ class PackCache:
                 _PLAN.append(weakref.ref(self))
             self.params, self.build = params, build
         return self.val
+
+
+_FROZEN = [False]  # set while a step is captured: packs with in-place ops are not rebuilt by get()
+
+
+def freeze_packs(on: bool) -> None:
+    _FROZEN[0] = bool(on)
+    if on:
+        for ref in _PLAN:
+            c = ref()
+            if c is not None:
+                c.pending = None  # a prefetched copy would replace val; the frozen val is rewritten instead
+
+
+def plan_caches(pred=None):
+    """Live caches of the prefetch plan (first-use order) with a built value, filtered by pred."""
+    out = []
+    for ref in _PLAN:
+        c = ref()
+        if c is not None and c.val is not None and (pred is None or pred(c)):
+            out.append(c)
+    return out
+
+
+def repack_in_place(caches, group):
+    """Rewrite the packs of `caches` in place on the current stream from the current parameters:
+    one batched avc_pack_batch launch over the caches that describe their packs (PackCache.ops);
+    the others are rebuilt (new tensors, get() rebuilds them inline, they are not frozen).  A
+    captured step calls this after its optimizer step, so the next replay's forward reads packs of
+    the updated weights with no pack kernels of its own (~55 small launches, ~0.35 ms of the C2
+    main stream, in one).  The op table is made on the first (eager) call: call it once outside
+    the capture with the same `group` first."""
+    batched = [c for c in caches if c.ops is not None]
+    # one launch per <= _PACK_MAX_OPS ops (the kernel keeps its op table in LDS)
+    chunks, cur, n = [], [], 0
+    for c in batched:
+        k = len(c.ops(c.val))
+        if cur and n + k > _PACK_MAX_OPS:
+            chunks.append(cur)
+            cur, n = [], 0
+        cur.append(c)
+        n += k
+    if cur:
+        chunks.append(cur)
+    for i, chunk in enumerate(chunks):
+        plan = _batch_plan(chunk, (group, i))
+        K.L.call("avc_pack_batch", plan["ops"].data_ptr(), plan["prefix"].data_ptr(), plan["n"], plan["total"],
+                 K.stream())
+
+
+_PACK_MAX_OPS = 128  # PACK_MAX_OPS of pack_batch_kernel (elem.hip)
 
 
 _BATCH = {}       # group index -> device op table of that group of packs

@@ -280,6 +280,13 @@ def _gelu_gemm(M, N, Kd, a, b, bias, dev, batch=1):
         U = torch.empty(batch * M, N, device=dev)
         K.gemm(M, N, Kd, a, b, U, bias=bias, batch=batch, c_batch_stride=M * N)
         return U, K.gelu_fwd_operand(U)
+    if not _vec(Kd, N, a, b):
+        # non-vectorisable operands take the generic kernel, which writes fp32 C only: U in fp32,
+        # V made from it by the GELU pass (a dim outside the MetaConv / MetaPool shapes)
+        U = torch.empty(batch * M, N, device=dev)
+        V = torch.empty(batch * M, N, device=dev, dtype=torch.bfloat16)
+        K.gemm(M, N, Kd, a, b, U, bias=bias, batch=batch, c_batch_stride=M * N, c_bf16=V, c_bf16_act=K.ACT_GELU)
+        return U, V
     # bf16 mode: U is only the backward's GELU' input -- stored in bf16 (avc_gemm_desc.c_pre_bf16)
     U = torch.empty(batch * M, N, device=dev, dtype=torch.bfloat16)
     V = torch.empty(batch * M, N, device=dev, dtype=torch.bfloat16)
@@ -307,8 +314,18 @@ def _dgelu_gemm(M, N, Kd, a, b, U, dev, batch=1, bias_grad=None):
         if not acc:
             out.zero_()
         kw = dict(col_sum=out, col_sum_n=n)
+    if not _vec(Kd, N, a, b):  # generic kernel: an fp32 C, the bf16 copy made from it by the GELU' pass
+        dU = torch.empty(batch * M, N, device=dev)
+        K.gemm(M, N, Kd, a, b, dU, batch=batch, c_batch_stride=M * N, c_bf16=d16, act_grad_of=U, **kw)
+        return d16
     K.gemm(M, N, Kd, a, b, d16, batch=batch, c_batch_stride=M * N, act_grad_of=U, **kw)
     return d16
+
+
+def _vec(Kd, N, *ops):
+    """Whether a product's operands are vectorisable (contiguous dims and row strides multiples of 4
+    elements: avc_gemm's fast / ring kernels, which write the bf16-only GELU outputs)."""
+    return Kd % 4 == 0 and N % 4 == 0 and all(o.ld % 4 == 0 and o.batch_stride % 4 == 0 for o in ops)
 
 
 class _MLPMixerFn(torch.autograd.Function):
@@ -420,7 +437,7 @@ class _MLPMixerFn(torch.autograd.Function):
         # bf16 mode: dZ1's row sums come out of the same pass -- dbb2[p] = sum over (b, d) of
         # dRT_b[d][p] = sum over b of rowsum(dZ1)[b*NP + p] -- and the padded bf16 dRT operand is
         # ONE transpose of dZ1 (no fp32 dRT, no colsum / pad passes over it)
-        tr = K.compute() == K.BF16 and D % 4 == 0
+        tr = K.compute() == K.BF16 and K.ln_vec(D)
         rs1 = torch.empty(B * NP, device=dev) if tr else None
         dZ1 = K.layer_norm_bwd(dY2, Z1, g2, m2, r2, dg2, db2n, accumulate=sink, residual=dZ2, row_sum=rs1)
         # token FF: Z1 = Z + (GELU(Y1^T W1^T + b1) W2^T + b2)^T   per utterance.  dRT_b = dZ1_b^T is

@@ -25,8 +25,8 @@ import torch
 
 from . import dist as D
 from . import kernels as K
-from .layers import (ev_record, join_side, on_stream, prefetch_packs, set_grad_sink, side_stream,
-                     stream_wait, weights_changed)
+from .layers import (ev_record, freeze_packs, join_side, on_stream, plan_caches, prefetch_packs, record_join_tails,
+                     repack_in_place, set_grad_sink, side_stream, stream_wait, weights_changed)
 
 
 def _load_state(model, path, device):
@@ -250,6 +250,8 @@ class TrainStep:
         self.opt = FusedAdam(self.flat, self.gflat, lr)
         self.graph_fb = None
         self.graph_f = None  # forward-only graph (capture(forward_only=True)); the backward stays eager
+        self.graph_split = None  # the captured step as main / side graph segments (capture(split=True))
+        self._graph_adam = False  # the optimizer step is inside the captured graph (world 1)
         self.world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
         self.loss = None
         # The decoder / postnet (/ discriminator) gradients are final once the backward reaches
@@ -266,6 +268,8 @@ class TrainStep:
             self.comm = torch.cuda.Stream()
         self._early = None
         self._early_adam = False
+        self._capturing = False
+        self._pack_groups = None  # (encoder-slice caches, decoder-slice caches) of a captured step
         # fault word (kernels.fault_word): read back asynchronously after every step into a
         # pinned word and checked at the next step, so a failed persistent recurrence raises
         # within one step without a host sync; check() is the synchronous form
@@ -289,6 +293,17 @@ class TrainStep:
         K.raise_on_fault(self._fault.item())
 
     def _decoder_done(self):
+        if self._capturing:
+            # captured step (world 1): the decoder-slice Adam and the in-place repack of the decoder's
+            # weight packs run on the weight-gradient stream, after the decoder's weight gradients
+            # queued there and beside the encoder backward
+            side = side_stream()
+            stream_wait(side.cuda_stream, ev_record())
+            with on_stream(side):
+                self.opt.step_slice(self.split, self.flat.numel(), advance=True, max_blocks=_SIDE_ADAM_BLOCKS)
+                repack_in_place(self._pack_groups[1], "graph_dec")
+            self._early_adam = True
+            return
         comm = self.comm.cuda_stream
         stream_wait(comm, ev_record())
         side = side_stream()
@@ -345,6 +360,17 @@ class TrainStep:
         return self._step(x, emb)
 
     def _step(self, x, emb):
+        if self.graph_split is not None:
+            # host-free step: the main chain and the weight-gradient branch replay as graph
+            # segments on their own streams (graph.hip); with world 1 the Adam step and the
+            # in-place weight repack are in the graph
+            self.graph_split.launch(K.stream(), side_stream().cuda_stream)
+            loss = self.loss
+            if not self._graph_adam:
+                self._finish()  # gradient average over ranks + Adam
+                repack_in_place(self._pack_groups[0] + self._pack_groups[1], "graph_all")
+            self._probe_fault()
+            return loss
         if self.graph_fb is not None:
             self.graph_fb.replay()
             loss = self.loss
@@ -376,9 +402,14 @@ class TrainStep:
         self._probe_fault()
         return loss
 
-    def capture(self, x, emb, warmup=2, forward_only=False):
+    def capture(self, x, emb, warmup=2, forward_only=False, split=None):
         """Capture zero_grad + forward + re-pass + losses + backward into one hipGraph
         (x, emb must stay the same tensors: the synthetic batch is resident in HBM).
+        split (default: on whenever the weight-gradient side stream exists): the captured graph is
+        rebuilt as main-stream / side-stream graph segments that replay concurrently (graph.hip,
+        avc_graph_split), so the weight-gradient branch overlaps the main chain as in the eager
+        step; with world 1 the Adam step is captured too (after the join), so a step is one
+        native call.
         forward_only: capture the forward + re-pass + losses only and keep their autograd graph;
         every step replays the forward (no host work for its ~half of the step's launches) and
         runs the backward eagerly over the retained graph, so the weight-gradient side stream
@@ -394,9 +425,8 @@ class TrainStep:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         weights_changed()  # the captured forward must contain the weight repacks
-        # One graph: the runtime executes it in one queue, so the weight-gradient branch captured
-        # from the side stream runs after the main chain instead of beside it (the
-        # round-3 main / side split replayed NaN from its second replay and was removed).
+        # split=False keeps ONE graph: the runtime executes it in one queue, so the weight-gradient
+        # branch captured from the side stream runs after the main chain instead of beside it
         g = torch.cuda.CUDAGraph()
         if forward_only:
             # the decoder hook (early decoder-slice Adam) is registered on the captured tensors and
@@ -412,6 +442,50 @@ class TrainStep:
             self.loss = loss
             self.graph_f = g
             self._gx, self._ge = x, emb
+            return
+        if split is None:
+            split = side_stream() is not None and os.environ.get("AVC_GRAPH_SPLIT", "1") != "0"
+        if split:
+            # Weight packs: the captured forward reads the pack buffers as they are (freeze_packs) and
+            # the graph rewrites them in place after its Adam step (repack_in_place: the decoder's
+            # on the side stream right after the decoder-slice Adam, the encoder's after the join),
+            # so a replay runs no per-pack kernels on the main chain.  Bring them up to date first.
+            bound = self.flat[self.split].data_ptr() if self.split is not None else None
+            dec = (lambda c: c.params[0].data_ptr() >= bound) if bound is not None else (lambda c: False)
+            self._pack_groups = (plan_caches(lambda c: not dec(c)), plan_caches(dec))
+            for caches, grp in ((self._pack_groups[0], "graph_enc"), (self._pack_groups[1], "graph_dec"),
+                                (self._pack_groups[0] + self._pack_groups[1], "graph_all")):
+                repack_in_place(caches, grp)  # eager: builds the op tables (and the current packs)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph(keep_graph=True)
+            record_join_tails(True)
+            freeze_packs(True)
+            adam = self.world == 1
+            overlap = adam and self.split is not None
+            self._capturing = overlap
+            try:
+                with torch.cuda.graph(g):
+                    self.loss = self._fwd_bwd(x, emb, overlap=overlap)
+                    if adam:
+                        if self._early_adam:
+                            self.opt.step_slice(0, self.split, advance=False)
+                            repack_in_place(self._pack_groups[0], "graph_enc")
+                        else:
+                            K.adam(self.flat, self.gflat, self.opt.m, self.opt.v, self.opt.lr, self.opt.betas[0],
+                                   self.opt.betas[1], self.opt.eps, self.opt.state)
+                            repack_in_place(self._pack_groups[0] + self._pack_groups[1], "graph_all")
+            finally:
+                self._capturing = False
+                self._early_adam = False
+                freeze_packs(False)
+                tails = record_join_tails(False)
+            weights_changed()  # eager steps after this rebuild the packs that are not rewritten in place
+            if not tails or not all(tails):
+                raise RuntimeError("TrainStep.capture: the step recorded no main / side join to split at")
+            self._tails = tails  # (tools/graph_split_probe.py re-splits the same capture)
+            self.graph_split = K.GraphSplit(g.raw_cuda_graph(), tails[0], tails[1])
+            self._graph_adam = adam
+            self.graph_fb = g  # keeps the captured graph and its memory pool alive
             return
         with torch.cuda.graph(g):
             self.loss = self._fwd_bwd(x, emb)

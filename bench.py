@@ -243,7 +243,10 @@ def main():
                     help="AutoVC + Discriminator two-model step (train_with_discriminator.py), T=176")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--graph", action="store_true",
-                    help="replay the fwd+bwd as one hipGraph (serialises the side-stream wgrad branch on ROCm 7)")
+                    help="replay the captured step as main / side graph segments (graph.hip): the whole step "
+                         "(fwd + re-pass + losses + bwd + Adam + weight repack) without host work per kernel")
+    ap.add_argument("--graph-one", action="store_true",
+                    help="replay the fwd+bwd as ONE hipGraph (the runtime serialises the side-stream branch)")
     ap.add_argument("--graph-fwd", action="store_true",
                     help="replay the forward + losses as a hipGraph, backward eager over the retained autograd graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -305,8 +308,8 @@ def main():
 
     for _ in range(args.warmup):
         trainer.step(x, e)
-    if args.graph or args.graph_fwd:
-        trainer.capture(x, e, forward_only=args.graph_fwd)
+    if args.graph or args.graph_fwd or args.graph_one:
+        trainer.capture(x, e, forward_only=args.graph_fwd, split=False if args.graph_one else None)
         trainer.step(x, e)
     torch.cuda.synchronize()
     if world > 1:
@@ -358,7 +361,8 @@ def main():
            "config": {"workload": f"{name} {step}, B={B}/GPU, T={T}, freq={freq}, dim_neck=44, dim_emb=256, "
                                   f"dim_pre=512",
                       "global_batch": B * world, "seq_len": T, "freq": freq, "parallelism": f"dp{world}",
-                      "graph": "fwd+bwd" if args.graph else ("fwd" if args.graph_fwd else False)},
+                      "graph": ("split" if args.graph else "one" if args.graph_one else
+                                "fwd" if args.graph_fwd else False)},
            "step_mfma_frac": round(value * fpf / (world * peak * 1e12), 5) if fpf else None,
            "final_loss": loss_v}
     if world > 1:

@@ -237,6 +237,45 @@ def test_mlp_mixer_vs_torch(B, L, ps, out):
         assert rel_inf(grads[n].cpu(), p.grad.cpu()) < 1e-4, n
 
 
+@pytest.mark.parametrize("comp,dim", [("fp32", 90), ("fp32", 516), ("bf16", 90), ("bf16", 516), ("bf16", 768)])
+def test_mlp_mixer_general_dim(comp, dim):
+    """A mixer dim outside the one-pass LayerNorm forms (D % 4 != 0, or D > 512: the reference
+    MetaDV's dim=768) takes the plain LayerNorm + add / convert passes, in both compute
+    modes, against plain PyTorch fp32."""
+    import autoformer_amd as A
+    from autoformer_amd import metaformer as MF
+    from autoformer_amd.factory.MLPMixer import MLPMixer
+
+    A.set_compute(comp)
+    torch.manual_seed(0)
+    B, L, ps, out = 2, 176, 16, 88
+    mix = MLPMixer(image_size=L, channels=1, patch_size=ps, dim=dim, depth=1, out_dim=out).to(DEV)
+    x = _t(B * L, L, seed=12).requires_grad_()
+    dy = _t(B * dim, out, seed=13)
+    y = MF.mlp_mixer(x, mix, B, L)
+    y.backward(dy)
+    torch.cuda.synchronize()
+    grads = {n: p.grad.clone() for n, p in mix.named_parameters()}
+    mix.zero_grad()
+    xr = x.detach().clone().requires_grad_()
+    yr = _torch_mixer(mix, _frames_to_bcl(xr, B, L).unsqueeze(1))  # (B, out, dim)
+    yr.transpose(1, 2).reshape(B * dim, out).backward(dy)
+    yr2 = yr.transpose(1, 2).reshape(B * dim, out).detach()
+    if comp == "fp32":
+        assert rel_inf(y.detach().cpu(), yr2.cpu()) < 1e-4
+        assert rel_inf(x.grad.cpu(), xr.grad.cpu()) < 1e-4
+        for n, p in mix.named_parameters():
+            assert rel_inf(grads[n].cpu(), p.grad.cpu()) < 1e-4, n
+    else:  # bf16 operands: relative Frobenius at bf16 rounding scale
+        def rel(a, b):
+            return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
+
+        assert rel(y.detach(), yr2) < 2e-2
+        assert rel(x.grad, xr.grad) < 3e-2
+        for n, p in mix.named_parameters():
+            assert rel(grads[n], p.grad) < 5e-2, n
+
+
 # ------------------------------------------------------------------------------------ models
 def _model(kind, comp="fp32"):
     import autoformer_amd as A

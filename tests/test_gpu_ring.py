@@ -225,3 +225,35 @@ def test_transposed_store(ring, B, D, NP, Kd):
     rt = (v.float() @ w.float().t() + bias).view(B, D, NP)
     ref = z + rt.transpose(1, 2).reshape(B * NP, D)
     assert _rel(z1, ref) < 1e-5
+
+
+def test_generic_gemm_fused_gelu_outputs():
+    """A non-vectorisable operand (odd row stride) sends the fused-GELU products to the generic kernel
+    (fp32 C only) + the GELU pass: with an fp32 C both bf16 outputs are made from it --
+    GELU(C) and, when asked for, the bf16 pre-activation slot (c_pre_bf16); a bf16-only output has
+    no fp32 C to make them from and must be refused with an error, not a fault."""
+    from autoformer_amd import _lib
+    from autoformer_amd import kernels as K
+
+    torch.manual_seed(11)
+    M, N, Kd = 256, 320, 96
+    abuf = torch.randn(M, Kd + 1, device=DEV).bfloat16()  # ld = 97: rows not 16-B aligned
+    b = (torch.randn(N, Kd, device=DEV) * 0.1).bfloat16()
+    u = torch.empty(M, N, device=DEV)
+    v = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    K.gemm(M, N, Kd, K.operand(abuf, Kd + 1), K.operand(b, Kd), u, c_bf16=v, c_bf16_act=K.ACT_GELU)
+    torch.cuda.synchronize()
+    ref = abuf[:, :Kd].float() @ b.float().t()
+    assert _rel(u, ref) < 1e-5
+    assert _rel(v.float(), torch.nn.functional.gelu(ref.double())) < 1e-2
+    # the bf16 pre-activation form: pre-activation and activation in bf16 only, no fp32 C
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="bf16-only output"):
+        K.gemm(M, N, Kd, K.operand(abuf, Kd + 1), K.operand(b, Kd), pre, c_bf16=v, c_bf16_act=K.ACT_GELU)
+    # a bf16-only GELU-backward output
+    x = torch.randn(M, N, device=DEV)
+    d = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="bf16-only output"):
+        K.gemm(M, N, Kd, K.operand(abuf, Kd + 1), K.operand(b, Kd), d, act_grad_of=x)
+    torch.cuda.synchronize()
+    assert _lib.lib().avc_abi_version() == _lib.ABI_VERSION

@@ -1,10 +1,12 @@
-# kernel-trace profile of the C2 bench -> gpurun_out/$1 (CSV), plus step breakdown / gaps
+# kernel-trace profile of the C2 bench -> gpurun_out/$1 (CSV), plus step breakdown / gaps;
+# further arguments go to bench.py (e.g. --graph)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/$1
+shift
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-kernel-timing > $OUT/prof.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-kernel-timing "$@" > $OUT/prof.log 2>&1 || exit 1
 CSV=$(find $OUT/prof -name "run_kernel_trace.csv" | head -1)
 python3 $R/tools/step_breakdown.py $CSV 25 > $OUT/breakdown.txt
 Q=$(python3 - "$CSV" <<'PY'
