@@ -93,10 +93,16 @@ struct RingLoader {
   bool rok[NI];
   int kc;              // this lane's K offset inside the 64-wide slot
   int ld, pad, t_in, chans;
+  const void* zp;      // the 16-B zero granule, held in VGPRs (see init)
 
   __device__ __forceinline__ void init(const OpDev& o, int row0, int bz) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     base = reinterpret_cast<const bf16*>(o.ptr) + (long long)bz * o.bstride;
+    // the zero granule's address pinned in a VGPR pair once: referenced per glds, hipcc had
+    // re-materialised it from the GOT (s_getpc + s_load + lgkmcnt(0)) before every fill under
+    // SGPR pressure
+    zp = (const void*)g_zero16_rg;
+    asm volatile("" : "+v"(zp));
     kc = 8 * ((lane & 7) ^ ((4 * (w & 1) + (lane >> 4)) & 7));
     ld = (int)o.ld;
     pad = o.pad;
@@ -138,7 +144,7 @@ struct RingLoader {
       } else {
         off = roff[i] + k;
       }
-      glds16(ok ? (const void*)(base + off) : (const void*)g_zero16_rg, lds + (8 * i + w) * 8 * RROW);
+      glds16(ok ? (const void*)(base + off) : zp, lds + (8 * i + w) * 8 * RROW);
     }
   }
 };
@@ -900,16 +906,19 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
   // [qi KiB, +1 KiB) = rows 16*qi + (lane>>2) of 64 B, 16-B slot lane&3 holding the global chunk
   // (lane&3) ^ ((row>>1)&3)
   const int b0 = (int)fdiv((uint32_t)m0, A.tdiv);  // utterance of the tile's first row
+  // a lane whose row is padding reads the 16-B zero granule at every stage (stride 0): no select
+  // in the issue loop, and the granule's address pinned in VGPRs (hipcc had re-loaded it from the
+  // GOT, s_load + lgkmcnt(0), before every fill: 30 per stage loop)
+  const bf16* zp = reinterpret_cast<const bf16*>(g_zero16_rg);
+  asm volatile("" : "+v"(zp));
   const bf16* src[CV_LW];
-  bool sok[CV_LW];
   long long sst[CV_LW];  // elements per stage
 #pragma unroll
   for (int i = 0; i < CV_LW; ++i) {
     const int qi = i * 8 + wid;
     const int lrow = lane >> 2, slot = lane & 3;
-    src[i] = reinterpret_cast<const bf16*>(g_zero16_rg);
-    sok[i] = false;
-    sst[i] = CV_CBK;
+    src[i] = zp;
+    sst[i] = 0;
     if (qi < CV_AI) {
       const int hr = 16 * qi + lrow;  // halo row
       const int f = m0 - pad + hr;
@@ -917,7 +926,7 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
       if (ALIGNED && ok) ok = (int)fdiv((uint32_t)f, A.tdiv) == b0;
       if (ok) {
         src[i] = xa + (long long)f * A.ld + 8 * (slot ^ ((hr >> 1) & 3));
-        sok[i] = true;
+        sst[i] = CV_CBK;
       }
     } else if (qi < CV_TOT) {
       const int wr = 16 * (qi - CV_AI) + lrow;  // weight row = tap * 128 + column
@@ -928,8 +937,8 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
           sst[i] = (long long)CV_TAPS * g.N * CV_CBK;
         } else {
           src[i] = wb + (long long)n * Bo.ld + (long long)tap * chans + 8 * (slot ^ ((wr >> 1) & 3));
+          sst[i] = CV_CBK;
         }
-        sok[i] = true;
       }
     }
   }
@@ -938,8 +947,7 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
 #pragma unroll
     for (int i = 0; i < CV_LW; ++i) {
       const int qi = i * 8 + wid;
-      if (qi < CV_TOT)
-        glds16(sok[i] ? (const void*)(src[i] + cs * sst[i]) : (const void*)g_zero16_rg, base + qi * 1024);
+      if (qi < CV_TOT) glds16(src[i] + cs * sst[i], base + qi * 1024);
     }
   };
 
@@ -1040,6 +1048,219 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
   ring_epilogue<CV_TM, CV_TN>(g, acc, m0, n0, 0, 0, smem_raw);
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same conv tile, warp-specialised: waves 0-3 are MMA waves (2 x 2, 64 x 64 each: 8 fragment
+// reads per 16 MFMAs, half the LDS reads per FLOP of the 64 x 32 wave tile -- whose 6 reads per 8
+// MFMAs kept the LDS array ~75 % busy and the MFMA pipe at 0.28 with the loads removed,
+// profiles/r4_pmc_conv_ring.txt), waves 4-7 are loader waves that issue every LDS-DMA fill of the
+// ring (49 per stage: 13 / 12 / 12 / 12), so the MMA waves' instruction streams hold only fragment
+// reads and MFMAs.  One MMA wave and one loader wave per SIMD.  The stage protocol is the 8-wave
+// kernel's: loaders wait for their own fills of stage cs (counted vmcnt), one raw barrier per stage,
+// after which the slot of stage cs-1 is free (the MMA waves drained its reads before the barrier)
+// and receives stage cs+2.  After the K loop the MMA waves' 64 x 64 accumulators are redistributed
+// through LDS into the 2 x 4 layout of ring_epilogue, which all 8 waves then run unchanged.
+constexpr int CW_LI = (CV_TOT + 3) / 4;  // 13: fills per stage of loader wave 4 (12 for waves 5-7)
+
+template <bool ALIGNED>
+__global__ void __launch_bounds__(RNT, 2) conv_ring_ws_kernel(GemmArgs g, int gm) {
+  constexpr int P = CV_NST - 1;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool loader = wid >= 4;
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int nN = (g.N + CV_TN - 1) / CV_TN, nM = (g.M + CV_TM - 1) / CV_TM;
+  const int grp = lid / (gm * nN), fm = grp * gm, gsz = min(nM - fm, gm);
+  const int wi = lid - grp * gm * nN;
+  const int mt = fm + wi % gsz, nt = wi / gsz;
+  const int m0 = mt * CV_TM, n0 = nt * CV_TN;
+
+  const OpDev& A = g.a;
+  const OpDev& Bo = g.b;
+  const int pad = A.pad, T = A.t_out, chans = A.chans;
+  const int nst = chans / CV_CBK;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (loader) {
+    // ---- loader waves: fill qi = i*4 + lw writes stage bytes [qi KiB, +1 KiB), rows 16*qi + (lane>>2)
+    // of 64 B, 16-B slot lane&3 holding global chunk (lane&3) ^ ((row>>1)&3) (the 8-wave layout)
+    const int lw = wid - 4;
+    const bool full = lw < CV_TOT % 4;  // issues CW_LI fills per stage, else CW_LI - 1
+    const bf16* xa = reinterpret_cast<const bf16*>(A.ptr);
+    const bf16* wb = reinterpret_cast<const bf16*>(Bo.ptr);
+    const int b0 = (int)fdiv((uint32_t)m0, A.tdiv);
+    const bf16* zp = reinterpret_cast<const bf16*>(g_zero16_rg);
+    asm volatile("" : "+v"(zp));
+    const bf16* src[CW_LI];
+    int sst[CW_LI];
+#pragma unroll
+    for (int i = 0; i < CW_LI; ++i) {
+      const int qi = i * 4 + lw;
+      const int lrow = lane >> 2, slot = lane & 3;
+      src[i] = zp;
+      sst[i] = 0;
+      if (qi < CV_AI) {
+        const int hr = 16 * qi + lrow;
+        const int f = m0 - pad + hr;
+        bool ok = hr < CV_TM + CV_TAPS - 1 && f >= 0 && f < g.M;
+        if (ALIGNED && ok) ok = (int)fdiv((uint32_t)f, A.tdiv) == b0;
+        if (ok) {
+          src[i] = xa + (long long)f * A.ld + 8 * (slot ^ ((hr >> 1) & 3));
+          sst[i] = CV_CBK;
+        }
+      } else if (qi < CV_TOT) {
+        const int wr = 16 * (qi - CV_AI) + lrow;
+        const int tap = wr / CV_TN, n = n0 + (wr - tap * CV_TN);
+        if (n < g.N) {
+          src[i] = wb + (long long)n * Bo.ld + (long long)tap * chans + 8 * (slot ^ ((wr >> 1) & 3));
+          sst[i] = CV_CBK;
+        }
+      }
+    }
+    auto issue = [&](int stg, int cs) {
+      char* base = smem_raw + stg * CV_STAGE;
+#pragma unroll
+      for (int i = 0; i < CW_LI; ++i) {
+        const int qi = i * 4 + lw;
+        if (qi < CV_TOT) glds16(src[i] + (long long)cs * sst[i], base + qi * 1024);
+      }
+    };
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+      if (p < nst) issue(p, p);
+    for (int cs = 0; cs < nst; ++cs) {
+      if (cs + 1 < nst) {
+        if (full) wait_vm<CW_LI>();
+        else wait_vm<CW_LI - 1>();
+      } else {
+        wait_vm<0>();
+      }
+      raw_barrier();
+      if (cs + P < nst) issue((cs + P) % CV_NST, cs + P);
+    }
+  } else {
+    // ---- MMA waves (wm, wn) = (wid >> 1, wid & 1): rows wm*64 .. +64, columns wn*64 .. +64
+    const int wm = wid >> 1, wn = wid & 1;
+    const int frow = lane & 15, kq = lane >> 4;
+    int aaddr[CV_TAPS];
+#pragma unroll
+    for (int k = 0; k < CV_TAPS; ++k) {
+      const int r = wm * 64 + frow + k;
+      aaddr[k] = r * 64 + 16 * (kq ^ ((r >> 1) & 3));
+    }
+    const int baddr = CV_ABYTES + (wn * 64 + frow) * 64 + 16 * (kq ^ ((frow >> 1) & 3));
+    unsigned vmask = 0xFFFFFFFFu;
+    if (!ALIGNED) {
+      vmask = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = min(m0 + wm * 64 + i * 16 + frow, g.M - 1);
+        const int b = (int)fdiv((uint32_t)m, A.tdiv);
+        const int t = m - b * T;
+#pragma unroll
+        for (int k = 0; k < CV_TAPS; ++k) {
+          const int t2 = t + k - pad;
+          if (t2 >= 0 && t2 < T) vmask |= 1u << (i * 8 + k);
+        }
+      }
+    }
+    for (int cs = 0; cs < nst; ++cs) {
+      raw_barrier();
+      const unsigned st = lds_addr(smem_raw + (cs % CV_NST) * CV_STAGE);
+      bf16x8 af[2][4], bfr[2][4];
+      auto read_tap = [&](auto kc, int slot) {
+        constexpr int k = decltype(kc)::value;
+        const unsigned a0 = st + aaddr[k], b0 = st + baddr;
+        af[slot][0] = ds_read16<0>(a0);
+        af[slot][1] = ds_read16<1024>(a0);
+        af[slot][2] = ds_read16<2048>(a0);
+        af[slot][3] = ds_read16<3072>(a0);
+        bfr[slot][0] = ds_read16<(k * CV_TN) * 64>(b0);
+        bfr[slot][1] = ds_read16<(k * CV_TN + 16) * 64>(b0);
+        bfr[slot][2] = ds_read16<(k * CV_TN + 32) * 64>(b0);
+        bfr[slot][3] = ds_read16<(k * CV_TN + 48) * 64>(b0);
+      };
+      auto mfma_tap = [&](auto kc, int slot) {
+        constexpr int k = decltype(kc)::value;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bf16x8 av = (ALIGNED || ((vmask >> (i * 8 + k)) & 1u)) ? af[slot][i] : bf16x8{};
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bfr[slot][j], acc[i][j], 0, 0, 0);
+        }
+      };
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      using I2 = std::integral_constant<int, 2>;
+      using I3 = std::integral_constant<int, 3>;
+      using I4 = std::integral_constant<int, 4>;
+      // tap k+1's eight reads in flight during tap k's sixteen MFMAs
+      read_tap(I0{}, 0);
+      read_tap(I1{}, 1);
+      wait_lgkm<8>();
+      mfma_tap(I0{}, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      read_tap(I2{}, 0);
+      wait_lgkm<8>();
+      mfma_tap(I1{}, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      read_tap(I3{}, 1);
+      wait_lgkm<8>();
+      mfma_tap(I2{}, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      read_tap(I4{}, 0);
+      wait_lgkm<8>();
+      mfma_tap(I3{}, 1);
+      wait_lgkm<0>();
+      mfma_tap(I4{}, 0);
+    }
+  }
+  // ---- redistribution into the 2 x 4 layout: MMA wave w's block (i, j) -> LDS [w][i][j][lane] (16 B)
+  __syncthreads();  // every wave is past the K loop (the stages are free)
+  f32x4* red = reinterpret_cast<f32x4*>(smem_raw);
+  if (!loader) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[((wid * 4 + i) * 4 + j) * 64 + lane] = acc[i][j];
+  }
+  __syncthreads();
+  // epilogue wave w' = (wm', wn') = (wid >> 2, wid & 3): rows wm'*64, columns wn'*32 = MMA wave
+  // (wm', wn' >> 1), its blocks j = 2 (wn' & 1) + j'
+  f32x4 acc2[4][2];
+  {
+    const int mw = (wid >> 2) * 2 + ((wid & 3) >> 1), jo = 2 * (wid & 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc2[i][j] = red[((mw * 4 + i) * 4 + jo + j) * 64 + lane];
+  }
+  __syncthreads();  // the epilogue reuses the LDS
+  ring_epilogue<CV_TM, CV_TN>(g, acc2, m0, n0, 0, 0, smem_raw);
+}
+
+template <bool ALIGNED>
+void launch_conv_ws(const GemmArgs& g, int gm, hipStream_t s) {
+  const size_t lds = std::max((size_t)CV_NST * CV_STAGE, ring_epi_lds<CV_TM, CV_TN>());
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_ws_kernel<ALIGNED>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const int nb = ((g.M + CV_TM - 1) / CV_TM) * ((g.N + CV_TN - 1) / CV_TN);
+  conv_ring_ws_kernel<ALIGNED><<<nb, RNT, lds, s>>>(g, gm);
+}
+
 template <bool ALIGNED, int ABL = 0>
 void launch_conv(const GemmArgs& g, int gm, hipStream_t s) {
   const size_t lds = std::max((size_t)CV_NST * CV_STAGE, ring_epi_lds<CV_TM, CV_TN>());
@@ -1069,6 +1290,7 @@ struct RingCfg {
   int mode = -1;  // -1 auto, 0 off, 1 forced
   int bm = 0, bn = 0, nst = 0, gm = 8, win = 2;
   int abl = 0;  // timing ablations of the halo conv (win 3 / 4 through avc_gemm_set_ring)
+  int ws = 0;   // the warp-specialised halo conv (AVC_CONV_WS=1, or win 6 through avc_gemm_set_ring)
 };
 RingCfg init_cfg() {
   RingCfg r;
@@ -1085,6 +1307,7 @@ RingCfg init_cfg() {
     if (n >= 4 && a3 > 0) r.gm = a3;
   }
   if (const char* e = getenv("AVC_RING_WIN")) r.win = atoi(e);
+  if (const char* e = getenv("AVC_CONV_WS")) r.ws = atoi(e);
   return r;
 }
 RingCfg g_ring = init_cfg();
@@ -1111,7 +1334,10 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
     if (c.abl == 1) launch_conv<true, 1>(g, c.gm, s);
     else if (c.abl == 2) launch_conv<true, 2>(g, c.gm, s);
     else if (c.abl == 3) launch_conv<true, 3>(g, c.gm, s);
-    else if (a.t_out % CV_TM == 0) launch_conv<true>(g, c.gm, s);
+    else if (c.ws) {
+      if (a.t_out % CV_TM == 0) launch_conv_ws<true>(g, c.gm, s);
+      else launch_conv_ws<false>(g, c.gm, s);
+    } else if (a.t_out % CV_TM == 0) launch_conv<true>(g, c.gm, s);
     else launch_conv<false>(g, c.gm, s);
     return true;
   }
@@ -1187,6 +1413,10 @@ extern "C" int avc_gemm_set_ring(int mode, int bm, int bn, int nst, int gm, int 
   avcg::g_ring.nst = nst;
   if (gm > 0) avcg::g_ring.gm = gm;
   avcg::g_ring.win = win >= 3 ? 2 : win;
-  avcg::g_ring.abl = win >= 3 ? win - 2 : 0;  // 3: loads only, 4: reads + MFMAs only, 5: contiguous weight pieces
+  // 3: loads only, 4: reads + MFMAs only, 5: contiguous weight pieces (timing ablations);
+  // 6: the warp-specialised halo conv, 2: the 8-wave one
+  avcg::g_ring.abl = (win >= 3 && win <= 5) ? win - 2 : 0;
+  if (win == 6) avcg::g_ring.ws = 1;
+  else if (win == 2) avcg::g_ring.ws = 0;
   return 0;
 }

@@ -66,7 +66,9 @@ CONFIGS = [("old", (0, 0, 0, 0, 0, 1)), ("auto", (-1, 0, 0, 0, 8, 1)), ("halo", 
            ("auto-gm4", (-1, 0, 0, 0, 4, 1)), ("auto-gm16", (-1, 0, 0, 0, 16, 1)),
            # timing ablations of the halo conv (wrong results): its loads alone / its reads + MFMAs alone
            ("halo-loads", (-1, 0, 0, 0, 8, 3)), ("halo-math", (-1, 0, 0, 0, 8, 4)),
-           ("halo-contig", (-1, 0, 0, 0, 8, 5))]
+           ("halo-contig", (-1, 0, 0, 0, 8, 5)),
+           # the warp-specialised halo conv (4 MMA waves of 64 x 64 + 4 loader waves)
+           ("halo-ws", (-1, 0, 0, 0, 8, 6))]
 
 
 def main():
