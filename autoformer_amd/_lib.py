@@ -108,8 +108,7 @@ _SIGS = {
     "avc_event_record": (c_int, [c_void_p, c_void_p]),
     "avc_stream_wait_event": (c_int, [c_void_p, c_void_p]),
     "avc_capture_deps": (c_int, [c_void_p, c_void_p, c_int]),
-    "avc_graph_split": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
-                                 c_void_p]),
+    "avc_graph_split": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "avc_graph_launch2": (c_int, [c_void_p, c_void_p, c_void_p]),
     "avc_graph_split_destroy": (c_int, [c_void_p]),
     "avc_conv_pack_slice": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

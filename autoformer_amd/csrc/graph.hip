@@ -1,32 +1,32 @@
-// graph.hip — the captured training step replayed as main-stream and side-stream graph segments,
-// plus the host-side event helpers of the eager step's stream plumbing.
+// graph.hip — the captured training step replayed as main-stream and side-stream graphs, plus the
+// host-side event helpers of the eager step's stream plumbing.
 //
 // The eager step queues ~290 kernels from Python (5.1 of a 5.9 ms C2 step is host enqueue,
 // profiles/r4_host_time.txt).  One captured hipGraph removes the host cost, but the HIP runtime
 // executes a graph's nodes in one queue, so the weight-gradient branch captured from the side
-// stream (3.5 ms of GEMMs that overlap the main stream's recurrences in eager mode) runs serially
-// with the main chain (7.0 vs 5.8 ms, profiles/r4_graph_queues.txt).  Event record / wait NODES
-// inside two separately launched graphs do not order them at node granularity on ROCm 7 (the
-// side graph's waits resolved only when the whole main graph had finished, round 3), so the
-// cross-stream edges are cut BETWEEN launches:
+// stream (2-3.5 ms of GEMMs that overlap the main stream's recurrences in eager mode) runs serially
+// with the main chain (7.0 vs 5.8 ms, profiles/r4_graph_queues.txt).
 //
 // avc_graph_split takes the single graph PyTorch captured (main stream + the side stream forked
-// from it, joined at the end) and rebuilds it as segments:
+// from it, joined at the end) and rebuilds it:
 //   * main nodes = every ancestor of the main stream's capture tail at the join (the main chain
 //     never waits for the side stream before the join; a side -> main edge is refused);
 //   * post nodes = the main-stream nodes captured after the join (the optimizer step): one more
 //     graph, launched on the main stream after it has waited for the side stream;
 //   * side nodes = ancestors of the side stream's tail that are not main nodes;
-//   * the main chain is cut after every main node a side node waits for ("source"; at most
-//     max_segments segments, cuts spread evenly over the sources beyond that); side segment k
-//     holds the side nodes whose latest main ancestor lies in main segment k.
-// avc_graph_launch2 launches, per segment, main graph k on the main stream, records event k there,
-// makes the side stream wait for it and launches side graph k; the main stream finally waits for
-// the side stream.  That is mode 0; each boundary cost 15-100 us of main-stream idle time (22
-// boundaries: a C2 replay at 6.2 ms against 5.8 eager).  Mode 1 (the default) keeps ONE main graph
-// and ONE side graph and orders them on the device instead: a tiny signal kernel after every
-// source on the main chain publishes the replay number, a tiny wait kernel on the side chain polls
-// for it (build_flags below).
+//   * "sources" = the main nodes a side node waits for directly.
+// mode 0 (default): the main chain cut into <= max_segments graphs after sources (spread evenly),
+//   side segment k = the side nodes whose latest main ancestor lies in main segment k; a replay
+//   launches main segment k, records an event, makes the side stream wait for it and launches side
+//   segment k.  Each boundary costs 15-100 us of main-stream idle time (C2: 6.1-6.2 ms against 5.8
+//   eager, profiles/r5_graph_modes.txt).
+// mode 1: ONE main graph with an event-record node after every source; each side segment is
+//   launched behind a host-side wait for its source's event.  Correct, but the record nodes complete
+//   only near the end of the main graph, so the side branch runs after it (6.14 ms).
+// Measured and removed (profiles/r5_graph_modes.txt): ordering the side graph on the device -- tiny
+// signal kernels on the main chain with polling wait kernels, or hipStreamWaitValue32, on the side
+// -- deadlocks against the decoder's full-chip persistent recurrences (one 8-wave, 250-VGPR
+// workgroup per CU: a waiting wave on any CU keeps one of them from starting).
 //
 // Nodes are re-created from their parameters into fresh graphs (never cloned-and-pruned:
 // destroying the unwanted nodes of a hipGraphClone left the surviving graphs reading stale kernel
@@ -40,6 +40,17 @@
 #include <vector>
 
 #include "common.h"
+
+// cross-stream events of one device: no system-scope fence on record / wait (the default flushes and
+// invalidates the L2s for host visibility; the consumers here are kernels on the same GPU, for which
+// the device-scope release is enough).  AVC_EV_SYSFENCE=1 restores the default (A/B).
+static unsigned ev_flags() {
+  static const unsigned f = (getenv("AVC_EV_SYSFENCE") && getenv("AVC_EV_SYSFENCE")[0] == '1')
+                                ? hipEventDisableTiming
+                                : hipEventDisableTiming | hipEventDisableSystemFence;
+  return f;
+}
+#define kEvFlags ev_flags()
 
 #define GCHK(x, what)                                                    \
   do {                                                                   \
@@ -62,41 +73,6 @@ __global__ void graph_fill_bytes_kernel(unsigned char* p, long long n, unsigned 
     p[i] = v;
 }
 
-// Device-flag form (mode 1): the main chain is ONE graph that publishes its progress, the side
-// branch ONE graph that waits for it on the device.  sync[0] / sync[1] = replay counters of the main
-// / side graph (each graph's first node increments its own, so they agree within a replay: the main
-// stream waits for the side at the end of every replay); sync[2 + f] = the main counter as of the
-// last time source f completed.  Every sync word is read and written agent-coherently (sc1: the
-// per-XCD L2s are not coherent with each other); a kernel boundary on the producing queue has
-// already made the source's outputs visible (end-of-kernel release) before its signal runs.
-__device__ __forceinline__ unsigned ld_u32_sc1(const unsigned* p) {
-  return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_u32_sc1(unsigned* p, unsigned v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__global__ void graph_epoch_kernel(unsigned* ctr) {
-  if (threadIdx.x == 0) st_u32_sc1(ctr, ld_u32_sc1(ctr) + 1u);
-}
-__global__ void graph_signal_kernel(const unsigned* main_ctr, unsigned* flag) {
-  if (threadIdx.x == 0) st_u32_sc1(flag, ld_u32_sc1(main_ctr));
-}
-// spins (s_sleep between polls) until the source's flag reaches this replay; bounded: after ~2 s of
-// the 100 MHz REALTIME clock it raises fault bit 1 (value 2) and lets the side branch run on, so a
-// stalled main chain shows at the next fault check instead of hanging the queue
-__global__ void graph_wait_kernel(const unsigned* side_ctr, const unsigned* flag, unsigned* fault) {
-  if (threadIdx.x != 0) return;
-  const unsigned want = ld_u32_sc1(side_ctr);
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (ld_u32_sc1(flag) != want) {
-    __builtin_amdgcn_s_sleep(2);
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
-      if (fault) atomicOr(fault, 2u);
-      break;
-    }
-  }
-}
-
 struct Split {
   std::vector<hipGraph_t> gm, gs;
   std::vector<hipGraphExec_t> em, es;  // es[k] null when segment k has no side nodes
@@ -104,10 +80,12 @@ struct Split {
   hipEvent_t join = nullptr;
   hipGraph_t gp = nullptr;  // the main-stream nodes after the join (optimizer step), if any
   hipGraphExec_t ep = nullptr;
-  unsigned* sync = nullptr;  // mode 1: replay counters + source flags (device)
+  int mode = 0;
+  std::vector<int> wait_src;       // mode 1: the source side segment k waits for (-1: none)
+  std::vector<hipEvent_t> src_ev;  // mode 1: one event per source, recorded by a node of the main graph
   // census: main nodes before the join, side nodes, main -> side edges, segments, kernel nodes,
   // memset nodes (rebuilt as kernels), memcpy nodes, empty nodes, main nodes after the join,
-  // wait nodes and signal nodes (mode 1)
+  // event-record nodes (mode 1)
   int counts[AVC_GRAPH_COUNTS] = {};
 };
 
@@ -141,7 +119,7 @@ void destroy(Split* s) {
   if (s->join) (void)hipEventDestroy(s->join);
   if (s->ep) (void)hipGraphExecDestroy(s->ep);
   if (s->gp) (void)hipGraphDestroy(s->gp);
-  if (s->sync) (void)hipFree(s->sync);
+  for (hipEvent_t e : s->src_ev) if (e) (void)hipEventDestroy(e);
   delete s;
 }
 
@@ -167,16 +145,6 @@ int fill_node(hipGraph_t dst, const hipMemsetParams& p, const hipGraphNode_t* d,
     k.kernelParams = args_b;
   }
   GCHK(hipGraphAddKernelNode(out, dst, d, nd, &k), "avc_graph_split (memset as kernel)");
-  return 0;
-}
-
-int tiny_node(hipGraph_t dst, void* fn, void** args, const std::vector<hipGraphNode_t>& deps, hipGraphNode_t* out) {
-  hipKernelNodeParams k = {};
-  k.blockDim = dim3(64);
-  k.gridDim = dim3(1);
-  k.func = fn;
-  k.kernelParams = args;
-  GCHK(hipGraphAddKernelNode(out, dst, deps.empty() ? nullptr : deps.data(), deps.size(), &k), "avc_graph_split");
   return 0;
 }
 
@@ -231,94 +199,31 @@ int sub_graph(const std::vector<hipGraphNode_t>& nodes, const std::vector<int>& 
   return 0;
 }
 
-// Mode 1: one main graph (a replay-counter node first, a signal node after every source on the
-// chain) and one side graph (its counter node first, a wait node before the first side node that
-// needs each source).  pos / need / sources as in build(); side nodes are a chain (one captured
-// stream), so a wait for the latest source a node needs covers every earlier one.
-int build_flags(const std::vector<hipGraphNode_t>& nodes, const std::vector<int>& order,
-                const std::vector<std::vector<int>>& pr, const std::vector<int>& pos, const std::vector<char>& post,
-                const std::vector<int>& sources, unsigned* fault, Split* s) {
-  const size_t nn = nodes.size();
-  const int ns = (int)sources.size();
-  GCHK(hipMalloc(&s->sync, sizeof(unsigned) * (2 + ns)), "avc_graph_split");
-  GCHK(hipMemset(s->sync, 0, sizeof(unsigned) * (2 + ns)), "avc_graph_split");
-  GCHK(hipDeviceSynchronize(), "avc_graph_split");
-  unsigned* main_ctr = s->sync;
-  unsigned* side_ctr = s->sync + 1;
-  std::vector<int> flag_of(nn, -1);  // main node -> its source flag
-  for (size_t i = 0; i < nn; ++i)
-    if (pos[i] >= 0) {
-      auto it = std::lower_bound(sources.begin(), sources.end(), pos[i]);
-      if (it != sources.end() && *it == pos[i]) flag_of[i] = (int)(it - sources.begin());
-    }
-  s->gm.assign(1, nullptr);
-  s->gs.assign(1, nullptr);
-  s->em.assign(1, nullptr);
-  s->es.assign(1, nullptr);
-  s->ev.assign(1, nullptr);
-  std::vector<hipGraphNode_t> made(nn, nullptr), deps;
-  // main graph
+// ONE graph of every main node (s->gm[0] / em[0]) with an event record node after every source (on the
+// chain: the source's successors depend on it); flag_of[main node] = its source index
+int main_record_graph(const std::vector<hipGraphNode_t>& nodes, const std::vector<int>& order,
+                      const std::vector<std::vector<int>>& pr, const std::vector<int>& pos,
+                      const std::vector<int>& flag_of, Split* s) {
+  std::vector<hipGraphNode_t> made(nodes.size(), nullptr), deps;
   GCHK(hipGraphCreate(&s->gm[0], 0), "avc_graph_split");
-  hipGraphNode_t mroot;
-  {
-    void* a[1] = {&main_ctr};
-    if (tiny_node(s->gm[0], reinterpret_cast<void*>(&graph_epoch_kernel), a, {}, &mroot)) return -1;
-  }
   for (int i : order) {
     if (pos[i] < 0) continue;
     deps.clear();
     for (int j : pr[i]) deps.push_back(made[j]);
-    if (deps.empty()) deps.push_back(mroot);
     if (copy_node(s->gm[0], nodes[i], deps, &made[i])) return -1;
     if (flag_of[i] >= 0) {
-      // the chain continues through the signal: successors of the source depend on it
-      unsigned* flag = s->sync + 2 + flag_of[i];
-      void* a[2] = {&main_ctr, &flag};
-      hipGraphNode_t sig;
-      if (tiny_node(s->gm[0], reinterpret_cast<void*>(&graph_signal_kernel), a, {made[i]}, &sig)) return -1;
-      made[i] = sig;
-      ++s->counts[10];
+      hipGraphNode_t ev;
+      GCHK(hipGraphAddEventRecordNode(&ev, s->gm[0], &made[i], 1, s->src_ev[flag_of[i]]), "avc_graph_split");
+      made[i] = ev;
+      ++s->counts[9];
     }
   }
   GCHK(hipGraphInstantiate(&s->em[0], s->gm[0], nullptr, nullptr, 0), "avc_graph_split");
-  // side graph
-  GCHK(hipGraphCreate(&s->gs[0], 0), "avc_graph_split");
-  hipGraphNode_t sroot;
-  {
-    void* a[1] = {&side_ctr};
-    if (tiny_node(s->gs[0], reinterpret_cast<void*>(&graph_epoch_kernel), a, {}, &sroot)) return -1;
-  }
-  std::vector<hipGraphNode_t> wait_node(ns, nullptr);
-  int waited = -1;  // the latest source waited for so far
-  hipGraphNode_t last_wait = nullptr;
-  for (int i : order) {
-    if (pos[i] >= 0 || post[i]) continue;
-    deps.clear();
-    int f = -1;
-    for (int j : pr[i]) {
-      if (pos[j] >= 0) f = std::max(f, flag_of[j]);
-      else deps.push_back(made[j]);
-    }
-    if (f > waited) {
-      std::vector<hipGraphNode_t> wd = deps;
-      if (wd.empty()) wd.push_back(last_wait ? last_wait : sroot);
-      const unsigned* flag = s->sync + 2 + f;
-      void* a[3] = {&side_ctr, &flag, &fault};
-      if (tiny_node(s->gs[0], reinterpret_cast<void*>(&graph_wait_kernel), a, wd, &wait_node[f])) return -1;
-      last_wait = wait_node[f];
-      waited = f;
-      ++s->counts[9];
-    }
-    if (f >= 0 || deps.empty()) deps.push_back(last_wait ? last_wait : sroot);
-    if (copy_node(s->gs[0], nodes[i], deps, &made[i])) return -1;
-  }
-  GCHK(hipGraphInstantiate(&s->es[0], s->gs[0], nullptr, nullptr, 0), "avc_graph_split");
-  s->counts[3] = 1;
   return 0;
 }
 
 int build(hipGraph_t g, hipGraphNode_t const* main_tails, int n_main, hipGraphNode_t const* side_tails, int n_side,
-          int max_seg, int mode, unsigned* fault, Split* s) {
+          int max_seg, int mode, Split* s) {
   size_t nn = 0;
   GCHK(hipGraphGetNodes(g, nullptr, &nn), "avc_graph_split");
   std::vector<hipGraphNode_t> nodes(nn);
@@ -400,25 +305,37 @@ int build(hipGraph_t g, hipGraphNode_t const* main_tails, int n_main, hipGraphNo
   s->counts[0] = (int)mainset.size();
   s->counts[1] = (int)sideset.size();
   s->counts[8] = npost;
-  if (mode == 1) {
-    if (build_flags(nodes, order, pr, pos, post, sources, fault, s)) return -1;
-    if (npost && sub_graph(nodes, order, pr, post, &s->gp, &s->ep)) return -1;
-    GCHK(hipEventCreateWithFlags(&s->join, hipEventDisableTiming), "avc_graph_split");
-    return 0;
-  }
-  // cuts: after every source (at most max_seg - 1 of them, spread evenly); the last segment ends the graph
+  // cuts: after every source (at most max_seg - 1 of them, spread evenly; mode 1: all of them); the
+  // last segment ends the graph
   std::vector<int> cuts;
-  const int ns = (int)sources.size(), K = std::min(max_seg - 1, ns);
+  const int ns = (int)sources.size(), K = mode == 1 ? ns : std::min(max_seg - 1, ns);
   for (int k = 1; k <= K; ++k) cuts.push_back(sources[(long long)k * ns / K - 1]);
   cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
   if (cuts.empty() || cuts.back() != nm - 1) cuts.push_back(nm - 1);
   const int S = (int)cuts.size();
   auto seg_of = [&](int mp) { return (int)(std::lower_bound(cuts.begin(), cuts.end(), mp) - cuts.begin()); };
-  s->gm.assign(S, nullptr);
+  const int SM = mode == 1 ? 1 : S;  // mode 1: ONE main graph, S side segments
+  s->gm.assign(SM, nullptr);
+  s->em.assign(SM, nullptr);
   s->gs.assign(S, nullptr);
-  s->em.assign(S, nullptr);
   s->es.assign(S, nullptr);
   s->ev.assign(S, nullptr);
+  if (mode == 1) {
+    std::vector<int> src_of(nn, -1);  // main node -> its source index
+    for (size_t i = 0; i < nn; ++i)
+      if (pos[i] >= 0) {
+        auto it = std::lower_bound(sources.begin(), sources.end(), pos[i]);
+        if (it != sources.end() && *it == pos[i]) src_of[i] = (int)(it - sources.begin());
+      }
+    s->src_ev.assign(sources.size(), nullptr);
+    for (auto& e : s->src_ev) GCHK(hipEventCreateWithFlags(&e, kEvFlags), "avc_graph_split");
+    if (main_record_graph(nodes, order, pr, pos, src_of, s)) return -1;
+    s->wait_src.assign(S, -1);
+    for (int k = 0; k < S; ++k) {
+      auto it = std::lower_bound(sources.begin(), sources.end(), cuts[k]);
+      if (it != sources.end() && *it == cuts[k]) s->wait_src[k] = (int)(it - sources.begin());
+    }
+  }
   for (int k = 0; k < S; ++k) {
     std::vector<char> km(nn, 0), ks(nn, 0);
     bool any_side = false;
@@ -427,14 +344,14 @@ int build(hipGraph_t g, hipGraphNode_t const* main_tails, int n_main, hipGraphNo
       if (pos[i] >= 0) km[i] = seg_of(pos[i]) == k;
       else if (seg_of(std::max(need[i], 0)) == k) ks[i] = any_side = true;
     }
-    if (sub_graph(nodes, order, pr, km, &s->gm[k], &s->em[k])) return -1;
+    if (mode == 0 && sub_graph(nodes, order, pr, km, &s->gm[k], &s->em[k])) return -1;
     if (any_side) {
       if (sub_graph(nodes, order, pr, ks, &s->gs[k], &s->es[k])) return -1;
-      GCHK(hipEventCreateWithFlags(&s->ev[k], hipEventDisableTiming), "avc_graph_split");
+      GCHK(hipEventCreateWithFlags(&s->ev[k], kEvFlags), "avc_graph_split");
     }
   }
   if (npost && sub_graph(nodes, order, pr, post, &s->gp, &s->ep)) return -1;
-  GCHK(hipEventCreateWithFlags(&s->join, hipEventDisableTiming), "avc_graph_split");
+  GCHK(hipEventCreateWithFlags(&s->join, kEvFlags), "avc_graph_split");
   s->counts[3] = S;
   return 0;
 }
@@ -456,14 +373,14 @@ extern "C" int avc_capture_deps(void* stream, void** out, int max_out) {
 }
 
 extern "C" int avc_graph_split(void* graph, void* const* main_tails, int n_main, void* const* side_tails, int n_side,
-                               int max_segments, int mode, void* fault_word, void** handle, int* counts) {
+                               int max_segments, int mode, void** handle, int* counts) {
   AVC_CHECK_ARG(graph && main_tails && side_tails && n_main > 0 && n_side > 0 && handle && max_segments >= 1 &&
                     (mode == 0 || mode == 1),
                 "avc_graph_split: bad args");
   Split* s = new Split;
+  s->mode = mode;
   if (build(reinterpret_cast<hipGraph_t>(graph), reinterpret_cast<hipGraphNode_t const*>(main_tails), n_main,
-            reinterpret_cast<hipGraphNode_t const*>(side_tails), n_side, max_segments, mode,
-            static_cast<unsigned*>(fault_word), s)) {
+            reinterpret_cast<hipGraphNode_t const*>(side_tails), n_side, max_segments, mode, s)) {
     destroy(s);
     return -1;
   }
@@ -480,23 +397,21 @@ extern "C" int avc_graph_launch2(void* handle, void* main_stream, void* side_str
   // the side stream starts after everything queued on the main stream before the replay
   GCHK(hipEventRecord(s->join, m), "avc_graph_launch2");
   GCHK(hipStreamWaitEvent(sd, s->join, 0), "avc_graph_launch2");
-  if (s->sync) {
-    // mode 1: the side graph's wait nodes order it after the main graph's signals on the device
+  if (s->mode == 1) {
     GCHK(hipGraphLaunch(s->em[0], m), "avc_graph_launch2");
-    // diagnostic (AVC_GRAPH_M1_SERIAL=1): the side graph starts after the whole main graph
-    static const bool serial = getenv("AVC_GRAPH_M1_SERIAL") && getenv("AVC_GRAPH_M1_SERIAL")[0] == '1';
-    if (serial) {
-      GCHK(hipEventRecord(s->join, m), "avc_graph_launch2");
-      GCHK(hipStreamWaitEvent(sd, s->join, 0), "avc_graph_launch2");
-    }
-    GCHK(hipGraphLaunch(s->es[0], sd), "avc_graph_launch2");
-  }
-  for (size_t k = 0; k < s->em.size() && !s->sync; ++k) {
-    GCHK(hipGraphLaunch(s->em[k], m), "avc_graph_launch2");
-    if (s->es[k]) {
-      GCHK(hipEventRecord(s->ev[k], m), "avc_graph_launch2");
-      GCHK(hipStreamWaitEvent(sd, s->ev[k], 0), "avc_graph_launch2");
+    for (size_t k = 0; k < s->es.size(); ++k) {
+      if (!s->es[k]) continue;
+      if (s->wait_src[k] >= 0) GCHK(hipStreamWaitEvent(sd, s->src_ev[s->wait_src[k]], 0), "avc_graph_launch2");
       GCHK(hipGraphLaunch(s->es[k], sd), "avc_graph_launch2");
+    }
+  } else {
+    for (size_t k = 0; k < s->em.size(); ++k) {
+      GCHK(hipGraphLaunch(s->em[k], m), "avc_graph_launch2");
+      if (s->es[k]) {
+        GCHK(hipEventRecord(s->ev[k], m), "avc_graph_launch2");
+        GCHK(hipStreamWaitEvent(sd, s->ev[k], 0), "avc_graph_launch2");
+        GCHK(hipGraphLaunch(s->es[k], sd), "avc_graph_launch2");
+      }
     }
   }
   GCHK(hipEventRecord(s->join, sd), "avc_graph_launch2");
@@ -518,7 +433,7 @@ extern "C" int avc_graph_split_destroy(void* handle) {
 extern "C" int avc_event_create(void** out) {
   AVC_CHECK_ARG(out, "avc_event_create: null");
   hipEvent_t e = nullptr;
-  GCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming), "avc_event_create");
+  GCHK(hipEventCreateWithFlags(&e, kEvFlags), "avc_event_create");
   *out = e;
   return 0;
 }

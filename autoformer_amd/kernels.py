@@ -361,9 +361,7 @@ class DeviceFault(RuntimeError):
 
 
 FAULT_BITS = {1: "persistent LSTM recurrence spin timeout (a workgroup of the grid was not resident or stalled; "
-                 "the step's outputs are invalid)",
-              2: "graph replay: a side-stream wait for the main stream timed out (the step's weight gradients are "
-                 "invalid)"}
+                 "the step's outputs are invalid)"}
 
 
 def raise_on_fault(value):
@@ -937,29 +935,29 @@ def capture_deps(stream_raw):
 
 
 class GraphSplit:
-    """A captured step rebuilt as main-stream / side-stream graph segments (graph.hip): the
-    weight-gradient branch replays beside the main chain instead of after it."""
+    """A captured step rebuilt as main-stream / side-stream graphs (graph.hip): the weight-gradient
+    branch replays beside the main chain instead of after it."""
 
     FIELDS = ("main_nodes", "side_nodes", "cross_edges", "segments", "kernel_nodes", "memset_nodes",
-              "memcpy_nodes", "empty_nodes", "post_nodes", "wait_nodes", "signal_nodes")
+              "memcpy_nodes", "empty_nodes", "post_nodes", "record_nodes")
 
     def __init__(self, raw_graph, main_tails, side_tails, max_segments=None, mode=None):
-        """mode 1 (default): one main and one side graph ordered on the device by signal / wait
-        kernel nodes; mode 0: up to max_segments main / side graph pairs ordered by events."""
+        """mode 0 (default): up to max_segments main / side graph pairs ordered by events between
+        launches; mode 1: one main graph with event-record nodes, side segments behind waits on them
+        (profiles/r5_graph_modes.txt)."""
         import ctypes
 
         if max_segments is None:
-            max_segments = int(os.environ.get("AVC_GRAPH_SEGMENTS", "64"))
+            max_segments = int(os.environ.get("AVC_GRAPH_SEGMENTS", "8"))
         if mode is None:
-            mode = int(os.environ.get("AVC_GRAPH_MODE", "1"))
+            mode = int(os.environ.get("AVC_GRAPH_MODE", "0"))
         self.mode = mode
         mt = (ctypes.c_void_p * len(main_tails))(*main_tails)
         st = (ctypes.c_void_p * len(side_tails))(*side_tails)
         h = ctypes.c_void_p()
         counts = (ctypes.c_int * len(self.FIELDS))()
-        fw = fault_word().data_ptr()
         L.call("avc_graph_split", ctypes.c_void_p(raw_graph), mt, len(main_tails), st, len(side_tails),
-               int(max_segments), int(mode), ctypes.c_void_p(fw), ctypes.byref(h), counts)
+               int(max_segments), int(mode), ctypes.byref(h), counts)
         self.handle = h
         self.counts = dict(zip(self.FIELDS, tuple(counts)))
 

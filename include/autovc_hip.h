@@ -535,24 +535,23 @@ int avc_event_record(void* ev, void* stream);
 int avc_stream_wait_event(void* stream, void* ev);
 
 /* The captured training step (TrainStep.capture of train.py:82-99) replayed as main-stream and
- * side-stream graph segments that run concurrently (graph.hip): the HIP runtime executes one graph
- * in one queue, which serialises the weight-gradient branch.
+ * side-stream graphs (graph.hip): the HIP runtime executes one graph in one queue, which serialises
+ * the weight-gradient branch.
  * avc_capture_deps: the capture dependencies (graph node handles) of a capturing stream, at most
  *   max_out; returns their count (negative on error).
  * avc_graph_split: rebuilds `graph` (a hipGraph_t captured over the main stream with the side
  *   stream forked from it and joined at the end) from the two streams' tails at the join, plus one
  *   graph of the main-stream nodes captured after the join (the optimizer step).  mode 0: <=
- *   max_segments main / side graph pairs ordered by events between launches; mode 1: one main
- *   graph and one side graph ordered on the device (signal / wait kernel nodes; a wait that
- *   spins ~2 s raises bit 1 of fault_word, a device u32, nullable).  *handle for
+ *   max_segments main / side graph pairs ordered by events between launches; mode 1: one main graph
+ *   with event-record nodes, side segments behind host-side waits on them.  *handle for
  *   avc_graph_launch2.  counts[AVC_GRAPH_COUNTS] (optional): main nodes before the join, side
  *   nodes, main -> side edges, segments, kernel, memset (rebuilt as kernels), memcpy and empty
- *   nodes, main nodes after the join, wait nodes, signal nodes.
+ *   nodes, main nodes after the join, event-record nodes.
  * avc_graph_launch2: one replay on (main, side); the main stream waits for the side at the end. */
-#define AVC_GRAPH_COUNTS 11
+#define AVC_GRAPH_COUNTS 10
 int avc_capture_deps(void* stream, void** out, int max_out);
 int avc_graph_split(void* graph, void* const* main_tails, int n_main, void* const* side_tails, int n_side,
-                    int max_segments, int mode, void* fault_word, void** handle, int* counts);
+                    int max_segments, int mode, void** handle, int* counts);
 int avc_graph_launch2(void* handle, void* main_stream, void* side_stream);
 int avc_graph_split_destroy(void* handle);
 

@@ -47,7 +47,7 @@ def _compare(comp, B, T, freq, gtol, steps=4, forward_only=False, split=None, lr
             assert tb.graph_split is not None, "the default capture is the segmented main / side replay"
             c = tb.graph_split.counts
             assert c["side_nodes"] > 0 and c["cross_edges"] > 0, c
-            assert c["segments"] > 1 or c["wait_nodes"] > 1, c
+            assert c["segments"] > 1, c
         for i, (x, e) in enumerate(batches):
             la = ta.step(x, e)
             ga = ta.gflat.clone()

@@ -35,8 +35,9 @@ torch.cuda.synchronize()
 print(f"eager: {(time.perf_counter() - t0) / steps * 1e3:.3f} ms/step")
 ts.capture(x, e)
 raw = ts.graph_fb.raw_cuda_graph()
-# CONFIGS: "1" = device-flag form; "0:<cap>" = event-ordered segments with at most <cap> segments
-for cfg in os.environ.get("CONFIGS", "1,0:8,0:64,1").split(","):
+# CONFIGS: "0:<cap>" = event-ordered segments with at most <cap> segments, "1" = one main graph with
+# event-record nodes (graph.hip modes)
+for cfg in os.environ.get("CONFIGS", "0:4,0:8,0:64,1").split(","):
     mode, _, cap = cfg.partition(":")
     cap = int(cap or 64)
     ts.graph_split = K.GraphSplit(raw, ts._tails[0], ts._tails[1], max_segments=cap, mode=int(mode))
