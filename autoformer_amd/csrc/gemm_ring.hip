@@ -876,7 +876,9 @@ __device__ __forceinline__ void wait_cv(bool full) {
 // ABL (timing diagnostics only, wrong results; tools/ring_ab.py): 1 = no fragment reads / MFMAs
 // (the ring's loads alone), 2 = no loads after the prologue (fragment reads + MFMAs alone),
 // 3 = the weight slices fetched as 1-KiB contiguous pieces ([Ci/32][K][Co][32] addressing applied
-// to the [Co][K][Ci] buffer: the timing of a repacked weight layout)
+// to the [Co][K][Ci] buffer: the timing of a repacked weight layout), 4 = MFMAs alone (no loads
+// after the prologue, fragments read in the first stage only), 5 = fragment reads alone (no loads
+// after the prologue, no MFMAs), 6 = production with s_setprio(1) around every MFMA group
 template <bool ALIGNED, int ABL = 0>
 __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
   constexpr int MI = 4, NJ = 2, P = CV_NST - 1;
@@ -983,6 +985,7 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][MI], bfr[2][NJ];
 
 #pragma unroll
   for (int p = 0; p < P; ++p)
@@ -993,11 +996,11 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
     if (ahead >= 1) wait_cv<1>(full);
     else wait_vm<0>();
     raw_barrier();
-    if (ABL != 2 && cs + P < nst) issue((cs + P) % CV_NST, cs + P);
+    if ((ABL == 0 || ABL == 3 || ABL == 6) && cs + P < nst) issue((cs + P) % CV_NST, cs + P);
     if (ABL == 1) continue;
     const unsigned st = lds_addr(smem_raw + (cs % CV_NST) * CV_STAGE);
-    bf16x8 af[2][MI], bfr[2][NJ];
     auto read_tap = [&](auto kc, int slot) {
+      if (ABL == 4 && cs > 0) return;
       constexpr int k = decltype(kc)::value;
       const unsigned a0 = st + aaddr[k], b0 = st + baddr;
       af[slot][0] = ds_read16<0>(a0);
@@ -1009,12 +1012,21 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
     };
     auto mfma_tap = [&](auto kc, int slot) {
       constexpr int k = decltype(kc)::value;
+      if (ABL == 5) {  // keep the reads live without MFMAs
+#pragma unroll
+        for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(af[slot][i]));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) asm volatile("" ::"v"(bfr[slot][j]));
+        return;
+      }
+      if (ABL == 6) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const bf16x8 av = (ALIGNED || ((vmask >> (i * 8 + k)) & 1u)) ? af[slot][i] : bf16x8{};
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bfr[slot][j], acc[i][j], 0, 0, 0);
       }
+      if (ABL == 6) __builtin_amdgcn_s_setprio(0);
     };
     // Software pipeline with inline-asm fragment reads and counted waits: tap k+1's six reads are
     // in flight while tap k's eight MFMAs issue (the wave waits only for tap k's reads).  Left to
@@ -1334,6 +1346,9 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
     if (c.abl == 1) launch_conv<true, 1>(g, c.gm, s);
     else if (c.abl == 2) launch_conv<true, 2>(g, c.gm, s);
     else if (c.abl == 3) launch_conv<true, 3>(g, c.gm, s);
+    else if (c.abl == 4) launch_conv<true, 4>(g, c.gm, s);
+    else if (c.abl == 5) launch_conv<true, 5>(g, c.gm, s);
+    else if (c.abl == 6) launch_conv<true, 6>(g, c.gm, s);
     else if (c.ws) {
       if (a.t_out % CV_TM == 0) launch_conv_ws<true>(g, c.gm, s);
       else launch_conv_ws<false>(g, c.gm, s);
@@ -1413,9 +1428,10 @@ extern "C" int avc_gemm_set_ring(int mode, int bm, int bn, int nst, int gm, int 
   avcg::g_ring.nst = nst;
   if (gm > 0) avcg::g_ring.gm = gm;
   avcg::g_ring.win = win >= 3 ? 2 : win;
-  // 3: loads only, 4: reads + MFMAs only, 5: contiguous weight pieces (timing ablations);
-  // 6: the warp-specialised halo conv, 2: the 8-wave one
-  avcg::g_ring.abl = (win >= 3 && win <= 5) ? win - 2 : 0;
+  // 3: loads only, 4: reads + MFMAs only, 5: contiguous weight pieces, 7: MFMAs only, 8: reads only,
+  // 9: s_setprio around the MFMA groups (timing ablations); 6: the warp-specialised halo conv, 2: the
+  // 8-wave one
+  avcg::g_ring.abl = (win >= 3 && win <= 5) ? win - 2 : (win >= 7 && win <= 9) ? win - 3 : 0;
   if (win == 6) avcg::g_ring.ws = 1;
   else if (win == 2) avcg::g_ring.ws = 0;
   return 0;

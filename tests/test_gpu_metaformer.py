@@ -322,9 +322,10 @@ def test_metaformer_fp32_matches_reference_goldens(golden, kind):
 
     # MetaPool's heads are chaotic at B=2: 1 ulp of noise on the norm outputs of the fp32 oracle
     # itself moves them by up to 2.8 % of the tensor scale (ReLU decisions near 0 flip; MetaConv:
-    # 0.6 %), and the GPU's different summation order everywhere by up to 6 % (decoder.output_conv_2
-    # BN, profiles/r4_metaformer_flip_spread.txt): heads at 1e-1 there, norms unchanged at 1e-2
-    bad = grad_mismatches(m, g, tol=1e-2, head_tol=5e-2 if kind == "metaconv" else 1e-1, bn_fed_bias=zero_grad)
+    # 0.6 %; profiles/r4_metaformer_flip_spread.txt).  The GPU's worst head sits at 2.9 % (round 5,
+    # profiles/r5_metapool_heads.txt; decoder.output_conv_2.1.bias, 6 % in round 4, at 0.8 %): both
+    # families are held to the 5e-2 head bar, norms to 1e-2
+    bad = grad_mismatches(m, g, tol=1e-2, head_tol=5e-2, bn_fed_bias=zero_grad)
     assert not bad, sorted(bad.items())
     assert not bn_state_mismatches(m, g)
 

@@ -102,11 +102,11 @@ def test_autovc_three_adam_steps_match_reference_solver(golden, fname):
 @pytest.mark.parametrize("fname", ["autovc_T128.npz", "autovc_T176.npz"])
 def test_autovc_bf16_loose(golden, fname):
     """The bf16 production model against the reference's fp32 goldens (B=2), held to the SURVEY
-    §8(c) bf16 bar of 5e-2 as a relative Frobenius norm.  No max-norm bar at B=2: there it is set
-    by one element and moves by +-1.3e-2 when only the fp32 summation order of one layer changes
-    (tools/bf16_margin.py); the max-norm bars are measured at the bench batch against the oracle
-    (test_autovc_bf16_b64_vs_oracle).  Every production op is held to 1e-2 against fp64 on its own
-    inputs by tests/test_gpu_capture.py."""
+    §8(c) bf16 bar of 5e-2 as a relative Frobenius norm, and in the max norm to twice the
+    reference's own bf16 drift on these inputs (the oracle under bf16 autocast against fp32,
+    tools/bf16_drift.py, profiles/r5_bf16_drift_oracle.txt: mel_psnt rel-inf 4.95e-2 at T=128,
+    4.19e-2 at T=176, mel 1.88e-2 / 1.68e-2 -- at B=2 one element sets it).  Every production op is
+    held to 1e-2 against fp64 on its own inputs by tests/test_gpu_capture.py."""
     g = golden(fname)
     m = _model(int(g["freq"]), "bf16")
     x, e = torch.from_numpy(g["x"]).to(DEV), torch.from_numpy(g["emb"]).to(DEV)
@@ -115,8 +115,10 @@ def test_autovc_bf16_loose(golden, fname):
     torch.cuda.synchronize()
     got, ref = outs[1].detach().cpu().double().numpy().ravel(), g["mel_psnt"].astype(np.float64).ravel()
     assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 5e-2
+    assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-1
     mel = outs[0].detach().cpu().double().numpy().ravel()
     assert np.linalg.norm(mel - g["mel"].ravel()) / np.linalg.norm(g["mel"]) < 5e-2
+    assert np.abs(mel - g["mel"].ravel()).max() / np.abs(g["mel"]).max() < 4e-2
     np.testing.assert_allclose([l.item() for l in losses], g["losses"], rtol=5e-2)
     for p in m.parameters():
         assert torch.isfinite(p.grad).all()
@@ -144,13 +146,14 @@ def _rel_frob(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
 
 
-# bf16 bars at the bench configuration (B=64, T=128, freq=16), measured in round 4 against the fp32
-# oracle on identical weights and inputs with ~1.6-1.8x headroom (profiles/r4_bf16_b64_vs_oracle.txt:
-# mel_psnt rel-Frobenius 1.81e-2 / rel-inf 2.51e-2, mel 8.8e-3 / 1.07e-2, losses 2.8e-5, worst
-# parameter gradient 0.138 (encoder conv BN bias, through the code loss and the BiLSTM), gradients
-# that are analytically zero 2.1e-5 of the largest gradient norm)
-B64_BARS = {"mel_psnt_frob": 3e-2, "mel_psnt_inf": 4e-2, "mel_frob": 1.5e-2, "mel_inf": 2e-2, "loss_rtol": 1e-3,
-            "grad_frob": 0.25, "zero_grad_abs": 1e-4}
+# bf16 bars at the bench configuration (B=64, T=128, freq=16): the REFERENCE computation's own bf16
+# drift x 1.5 -- the CPU oracle under bf16 autocast (recurrences with bf16 operands and fp32 state, as
+# on the GPU) against the same oracle in fp32, on these inputs (tools/bf16_drift.py,
+# profiles/r5_bf16_drift_oracle.txt: mel_psnt rel-Frobenius 1.85e-2 / rel-inf 2.31e-2, mel 9.1e-3 /
+# 9.6e-3, losses 1.7e-4, worst parameter gradient 0.132 (encoder conv BN bias, as on the GPU: 0.138),
+# analytically-zero gradients 6.4e-4 of the largest norm)
+B64_BARS = {"mel_psnt_frob": 2.8e-2, "mel_psnt_inf": 3.5e-2, "mel_frob": 1.4e-2, "mel_inf": 1.5e-2, "loss_rtol": 3e-4,
+            "grad_frob": 0.2, "zero_grad_abs": 1e-3}
 
 
 @pytest.mark.timeout(900)

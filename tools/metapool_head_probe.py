@@ -51,11 +51,15 @@ def run(label):
         rows.append((err / scale, abs(got.norm().item() - ref_n) / max(ref_n, 1e-12), name))
     rows.sort(reverse=True)
     print(f"== {label}: losses {[round(v.item(), 7) for v in (l1, l2, l3)]} golden {g['losses'].tolist()}")
+    for r in rows:
+        if "output_conv_2.1.bias" in r[2]:
+            print(f"   head {r[0]:.4f}  norm {r[1]:.2e}  {r[2]}  (VERDICT r4 item 3)")
     for r in rows[:6]:
         print(f"   head {r[0]:.4f}  norm {r[1]:.2e}  {r[2]}")
 
 
-run("default")
+for rep in range(int(os.environ.get("REPS", "1"))):
+    run(f"default #{rep}")
 orig = K.ln_vec
 K.ln_vec = lambda D: False
 try:

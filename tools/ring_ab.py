@@ -38,6 +38,9 @@ def shapes(only):
     if only == "conv":
         return [("conv 8192x512x2560 w5", 8192, 512, 2560, dict(win=(64, 128, 512)), False),
                 ("xproj 8192x4096x512", 8192, 4096, 512, {}, False)]
+    if only == "convk":  # the halo conv at 4 / 8 / 16 / 32 channel stages: per-stage slope vs fixed cost
+        return [(f"conv 8192x512x{5 * ci} w5", 8192, 512, 5 * ci, dict(win=(64, 128, ci)), False)
+                for ci in (128, 256, 512, 1024)]
     if only in (None, "c2"):
         out += [
             ("conv 8192x512x2560 w5", 8192, 512, 2560, dict(win=(64, 128, 512)), False),
@@ -68,7 +71,9 @@ CONFIGS = [("old", (0, 0, 0, 0, 0, 1)), ("auto", (-1, 0, 0, 0, 8, 1)), ("halo", 
            ("halo-loads", (-1, 0, 0, 0, 8, 3)), ("halo-math", (-1, 0, 0, 0, 8, 4)),
            ("halo-contig", (-1, 0, 0, 0, 8, 5)),
            # the warp-specialised halo conv (4 MMA waves of 64 x 64 + 4 loader waves)
-           ("halo-ws", (-1, 0, 0, 0, 8, 6))]
+           ("halo-ws", (-1, 0, 0, 0, 8, 6)),
+           ("halo-mfma", (-1, 0, 0, 0, 8, 7)), ("halo-reads", (-1, 0, 0, 0, 8, 8)),
+           ("halo-prio", (-1, 0, 0, 0, 8, 9))]
 
 
 def main():
