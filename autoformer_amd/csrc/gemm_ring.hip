@@ -408,11 +408,152 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
   }
 }
 
+// BatchNorm BACKWARD reduction of the layer that produced this data-gradient GEMM's output
+// (avc_gemm_bnb on the halo conv ring: C = dL/da of the producing conv + BN + act layer, whose
+// stored conv output y, statistics and affine parameters come in g.bnb_*): per column of this
+// 128 x 128 tile, over its rows, (sum dz, sum dz*yhat, sum yhat) with yhat = (y - mean)*rstd and
+// dz = C * act'(yhat*gamma + beta) -- C rounded to bf16 first when only the bf16 C is stored (the
+// value the apply pass reads) -- into the 128-row-tile partials; the last-arriving row tile of the
+// column tile reduces them into the apply constants coef[6][N] and the parameter gradients
+// (avcbn::bwd_finalize_store).  The separate reduce + finalize launches of the BN backward
+// (bn.hip) are gone.  y (bf16, the bf16 step's conv output) is staged through LDS as 16-B rows.
+// y prefetch of the tile: 4 x 16 B per thread, issued at kernel start into registers so it lands
+// under the K loop (a load-then-store loop in the epilogue had serialised four HBM round trips)
+constexpr int BNB_YQ = 128 * 16 / RNT;  // 16-B chunks per thread (128 rows x 16 chunks of 8 bf16)
+__device__ __forceinline__ void ring_bnb_prefetch(const GemmArgs& g, int m0, int n0, u32x4 (&yv)[BNB_YQ]) {
+  const bf16* yb = static_cast<const bf16*>(g.bnb_y);
+  // unconditional loads at clamped addresses (N % 8 == 0 on this path), zeroed after: a load inside
+  // a bounds branch is waited for at the branch join
+#pragma unroll
+  for (int k = 0; k < BNB_YQ; ++k) {
+    const int q = threadIdx.x + k * RNT, r = q >> 4, cc = q & 15;
+    const int row = m0 + r, col = n0 + cc * 8;
+    yv[k] = *reinterpret_cast<const u32x4*>(yb + (long long)min(row, g.M - 1) * g.ldc + min(col, g.N - 8));
+  }
+  // (rows / columns outside the tensor are zeroed where the values are written to LDS: a select
+  // here would be a use, and hipcc would wait for the loads right away)
+}
+
+__device__ __forceinline__ bool ring_bnb_epilogue(const GemmArgs& g, f32x4 (&acc)[4][2], int m0, int n0,
+                                                  char* smem_raw, const u32x4* yv) {
+  constexpr int BN_ = 128, NJ = 2, FGR = 4;  // 512 threads = 128 columns x 4 row groups (finalize)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int rbase = m0 + wm * 64 + 4 * (lane >> 4);
+  const int cbase = n0 + wn * 32 + (lane & 15);
+  const avcbn::BwdFin& f = g.bnb_fin;
+  float* red = reinterpret_cast<float*>(smem_raw);  // [3][2 wm][BN_] / the finalize's [3][FGR][BN_]
+  constexpr int YP = 2 * BN_ + 16;                  // LDS row pitch of the staged y tile (bytes)
+  char* ys = smem_raw + 8192;
+  unsigned* flag = reinterpret_cast<unsigned*>(ys + 128 * YP);
+  __syncthreads();  // the K loop's fragment reads are done with the LDS
+#pragma unroll
+  for (int k = 0; k < BNB_YQ; ++k) {
+    const int q = tid + k * RNT, r = q >> 4, cc = q & 15;
+    const bool in = m0 + r < g.M && n0 + cc * 8 < g.N;
+    *reinterpret_cast<u32x4*>(ys + r * YP + cc * 16) = in ? yv[k] : u32x4{0u, 0u, 0u, 0u};
+  }
+  __syncthreads();
+  const bool round16 = g.c == nullptr;
+  float s0[NJ], s1[NJ], s2[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int col = cbase + j * 16;
+    const bool cv = col < g.N;
+    const float mu = cv ? f.mean[col] : 0.f, rs = cv ? f.rstd[col] : 0.f;
+    const float gm = cv && f.gamma ? f.gamma[col] : 1.f, bt = cv && f.beta ? f.beta[col] : 0.f;
+    float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = rbase + i * 16 + e;
+        if (!cv || row >= g.M) continue;
+        float v = acc[i][j][e];
+        if (round16) v = (float)(bf16)v;
+        const float yf = __builtin_bit_cast(
+            float, (unsigned)*reinterpret_cast<const unsigned short*>(ys + (row - m0) * YP + (col - n0) * 2) << 16);
+        const float yh = (yf - mu) * rs;
+        const float dz = act_bwd_from_pre(v, yh * gm + bt, g.bnb_act);
+        t0 += dz;
+        t1 += dz * yh;
+        t2 += yh;
+      }
+    t0 += __shfl_xor(t0, 16, 64);
+    t0 += __shfl_xor(t0, 32, 64);
+    t1 += __shfl_xor(t1, 16, 64);
+    t1 += __shfl_xor(t1, 32, 64);
+    t2 += __shfl_xor(t2, 16, 64);
+    t2 += __shfl_xor(t2, 32, 64);
+    s0[j] = t0;
+    s1[j] = t1;
+    s2[j] = t2;
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int cl = wn * 32 + j * 16 + lane;
+      red[(0 * 2 + wm) * BN_ + cl] = s0[j];
+      red[(1 * 2 + wm) * BN_ + cl] = s1[j];
+      red[(2 * 2 + wm) * BN_ + cl] = s2[j];
+    }
+  }
+  __syncthreads();
+  const int mt = m0 / 128;
+  if (tid < BN_) {
+    const int col = n0 + tid;
+    if (col < g.N) {
+      float* p = g.bnb_ws + ((long long)mt * g.N + col) * 3;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) st_sc1(p + q, red[(q * 2) * BN_ + tid] + red[(q * 2 + 1) * BN_ + tid]);
+    }
+  }
+  const int nrb = (g.M + 127) / 128;
+  return ring_arrive_last(g.bnb_cnt + n0 / BN_, (unsigned)nrb, 1u, flag);
+}
+
+// the last-arriving row tile of a column tile: the apply constants and parameter gradients of its
+// 128 columns from every row tile's partials (after this workgroup's C stores are issued, so their
+// drain overlaps these loads)
+__device__ __forceinline__ void ring_bnb_finalize(const GemmArgs& g, int n0, char* smem_raw) {
+  constexpr int BN_ = 128, FGR = 4;
+  const int tid = threadIdx.x;
+  const avcbn::BwdFin& f = g.bnb_fin;
+  float* red = reinterpret_cast<float*>(smem_raw);
+  const int nrb = (g.M + 127) / 128;
+  {
+    // 128 columns x FGR row groups, the partials handed over within the launch (sc1 loads)
+    const int cl = tid & (BN_ - 1), grp = tid >> 7;
+    const int c = n0 + cl;
+    const bool cv = c < g.N;
+    float sv[3] = {0.f, 0.f, 0.f};
+    // 16 partial rows per thread in flight (a sequential loop of sc1 loads had cost ~25 us per conv)
+    static_assert(FGR == avcbn::FG, "row groups of strided_sums");
+    if (cv) avcbn::strided_sums<3, true, 16>(g.bnb_ws, nrb, g.N, c, grp, sv);
+    __syncthreads();
+    red[(0 * FGR + grp) * BN_ + cl] = sv[0];
+    red[(1 * FGR + grp) * BN_ + cl] = sv[1];
+    red[(2 * FGR + grp) * BN_ + cl] = sv[2];
+    __syncthreads();
+    if (grp == 0 && cv) {
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < FGR; ++k) {
+        a0 += red[(0 * FGR + k) * BN_ + cl];
+        a1 += red[(1 * FGR + k) * BN_ + cl];
+        a2 += red[(2 * FGR + k) * BN_ + cl];
+      }
+      avcbn::bwd_finalize_store(c, a0, a1, a2, g.M, g.N, f);
+    }
+  }
+}
+
 // Epilogue for the 2 x 4 wave layout (see ring_store_tile): bias and conv0-fold row bias in the
 // accumulators, the staged stores, then the BatchNorm partial statistics / finalize.
-template <int BM_, int BN_>
+// BNB: compile the BN-backward reduction (128 x 128 only; yv = the y tile prefetched at kernel start)
+template <int BM_, int BN_, bool BNB = false>
 __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM_ / 32][BN_ / 64], int m0, int n0,
-                                              int bz, int ks, char* smem_raw) {
+                                              int bz, int ks, char* smem_raw, const u32x4* yv = nullptr) {
   constexpr int TWM = BM_ / 2, TWN = BN_ / 4, MI = TWM / 16, NJ = TWN / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
@@ -445,7 +586,18 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
         }
       }
   }
+  bool bnb_last = false;
+  if constexpr (BNB && BM_ == 128 && BN_ == 128) {
+    // before the C stores, so the last-arrival wait covers the partials only
+    if (g.bnb_ws) bnb_last = ring_bnb_epilogue(g, acc, m0, n0, smem_raw, yv);
+  }
   ring_store_tile<BM_, BN_>(g, acc, m0, n0, bz, ks, smem_raw);
+  if constexpr (BNB && BM_ == 128 && BN_ == 128) {
+    if (bnb_last) {
+      __syncthreads();  // the staged stores are done with the LDS
+      ring_bnb_finalize(g, n0, smem_raw);
+    }
+  }
   if (g.bn_partial) {
     // per 128-row statistics tile: column sum and M2 about the tile mean (Chan's form, merged by
     // the finalize).  Waves w with (w's rows)/128 == h contribute to tile h of this workgroup.
@@ -879,7 +1031,7 @@ __device__ __forceinline__ void wait_cv(bool full) {
 // to the [Co][K][Ci] buffer: the timing of a repacked weight layout), 4 = MFMAs alone (no loads
 // after the prologue, fragments read in the first stage only), 5 = fragment reads alone (no loads
 // after the prologue, no MFMAs), 6 = production with s_setprio(1) around every MFMA group
-template <bool ALIGNED, int ABL = 0>
+template <bool ALIGNED, int ABL = 0, bool BNB = false>
 __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
   constexpr int MI = 4, NJ = 2, P = CV_NST - 1;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -986,6 +1138,10 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[2][MI], bfr[2][NJ];
+  u32x4 bnb_y[BNB ? BNB_YQ : 1];
+  if constexpr (BNB) {
+    if (g.bnb_ws) ring_bnb_prefetch(g, m0, n0, bnb_y);
+  }
 
 #pragma unroll
   for (int p = 0; p < P; ++p)
@@ -1057,7 +1213,7 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
     mfma_tap(I4{}, 0);
   }
   __syncthreads();
-  ring_epilogue<CV_TM, CV_TN>(g, acc, m0, n0, 0, 0, smem_raw);
+  ring_epilogue<CV_TM, CV_TN, BNB>(g, acc, m0, n0, 0, 0, smem_raw, bnb_y);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1273,17 +1429,17 @@ void launch_conv_ws(const GemmArgs& g, int gm, hipStream_t s) {
   conv_ring_ws_kernel<ALIGNED><<<nb, RNT, lds, s>>>(g, gm);
 }
 
-template <bool ALIGNED, int ABL = 0>
+template <bool ALIGNED, int ABL = 0, bool BNB = false>
 void launch_conv(const GemmArgs& g, int gm, hipStream_t s) {
   const size_t lds = std::max((size_t)CV_NST * CV_STAGE, ring_epi_lds<CV_TM, CV_TN>());
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<ALIGNED, ABL>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<ALIGNED, ABL, BNB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int nb = ((g.M + CV_TM - 1) / CV_TM) * ((g.N + CV_TN - 1) / CV_TN);
-  conv_ring_kernel<ALIGNED, ABL><<<nb, RNT, lds, s>>>(g, gm);
+  conv_ring_kernel<ALIGNED, ABL, BNB><<<nb, RNT, lds, s>>>(g, gm);
 }
 
 bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -1329,7 +1485,7 @@ RingCfg g_ring = init_cfg();
 bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
   const RingCfg& c = g_ring;
   if (c.mode == 0 || (g.a.win && !c.win)) return false;
-  if (g.K % 8 || g.klen % RBK || g.bnb_ws || g.atomic || g.cperm) return false;  // (no atomic / cperm stores)
+  if (g.K % 8 || g.klen % RBK || g.atomic || g.cperm) return false;  // (no atomic / cperm stores)
   if (g.ctr && ((reinterpret_cast<uintptr_t>(g.c) & 15) || (reinterpret_cast<uintptr_t>(g.res) & 15) ||
                 (g.cbs & 3)))
     return false;  // the transposed stores are 16-B vectors
@@ -1340,16 +1496,25 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
   // unless forced (T % 128 != 0 leaves 1.4 tiles per CU at B=64 T=176, where the 128 x 64 tiles of
   // gemm_conv.hip spread better -- tools/ring_ab.py, profiles/r4_ring_ab.txt)
   const OpDev& a = g.a;
-  if (win && c.win == 2 && a.taps == CV_TAPS && a.t_in == a.t_out && 2 * a.pad == a.taps - 1 &&
-      g.K == a.taps * a.chans && a.chans % CV_CBK == 0 && g.batch == 1 && g.split_k == 1 && !g.b.win &&
-      (c.mode == 1 || (a.t_out % CV_TM == 0 && g.N >= 128))) {
+  const bool halo = win && c.win == 2 && a.taps == CV_TAPS && a.t_in == a.t_out && 2 * a.pad == a.taps - 1 &&
+                    g.K == a.taps * a.chans && a.chans % CV_CBK == 0 && g.batch == 1 && g.split_k == 1 && !g.b.win &&
+                    (c.mode == 1 || (a.t_out % CV_TM == 0 && g.N >= 128));
+  // the BatchNorm-backward reduction epilogue (avc_gemm_bnb) exists on the halo conv tile only, for a
+  // bf16 y (ring_bnb_epilogue)
+  if (g.bnb_ws && !(halo && g.bnb_ydt == AVC_BF16 && g.N % 8 == 0 && g.ldc % 8 == 0 &&
+                    (reinterpret_cast<uintptr_t>(g.bnb_y) & 15) == 0 && !g.c16_act && !g.agrad && !g.csum))
+    return false;
+  if (halo) {
     if (c.abl == 1) launch_conv<true, 1>(g, c.gm, s);
     else if (c.abl == 2) launch_conv<true, 2>(g, c.gm, s);
     else if (c.abl == 3) launch_conv<true, 3>(g, c.gm, s);
     else if (c.abl == 4) launch_conv<true, 4>(g, c.gm, s);
     else if (c.abl == 5) launch_conv<true, 5>(g, c.gm, s);
     else if (c.abl == 6) launch_conv<true, 6>(g, c.gm, s);
-    else if (c.ws) {
+    else if (g.bnb_ws) {  // the BN-backward reduction epilogue (8-wave tile only)
+      if (a.t_out % CV_TM == 0) launch_conv<true, 0, true>(g, c.gm, s);
+      else launch_conv<false, 0, true>(g, c.gm, s);
+    } else if (c.ws) {
       if (a.t_out % CV_TM == 0) launch_conv_ws<true>(g, c.gm, s);
       else launch_conv_ws<false>(g, c.gm, s);
     } else if (a.t_out % CV_TM == 0) launch_conv<true>(g, c.gm, s);

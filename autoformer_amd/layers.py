@@ -629,14 +629,22 @@ class BnbLink:
 def _links(ctx, x, core, a, saved, fuse_prev):
     """Forward bookkeeping of the fused BN-backward statistics (BnbLink), bf16 training only."""
     on = _BNB_ON and K.compute() == K.BF16 and core.bn.training
-    ctx.self_link = BnbLink(core, saved) if on else None
+    # only where the consumer's data-gradient conv runs on the halo conv ring (utterance-aligned
+    # 128-frame tiles, >= 128 channels): on gemm_conv's epilogue the fusion measured slower (round 2)
+    Co = core.conv.weight.shape[0]
+    ring_ok = saved[3] % 128 == 0 and Co >= 128 and Co % 32 == 0
+    ctx.self_link = BnbLink(core, saved) if (on and ring_ok) else None
+    on = on and ring_ok
     if on:
         a._bnb_link = ctx.self_link
     prev = getattr(x, "_bnb_link", None) if (on and fuse_prev) else None
     ctx.prev_link = prev if (prev is not None and prev.core.bn.training) else None
 
 
-_BNB_ON = os.environ.get("AVC_BNB", "0") == "1"  # opt-in: measured slower in the C2 step (DESIGN §3)
+# the BN-backward statistics of a conv + BN layer in its consumer's data-gradient conv (the halo conv
+# ring's ring_bnb_epilogue, aligned T only -- see _links): on since round 5 (C2 5.74 -> 5.67 ms,
+# profiles/r5_bnb_ab.txt); "0": the separate reduce / finalize passes
+_BNB_ON = os.environ.get("AVC_BNB", "1") != "0"
 
 
 class _ConvBNFn(torch.autograd.Function):

@@ -38,6 +38,10 @@ def shapes(only):
     if only == "conv":
         return [("conv 8192x512x2560 w5", 8192, 512, 2560, dict(win=(64, 128, 512)), False),
                 ("xproj 8192x4096x512", 8192, 4096, 512, {}, False)]
+    if only == "bnb":  # the halo conv with / without the BN-backward reduction epilogue (avc_gemm_bnb)
+        return [("conv 8192x512x2560 w5", 8192, 512, 2560, dict(win=(64, 128, 512)), False),
+                ("conv 8192x512x2560 w5 bnb", 8192, 512, 2560, dict(win=(64, 128, 512)), "bnb"),
+                ("conv 8192x512x2560 w5 bnb16", 8192, 512, 2560, dict(win=(64, 128, 512)), "bnb16")]
     if only == "convk":  # the halo conv at 4 / 8 / 16 / 32 channel stages: per-stage slope vs fixed cost
         return [(f"conv 8192x512x{5 * ci} w5", 8192, 512, 5 * ci, dict(win=(64, 128, ci)), False)
                 for ci in (128, 256, 512, 1024)]
@@ -102,7 +106,16 @@ def main():
         c = torch.empty(M, N, device=dev)
         ref = aref @ b.float().t()
         kwb = {}
-        if bn:
+        if bn in ("bnb", "bnb16"):
+            y = torch.randn(M, N, device=dev).bfloat16()
+            mean, rstd = y.float().mean(0), 1 / (y.float().var(0) + 1e-5).sqrt()
+            coef = torch.empty(6 * N, device=dev)
+            dg, db, dbi = (torch.zeros(N, device=dev) for _ in range(3))
+            kwb = dict(bnb=(y, mean, rstd, torch.ones(N, device=dev), torch.zeros(N, device=dev), K.ACT_RELU, coef,
+                            dg, db, dbi, 1))
+            if bn == "bnb16":
+                c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        elif bn:
             part = K.bn_partial_buffer(M, N, dev)
             g_, b_ = torch.ones(N, device=dev), torch.zeros(N, device=dev)
             rm, rv = torch.zeros(N, device=dev), torch.ones(N, device=dev)
