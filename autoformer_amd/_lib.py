@@ -251,6 +251,9 @@ def check(rc: int, what: str = "") -> None:
 _FNS = {}  # name -> bound ctypes function (one dict lookup per launch instead of lib() + getattr)
 
 
+_REC = None  # a replay.StepRecord while a step is being recorded (replay.recording)
+
+
 def call(name: str, *args) -> None:
     fn = _FNS.get(name)
     if fn is None:
@@ -258,6 +261,8 @@ def call(name: str, *args) -> None:
     rc = fn(*args)
     if rc != 0:
         check(rc, name)
+    if _REC is not None:
+        _REC.add_native(fn, name, args)
 
 
 def exported_symbols():

@@ -171,7 +171,7 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
         bb.dgamma, bb.dbeta, bb.dbias, bb.accumulate = _ptr(dgamma), _ptr(dbeta), _ptr(dbias), int(acc)
         ws = torch.empty(int(L.lib().avc_gemm_bnb_ws(int(M), int(N))), device=y.device)
         bb.ws = ws.data_ptr()
-        L.check(L.lib().avc_gemm_bnb(d, bb, stream()), "avc_gemm_bnb")
+        L.call("avc_gemm_bnb", d, bb, stream())
         return None
     if bn_fin is None:
         L.call("avc_gemm", d, stream())
@@ -184,7 +184,7 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
                                                                             _ptr(rvar), _ptr(nbt))
     f.momentum, f.eps, f.nupd = float(momentum), float(eps), int(nupd)
     f.mean, f.rstd, f.scale, f.shift = (t.data_ptr() for t in stats)
-    L.check(L.lib().avc_gemm_bn(d, f, stream()), "avc_gemm_bn")
+    L.call("avc_gemm_bn", d, f, stream())
     return stats
 
 
@@ -478,12 +478,29 @@ def lstm_bwd(dh, h, c, g, w_hh, w_hh_t, B, T, H, dirs, gbuf=None):
     if timed:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
+    rec = L._REC if dg16 is not None and H == LAUNCH_TIMING_H else None
+    if rec is not None:  # a recorded step (replay.py) times this launch whenever LAUNCH_TIMING is on at replay
+        box, s = [], torch.cuda.current_stream()
+        rec.add_marker(lambda: _timing_mark(box, s, 0))
     L.call("avc_lstm_bwd", dh.data_ptr(), h.data_ptr(), c.data_ptr(), g.data_ptr(), _ptr(w_hh), _ptr(w_hh_t), wdt, B,
            T, H, dirs, dg.data_ptr(), _ptr(dg16), _ptr(dcbuf), _ptr(gbuf), _COMPUTE, stream())
+    if rec is not None:
+        rec.add_marker(lambda: _timing_mark(box, s, 1))
     if timed:
         ev[1].record()
         LAUNCH_TIMING.append(ev)
     return attach_twin(dg, dg16)
+
+
+def _timing_mark(box, s, end):
+    if LAUNCH_TIMING is None:
+        return
+    if not end:
+        box[:] = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
+        box[0][0].record(s)
+    elif box:
+        box[0][1].record(s)
+        LAUNCH_TIMING.append(box.pop())
 
 
 # ------------------------------------------------------------------------- glue

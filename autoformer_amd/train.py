@@ -16,6 +16,7 @@ backward, Adam(lr = 1e-4, betas (0.9, 0.999), eps 1e-8).
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
 import importlib
 import os
@@ -25,6 +26,7 @@ import torch
 
 from . import dist as D
 from . import kernels as K
+from .replay import collective
 from .layers import (ev_record, freeze_packs, join_side, on_stream, plan_caches, prefetch_packs, record_join_tails,
                      repack_in_place, set_grad_sink, side_stream, stream_wait, weights_changed)
 
@@ -269,6 +271,7 @@ class TrainStep:
         self._early = None
         self._early_adam = False
         self._capturing = False
+        self._recording = False  # record(): the decoder slice's Adam stays on the comm stream (eager form)
         self._pack_groups = None  # (encoder-slice caches, decoder-slice caches) of a captured step
         # fault word (kernels.fault_word): read back asynchronously after every step into a
         # pinned word and checked at the next step, so a failed persistent recurrence raises
@@ -276,6 +279,9 @@ class TrainStep:
         self._fault = K.fault_word(self.flat.device)
         self._fault_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         self._fault_ev = None
+        self._one = torch.ones((), device=self.flat.device)
+        self.recorded = None  # replay.StepRecord of record(): step() replays it
+        self._rstream = None
         # optional exposed all-reduce time: a list of (start, end) HIP event pairs recorded on
         # the main stream around its wait for the collective (bench.py's allreduce_ms)
         self.comm_timing = None
@@ -293,7 +299,7 @@ class TrainStep:
         K.raise_on_fault(self._fault.item())
 
     def _decoder_done(self):
-        if self._capturing:
+        if self._capturing and not self._recording:
             # captured step (world 1): the decoder-slice Adam and the in-place repack of the decoder's
             # weight packs run on the weight-gradient stream, after the decoder's weight gradients
             # queued there and beside the encoder backward
@@ -312,9 +318,13 @@ class TrainStep:
         with on_stream(self.comm):
             if self.world > 1:
                 # RCCL: the comm stream waits for the collective; the Adam slice follows it
-                self._early = D.allreduce_mean_async_(self.gflat[self.split:])
-                D.finish_allreduce_(self._early)
+                g = self.gflat[self.split:]
+                collective(lambda: D.finish_allreduce_(D.allreduce_mean_async_(g)))
             self.opt.step_slice(self.split, self.flat.numel(), advance=True, max_blocks=_SIDE_ADAM_BLOCKS)
+            if self._recording:
+                # recorded step: the decoder's weight packs rewritten in place right after its Adam
+                # slice, on this stream (the next step's forward is ordered after it by the tail's wait)
+                repack_in_place(self._pack_groups[1], "graph_dec")
         self._early_adam = True
 
     def _fwd_bwd(self, x, emb, overlap=False):
@@ -324,7 +334,9 @@ class TrainStep:
             loss, parts, x_psnt = self.loss_fn(self.model, x, emb, self.lambda_cd)
             if self.extra is not None:
                 loss = loss + self.extra(x, emb, x_psnt)
-            loss.backward()
+            # the seed gradient is a persistent tensor: backward() alone would allocate and fill
+            # a ones_like per step (one more kernel, and a closure in a recorded step)
+            loss.backward(self._one if loss.dim() == 0 else None)
         finally:
             self.model._decoder_bwd_done = None
         join_side()  # weight-gradient GEMMs ran on the side stream
@@ -360,6 +372,22 @@ class TrainStep:
         return self._step(x, emb)
 
     def _step(self, x, emb):
+        if self.recorded is not None:
+            # the recorded step's native calls, re-issued without the Python that made them: the
+            # same kernels on the same main / side streams and event edges (replay.py)
+            if x is not self._rx:
+                self._rx.copy_(x)
+            if emb is not self._re:
+                self._re.copy_(emb)
+            if self._rstream is not None:
+                rs = self._rstream.cuda_stream
+                stream_wait(rs, ev_record())
+                self.recorded.replay()
+                stream_wait(K.stream(), ev_record(rs))
+            else:
+                self.recorded.replay()
+            self._probe_fault()
+            return self.loss
         if self.graph_split is not None:
             # host-free step: the main chain and the weight-gradient branch replay as graph
             # segments on their own streams (graph.hip); with world 1 the Adam step and the
@@ -401,6 +429,107 @@ class TrainStep:
             prefetch_packs()  # next step's weight packs (the backward's, with a forward graph), on the side stream
         self._probe_fault()
         return loss
+
+    def _freeze_pack_groups(self):
+        """Split the live weight packs into the encoder / decoder slices' groups and bring their
+        in-place op tables and contents up to date (eager); the caller then freezes them."""
+        bound = self.flat[self.split].data_ptr() if self.split is not None else None
+        dec = (lambda c: c.params[0].data_ptr() >= bound) if bound is not None else (lambda c: False)
+        self._pack_groups = (plan_caches(lambda c: not dec(c)), plan_caches(dec))
+        for caches, grp in ((self._pack_groups[0], "graph_enc"), (self._pack_groups[1], "graph_dec"),
+                            (self._pack_groups[0] + self._pack_groups[1], "graph_all")):
+            repack_in_place(caches, grp)  # eager: builds the op tables (and the current packs)
+
+    def _recordable_tail(self):
+        """The optimizer step + in-place weight repack that end a captured / recorded step (with the
+        gradient average over ranks first when world > 1: recorded steps only)."""
+        if self._early_adam:
+            if self._recording:  # the decoder slice's average + Adam + repack ran on the comm stream
+                comm = self.comm.cuda_stream
+                if self.world > 1:
+                    box = self._comm_timing_mark(None)
+                    stream_wait(comm, ev_record())
+                    g = self.gflat[:self.split]
+                    with on_stream(self.comm):
+                        collective(lambda: D.finish_allreduce_(D.allreduce_mean_async_(g)))
+                stream_wait(K.stream(), ev_record(comm))
+                if self.world > 1:
+                    self._comm_timing_mark(box)
+            self.opt.step_slice(0, self.split, advance=False)
+            repack_in_place(self._pack_groups[0], "graph_enc")
+        else:
+            if self.world > 1:
+                collective(lambda: D.allreduce_mean_(self.gflat))
+            K.adam(self.flat, self.gflat, self.opt.m, self.opt.v, self.opt.lr, self.opt.betas[0],
+                   self.opt.betas[1], self.opt.eps, self.opt.state)
+            repack_in_place(self._pack_groups[0] + self._pack_groups[1], "graph_all")
+
+    def _comm_timing_mark(self, box):
+        """Recorded step: a marker that brackets the main stream's wait for the gradient average with
+        HIP events whenever comm_timing is a list at replay (bench.py's allreduce_ms); box=None
+        starts a bracket and returns it, a box closes it."""
+        from . import _lib as L
+
+        s = torch.cuda.current_stream()
+        if box is None:
+            box = []
+
+            def start():
+                if self.comm_timing is not None:
+                    box[:] = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
+                    box[0][0].record(s)
+            L._REC.add_marker(start)
+            return box
+
+        def end():
+            if self.comm_timing is not None and box:
+                box[0][1].record(s)
+                self.comm_timing.append(box.pop())
+        L._REC.add_marker(end)
+        return box
+
+    def replayable(self):
+        """Whether record() applies (every TrainStep; kept for callers that probe it)."""
+        return True
+
+    def record(self, x, emb, warmup=2):
+        """Run one step while recording its native calls (replay.py); every later step() replays
+        them: the whole step (zero_grad, forward, re-pass, losses, backward with the weight-gradient
+        side stream, both Adam slices, the in-place weight repack) with no Python per kernel.
+        x, emb become the step's input buffers: step() with other tensors copies them in.  With
+        world > 1 the gradient average (RCCL) is re-issued at its place by replay.collective."""
+        from . import replay as R
+
+        for _ in range(warmup):
+            self.step(x, emb)
+        torch.cuda.synchronize()
+        weights_changed()
+        self._freeze_pack_groups()
+        torch.cuda.synchronize()
+        freeze_packs(True)
+        # AVC_REC_EARLY=0: no decoder-slice Adam beside the encoder backward (one Adam at the end)
+        self._capturing = self._recording = self.split is not None and os.environ.get("AVC_REC_EARLY", "1") != "0"
+        rec = R.StepRecord()
+        # AVC_REC_PRIO=1: the recorded main chain runs on a high-priority stream (the dispatcher hands
+        # freed CUs to its workgroups before the weight-gradient / optimizer streams')
+        self._rstream = torch.cuda.Stream(priority=-1) if os.environ.get("AVC_REC_PRIO", "0") != "0" else None
+        try:
+            with R.recording(rec), contextlib.ExitStack() as es:
+                if self._rstream is not None:
+                    stream_wait(self._rstream.cuda_stream, ev_record())
+                    es.enter_context(on_stream(self._rstream))
+                self.loss = self._fwd_bwd(x, emb, overlap=self._capturing)
+                self._recordable_tail()
+            if self._rstream is not None:
+                stream_wait(K.stream(), ev_record(self._rstream.cuda_stream))
+        finally:
+            self._capturing = self._recording = False
+            self._early_adam = False
+            freeze_packs(False)
+        weights_changed()
+        self._probe_fault()
+        self.recorded, self._rx, self._re = rec, x, emb
+        return rec
 
     def capture(self, x, emb, warmup=2, forward_only=False, split=None):
         """Capture zero_grad + forward + re-pass + losses + backward into one hipGraph
@@ -450,12 +579,7 @@ class TrainStep:
             # the graph rewrites them in place after its Adam step (repack_in_place: the decoder's
             # on the side stream right after the decoder-slice Adam, the encoder's after the join),
             # so a replay runs no per-pack kernels on the main chain.  Bring them up to date first.
-            bound = self.flat[self.split].data_ptr() if self.split is not None else None
-            dec = (lambda c: c.params[0].data_ptr() >= bound) if bound is not None else (lambda c: False)
-            self._pack_groups = (plan_caches(lambda c: not dec(c)), plan_caches(dec))
-            for caches, grp in ((self._pack_groups[0], "graph_enc"), (self._pack_groups[1], "graph_dec"),
-                                (self._pack_groups[0] + self._pack_groups[1], "graph_all")):
-                repack_in_place(caches, grp)  # eager: builds the op tables (and the current packs)
+            self._freeze_pack_groups()
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph(keep_graph=True)
             record_join_tails(True)
@@ -467,13 +591,7 @@ class TrainStep:
                 with torch.cuda.graph(g):
                     self.loss = self._fwd_bwd(x, emb, overlap=overlap)
                     if adam:
-                        if self._early_adam:
-                            self.opt.step_slice(0, self.split, advance=False)
-                            repack_in_place(self._pack_groups[0], "graph_enc")
-                        else:
-                            K.adam(self.flat, self.gflat, self.opt.m, self.opt.v, self.opt.lr, self.opt.betas[0],
-                                   self.opt.betas[1], self.opt.eps, self.opt.state)
-                            repack_in_place(self._pack_groups[0] + self._pack_groups[1], "graph_all")
+                        self._recordable_tail()
             finally:
                 self._capturing = False
                 self._early_adam = False

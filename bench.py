@@ -249,6 +249,11 @@ def main():
                     help="replay the fwd+bwd as ONE hipGraph (the runtime serialises the side-stream branch)")
     ap.add_argument("--graph-fwd", action="store_true",
                     help="replay the forward + losses as a hipGraph, backward eager over the retained autograd graph")
+    ap.add_argument("--replay", action="store_true",
+                    help="record one step's native calls and replay them (autoformer_amd/replay.py): the eager "
+                         "step's kernels, streams and event edges without its Python -- the default")
+    ap.add_argument("--eager", action="store_true",
+                    help="step from Python every time (no recorded replay)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
@@ -306,10 +311,17 @@ def main():
     else:
         trainer = TrainStep(model, lr=1e-4)
 
+    graph = args.graph or args.graph_fwd or args.graph_one
+    # the recorded replay (replay.py) is the default step form: the same kernels, streams and event
+    # edges as the eager step, with no per-kernel Python, so a slow host does not set the step time
+    replay = not (args.eager or graph) and trainer.replayable()
     for _ in range(args.warmup):
         trainer.step(x, e)
-    if args.graph or args.graph_fwd or args.graph_one:
+    if graph:
         trainer.capture(x, e, forward_only=args.graph_fwd, split=False if args.graph_one else None)
+        trainer.step(x, e)
+    elif replay:
+        trainer.record(x, e, warmup=0)
         trainer.step(x, e)
     torch.cuda.synchronize()
     if world > 1:
@@ -362,7 +374,8 @@ def main():
                                   f"dim_pre=512",
                       "global_batch": B * world, "seq_len": T, "freq": freq, "parallelism": f"dp{world}",
                       "graph": ("split" if args.graph else "one" if args.graph_one else
-                                "fwd" if args.graph_fwd else False)},
+                                "fwd" if args.graph_fwd else False),
+                      "launch": "replay" if replay else "graph" if graph else "eager"},
            "step_mfma_frac": round(value * fpf / (world * peak * 1e12), 5) if fpf else None,
            "final_loss": loss_v}
     if world > 1:

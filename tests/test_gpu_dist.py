@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _run_steps(name="AutoVC", steps=2):
+def _run_steps(name="AutoVC", steps=2, replay=False):
     import importlib
 
     import autoformer_amd as A
@@ -39,8 +39,11 @@ def _run_steps(name="AutoVC", steps=2):
     x, e = torch.from_numpy(x).cuda(), torch.from_numpy(e).cuda()
     ts = TrainStep(m, lr=1e-4)
     try:
-        for _ in range(steps):
-            ts.step(x, e)
+        for i in range(steps):
+            if replay and i == 1:
+                ts.record(x, e, warmup=0)  # the recorded step is step 1; later steps replay it
+            else:
+                ts.step(x, e)
         torch.cuda.synchronize()
         overlapped = ts.split is not None
     finally:
@@ -48,7 +51,7 @@ def _run_steps(name="AutoVC", steps=2):
     return ts.flat.cpu().numpy(), overlapped  # numpy: pickled by value through the queue
 
 
-def _worker(rank, world, port, q, name):
+def _worker(rank, world, port, q, name, steps=2, replay=False):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     import torch.distributed as dist
@@ -57,7 +60,7 @@ def _worker(rank, world, port, q, name):
 
     try:
         D.init_from_env("gloo")
-        flat, overlapped = _run_steps(name)
+        flat, overlapped = _run_steps(name, steps, replay)
         q.put((rank, flat, overlapped))
         dist.barrier()
         dist.destroy_process_group()
@@ -84,6 +87,33 @@ def test_dp_world2_overlapped_allreduce_matches_single_process(name, expect_over
         rank, flat, overlapped = q.get(timeout=200)
         assert not isinstance(flat, str), flat
         assert overlapped == expect_overlap, "unexpected all-reduce overlap mode"
+        res[rank] = flat
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    r0, r1, single = (torch.from_numpy(a) for a in (res[0], res[1], single))
+    torch.testing.assert_close(r0, r1, rtol=0, atol=0)
+    torch.testing.assert_close(r0, single, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("name,expect_overlap", [("AutoVC", True), ("AutoVC_Adjust", False)])
+def test_dp_world2_recorded_replay_matches_single_process(name, expect_overlap):
+    """The recorded step with world 2 (TrainStep.record): the gradient averages are re-issued at
+    their places on the comm / main streams by replay.collective at every replay; 4 steps (eager,
+    recorded, 2 replays) must land where 4 eager single-process steps do."""
+    single, _ = _run_steps(name, steps=4)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, name, 4, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        rank, flat, overlapped = q.get(timeout=200)
+        assert not isinstance(flat, str), flat
+        assert overlapped == expect_overlap
         res[rank] = flat
     for p in procs:
         p.join(60)

@@ -15,6 +15,7 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--replay", action="store_true", help="TrainStep.record + replayed steps")
     args = ap.parse_args()
     import autoformer_amd as A
     from autoformer_amd.detinit import det_init_, det_inputs
@@ -29,6 +30,10 @@ def main():
     x, e = torch.from_numpy(x).cuda(), torch.from_numpy(e).cuda()
     ts = TrainStep(m)
     for _ in range(3):
+        ts.step(x, e)
+    if args.replay:
+        rec = ts.record(x, e, warmup=0)
+        print(f"recorded: {rec.native_calls()} native calls, torch ops {rec.torch_ops}")
         ts.step(x, e)
     torch.cuda.synchronize()
     host = []
