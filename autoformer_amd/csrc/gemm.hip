@@ -891,6 +891,7 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
                              g.batch == 1 && !d->a.kstrided && !d->b.kstrided),
                 "avc_gemm: row_bias needs rb_t > 2 rb_pad, M %% rb_t == 0, batch 1, no cperm, non-K-strided operands");
   g.bn_cnt = nullptr;
+  g.bn_rows = 0;
   g.bnb_ws = nullptr;
   g.bnb_cnt = nullptr;
   g.bnb_y = nullptr;

@@ -60,6 +60,7 @@ struct GemmArgs {
   float* bn_shift;
   float bn_momentum, bn_eps;
   int bn_nupd;
+  int bn_rows;  // rows per bn_partial statistics tile: 0 = BM (128); the one-utterance conv tile: T
   // BatchNorm BACKWARD reduction of the layer that produced this GEMM's output gradient
   // (bnb_ws != null, avc_gemm_bnb): per 128-row tile and column (sum dz, sum dz*yhat,
   // sum yhat) with dz = C * act'(z), z = (y - mean)*rstd*gamma + beta recomputed from the
@@ -80,10 +81,11 @@ __device__ __forceinline__ void bn_finalize_cols(const GemmArgs& g, int n0, floa
   const int tid = threadIdx.x, cl = tid % BN_, grp = tid / BN_;
   const int col = n0 + cl;
   const bool cv = col < g.N && grp < ng;
-  const int nt = (g.M + BM - 1) / BM;
+  const int tr = g.bn_rows ? g.bn_rows : BM;
+  const int nt = (g.M + tr - 1) / tr;
   const float n = (float)g.M;
   float mean, m2;
-  chan_merge<64 / (256 / BN_), true>(g.bn_partial, nt, g.N, col, cv, grp, ng, cl, BN_, g.M, BM, red, mean, m2);
+  chan_merge<64 / (256 / BN_), true>(g.bn_partial, nt, g.N, col, cv, grp, ng, cl, BN_, g.M, tr, red, mean, m2);
   if (grp == 0 && col < g.N) {
     const float var = m2 / n;
     const float rstd = 1.f / sqrtf(var + g.bn_eps);

@@ -181,10 +181,13 @@ __device__ __forceinline__ float* csum_dst(const GemmArgs& g, int row_tile, int 
 // uniform conditions tested once per vector, not per element (the per-element form carried ~1,800
 // uniform branches per 256 x 256 tile: 60 -> 90 us on the 8192 x 4096 x 512 projection).
 // Column tails and row strides that are not 16-B multiples take the per-element path.
+// Rows >= mlim are not stored (g.M, or the end of a one-utterance conv tile); a wave's rows go in
+// 64-row chunks, the last one partial when TWM % 64 != 0 (the 192-row conv tile: 64 + 32).
 template <int BM_, int BN_>
 __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[BM_ / 32][BN_ / 64], int m0, int n0,
-                                                int bz, int ks, char* smem_raw) {
+                                                int bz, int ks, char* smem_raw, int mlim) {
   constexpr int TWM = BM_ / 2, TWN = BN_ / 4, NJ = TWN / 16, RP = TWN + 4, NIT = TWN / 4;
+  constexpr int MI = TWM / 16, NCH = (MI + 3) / 4;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
   float* reg = reinterpret_cast<float*>(smem_raw) + wid * 64 * RP;
@@ -205,20 +208,21 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
     // transposed blocks (avc_gemm_desc.c_trans_rows): a lane stores 4 consecutive ROWS of one
     // column (contiguous in C, ctr % 4 == 0), consecutive lanes consecutive row quads
 #pragma unroll
-    for (int ch = 0; ch < TWM / 64; ++ch) {
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int rlim = min(mlim, m0 + wm * TWM + min(TWM, ch * 64 + 64));
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            reg[(ii * 16 + 4 * (lane >> 4) + e) * RP + j * 16 + (lane & 15)] = acc[ch * 4 + ii][j][e];
+            if (ch * 4 + ii < MI) reg[(ii * 16 + 4 * (lane >> 4) + e) * RP + j * 16 + (lane & 15)] = acc[ch * 4 + ii][j][e];
       __syncthreads();
 #pragma unroll 4
       for (int it = 0; it < NIT; ++it) {
         const int q = it * 64 + lane, r4 = q & 15, cl = q >> 4;
         const int row = m0 + wm * TWM + ch * 64 + 4 * r4, col = n0 + wn * TWN + cl;
-        if (row >= g.M || col >= g.N) continue;
+        if (row >= rlim || col >= g.N) continue;
         f32x4 v = {reg[(4 * r4) * RP + cl], reg[(4 * r4 + 1) * RP + cl], reg[(4 * r4 + 2) * RP + cl],
                    reg[(4 * r4 + 3) * RP + cl]};
         const long long o = out_off(g, row, col);
@@ -237,14 +241,15 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
     constexpr int L8 = TWN / 8, R8 = 64 / L8;
     f32x4 cs0 = {0.f, 0.f, 0.f, 0.f}, cs1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ch = 0; ch < TWM / 64; ++ch) {
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int rlim = min(mlim, m0 + wm * TWM + min(TWM, ch * 64 + 64));
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            reg[(ii * 16 + 4 * (lane >> 4) + e) * RP + j * 16 + (lane & 15)] = acc[ch * 4 + ii][j][e];
+            if (ch * 4 + ii < MI) reg[(ii * 16 + 4 * (lane >> 4) + e) * RP + j * 16 + (lane & 15)] = acc[ch * 4 + ii][j][e];
       __syncthreads();
       // the GELU-backward input is read G4 iterations at a time by UNCONDITIONAL loads (row and
       // column clamped into the tensor: ldc == N, N % 8 == 0 on this path), so the G4 loads are in
@@ -266,7 +271,7 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
           const int it = it0 + k4;
           const int lr = it * R8 + lane / L8, c8 = lane % L8;
           const int row = m0 + wm * TWM + ch * 64 + lr, col = n0 + wn * TWN + 8 * c8;
-          if (row >= g.M || col >= g.N) continue;
+          if (row >= rlim || col >= g.N) continue;
           f32x4 v0 = *reinterpret_cast<const f32x4*>(reg + lr * RP + 8 * c8);
           f32x4 v1 = *reinterpret_cast<const f32x4*>(reg + lr * RP + 8 * c8 + 4);
           const long long o = (long long)row * g.ldc + col;
@@ -336,7 +341,8 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
   // column-sum epilogue: lane's 4 columns are the same for every iteration (64 % (TWN/4) == 0)
   f32x4 cs = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int ch = 0; ch < TWM / 64; ++ch) {
+  for (int ch = 0; ch < NCH; ++ch) {
+      const int rlim = min(mlim, m0 + wm * TWM + min(TWM, ch * 64 + 64));
     // this wave's rows ch*64 .. +64 -> its LDS region (the region is the wave's own: the read below
     // only needs the wave's LDS writes retired, which the barrier also guarantees)
 #pragma unroll
@@ -345,13 +351,13 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          reg[(ii * 16 + 4 * (lane >> 4) + e) * RP + j * 16 + (lane & 15)] = acc[ch * 4 + ii][j][e];
+          if (ch * 4 + ii < MI) reg[(ii * 16 + 4 * (lane >> 4) + e) * RP + j * 16 + (lane & 15)] = acc[ch * 4 + ii][j][e];
     __syncthreads();
 #pragma unroll 4
     for (int it = 0; it < NIT; ++it) {
       const int q = it * 64 + lane, lr = q / (TWN / 4), c4 = q - lr * (TWN / 4);
       const int row = m0 + wm * TWM + ch * 64 + lr, col = n0 + wn * TWN + 4 * c4;
-      if (row >= g.M || col >= g.N) continue;
+      if (row >= rlim || col >= g.N) continue;
       f32x4 v = *reinterpret_cast<const f32x4*>(reg + lr * RP + 4 * c4);
       const long long o = (long long)row * g.ldc + col;
       if (vec && col + 3 < g.N) {
@@ -551,10 +557,14 @@ __device__ __forceinline__ void ring_bnb_finalize(const GemmArgs& g, int n0, cha
 // Epilogue for the 2 x 4 wave layout (see ring_store_tile): bias and conv0-fold row bias in the
 // accumulators, the staged stores, then the BatchNorm partial statistics / finalize.
 // BNB: compile the BN-backward reduction (128 x 128 only; yv = the y tile prefetched at kernel start)
+// mlim < 0: g.M; the one-utterance conv tile passes the end of its utterance.  BM_ == 192 (that tile)
+// computes ONE BatchNorm statistics tile of g.bn_rows rows (both wave rows); otherwise 128-row ones.
 template <int BM_, int BN_, bool BNB = false>
 __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM_ / 32][BN_ / 64], int m0, int n0,
-                                              int bz, int ks, char* smem_raw, const u32x4* yv = nullptr) {
+                                              int bz, int ks, char* smem_raw, const u32x4* yv = nullptr,
+                                              int mlim = -1) {
   constexpr int TWM = BM_ / 2, TWN = BN_ / 4, MI = TWM / 16, NJ = TWN / 16;
+  if (mlim < 0) mlim = g.M;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
   const int rbase = m0 + wm * TWM + 4 * (lane >> 4);
@@ -575,7 +585,7 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = rbase + i * 16 + e;
-        if (row >= g.M) continue;
+        if (row >= mlim) continue;
         const int b = (int)fdiv((uint32_t)row, g.rb_div), t = row - b * T;
         const int cls = t < pad ? t : (t >= T - pad ? 2 * pad - (T - 1 - t) : pad);
         const float* rp = g.rbias + (long long)(b * ncls + cls) * g.N;
@@ -591,7 +601,7 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
     // before the C stores, so the last-arrival wait covers the partials only
     if (g.bnb_ws) bnb_last = ring_bnb_epilogue(g, acc, m0, n0, smem_raw, yv);
   }
-  ring_store_tile<BM_, BN_>(g, acc, m0, n0, bz, ks, smem_raw);
+  ring_store_tile<BM_, BN_>(g, acc, m0, n0, bz, ks, smem_raw, mlim);
   if constexpr (BNB && BM_ == 128 && BN_ == 128) {
     if (bnb_last) {
       __syncthreads();  // the staged stores are done with the LDS
@@ -601,13 +611,15 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
   if (g.bn_partial) {
     // per 128-row statistics tile: column sum and M2 about the tile mean (Chan's form, merged by
     // the finalize).  Waves w with (w's rows)/128 == h contribute to tile h of this workgroup.
-    constexpr int NH = BM_ / 128;       // statistics tiles per workgroup tile
-    constexpr int WPT = 128 / TWM;      // waves (along M) per statistics tile
+    constexpr bool UTT = BM_ == 192;              // one statistics tile of g.bn_rows rows
+    constexpr int NH = UTT ? 1 : BM_ / 128;       // statistics tiles per workgroup tile
+    constexpr int WPT = UTT ? 2 : 128 / TWM;      // waves (along M) per statistics tile
+    const int srows = UTT ? g.bn_rows : 128;
     float* red = reinterpret_cast<float*>(smem_raw);  // [2][BN_] sums, then [2][BN_] M2
     float* red2 = red + 2 * BN_;
     unsigned* flag = reinterpret_cast<unsigned*>(red2 + 2 * BN_);
     const int h = wm / WPT;
-    const int cnt = max(1, min(128, g.M - (m0 + 128 * h)));
+    const int cnt = max(1, min(srows, mlim - (m0 + srows * h)));
     float s[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -615,7 +627,7 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) t += (rbase + i * 16 + e < g.M) ? acc[i][j][e] : 0.f;
+        for (int e = 0; e < 4; ++e) t += (rbase + i * 16 + e < mlim) ? acc[i][j][e] : 0.f;
       t += __shfl_xor(t, 16, 64);
       t += __shfl_xor(t, 32, 64);
       s[j] = t;
@@ -640,7 +652,7 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float d = acc[i][j][e] - mean;
-          t += (rbase + i * 16 + e < g.M) ? d * d : 0.f;
+          t += (rbase + i * 16 + e < mlim) ? d * d : 0.f;
         }
       t += __shfl_xor(t, 16, 64);
       t += __shfl_xor(t, 32, 64);
@@ -651,11 +663,11 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
       for (int j = 0; j < NJ; ++j) red2[wm * BN_ + wn * TWN + j * 16 + lane] = qv[j];
     }
     __syncthreads();
-    const int mt0 = m0 / 128;
+    const int mt0 = m0 / srows;
     if (tid < NH * BN_) {
       const int hh = tid / BN_, cl = tid - hh * BN_;
       const int col = n0 + cl;
-      if (col < g.N && m0 + 128 * hh < g.M) {
+      if (col < g.N && m0 + srows * hh < g.M) {
         float s0 = 0.f, s1 = 0.f;
 #pragma unroll
         for (int w = 0; w < WPT; ++w) {
@@ -673,7 +685,7 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
       }
     }
     if (g.bn_cnt) {
-      const int ntile = (g.M + 127) / 128;
+      const int ntile = (g.M + srows - 1) / srows;
       const int mine = min(NH, ntile - mt0);
       if (ring_arrive_last(g.bn_cnt + n0 / BN_, (unsigned)ntile, (unsigned)mine, flag))
         bn_finalize_cols<BN_>(g, n0, red);
@@ -1217,6 +1229,174 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_kernel(GemmArgs g, int gm) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// The halo conv with ONE UTTERANCE per row tile (128 < T <= 192, T = 176 for C4 / C5): a 192 x 128
+// tile (the 2 x 4 waves own 96 x 32 each, 6 x 2 MFMA blocks) whose rows T .. 191 are computed from
+// zero halo rows and never stored, so B = 64 utterances x 4 column tiles = 256 tiles = one round of
+// the CUs (the 128-row tiles of conv_ring_kernel number 352 at T = 176: two rounds, no faster than
+// gemm_conv.hip).  A stage holds the utterance's T + 4 halo rows (13 fill instructions of 16 rows)
+// and the five weight slices (40): 53 KiB, three stages = 159 KiB.  The BatchNorm statistics of the
+// forward come as one T-row tile per workgroup (GemmArgs::bn_rows = T, merged by bn_finalize_cols).
+constexpr int CU_TM = 192, CU_AI = 13, CU_TOT = CU_AI + CV_BI, CU_LW = (CU_TOT + 7) / 8;
+constexpr int CU_ABYTES = CU_AI * 1024, CU_STAGE = CU_TOT * 1024;
+
+template <int N>
+__device__ __forceinline__ void wait_cu(bool full) {
+  if (full) wait_vm<N * CU_LW>();
+  else wait_vm<N * (CU_LW - 1)>();
+}
+
+__global__ void __launch_bounds__(RNT, 2) conv_utt_kernel(GemmArgs g, int gm) {
+  constexpr int MI = 6, NJ = 2, P = CV_NST - 1;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const bool full = wid < (CU_TOT % 8 ? CU_TOT % 8 : 8);  // this wave issues CU_LW per stage
+
+  const OpDev& A = g.a;
+  const OpDev& Bo = g.b;
+  const int pad = A.pad, T = A.t_out, chans = A.chans;
+  const int nst = chans / CV_CBK;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int nN = (g.N + CV_TN - 1) / CV_TN, nM = g.M / T;
+  const int grp = lid / (gm * nN), fm = grp * gm, gsz = min(nM - fm, gm);
+  const int wi = lid - grp * gm * nN;
+  const int mt = fm + wi % gsz, nt = wi / gsz;
+  const int m0 = mt * T, n0 = nt * CV_TN;
+  const bf16* xa = reinterpret_cast<const bf16*>(A.ptr);
+  const bf16* wb = reinterpret_cast<const bf16*>(Bo.ptr);
+
+  // loader: instruction qi = i*8 + wid writes stage bytes [qi KiB, +1 KiB): rows 16*qi + (lane>>2)
+  // of 64 B; halo rows outside the utterance read the zero granule (stride 0)
+  const bf16* zp = reinterpret_cast<const bf16*>(g_zero16_rg);
+  asm volatile("" : "+v"(zp));
+  const bf16* src[CU_LW];
+  long long sst[CU_LW];
+#pragma unroll
+  for (int i = 0; i < CU_LW; ++i) {
+    const int qi = i * 8 + wid;
+    const int lrow = lane >> 2, slot = lane & 3;
+    src[i] = zp;
+    sst[i] = 0;
+    if (qi < CU_AI) {
+      const int hr = 16 * qi + lrow;
+      const int t = hr - pad;  // frame within the utterance
+      if (t >= 0 && t < T) {
+        src[i] = xa + (long long)(m0 + t) * A.ld + 8 * (slot ^ ((hr >> 1) & 3));
+        sst[i] = CV_CBK;
+      }
+    } else if (qi < CU_TOT) {
+      const int wr = 16 * (qi - CU_AI) + lrow;  // weight row = tap * 128 + column
+      const int tap = wr / CV_TN, n = n0 + (wr - tap * CV_TN);
+      if (n < g.N) {
+        src[i] = wb + (long long)n * Bo.ld + (long long)tap * chans + 8 * (slot ^ ((wr >> 1) & 3));
+        sst[i] = CV_CBK;
+      }
+    }
+  }
+  auto issue = [&](int stg, int cs) {
+    char* base = smem_raw + stg * CU_STAGE;
+#pragma unroll
+    for (int i = 0; i < CU_LW; ++i) {
+      const int qi = i * 8 + wid;
+      if (qi < CU_TOT) glds16(src[i] + cs * sst[i], base + qi * 1024);
+    }
+  };
+
+  // fragments: A row (halo) wm*96 + i*16 + frow + k (i an immediate offset of 1 KiB), B row
+  // k*128 + wn*32 + j*16 + frow
+  const int frow = lane & 15, kq = lane >> 4;
+  int aaddr[CV_TAPS];
+#pragma unroll
+  for (int k = 0; k < CV_TAPS; ++k) {
+    const int r = wm * 96 + frow + k;
+    aaddr[k] = r * 64 + 16 * (kq ^ ((r >> 1) & 3));
+  }
+  const int baddr = CU_ABYTES + (wn * 32 + frow) * 64 + 16 * (kq ^ ((frow >> 1) & 3));
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][MI], bfr[2][NJ];
+
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+    if (p < nst) issue(p, p);
+
+  for (int cs = 0; cs < nst; ++cs) {
+    const int ahead = min(P - 1, nst - 1 - cs);
+    if (ahead >= 1) wait_cu<1>(full);
+    else wait_vm<0>();
+    raw_barrier();
+    if (cs + P < nst) issue((cs + P) % CV_NST, cs + P);
+    const unsigned st = lds_addr(smem_raw + (cs % CV_NST) * CU_STAGE);
+    auto read_tap = [&](auto kc, int slot) {
+      constexpr int k = decltype(kc)::value;
+      const unsigned a0 = st + aaddr[k], b0 = st + baddr;
+      af[slot][0] = ds_read16<0>(a0);
+      af[slot][1] = ds_read16<1024>(a0);
+      af[slot][2] = ds_read16<2048>(a0);
+      af[slot][3] = ds_read16<3072>(a0);
+      af[slot][4] = ds_read16<4096>(a0);
+      af[slot][5] = ds_read16<5120>(a0);
+      bfr[slot][0] = ds_read16<(k * CV_TN) * 64>(b0);
+      bfr[slot][1] = ds_read16<(k * CV_TN + 16) * 64>(b0);
+    };
+    auto mfma_tap = [&](int slot) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[slot][i], bfr[slot][j], acc[i][j], 0, 0, 0);
+    };
+    // tap k+1's eight reads in flight while tap k's twelve MFMAs issue (conv_ring_kernel's pipeline)
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    read_tap(I0{}, 0);
+    read_tap(I1{}, 1);
+    wait_lgkm<8>();
+    mfma_tap(0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_tap(I2{}, 0);
+    wait_lgkm<8>();
+    mfma_tap(1);
+    __builtin_amdgcn_sched_barrier(0);
+    read_tap(I3{}, 1);
+    wait_lgkm<8>();
+    mfma_tap(0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_tap(I4{}, 0);
+    wait_lgkm<8>();
+    mfma_tap(1);
+    wait_lgkm<0>();
+    mfma_tap(0);
+  }
+  __syncthreads();
+  ring_epilogue<CU_TM, CV_TN>(g, acc, m0, n0, 0, 0, smem_raw, nullptr, m0 + T);
+}
+
+void launch_conv_utt(const GemmArgs& g0, int gm, hipStream_t s) {
+  GemmArgs g = g0;
+  g.bn_rows = g.a.t_out;  // one statistics tile per utterance
+  const size_t lds = std::max((size_t)CV_NST * CU_STAGE, ring_epi_lds<CU_TM, CV_TN>());
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_utt_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const int nb = (g.M / g.a.t_out) * ((g.N + CV_TN - 1) / CV_TN);
+  conv_utt_kernel<<<nb, RNT, lds, s>>>(g, gm);
+}
+
+// ---------------------------------------------------------------------------------------------
 // The same conv tile, warp-specialised: waves 0-3 are MMA waves (2 x 2, 64 x 64 each: 8 fragment
 // reads per 16 MFMAs, half the LDS reads per FLOP of the 64 x 32 wave tile -- whose 6 reads per 8
 // MFMAs kept the LDS array ~75 % busy and the MFMA pipe at 0.28 with the loads removed,
@@ -1444,6 +1624,11 @@ void launch_conv(const GemmArgs& g, int gm, hipStream_t s) {
 
 bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+bool getenv_flag(const char* name, bool dflt) {
+  const char* e = getenv(name);
+  return e ? e[0] != '0' : dflt;
+}
+
 bool operand_ok(const OpDev& o, bool allow_win) {
   if (o.dtype != AVC_BF16 || !ok16(o.ptr) || o.ld % 8 || o.bstride % 8) return false;
   if (o.win && (!allow_win || o.chans % 8)) return false;
@@ -1459,6 +1644,7 @@ struct RingCfg {
   int bm = 0, bn = 0, nst = 0, gm = 8, win = 2;
   int abl = 0;  // timing ablations of the halo conv (win 3 / 4 through avc_gemm_set_ring)
   int ws = 0;   // the warp-specialised halo conv (AVC_CONV_WS=1, or win 6 through avc_gemm_set_ring)
+  bool utt = true;  // one-utterance conv tiles for 128 < T <= 192 (AVC_CONV_UTT=0: gemm_conv.hip)
 };
 RingCfg init_cfg() {
   RingCfg r;
@@ -1476,13 +1662,23 @@ RingCfg init_cfg() {
   }
   if (const char* e = getenv("AVC_RING_WIN")) r.win = atoi(e);
   if (const char* e = getenv("AVC_CONV_WS")) r.ws = atoi(e);
+  r.utt = getenv_flag("AVC_CONV_UTT", true);
   return r;
 }
 RingCfg g_ring = init_cfg();
 
 }  // namespace
 
+thread_local int g_ring_last = 0;  // avc_gemm_ring_last
+bool gemm_ring_launch_(const GemmArgs& g, hipStream_t s);
+
 bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
+  g_ring_last = 0;
+  const bool r = gemm_ring_launch_(g, s);
+  return r;
+}
+
+bool gemm_ring_launch_(const GemmArgs& g, hipStream_t s) {
   const RingCfg& c = g_ring;
   if (c.mode == 0 || (g.a.win && !c.win)) return false;
   if (g.K % 8 || g.klen % RBK || g.atomic || g.cperm) return false;  // (no atomic / cperm stores)
@@ -1504,6 +1700,20 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
   if (g.bnb_ws && !(halo && g.bnb_ydt == AVC_BF16 && g.N % 8 == 0 && g.ldc % 8 == 0 &&
                     (reinterpret_cast<uintptr_t>(g.bnb_y) & 15) == 0 && !g.c16_act && !g.agrad && !g.csum))
     return false;
+  // one utterance per row tile (T = 176 of C4 / C5): the 192-row tile, when every epilogue it has is
+  // one the 2 x 4 ring epilogue covers (no BN-backward / GELU / column-sum / transposed stores) and
+  // the forward BatchNorm statistics are finalized in the kernel (their tiles are T rows, which
+  // only bn_finalize_cols is told)
+  const int T = a.t_out;
+  const bool utt = win && c.win == 2 && c.mode != 1 && a.taps == CV_TAPS && a.t_in == T && 2 * a.pad == a.taps - 1 &&
+                   g.K == a.taps * a.chans && a.chans % CV_CBK == 0 && g.batch == 1 && g.split_k == 1 && !g.b.win &&
+                   T > CV_TM && T <= CU_TM && g.M % T == 0 && g.N >= 128 && !g.bnb_ws && !g.c16_act && !g.agrad &&
+                   !g.csum && !g.ctr && (!g.bn_partial || g.bn_cnt) && !c.abl && !c.ws && c.utt;
+  if (utt) {
+    launch_conv_utt(g, c.gm, s);
+    g_ring_last = 3;
+    return true;
+  }
   if (halo) {
     if (c.abl == 1) launch_conv<true, 1>(g, c.gm, s);
     else if (c.abl == 2) launch_conv<true, 2>(g, c.gm, s);
@@ -1519,6 +1729,7 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
       else launch_conv_ws<false>(g, c.gm, s);
     } else if (a.t_out % CV_TM == 0) launch_conv<true>(g, c.gm, s);
     else launch_conv<false>(g, c.gm, s);
+    g_ring_last = c.ws && !g.bnb_ws && !c.abl ? 4 : 2;
     return true;
   }
   int bm, bn, nst;
@@ -1565,6 +1776,7 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
   if (bm == BMV && bn == BNV && nst == NSV) {          \
     if (win) launch<BMV, BNV, NSV, true>(g, c.gm, s);  \
     else launch<BMV, BNV, NSV, false>(g, c.gm, s);     \
+    g_ring_last = 1;                                   \
     return true;                                       \
   }
   RING_CASE(256, 256, 2) RING_CASE(256, 128, 3) RING_CASE(128, 128, 4) RING_CASE(128, 128, 3)
@@ -1575,6 +1787,7 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
   if (bm == BMV && bn == BNV && nst == 10 + NSV) {        \
     if (win) launch32<BMV, BNV, NSV, true>(g, c.gm, s);   \
     else launch32<BMV, BNV, NSV, false>(g, c.gm, s);      \
+    g_ring_last = 5;                                      \
     return true;                                          \
   }
   RING32_CASE(256, 256, 4) RING32_CASE(256, 128, 5) RING32_CASE(128, 128, 6)
@@ -1583,6 +1796,8 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
 }
 
 }  // namespace avcg
+
+extern "C" int avc_gemm_ring_last(void) { return avcg::g_ring_last; }
 
 // Benchmarking hook (tools/ring_ab.py): mode -1 auto, 0 off, 1 forced (bm, bn, nst); gm row
 // tiles per group (<= 0 keeps it); win: as AVC_RING_WIN.

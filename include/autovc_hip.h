@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 24
+#define AVC_ABI_VERSION 25
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -285,6 +285,12 @@ int avc_lstm_set_spin(unsigned spins);
  * 1 = forced configurations stream them as im2col windows, 2 = 5-tap convs take the halo ring.
  * Same as the AVC_RING / AVC_RING_WIN environment variables.  Returns 0. */
 int avc_gemm_set_ring(int mode, int bm, int bn, int nst, int gm, int win);
+
+/* Which deep-ring kernel the last avc_gemm on this host thread launched (tests, tools): 0 none (an
+ * older kernel), 1 gemm_ring_kernel, 2 the 128-row halo conv (conv_ring_kernel, its BN-backward
+ * form included), 3 the one-utterance halo conv (conv_utt_kernel, 128 < T <= 192), 4 the
+ * warp-specialised halo conv, 5 the 32-deep-slot ring.  Replaces no reference interface. */
+int avc_gemm_ring_last(void);
 
 /* 1 when avc_lstm_fwd (backward = 0) / avc_lstm_bwd (backward = 1) take the one-launch
  * persistent path for this shape on the current device: bf16 compute, dirs == 1, H in

@@ -124,6 +124,51 @@ def test_conv_ring(B, T, Cin, Cout, forced, bn):
             assert _rel(st[1], 1 / torch.sqrt(ref.var(0, unbiased=False) + 1e-5)) < 1e-4
 
 
+@pytest.mark.parametrize("B,T,Cin,Cout", [(4, 176, 64, 200), (64, 176, 512, 512), (3, 160, 96, 136), (2, 192, 32, 128)])
+@pytest.mark.parametrize("bn", [False, True])
+def test_conv_utterance_tile(B, T, Cin, Cout, bn):
+    """conv_utt_kernel: one utterance per 192-row tile (128 < T <= 192; T = 176 is C4 / C5), rows
+    T..191 computed from zero halo rows and not stored; the BatchNorm statistics as one T-row tile
+    per workgroup, merged by the in-kernel finalize (bn_rows = T)."""
+    from autoformer_amd import _lib
+    from autoformer_amd import kernels as K
+
+    torch.manual_seed(B * T + Cin + Cout)
+    M = B * T
+    x = torch.randn(M, Cin, device=DEV).bfloat16()
+    Wf = (torch.randn(Cout, 5 * Cin, device=DEV) * 0.1).bfloat16()
+    bias = torch.randn(Cout, device=DEV)
+    xp = torch.nn.functional.pad(x.float().view(B, T, Cin), (0, 0, 2, 2))
+    win = torch.cat([xp[:, k:k + T] for k in range(5)], dim=2).reshape(M, 5 * Cin)
+    ref = win @ Wf.float().t() + bias
+    _ring(-1)
+    y = torch.full((M + 64, Cout), 7.0, device=DEV)  # rows past M must stay untouched
+    xo, wo = K.operand(x, Cin, window=(5, 2, T, T, Cin)), K.operand(Wf, 5 * Cin)
+    if bn:
+        p = K.bn_partial_buffer(M, Cout, DEV)
+        g_, b_ = torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV)
+        rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+        nbt = torch.zeros(1, device=DEV, dtype=torch.int64)
+        st = K.gemm(M, Cout, 5 * Cin, xo, wo, y, bias=bias, bn_partial=p, bn_fin=(g_, b_, rm, rv, nbt, 0.1, 1e-5, 1))
+    else:
+        K.gemm(M, Cout, 5 * Cin, xo, wo, y, bias=bias)
+    assert _lib.lib().avc_gemm_ring_last() == 3, "the one-utterance halo conv did not run"
+    y16 = torch.empty(M, Cout, device=DEV, dtype=torch.bfloat16)
+    K.gemm(M, Cout, 5 * Cin, xo, wo, y16, bias=bias)  # bf16-only output (the 16-B store path)
+    torch.cuda.synchronize()
+    assert _rel(y[:M], ref) < 1e-5
+    assert bool((y[M:] == 7.0).all())
+    assert _rel(y16.float(), ref) < 1e-2
+    if bn:
+        mean, var = ref.double().mean(0), ref.double().var(0, unbiased=False)
+        assert _rel(st[0], mean) < 1e-5
+        assert _rel(st[1], 1 / torch.sqrt(var + 1e-5)) < 1e-4
+        assert _rel(st[2], g_.double() / torch.sqrt(var + 1e-5)) < 1e-4
+        assert _rel(rm, 0.1 * mean) < 1e-5
+        assert _rel(rv, 0.9 + 0.1 * ref.double().var(0, unbiased=True)) < 1e-5
+        assert int(nbt.item()) == 1
+
+
 def _gelu_grad(x):
     xd = x.double()
     return 0.5 * (1 + torch.erf(xd / 2 ** 0.5)) + xd * torch.exp(-0.5 * xd * xd) / (2 * torch.pi) ** 0.5
