@@ -1813,6 +1813,9 @@ extern "C" int avc_gemm_set_ring(int mode, int bm, int bn, int nst, int gm, int 
   // 8-wave one
   avcg::g_ring.abl = (win >= 3 && win <= 5) ? win - 2 : (win >= 7 && win <= 9) ? win - 3 : 0;
   if (win == 6) avcg::g_ring.ws = 1;
-  else if (win == 2) avcg::g_ring.ws = 0;
+  else if (win == 2 || win == 10) avcg::g_ring.ws = 0;
+  // 10: the halo convs without the one-utterance tile (T = 176 back on gemm_conv.hip); any other
+  // value restores the default
+  avcg::g_ring.utt = win != 10;
   return 0;
 }

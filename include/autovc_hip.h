@@ -282,7 +282,8 @@ int avc_lstm_set_spin(unsigned spins);
  * (256 x 256 tiles for N >= 1024 with a tile per CU, the halo ring for utterance-aligned 5-tap
  * convs), 0 = off (the older kernels), 1 = forced bm x bn tile with nst ring slots; gm = row tiles
  * per tile group (<= 0 keeps the current value); win: 0 = conv window operands never take it,
- * 1 = forced configurations stream them as im2col windows, 2 = 5-tap convs take the halo ring.
+ * 1 = forced configurations stream them as im2col windows, 2 = 5-tap convs take the halo ring
+ * (10 = the same without the one-utterance tile for 128 < T <= 192).
  * Same as the AVC_RING / AVC_RING_WIN environment variables.  Returns 0. */
 int avc_gemm_set_ring(int mode, int bm, int bn, int nst, int gm, int win);
 

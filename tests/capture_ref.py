@@ -240,10 +240,14 @@ class Capture:
             r16 = torch.nn.functional.gelu(ref) if c_bf16_act else ref
             res["C_bf16"] = _rel(_c_view(c_bf16, M, N, ldc_, batch, c_batch_stride, 0), r16, before)
         if bn_partial is not None:
-            # per 128-row tile (sum, M2) of the stored values -> column mean / variance
-            nt = (M + 127) // 128
-            part = bn_partial.double().view(nt, N, 2)
-            cnt = torch.tensor([min(128, M - 128 * i) for i in range(nt)], dtype=torch.float64, device=c.device)
+            # per statistics tile (sum, M2) of the stored values -> column mean / variance; the tiles are
+            # 128 rows, or one utterance (a.t_out rows) when the one-utterance halo conv ran
+            from autoformer_amd import _lib
+
+            tr = a.t_out if _lib.lib().avc_gemm_ring_last() == 3 else 128
+            nt = (M + tr - 1) // tr
+            part = bn_partial.double().reshape(-1)[:nt * N * 2].view(nt, N, 2)
+            cnt = torch.tensor([min(tr, M - tr * i) for i in range(nt)], dtype=torch.float64, device=c.device)
             mean = part[:, :, 0].sum(0) / M
             tmean = part[:, :, 0] / cnt[:, None]
             var = (part[:, :, 1].sum(0) + (cnt[:, None] * (tmean - mean[None]) ** 2).sum(0)) / M

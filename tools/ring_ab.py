@@ -45,6 +45,10 @@ def shapes(only):
     if only == "convk":  # the halo conv at 4 / 8 / 16 / 32 channel stages: per-stage slope vs fixed cost
         return [(f"conv 8192x512x{5 * ci} w5", 8192, 512, 5 * ci, dict(win=(64, 128, ci)), False)
                 for ci in (128, 256, 512, 1024)]
+    if only == "utt":  # T = 176: the one-utterance halo conv (halo) vs gemm_conv.hip (halo-noutt)
+        return [("conv T176 11264x512x2560 w5", 11264, 512, 2560, dict(win=(64, 176, 512)), False),
+                ("conv T176 11264x512x2560 w5 bn", 11264, 512, 2560, dict(win=(64, 176, 512)), True),
+                ("conv T176 11264x176x2560 w5", 11264, 176, 2560, dict(win=(64, 176, 512)), False)]
     if only in (None, "c2"):
         out += [
             ("conv 8192x512x2560 w5", 8192, 512, 2560, dict(win=(64, 128, 512)), False),
@@ -77,7 +81,7 @@ CONFIGS = [("old", (0, 0, 0, 0, 0, 1)), ("auto", (-1, 0, 0, 0, 8, 1)), ("halo", 
            # the warp-specialised halo conv (4 MMA waves of 64 x 64 + 4 loader waves)
            ("halo-ws", (-1, 0, 0, 0, 8, 6)),
            ("halo-mfma", (-1, 0, 0, 0, 8, 7)), ("halo-reads", (-1, 0, 0, 0, 8, 8)),
-           ("halo-prio", (-1, 0, 0, 0, 8, 9))]
+           ("halo-prio", (-1, 0, 0, 0, 8, 9)), ("halo-noutt", (-1, 0, 0, 0, 8, 10))]
 
 
 def main():
