@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AVC_LIB_PATH") or os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["gemm_ring.hip", "gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "graph.hip", "fold.hip", "disc.hip"]
-ABI_VERSION = 25
+ABI_VERSION = 26
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -44,13 +44,14 @@ class GemmDesc(ctypes.Structure):
 class BnFin(ctypes.Structure):
     _fields_ = [("gamma", c_void_p), ("beta", c_void_p), ("running_mean", c_void_p), ("running_var", c_void_p),
                 ("num_batches_tracked", c_void_p), ("momentum", c_float), ("eps", c_float), ("nupd", c_int),
-                ("mean", c_void_p), ("rstd", c_void_p), ("scale", c_void_p), ("shift", c_void_p)]
+                ("mean", c_void_p), ("rstd", c_void_p), ("scale", c_void_p), ("shift", c_void_p),
+                ("apply_bf16", c_void_p), ("apply_act", c_int)]
 
 
 class BnbArgs(ctypes.Structure):
     _fields_ = [("y", c_void_p), ("y_dtype", c_int), ("mean", c_void_p), ("rstd", c_void_p), ("gamma", c_void_p),
                 ("beta", c_void_p), ("act", c_int), ("coef", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p),
-                ("dbias", c_void_p), ("accumulate", c_int), ("ws", c_void_p)]
+                ("dbias", c_void_p), ("accumulate", c_int), ("ws", c_void_p), ("dy_bf16", c_void_p)]
 
 
 class PackOp(ctypes.Structure):

@@ -46,6 +46,8 @@ struct BwdFin {
 
 // Channel c's apply constants (planar coef[6][C]) and parameter gradients from its three column
 // sums over all rows: s0 = sum dz, s1 = sum dz*yhat, s2 = sum yhat.
+// SC1: the coefficients are read within the launch (the fused apply of the halo conv): write-through
+template <bool SC1 = false>
 __device__ __forceinline__ void bwd_finalize_store(int c, float s0, float s1, float s2, int M, int C, const BwdFin& f) {
   const float g = f.gamma ? f.gamma[c] : 1.f;
   const float rs = f.rstd[c], mu = f.mean[c];
@@ -54,9 +56,15 @@ __device__ __forceinline__ void bwd_finalize_store(int c, float s0, float s1, fl
   const float m1 = s0 * invn, m2 = s1 * invn;
   // planar per-channel constants of the apply pass (one 16-B load per plane per 4 channels):
   //   yhat = (y - mu)*rs,  z = (y - mu)*k1 + beta,  dy = k1*(dz - m1 - yhat*m2)
-  f.coef[c] = k1;
-  f.coef[C + c] = m1;
-  f.coef[2 * C + c] = m2;
+  if (SC1) {
+    st_sc1(f.coef + c, k1);
+    st_sc1(f.coef + C + c, m1);
+    st_sc1(f.coef + 2 * C + c, m2);
+  } else {
+    f.coef[c] = k1;
+    f.coef[C + c] = m1;
+    f.coef[2 * C + c] = m2;
+  }
   f.coef[3 * C + c] = mu;
   f.coef[4 * C + c] = rs;
   f.coef[5 * C + c] = f.beta ? f.beta[c] : 0.f;

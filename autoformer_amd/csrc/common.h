@@ -139,6 +139,8 @@ static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b)
 // use inside a stream capture, allocation failure).  The last arrival of a launch resets its
 // slot to 0, so slots are reused without a reset pass.
 unsigned* avc_counter_slots(int n, hipStream_t s);
+// the process fault word of the current device (avc_set_fault_word; lstm.hip), nullable
+unsigned* avc_fault_ptr();
 // n floats of a device pool that is all zero between uses: the user leaves its region zeroed
 // (a ring like avc_counter_slots; created on first use outside a stream capture)
 float* avc_zero_slots(int n, hipStream_t s);

@@ -717,6 +717,18 @@ static int bnb_after(const avc_gemm_desc* d, const avc_bnb_args* bb, hipStream_t
                                        fin, s);
 }
 
+// The BatchNorm apply outputs of avc_gemm_bn / avc_gemm_bnb when the GEMM's epilogue did not write
+// them (every kernel but the halo conv ring): the apply passes after the statistics
+static int bn_apply_after(const avc_gemm_desc* d, const avc_bn_fin* f, const avc_bnb_args* bb, hipStream_t s) {
+  const void* y = d->c ? (const void*)d->c : d->c_bf16;
+  const int ydt = d->c ? AVC_F32 : AVC_BF16;
+  if (f && f->apply_bf16)
+    return avc_bn_apply(y, ydt, f->scale, f->shift, nullptr, nullptr, f->apply_bf16, d->M, d->N, f->apply_act, s);
+  if (bb && bb->dy_bf16)
+    return avc_bn_bwd_apply(y, ydt, bb->y, bb->y_dtype, bb->coef, d->M, d->N, bb->act, nullptr, bb->dy_bf16, s);
+  return 0;
+}
+
 // The fused GELU / column-sum epilogues (avc_gemm_desc.c_bf16_act / act_grad_of / col_sum) exist in
 // the ring kernels only; the other kernels store the plain product (fp32 C and / or bf16: the
 // pre-activation slot, or the bf16 C itself when there is no fp32 C) and one pass follows.
@@ -898,6 +910,18 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
   g.bnb_ydt = AVC_F32;
   g.bnb_act = 0;
   g.bnb_fin = avcbn::BwdFin{};
+  g.bn_apply16 = f ? reinterpret_cast<bf16*>(f->apply_bf16) : nullptr;
+  g.bn_act = f ? f->apply_act : 0;
+  g.bnb_dy16 = bb ? reinterpret_cast<bf16*>(bb->dy_bf16) : nullptr;
+  g.fault = (g.bn_apply16 || g.bnb_dy16) ? avc_fault_ptr() : nullptr;
+  static const int nap = [] {
+    const char* e = getenv("AVC_BN_NAP");
+    return e ? std::max(1, atoi(e)) : 4;
+  }();
+  g.nap = nap;
+  AVC_CHECK_ARG(!g.bn_apply16 || (d->ldc == d->N && g.batch == 1 && !d->residual),
+                "avc_gemm_bn: apply_bf16 needs ldc == N, batch 1, no residual");
+  AVC_CHECK_ARG(!g.bnb_dy16 || d->ldc == d->N, "avc_gemm_bnb: dy_bf16 needs ldc == N");
   if (f) {
     AVC_CHECK_ARG(g.bn_partial && f->mean && f->rstd && f->scale && f->shift && f->nupd >= 1 &&
                       (!f->running_mean == !f->running_var),
@@ -981,8 +1005,10 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
       if (avc_check_launch("avc_gemm(col_sum slots)")) return -1;
     }
     if (gelu_after(g, post, s)) return -1;
-    if (bb && !bnb_fused) return bnb_after(d, bb, s);
-    return (f && !g.bn_cnt) ? bn_finalize_after(g, f, stream) : 0;
+    const bool applied = ring && gemm_ring_applied();  // the BN apply ran in the halo conv's epilogue
+    if (bb && !bnb_fused && bnb_after(d, bb, s)) return -1;
+    if (f && !g.bn_cnt && bn_finalize_after(g, f, stream)) return -1;
+    return applied ? 0 : bn_apply_after(d, f, bb, s);
   }
   const GeluPost post = strip_gelu(g);
   // the generic kernel writes fp32 C only: a bf16 output is produced afterwards from C by the GELU
@@ -1013,8 +1039,9 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
 #undef AVC_GEMM_LAUNCH
   if (avc_check_launch("avc_gemm")) return -1;
   if (gelu_after(g, post, s, true)) return -1;
-  if (bb) return bnb_after(d, bb, s);
-  return f ? bn_finalize_after(g, f, stream) : 0;  // generic kernels: finalize launch(es) after the GEMM
+  if (bb && bnb_after(d, bb, s)) return -1;
+  if (f && bn_finalize_after(g, f, stream)) return -1;  // generic kernels: finalize launch(es) after the GEMM
+  return bn_apply_after(d, f, bb, s);
 }
 
 extern "C" int avc_gemm(const avc_gemm_desc* d, void* stream) { return gemm_impl(d, nullptr, stream); }

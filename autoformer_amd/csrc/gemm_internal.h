@@ -70,6 +70,15 @@ struct GemmArgs {
   float* bnb_ws;
   unsigned* bnb_cnt;
   avcbn::BwdFin bnb_fin;
+  // fused BatchNorm APPLY outputs (halo conv ring only; gemm_ring_launch clears them for the other
+  // kernels and the caller runs the apply pass instead): act(y*scale + shift) of the forward
+  // (bn_apply16, with bn_cnt) / the producing layer's dy of the backward (bnb_dy16, with bnb_ws),
+  // both bf16, written after a column-tile barrier behind the last row tile's finalize
+  bf16* bn_apply16;
+  int bn_act;
+  bf16* bnb_dy16;
+  unsigned* fault;  // process fault word (bit 1: a barrier wait timed out); nullable
+  int nap;          // s_sleep(1)s between the barrier's polls (AVC_BN_NAP)
 };
 
 // Last-arriving row tile of a column tile: merge the per-row-tile (sum, M2) partials of columns
@@ -91,10 +100,11 @@ __device__ __forceinline__ void bn_finalize_cols(const GemmArgs& g, int n0, floa
     const float rstd = 1.f / sqrtf(var + g.bn_eps);
     const float ga = g.bn_gamma ? g.bn_gamma[col] : 1.f;
     const float be = g.bn_beta ? g.bn_beta[col] : 0.f;
-    g.bn_mean[col] = mean;
-    g.bn_rstd[col] = rstd;
-    g.bn_scale[col] = ga * rstd;
-    g.bn_shift[col] = be - mean * ga * rstd;
+    // write-through: the fused apply's workgroups read scale / shift within the launch (ld_sc1)
+    st_sc1(g.bn_mean + col, mean);
+    st_sc1(g.bn_rstd + col, rstd);
+    st_sc1(g.bn_scale + col, ga * rstd);
+    st_sc1(g.bn_shift + col, be - mean * ga * rstd);
     if (g.bn_rmean) {
       const float unb = n > 1.f ? m2 / (n - 1.f) : var;
       float rm = g.bn_rmean[col], rv = g.bn_rvar[col];
@@ -385,5 +395,6 @@ bool gemm_tt_launch(const GemmArgs& g, hipStream_t s);
 // Entry of the 8-wave deep-ring NT kernel (gemm_ring.hip); false when the shape / operands do
 // not qualify or AVC_RING=0.
 bool gemm_ring_launch(const GemmArgs& g, hipStream_t s);
+bool gemm_ring_applied();  // the last gemm_ring_launch on this thread wrote the BN apply outputs
 
 }  // namespace avcg

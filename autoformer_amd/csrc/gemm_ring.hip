@@ -163,6 +163,82 @@ __device__ __forceinline__ bool ring_arrive_last(unsigned* cnt, unsigned arrival
   return *flag != 0;
 }
 
+// Column-tile barrier of the fused BatchNorm apply: every row tile arrives on the column tile's
+// counter WITHOUT the last one resetting it; the last one runs the finalize (write-through stores),
+// drains them and only then resets the counter to 0 -- the release the others poll for (the counter
+// returns to 0 at no other time within the launch).  Needs every row tile of a column tile resident
+// at once: gemm_ring_launch allows it only for grids of at most one workgroup per CU.
+__device__ __forceinline__ bool ring_arrive_hold(unsigned* cnt, unsigned arrivals, unsigned mine, unsigned* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(cnt, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = old + mine == arrivals ? 1u : 0u;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+__device__ __forceinline__ void ring_release(unsigned* cnt) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the finalize's write-through stores are out
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+}
+constexpr unsigned RING_SPIN = 1u << 22;  // ~0.3 s of s_sleep 1 polls: a stalled grid, not contention
+__device__ __forceinline__ void ring_wait(unsigned* cnt, unsigned* fault, int nap) {
+  if (threadIdx.x == 0) {
+    unsigned n = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+      for (int k = 0; k < nap; ++k) __builtin_amdgcn_s_sleep(1);  // fewer polls on the one address
+      if ((n += nap) >= RING_SPIN) {
+        if (fault) atomicOr(fault, 2u);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// bf16 stores of a 2 x 4-wave-layout accumulator tile (the fused BN apply outputs; row-major, ld):
+// staged through each wave's LDS region like ring_store_tile's bf16 path, 16-B stores
+template <int BM_, int BN_>
+__device__ __forceinline__ void ring_store16(f32x4 (&v)[BM_ / 32][BN_ / 64], bf16* out, long long ld, int N, int m0,
+                                             int n0, int mlim, char* smem_raw) {
+  constexpr int TWM = BM_ / 2, TWN = BN_ / 4, NJ = TWN / 16, RP = TWN + 4, MI = TWM / 16, NCH = (MI + 3) / 4;
+  constexpr int L8 = TWN / 8, R8 = 64 / L8;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  float* reg = reinterpret_cast<float*>(smem_raw) + wid * 64 * RP;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int rlim = min(mlim, m0 + wm * TWM + min(TWM, ch * 64 + 64));
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (ch * 4 + ii < MI) reg[(ii * 16 + 4 * (lane >> 4) + e) * RP + j * 16 + (lane & 15)] = v[ch * 4 + ii][j][e];
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 64 / R8; ++it) {
+      const int lr = it * R8 + lane / L8, c8 = lane % L8;
+      const int row = m0 + wm * TWM + ch * 64 + lr, col = n0 + wn * TWN + 8 * c8;
+      if (row >= rlim || col >= N) continue;
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(reg + lr * RP + 8 * c8);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(reg + lr * RP + 8 * c8 + 4);
+      bf16* o = out + (long long)row * ld + col;
+      if (col + 7 < N && (ld & 7) == 0) {
+        *reinterpret_cast<bf16x8*>(o) = bf16x8{(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3],
+                                               (bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
+      } else {
+        for (int k = 0; k < 8 && col + k < N; ++k) o[k] = (bf16)(k < 4 ? v0[k] : v1[k - 4]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // LDS bytes the staged stores need (ring_store_tile): per wave 64 rows x (TWN + 4) fp32
 template <int BM_, int BN_>
 constexpr size_t ring_epi_lds() {
@@ -426,6 +502,7 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
 // y prefetch of the tile: 4 x 16 B per thread, issued at kernel start into registers so it lands
 // under the K loop (a load-then-store loop in the epilogue had serialised four HBM round trips)
 constexpr int BNB_YQ = 128 * 16 / RNT;  // 16-B chunks per thread (128 rows x 16 chunks of 8 bf16)
+constexpr int BNB_YS = 80 * 1024;        // LDS offset of the staged y tile (128 rows x 272 B + flag)
 __device__ __forceinline__ void ring_bnb_prefetch(const GemmArgs& g, int m0, int n0, u32x4 (&yv)[BNB_YQ]) {
   const bf16* yb = static_cast<const bf16*>(g.bnb_y);
   // unconditional loads at clamped addresses (N % 8 == 0 on this path), zeroed after: a load inside
@@ -450,7 +527,8 @@ __device__ __forceinline__ bool ring_bnb_epilogue(const GemmArgs& g, f32x4 (&acc
   const avcbn::BwdFin& f = g.bnb_fin;
   float* red = reinterpret_cast<float*>(smem_raw);  // [3][2 wm][BN_] / the finalize's [3][FGR][BN_]
   constexpr int YP = 2 * BN_ + 16;                  // LDS row pitch of the staged y tile (bytes)
-  char* ys = smem_raw + 8192;
+  // above the staged stores' LDS (ring_epi_lds: 72 KiB): the fused apply reads y again after them
+  char* ys = smem_raw + BNB_YS;
   unsigned* flag = reinterpret_cast<unsigned*>(ys + 128 * YP);
   __syncthreads();  // the K loop's fragment reads are done with the LDS
 #pragma unroll
@@ -515,7 +593,52 @@ __device__ __forceinline__ bool ring_bnb_epilogue(const GemmArgs& g, f32x4 (&acc
     }
   }
   const int nrb = (g.M + 127) / 128;
+  if (g.bnb_dy16) return ring_arrive_hold(g.bnb_cnt + n0 / BN_, (unsigned)nrb, 1u, flag);
   return ring_arrive_last(g.bnb_cnt + n0 / BN_, (unsigned)nrb, 1u, flag);
+}
+
+// The fused apply of the BatchNorm backward (avc_bnb_args.dy_bf16): after the column-tile barrier,
+// dy = k1*(dz - m1 - yc*rs*m2) from this tile's dL/da (the accumulators, rounded like the stored C),
+// y (still staged in LDS) and the constants -- the arithmetic of bn_bwd_apply_rows_kernel, so the
+// result is the apply pass's bit for bit
+__device__ __forceinline__ void ring_bnb_apply(const GemmArgs& g, f32x4 (&acc)[4][2], int m0, int n0, char* smem_raw) {
+  constexpr int NJ = 2, YP = 2 * 128 + 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int rbase = m0 + wm * 64 + 4 * (lane >> 4);
+  const int cbase = n0 + wn * 32 + (lane & 15);
+  const avcbn::BwdFin& f = g.bnb_fin;
+  const char* ys = smem_raw + BNB_YS;
+  const bool round16 = g.c == nullptr;
+  const int C = g.N;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int col = cbase + j * 16;
+    const bool cv = col < C;
+    const int cc = cv ? col : 0;
+    const float rs = f.rstd[cc], mu = f.mean[cc];
+    const float k1 = (f.gamma ? f.gamma[cc] : 1.f) * rs;
+    const float bt = f.beta ? f.beta[cc] : 0.f;
+    const float m1 = ld_sc1(f.coef + C + cc), m2 = ld_sc1(f.coef + 2 * C + cc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = rbase + i * 16 + e;
+        float v = acc[i][j][e];
+        if (round16) v = (float)(bf16)v;
+        const float yf = (cv && row < g.M)
+                             ? __builtin_bit_cast(float, (unsigned)*reinterpret_cast<const unsigned short*>(
+                                                             ys + (row - m0) * YP + (col - n0) * 2)
+                                                             << 16)
+                             : 0.f;
+        const float yc = yf - mu;
+        const float dz = act_bwd_from_pre(v, yc * k1 + bt, g.bnb_act);
+        acc[i][j][e] = k1 * (dz - m1 - yc * rs * m2);
+      }
+  }
+  __syncthreads();  // every wave is done with the y tile before the staged stores reuse the LDS
+  ring_store16<128, 128>(acc, g.bnb_dy16, g.N, g.N, m0, n0, g.M, smem_raw);
 }
 
 // the last-arriving row tile of a column tile: the apply constants and parameter gradients of its
@@ -549,7 +672,8 @@ __device__ __forceinline__ void ring_bnb_finalize(const GemmArgs& g, int n0, cha
         a1 += red[(1 * FGR + k) * BN_ + cl];
         a2 += red[(2 * FGR + k) * BN_ + cl];
       }
-      avcbn::bwd_finalize_store(c, a0, a1, a2, g.M, g.N, f);
+      if (g.bnb_dy16) avcbn::bwd_finalize_store<true>(c, a0, a1, a2, g.M, g.N, f);
+      else avcbn::bwd_finalize_store(c, a0, a1, a2, g.M, g.N, f);
     }
   }
 }
@@ -606,6 +730,12 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
     if (bnb_last) {
       __syncthreads();  // the staged stores are done with the LDS
       ring_bnb_finalize(g, n0, smem_raw);
+    }
+    if (g.bnb_ws && g.bnb_dy16) {
+      unsigned* cnt = g.bnb_cnt + n0 / BN_;
+      if (bnb_last) ring_release(cnt);
+      else ring_wait(cnt, g.fault, g.nap);
+      ring_bnb_apply(g, acc, m0, n0, smem_raw);
     }
   }
   if (g.bn_partial) {
@@ -687,8 +817,36 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
     if (g.bn_cnt) {
       const int ntile = (g.M + srows - 1) / srows;
       const int mine = min(NH, ntile - mt0);
-      if (ring_arrive_last(g.bn_cnt + n0 / BN_, (unsigned)ntile, (unsigned)mine, flag))
-        bn_finalize_cols<BN_>(g, n0, red);
+      unsigned* cnt = g.bn_cnt + n0 / BN_;
+      if (!g.bn_apply16) {
+        if (ring_arrive_last(cnt, (unsigned)ntile, (unsigned)mine, flag)) bn_finalize_cols<BN_>(g, n0, red);
+      } else {
+        // fused apply (avc_bn_fin.apply_bf16): act(y*scale + shift) of this tile once the column tile's
+        // statistics are final -- y as stored (bf16-rounded when C is bf16 only), bn_apply_kernel's
+        // arithmetic
+        if (ring_arrive_hold(cnt, (unsigned)ntile, (unsigned)mine, flag)) {
+          bn_finalize_cols<BN_>(g, n0, red);
+          ring_release(cnt);
+        } else {
+          ring_wait(cnt, g.fault, g.nap);
+        }
+        const bool round16 = g.c == nullptr;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int col = cbase + j * 16;
+          const int cc = col < g.N ? col : 0;
+          const float sc = ld_sc1(g.bn_scale + cc), sh = ld_sc1(g.bn_shift + cc);
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float v = acc[i][j][e];
+              if (round16) v = (float)(bf16)v;
+              acc[i][j][e] = act_fwd(v * sc + sh, g.bn_act);
+            }
+        }
+        ring_store16<BM_, BN_>(acc, g.bn_apply16, g.N, g.N, m0, n0, mlim, smem_raw);
+      }
     }
   }
 }
@@ -1678,8 +1836,28 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
   return r;
 }
 
-bool gemm_ring_launch_(const GemmArgs& g, hipStream_t s) {
+thread_local bool g_ring_applied = false;
+bool gemm_ring_applied() { return g_ring_applied; }
+
+int ring_num_cus() {
+  static int n = [] {
+    int dev = 0;
+    hipDeviceProp_t p;
+    return (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ? p.multiProcessorCount
+                                                                                                : 0;
+  }();
+  return n;
+}
+
+bool gemm_ring_launch_(const GemmArgs& g_in, hipStream_t s) {
   const RingCfg& c = g_ring;
+  g_ring_applied = false;
+  // the fused BN apply outputs only on the halo convs below (one workgroup per CU, every row tile
+  // of a column tile resident for the barrier); every other launch gets them cleared
+  GemmArgs g = g_in;
+  const bool want_apply = (g.bn_apply16 && g.bn_cnt && g.bn_partial) || (g.bnb_dy16 && g.bnb_ws);
+  g.bn_apply16 = nullptr;
+  g.bnb_dy16 = nullptr;
   if (c.mode == 0 || (g.a.win && !c.win)) return false;
   if (g.K % 8 || g.klen % RBK || g.atomic || g.cperm) return false;  // (no atomic / cperm stores)
   if (g.ctr && ((reinterpret_cast<uintptr_t>(g.c) & 15) || (reinterpret_cast<uintptr_t>(g.res) & 15) ||
@@ -1710,7 +1888,15 @@ bool gemm_ring_launch_(const GemmArgs& g, hipStream_t s) {
                    T > CV_TM && T <= CU_TM && g.M % T == 0 && g.N >= 128 && !g.bnb_ws && !g.c16_act && !g.agrad &&
                    !g.csum && !g.ctr && (!g.bn_partial || g.bn_cnt) && !c.abl && !c.ws && c.utt;
   if (utt) {
-    launch_conv_utt(g, c.gm, s);
+    const int nb = (g.M / T) * ((g.N + CV_TN - 1) / CV_TN);
+    if (want_apply && g_in.bn_apply16 && nb <= ring_num_cus()) {
+      GemmArgs ga = g;
+      ga.bn_apply16 = g_in.bn_apply16;
+      launch_conv_utt(ga, c.gm, s);
+      g_ring_applied = true;
+    } else {
+      launch_conv_utt(g, c.gm, s);
+    }
     g_ring_last = 3;
     return true;
   }
@@ -1722,8 +1908,21 @@ bool gemm_ring_launch_(const GemmArgs& g, hipStream_t s) {
     else if (c.abl == 5) launch_conv<true, 5>(g, c.gm, s);
     else if (c.abl == 6) launch_conv<true, 6>(g, c.gm, s);
     else if (g.bnb_ws) {  // the BN-backward reduction epilogue (8-wave tile only)
-      if (a.t_out % CV_TM == 0) launch_conv<true, 0, true>(g, c.gm, s);
-      else launch_conv<false, 0, true>(g, c.gm, s);
+      const int nb = ((g.M + CV_TM - 1) / CV_TM) * ((g.N + CV_TN - 1) / CV_TN);
+      GemmArgs ga = g;
+      if (want_apply && g_in.bnb_dy16 && nb <= ring_num_cus()) {
+        ga.bnb_dy16 = g_in.bnb_dy16;
+        g_ring_applied = true;
+      }
+      if (a.t_out % CV_TM == 0) launch_conv<true, 0, true>(ga, c.gm, s);
+      else launch_conv<false, 0, true>(ga, c.gm, s);
+    } else if (!c.ws && want_apply && g_in.bn_apply16 &&
+               ((g.M + CV_TM - 1) / CV_TM) * ((g.N + CV_TN - 1) / CV_TN) <= ring_num_cus()) {
+      GemmArgs ga = g;
+      ga.bn_apply16 = g_in.bn_apply16;
+      if (a.t_out % CV_TM == 0) launch_conv<true>(ga, c.gm, s);
+      else launch_conv<false>(ga, c.gm, s);
+      g_ring_applied = true;
     } else if (c.ws) {
       if (a.t_out % CV_TM == 0) launch_conv_ws<true>(g, c.gm, s);
       else launch_conv_ws<false>(g, c.gm, s);

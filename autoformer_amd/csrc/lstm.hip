@@ -1651,6 +1651,8 @@ void launch_small_bwd(dim3 g, hipStream_t s, bool fast, const float* dh, const f
 
 }  // namespace
 
+unsigned* avc_fault_ptr() { return fault_word(); }
+
 extern "C" int avc_lstm_trace(void* buf) {
   g_trace = reinterpret_cast<unsigned long long*>(buf);
   return 0;

@@ -92,7 +92,8 @@ def operand(t: torch.Tensor, ld: int, kstrided: bool = False, window=None, batch
 
 def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=None, accumulate=False, split_k=1,
          bn_partial=None, batch=1, c_batch_stride=0, comp=None, c_bf16=None, residual=None, cperm=0, bn_fin=None,
-         bnb=None, row_bias=None, c_bf16_act=0, act_grad_of=None, col_sum=None, col_sum_n=0, c_trans_rows=0):
+         bnb=None, row_bias=None, c_bf16_act=0, act_grad_of=None, col_sum=None, col_sum_n=0, c_trans_rows=0,
+         bn_apply=None, bnb_dy=None):
     """cperm = taps > 1: C's columns are (tap, channel) pairs written in nn.Conv1d's [Co][Ci][K]
     weight layout (a conv weight gradient straight into .grad).
     bn_fin = (gamma, beta, running_mean, running_var, nbt, momentum, eps, nupd): the BatchNorm
@@ -105,7 +106,10 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     fp32, or bf16 (avc_gemm_desc.c_pre_bf16) when c is a bf16 tensor; act_grad_of = x (fp32 or
     bf16): C *= GELU'(x) -- the MLP-Mixer GELU forward / backward folded into the GEMM epilogue.
     col_sum: col_sum[:col_sum_n or N] += column sums of C (a bias gradient, float atomics).
-    c_trans_rows = R: every R-row block of C stored transposed (avc_gemm_desc.c_trans_rows)."""
+    c_trans_rows = R: every R-row block of C stored transposed (avc_gemm_desc.c_trans_rows).
+    bn_apply = (out16, act) with bn_fin: act(y*scale + shift) into the bf16 out16 as well (avc_bn_fin.apply_bf16);
+    bnb_dy = dy16 with bnb: the producing layer's dy into the bf16 dy16 as well (avc_bnb_args.dy_bf16) --
+    fused into the halo conv's epilogue where it runs, a pass after the GEMM otherwise."""
     # every pointer argument must be device memory (operands are checked by operand()); a CPU
     # tensor would reach the kernel as a host pointer and fault the GPU instead of raising here
     _dev(c, bias, residual, c_bf16, bn_partial)
@@ -171,6 +175,10 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
         bb.dgamma, bb.dbeta, bb.dbias, bb.accumulate = _ptr(dgamma), _ptr(dbeta), _ptr(dbias), int(acc)
         ws = torch.empty(int(L.lib().avc_gemm_bnb_ws(int(M), int(N))), device=y.device)
         bb.ws = ws.data_ptr()
+        if bnb_dy is not None:
+            _dev(bnb_dy)
+            assert bnb_dy.dtype == torch.bfloat16 and bnb_dy.shape == (M, N)
+            bb.dy_bf16 = bnb_dy.data_ptr()
         L.call("avc_gemm_bnb", d, bb, stream())
         return None
     if bn_fin is None:
@@ -184,6 +192,11 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
                                                                             _ptr(rvar), _ptr(nbt))
     f.momentum, f.eps, f.nupd = float(momentum), float(eps), int(nupd)
     f.mean, f.rstd, f.scale, f.shift = (t.data_ptr() for t in stats)
+    if bn_apply is not None:
+        out16, act = bn_apply
+        _dev(out16)
+        assert out16.dtype == torch.bfloat16 and out16.shape == (M, N)
+        f.apply_bf16, f.apply_act = out16.data_ptr(), int(act)
     L.call("avc_gemm_bn", d, f, stream())
     return stats
 
@@ -361,7 +374,9 @@ class DeviceFault(RuntimeError):
 
 
 FAULT_BITS = {1: "persistent LSTM recurrence spin timeout (a workgroup of the grid was not resident or stalled; "
-                 "the step's outputs are invalid)"}
+                 "the step's outputs are invalid)",
+              2: "fused BatchNorm apply: column-tile barrier timeout in a halo conv epilogue (the step's outputs "
+                 "are invalid)"}
 
 
 def raise_on_fault(value):

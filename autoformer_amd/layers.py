@@ -498,20 +498,27 @@ class ConvBNCore:
         Co = conv.weight.shape[0]
         bf = K.compute() == K.BF16
         y = torch.empty(M, Co, device=dev, dtype=torch.bfloat16 if bf else torch.float32)
+        a = None
         if bn.training:
             # batch statistics from the epilogue, finalized by the GEMM's last row tiles; the
-            # running statistics take stat_updates updates (the *_Adjust double pass)
+            # running statistics take stat_updates updates (the *_Adjust double pass).  A bf16-only
+            # activation without residual comes out of the same call (avc_bn_fin.apply_bf16: the halo
+            # conv applies BN + act in its epilogue behind a column-tile barrier)
             partial = K.bn_partial_buffer(M, Co, dev)
             nbt = bn.num_batches_tracked if bn.track_running_stats else None
             mom = bn.momentum if bn.momentum is not None else 0.1
+            fused = _BN_APPLY_FUSED and out_bf16 and bf and residual is None
+            a = torch.empty(M, Co, device=dev, dtype=torch.bfloat16) if fused else None
             stats = K.gemm(M, Co, Kdim, xop, wop, y, bias=conv.bias, bn_partial=partial,
                            bn_fin=(bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, mom, bn.eps,
-                                   self.stat_updates), row_bias=row_bias)
+                                   self.stat_updates), row_bias=row_bias,
+                           bn_apply=(a, self.act) if fused else None)
         else:
             K.gemm(M, Co, Kdim, xop, wop, y, bias=conv.bias, row_bias=row_bias)
             stats = K.bn_eval(bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.eps)
         mean, rstd, scale, shift = stats
-        a = K.bn_apply(y, scale, shift, self.act, residual, out_bf16=out_bf16 and bf and residual is None)
+        if a is None:
+            a = K.bn_apply(y, scale, shift, self.act, residual, out_bf16=out_bf16 and bf and residual is None)
         return a, (y, mean, rstd, T_out)
 
     def bn_grad(self, dA, saved, self_link=None):
@@ -523,13 +530,15 @@ class ConvBNCore:
         conv, bn = self.conv, self.bn
         dy_bf16 = K.compute() == K.BF16
         if self_link is not None and self_link.coef is not None:
-            # statistics (and the parameter gradients) came from the consumer's GEMM epilogue
+            # statistics (and the parameter gradients) came from the consumer's GEMM epilogue, and
+            # dy too (avc_bnb_args.dy_bf16) when the link asked for it
             if dA.data_ptr() != self_link.dA_ptr:
                 raise RuntimeError("fused BatchNorm backward: dL/da is not the linked consumer's data gradient "
                                    "(the output was used twice?)")
-            dy = K.bn_bwd_apply(dA, y, self_link.coef, self.act, dy_bf16=dy_bf16)
+            dy = self_link.dy if self_link.dy is not None else K.bn_bwd_apply(dA, y, self_link.coef, self.act,
+                                                                              dy_bf16=dy_bf16)
             dgamma, dbeta, dbias = self_link.grads
-            self_link.coef = None
+            self_link.coef = self_link.dy = None
             return dy, dgamma, dbeta, dbias
         into = (_grad_of(bn.weight), _grad_of(bn.bias), _grad_of(conv.bias)) if _SINK["on"] else None
         # act' from the recomputed pre-activation: the activation output `a` is not re-read
@@ -574,7 +583,7 @@ class ConvBNCore:
             dx = torch.empty(B * T_in, n_dx, device=x.device, dtype=x.dtype)
             bnb = prev_link.gemm_args(B * T_in, n_dx, sink) if prev_link is not None and n_dx == Ci else None
             K.gemm(B * T_in, n_dx, Kw * Co, operand(dy, Co, window=(Kw, Kw - 1 - self.pad, T_in, T_out, Co)),
-                   operand(Wd, Kw * Co), dx, bnb=bnb)
+                   operand(Wd, Kw * Co), dx, bnb=bnb, bnb_dy=prev_link.dy if bnb is not None else None)
             if bnb is not None:
                 prev_link.dA_ptr = dx.data_ptr()
         if sink and (n_dx or not _LAST_WGRAD_MAIN):
@@ -602,11 +611,11 @@ class BnbLink:
     and finalize launches of nn.BatchNorm1d.backward's statistics (AutoVC.py:38,91,138,154,169)
     are gone.  One-shot per forward."""
 
-    __slots__ = ("core", "saved", "coef", "dA_ptr", "grads")
+    __slots__ = ("core", "saved", "coef", "dA_ptr", "grads", "dy")
 
     def __init__(self, core, saved):
         self.core, self.saved = core, saved
-        self.coef, self.dA_ptr, self.grads = None, None, (None, None, None)
+        self.coef, self.dA_ptr, self.grads, self.dy = None, None, (None, None, None), None
 
     def gemm_args(self, M, C, sink):
         core = self.core
@@ -623,6 +632,8 @@ class BnbLink:
             dbi = torch.empty(C, device=dev) if conv.bias is not None else None
             self.grads = (dg, db, dbi)
         self.coef = torch.empty(6 * C, device=dev)
+        # the layer's dy (bf16) from the same GEMM (avc_bnb_args.dy_bf16; on the halo conv: its epilogue)
+        self.dy = torch.empty(M, C, device=dev, dtype=torch.bfloat16) if _BN_BWD_APPLY_FUSED else None
         return (y, mean, rstd, bn.weight, bn.bias, core.act, self.coef, dg, db, dbi, int(sink))
 
 
@@ -645,6 +656,14 @@ def _links(ctx, x, core, a, saved, fuse_prev):
 # ring's ring_bnb_epilogue, aligned T only -- see _links): on since round 5 (C2 5.74 -> 5.67 ms,
 # profiles/r5_bnb_ab.txt); "0": the separate reduce / finalize passes
 _BNB_ON = os.environ.get("AVC_BNB", "1") != "0"
+# the BatchNorm apply passes in the same GEMM call (avc_bn_fin.apply_bf16 / avc_bnb_args.dy_bf16: on the
+# halo conv ring inside its epilogue behind a column-tile barrier, elsewhere a pass after the GEMM).
+# Measured slower in the C2 step (profiles/r5_bn_apply_fused_ab.txt: the barrier adds ~12 us per conv
+# against a 6 us apply pass; beside the side stream the waiting row tiles also hold their CUs), so off:
+# "1" both, "fwd" / "bwd" one side, "0" (default) the separate bn_apply / bn_bwd_apply calls
+_BN_APPLY_MODE = os.environ.get("AVC_BN_APPLY_FUSED", "0")
+_BN_APPLY_FUSED = _BN_APPLY_MODE in ("1", "fwd")
+_BN_BWD_APPLY_FUSED = _BN_APPLY_MODE in ("1", "bwd")
 
 
 class _ConvBNFn(torch.autograd.Function):

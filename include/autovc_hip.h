@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 25
+#define AVC_ABI_VERSION 26
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -137,6 +137,11 @@ typedef struct {
   float* dbias;
   int accumulate;
   float* ws;
+  /* nullable (ABI 26): the layer's dy (bf16, avc_bn_bwd_apply's output with these constants) is
+   * written too -- by the epilogue itself on the halo conv ring, whose row tiles of a column tile
+   * are all resident (a column-tile barrier after the last row tile's finalize), else by an apply
+   * pass after the GEMM.  y bf16, N % 8 == 0 on the fused form. */
+  void* dy_bf16;
 } avc_bnb_args;
 
 size_t avc_gemm_bnb_ws(int M, int N);
@@ -174,6 +179,10 @@ typedef struct {
   float* rstd;
   float* scale;
   float* shift;
+  /* nullable (ABI 26): act(y*scale + shift) in bf16 (avc_bn_apply without residual, ldc == N) written
+   * too -- by the halo conv ring's epilogue behind a column-tile barrier, else by a pass after. */
+  void* apply_bf16;
+  int apply_act;
 } avc_bn_fin;
 int avc_gemm_bn(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream);
 
