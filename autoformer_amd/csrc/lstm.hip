@@ -1102,7 +1102,7 @@ struct PersistBwdArgs {
   unsigned spin;
   int nap;
   int B, T, ng;
-  int abl;  // diagnostic (AVC_LSTM_BWD_ABL=1): gather the group's payload twice per step -- the
+  int abl;  // diagnostic (AVC_LSTM_BWD_ABL=n): gather the group's payload 1 + n times per step -- the
             // 128 KB per consumer a 16-utterance group would read
 };
 
@@ -1175,7 +1175,7 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
         __syncthreads();
         if (*quit) return;  // block-uniform exit after a spin timeout
         load_group<G, NCH, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
-        if (a.abl & 1) {
+        for (int k = 0; k < a.abl; ++k) {  // AVC_LSTM_BWD_ABL=n: n extra gathers (diagnostic)
           __syncthreads();
           load_group<G, NCH, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
         }
