@@ -1490,6 +1490,236 @@ __global__ void __launch_bounds__(PNT, 1) lstm2_persist_fwd(Persist2Args a) {
   if (w > 0) lstm2_store_outputs<H>(a, outs, T, b0, j0);  // the last tick's (staged above its barrier)
 }
 
+// =============================================================== two stacked layers, backward
+// Decoder lstm2 backward as a layer WAVEFRONT (the forward's mirror): tick k runs layer 1 at step
+// T-1-k and layer 0 at step T-k, so one hand-off per tick serves both layers, and layer 1's input
+// gradient dX1 = dG1 W_ih1 -- layer 0's upstream gradient -- is formed inside the recurrence (no
+// 8192 x 1024 x 4096 GEMM between two single-layer launches).  Tick k hands over dG1 and dG0 of
+// tick k-1 (2 x 16 x 4H bf16 = 256 KB per consumer); member r owns units j0..j0+15 of EACH layer:
+//   dh1_t  = dG1_{t+1} W_hh1[:, j] + dL/dh1_t (upstream)
+//   dh0_t' = dG0_{t'+1} W_hh0[:, j] + dG1_{t'} W_ih1[:, j]       (t' = t + 1: dG1_{t'} = the same payload)
+// so each member keeps three 4H x 16 slices (W_hh1^T, W_ih1^T, W_hh0^T rows j0..) as MFMA B fragments:
+// 40 in VGPRs and 8 per wave in LDS.  The payload does not fit the LDS as one A tile: it is staged
+// in four 64 KB K-chunks (both layers' 16 rows x 1024 gate rows), the loads of chunk c + 1 in flight
+// under chunk c's products; wave w takes k-blocks 4w .. 4w+3 of every chunk, and the eight waves'
+// partial 16 x 16 products meet in LDS.  Thread tid is the cell (layer tid >> 8, utterance
+// (tid >> 4) & 15, unit tid & 15); dc stays in its register.  Hand-off: the forward's write-through
+// flag form, one flag per member per tick for both layers' tiles.
+struct Persist2BwdArgs {
+  const float* dhout1;  // (B,T,H) dL/dh of the top layer's output
+  const float* call[2];  // (B,T,H) cell states of layer 0 / 1
+  const float* gall[2];  // (B,T,4H) activated gates
+  const bf16* wt0;       // W_hh0^T [H][4H]
+  const bf16* wti1;      // W_ih1^T [H][4H]
+  const bf16* wt1;       // W_hh1^T [H][4H]
+  float* dg[2];          // (B,T,4H) dL/d(pre-activation gates)
+  bf16* dg16[2];
+  unsigned* ctl;
+  bf16* pay;  // [layer][2 parities][B][4H]
+  unsigned long long* trace;
+  unsigned* fault;
+  unsigned spin;
+  int B, T, ng;
+};
+
+constexpr int BKC = 1024, BNC = 4, BCP = BKC + 8, BNLW = 3;  // K-chunk, chunks, LDS pitch, W_hh0 frags in LDS
+
+// two chunk tiles (LDS-DMA double buffer; the wave partials and the publish tile reuse the first after
+// the last chunk), then the LDS-resident weight fragments
+template <int H>
+constexpr size_t persist2_bwd_lds() {
+  return (size_t)2 * 2 * QRG * BCP * 2 + (size_t)8 * BNLW * 64 * 16 + 16;
+}
+
+__device__ __attribute__((aligned(16))) unsigned g_zero16_l2[4] = {0u, 0u, 0u, 0u};
+typedef __attribute__((address_space(3))) void* l2_lds_ptr;
+typedef const __attribute__((address_space(1))) void* l2_gbl_ptr;
+// 16-B LDS fragment read as inline asm: the compiler's waitcnt pass would otherwise wait for every
+// LDS-DMA in flight (the next chunk's) before it
+__device__ __forceinline__ bf16x8 l2_ds_read16(unsigned addr) {
+  u32x4_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int H>
+__global__ void __launch_bounds__(PNT, 1) lstm2_persist_bwd(Persist2BwdArgs a) {
+  constexpr int G = 4 * H, NR = H / QJU, KPW = BKC / 32 / 8, NF0 = BNC * KPW - BNLW;
+  constexpr int CB = 2 * QRG * BCP * 2;  // bytes of one chunk tile
+  static_assert(G == BNC * BKC && 2 * QRG * 2 == 8 * 8 && NR <= 64 && NF0 > 0, "wavefront tiling");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  float* red = reinterpret_cast<float*>(smem_raw);                     // [w][L][16][16] (in tile 0)
+  bf16* ds16 = reinterpret_cast<bf16*>(red + 8 * 2 * QRG * QJU);       // [L][16][4 gates x 16] (in tile 0)
+  bf16x8* wlb = reinterpret_cast<bf16x8*>(smem_raw + 2 * CB);          // [w][BNLW][64]
+  int* quit = reinterpret_cast<int*>(wlb + 8 * BNLW * 64);
+  static_assert((8 * 2 * QRG * QJU * 4 + 2 * QRG * 4 * QJU * 2) <= CB, "partials fit a chunk tile");
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = blockIdx.x % a.ng, r = blockIdx.x / a.ng;
+  const int j0 = r * QJU, b0 = g * QRG;
+  const int T = a.T, B = a.B, rows = min(QRG, B - b0);
+  const __amdgpu_buffer_rsrc_t pay = rsrc_of(a.pay, (long long)4 * B * G * 2);
+  unsigned* flags = a.ctl + 4 + g * PFL;
+
+  // B fragments: column n = unit j0 + (lane & 15), k = gate row c*BKC + (w*KPW + i)*32 + 8*(lane >> 4)
+  bf16x8 f1[BNC][KPW], fi[BNC][KPW], f0[NF0];
+  bf16x8* wl = wlb + (w * BNLW) * 64 + lane;
+  {
+    const long long ro = (long long)(j0 + (lane & 15)) * G + 8 * (lane >> 4);
+#pragma unroll
+    for (int c = 0; c < BNC; ++c)
+#pragma unroll
+      for (int i = 0; i < KPW; ++i) {
+        const long long o = ro + c * BKC + (w * KPW + i) * 32;
+        f1[c][i] = *reinterpret_cast<const bf16x8*>(a.wt1 + o);
+        fi[c][i] = *reinterpret_cast<const bf16x8*>(a.wti1 + o);
+        const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(a.wt0 + o);
+        const int idx = c * KPW + i;
+        if (idx < NF0) f0[idx < NF0 ? idx : 0] = v0;
+        else wl[(idx - NF0) * 64] = v0;
+      }
+  }
+  // this wave's 8 LDS-DMA fills per chunk: q = 8w + i -> layer q >> 5, row (q >> 1) & 15, half q & 1
+  // (1 KiB = 512 gate rows): wave-uniform bases + the lane's 16-B offset; rows past the batch read
+  // the zero granule
+  const long long slot_el = (long long)B * G;  // parity slot stride (elements)
+  auto issue = [&](int c, int slot) {
+    char* tile = smem_raw + (c & 1) * CB;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int q = 8 * w + i, l = q >> 5, row = (q >> 1) & 15, half = q & 1;
+      const bf16* src = row < rows ? a.pay + ((long long)(l * 2 + slot) * B + b0 + row) * G + c * BKC + half * 512 +
+                                         lane * 8
+                                   : reinterpret_cast<const bf16*>(g_zero16_l2);
+      __builtin_amdgcn_global_load_lds((l2_gbl_ptr)src, (l2_lds_ptr)(tile + ((l * QRG + row) * BCP + half * 512) * 2),
+                                       16, 0, AUX_SC1);
+    }
+  };
+  if (tid == 0) *quit = 0;
+  const int L = tid >> 8, cr = (tid >> 4) & 15, cu = tid & 15, cb = b0 + cr, cj = j0 + cu;
+  const bool cv = cb < B;
+  const unsigned aoff = (unsigned)(((lane & 15) * BCP + w * KPW * 32 + 8 * (lane >> 4)) * 2);
+  float dc = 0.f;
+  __syncthreads();
+
+  for (int k = 0; k <= T; ++k) {
+    const int t = L == 1 ? T - 1 - k : T - k;  // this thread's step
+    const bool act = (L == 1 ? k < T : k >= 1) && cv;
+    if (k < T) stamp(a.trace, T, k, 0);
+    // per-cell inputs of this step (independent of the exchange: issued first)
+    float dhu = 0.f, ct = 0.f, cp = 0.f, gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f;
+    if (act) {
+      const long long oh = ((long long)cb * T + t) * H + cj;
+      if (L == 1) dhu = a.dhout1[oh];
+      ct = a.call[L][oh];
+      cp = t > 0 ? a.call[L][oh - H] : 0.f;
+      const float* gp = a.gall[L] + ((long long)cb * T + t) * G + cj;
+      gi = gp[0];
+      gf = gp[H];
+      gg = gp[2 * H];
+      go = gp[3 * H];
+    }
+    f32x4 p1 = {0.f, 0.f, 0.f, 0.f}, p0 = {0.f, 0.f, 0.f, 0.f};
+    if (k > 0) {
+      if (w == 0 && !poll_flags(flags, NR, (unsigned)k, a.ctl, a.fault, a.spin)) *quit = 1;
+      __syncthreads();
+      if (*quit) return;  // block-uniform exit after a spin timeout
+      const int slot = (k - 1) & 1;
+      issue(0, slot);
+      issue(1, slot);
+#pragma unroll
+      for (int c = 0; c < BNC; ++c) {
+        // this wave's fills of chunk c have landed (the next chunk's 8 may be in flight), then
+        // every wave's
+        if (c < BNC - 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_barrier" ::: "memory");
+        const unsigned base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)(smem_raw + (c & 1) * CB) + aoff;
+        // XB k-blocks of A fragments at a time (the weight fragments hold ~180 VGPRs)
+        constexpr int XB = 1;
+#pragma unroll
+        for (int i2 = 0; i2 < KPW; i2 += XB) {
+          bf16x8 x0[XB], x1[XB];
+#pragma unroll
+          for (int i = 0; i < XB; ++i) {
+            x0[i] = l2_ds_read16(base + 64 * (i2 + i));
+            x1[i] = l2_ds_read16(base + QRG * BCP * 2 + 64 * (i2 + i));
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < XB; ++i) {
+            const int idx = c * KPW + i2 + i;
+            const bf16x8 wb = idx < NF0 ? f0[idx < NF0 ? idx : 0] : wl[(idx >= NF0 ? idx - NF0 : 0) * 64];
+            p1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1[i], f1[c][i2 + i], p1, 0, 0, 0);
+            p0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1[i], fi[c][i2 + i], p0, 0, 0, 0);
+            p0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0[i], wb, p0, 0, 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        asm volatile("s_barrier" ::: "memory");  // every wave is done reading this tile
+        if (c + 2 < BNC) issue(c + 2, slot);
+      }
+    }
+    // wave partials -> LDS: red[((w * 2 + L) * 16 + row) * 16 + unit]
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[((w * 2 + 0) * QRG + 4 * (lane >> 4) + e) * QJU + (lane & 15)] = p0[e];
+      red[((w * 2 + 1) * QRG + 4 * (lane >> 4) + e) * QJU + (lane & 15)] = p1[e];
+    }
+    __syncthreads();
+    if (k < T) stamp(a.trace, T, k, 2);
+    float dh = dhu;
+#pragma unroll
+    for (int ww = 0; ww < 8; ++ww) dh += red[((ww * 2 + L) * QRG + cr) * QJU + cu];
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+    if (act) {
+      const float tc = ftanh(ct);
+      const float dcs = dc + dh * go * (1.f - tc * tc);
+      v0 = dcs * gg * gi * (1.f - gi);  // d(pre i)
+      v1 = dcs * cp * gf * (1.f - gf);  // d(pre f)
+      v2 = dcs * gi * (1.f - gg * gg);  // d(pre g)
+      v3 = dh * tc * go * (1.f - go);   // d(pre o)
+      dc = dcs * gf;
+    }
+    bf16* dsr = ds16 + (L * QRG + cr) * (4 * QJU) + cu;
+    dsr[0] = (bf16)v0;
+    dsr[QJU] = (bf16)v1;
+    dsr[2 * QJU] = (bf16)v2;
+    dsr[3 * QJU] = (bf16)v3;
+    __syncthreads();
+    // ---- publish dG1_{t1} and dG0_{t0} (needed by tick k + 1; none after tick T - 1): wave 0, four
+    // 16-B chunks per lane (2 layers x 16 rows x 8 chunks), then the flag
+    if (w == 0 && k < T) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ch = lane + 64 * i, l = ch >> 7, row = (ch >> 3) & 15, q8 = ch & 7;
+        if (row < rows) {
+          const u32x4_t pv = *reinterpret_cast<const u32x4_t*>(ds16 + (l * QRG + row) * (4 * QJU) + q8 * 8);
+          __builtin_amdgcn_raw_buffer_store_b128(
+              pv, pay, (((l * 2 + (k & 1)) * B + b0 + row) * G + (q8 >> 1) * H + j0 + (q8 & 1) * 8) * 2, 0, AUX_SC1);
+        }
+      }
+      raise_flag(flags, r, (unsigned)(k + 1));
+    }
+    if (act) {  // (wave 0 issues these after its flag: they stay off the hand-off's vmcnt wait)
+      const long long og = ((long long)cb * T + t) * G + cj;
+      float* d = a.dg[L] + og;
+      d[0] = v0;
+      d[H] = v1;
+      d[2 * H] = v2;
+      d[3 * H] = v3;
+      if (a.dg16[L]) {
+        bf16* d16 = a.dg16[L] + og;
+        d16[0] = (bf16)v0;
+        d16[H] = (bf16)v1;
+        d16[2 * H] = (bf16)v2;
+        d16[3 * H] = (bf16)v3;
+      }
+    }
+    if (k < T) stamp(a.trace, T, k, 3);
+  }
+}
+
 template <int H>
 constexpr size_t persist_bwd_lds() {
   return (size_t)(PRG + 1) * (4 * H + 8) * 2 + (size_t)(PNT / 64) * PRG * (PJU + 1) * 4 + (size_t)PRG * 4 * PJU * 2 +
@@ -1743,6 +1973,67 @@ extern "C" int avc_lstm2_fwd(const float* xproj0, const void* w_hh0, const void*
     default: lstm2_persist_fwd<1024, 2, 2, false><<<grid, PNT, lds, s>>>(p); break;
   }
   return avc_check_launch("avc_lstm2_fwd");
+}
+
+// Two-layer wavefront backward (lstm2_persist_bwd): shape, compute mode and residency.
+bool persist2_bwd_path(int B, int H, bool bf) {
+  if (!bf || H != 1024 || no_persist_env() || getenv("AVC_LSTM2_OFF") || getenv("AVC_LSTM2_BWD_OFF")) return false;
+  const int ng = (B + QRG - 1) / QRG, grid = ng * (H / QJU);
+  if (grid > num_cus()) return false;
+  static std::once_flag once[MAXDEV];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const void* fn = reinterpret_cast<const void*>(&lstm2_persist_bwd<1024>);
+  std::call_once(once[dev & (MAXDEV - 1)], [fn] {
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist2_bwd_lds<1024>());
+  });
+  return fits_resident(fn, PNT, persist2_bwd_lds<1024>(), grid);
+}
+
+extern "C" int avc_lstm2_bwd_persistent(int B, int H, int compute) {
+  return persist2_bwd_path(B, H, compute == AVC_BF16) ? 1 : 0;
+}
+
+extern "C" size_t avc_lstm2_bwd_scratch_bytes(int B, int H) {
+  if (B <= 0 || H <= 0) return 0;
+  return px_payload_off((B + QRG - 1) / QRG) + (size_t)32 * B * H;  // [2 layers][2 parities][B][4H] bf16
+}
+
+extern "C" int avc_lstm2_bwd(const float* dh1, const float* c0, const float* gates0, const float* c1,
+                             const float* gates1, const void* w_hh0_t, const void* w_ih1_t, const void* w_hh1_t, int B,
+                             int T, int H, float* dg0, void* dg0_bf16, float* dg1, void* dg1_bf16, void* buf,
+                             void* stream) {
+  AVC_CHECK_ARG(dh1 && c0 && gates0 && c1 && gates1 && w_hh0_t && w_ih1_t && w_hh1_t && dg0 && dg1 && buf && B > 0 &&
+                    T > 0,
+                "avc_lstm2_bwd: bad args");
+  AVC_CHECK_ARG(persist2_bwd_path(B, H, true), "avc_lstm2_bwd: shape B=%d H=%d not supported (see avc_lstm2_bwd_persistent)",
+                B, H);
+  hipStream_t s = as_stream(stream);
+  const int ng = (B + QRG - 1) / QRG;
+  Persist2BwdArgs p;
+  p.dhout1 = dh1;
+  p.call[0] = c0;
+  p.call[1] = c1;
+  p.gall[0] = gates0;
+  p.gall[1] = gates1;
+  p.wt0 = reinterpret_cast<const bf16*>(w_hh0_t);
+  p.wti1 = reinterpret_cast<const bf16*>(w_ih1_t);
+  p.wt1 = reinterpret_cast<const bf16*>(w_hh1_t);
+  p.dg[0] = dg0;
+  p.dg[1] = dg1;
+  p.dg16[0] = reinterpret_cast<bf16*>(dg0_bf16);
+  p.dg16[1] = reinterpret_cast<bf16*>(dg1_bf16);
+  p.ctl = reinterpret_cast<unsigned*>(buf);
+  p.pay = reinterpret_cast<bf16*>(reinterpret_cast<char*>(buf) + px_payload_off(ng));
+  p.trace = g_trace;
+  p.fault = fault_word();
+  p.spin = spin_bound();
+  p.B = B;
+  p.T = T;
+  p.ng = ng;
+  if (avc_zero_async(buf, px_ctl_bytes(ng), s)) return -1;
+  lstm2_persist_bwd<1024><<<dim3(ng * (H / QJU)), PNT, persist2_bwd_lds<1024>(), s>>>(p);
+  return avc_check_launch("avc_lstm2_bwd");
 }
 
 extern "C" size_t avc_lstm_bwd_scratch_bytes(int B, int H, int dirs) {

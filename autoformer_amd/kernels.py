@@ -443,6 +443,39 @@ def lstm2_fwd(xproj0, w_hh0, w_ih1, w_hh1, bias1, B, T, H):
     return attach_twin(h0, h0b), c0, g0, attach_twin(h1, h1b), c1, g1
 
 
+def lstm2_bwd_persistent(B, H):
+    """Whether avc_lstm2_bwd (both lstm2 layers' backward in one wavefront launch) applies."""
+    return bool(L.lib().avc_lstm2_bwd_persistent(int(B), int(H), _COMPUTE))
+
+
+def lstm2_bwd(dh1, c0, g0, c1, g1, wt0, wti1, wt1, B, T, H):
+    """Backward of the two stacked layers in one persistent launch: (dG0, dG1), each fp32 with its
+    bf16 twin.  wt0 / wti1 / wt1: W_hh0^T, W_ih1^T, W_hh1^T as bf16 [H][4H]."""
+    dev = dh1.device
+    fault_word(dev)
+    outs = [torch.empty(B * T, 4 * H, device=dev) for _ in range(2)]
+    o16 = [torch.empty(B * T, 4 * H, device=dev, dtype=torch.bfloat16) for _ in range(2)]
+    buf = torch.empty(int(L.lib().avc_lstm2_bwd_scratch_bytes(int(B), int(H))), device=dev, dtype=torch.uint8)
+    timed = LAUNCH_TIMING is not None and H == LAUNCH_TIMING_H
+    if timed:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+    rec = L._REC if H == LAUNCH_TIMING_H else None
+    if rec is not None:
+        box, s = [], torch.cuda.current_stream()
+        rec.add_marker(lambda: _timing_mark(box, s, 0))
+    L.call("avc_lstm2_bwd", dh1.data_ptr(), c0.data_ptr(), g0.data_ptr(), c1.data_ptr(), g1.data_ptr(), wt0.data_ptr(),
+           wti1.data_ptr(), wt1.data_ptr(), B, T, H, outs[0].data_ptr(), o16[0].data_ptr(), outs[1].data_ptr(),
+           o16[1].data_ptr(), buf.data_ptr(), stream())
+    if rec is not None:
+        rec.add_marker(lambda: _timing_mark(box, s, 1))
+    if timed:
+        ev[1].record()
+        LAUNCH_TIMING.append(ev)
+    _CACHE["lstm2_bwd_buf"] = buf  # kept alive until the next call (the launch is asynchronous)
+    return attach_twin(outs[0], o16[0]), attach_twin(outs[1], o16[1])
+
+
 def lstm_persistent_bwd(B, H, dirs):
     """Whether avc_lstm_bwd takes the one-launch persistent path (asked of lstm.hip)."""
     return bool(L.lib().avc_lstm_persistent(int(B), int(H), int(dirs), _COMPUTE, 1))

@@ -901,12 +901,14 @@ class LSTMLayerCore:
         h, c, g = K.lstm_fwd(xproj, whh, B, T, H, dirs, hbuf)
         return h, (c, g)
 
-    def backward(self, dh, x, h, saved, B, T, need_dx):
+    def backward(self, dh, x, h, saved, B, T, need_dx, dg=None):
+        """dg: the gate gradients when a fused launch already produced them (the lstm2 wavefront)."""
         c, g = saved
         H, dirs = self.H, self.dirs
         In = x.shape[1]
         wih, _, whh, whh_t, wih_t = self.packs()
-        dg = K.lstm_bwd(dh, h, c, g, whh if H <= 64 else None, whh_t, B, T, H, dirs)
+        if dg is None:
+            dg = K.lstm_bwd(dh, h, c, g, whh if H <= 64 else None, whh_t, B, T, H, dirs)
         G = dirs * 4 * H
         M = B * T
         sink = _SINK["on"]
@@ -1011,12 +1013,24 @@ class _LSTMPairFn(torch.autograd.Function):
         for t, tw in zip((x, h0, h1), ctx.twins):
             K.attach_twin(t, tw)
         c0, c1 = ctx.cores
-        dh0, g1 = c1.backward(dh1.contiguous(), h0, h1, ctx.saved[1], ctx.B, ctx.T, True)
-        dx, g0 = c0.backward(dh0, x, h0, ctx.saved[0], ctx.B, ctx.T, ctx.needs_input_grad[0])
+        B, T, H = ctx.B, ctx.T, c0.H
+        if _PAIR_BWD and K.lstm2_bwd_persistent(B, H):
+            # both layers in one wavefront launch (avc_lstm2_bwd): dG1 W_ih1 inside the recurrence
+            (cs0, gs0), (cs1, gs1) = ctx.saved
+            wt0 = c0.packs()[3]
+            _, _, _, wt1, wti1 = c1.packs()
+            dg0, dg1 = K.lstm2_bwd(dh1.contiguous(), cs0, gs0, cs1, gs1, wt0, wti1, wt1, B, T, H)
+            _, g1 = c1.backward(None, h0, h1, ctx.saved[1], B, T, False, dg=dg1)
+            dx, g0 = c0.backward(None, x, h0, ctx.saved[0], B, T, ctx.needs_input_grad[0], dg=dg0)
+            return (dx, None, None, None, None, *g0, *g1)
+        dh0, g1 = c1.backward(dh1.contiguous(), h0, h1, ctx.saved[1], B, T, True)
+        dx, g0 = c0.backward(dh0, x, h0, ctx.saved[0], B, T, ctx.needs_input_grad[0])
         return (dx, None, None, None, None, *g0, *g1)
 
 
 _PAIR_OFF = bool(os.environ.get("AVC_LSTM2_OFF"))
+# the pair's backward as one wavefront launch (avc_lstm2_bwd); "0": two single-layer launches + the dX1 GEMM
+_PAIR_BWD = os.environ.get("AVC_LSTM2_BWD", "1") != "0"
 
 
 def lstm(mod, cores, x, B, T):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 26
+#define AVC_ABI_VERSION 27
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -295,6 +295,20 @@ int avc_lstm_set_spin(unsigned spins);
  * (10 = the same without the one-utterance tile for 128 < T <= 192).
  * Same as the AVC_RING / AVC_RING_WIN environment variables.  Returns 0. */
 int avc_gemm_set_ring(int mode, int bm, int bn, int nst, int gm, int win);
+
+/* Decoder lstm2 BACKWARD, both layers in one persistent launch (layer wavefront, lstm.hip
+ * lstm2_persist_bwd): tick k runs layer 1 at step T-1-k and layer 0 at step T-k; layer 0's upstream
+ * gradient dG1 W_ih1 is formed inside the recurrence.  dh1 = dL/dh of layer 1's output (B,T,H);
+ * c0/gates0, c1/gates1 the forward's cell states and activated gates (avc_lstm2_fwd); w_hh0_t,
+ * w_ih1_t, w_hh1_t the transposed bf16 weights [H][4H]; outputs dg0 / dg1 = dL/d(pre-activation
+ * gates) (B,T,4H) fp32 with optional bf16 twins.  buf: avc_lstm2_bwd_scratch_bytes(B, H) bytes.
+ * bf16 compute, H = 1024, the whole grid resident (avc_lstm2_bwd_persistent).  Replaces
+ * nn.LSTM.backward of AutoVC.py:96,110's two-layer lstm2 (two avc_lstm_bwd + the dX1 GEMM). */
+int avc_lstm2_bwd_persistent(int B, int H, int compute);
+size_t avc_lstm2_bwd_scratch_bytes(int B, int H);
+int avc_lstm2_bwd(const float* dh1, const float* c0, const float* gates0, const float* c1, const float* gates1,
+                  const void* w_hh0_t, const void* w_ih1_t, const void* w_hh1_t, int B, int T, int H, float* dg0,
+                  void* dg0_bf16, float* dg1, void* dg1_bf16, void* buf, void* stream);
 
 /* Which deep-ring kernel the last avc_gemm on this host thread launched (tests, tools): 0 none (an
  * older kernel), 1 gemm_ring_kernel, 2 the 128-row halo conv (conv_ring_kernel, its BN-backward
