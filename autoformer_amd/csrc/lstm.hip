@@ -1520,6 +1520,7 @@ struct Persist2BwdArgs {
   unsigned* fault;
   unsigned spin;
   int B, T, ng;
+  int opt;  // AVC_LSTM2_BWD_OPT bits (A/B): 1 = dG stores after a barrier behind the flag, 2 = no bf16 twin
 };
 
 constexpr int BKC = 1024, BNC = 4, BCP = BKC + 8, BNLW = 3;  // K-chunk, chunks, LDS pitch, W_hh0 frags in LDS
@@ -1701,6 +1702,7 @@ __global__ void __launch_bounds__(PNT, 1) lstm2_persist_bwd(Persist2BwdArgs a) {
       }
       raise_flag(flags, r, (unsigned)(k + 1));
     }
+    if (a.opt & 1) __syncthreads();  // every wave's stores behind wave 0's flag
     if (act) {  // (wave 0 issues these after its flag: they stay off the hand-off's vmcnt wait)
       const long long og = ((long long)cb * T + t) * G + cj;
       float* d = a.dg[L] + og;
@@ -1708,7 +1710,7 @@ __global__ void __launch_bounds__(PNT, 1) lstm2_persist_bwd(Persist2BwdArgs a) {
       d[H] = v1;
       d[2 * H] = v2;
       d[3 * H] = v3;
-      if (a.dg16[L]) {
+      if (a.dg16[L] && !(a.opt & 2)) {
         bf16* d16 = a.dg16[L] + og;
         d16[0] = (bf16)v0;
         d16[H] = (bf16)v1;
@@ -2031,6 +2033,8 @@ extern "C" int avc_lstm2_bwd(const float* dh1, const float* c0, const float* gat
   p.B = B;
   p.T = T;
   p.ng = ng;
+  static const int opt = getenv("AVC_LSTM2_BWD_OPT") ? atoi(getenv("AVC_LSTM2_BWD_OPT")) : 1;
+  p.opt = opt;
   if (avc_zero_async(buf, px_ctl_bytes(ng), s)) return -1;
   lstm2_persist_bwd<1024><<<dim3(ng * (H / QJU)), PNT, persist2_bwd_lds<1024>(), s>>>(p);
   return avc_check_launch("avc_lstm2_bwd");

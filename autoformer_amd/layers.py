@@ -1029,8 +1029,9 @@ class _LSTMPairFn(torch.autograd.Function):
 
 
 _PAIR_OFF = bool(os.environ.get("AVC_LSTM2_OFF"))
-# the pair's backward as one wavefront launch (avc_lstm2_bwd); "0": two single-layer launches + the dX1 GEMM
-_PAIR_BWD = os.environ.get("AVC_LSTM2_BWD", "0") != "0"
+# the pair's backward as one wavefront launch (avc_lstm2_bwd; C2 5.83 -> 5.81 ms, isolated 1127 -> ~1050 us,
+# profiles/r5_lstm2_bwd_wavefront.txt); "0": two single-layer launches + the dX1 GEMM
+_PAIR_BWD = os.environ.get("AVC_LSTM2_BWD", "1") != "0"
 
 
 def lstm(mod, cores, x, B, T):

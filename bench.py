@@ -50,7 +50,50 @@ def synthetic_batch(B, T, rank, device):
 
 
 DOMINANT = "lstm_persist_bwd<1024>"
+DOMINANT_WAVE = "lstm2_persist_bwd<1024>"
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def wavefront_bwd(B):
+    """Whether the step runs the decoder lstm2 backward as the two-layer wavefront launch."""
+    from autoformer_amd import kernels as K
+    from autoformer_amd import layers as Ly
+
+    return Ly._PAIR_BWD and K.lstm2_bwd_persistent(B, 1024)
+
+
+def kernel_timing_wave(model, B, T, reps=3):
+    """Isolated replays of lstm2_persist_bwd<1024> (the decoder lstm2 backward, BOTH layers in one
+    wavefront launch of T + 1 ticks): the dominant kernel when the step runs it.  FLOP per launch: the
+    three recurrent products per step (W_hh1^T, W_ih1^T, W_hh0^T: 2 * B * 4H * H each) over T steps.
+    Algorithmic bytes: the three transposed weights once (3 * 4H * H bf16) + per step
+    dL/dh1 fp32 (B*H*4) + per layer c_t, c_{t-1} fp32 (2*B*H*4) + gates fp32 (B*4H*4) + dG fp32 and
+    bf16 out (B*4H*6)."""
+    from autoformer_amd import kernels as K
+
+    c0, c1 = model.decoder._lstm2
+    wt0 = c0.packs()[3]
+    _, _, _, wt1, wti1 = c1.packs()
+    H = c0.H
+    dev = wt0.device
+    g = torch.Generator(device=dev).manual_seed(7)
+    dh = torch.randn(B * T, H, device=dev, generator=g) * 0.1
+    cs = [torch.randn(B * T, H, device=dev, generator=g) * 0.5 for _ in range(2)]
+    gs = [torch.rand(B * T, 4 * H, device=dev, generator=g) for _ in range(2)]
+    K.lstm2_bwd(dh, cs[0], gs[0], cs[1], gs[1], wt0, wti1, wt1, B, T, H)  # warm
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        K.lstm2_bwd(dh, cs[0], gs[0], cs[1], gs[1], wt0, wti1, wt1, B, T, H)
+    e1.record(s)
+    torch.cuda.synchronize()
+    K.check_faults()
+    avg_us = e0.elapsed_time(e1) * 1e3 / reps
+    G = 4 * H
+    alg_bytes = 3 * G * H * 2 + T * (B * H * 4 + 2 * (2 * B * H * 4 + B * G * 4 + B * G * 6))
+    return {"kernel": DOMINANT_WAVE + " (decoder lstm2 backward, both layers in one wavefront launch, T=%d, B=%d, "
+            "H=%d)" % (T, B, H), "avg_us": avg_us, "bytes": float(alg_bytes), "flops": 3 * 2.0 * B * G * H * T}
 
 
 def kernel_timing(model, B, T, reps=3):
@@ -155,7 +198,8 @@ def pmc_mfma(kernel):
             return {"mfma_instr_tflops": round(e.get("bf16_tflops", 0.0), 1),
                     "mfma_instr_frac": round(e.get("bf16_tflops", 0.0) / PEAK_BF16_TFLOPS, 4),
                     "wave_wait_frac": round(e.get("wait", 0.0), 3), "source": os.path.relpath(files[-1], ROOT),
-                    "note": "MFMA instruction rate (16-row tiles, 8 of 16 rows are utterances: 2x the useful FLOPs)"}
+                    "note": "MFMA instruction rate (lstm_persist_bwd: 16-row tiles with 8 utterances, 2x the useful "
+                            "FLOPs; lstm2_persist_bwd: full 16-utterance tiles)"}
     return None
 
 
@@ -386,7 +430,10 @@ def main():
         out["collective"] = f"{dist.get_backend()} all_reduce AVG, {D.BUCKET_BYTES >> 20} MiB buckets"
     if not args.no_kernel_timing and args.model == "AutoVC":
         evs, K.LAUNCH_TIMING = K.LAUNCH_TIMING or [], None
-        kt = kernel_timing(model, B, T)  # isolated replays (also: algorithmic bytes / FLOP)
+        wave = wavefront_bwd(B)
+        dominant = DOMINANT_WAVE if wave else DOMINANT
+        # isolated replays (also: algorithmic bytes / FLOP)
+        kt = kernel_timing_wave(model, B, T) if wave else kernel_timing(model, B, T)
         if evs:  # the in-step launches of the timed region (beside the side-stream GEMMs)
             step_us = sum(a.elapsed_time(b) for a, b in evs) * 1e3 / len(evs)
         else:
@@ -394,14 +441,14 @@ def main():
         # the path's roofline is dense bf16 MFMA; HBM is the secondary counter
         tfs = kt["flops"] / (step_us * 1e-6) / 1e12
         gbs = kt["bytes"] / (step_us * 1e-6) / 1e9
-        traffic, src = pmc_traffic(DOMINANT)
+        traffic, src = pmc_traffic(dominant)
         out["roofline"] = {"bound": "mfma", "achieved": round(tfs, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                            "frac": round(tfs / PEAK_BF16_TFLOPS, 5), "traffic": traffic, "kernel": kt["kernel"],
                            "avg_us": round(step_us, 3), "launches_timed": len(evs),
                            "avg_us_isolated": round(kt["avg_us"], 3), "flop_per_launch": kt["flops"],
                            "alg_bytes_per_launch": kt["bytes"], "hbm_achieved_gbs": round(gbs, 1),
                            "hbm_frac": round(gbs / PEAK_HBM_GBS, 5), "traffic_source": src,
-                           "counters": pmc_mfma(DOMINANT)}
+                           "counters": pmc_mfma(dominant)}
     if world == 1 and not args.no_cpu_baseline and default:
         out["cpu_baseline"] = cpu_baseline(B, T, freq)
     print(json.dumps(out), flush=True)
