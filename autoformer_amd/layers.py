@@ -512,7 +512,7 @@ class ConvBNCore:
             stats = K.gemm(M, Co, Kdim, xop, wop, y, bias=conv.bias, bn_partial=partial,
                            bn_fin=(bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, mom, bn.eps,
                                    self.stat_updates), row_bias=row_bias,
-                           bn_apply=(a, self.act) if fused else None)
+                           **({"bn_apply": (a, self.act)} if fused else {}))
         else:
             K.gemm(M, Co, Kdim, xop, wop, y, bias=conv.bias, row_bias=row_bias)
             stats = K.bn_eval(bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.eps)
@@ -583,7 +583,8 @@ class ConvBNCore:
             dx = torch.empty(B * T_in, n_dx, device=x.device, dtype=x.dtype)
             bnb = prev_link.gemm_args(B * T_in, n_dx, sink) if prev_link is not None and n_dx == Ci else None
             K.gemm(B * T_in, n_dx, Kw * Co, operand(dy, Co, window=(Kw, Kw - 1 - self.pad, T_in, T_out, Co)),
-                   operand(Wd, Kw * Co), dx, bnb=bnb, bnb_dy=prev_link.dy if bnb is not None else None)
+                   operand(Wd, Kw * Co), dx, bnb=bnb,
+                   **({"bnb_dy": prev_link.dy} if bnb is not None and prev_link.dy is not None else {}))
             if bnb is not None:
                 prev_link.dA_ptr = dx.data_ptr()
         if sink and (n_dx or not _LAST_WGRAD_MAIN):

@@ -10,10 +10,12 @@ kernels on the same two streams with the same event edges as the eager step -- t
 still runs beside the main chain -- with none of the Python that produced them.
 
 What makes a recorded argument list valid again at the next step:
-  * every tensor the step allocates comes from a private memory pool that stays reserved while
-    the record lives (torch.cuda.MemPool), so the addresses frozen in the calls stay owned by the
-    record, and the allocator's reuse decisions of the recording step are the replay's too (same
-    order of calls on the same streams);
+  * every tensor the step allocates (each aten allocation is seen by the dispatch mode below) is
+    held by the record, so no address frozen in the calls is ever freed or handed to anything else
+    -- not within the step either, so the recording step's buffers are all distinct and no
+    cross-stream reuse hazard exists in the replays (a private MemPool had been used first: its
+    freed blocks were taken by other allocations of the process, tests/test_gpu_replay.py with an
+    eager trainer beside the replaying one);
   * weight packs are frozen and rewritten in place after the optimizer step inside the recorded
     step (layers.freeze_packs / repack_in_place, as for the captured graph);
   * device-side state (Adam's step count, BN running statistics, the LSTM hand-off flags and
@@ -64,6 +66,11 @@ class _TorchOpRecorder(TorchDispatchMode):
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
         out = func(*args, **kwargs)
+        if not self.rec.paused:
+            # every device tensor the step allocates stays allocated while the record lives: the
+            # addresses frozen in the calls can never be handed to anything else
+            flat, _ = tree_flatten(out)
+            self.rec.keep.extend(t for t in flat if isinstance(t, torch.Tensor) and t.is_cuda)
         if (self.rec.paused or func.is_view or func.overloadpacket.__name__ in _NO_KERNEL
                 or not _cuda_tensors(args, kwargs)):
             return out
@@ -92,13 +99,12 @@ def _frozen(a):
 
 
 class StepRecord:
-    """The recorded calls of one step; replay() re-issues them.  Keeps the memory pool (and every
-    tensor a torch-op closure references) alive."""
+    """The recorded calls of one step; replay() re-issues them.  Keeps every device tensor the
+    recorded step allocated (and every tensor a torch-op closure references) alive."""
 
     def __init__(self):
         self.calls = []       # (ctypes function, name, args) | (None, closure, None)
         self.torch_ops = []   # names of the torch ops recorded as closures
-        self.pool = None
         self.keep = []
         self.paused = False   # inside collective(): nothing is recorded call by call
 
@@ -147,18 +153,16 @@ def collective(fn):
 
 @contextlib.contextmanager
 def recording(rec: StepRecord):
-    """Record every library call (and torch op) issued inside the block into `rec`; the block's
-    allocations come from rec's private pool; autograd runs its backward on this thread so that
-    the pool and the dispatch mode see it too."""
+    """Record every library call (and torch op) issued inside the block into `rec`, holding every
+    device tensor allocated inside it; autograd runs its backward on this thread so that the
+    dispatch mode sees it too."""
     if L._REC is not None:
         raise RuntimeError("replay.recording: already recording")
-    dev = torch.cuda.current_device()
-    rec.pool = torch.cuda.MemPool()
     mt = torch.autograd.is_multithreading_enabled()
     torch.autograd.set_multithreading_enabled(False)
     L._REC = rec
     try:
-        with torch.cuda.use_mem_pool(rec.pool, dev), _TorchOpRecorder(rec):
+        with _TorchOpRecorder(rec):
             yield rec
     finally:
         L._REC = None

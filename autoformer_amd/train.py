@@ -435,7 +435,12 @@ class TrainStep:
         in-place op tables and contents up to date (eager); the caller then freezes them."""
         bound = self.flat[self.split].data_ptr() if self.split is not None else None
         dec = (lambda c: c.params[0].data_ptr() >= bound) if bound is not None else (lambda c: False)
-        self._pack_groups = (plan_caches(lambda c: not dec(c)), plan_caches(dec))
+        # only this trainer's packs (the plan is process-wide: another model's caches would be frozen
+        # into this step's repack and rewritten through pointers that model may free later)
+        lo = self.flat.data_ptr()
+        hi = lo + self.flat.numel() * self.flat.element_size()
+        own = lambda c: lo <= c.params[0].data_ptr() < hi  # noqa: E731
+        self._pack_groups = (plan_caches(lambda c: own(c) and not dec(c)), plan_caches(lambda c: own(c) and dec(c)))
         for caches, grp in ((self._pack_groups[0], "graph_enc"), (self._pack_groups[1], "graph_dec"),
                             (self._pack_groups[0] + self._pack_groups[1], "graph_all")):
             repack_in_place(caches, grp)  # eager: builds the op tables (and the current packs)

@@ -299,6 +299,19 @@ class Capture:
         self.records.append(("lstm_bwd", f"lstm_bwd B{B} T{T} H{H} dirs{dirs}", res))
         return dg
 
+    def _lstm2_bwd(self, dh1, c0, g0, c1, g1, wt0, wti1, wt1, B, T, H):
+        """The two-layer wavefront backward against the layer-by-layer fp64 reference: layer 1 from
+        dh1, layer 0 from dG1 W_ih1 (the dX1 the wavefront forms inside its recurrence)."""
+        torch.cuda.synchronize()
+        dg0, dg1 = self._orig["lstm2_bwd"](dh1, c0, g0, c1, g1, wt0, wti1, wt1, B, T, H)
+        torch.cuda.synchronize()
+        ref1 = lstm_bwd_ref(dh1, c1, g1, wt1.t(), B, T, H, 1)
+        ref0 = lstm_bwd_ref(ref1 @ wti1.double().t(), c0, g0, wt0.t(), B, T, H, 1)
+        res = {"dG0": _rel(dg0, ref0), "dG1": _rel(dg1, ref1), "dG0_bf16": _rel(dg0._bf16, ref0),
+               "dG1_bf16": _rel(dg1._bf16, ref1)}
+        self.records.append(("lstm2_bwd", f"lstm2_bwd B{B} T{T} H{H}", res))
+        return dg0, dg1
+
     def _bn_apply(self, y, scale, shift, act, residual=None, out=None, twin16=None, out_bf16=False):
         torch.cuda.synchronize()
         o = self._orig["bn_apply"](y, scale, shift, act, residual=residual, out=out, twin16=twin16,
@@ -624,7 +637,7 @@ class Capture:
 
     # ---------------------------------------------------------------- context
     def __enter__(self):
-        for name in ("gemm", "lstm_fwd", "lstm2_fwd", "lstm_bwd", "bn_apply", "bn_bwd", "expand_codes",
+        for name in ("gemm", "lstm_fwd", "lstm2_fwd", "lstm_bwd", "lstm2_bwd", "bn_apply", "bn_bwd", "expand_codes",
                      "conv_edge_table", "conv_edge_colsum", "group_norm_fwd", "group_norm_bwd", "layer_norm_fwd",
                      "layer_norm_bwd", "gelu_fwd_operand", "gelu_bwd_twin", "pool3_mixer", "patchify",
                      "transpose_batched", "transpose_pad", "disc_dense_fwd", "disc_dense_bwd", "vc_loss", "vc_loss_grad", "bce_loss",
