@@ -384,6 +384,19 @@ __global__ void zero2d_kernel(float* c, long long ldc, long long cbs, int M, int
   c[(long long)blockIdx.y * cbs + (long long)r * ldc + col] = 0.f;
 }
 
+}  // namespace
+
+// the zero fill of C before an atomic split-K / batch sum (deferred to here for the TT dispatch)
+void avcg::gemm_zero_c(GemmArgs& g, hipStream_t s) {
+  if (!g.zero_c) return;
+  g.zero_c = 0;
+  const long long tot = (long long)g.M * g.N;
+  dim3 zg(cdiv(tot, 256), g.cbs == 0 ? 1 : g.batch);
+  zero2d_kernel<<<zg, 256, 0, s>>>(g.c, g.ldc, g.cbs, g.M, g.N);
+}
+
+namespace {
+
 bool aligned4(const void* p, int dtype) {
   uintptr_t a = reinterpret_cast<uintptr_t>(p);
   return dtype == AVC_F32 ? (a % 16 == 0) : (a % 8 == 0);
@@ -946,13 +959,14 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
   hipStream_t s = as_stream(stream);
   AVC_CHECK_ARG(!(g.res && g.atomic && g.batch > 1 && d->c_batch_stride == 0),
                 "avc_gemm: residual with a batch-summed output is not supported");
-  if (g.atomic && !d->accumulate) {
-    long long tot = (long long)g.M * g.N;
-    dim3 zg(cdiv(tot, 256), d->c_batch_stride == 0 ? 1 : g.batch);
-    zero2d_kernel<<<zg, 256, 0, s>>>(g.c, g.ldc, g.cbs, g.M, g.N);
-  }
   const bool bf = d->compute == AVC_BF16;
   const bool aks = d->a.kstrided != 0, bks = d->b.kstrided != 0;
+  g.sk_ws = nullptr;
+  g.sk_cnt = nullptr;
+  g.zero_c = g.atomic && !d->accumulate;
+  // a TT product may reduce its split-K partials without atomics (gemm_tt_launch): its zero fill
+  // waits for that decision; every other path zeroes now
+  if (!(bf && aks && bks)) gemm_zero_c(g, s);
   if (bf && g.a.vec && g.b.vec && fits32(g.a, g.M, g.K, aks) && fits32(g.b, g.N, g.K, bks)) {
     // re-split K in units of the fast kernel's BK
     int klf = (d->K + g.split_k - 1) / g.split_k;
@@ -992,6 +1006,7 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
     else if (!aks && !bks && gemm_nt_launch(g, s)) what = "avc_gemm(nt)";
     else if (aks && bks && gemm_tt_launch(g, s)) what = "avc_gemm(tt)";
     else {
+      gemm_zero_c(g, s);
       const long long t128 = (long long)cdiv(g.M, BM) * cdiv(g.N, 128) * g.batch * g.split_k;
       const bool narrow = g.N <= 64 || t128 < 384;
       const int nb = narrow ? cdiv(g.M, BM) * cdiv(g.N, 64) * g.batch * g.split_k : (int)t128;
@@ -1010,6 +1025,7 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
     if (f && !g.bn_cnt && bn_finalize_after(g, f, stream)) return -1;
     return applied ? 0 : bn_apply_after(d, f, bb, s);
   }
+  gemm_zero_c(g, s);
   const GeluPost post = strip_gelu(g);
   // the generic kernel writes fp32 C only: a bf16 output is produced afterwards from C by the GELU
   // pass (fused GELU / GELU' epilogues), so C must exist and a plain bf16 twin is refused

@@ -79,7 +79,62 @@ struct GemmArgs {
   bf16* bnb_dy16;
   unsigned* fault;  // process fault word (bit 1: a barrier wait timed out); nullable
   int nap;          // s_sleep(1)s between the barrier's polls (AVC_BN_NAP)
+  // split-K without atomics (TT kernels, sk_ws != null): per-stream workspace of split_k partial
+  // tiles per output tile and one self-resetting arrival counter per output tile (splitk_last)
+  float* sk_ws;
+  unsigned* sk_cnt;
+  int zero_c;  // C still needs the zero fill of an atomic split-K (deferred to the TT dispatch)
 };
+
+// Split-K without atomics (sk_ws != null): every split stores its NF accumulator fragments in
+// register order (16 B per lane, write-through sc1, so no fence) into slot ks of its output tile's
+// workspace and arrives on the tile's counter; the split that arrives last adds the S slots in
+// split order (sc1 loads, its own slot included) so the sum does not depend on which split
+// finishes last (deterministic, unlike the atomics), and returns true to run the
+// plain epilogue.  The others return false.  Replaces the zero fill of C plus S x M x N float
+// atomics (~1.3 TB/s chip-wide, MI355X_MICROARCH.md) with S x M x N write-through stores and
+// (S-1) x M x N loads by the last splits.
+template <int NF>
+__device__ __forceinline__ bool splitk_last(const GemmArgs& g, f32x4* acc, int tile, int ks) {
+  constexpr int SC1 = 16;  // buffer-instruction cache-policy bits: sc1
+  const int S = g.split_k, nth = blockDim.x, tid = threadIdx.x;
+  float* base = g.sk_ws + (long long)tile * S * NF * nth * 4;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, S * NF * nth * 16, 0x00020000);
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[f]), rs, ((ks * NF + f) * nth + tid) * 16, 0,
+                                           SC1);
+  if (!arrive_last(g.sk_cnt + tile, (unsigned)S)) return false;
+  f32x4 sum[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) sum[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // its own slot is re-read too (acc is dead after the stores: VGPRs); the loads of slot s + 1 are
+  // in flight while slot s is added, one memory round trip per slot instead of two
+  u32x4 v[2][NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) v[0][f] = __builtin_amdgcn_raw_buffer_load_b128(rs, (f * nth + tid) * 16, 0, SC1);
+  for (int s = 0; s < S; s += 2) {
+    if (s + 1 < S) {
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+        v[1][f] = __builtin_amdgcn_raw_buffer_load_b128(rs, (((s + 1) * NF + f) * nth + tid) * 16, 0, SC1);
+    }
+#pragma unroll
+    for (int f = 0; f < NF; ++f) sum[f] += __builtin_bit_cast(f32x4, v[0][f]);
+    if (s + 1 < S) {
+      if (s + 2 < S) {
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+          v[0][f] = __builtin_amdgcn_raw_buffer_load_b128(rs, (((s + 2) * NF + f) * nth + tid) * 16, 0, SC1);
+      }
+#pragma unroll
+      for (int f = 0; f < NF; ++f) sum[f] += __builtin_bit_cast(f32x4, v[1][f]);
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < NF; ++f) acc[f] = sum[f];
+  return true;
+}
 
 // Last-arriving row tile of a column tile: merge the per-row-tile (sum, M2) partials of columns
 // n0 .. n0+BN_-1 (Chan's parallel form, two passes over the L2/MALL-resident partials) and
@@ -205,7 +260,7 @@ __device__ __forceinline__ void fast_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
         const long long o = out_off(g, row, col);
         float v = acc[i][j][e];
         if (g.res && ks == 0) v += g.res[(long long)bz * g.cbs + o];
-        if (g.atomic) {
+        if (g.atomic && !g.sk_ws) {
           atomicAdd(C + o, v);
         } else {
           if (g.accumulate) v += C[o];
@@ -392,6 +447,11 @@ bool gemm_nt_launch(const GemmArgs& g, hipStream_t s);
 bool gemm_conv_launch(const GemmArgs& g, hipStream_t s);
 // Entry of the TT (both operands K-strided, bf16) weight-gradient kernel (gemm_tt.hip).
 bool gemm_tt_launch(const GemmArgs& g, hipStream_t s);
+// launch the zero fill of C when g.zero_c is set (clears it; gemm.hip)
+void gemm_zero_c(GemmArgs& g, hipStream_t s);
+// per-stream split-K workspace of at least `bytes` (grown, never shrunk; null inside a stream
+// capture or on allocation failure: the caller keeps the atomics; gemm_tt.hip)
+float* gemm_splitk_ws(size_t bytes, hipStream_t s);
 // Entry of the 8-wave deep-ring NT kernel (gemm_ring.hip); false when the shape / operands do
 // not qualify or AVC_RING=0.
 bool gemm_ring_launch(const GemmArgs& g, hipStream_t s);

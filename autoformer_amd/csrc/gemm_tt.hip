@@ -13,6 +13,10 @@
 // transposing LDS read ds_read_b64_tr_b16 (cdna_hip_programming.md §5.5 T10, layout (b):
 // conflict-free for the 16x16x32 operands).  128 x 128 tile, BK = 64, 4 waves as 2 x 2,
 // 2 LDS stages, counted vmcnt + raw barrier, shared fused epilogue (gemm_internal.h).
+#include <algorithm>
+#include <map>
+#include <mutex>
+
 #include "gemm_internal.h"
 
 namespace avcg {
@@ -202,6 +206,7 @@ __global__ void __launch_bounds__(256, 2) gemm_tt_kernel(GemmArgs g) {
     }
   }
   __syncthreads();
+  if (g.sk_ws && !splitk_last<4 * NJ>(g, &acc[0][0], rem, ks)) return;  // (batch 1: z = ks)
   fast_epilogue<BN_, false>(g, acc, m0, n0, mt, bz, ks, smem_raw);  // (weight gradients: no BN-backward epilogue)
 }
 
@@ -321,7 +326,7 @@ __global__ void __launch_bounds__(BMT * 2, 1) gemm_tt2_kernel(GemmArgs g) {
         if (col >= g.N) continue;
         float* cp = C + (long long)row * g.ldc + out_col(g, col);
         const float v = acc[i][j][e];
-        if (g.atomic) atomicAdd(cp, v);
+        if (g.atomic && !g.sk_ws) atomicAdd(cp, v);
         else *cp = g.accumulate ? *cp + v : v;
       }
     }
@@ -495,6 +500,7 @@ __global__ void __launch_bounds__(256, 2) gemm_tt_halo_kernel(GemmArgs g) {
           acc[i][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[k], acc[i][k], 0, 0, 0);
     }
   }
+  if (g.sk_ws && !splitk_last<4 * TAPS>(g, &acc[0][0], rem, ks)) return;
   // epilogue: row m0 + wm*64 + 16i + 4*(lane>>4) + e, column tap*chans + c0 + 16*wn + (lane & 15)
   const int rbase = m0 + wm * 64 + 4 * (lane >> 4);
   const int cl = c0 + 16 * wn + (lane & 15);
@@ -508,7 +514,7 @@ __global__ void __launch_bounds__(256, 2) gemm_tt_halo_kernel(GemmArgs g) {
       for (int k = 0; k < TAPS; ++k) {
         float* cp = g.c + (long long)row * g.ldc + (g.cperm ? (long long)cl * TAPS + k : (long long)k * chans + cl);
         const float v = acc[i][k][e];
-        if (g.atomic) atomicAdd(cp, v);
+        if (g.atomic && !g.sk_ws) atomicAdd(cp, v);
         else *cp = g.accumulate ? *cp + v : v;
       }
     }
@@ -529,8 +535,58 @@ void launch_halo(const GemmArgs& g, hipStream_t s) {
 
 }  // namespace
 
-bool gemm_tt_launch(const GemmArgs& g, hipStream_t s) {
+float* gemm_splitk_ws(size_t bytes, hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> ws;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || hipStreamIsCapturing(s, &st) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& e = ws[{dev, s}];
+  if (e.second >= bytes) return e.first;
+  if (st != hipStreamCaptureStatusNone) return nullptr;  // no allocation inside a capture
+  // grow: the old buffer may still be read by this stream's queued kernels, so it is kept (a
+  // stream grows a few times per process: the largest weight gradient it runs)
+  float* p = nullptr;
+  const size_t want = std::max(bytes, (size_t)32 << 20);
+  if (hipMalloc(&p, want) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  e = {p, want};
+  return p;
+}
+
+bool gemm_tt_launch(const GemmArgs& g0, hipStream_t s) {
   static const bool off = getenv("AVC_TT_DISABLE") != nullptr;
+  // AVC_TT_ABL=1 (timing diagnostic, wrong results): split-K partials stored instead of added
+  static const bool abl = getenv("AVC_TT_ABL") != nullptr;
+  // AVC_TT_SPLITK=n: split-K reduced without atomics up to n splits (default 6); 0 = every split-K
+  // product by atomics into the zeroed C (the pre-round-5 form)
+  static const int fix_max = [] {
+    const char* e = getenv("AVC_TT_SPLITK");
+    return e ? atoi(e) : 6;
+  }();
+  const bool fix_on = fix_max > 1;
+  GemmArgs ga = g0;
+  if (abl) ga.atomic = false;
+  const GemmArgs& g = ga;
+  // the split-K reduction without atomics: `tiles` output tiles of `tile_bytes` each
+  auto fixup = [&](int tiles, size_t tile_bytes) {
+    // the last split's reduction takes ~one memory round trip per split: past SK_MAX splits the
+    // atomics win (AVC_TT_SPLITK=n sets the bound; tools/tt_bench.py)
+    if (!fix_on || abl || g.split_k <= 1 || g.split_k > fix_max || g.batch != 1 || !g.c || g.bias || g.res ||
+        g.bn_partial || g.rbias)
+      return;
+    const size_t bytes = (size_t)tiles * g.split_k * tile_bytes;
+    if (bytes > ((size_t)1 << 30)) return;
+    float* w = gemm_splitk_ws(bytes, s);
+    unsigned* c = w ? avc_counter_slots(tiles, s) : nullptr;
+    if (!c) return;
+    ga.sk_ws = w;
+    ga.sk_cnt = c;
+    ga.zero_c = 0;
+  };
   if (off || g.klen % FBK || g.M % 8 || g.N % 8) return false;
   for (const OpDev* o : {&g.a, &g.b})
     if (o->dtype != AVC_BF16 || !ok16(o->ptr) || o->ld % 8 || o->bstride % 8) return false;
@@ -542,6 +598,8 @@ bool gemm_tt_launch(const GemmArgs& g, hipStream_t s) {
   const OpDev& x = g.b;
   if (!halo_off && x.win && x.taps == 5 && x.t_in == x.t_out && 2 * x.pad == x.taps - 1 && x.chans % 32 == 0 &&
       g.K % x.t_out == 0 && g.batch == 1 && g.N == x.taps * x.chans && !g.res && !g.c16 && !g.bias && !g.bn_partial) {
+    fixup(((g.M + BM - 1) / BM) * (x.chans / 32), (size_t)BM * 32 * x.taps * 4);
+    gemm_zero_c(ga, s);
     if (halo == 2) launch_halo<2>(g, s);
     else launch_halo<3>(g, s);
     return true;
@@ -549,6 +607,8 @@ bool gemm_tt_launch(const GemmArgs& g, hipStream_t s) {
   int bmt, nst;
   tt_cfg(bmt, nst);
   if (g.c16 || g.res || g.bias || g.bn_partial) bmt = 0;  // the pipelined kernel has the plain epilogue only
+  if (bmt == 0) fixup(((g.M + BM - 1) / BM) * ((g.N + 127) / 128), (size_t)BM * 128 * 4);
+  gemm_zero_c(ga, s);
 #define TT2_CASE(BMV, NSV)                               \
   if (bmt == BMV && nst == NSV) {                        \
     if (g.b.win) launch2<true, BMV, NSV>(g, s);          \

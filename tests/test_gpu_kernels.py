@@ -633,6 +633,41 @@ def test_gemm_tt_conv_weight_gradient_window(B, T, Cin, Cout, Kw, pad, split):
     assert relf(c, ref) < 1e-5, relf(c, ref)
 
 
+@pytest.mark.parametrize("kind", ["tt", "halo"])
+def test_gemm_tt_splitk_reduction_accumulates_and_is_deterministic(kind):
+    """Split-K TT products reduce their partials without atomics (gemm_internal.h splitk_last: the
+    last-arriving split adds the write-through partial tiles in split order): accumulate=True adds
+    the sum to C, and repeated launches are bit-identical (the atomics were not)."""
+    import autoformer_amd as A
+    from autoformer_amd import kernels as Kr
+
+    A.set_compute("bf16")
+    g = torch.Generator().manual_seed(11)
+    if kind == "tt":
+        M, N, K = 384, 640, 4096
+        a = torch.randn(K, M, generator=g).to(torch.bfloat16)
+        b = torch.randn(K, N, generator=g).to(torch.bfloat16)
+        ref = a.double().t() @ b.double()
+        opa, opb = Kr.operand(a.to(DEV), M, kstrided=True), Kr.operand(b.to(DEV), N, kstrided=True)
+    else:
+        B, T, Cin, M = 32, 128, 128, 256
+        N, K = 5 * Cin, B * T
+        x = torch.randn(B * T, Cin, generator=g).to(torch.bfloat16)
+        dy = torch.randn(B * T, M, generator=g).to(torch.bfloat16)
+        ref = dy.double().t() @ _im2col(x.double(), B, T, Cin, 5, 2)
+        opa = Kr.operand(dy.to(DEV), M, kstrided=True)
+        opb = Kr.operand(x.to(DEV), Cin, kstrided=True, window=(5, 2, T, T, Cin))
+    base = torch.randn(M, N, generator=g)
+    outs = []
+    for split in (5, 5, 7):
+        c = base.to(DEV).clone()
+        Kr.gemm(M, N, K, opa, opb, c, accumulate=True, split_k=split)
+        torch.cuda.synchronize()
+        outs.append(c.cpu())
+        assert relf(c - base.to(DEV), ref) < 1e-5, relf(c - base.to(DEV), ref)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_gemm_tt_time_shift_window():
     """dW_hh = dG^T . h_{t-1}: B operand is h shifted one frame inside each utterance."""
     import autoformer_amd as A
