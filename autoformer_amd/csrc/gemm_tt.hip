@@ -504,6 +504,39 @@ __global__ void __launch_bounds__(256, 2) gemm_tt_halo_kernel(GemmArgs g) {
   // epilogue: row m0 + wm*64 + 16i + 4*(lane>>4) + e, column tap*chans + c0 + 16*wn + (lane & 15)
   const int rbase = m0 + wm * 64 + 4 * (lane >> 4);
   const int cl = c0 + 16 * wn + (lane & 15);
+  if (g.cperm == TAPS && (!g.atomic || g.sk_ws)) {
+    // Straight into the Conv1d [Co][Ci][K] layout: the tile's (32 channels x 5 taps) of a row are
+    // ONE contiguous 640-B run there, so each 64-row half is staged through LDS ([64][CPW] floats)
+    // and stored as 16-B row chunks (per-element stores 20 B apart had cost more than the
+    // separate unpack pass they replace)
+    constexpr int CPW = CW * TAPS + 4;  // 164: 16-B rows, row groups 4 apart land 16 banks apart
+    float* st = reinterpret_cast<float*>(smem_raw);
+    const int lc = (16 * wn + (lane & 15)) * TAPS;
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      __syncthreads();  // the K loop's last fragment reads / the previous half's row reads are done
+      if (wm == ph) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int k = 0; k < TAPS; ++k) st[(i * 16 + 4 * (lane >> 4) + e) * CPW + lc + k] = acc[i][k][e];
+      }
+      __syncthreads();
+      constexpr int C4 = CW * TAPS / 4;  // 40 16-B chunks per row
+      for (int q = tid; q < 64 * C4; q += 256) {
+        const int r = q / C4, c4 = q - r * C4;
+        const int row = m0 + ph * 64 + r;
+        if (row >= g.M) continue;
+        f32x4 v = *reinterpret_cast<const f32x4*>(st + r * CPW + 4 * c4);
+        f32x4* cp = reinterpret_cast<f32x4*>(g.c + (long long)row * g.ldc + (long long)c0 * TAPS + 4 * c4);
+        if (g.accumulate) v += *cp;
+        *cp = v;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -561,11 +594,11 @@ bool gemm_tt_launch(const GemmArgs& g0, hipStream_t s) {
   static const bool off = getenv("AVC_TT_DISABLE") != nullptr;
   // AVC_TT_ABL=1 (timing diagnostic, wrong results): split-K partials stored instead of added
   static const bool abl = getenv("AVC_TT_ABL") != nullptr;
-  // AVC_TT_SPLITK=n: split-K reduced without atomics up to n splits (default 6); 0 = every split-K
+  // AVC_TT_SPLITK=n: split-K reduced without atomics up to n splits (default 8); 0 = every split-K
   // product by atomics into the zeroed C (the pre-round-5 form)
   static const int fix_max = [] {
     const char* e = getenv("AVC_TT_SPLITK");
-    return e ? atoi(e) : 6;
+    return e ? atoi(e) : 8;
   }();
   const bool fix_on = fix_max > 1;
   GemmArgs ga = g0;

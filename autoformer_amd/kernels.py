@@ -201,6 +201,16 @@ def gemm(M, N, K, a: L.Operand, b: L.Operand, c: torch.Tensor, ldc=None, bias=No
     return stats
 
 
+_TT_SPLITK_MAX = int(os.environ.get("AVC_TT_SPLITK", "8") or 0)
+
+
+def tt_splitk_reduced(split_k):
+    """Whether a split-K weight-gradient (TT) product with this split reduces its partials in the
+    kernel (the last-arriving split adds them: gemm_internal.h splitk_last) rather than by atomics
+    into a zeroed C.  Mirrors gemm_tt.hip's AVC_TT_SPLITK bound (default 8)."""
+    return 1 < split_k <= _TT_SPLITK_MAX
+
+
 def auto_split_k(M, N, K, target=384, min_k=256):
     """Split-K factor for the weight-gradient GEMMs (K = frames): about `target` workgroups
     over the 128x128 output tiles (1.5 per CU: a K-loop alone is latency-bound, ~1.4 us per

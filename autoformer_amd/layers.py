@@ -436,8 +436,11 @@ def conv_wgrad(dy, x, B, T_in, T_out, w, pad, into=None):
     sk = K.auto_split_k(Co, Kw * Ci, M)
     # the direct [Co][Ci][K] epilogue scatters its columns 4*Kw bytes apart: with split-K atomics
     # that is ~Kw x the atomic requests of the packed layout (measured +0.9 ms per C2 step), so
-    # split products go through the packed dWf and one unpack pass instead
-    if not _CONV_DW_DIRECT or (sk > 1 and Kw > 1):
+    # split products reduced by atomics go through the packed dWf and one unpack pass instead;
+    # on the halo weight-gradient kernel (gemm_tt.hip: 5-tap 'same', Ci % 32 == 0) a product whose
+    # partials the last split reduces (K.tt_splitk_reduced) stores the layout directly, 16-B runs
+    halo = Kw == 5 and 2 * pad == Kw - 1 and T_in == T_out and Ci % 32 == 0 and M % T_out == 0
+    if not _CONV_DW_DIRECT or (sk > 1 and Kw > 1 and not (halo and K.tt_splitk_reduced(sk))):
         dWf = torch.empty(Co, Kw * Ci, device=x.device)
         K.gemm(Co, Kw * Ci, M, operand(dy, Co, kstrided=True),
                operand(x, Ci, kstrided=True, window=(Kw, pad, T_out, T_in, Ci)), dWf, split_k=sk)

@@ -633,7 +633,7 @@ def test_gemm_tt_conv_weight_gradient_window(B, T, Cin, Cout, Kw, pad, split):
     assert relf(c, ref) < 1e-5, relf(c, ref)
 
 
-@pytest.mark.parametrize("kind", ["tt", "halo"])
+@pytest.mark.parametrize("kind", ["tt", "halo", "halo-cperm"])
 def test_gemm_tt_splitk_reduction_accumulates_and_is_deterministic(kind):
     """Split-K TT products reduce their partials without atomics (gemm_internal.h splitk_last: the
     last-arriving split adds the write-through partial tiles in split order): accumulate=True adds
@@ -655,13 +655,15 @@ def test_gemm_tt_splitk_reduction_accumulates_and_is_deterministic(kind):
         x = torch.randn(B * T, Cin, generator=g).to(torch.bfloat16)
         dy = torch.randn(B * T, M, generator=g).to(torch.bfloat16)
         ref = dy.double().t() @ _im2col(x.double(), B, T, Cin, 5, 2)
+        if kind == "halo-cperm":  # columns (tap, ci) stored in nn.Conv1d's [Co][Ci][K] order
+            ref = ref.view(M, 5, Cin).transpose(1, 2).reshape(M, N)
         opa = Kr.operand(dy.to(DEV), M, kstrided=True)
         opb = Kr.operand(x.to(DEV), Cin, kstrided=True, window=(5, 2, T, T, Cin))
     base = torch.randn(M, N, generator=g)
     outs = []
-    for split in (5, 5, 7):
+    for split in (5, 5, 7, 1):
         c = base.to(DEV).clone()
-        Kr.gemm(M, N, K, opa, opb, c, accumulate=True, split_k=split)
+        Kr.gemm(M, N, K, opa, opb, c, accumulate=True, split_k=split, cperm=5 if kind == "halo-cperm" else 0)
         torch.cuda.synchronize()
         outs.append(c.cpu())
         assert relf(c - base.to(DEV), ref) < 1e-5, relf(c - base.to(DEV), ref)
