@@ -168,7 +168,36 @@ class _Side:
         return False
 
 
+# AVC_DEFER_LSTM2_WG (measured, off by default): the decoder lstm2 pair's four weight-gradient GEMMs
+# (4096 x 1024 x 8192 class) queued on the side stream only when the decoder lstm1 backward starts
+# ("1": beside that recurrence) or after it ("2": beside the encoder backward), instead of beside the
+# decoder conv stack's data-gradient convs that follow the lstm2 wavefront (those convs run 83-134 us
+# instead of ~40 beside them: profiles/r5_step_breakdown.txt, tools/timeline.py).  Both lose: C2
+# 5.89 / 6.10 vs 5.79-5.83 ms (the persistent lstm1 backward waits for CUs the GEMMs hold; mode 2
+# delays the decoder-slice Adam; profiles/r5_splitk_defer_ab.txt)
+_DEFER_MODE = os.environ.get("AVC_DEFER_LSTM2_WG", "0")
+_DEFER_LSTM2_WG = _DEFER_MODE != "0"
+
+
+def defer_side(fn, *keep) -> None:
+    """Queue `fn` (weight-gradient launches) for the side stream at the next flush_deferred()."""
+    _SINK.setdefault("deferred", []).append((fn, keep))
+
+
+def flush_deferred() -> None:
+    """Launch the deferred side-stream work now, after everything queued so far on this stream."""
+    pend = _SINK.get("deferred")
+    if not pend:
+        return
+    _SINK["deferred"] = []
+    with _Side() as sd:
+        for fn, keep in pend:
+            sd.keep(*keep)
+            fn()
+
+
 def join_side() -> None:
+    flush_deferred()
     side = _SINK["side"]
     if side is not None:
         if _SINK.get("tails") == []:
@@ -905,8 +934,9 @@ class LSTMLayerCore:
         h, c, g = K.lstm_fwd(xproj, whh, B, T, H, dirs, hbuf)
         return h, (c, g)
 
-    def backward(self, dh, x, h, saved, B, T, need_dx, dg=None):
-        """dg: the gate gradients when a fused launch already produced them (the lstm2 wavefront)."""
+    def backward(self, dh, x, h, saved, B, T, need_dx, dg=None, defer=False):
+        """dg: the gate gradients when a fused launch already produced them (the lstm2 wavefront).
+        defer: the weight gradients go to the side stream at the next flush_deferred()."""
         c, g = saved
         H, dirs = self.H, self.dirs
         In = x.shape[1]
@@ -952,7 +982,10 @@ class LSTMLayerCore:
         if need_dx:
             dx = torch.empty(M, In, device=x.device, dtype=x.dtype)  # bf16 for a bf16-stored input
             K.gemm(M, In, G, operand(dg, G), operand(wih_t, G), dx)
-        if sink:
+        if sink and defer and not _ABLATE_WGRAD:
+            defer_side(wgrads, dg, x, h, dg_op, h_op)
+            grads = [None] * (4 * dirs)
+        elif sink:
             with _Side(ev) as sd:
                 sd.keep(dg, x, h, dg_op, h_op)
                 if not _ABLATE_WGRAD:
@@ -1024,8 +1057,9 @@ class _LSTMPairFn(torch.autograd.Function):
             wt0 = c0.packs()[3]
             _, _, _, wt1, wti1 = c1.packs()
             dg0, dg1 = K.lstm2_bwd(dh1.contiguous(), cs0, gs0, cs1, gs1, wt0, wti1, wt1, B, T, H)
-            _, g1 = c1.backward(None, h0, h1, ctx.saved[1], B, T, False, dg=dg1)
-            dx, g0 = c0.backward(None, x, h0, ctx.saved[0], B, T, ctx.needs_input_grad[0], dg=dg0)
+            _, g1 = c1.backward(None, h0, h1, ctx.saved[1], B, T, False, dg=dg1, defer=_DEFER_LSTM2_WG)
+            dx, g0 = c0.backward(None, x, h0, ctx.saved[0], B, T, ctx.needs_input_grad[0], dg=dg0,
+                                 defer=_DEFER_LSTM2_WG)
             return (dx, None, None, None, None, *g0, *g1)
         dh0, g1 = c1.backward(dh1.contiguous(), h0, h1, ctx.saved[1], B, T, True)
         dx, g0 = c0.backward(dh0, x, h0, ctx.saved[0], B, T, ctx.needs_input_grad[0])
@@ -1093,7 +1127,10 @@ class _LSTM1FoldFn(torch.autograd.Function):
         In = cd + de
         _, _, whh, whh_t, wih_t = core.packs()
         dev = h.device
+        if _DEFER_MODE != "2":
+            flush_deferred()  # the lstm2 weight gradients: beside this recurrence (AVC_DEFER_LSTM2_WG)
         dg = K.lstm_bwd(dh.contiguous(), h, c, g, whh if H <= 64 else None, whh_t, B, T, H, 1)
+        flush_deferred()  # mode 2: after it, beside the encoder backward
         M = B * T
         c2 = codes.reshape(B * nc, cd)
         s_code = K.segsum(dg, B * nc, T // nc, G, ld=G)  # (B*nc, G): dG summed over each code's frames

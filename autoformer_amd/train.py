@@ -27,8 +27,8 @@ import torch
 from . import dist as D
 from . import kernels as K
 from .replay import collective
-from .layers import (ev_record, freeze_packs, join_side, on_stream, plan_caches, prefetch_packs, record_join_tails,
-                     repack_in_place, set_grad_sink, side_stream, stream_wait, weights_changed)
+from .layers import (ev_record, flush_deferred, freeze_packs, join_side, on_stream, plan_caches, prefetch_packs,
+                     record_join_tails, repack_in_place, set_grad_sink, side_stream, stream_wait, weights_changed)
 
 
 def _load_state(model, path, device):
@@ -299,6 +299,7 @@ class TrainStep:
         K.raise_on_fault(self._fault.item())
 
     def _decoder_done(self):
+        flush_deferred()  # every decoder weight gradient is queued before its Adam slice waits for them
         if self._capturing and not self._recording:
             # captured step (world 1): the decoder-slice Adam and the in-place repack of the decoder's
             # weight packs run on the weight-gradient stream, after the decoder's weight gradients
