@@ -502,7 +502,11 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
 // y prefetch of the tile: 4 x 16 B per thread, issued at kernel start into registers so it lands
 // under the K loop (a load-then-store loop in the epilogue had serialised four HBM round trips)
 constexpr int BNB_YQ = 128 * 16 / RNT;  // 16-B chunks per thread (128 rows x 16 chunks of 8 bf16)
-constexpr int BNB_YS = 80 * 1024;        // LDS offset of the staged y tile (128 rows x 272 B + flag)
+// LDS offset of the staged y tile (128 rows x 272 B + flag): below the C staging (ring_epi_lds),
+// above the partial sums, so the 2-stage conv ring's 98 KiB hold it; the fused BN-backward apply
+// (bnb_dy16), which re-reads y after the C stores, keeps it above them (launch_conv sizes the LDS)
+constexpr int BNB_YS_LO = 8 * 1024, BNB_YS_HI = 80 * 1024, BNB_YBYTES = 128 * (2 * 128 + 16) + 16;
+__device__ __forceinline__ int bnb_ys(const GemmArgs& g) { return g.bnb_dy16 ? BNB_YS_HI : BNB_YS_LO; }
 __device__ __forceinline__ void ring_bnb_prefetch(const GemmArgs& g, int m0, int n0, u32x4 (&yv)[BNB_YQ]) {
   const bf16* yb = static_cast<const bf16*>(g.bnb_y);
   // unconditional loads at clamped addresses (N % 8 == 0 on this path), zeroed after: a load inside
@@ -528,7 +532,7 @@ __device__ __forceinline__ bool ring_bnb_epilogue(const GemmArgs& g, f32x4 (&acc
   float* red = reinterpret_cast<float*>(smem_raw);  // [3][2 wm][BN_] / the finalize's [3][FGR][BN_]
   constexpr int YP = 2 * BN_ + 16;                  // LDS row pitch of the staged y tile (bytes)
   // above the staged stores' LDS (ring_epi_lds: 72 KiB): the fused apply reads y again after them
-  char* ys = smem_raw + BNB_YS;
+  char* ys = smem_raw + bnb_ys(g);
   unsigned* flag = reinterpret_cast<unsigned*>(ys + 128 * YP);
   __syncthreads();  // the K loop's fragment reads are done with the LDS
 #pragma unroll
@@ -608,7 +612,7 @@ __device__ __forceinline__ void ring_bnb_apply(const GemmArgs& g, f32x4 (&acc)[4
   const int rbase = m0 + wm * 64 + 4 * (lane >> 4);
   const int cbase = n0 + wn * 32 + (lane & 15);
   const avcbn::BwdFin& f = g.bnb_fin;
-  const char* ys = smem_raw + BNB_YS;
+  const char* ys = smem_raw + bnb_ys(g);
   const bool round16 = g.c == nullptr;
   const int C = g.N;
 #pragma unroll
@@ -1181,7 +1185,12 @@ void launch(const GemmArgs& g, int gm, hipStream_t s) {
 // rows of other utterances and the fragments need no per-lane predicate; otherwise a per-lane,
 // per-tap mask zeroes the A fragment rows whose shifted frame leaves the utterance.
 // X = activation, W = Wf[co][tap][ci] (forward) or dy and Wd[ci][tap'][co] (data gradient).
-constexpr int CV_TM = 128, CV_TN = 128, CV_TAPS = 5, CV_CBK = 32, CV_NST = 3;
+// CV_NST: LDS stages of the halo conv ring.  Two (98 KiB) rather than three (147 KiB): alone the
+// same time (29.0 vs 28.6 us at 8192 x 512 x 2560), but a side-stream weight-gradient workgroup
+// (48 KiB) now fits on a CU beside it, so a backward conv no longer waits for those to drain from
+// its CUs: C2 5.78-5.80 -> 5.74-5.75 ms (profiles/r5_conv_ring_slope.txt).  The one-utterance tile
+// (CU_NST) and the warp-specialised diagnostic form (WS_NST) keep three.
+constexpr int CV_TM = 128, CV_TN = 128, CV_TAPS = 5, CV_CBK = 32, CV_NST = 2, CU_NST = 3, WS_NST = 3;
 constexpr int CV_AI = (CV_TM + CV_TAPS - 1 + 15) / 16;  // 9 halo instructions (16 rows of 64 B)
 constexpr int CV_BI = CV_TAPS * CV_TN / 16;             // 40 weight instructions
 constexpr int CV_TOT = CV_AI + CV_BI;                   // 49
@@ -1404,7 +1413,7 @@ __device__ __forceinline__ void wait_cu(bool full) {
 }
 
 __global__ void __launch_bounds__(RNT, 2) conv_utt_kernel(GemmArgs g, int gm) {
-  constexpr int MI = 6, NJ = 2, P = CV_NST - 1;
+  constexpr int MI = 6, NJ = 2, P = CU_NST - 1;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1490,8 +1499,8 @@ __global__ void __launch_bounds__(RNT, 2) conv_utt_kernel(GemmArgs g, int gm) {
     if (ahead >= 1) wait_cu<1>(full);
     else wait_vm<0>();
     raw_barrier();
-    if (cs + P < nst) issue((cs + P) % CV_NST, cs + P);
-    const unsigned st = lds_addr(smem_raw + (cs % CV_NST) * CU_STAGE);
+    if (cs + P < nst) issue((cs + P) % CU_NST, cs + P);
+    const unsigned st = lds_addr(smem_raw + (cs % CU_NST) * CU_STAGE);
     auto read_tap = [&](auto kc, int slot) {
       constexpr int k = decltype(kc)::value;
       const unsigned a0 = st + aaddr[k], b0 = st + baddr;
@@ -1543,7 +1552,7 @@ __global__ void __launch_bounds__(RNT, 2) conv_utt_kernel(GemmArgs g, int gm) {
 void launch_conv_utt(const GemmArgs& g0, int gm, hipStream_t s) {
   GemmArgs g = g0;
   g.bn_rows = g.a.t_out;  // one statistics tile per utterance
-  const size_t lds = std::max((size_t)CV_NST * CU_STAGE, ring_epi_lds<CU_TM, CV_TN>());
+  const size_t lds = std::max((size_t)CU_NST * CU_STAGE, ring_epi_lds<CU_TM, CV_TN>());
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_utt_kernel),
@@ -1569,7 +1578,7 @@ constexpr int CW_LI = (CV_TOT + 3) / 4;  // 13: fills per stage of loader wave 4
 
 template <bool ALIGNED>
 __global__ void __launch_bounds__(RNT, 2) conv_ring_ws_kernel(GemmArgs g, int gm) {
-  constexpr int P = CV_NST - 1;
+  constexpr int P = WS_NST - 1;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1650,7 +1659,7 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_ws_kernel(GemmArgs g, int gm
         wait_vm<0>();
       }
       raw_barrier();
-      if (cs + P < nst) issue((cs + P) % CV_NST, cs + P);
+      if (cs + P < nst) issue((cs + P) % WS_NST, cs + P);
     }
   } else {
     // ---- MMA waves (wm, wn) = (wid >> 1, wid & 1): rows wm*64 .. +64, columns wn*64 .. +64
@@ -1680,7 +1689,7 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_ws_kernel(GemmArgs g, int gm
     }
     for (int cs = 0; cs < nst; ++cs) {
       raw_barrier();
-      const unsigned st = lds_addr(smem_raw + (cs % CV_NST) * CV_STAGE);
+      const unsigned st = lds_addr(smem_raw + (cs % WS_NST) * CV_STAGE);
       bf16x8 af[2][4], bfr[2][4];
       auto read_tap = [&](auto kc, int slot) {
         constexpr int k = decltype(kc)::value;
@@ -1756,7 +1765,7 @@ __global__ void __launch_bounds__(RNT, 2) conv_ring_ws_kernel(GemmArgs g, int gm
 
 template <bool ALIGNED>
 void launch_conv_ws(const GemmArgs& g, int gm, hipStream_t s) {
-  const size_t lds = std::max((size_t)CV_NST * CV_STAGE, ring_epi_lds<CV_TM, CV_TN>());
+  const size_t lds = std::max((size_t)WS_NST * CV_STAGE, ring_epi_lds<CV_TM, CV_TN>());
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_ws_kernel<ALIGNED>),
@@ -1769,11 +1778,13 @@ void launch_conv_ws(const GemmArgs& g, int gm, hipStream_t s) {
 
 template <bool ALIGNED, int ABL = 0, bool BNB = false>
 void launch_conv(const GemmArgs& g, int gm, hipStream_t s) {
-  const size_t lds = std::max((size_t)CV_NST * CV_STAGE, ring_epi_lds<CV_TM, CV_TN>());
+  const size_t base = std::max((size_t)CV_NST * CV_STAGE, ring_epi_lds<CV_TM, CV_TN>());
+  const size_t hi = std::max(base, (size_t)BNB_YS_HI + BNB_YBYTES);  // the fused BN-backward apply's y tile
+  const size_t lds = (BNB && g.bnb_dy16) ? hi : base;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<ALIGNED, ABL, BNB>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)hi);
     attr = true;
   }
   const int nb = ((g.M + CV_TM - 1) / CV_TM) * ((g.N + CV_TN - 1) / CV_TN);
