@@ -1412,8 +1412,9 @@ __device__ __forceinline__ void wait_cu(bool full) {
   else wait_vm<N * (CU_LW - 1)>();
 }
 
+template <int NSTU>
 __global__ void __launch_bounds__(RNT, 2) conv_utt_kernel(GemmArgs g, int gm) {
-  constexpr int MI = 6, NJ = 2, P = CU_NST - 1;
+  constexpr int MI = 6, NJ = 2, P = NSTU - 1;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1499,8 +1500,8 @@ __global__ void __launch_bounds__(RNT, 2) conv_utt_kernel(GemmArgs g, int gm) {
     if (ahead >= 1) wait_cu<1>(full);
     else wait_vm<0>();
     raw_barrier();
-    if (cs + P < nst) issue((cs + P) % CU_NST, cs + P);
-    const unsigned st = lds_addr(smem_raw + (cs % CU_NST) * CU_STAGE);
+    if (cs + P < nst) issue((cs + P) % NSTU, cs + P);
+    const unsigned st = lds_addr(smem_raw + (cs % NSTU) * CU_STAGE);
     auto read_tap = [&](auto kc, int slot) {
       constexpr int k = decltype(kc)::value;
       const unsigned a0 = st + aaddr[k], b0 = st + baddr;
@@ -1552,15 +1553,22 @@ __global__ void __launch_bounds__(RNT, 2) conv_utt_kernel(GemmArgs g, int gm) {
 void launch_conv_utt(const GemmArgs& g0, int gm, hipStream_t s) {
   GemmArgs g = g0;
   g.bn_rows = g.a.t_out;  // one statistics tile per utterance
-  const size_t lds = std::max((size_t)CU_NST * CU_STAGE, ring_epi_lds<CU_TM, CV_TN>());
+  // AVC_CU_NST = 2: two LDS stages (106 KiB, room for a side-stream workgroup beside it)
+  static const int nstu = [] {
+    const char* e = getenv("AVC_CU_NST");
+    return e && atoi(e) == 2 ? 2 : CU_NST;
+  }();
+  const size_t lds = std::max((size_t)nstu * CU_STAGE, ring_epi_lds<CU_TM, CV_TN>());
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_utt_kernel),
+    (void)hipFuncSetAttribute(nstu == 2 ? reinterpret_cast<const void*>(&conv_utt_kernel<2>)
+                                        : reinterpret_cast<const void*>(&conv_utt_kernel<3>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int nb = (g.M / g.a.t_out) * ((g.N + CV_TN - 1) / CV_TN);
-  conv_utt_kernel<<<nb, RNT, lds, s>>>(g, gm);
+  if (nstu == 2) conv_utt_kernel<2><<<nb, RNT, lds, s>>>(g, gm);
+  else conv_utt_kernel<3><<<nb, RNT, lds, s>>>(g, gm);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1964,7 +1972,13 @@ bool gemm_ring_launch_(const GemmArgs& g_in, hipStream_t s) {
       int bm, bn, nst, occ;
       double eff;
     };
-    const Opt opts[4] = {{256, 256, 2, 1, 1.0}, {256, 128, 3, 1, 0.85}, {128, 128, 4, 1, 0.75},
+    // AVC_RING_NST128: ring slots of the 128 x 128 tile (4 = 128 KiB; 3 = 96 KiB leaves room for a
+    // side-stream workgroup beside it, as the 2-stage halo conv does)
+    static const int nst128 = [] {
+      const char* e = getenv("AVC_RING_NST128");
+      return e && atoi(e) == 3 ? 3 : 4;
+    }();
+    const Opt opts[4] = {{256, 256, 2, 1, 1.0}, {256, 128, 3, 1, 0.85}, {128, 128, nst128, 1, 0.75},
                          {128, 128, 2, 2, g.agrad ? 0.38 : 0.47}};
     double best = 0;
     bm = 0;
