@@ -356,9 +356,12 @@ def main():
         trainer = TrainStep(model, lr=1e-4)
 
     graph = args.graph or args.graph_fwd or args.graph_one
-    # the recorded replay (replay.py) is the default step form: the same kernels, streams and event
-    # edges as the eager step, with no per-kernel Python, so a slow host does not set the step time
-    replay = not (args.eager or graph) and trainer.replayable()
+    # the recorded replay (replay.py) is the default step form of the AutoVC steps: the same kernels,
+    # streams and event edges as the eager step, with no per-kernel Python, so a slow host does not
+    # set the step time.  The MetaConv / MetaPool steps (~29 ms) are never host-bound and ran ~1 %
+    # faster eager (29.13-29.23 vs 29.52-29.54 ms, profiles/r5_replay_ab.txt): eager unless --replay
+    host_bound = args.model not in ("MetaConv", "MetaPool")
+    replay = not (args.eager or graph) and trainer.replayable() and (args.replay or host_bound)
     for _ in range(args.warmup):
         trainer.step(x, e)
     if graph:
