@@ -29,6 +29,9 @@ _ABLATE_WGRAD = os.environ.get("AVC_ABLATE_WGRAD") == "1"
 # start later than the per-pack events do), so off unless asked for
 _PACK_BATCH = os.environ.get("AVC_PACK_BATCH", "0") == "1"
 _CONV_DW_DIRECT = os.environ.get("AVC_CONV_DW_DIRECT", "1") != "0"
+# conv dW split over the halo kernel's own 128 x 160 tiles (6 instead of 5 at 512 x 2560: 49.2 vs 50.7 us
+# isolated) -- in the C2 step no different (5.783 / 5.784 vs 5.782 / 5.762 ms, r5full4): off
+_HALO_SPLIT = os.environ.get("AVC_HALO_SPLIT", "0") != "0"
 
 # ---------------------------------------------------------------- gradient sink / side stream
 # In "sink" mode (set by TrainStep) parameter gradients are accumulated by the kernels
@@ -462,13 +465,20 @@ def conv_wgrad(dy, x, B, T_in, T_out, w, pad, into=None):
     (accumulated into `into`, e.g. the parameter's .grad, when given)."""
     Co, Ci, Kw = w.shape
     M = B * T_out
+    halo = Kw == 5 and 2 * pad == Kw - 1 and T_in == T_out and Ci % 32 == 0 and M % T_out == 0
     sk = K.auto_split_k(Co, Kw * Ci, M)
+    if halo and _HALO_SPLIT:
+        # the halo dW kernel's output tiles are 128 channels x (5 taps x 32 input channels): split over
+        # those when the partials are reduced in the kernel (512 x 2560: 64 tiles -> 6 splits, 49.2 vs
+        # 50.7 us at 5; tools/tt_bench.py)
+        sk_h = K.auto_split_k(Co, Kw * Ci, M, tiles=-(-Co // 128) * (Ci // 32))
+        if K.tt_splitk_reduced(sk_h):
+            sk = sk_h
     # the direct [Co][Ci][K] epilogue scatters its columns 4*Kw bytes apart: with split-K atomics
     # that is ~Kw x the atomic requests of the packed layout (measured +0.9 ms per C2 step), so
     # split products reduced by atomics go through the packed dWf and one unpack pass instead;
     # on the halo weight-gradient kernel (gemm_tt.hip: 5-tap 'same', Ci % 32 == 0) a product whose
     # partials the last split reduces (K.tt_splitk_reduced) stores the layout directly, 16-B runs
-    halo = Kw == 5 and 2 * pad == Kw - 1 and T_in == T_out and Ci % 32 == 0 and M % T_out == 0
     if not _CONV_DW_DIRECT or (sk > 1 and Kw > 1 and not (halo and K.tt_splitk_reduced(sk))):
         dWf = torch.empty(Co, Kw * Ci, device=x.device)
         K.gemm(Co, Kw * Ci, M, operand(dy, Co, kstrided=True),
