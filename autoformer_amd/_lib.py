@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AVC_LIB_PATH") or os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["gemm_ring.hip", "gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "graph.hip", "fold.hip", "disc.hip"]
-ABI_VERSION = 27
+ABI_VERSION = 28
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -101,7 +101,7 @@ _SIGS = {
     "avc_lstm2_bwd_persistent": (c_int, [c_int, c_int, c_int]),
     "avc_lstm2_bwd_scratch_bytes": (c_size, [c_int, c_int]),
     "avc_lstm2_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
-                              c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                              c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "avc_lstm_persistent": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "avc_enc_concat": (c_int, [c_void_p, c_ll, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_codes_gather": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),

@@ -1512,8 +1512,10 @@ struct Persist2BwdArgs {
   const bf16* wt0;       // W_hh0^T [H][4H]
   const bf16* wti1;      // W_ih1^T [H][4H]
   const bf16* wt1;       // W_hh1^T [H][4H]
-  float* dg[2];          // (B,T,4H) dL/d(pre-activation gates)
+  float* dg[2];          // (B,T,4H) dL/d(pre-activation gates); nullable (bf16 twin only)
   bf16* dg16[2];
+  float* dbp;            // [layer][group][4H] per-group bias-gradient partials (sum of dG over the group's
+                         // utterances and steps); nullable
   unsigned* ctl;
   bf16* pay;  // [layer][2 parities][B][4H]
   unsigned long long* trace;
@@ -1600,6 +1602,7 @@ __global__ void __launch_bounds__(PNT, 1) lstm2_persist_bwd(Persist2BwdArgs a) {
   const bool cv = cb < B;
   const unsigned aoff = (unsigned)(((lane & 15) * BCP + w * KPW * 32 + 8 * (lane >> 4)) * 2);
   float dc = 0.f;
+  float sb0 = 0.f, sb1 = 0.f, sb2 = 0.f, sb3 = 0.f;  // this cell's dG summed over its steps (dbp)
   __syncthreads();
 
   for (int k = 0; k <= T; ++k) {
@@ -1681,6 +1684,10 @@ __global__ void __launch_bounds__(PNT, 1) lstm2_persist_bwd(Persist2BwdArgs a) {
       v2 = dcs * gi * (1.f - gg * gg);  // d(pre g)
       v3 = dh * tc * go * (1.f - go);   // d(pre o)
       dc = dcs * gf;
+      sb0 += v0;
+      sb1 += v1;
+      sb2 += v2;
+      sb3 += v3;
     }
     bf16* dsr = ds16 + (L * QRG + cr) * (4 * QJU) + cu;
     dsr[0] = (bf16)v0;
@@ -1705,11 +1712,13 @@ __global__ void __launch_bounds__(PNT, 1) lstm2_persist_bwd(Persist2BwdArgs a) {
     if (a.opt & 1) __syncthreads();  // every wave's stores behind wave 0's flag
     if (act) {  // (wave 0 issues these after its flag: they stay off the hand-off's vmcnt wait)
       const long long og = ((long long)cb * T + t) * G + cj;
-      float* d = a.dg[L] + og;
-      d[0] = v0;
-      d[H] = v1;
-      d[2 * H] = v2;
-      d[3 * H] = v3;
+      if (a.dg[L]) {
+        float* d = a.dg[L] + og;
+        d[0] = v0;
+        d[H] = v1;
+        d[2 * H] = v2;
+        d[3 * H] = v3;
+      }
       if (a.dg16[L] && !(a.opt & 2)) {
         bf16* d16 = a.dg16[L] + og;
         d16[0] = (bf16)v0;
@@ -1719,6 +1728,25 @@ __global__ void __launch_bounds__(PNT, 1) lstm2_persist_bwd(Persist2BwdArgs a) {
       }
     }
     if (k < T) stamp(a.trace, T, k, 3);
+  }
+  if (a.dbp) {
+    // the bias gradients' share of this member: dG summed over the group's 16 utterances (LDS, in
+    // row order) and T steps (registers, in step order), one plain store per (layer, gate, unit) --
+    // deterministic, and the fp32 dG (B x T x 4H per layer) need not be stored for a column sum
+    float* sb = red;  // [L][q][16 rows][16 units] = 8 KiB of chunk tile 0
+    __syncthreads();  // the last tick's reads of red / ds16 are done
+    sb[((L * 4 + 0) * QRG + cr) * QJU + cu] = sb0;
+    sb[((L * 4 + 1) * QRG + cr) * QJU + cu] = sb1;
+    sb[((L * 4 + 2) * QRG + cr) * QJU + cu] = sb2;
+    sb[((L * 4 + 3) * QRG + cr) * QJU + cu] = sb3;
+    __syncthreads();
+    if (tid < 2 * 4 * QJU) {
+      const int l = tid >> 6, q = (tid >> 4) & 3, u = tid & 15;
+      float sum = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < QRG; ++rr) sum += sb[((l * 4 + q) * QRG + rr) * QJU + u];
+      a.dbp[((long long)l * a.ng + g) * G + q * H + j0 + u] = sum;
+    }
   }
 }
 
@@ -2004,9 +2032,9 @@ extern "C" size_t avc_lstm2_bwd_scratch_bytes(int B, int H) {
 extern "C" int avc_lstm2_bwd(const float* dh1, const float* c0, const float* gates0, const float* c1,
                              const float* gates1, const void* w_hh0_t, const void* w_ih1_t, const void* w_hh1_t, int B,
                              int T, int H, float* dg0, void* dg0_bf16, float* dg1, void* dg1_bf16, void* buf,
-                             void* stream) {
-  AVC_CHECK_ARG(dh1 && c0 && gates0 && c1 && gates1 && w_hh0_t && w_ih1_t && w_hh1_t && dg0 && dg1 && buf && B > 0 &&
-                    T > 0,
+                             float* db_part, void* stream) {
+  AVC_CHECK_ARG(dh1 && c0 && gates0 && c1 && gates1 && w_hh0_t && w_ih1_t && w_hh1_t && (dg0 || dg0_bf16) &&
+                    (dg1 || dg1_bf16) && buf && B > 0 && T > 0,
                 "avc_lstm2_bwd: bad args");
   AVC_CHECK_ARG(persist2_bwd_path(B, H, true), "avc_lstm2_bwd: shape B=%d H=%d not supported (see avc_lstm2_bwd_persistent)",
                 B, H);
@@ -2025,6 +2053,7 @@ extern "C" int avc_lstm2_bwd(const float* dh1, const float* c0, const float* gat
   p.dg[1] = dg1;
   p.dg16[0] = reinterpret_cast<bf16*>(dg0_bf16);
   p.dg16[1] = reinterpret_cast<bf16*>(dg1_bf16);
+  p.dbp = db_part;
   p.ctl = reinterpret_cast<unsigned*>(buf);
   p.pay = reinterpret_cast<bf16*>(reinterpret_cast<char*>(buf) + px_payload_off(ng));
   p.trace = g_trace;

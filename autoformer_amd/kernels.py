@@ -459,13 +459,16 @@ def lstm2_bwd_persistent(B, H):
     return bool(L.lib().avc_lstm2_bwd_persistent(int(B), int(H), _COMPUTE))
 
 
-def lstm2_bwd(dh1, c0, g0, c1, g1, wt0, wti1, wt1, B, T, H):
+def lstm2_bwd(dh1, c0, g0, c1, g1, wt0, wti1, wt1, B, T, H, fp32=True, db=False):
     """Backward of the two stacked layers in one persistent launch: (dG0, dG1), each fp32 with its
-    bf16 twin.  wt0 / wti1 / wt1: W_hh0^T, W_ih1^T, W_hh1^T as bf16 [H][4H]."""
+    bf16 twin, or (fp32=False) the bf16 tensors alone.  wt0 / wti1 / wt1: W_hh0^T, W_ih1^T, W_hh1^T
+    as bf16 [H][4H].  db: also return the (2, ceil(B/16), 4H) per-group sums of dG over utterances
+    and steps (avc_lstm2_bwd db_part), whose column sums are the layers' bias gradients."""
     dev = dh1.device
     fault_word(dev)
-    outs = [torch.empty(B * T, 4 * H, device=dev) for _ in range(2)]
+    outs = [torch.empty(B * T, 4 * H, device=dev) for _ in range(2)] if fp32 else [None, None]
     o16 = [torch.empty(B * T, 4 * H, device=dev, dtype=torch.bfloat16) for _ in range(2)]
+    dbp = torch.empty(2, -(-B // 16), 4 * H, device=dev) if db else None
     buf = torch.empty(int(L.lib().avc_lstm2_bwd_scratch_bytes(int(B), int(H))), device=dev, dtype=torch.uint8)
     timed = LAUNCH_TIMING is not None and H == LAUNCH_TIMING_H
     if timed:
@@ -476,15 +479,16 @@ def lstm2_bwd(dh1, c0, g0, c1, g1, wt0, wti1, wt1, B, T, H):
         box, s = [], torch.cuda.current_stream()
         rec.add_marker(lambda: _timing_mark(box, s, 0))
     L.call("avc_lstm2_bwd", dh1.data_ptr(), c0.data_ptr(), g0.data_ptr(), c1.data_ptr(), g1.data_ptr(), wt0.data_ptr(),
-           wti1.data_ptr(), wt1.data_ptr(), B, T, H, outs[0].data_ptr(), o16[0].data_ptr(), outs[1].data_ptr(),
-           o16[1].data_ptr(), buf.data_ptr(), stream())
+           wti1.data_ptr(), wt1.data_ptr(), B, T, H, _ptr(outs[0]), o16[0].data_ptr(), _ptr(outs[1]),
+           o16[1].data_ptr(), buf.data_ptr(), _ptr(dbp), stream())
     if rec is not None:
         rec.add_marker(lambda: _timing_mark(box, s, 1))
     if timed:
         ev[1].record()
         LAUNCH_TIMING.append(ev)
     _CACHE["lstm2_bwd_buf"] = buf  # kept alive until the next call (the launch is asynchronous)
-    return attach_twin(outs[0], o16[0]), attach_twin(outs[1], o16[1])
+    dg = (attach_twin(outs[0], o16[0]), attach_twin(outs[1], o16[1])) if fp32 else (o16[0], o16[1])
+    return (*dg, dbp) if db else dg
 
 
 def lstm_persistent_bwd(B, H, dirs):

@@ -944,9 +944,11 @@ class LSTMLayerCore:
         h, c, g = K.lstm_fwd(xproj, whh, B, T, H, dirs, hbuf)
         return h, (c, g)
 
-    def backward(self, dh, x, h, saved, B, T, need_dx, dg=None, defer=False):
-        """dg: the gate gradients when a fused launch already produced them (the lstm2 wavefront).
-        defer: the weight gradients go to the side stream at the next flush_deferred()."""
+    def backward(self, dh, x, h, saved, B, T, need_dx, dg=None, defer=False, dbp=None):
+        """dg: the gate gradients when a fused launch already produced them (the lstm2 wavefront:
+        bf16 only when it also gave dbp, the (groups, 4H) partial sums of dg whose column sums are
+        the bias gradients).  defer: the weight gradients go to the side stream at the next
+        flush_deferred()."""
         c, g = saved
         H, dirs = self.H, self.dirs
         In = x.shape[1]
@@ -979,11 +981,12 @@ class LSTMLayerCore:
                 K.gemm(4 * H, H, M, operand(dgd, G, kstrided=True),
                        operand(hd, dirs * H, kstrided=True, window=(1, shift, T, T, H)), dwhh,
                        split_k=K.auto_split_k(4 * H, H, M), accumulate=sink)
-                dg32 = dg if dirs == 1 else dg[:, d * 4 * H:]
+                # bias gradients: column sums of dG, or of the wavefront's per-group partials
+                dg32, rows = (dg if dirs == 1 else dg[:, d * 4 * H:], M) if dbp is None else (dbp, dbp.shape[0])
                 if sink:
-                    K.colsum(dg32, M, 4 * H, ld=G, out=_grad_of(b_ih), out2=_grad_of(b_hh), accumulate=True)
+                    K.colsum(dg32, rows, 4 * H, ld=G, out=_grad_of(b_ih), out2=_grad_of(b_hh), accumulate=True)
                     continue
-                dbd = K.colsum(dg32, M, 4 * H, ld=G)
+                dbd = K.colsum(dg32, rows, 4 * H, ld=G)
                 # b_ih and b_hh receive the same gradient but must not share storage
                 grads += [dwih, dwhh, dbd, K.convert(dbd, K.F32)]
             return grads
@@ -993,11 +996,11 @@ class LSTMLayerCore:
             dx = torch.empty(M, In, device=x.device, dtype=x.dtype)  # bf16 for a bf16-stored input
             K.gemm(M, In, G, operand(dg, G), operand(wih_t, G), dx)
         if sink and defer and not _ABLATE_WGRAD:
-            defer_side(wgrads, dg, x, h, dg_op, h_op)
+            defer_side(wgrads, dg, x, h, dg_op, h_op, dbp)
             grads = [None] * (4 * dirs)
         elif sink:
             with _Side(ev) as sd:
-                sd.keep(dg, x, h, dg_op, h_op)
+                sd.keep(dg, x, h, dg_op, h_op, dbp)
                 if not _ABLATE_WGRAD:
                     wgrads()
             grads = [None] * (4 * dirs)
@@ -1066,10 +1069,16 @@ class _LSTMPairFn(torch.autograd.Function):
             (cs0, gs0), (cs1, gs1) = ctx.saved
             wt0 = c0.packs()[3]
             _, _, _, wt1, wti1 = c1.packs()
-            dg0, dg1 = K.lstm2_bwd(dh1.contiguous(), cs0, gs0, cs1, gs1, wt0, wti1, wt1, B, T, H)
-            _, g1 = c1.backward(None, h0, h1, ctx.saved[1], B, T, False, dg=dg1, defer=_DEFER_LSTM2_WG)
+            if _PAIR_DB:  # bf16 dG only, the bias gradients from the kernel's per-group partials
+                dg0, dg1, dbp = K.lstm2_bwd(dh1.contiguous(), cs0, gs0, cs1, gs1, wt0, wti1, wt1, B, T, H,
+                                            fp32=False, db=True)
+                dbp0, dbp1 = dbp[0], dbp[1]
+            else:
+                dg0, dg1 = K.lstm2_bwd(dh1.contiguous(), cs0, gs0, cs1, gs1, wt0, wti1, wt1, B, T, H)
+                dbp0 = dbp1 = None
+            _, g1 = c1.backward(None, h0, h1, ctx.saved[1], B, T, False, dg=dg1, defer=_DEFER_LSTM2_WG, dbp=dbp1)
             dx, g0 = c0.backward(None, x, h0, ctx.saved[0], B, T, ctx.needs_input_grad[0], dg=dg0,
-                                 defer=_DEFER_LSTM2_WG)
+                                 defer=_DEFER_LSTM2_WG, dbp=dbp0)
             return (dx, None, None, None, None, *g0, *g1)
         dh0, g1 = c1.backward(dh1.contiguous(), h0, h1, ctx.saved[1], B, T, True)
         dx, g0 = c0.backward(dh0, x, h0, ctx.saved[0], B, T, ctx.needs_input_grad[0])
@@ -1080,6 +1089,9 @@ _PAIR_OFF = bool(os.environ.get("AVC_LSTM2_OFF"))
 # the pair's backward as one wavefront launch (avc_lstm2_bwd; C2 5.83 -> 5.81 ms, isolated 1127 -> ~1050 us,
 # profiles/r5_lstm2_bwd_wavefront.txt); "0": two single-layer launches + the dX1 GEMM
 _PAIR_BWD = os.environ.get("AVC_LSTM2_BWD", "1") != "0"
+# the wavefront backward writes bf16 dG only (its GEMM operands) plus per-group bias-gradient partials,
+# instead of fp32 dG + bf16 twin and a column-sum pass over the fp32 dG (ABI 28); "0": the fp32 form
+_PAIR_DB = os.environ.get("AVC_LSTM2_DB", "1") != "0"
 
 
 def lstm(mod, cores, x, B, T):

@@ -67,9 +67,11 @@ def kernel_timing_wave(model, B, T, reps=3):
     wavefront launch of T + 1 ticks): the dominant kernel when the step runs it.  FLOP per launch: the
     three recurrent products per step (W_hh1^T, W_ih1^T, W_hh0^T: 2 * B * 4H * H each) over T steps.
     Algorithmic bytes: the three transposed weights once (3 * 4H * H bf16) + per step
-    dL/dh1 fp32 (B*H*4) + per layer c_t, c_{t-1} fp32 (2*B*H*4) + gates fp32 (B*4H*4) + dG fp32 and
-    bf16 out (B*4H*6)."""
+    dL/dh1 fp32 (B*H*4) + per layer c_t, c_{t-1} fp32 (2*B*H*4) + gates fp32 (B*4H*4) + dG out: bf16
+    (B*4H*2) in the step's form (layers._PAIR_DB: bf16 dG + per-group bias partials, ABI 28), fp32 and
+    bf16 (B*4H*6) otherwise; timed in the form the step runs."""
     from autoformer_amd import kernels as K
+    from autoformer_amd import layers as Ly
 
     c0, c1 = model.decoder._lstm2
     wt0 = c0.packs()[3]
@@ -80,18 +82,19 @@ def kernel_timing_wave(model, B, T, reps=3):
     dh = torch.randn(B * T, H, device=dev, generator=g) * 0.1
     cs = [torch.randn(B * T, H, device=dev, generator=g) * 0.5 for _ in range(2)]
     gs = [torch.rand(B * T, 4 * H, device=dev, generator=g) for _ in range(2)]
-    K.lstm2_bwd(dh, cs[0], gs[0], cs[1], gs[1], wt0, wti1, wt1, B, T, H)  # warm
+    db = Ly._PAIR_DB
+    K.lstm2_bwd(dh, cs[0], gs[0], cs[1], gs[1], wt0, wti1, wt1, B, T, H, fp32=not db, db=db)  # warm
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(reps):
-        K.lstm2_bwd(dh, cs[0], gs[0], cs[1], gs[1], wt0, wti1, wt1, B, T, H)
+        K.lstm2_bwd(dh, cs[0], gs[0], cs[1], gs[1], wt0, wti1, wt1, B, T, H, fp32=not db, db=db)
     e1.record(s)
     torch.cuda.synchronize()
     K.check_faults()
     avg_us = e0.elapsed_time(e1) * 1e3 / reps
     G = 4 * H
-    alg_bytes = 3 * G * H * 2 + T * (B * H * 4 + 2 * (2 * B * H * 4 + B * G * 4 + B * G * 6))
+    alg_bytes = 3 * G * H * 2 + T * (B * H * 4 + 2 * (2 * B * H * 4 + B * G * 4 + B * G * (2 if db else 6)))
     return {"kernel": DOMINANT_WAVE + " (decoder lstm2 backward, both layers in one wavefront launch, T=%d, B=%d, "
             "H=%d)" % (T, B, H), "avg_us": avg_us, "bytes": float(alg_bytes), "flops": 3 * 2.0 * B * G * H * T}
 

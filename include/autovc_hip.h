@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 27
+#define AVC_ABI_VERSION 28
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -301,14 +301,18 @@ int avc_gemm_set_ring(int mode, int bm, int bn, int nst, int gm, int win);
  * gradient dG1 W_ih1 is formed inside the recurrence.  dh1 = dL/dh of layer 1's output (B,T,H);
  * c0/gates0, c1/gates1 the forward's cell states and activated gates (avc_lstm2_fwd); w_hh0_t,
  * w_ih1_t, w_hh1_t the transposed bf16 weights [H][4H]; outputs dg0 / dg1 = dL/d(pre-activation
- * gates) (B,T,4H) fp32 with optional bf16 twins.  buf: avc_lstm2_bwd_scratch_bytes(B, H) bytes.
+ * gates) (B,T,4H) fp32 and / or their bf16 twins (each layer needs one of the two; ABI 28: the fp32
+ * form is optional).  db_part (nullable, ABI 28): [2 layers][ceil(B/16) groups][4H] floats, each the
+ * layer's dG summed over one 16-utterance group and every step -- the column sums of dG that make
+ * the bias gradients (b_ih, b_hh: AutoVC.py:96's nn.LSTM), so the fp32 dG need not be stored for them.
+ * buf: avc_lstm2_bwd_scratch_bytes(B, H) bytes.
  * bf16 compute, H = 1024, the whole grid resident (avc_lstm2_bwd_persistent).  Replaces
  * nn.LSTM.backward of AutoVC.py:96,110's two-layer lstm2 (two avc_lstm_bwd + the dX1 GEMM). */
 int avc_lstm2_bwd_persistent(int B, int H, int compute);
 size_t avc_lstm2_bwd_scratch_bytes(int B, int H);
 int avc_lstm2_bwd(const float* dh1, const float* c0, const float* gates0, const float* c1, const float* gates1,
                   const void* w_hh0_t, const void* w_ih1_t, const void* w_hh1_t, int B, int T, int H, float* dg0,
-                  void* dg0_bf16, float* dg1, void* dg1_bf16, void* buf, void* stream);
+                  void* dg0_bf16, float* dg1, void* dg1_bf16, void* buf, float* db_part, void* stream);
 
 /* Which deep-ring kernel the last avc_gemm on this host thread launched (tests, tools): 0 none (an
  * older kernel), 1 gemm_ring_kernel, 2 the 128-row halo conv (conv_ring_kernel, its BN-backward

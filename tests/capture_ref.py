@@ -299,18 +299,29 @@ class Capture:
         self.records.append(("lstm_bwd", f"lstm_bwd B{B} T{T} H{H} dirs{dirs}", res))
         return dg
 
-    def _lstm2_bwd(self, dh1, c0, g0, c1, g1, wt0, wti1, wt1, B, T, H):
+    def _lstm2_bwd(self, dh1, c0, g0, c1, g1, wt0, wti1, wt1, B, T, H, fp32=True, db=False):
         """The two-layer wavefront backward against the layer-by-layer fp64 reference: layer 1 from
-        dh1, layer 0 from dG1 W_ih1 (the dX1 the wavefront forms inside its recurrence)."""
+        dh1, layer 0 from dG1 W_ih1 (the dX1 the wavefront forms inside its recurrence); with db, the
+        per-group bias-gradient partials against the fp64 dG summed over each 16-utterance group."""
         torch.cuda.synchronize()
-        dg0, dg1 = self._orig["lstm2_bwd"](dh1, c0, g0, c1, g1, wt0, wti1, wt1, B, T, H)
+        out = self._orig["lstm2_bwd"](dh1, c0, g0, c1, g1, wt0, wti1, wt1, B, T, H, fp32=fp32, db=db)
         torch.cuda.synchronize()
+        dg0, dg1 = out[0], out[1]
         ref1 = lstm_bwd_ref(dh1, c1, g1, wt1.t(), B, T, H, 1)
         ref0 = lstm_bwd_ref(ref1 @ wti1.double().t(), c0, g0, wt0.t(), B, T, H, 1)
-        res = {"dG0": _rel(dg0, ref0), "dG1": _rel(dg1, ref1), "dG0_bf16": _rel(dg0._bf16, ref0),
-               "dG1_bf16": _rel(dg1._bf16, ref1)}
+        res = {}
+        if fp32:
+            res["dG0"], res["dG1"] = _rel(dg0, ref0), _rel(dg1, ref1)
+            dg0, dg1 = dg0._bf16, dg1._bf16
+        res["dG0_bf16"], res["dG1_bf16"] = _rel(dg0, ref0), _rel(dg1, ref1)
+        if db:
+            ng = -(-B // 16)
+            for layer, ref in ((0, ref0), (1, ref1)):
+                r = torch.zeros(ng * 16, T, 4 * H, dtype=torch.float64, device=ref.device)
+                r[:B] = ref.reshape(B, T, 4 * H)
+                res[f"db{layer}"] = _rel(out[2][layer], r.view(ng, 16 * T, 4 * H).sum(1))
         self.records.append(("lstm2_bwd", f"lstm2_bwd B{B} T{T} H{H}", res))
-        return dg0, dg1
+        return out
 
     def _bn_apply(self, y, scale, shift, act, residual=None, out=None, twin16=None, out_bf16=False):
         torch.cuda.synchronize()

@@ -40,6 +40,9 @@ def main():
     def wave():
         return K.lstm2_bwd(gy, cs0, gs0, cs1, gs1, wt0, wti1, wt1, B, T, H)
 
+    def wave16():  # the step's form (ABI 28): bf16 dG + per-group bias partials
+        return K.lstm2_bwd(gy, cs0, gs0, cs1, gs1, wt0, wti1, wt1, B, T, H, fp32=False, db=True)
+
     def two():
         dg1 = K.lstm_bwd(gy, h1, cs1, gs1, None, wt1, B, T, H, 1)
         dh0 = torch.empty(B * T, H, device=dev)
@@ -59,7 +62,8 @@ def main():
             ts.append(a.elapsed_time(b) * 1e3)
         return min(ts), sorted(ts)[len(ts) // 2]
 
-    for name, f in (("wavefront", wave), ("two launches + GEMM", two), ("wavefront", wave), ("two launches + GEMM", two)):
+    for name, f in (("wavefront", wave), ("wavefront bf16 + db", wave16), ("two launches + GEMM", two),
+                    ("wavefront", wave), ("wavefront bf16 + db", wave16), ("two launches + GEMM", two)):
         mn, md = ev(f)
         print(f"{name:22s} min {mn:7.1f} us  med {md:7.1f} us", flush=True)
     (a0, a1), (b0, b1) = wave(), two()
