@@ -28,6 +28,7 @@ class Adjust(nn.Module):
     def forward(self, x, emb, stat_updates=1):
         """stat_updates = 2: this call stands for two reference calls on identical inputs (the
         outputs are identical; each BatchNorm's running statistics move twice, as there)."""
+        K.require_device(x, emb)
         mel, B, T = _frames(x)
         for core in self._convs:
             core.stat_updates = stat_updates

@@ -75,6 +75,7 @@ class Encoder(nn.Module):
         return Lyr.codes(h, B, T, self.dim_neck, self.freq)
 
     def forward(self, x, c_org):
+        K.require_device(x, c_org)
         return list(self.codes_flat(x, c_org).split(2 * self.dim_neck, dim=-1))
 
 
@@ -109,6 +110,7 @@ class Decoder(nn.Module):
         return Lyr.linear(h, lin.weight, lin.bias, self._lin)
 
     def forward(self, x):
+        K.require_device(x)
         xf, B, T = _frames(x)
         return self.frames(xf, B, T).view(B, T, -1)
 
@@ -134,6 +136,7 @@ class Postnet(nn.Module):
 
     def forward(self, x):
         """Reference layout (B, 80, T) in and out."""
+        K.require_device(x)
         B, C, T = x.shape
         xf = Lyr.bct_to_frames(x)
         return Lyr.frames_to_bct(self.frames(xf, B, T), B, T)
@@ -150,6 +153,7 @@ class AutoVC(nn.Module):
         self.dim_neck = dim_neck
 
     def forward(self, x, c_org, c_trg):
+        K.require_device(x, c_org, c_trg)
         codes = self.encoder.codes_flat(x, c_org)
         if c_trg is None:
             return codes

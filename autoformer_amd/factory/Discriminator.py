@@ -123,6 +123,7 @@ class Discriminator(nn.Module):
         return K.bn_eval(bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.eps)
 
     def forward(self, x):
+        K.require_device(x)
         ps = [self.conv1.weight, self.conv1.bias, self.conv2.weight, self.conv2.bias, self.conv3.weight,
               self.conv3.bias, self.bn1.weight, self.bn1.bias, self.bn2.weight, self.bn2.bias, self.dense1.weight,
               self.dense1.bias]

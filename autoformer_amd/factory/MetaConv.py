@@ -90,6 +90,7 @@ class Encoder(nn.Module):
         return Lyr.codes(h, B, T, self.dim_neck, self.freq)
 
     def forward(self, x, c_org):
+        K.require_device(x, c_org)
         return list(self.codes_flat(x, c_org).split(2 * self.dim_neck, dim=-1))
 
 
@@ -124,6 +125,7 @@ class Decoder(nn.Module):
         return Lyr.linear(h2, lin.weight, lin.bias, self._lin)
 
     def forward(self, x):
+        K.require_device(x)
         xf, B, T = _frames(x)
         return self.frames(xf, B, T).view(B, T, -1)
 
@@ -139,6 +141,7 @@ class MetaConv(nn.Module):
         self.dim_neck = dim_neck
 
     def forward(self, x, c_org, c_trg):
+        K.require_device(x, c_org, c_trg)
         codes = self.encoder.codes_flat(x, c_org)
         if c_trg is None:
             return codes

@@ -56,6 +56,7 @@ def adain_encoder(Base):
             return self.codes_frames(h, c_org, B, T), feats
 
         def forward(self, x, c_org):
+            K.require_device(x, c_org)
             codes, feats = self.codes_and_features(x, c_org)
             return list(codes.split(2 * self.dim_neck, dim=-1)), feats
 
@@ -85,6 +86,7 @@ class PostnetAdaIN(Postnet):
 
     def forward(self, x, features):
         """Reference layout (B, 80, T) in and out."""
+        K.require_device(x, features)
         B, C, T = x.shape
         return Lyr.frames_to_bct(self.frames(Lyr.bct_to_frames(x), B, T, features), B, T)
 
@@ -93,6 +95,7 @@ class AdaINModel(nn.Module):
     """forward of AutoVC2 / MetaConv2 / MetaPool2 (AutoVC2.py:213-242)."""
 
     def forward(self, x, c_org, c_trg, target_feature=None):
+        K.require_device(x, c_org, c_trg, target_feature)
         codes, feats = self.encoder.codes_and_features(x, c_org)
         if c_trg is None and target_feature is None:
             return codes, feats
@@ -108,6 +111,7 @@ class AdjustModel(nn.Module):
         self.adjust = Adjust(dim_emb)
 
     def forward(self, x, c_org, c_trg, isConvert=False, x_target=None):
+        K.require_device(x, c_org, c_trg, x_target)
         # train_with_adjust.py:99 passes emb_org as both c_org and c_trg, so the reference runs
         # Adjust twice on identical inputs (AutoVC_Adjust.py:179, :189): identical outputs, and
         # each BatchNorm's running statistics moved twice.  One pass with two statistics

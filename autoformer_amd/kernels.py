@@ -70,6 +70,12 @@ def _dev(*ts):
             raise RuntimeError("autoformer_amd kernels need HIP device tensors (no CPU fallback)")
 
 
+def require_device(*ts):
+    """Model entry points: every tensor argument on the HIP device, or a RuntimeError here -- a host
+    pointer reaching a kernel faults the GPU instead of raising."""
+    _dev(*(t for t in ts if isinstance(t, torch.Tensor)))
+
+
 # ------------------------------------------------------------------------- GEMM
 def operand(t: torch.Tensor, ld: int, kstrided: bool = False, window=None, batch_stride: int = 0) -> L.Operand:
     """window = (taps, pad, t_out, t_in, chans) or None."""
@@ -967,6 +973,7 @@ def rownorm_bwd(dy, y, norms):
 
 def pad_cols(src, Cd, dtype=F32, C=None):
     """(R, Cd) copy of the first C columns of the row-major 2-D src, zero-padded (or cropped)."""
+    _dev(src)
     R, lds = src.shape
     C = lds if C is None else C
     tdt = torch.bfloat16 if dtype == BF16 else torch.float32
