@@ -285,3 +285,20 @@ def test_trainstep_graph_replay_equals_eager():
             assert torch.allclose(ba.double(), bb.double(), rtol=1e-4, atol=1e-6), n
     finally:
         set_grad_sink(False)
+
+
+def test_host_inputs_refused_before_any_kernel():
+    """A CPU input to a device model raises at the model's entry (K.require_device) instead of
+    reaching a kernel as a host pointer (which faults the GPU)."""
+    import factory.AutoVC as AV
+    import factory.Discriminator as D
+
+    m = AV.AutoVC(44, 256, 512, 16).to(DEV)
+    x, e = torch.zeros(2, 128, 80), torch.zeros(2, 256)
+    with pytest.raises(RuntimeError, match="HIP device tensors"):
+        m(x, e.to(DEV), e.to(DEV))
+    with pytest.raises(RuntimeError, match="HIP device tensors"):
+        m(x.to(DEV), e, e.to(DEV))
+    with pytest.raises(RuntimeError, match="HIP device tensors"):
+        D.Discriminator().to(DEV)(x)
+    torch.cuda.synchronize()
