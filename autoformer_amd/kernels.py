@@ -217,11 +217,15 @@ def tt_splitk_reduced(split_k):
     return 1 < split_k <= _TT_SPLITK_MAX
 
 
-def auto_split_k(M, N, K, target=384, min_k=256, tiles=None):
+_SPLIT_TARGET = int(os.environ.get("AVC_SPLIT_TARGET", "384") or 384)
+
+
+def auto_split_k(M, N, K, target=None, min_k=256, tiles=None):
     """Split-K factor for the weight-gradient GEMMs (K = frames): about `target` workgroups
     over the 128x128 output tiles (1.5 per CU: a K-loop alone is latency-bound, ~1.4 us per
     64-deep step), each split at least `min_k` long.  Chosen from a split-K sweep of every
     weight-gradient shape of the AutoVC step on MI355X (tools/gemm_census.py --sweep)."""
+    target = _SPLIT_TARGET if target is None else target
     if tiles is None:  # the 128 x 128 output tiles (the halo conv dW kernel passes its 128 x 160 count)
         tiles = math.ceil(M / 128) * math.ceil(N / 128)
     s = int(target / max(tiles, 1) + 0.5)
