@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AVC_LIB_PATH") or os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["gemm_ring.hip", "gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "graph.hip", "fold.hip", "disc.hip"]
-ABI_VERSION = 28
+ABI_VERSION = 29
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -65,6 +65,7 @@ PACK_COPY, PACK_TRANSPOSE, PACK_CONV_F, PACK_CONV_D, PACK_ADD = 0, 1, 2, 3, 4
 _SIGS = {
     "avc_abi_version": (c_int, []),
     "avc_last_error": (ctypes.c_char_p, []),
+    "avc_ring_reserve_test": (ctypes.c_uint, [ctypes.POINTER(ctypes.c_uint), ctypes.c_uint, ctypes.c_uint]),
     "avc_gemm": (c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "avc_expand_codes": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_gemm_bn": (c_int, [ctypes.POINTER(GemmDesc), ctypes.POINTER(BnFin), c_void_p]),
@@ -103,6 +104,8 @@ _SIGS = {
     "avc_lstm2_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                               c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "avc_lstm_persistent": (c_int, [c_int, c_int, c_int, c_int, c_int]),
+    "avc_lstm_small_mfma": (c_int, [c_int, c_int]),
+    "avc_lstm_set_small_mfma": (c_int, [c_int]),
     "avc_enc_concat": (c_int, [c_void_p, c_ll, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_codes_gather": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_codes_scatter": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),

@@ -520,9 +520,26 @@ unsigned* avc_counter_slots(int n, hipStream_t s) {
                   "eager step first)");
     return nullptr;
   }
-  unsigned b = next[dev].fetch_add((unsigned)n) % POOL;
-  if (b + (unsigned)n > POOL) b = 0;
-  return base + b;
+  return base + avc_ring_reserve(next[dev], (unsigned)n, POOL);
+}
+
+unsigned avc_ring_reserve(std::atomic<unsigned>& cursor, unsigned n, unsigned pool) {
+  unsigned cur = cursor.load(std::memory_order_relaxed);
+  for (;;) {
+    const unsigned b = cur & (pool - 1u);
+    const bool wrap = b + n > pool;
+    const unsigned start = wrap ? 0u : b;
+    const unsigned nxt = cur + (wrap ? pool - b : 0u) + n;  // modulo 2^32: pool divides it
+    if (cursor.compare_exchange_weak(cur, nxt, std::memory_order_relaxed)) return start;
+  }
+}
+
+// Host-only test hook of the ring reservation (tests/test_abi.py): no device, no HIP call.
+extern "C" unsigned avc_ring_reserve_test(unsigned* cursor, unsigned n, unsigned pool) {
+  std::atomic<unsigned> c(*cursor);
+  const unsigned r = avc_ring_reserve(c, n, pool);
+  *cursor = c.load();
+  return r;
 }
 
 float* avc_zero_slots(int n, hipStream_t s) {
@@ -549,9 +566,7 @@ float* avc_zero_slots(int n, hipStream_t s) {
   float* base = pool[dev].load(std::memory_order_acquire);
   if (!base) return nullptr;  // (the caller falls back to its direct form)
   const unsigned n64 = ((unsigned)n + 63u) & ~63u;  // 256-B aligned regions
-  unsigned b = next[dev].fetch_add(n64) % POOL;
-  if (b + n64 > POOL) b = 0;
-  return base + b;
+  return base + avc_ring_reserve(next[dev], n64, POOL);
 }
 
 namespace {

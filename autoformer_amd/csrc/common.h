@@ -1,6 +1,7 @@
 // Shared device/host helpers for libautovc_hip.so (gfx950 / CDNA4 only).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <stdint.h>
 #include <string>
 
@@ -139,6 +140,12 @@ static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b)
 // use inside a stream capture, allocation failure).  The last arrival of a launch resets its
 // slot to 0, so slots are reused without a reset pass.
 unsigned* avc_counter_slots(int n, hipStream_t s);
+// Reserve n consecutive slots of a ring of `pool` slots (pool a power of two <= 2^31) through
+// the shared cursor.  A request that would cross the end of the ring starts at 0 and the
+// cursor moves past the skipped tail AND the request, so the next request starts after it:
+// reserved ranges never overlap while fewer than `pool` slots are live (a plain
+// fetch_add(n) moved the crossing request to 0 but advanced the cursor by n only).
+unsigned avc_ring_reserve(std::atomic<unsigned>& cursor, unsigned n, unsigned pool);
 // the process fault word of the current device (avc_set_fault_word; lstm.hip), nullable
 unsigned* avc_fault_ptr();
 // n floats of a device pool that is all zero between uses: the user leaves its region zeroed

@@ -336,6 +336,225 @@ __global__ void __launch_bounds__(SNT) lstm_small_bwd(const float* __restrict__ 
   if (w == 4) flush(Tp / SC - 1);
 }
 
+// =============================================================== small H on MFMA (bf16 compute)
+// The encoder BiLSTM (H = 44, AutoVC.py:43,54-55) with its recurrent product on the 4x4x4 bf16
+// MFMA (v_mfma_f32_4x4x4_16b_bf16: 16 independent 4x4 blocks per instruction, K = 4 each).  One
+// workgroup = 4 utterances (the 4 columns of every block) x one direction; lane l of a wave is
+// block l >> 2, column l & 3 (tools/probes/mfma4x4_probe.hip verified the lane map on gfx950:
+// A row i / B column j / D column j of block b in lane 4b + i / 4b + j / 4b + j, D row i in
+// accumulator register i; 12.7 cycles per dependent MFMA, 8.5 independent).
+//
+// Forward: block b of compute wave w is hidden unit u = 16w + b and its 4 ROWS are that unit's
+// gates i, f, g, o (A = W_hh rows, bf16, in VGPRs for the whole sequence); the B operand is
+// h_{s-1} of the block's 4 utterances (bf16, LDS, the same 8 bytes for all 16 blocks).  After
+// H/4 MFMAs lane (b, j) holds the four pre-activation gates of cell (u, utterance j) in its four
+// accumulator registers: the cell update is lane-local (no DPP, no LDS between the product and
+// the cell), one cell per lane, 3 waves for H = 44, and each lane stores its own outputs.
+// Backward: dh_rec[u] = sum_r dG[r] W[r][u] over the 4H gate rows r.  Block b = (unit quad ug,
+// gate block kq) = (b & 3, b >> 2): its 4 rows are units 16w + 4ug + i, its K runs over gate block
+// kq's H rows, so the four blocks kq of a unit quad hold partial sums that two lane exchanges
+// (xor 32, xor 16) reduce, each lane keeping the sum of register kq: cell (16w + 4ug + kq, j).
+//
+// Measured against the packed-FMA kernels above (profiles/r6_bilstm_mfma_ab.txt, B=64, T=128):
+// forward 0.585 vs 0.457 us per step, backward 0.727 vs 0.504.  The product is no shorter than the
+// FMA dot (0.20 us: LDS read + 11 chained MFMAs), and a lane now activates four gates and tanh(c)
+// instead of one gate + tanh(c) (cell 0.22 vs 0.085 us): 64 cells per wave is 4x the
+// transcendental work per lane of the one-utterance-per-workgroup form.  Off by default
+// (avc_lstm_set_small_mfma / AVC_BILSTM_MFMA=1 select it).
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+constexpr int MU = 4;   // utterances per workgroup (block columns)
+constexpr int MSD = 8;  // input lead, steps (register ring)
+
+__device__ __forceinline__ f32x4 mfma4(s16x4 a, s16x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ s16x4 bf4(float a, float b, float c, float d) {
+  return __builtin_bit_cast(s16x4, bf16x4{(bf16)a, (bf16)b, (bf16)c, (bf16)d});
+}
+
+// Forward.  KC = H / 4 K-chunks, NW = ceil(H / 16) waves.
+template <int KC, int NW, bool TRACE>
+__global__ void __launch_bounds__(NW * 64) lstm_mfma_fwd(const float* __restrict__ xproj, const float* __restrict__ whh,
+                                                         int B, int T, int dirs, float* __restrict__ hout,
+                                                         bf16* __restrict__ hout16, float* __restrict__ cout,
+                                                         float* __restrict__ gout, unsigned long long* tr) {
+  constexpr int H = 4 * KC, G = 4 * H;
+  const int d = blockIdx.y, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int b0 = blockIdx.x * MU;
+  __shared__ __attribute__((aligned(16))) bf16 hs[2][MU][H];  // h_{s-1}, the B operand
+  const long long ldx = (long long)dirs * G, ldh = (long long)dirs * H;
+  const int t0 = d ? T - 1 : 0, dt = d ? -1 : 1;
+  const int nu = min(MU, B - b0);  // utterances of this workgroup
+
+  const int j = lane & 3, u = 16 * w + (lane >> 2);
+  const bool cell = u < H && j < nu;
+  const int bi = b0 + min(j, nu - 1), uc = min(u, H - 1);
+  s16x4 wa[KC];
+  {  // A: row (lane & 3) = gate of block (lane >> 2) = unit u
+    const float* W = whh + (long long)d * G * H + (long long)((lane & 3) * H + uc) * H;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+      wa[c] = u < H ? bf4(W[4 * c], W[4 * c + 1], W[4 * c + 2], W[4 * c + 3]) : s16x4{0, 0, 0, 0};
+  }
+  for (int i = tid; i < 2 * MU * H; i += blockDim.x) (&hs[0][0][0])[i] = (bf16)0.f;
+  const float* xl = xproj + (long long)bi * T * ldx + d * G + uc;
+  auto xload = [&](int sn) {
+    const float* p = xl + (long long)(t0 + dt * min(sn, T - 1)) * ldx;
+    return f32x4{p[0], p[H], p[2 * H], p[3 * H]};
+  };
+  f32x4 ring[MSD];
+#pragma unroll
+  for (int r = 0; r < MSD; ++r) ring[r] = xload(r);
+  float c = 0.f;
+  __syncthreads();
+
+  for (int s0 = 0; s0 < T; s0 += MSD) {
+#pragma unroll
+    for (int r = 0; r < MSD; ++r) {
+      const int s = s0 + r;
+      if (s >= T) break;
+      const f32x4 xv = ring[r];
+      ring[r] = xload(s + MSD);
+      if (TRACE && w == 0) sstamp(tr, T, s, 0, 0.f);
+      const bf16* hr = &hs[s & 1][j][0];
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+        const s16x4 hb = *reinterpret_cast<const s16x4*>(hr + 4 * k);
+        if (k & 1) a1 = mfma4(wa[k], hb, a1);
+        else a0 = mfma4(wa[k], hb, a0);
+      }
+      const f32x4 pre = a0 + a1 + xv;
+      if (TRACE && w == 0) sstamp(tr, T, s, 1, pre[0]);
+      const float ig = fsig(pre[0]), fg = fsig(pre[1]), gg = ftanh(pre[2]), og = fsig(pre[3]);
+      c = fg * c + ig * gg;
+      const float h = og * ftanh(c);
+      if (cell) {
+        hs[(s + 1) & 1][j][u] = (bf16)h;
+        const long long t = t0 + dt * s, oh = ((long long)bi * T + t) * ldh + d * H + u;
+        float* gp = gout + ((long long)bi * T + t) * ldx + d * G + u;
+        gp[0] = ig;
+        gp[H] = fg;
+        gp[2 * H] = gg;
+        gp[3 * H] = og;
+        hout[oh] = h;
+        cout[oh] = c;
+        if (hout16) hout16[oh] = (bf16)h;
+      }
+      if (TRACE && w == 0) sstamp(tr, T, s, 2, h);
+      __syncthreads();
+    }
+  }
+}
+
+// Backward.  Same workgroup shape; see the block comment above for the lane map.
+template <int KC, int NW, bool TRACE>
+__global__ void __launch_bounds__(NW * 64) lstm_mfma_bwd(const float* __restrict__ dhout, const float* __restrict__ call,
+                                                         const float* __restrict__ gall, const float* __restrict__ whh,
+                                                         int B, int T, int dirs, float* __restrict__ dg,
+                                                         bf16* __restrict__ dg16, unsigned long long* tr) {
+  constexpr int H = 4 * KC, G = 4 * H;
+  const int d = blockIdx.y, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int b0 = blockIdx.x * MU;
+  __shared__ __attribute__((aligned(16))) bf16 gs[2][MU][G];  // dG_{s-1}, the B operand
+  const long long ldg = (long long)dirs * G, ldh = (long long)dirs * H;
+  const int t0 = d ? 0 : T - 1, dt = d ? 1 : -1;  // opposite to the forward recurrence
+  const int fwd_prev = d ? 1 : -1;                // offset of the forward's previous time step
+  const int nu = min(MU, B - b0);
+
+  const int j = lane & 3, kq = lane >> 4, u = 16 * w + ((lane >> 2) & 3) * 4 + kq;
+  const bool cell = u < H && j < nu;
+  const int bi = b0 + min(j, nu - 1), uc = min(u, H - 1);
+  s16x4 wa[KC];
+  {  // A: block (lane >> 2) = (unit quad, gate block kq), row (lane & 3): unit 16w + (lane & 15)
+    const int ua = 16 * w + (lane & 15);
+    const float* W = whh + (long long)d * G * H + (long long)(kq * H) * H + min(ua, H - 1);
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+      wa[c] = ua < H ? bf4(W[(4 * c) * H], W[(4 * c + 1) * H], W[(4 * c + 2) * H], W[(4 * c + 3) * H])
+                     : s16x4{0, 0, 0, 0};
+  }
+  for (int i = tid; i < 2 * MU * G; i += blockDim.x) (&gs[0][0][0])[i] = (bf16)0.f;
+  struct In {
+    float dh, c, cp, i, f, g, o;
+  };
+  const float* dhb = dhout + (long long)bi * T * ldh + d * H + uc;
+  const float* cb = call + (long long)bi * T * ldh + d * H + uc;
+  const float* gb = gall + (long long)bi * T * ldg + d * G + uc;
+  auto fetch = [&](int sn) {  // unconditional loads; c_prev past the sequence start is zeroed at use
+    const int t = t0 + dt * min(sn, T - 1), tp = min(max(t + fwd_prev, 0), T - 1);
+    In v;
+    v.dh = dhb[(long long)t * ldh];
+    v.c = cb[(long long)t * ldh];
+    v.cp = cb[(long long)tp * ldh];
+    const float* g = gb + (long long)t * ldg;
+    v.i = g[0];
+    v.f = g[H];
+    v.g = g[2 * H];
+    v.o = g[3 * H];
+    return v;
+  };
+  In ring[MSD];
+#pragma unroll
+  for (int r = 0; r < MSD; ++r) ring[r] = fetch(r);
+  float dc = 0.f;
+  const bool hi = kq & 2, lo = kq & 1;
+  __syncthreads();
+
+  for (int s0 = 0; s0 < T; s0 += MSD) {
+#pragma unroll
+    for (int r = 0; r < MSD; ++r) {
+      const int s = s0 + r;
+      if (s >= T) break;
+      const In in = ring[r];
+      ring[r] = fetch(s + MSD);
+      if (TRACE && w == 0) sstamp(tr, T, s, 0, 0.f);
+      const bf16* gr = &gs[s & 1][j][kq * H];
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+        const s16x4 gb4 = *reinterpret_cast<const s16x4*>(gr + 4 * k);
+        if (k & 1) a1 = mfma4(wa[k], gb4, a1);
+        else a0 = mfma4(wa[k], gb4, a0);
+      }
+      const f32x4 v = a0 + a1;
+      // sum the four gate blocks kq (lanes xor 16, xor 32); this lane keeps register kq
+      const float k0 = hi ? v[2] : v[0], k1 = hi ? v[3] : v[1];
+      const float r0 = __shfl_xor(hi ? v[0] : v[2], 32, 64), r1 = __shfl_xor(hi ? v[1] : v[3], 32, 64);
+      const float e0 = k0 + r0, e1 = k1 + r1;
+      const float rec = (lo ? e1 : e0) + __shfl_xor(lo ? e0 : e1, 16, 64);
+      if (TRACE && w == 0) sstamp(tr, T, s, 1, rec);
+      const float dh = in.dh + rec;
+      const float cp = s == T - 1 ? 0.f : in.cp;  // the forward's c_{-1} = 0
+      const float tc = ftanh(in.c);
+      const float dcs = dc + dh * in.o * (1.f - tc * tc);
+      const float di = dcs * in.g * in.i * (1.f - in.i), df = dcs * cp * in.f * (1.f - in.f);
+      const float dgg = dcs * in.i * (1.f - in.g * in.g), dob = dh * tc * in.o * (1.f - in.o);
+      dc = dcs * in.f;
+      if (cell) {
+        bf16* gn = &gs[(s + 1) & 1][j][u];
+        gn[0] = (bf16)di;
+        gn[H] = (bf16)df;
+        gn[2 * H] = (bf16)dgg;
+        gn[3 * H] = (bf16)dob;
+        const long long o = ((long long)bi * T + t0 + dt * s) * ldg + d * G + u;
+        dg[o] = di;
+        dg[o + H] = df;
+        dg[o + 2 * H] = dgg;
+        dg[o + 3 * H] = dob;
+        if (dg16) {
+          dg16[o] = (bf16)di;
+          dg16[o + H] = (bf16)df;
+          dg16[o + 2 * H] = (bf16)dgg;
+          dg16[o + 3 * H] = (bf16)dob;
+        }
+      }
+      if (TRACE && w == 0) sstamp(tr, T, s, 2, dc);
+      __syncthreads();
+    }
+  }
+}
+
 // =============================================================== large H: per-step kernels
 struct StepArgs {
   const float* xproj;  // (B,T,dirs*4H)
@@ -1909,7 +2128,38 @@ void launch_small_bwd(dim3 g, hipStream_t s, bool fast, const float* dh, const f
   else lstm_small_bwd<HM, false, false><<<g, SNT, 0, s>>>(dh, c, gt, w, T, H, dirs, dg, dg16, nullptr);
 }
 
+// The MFMA form of the encoder BiLSTM (lstm_mfma_fwd / _bwd): bf16 compute, H in {16, 32, 44, 48, 64}.
+// Off by default (slower, see the kernels); avc_lstm_set_small_mfma(1) or AVC_BILSTM_MFMA=1 selects it.
+std::atomic<int> g_small_mfma{-1};
+bool small_mfma(int H, bool fast) {
+  int on = g_small_mfma.load(std::memory_order_relaxed);
+  if (on < 0) on = getenv("AVC_BILSTM_MFMA") ? atoi(getenv("AVC_BILSTM_MFMA")) != 0 : 0;
+  return on && fast && (H == 16 || H == 32 || H == 44 || H == 48 || H == 64);
+}
+template <int KC>
+void launch_mfma_fwd(hipStream_t s, const float* x, const float* w, int B, int T, int dirs, float* h, bf16* h16,
+                     float* c, float* gt) {
+  constexpr int NW = (4 * KC + 15) / 16;
+  const dim3 g(cdiv(B, MU), dirs);
+  if (g_trace) lstm_mfma_fwd<KC, NW, true><<<g, NW * 64, 0, s>>>(x, w, B, T, dirs, h, h16, c, gt, g_trace);
+  else lstm_mfma_fwd<KC, NW, false><<<g, NW * 64, 0, s>>>(x, w, B, T, dirs, h, h16, c, gt, nullptr);
+}
+template <int KC>
+void launch_mfma_bwd(hipStream_t s, const float* dh, const float* c, const float* gt, const float* w, int B, int T,
+                     int dirs, float* dg, bf16* dg16) {
+  constexpr int NW = (4 * KC + 15) / 16;
+  const dim3 g(cdiv(B, MU), dirs);
+  if (g_trace) lstm_mfma_bwd<KC, NW, true><<<g, NW * 64, 0, s>>>(dh, c, gt, w, B, T, dirs, dg, dg16, g_trace);
+  else lstm_mfma_bwd<KC, NW, false><<<g, NW * 64, 0, s>>>(dh, c, gt, w, B, T, dirs, dg, dg16, nullptr);
+}
+
 }  // namespace
+
+extern "C" int avc_lstm_small_mfma(int H, int compute) { return small_mfma(H, compute == AVC_BF16) ? 1 : 0; }
+extern "C" int avc_lstm_set_small_mfma(int mode) {
+  g_small_mfma.store(mode < 0 ? -1 : (mode ? 1 : 0), std::memory_order_relaxed);
+  return 0;
+}
 
 unsigned* avc_fault_ptr() { return fault_word(); }
 
@@ -2088,6 +2338,17 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
     AVC_CHECK_ARG(wdtype == AVC_F32, "avc_lstm_fwd: small-H path takes fp32 W_hh");
     const bool fast = compute == AVC_BF16;  // fp32 weights and state either way; fast activations in bf16 mode
     bf16* h16 = reinterpret_cast<bf16*>(h_bf16);
+    if (small_mfma(H, fast)) {
+      const float* w = (const float*)w_hh;
+      switch (H) {
+        case 16: launch_mfma_fwd<4>(s, xproj, w, B, T, dirs, h, h16, c, gates); break;
+        case 32: launch_mfma_fwd<8>(s, xproj, w, B, T, dirs, h, h16, c, gates); break;
+        case 44: launch_mfma_fwd<11>(s, xproj, w, B, T, dirs, h, h16, c, gates); break;
+        case 48: launch_mfma_fwd<12>(s, xproj, w, B, T, dirs, h, h16, c, gates); break;
+        default: launch_mfma_fwd<16>(s, xproj, w, B, T, dirs, h, h16, c, gates); break;
+      }
+      return avc_check_launch("avc_lstm_fwd(small, mfma)");
+    }
     dim3 g(B, dirs);
     if (H <= 16) launch_small_fwd<16>(g, s, fast, xproj, (const float*)w_hh, T, H, dirs, h, h16, c, gates);
     else if (H <= 32) launch_small_fwd<32>(g, s, fast, xproj, (const float*)w_hh, T, H, dirs, h, h16, c, gates);
@@ -2173,6 +2434,17 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
     AVC_CHECK_ARG(w_hh && wdtype == AVC_F32, "avc_lstm_bwd: small-H path takes fp32 W_hh");
     const bool fast = compute == AVC_BF16;
     bf16* dg16 = reinterpret_cast<bf16*>(dgates_bf16);
+    if (small_mfma(H, fast)) {
+      const float* w = (const float*)w_hh;
+      switch (H) {
+        case 16: launch_mfma_bwd<4>(s, dh_out, c, gates, w, B, T, dirs, dgates, dg16); break;
+        case 32: launch_mfma_bwd<8>(s, dh_out, c, gates, w, B, T, dirs, dgates, dg16); break;
+        case 44: launch_mfma_bwd<11>(s, dh_out, c, gates, w, B, T, dirs, dgates, dg16); break;
+        case 48: launch_mfma_bwd<12>(s, dh_out, c, gates, w, B, T, dirs, dgates, dg16); break;
+        default: launch_mfma_bwd<16>(s, dh_out, c, gates, w, B, T, dirs, dgates, dg16); break;
+      }
+      return avc_check_launch("avc_lstm_bwd(small, mfma)");
+    }
     dim3 g(B, dirs);
     if (H <= 16) launch_small_bwd<16>(g, s, fast, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates, dg16);
     else if (H <= 32) launch_small_bwd<32>(g, s, fast, dh_out, c, gates, (const float*)w_hh, T, H, dirs, dgates, dg16);

@@ -786,3 +786,114 @@ class GANSolver(Solver):
                     log += ", {}: {:.4f}".format(tag, loss[tag])
                 print(log)
         return history
+
+
+# ------------------------------------------------------------------------- command line (C1 driver)
+class Config:
+    """The reference's Config (train.py:134-150) plus the build's shape / precision flags."""
+
+    def __init__(self, model_name, data_dir, device, num_iters, isadain, batch_size=2, len_crop=176, freq=22,
+                 log_step=10):
+        self.model_name = model_name
+        self.data_dir = data_dir
+        self.num_iters = num_iters
+        self.isadain = isadain
+        self.device = device
+        self.batch_size = batch_size
+        self.len_crop = len_crop
+        self.lambda_cd = 1
+        self.lambda_ad = 1
+        self.dim_neck = 44
+        self.dim_emb = 256
+        self.dim_pre = 512
+        self.freq = freq
+        self.log_step = log_step
+
+
+class SyntheticUtterances:
+    """Endless synthetic batches of the metric's shape: batch i is
+    detinit.det_inputs(batch_size, len_crop, seed=seed + i) -- log10-mel-like values in [-5, 2]
+    and unit-norm 256-d speaker embeddings -- as CPU tensors, the form get_loader yields."""
+
+    def __init__(self, batch_size, len_crop, dim_emb=256, seed=1234):
+        self.batch_size, self.len_crop, self.dim_emb, self.seed = batch_size, len_crop, dim_emb, seed
+
+    def __iter__(self):
+        from .detinit import det_inputs
+
+        i = 0
+        while True:
+            x, e = det_inputs(self.batch_size, self.len_crop, self.dim_emb, seed=self.seed + i)
+            yield torch.from_numpy(x), torch.from_numpy(e)
+            i += 1
+
+
+def build_parser():
+    import argparse
+
+    p = argparse.ArgumentParser(
+        prog="python -m autoformer_amd.train",
+        description="AutoVC-family training on the MI355X: train.py (Solver), train_with_discriminator.py "
+                    "(--discriminator) and train_with_adjust.py (the *_Adjust models) over the HIP kernels.")
+    # the reference's flags (train.py:152-159)
+    p.add_argument("--model_name", default="AutoVC", help="traning model name (a factory plugin)")
+    p.add_argument("--data_dir", help="traning data folder (train.pkl + mel .npy files)")
+    p.add_argument("--save_model_name")
+    p.add_argument("--use_adain", default=False)
+    p.add_argument("--device", default="cuda:0")
+    p.add_argument("--num_iters", default=1000000, help="iter time")
+    # the build's flags (SURVEY §5 config row, BASELINE C1)
+    p.add_argument("--batch_size", type=int, default=2)
+    p.add_argument("--len_crop", type=int, default=176)
+    p.add_argument("--freq", type=int, default=22)
+    p.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
+                   help="compute precision of the HIP kernels (fp32: the reference's arithmetic)")
+    p.add_argument("--synthetic", action="store_true", help="synthetic batches instead of --data_dir")
+    p.add_argument("--seed", type=int, default=1234, help="first synthetic batch seed")
+    p.add_argument("--det_init", action="store_true",
+                   help="closed-form weights (autoformer_amd.detinit, the goldens' initialiser)")
+    p.add_argument("--discriminator", action="store_true", help="train_with_discriminator.py's two-model step")
+    p.add_argument("--log_step", type=int, default=10)
+    return p
+
+
+def main(argv=None):
+    """Parse, build the reference's Solver for the flags and train; returns the per-iteration losses."""
+    args = build_parser().parse_args(argv)
+    import autoformer_amd as A
+
+    if not args.synthetic and not args.data_dir:
+        raise SystemExit("one of --data_dir or --synthetic is required")
+    if not str(args.device).startswith("cuda"):
+        raise SystemExit(f"--device {args.device}: the HIP kernels need a GPU (the CPU counterpart is the "
+                         "oracle, oracle/autovc_cpu.py OracleSolver, test infrastructure only)")
+    A.set_compute(args.dtype)
+    config = Config(args.model_name, args.data_dir, args.device, int(args.num_iters), bool(args.use_adain),
+                    args.batch_size, args.len_crop, args.freq, args.log_step)
+    if args.synthetic:
+        loader = SyntheticUtterances(args.batch_size, args.len_crop, config.dim_emb, args.seed)
+    else:
+        from .data import get_loader
+
+        loader = get_loader(args.data_dir, dim_neck=config.dim_neck, batch_size=args.batch_size,
+                            len_crop=args.len_crop)
+    if args.model_name.endswith("_Adjust"):
+        cls = AdjustSolver
+    elif args.discriminator:
+        cls = GANSolver
+    else:
+        cls = Solver
+    solver = cls(loader, config)
+    if args.det_init:
+        from .detinit import det_init_
+
+        for m in [solver.VC] + ([solver.D] if args.discriminator else []):
+            det_init_(m)
+    history = solver.train()
+    if args.save_model_name:
+        torch.save(solver.VC.state_dict(), f"{args.save_model_name}.pt")
+    return history
+
+
+if __name__ == "__main__":
+    main()

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 28
+#define AVC_ABI_VERSION 29
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -104,6 +104,11 @@ typedef struct {
 
 int avc_abi_version(void);
 const char* avc_last_error(void);
+/* Host-only test hook (no device, no HIP call): one reservation of n slots from a ring of
+ * `pool` slots (power of two) through *cursor, the allocator behind the library's arrival-counter
+ * and zero-slot pools.  Returns the first slot; reserved ranges never overlap across the wrap
+ * (ABI 29). */
+unsigned avc_ring_reserve_test(unsigned* cursor, unsigned n, unsigned pool);
 
 /* Conv1d / Linear / LSTM-projection / weight-gradient GEMMs.
  * Replaces: nn.Conv1d (factory/Norm.py:21-28 via AutoVC.py:26-41, 79-94, 125-171,
@@ -325,6 +330,13 @@ int avc_gemm_ring_last(void);
  * {512, 768, 1024}, and the occupancy API admits the whole grid (ceil(B/8) * H/32
  * workgroups of 512 threads) resident at once.  0 otherwise (per-step kernels). */
 int avc_lstm_persistent(int B, int H, int dirs, int compute, int backward);
+/* 1 when avc_lstm_fwd / avc_lstm_bwd run this small-H shape (H <= 64) on the MFMA BiLSTM kernels
+ * (lstm_mfma_fwd / _bwd: bf16 compute, H in {16, 32, 44, 48, 64}; ABI 29), 0 when on the packed-FMA
+ * kernels.  avc_lstm_set_small_mfma: 1 selects the MFMA form, 0 the packed-FMA form (the default:
+ * measured faster, profiles/r6_bilstm_mfma_ab.txt), -1 back to the AVC_BILSTM_MFMA environment default.
+ * Replaces: the recurrent product of nn.LSTM(512, 44, 2, bidirectional) (AutoVC.py:43,54-55). */
+int avc_lstm_small_mfma(int H, int compute);
+int avc_lstm_set_small_mfma(int mode);
 
 /* Elementwise / layout kernels of the model glue (AutoVC.py:46-48, 56-66, 197-207). */
 int avc_enc_concat(const float* mel, long long mel_ld, const float* emb, float* out, int B, int T,

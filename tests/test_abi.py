@@ -44,7 +44,7 @@ def test_python_binding_covers_header(lib):
 
 
 def test_abi_version_and_error_channel(lib):
-    assert lib.avc_abi_version() == 28
+    assert lib.avc_abi_version() == 29
     assert isinstance(lib.avc_last_error(), bytes)
 
 
@@ -122,3 +122,27 @@ def test_metaformer_state_dict_layout_matches_reference(mod, cls):
     ref = json.load(open(os.path.join(ROOT, "tests", "golden", "state_dict_layout.json")))
     m = getattr(importlib.import_module(mod), cls)(44, 256, 512, 22)
     assert [[k, list(v.shape)] for k, v in m.state_dict().items()] == ref[cls]
+
+
+def test_counter_ring_reservations_never_overlap(lib):
+    """the slot ring behind the split-K / BN arrival counters must hand out
+    disjoint ranges across its wrap (a crossing request restarts at 0 and the cursor moves past it)."""
+    import random
+
+    pool = 1 << 10
+    cur = ctypes.c_uint(0)
+    rng = random.Random(7)
+    live = []  # the last reservations, fewer than `pool` slots in total
+    for i in range(5000):
+        n = rng.choice([1, 3, 16, 64, 200, 256, 511])
+        b = lib.avc_ring_reserve_test(ctypes.byref(cur), n, pool)
+        assert 0 <= b and b + n <= pool, (i, b, n)
+        live.append((b, n))
+        while sum(m for _, m in live) > pool // 2:
+            live.pop(0)
+        for b2, n2 in live[:-1]:
+            assert b + n <= b2 or b2 + n2 <= b, (i, (b, n), (b2, n2))
+    # the cursor also wraps modulo 2^32 cleanly (pool divides 2^32)
+    cur = ctypes.c_uint(0xFFFFFFFF - 5)
+    b = lib.avc_ring_reserve_test(ctypes.byref(cur), 16, pool)
+    assert b == 0 and lib.avc_ring_reserve_test(ctypes.byref(cur), 4, pool) == 16
