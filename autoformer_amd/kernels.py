@@ -422,7 +422,49 @@ def lstm_set_spin(spins: int) -> None:
     L.call("avc_lstm_set_spin", int(spins) & 0xFFFFFFFF)
 
 
+# ---------------------------------------------------------------- collective / recurrence ordering
+# A persistent recurrence (lstm_persist_* / lstm2_persist_*: every workgroup of the grid spins on flags
+# the others publish) needs its whole grid resident.  RCCL's kernels are polling waves that
+# hold CU slots until the peer ranks arrive, so a recurrence launched while a collective is resident
+# can wait on workgroups that cannot be scheduled (round 5 measured the same hazard with device-side
+# waits: `persistent LSTM recurrence spin timeout`, profiles/r5_graph_modes.txt).  The training step
+# keeps them apart by stream order: a collective is enqueued on the comm stream only after
+# the decoder recurrences' backward, and the main stream joins the comm stream before the next
+# recurrence.  TrainStep reports both points here, and every launch site of a decoder (H > 64)
+# recurrence asserts the invariant on the host -- in eager steps and while a step is recorded, so a
+# recorded replay inherits it.
+_OUTSTANDING = []  # collectives enqueued on another stream and not yet joined by the main stream
+_ORDER_STATS = {"checks": 0, "enqueued": 0}  # tests: the invariant was exercised
+
+
+def collective_enqueued(what: str) -> None:
+    _OUTSTANDING.append(what)
+    _ORDER_STATS["enqueued"] += 1
+
+
+def ordering_stats():
+    return dict(_ORDER_STATS)
+
+
+def collective_joined() -> None:
+    _OUTSTANDING.clear()
+
+
+def collectives_outstanding():
+    return list(_OUTSTANDING)
+
+
+def _assert_no_collective(what: str) -> None:
+    _ORDER_STATS["checks"] += 1
+    if _OUTSTANDING:
+        raise RuntimeError(f"{what}: a persistent recurrence was enqueued while the collective(s) {_OUTSTANDING} "
+                           "are outstanding on the comm stream; its grid could wait on CU slots held by RCCL's "
+                           "polling kernels (DESIGN §6: join the comm stream first)")
+
+
 def lstm_fwd(xproj, w_hh, B, T, H, dirs, hbuf=None):
+    if H > 64:
+        _assert_no_collective("avc_lstm_fwd")
     dev = xproj.device
     h = torch.empty(B * T, dirs * H, device=dev)
     c = torch.empty(B * T, dirs * H, device=dev)
@@ -447,6 +489,7 @@ def lstm2_persistent(B, H, in1):
 def lstm2_fwd(xproj0, w_hh0, w_ih1, w_hh1, bias1, B, T, H):
     """Forward of two stacked unidirectional layers in one persistent launch (layer wavefront).
     Returns (h0, c0, gates0, h1, c1, gates1); h0/h1 carry their bf16 twins."""
+    _assert_no_collective("avc_lstm2_fwd")
     dev = xproj0.device
     fault_word(dev)
     outs = []
@@ -474,6 +517,7 @@ def lstm2_bwd(dh1, c0, g0, c1, g1, wt0, wti1, wt1, B, T, H, fp32=True, db=False)
     bf16 twin, or (fp32=False) the bf16 tensors alone.  wt0 / wti1 / wt1: W_hh0^T, W_ih1^T, W_hh1^T
     as bf16 [H][4H].  db: also return the (2, ceil(B/16), 4H) per-group sums of dG over utterances
     and steps (avc_lstm2_bwd db_part), whose column sums are the layers' bias gradients."""
+    _assert_no_collective("avc_lstm2_bwd")
     dev = dh1.device
     fault_word(dev)
     outs = [torch.empty(B * T, 4 * H, device=dev) for _ in range(2)] if fp32 else [None, None]
@@ -533,6 +577,8 @@ LAUNCH_TIMING_H = 1024
 
 def lstm_bwd(dh, h, c, g, w_hh, w_hh_t, B, T, H, dirs, gbuf=None):
     """dL/d(pre-activation gates); in the persistent bf16 mode also its bf16 twin."""
+    if H > 64:
+        _assert_no_collective("avc_lstm_bwd")
     dev = dh.device
     dg = torch.empty(B * T, dirs * 4 * H, device=dev)
     dcbuf = dg16 = None

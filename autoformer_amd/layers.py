@@ -171,6 +171,22 @@ class _Side:
         return False
 
 
+def main_wgrad_into(param, compute):
+    """The last layer's weight gradient, computed on the main stream (beside the side stream's
+    backlog) into a fresh tensor by compute(), then added into param.grad ON THE SIDE STREAM.  The
+    side stream may still be accumulating an earlier contribution into the same .grad -- the
+    encoder's first conv runs in the full pass and in the re-pass, and the re-pass's weight gradient
+    is a side-stream kernel -- and two read-modify-writes of one .grad on two streams lose updates
+    (round 6: the recorded C2 step's conv0 gradient 1.1e-3 off the eager one,
+    tests/test_gpu_replay.py).  The side stream is in order, so the add follows its own
+    accumulation; the step's join waits for it."""
+    tmp = compute()
+    with _Side() as sd:
+        sd.keep(tmp)
+        g = _grad_of(param)
+        K.add(g, tmp, out=g)
+
+
 # AVC_DEFER_LSTM2_WG (measured, off by default): the decoder lstm2 pair's four weight-gradient GEMMs
 # (4096 x 1024 x 8192 class) queued on the side stream only when the decoder lstm1 backward starts
 # ("1": beside that recurrence) or after it ("2": beside the encoder backward), instead of beside the
@@ -639,7 +655,7 @@ class ConvBNCore:
             # no data gradient: this is the last layer of the backward (the encoder's first
             # conv), after which the main stream would only wait for the side stream -- its
             # weight gradient runs here, beside the side stream's remaining backlog
-            wgrad()
+            main_wgrad_into(conv.weight, lambda: conv_wgrad(dy, x, B, T_in, T_out, conv.weight, self.pad))
             dW = dgamma = dbeta = dbias = None
         else:
             dW = wgrad()
@@ -824,30 +840,32 @@ class _EncConv0FoldFn(torch.autograd.Function):
             demb = torch.empty(B, de, device=dy.device)
             K.gemm(B, de, Kw * Co, operand(Sdy, Kw * Co), operand(We, de, kstrided=True), demb)
 
-        def wgrad():
-            gw = _grad_of(conv.weight) if sink else torch.zeros_like(conv.weight)
+        def wgrad(gw, acc):
+            """dW into gw: accumulated (acc) or written -- the mel half [0, nm) and the embedding
+            half [nm, nm + de) of the input channels cover all of them."""
             dWm = torch.empty(Co, Kw * cp, device=dy.device)
             K.gemm(Co, Kw * cp, M, operand(dy, Co, kstrided=True),
                    operand(xm, cp, kstrided=True, window=(Kw, pad, T, T, cp)), dWm,
                    split_k=K.auto_split_k(Co, Kw * cp, M))
-            K.conv_grad_unpack_slice(dWm, Kw * cp, cp, gw, 0, nm)
+            K.conv_grad_unpack_slice(dWm, Kw * cp, cp, gw, 0, nm, accumulate=acc)
             # embedding half, one K = B product per tap: dWe[co][k][ci] = sum_b Sdy[b][k][co] emb[b][ci]
             dWe = torch.empty(Co, Kw * de, device=dy.device)
             K.gemm(Co, de, B, operand(Sdy, Kw * Co, kstrided=True, batch_stride=Co),
                    operand(emb, de, kstrided=True), dWe, ldc=Kw * de, batch=Kw, c_batch_stride=de)
-            K.conv_grad_unpack_slice(dWe, Kw * de, de, gw, nm, de)
+            K.conv_grad_unpack_slice(dWe, Kw * de, de, gw, nm, de, accumulate=acc)
             return gw
         if sink and (dmel is not None or demb is not None or not _LAST_WGRAD_MAIN):
             with _Side(ev) as sd:
                 sd.keep(dy, xm, Sdy, emb)
                 if not _ABLATE_WGRAD:
-                    wgrad()
+                    wgrad(_grad_of(conv.weight), True)
             dW = dgamma = dbeta = dbias = None
         elif sink:
-            wgrad()  # the last layer of the backward: on the main stream (see ConvBNCore.backward)
+            # the last layer of the backward: on the main stream (see ConvBNCore.backward)
+            main_wgrad_into(conv.weight, lambda: wgrad(torch.empty_like(conv.weight), False))
             dW = dgamma = dbeta = dbias = None
         else:
-            dW = wgrad()
+            dW = wgrad(torch.empty_like(conv.weight), False)
         return dmel, demb, None, None, None, None, dW, dbias, dgamma, dbeta
 
 

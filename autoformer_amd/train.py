@@ -321,6 +321,7 @@ class TrainStep:
                 # RCCL: the comm stream waits for the collective; the Adam slice follows it
                 g = self.gflat[self.split:]
                 collective(lambda: D.finish_allreduce_(D.allreduce_mean_async_(g)))
+                K.collective_enqueued("decoder-slice all-reduce")
             self.opt.step_slice(self.split, self.flat.numel(), advance=True, max_blocks=_SIDE_ADAM_BLOCKS)
             if self._recording:
                 # recorded step: the decoder's weight packs rewritten in place right after its Adam
@@ -360,7 +361,9 @@ class TrainStep:
                 self.comm.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(self.comm):
                     D.finish_allreduce_(D.allreduce_mean_async_(self.gflat[:self.split]))
+                K.collective_enqueued("encoder-slice all-reduce")
             stream_wait(K.stream(), ev_record(self.comm.cuda_stream))  # the early slice's Adam (and its step count)
+            K.collective_joined()
             if timed:
                 ev[1].record()
             self.opt.step_slice(0, self.split, advance=False)
@@ -458,7 +461,9 @@ class TrainStep:
                     g = self.gflat[:self.split]
                     with on_stream(self.comm):
                         collective(lambda: D.finish_allreduce_(D.allreduce_mean_async_(g)))
+                    K.collective_enqueued("encoder-slice all-reduce")
                 stream_wait(K.stream(), ev_record(comm))
+                K.collective_joined()
                 if self.world > 1:
                     self._comm_timing_mark(box)
             self.opt.step_slice(0, self.split, advance=False)

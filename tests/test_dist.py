@@ -86,3 +86,24 @@ def test_single_process_is_a_noop(monkeypatch):
     D.allreduce_mean_(g)
     D.broadcast_(g)
     assert torch.equal(g, torch.ones(10))
+
+
+def test_recurrence_launch_refused_while_collective_outstanding():
+    """DESIGN §6 invariant: no persistent (decoder, H > 64) recurrence is enqueued while an RCCL
+    collective is outstanding on the comm stream (its polling kernels can hold the CU slots the
+    recurrence's whole grid needs).  The host check fires before any device work."""
+    from autoformer_amd import kernels as K
+
+    K.collective_joined()
+    K.collective_enqueued("decoder-slice all-reduce")
+    try:
+        for fn, args in ((K.lstm2_fwd, (None,) * 5 + (64, 128, 1024)),
+                         (K.lstm2_bwd, (None,) * 8 + (64, 128, 1024)),
+                         (K.lstm_fwd, (None, None, 64, 128, 512, 1)),
+                         (K.lstm_bwd, (None,) * 6 + (64, 128, 512, 1))):
+            with pytest.raises(RuntimeError, match="outstanding"):
+                fn(*args)
+        assert K.collectives_outstanding() == ["decoder-slice all-reduce"]
+    finally:
+        K.collective_joined()
+    assert not K.collectives_outstanding()
