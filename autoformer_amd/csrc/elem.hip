@@ -371,20 +371,62 @@ __global__ void adam_prep_kernel(float* state, float lr, float beta1, float beta
   state[2] = (float)sqrt(bc2);
 }
 
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float beta1, float beta2, float eps,
+                                          float step_size, float bc2s) {
+  m = m + (1.f - beta1) * (g - m);
+  v = v * beta2 + (1.f - beta2) * g * g;
+  const float denom = sqrtf(v) / bc2s + eps;
+  p = p - step_size * (m / denom);
+}
+
+__device__ __forceinline__ void adam_vec(float4& p, const float4& g, float4& m, float4& v, float beta1, float beta2,
+                                         float eps, float step_size, float bc2s) {
+  adam_elem(p.x, g.x, m.x, v.x, beta1, beta2, eps, step_size, bc2s);
+  adam_elem(p.y, g.y, m.y, v.y, beta1, beta2, eps, step_size, bc2s);
+  adam_elem(p.z, g.z, m.z, v.z, beta1, beta2, eps, step_size, bc2s);
+  adam_elem(p.w, g.w, m.w, v.w, beta1, beta2, eps, step_size, bc2s);
+}
+
+// 16-B vectors, two per array in flight per thread and iteration (a capped grid beside other kernels
+// still keeps enough bytes in flight); the scalar tail / unaligned form does the same per-element math
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, long long n, float beta1, float beta2, float eps,
-                            const float* __restrict__ state) {
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+                            const float* __restrict__ state, int vec) {
   const float step_size = state[1], bc2s = state[2];
-  for (; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const float gi = g[i];
-    float mi = m[i];
-    mi = mi + (1.f - beta1) * (gi - mi);
-    float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long done = 0;
+  if (vec) {
+    float4* p4 = reinterpret_cast<float4*>(p);
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    float4* m4 = reinterpret_cast<float4*>(m);
+    float4* v4 = reinterpret_cast<float4*>(v);
+    const long long n4 = n >> 2;
+    long long i = tid;
+    for (; i + stride < n4; i += 2 * stride) {
+      float4 ga = g4[i], gb = g4[i + stride];
+      float4 ma = m4[i], mb = m4[i + stride];
+      float4 va = v4[i], vb = v4[i + stride];
+      float4 pa = p4[i], pb = p4[i + stride];
+      adam_vec(pa, ga, ma, va, beta1, beta2, eps, step_size, bc2s);
+      adam_vec(pb, gb, mb, vb, beta1, beta2, eps, step_size, bc2s);
+      m4[i] = ma; m4[i + stride] = mb;
+      v4[i] = va; v4[i + stride] = vb;
+      p4[i] = pa; p4[i + stride] = pb;
+    }
+    if (i < n4) {
+      float4 ga = g4[i], ma = m4[i], va = v4[i], pa = p4[i];
+      adam_vec(pa, ga, ma, va, beta1, beta2, eps, step_size, bc2s);
+      m4[i] = ma; v4[i] = va; p4[i] = pa;
+    }
+    done = n4 << 2;
+  }
+  for (long long i = done + tid; i < n; i += stride) {
+    float pi = p[i], mi = m[i], vi = v[i];
+    adam_elem(pi, g[i], mi, vi, beta1, beta2, eps, step_size, bc2s);
     m[i] = mi;
     v[i] = vi;
-    const float denom = sqrtf(vi) / bc2s + eps;
-    p[i] = p[i] - step_size * (mi / denom);
+    p[i] = pi;
   }
 }
 
@@ -588,8 +630,10 @@ extern "C" int avc_adam_blocks(float* p, const float* g, float* m, float* v, lon
   hipStream_t s = as_stream(stream);
   if (advance) adam_prep_kernel<<<1, 1, 0, s>>>(state, lr, beta1, beta2);
   if (n == 0) return avc_check_launch("avc_adam");
-  int grid = (int)std::min<long long>(max_blocks > 0 ? max_blocks : 4096, cdiv(n, 256));
-  adam_kernel<<<grid, 256, 0, s>>>(p, g, m, v, n, beta1, beta2, eps, state);
+  const int vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
+                    reinterpret_cast<uintptr_t>(v)) & 15) == 0;
+  int grid = (int)std::min<long long>(max_blocks > 0 ? max_blocks : 2048, cdiv(n, vec ? 2048 : 256));
+  adam_kernel<<<grid, 256, 0, s>>>(p, g, m, v, n, beta1, beta2, eps, state, vec);
   return avc_check_launch("avc_adam");
 }
 
