@@ -17,8 +17,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # AVC_LIB_PATH: another build of the same ABI (same-box A/B timing of two builds, tools/ only)
 LIB_PATH = os.environ.get("AVC_LIB_PATH") or os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["gemm_ring.hip", "gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "graph.hip", "fold.hip", "disc.hip"]
-ABI_VERSION = 29
+SOURCES = ["gemm_ring.hip", "gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "fold.hip", "disc.hip", "events.hip"]
+ABI_VERSION = 30
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -116,10 +116,6 @@ _SIGS = {
     "avc_event_create": (c_int, [c_void_p]),
     "avc_event_record": (c_int, [c_void_p, c_void_p]),
     "avc_stream_wait_event": (c_int, [c_void_p, c_void_p]),
-    "avc_capture_deps": (c_int, [c_void_p, c_void_p, c_int]),
-    "avc_graph_split": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
-    "avc_graph_launch2": (c_int, [c_void_p, c_void_p, c_void_p]),
-    "avc_graph_split_destroy": (c_int, [c_void_p]),
     "avc_conv_pack_slice": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_void_p]),
     "avc_conv_edge_table": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),

@@ -703,15 +703,6 @@ bool fits32(const OpDev& o, int rows, int K, bool ks) {
 
 }  // namespace
 
-// AVC_GEMM_BNFIN=0: finalize launches after the GEMM instead of its last row tiles (A/B check)
-static bool gemm_bnfin() {
-  static const bool on = [] {
-    const char* e = getenv("AVC_GEMM_BNFIN");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 static int bn_finalize_after(const GemmArgs& g, const avc_bn_fin* f, void* stream) {
   for (int k = 0; k < f->nupd; ++k)
     if (avc_bn_finalize(g.bn_partial, g.M, g.N, f->gamma, f->beta, f->running_mean, f->running_var,
@@ -923,18 +914,9 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
   g.bnb_ydt = AVC_F32;
   g.bnb_act = 0;
   g.bnb_fin = avcbn::BwdFin{};
-  g.bn_apply16 = f ? reinterpret_cast<bf16*>(f->apply_bf16) : nullptr;
-  g.bn_act = f ? f->apply_act : 0;
-  g.bnb_dy16 = bb ? reinterpret_cast<bf16*>(bb->dy_bf16) : nullptr;
-  g.fault = (g.bn_apply16 || g.bnb_dy16) ? avc_fault_ptr() : nullptr;
-  static const int nap = [] {
-    const char* e = getenv("AVC_BN_NAP");
-    return e ? std::max(1, atoi(e)) : 4;
-  }();
-  g.nap = nap;
-  AVC_CHECK_ARG(!g.bn_apply16 || (d->ldc == d->N && g.batch == 1 && !d->residual),
+  AVC_CHECK_ARG(!(f && f->apply_bf16) || (d->ldc == d->N && g.batch == 1 && !d->residual),
                 "avc_gemm_bn: apply_bf16 needs ldc == N, batch 1, no residual");
-  AVC_CHECK_ARG(!g.bnb_dy16 || d->ldc == d->N, "avc_gemm_bnb: dy_bf16 needs ldc == N");
+  AVC_CHECK_ARG(!(bb && bb->dy_bf16) || d->ldc == d->N, "avc_gemm_bnb: dy_bf16 needs ldc == N");
   if (f) {
     AVC_CHECK_ARG(g.bn_partial && f->mean && f->rstd && f->scale && f->shift && f->nupd >= 1 &&
                       (!f->running_mean == !f->running_var),
@@ -972,7 +954,7 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
     int klf = (d->K + g.split_k - 1) / g.split_k;
     g.klen = ((klf + FBK - 1) / FBK) * FBK;
     if (g.klen <= 0) g.klen = FBK;
-    if (f && gemm_bnfin()) {  // the BN finalize rides on the fast kernels' epilogue (one counter per 64 columns)
+    if (f) {  // the BN finalize rides on the fast kernels' epilogue (one counter per 64 columns)
       g.bn_cnt = avc_counter_slots(cdiv(g.N, 32), s);  // one per column tile (tiles >= 32 columns)
       if (!g.bn_cnt) return -1;
     }
@@ -989,11 +971,7 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
     }
     const char* what = "avc_gemm(fast)";
     GeluPost post;
-    static const bool slots_on = [] {
-      const char* e = getenv("AVC_COLSUM_SLOTS");
-      return !(e && e[0] == '0');
-    }();
-    if (g.csum && slots_on && (long long)g.M * g.batch >= 4096) {
+    if (g.csum && (long long)g.M * g.batch >= 4096) {
       const int nc = g.csum_n > 0 ? g.csum_n : g.N;
       g.csum_slots = 32;
       g.csum_ws = avc_zero_slots(g.csum_slots * nc, s);  // null: the direct atomics
@@ -1020,10 +998,9 @@ static int gemm_impl(const avc_gemm_desc* d, const avc_bn_fin* f, void* stream, 
       if (avc_check_launch("avc_gemm(col_sum slots)")) return -1;
     }
     if (gelu_after(g, post, s)) return -1;
-    const bool applied = ring && gemm_ring_applied();  // the BN apply ran in the halo conv's epilogue
     if (bb && !bnb_fused && bnb_after(d, bb, s)) return -1;
     if (f && !g.bn_cnt && bn_finalize_after(g, f, stream)) return -1;
-    return applied ? 0 : bn_apply_after(d, f, bb, s);
+    return bn_apply_after(d, f, bb, s);
   }
   gemm_zero_c(g, s);
   const GeluPost post = strip_gelu(g);

@@ -222,23 +222,10 @@ bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 }  // namespace
 
 bool gemm_conv_launch(const GemmArgs& g, hipStream_t s) {
-  // AVC_CONV_CFG = "stages,channels,columns" (benchmarking); "0" = off (window stream, gemm_nt)
-  static int cfg[3] = {-1, 0, 0};
-  if (cfg[0] < 0) {
-    cfg[0] = 2;  // measured (tools/gemm_census.py, AVC_CONV_CFG sweep): two 32-KiB stages, 32 channels,
-    cfg[1] = 32; // 64 columns -- two workgroups per CU -- beat 64-channel stages (44-47 us) and
-    cfg[2] = 64; // three or four stages at one workgroup per CU (50-69 us) on 8192x512x2560
-    if (const char* e = getenv("AVC_CONV_CFG")) {
-      int a0 = 0, a1 = 0, a2 = 0;
-      const int n = sscanf(e, "%d,%d,%d", &a0, &a1, &a2);
-      cfg[0] = a0;
-      if (n == 3) {
-        cfg[1] = a1;
-        cfg[2] = a2;
-      }
-    }
-  }
-  if (cfg[0] == 0) return false;
+  // stages, channels, columns -- measured (tools/gemm_census.py, a stage / channel / column sweep in
+  // round 2): two 32-KiB stages, 32 channels, 64 columns -- two workgroups per CU -- beat 64-channel
+  // stages (44-47 us) and three or four stages at one workgroup per CU (50-69 us) on 8192x512x2560
+  static const int cfg[3] = {2, 32, 64};
   const OpDev& a = g.a;
   const OpDev& b = g.b;
   if (!a.win || a.taps != 5 || a.t_in != a.t_out || 2 * a.pad != a.taps - 1) return false;

@@ -70,15 +70,6 @@ struct GemmArgs {
   float* bnb_ws;
   unsigned* bnb_cnt;
   avcbn::BwdFin bnb_fin;
-  // fused BatchNorm APPLY outputs (halo conv ring only; gemm_ring_launch clears them for the other
-  // kernels and the caller runs the apply pass instead): act(y*scale + shift) of the forward
-  // (bn_apply16, with bn_cnt) / the producing layer's dy of the backward (bnb_dy16, with bnb_ws),
-  // both bf16, written after a column-tile barrier behind the last row tile's finalize
-  bf16* bn_apply16;
-  int bn_act;
-  bf16* bnb_dy16;
-  unsigned* fault;  // process fault word (bit 1: a barrier wait timed out); nullable
-  int nap;          // s_sleep(1)s between the barrier's polls (AVC_BN_NAP)
   // split-K without atomics (TT kernels, sk_ws != null): per-stream workspace of split_k partial
   // tiles per output tile and one self-resetting arrival counter per output tile (splitk_last)
   float* sk_ws;
@@ -455,6 +446,5 @@ float* gemm_splitk_ws(size_t bytes, hipStream_t s);
 // Entry of the 8-wave deep-ring NT kernel (gemm_ring.hip); false when the shape / operands do
 // not qualify or AVC_RING=0.
 bool gemm_ring_launch(const GemmArgs& g, hipStream_t s);
-bool gemm_ring_applied();  // the last gemm_ring_launch on this thread wrote the BN apply outputs
 
 }  // namespace avcg

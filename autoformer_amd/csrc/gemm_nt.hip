@@ -209,31 +209,15 @@ bool operand_ok(const OpDev& o, bool allow_win) {
   return true;
 }
 
-int env_cfg(int which) {
-  static int cfg[3] = {-2, 0, 0};
-  if (cfg[0] == -2) {
-    cfg[0] = -1;
-    const char* e = getenv("AVC_NT_CFG");  // "BN,NST" (benchmarking); "0" disables the kernel
-    if (e) {
-      int bn = 0, ns = 0;
-      if (sscanf(e, "%d,%d", &bn, &ns) >= 1) {
-        cfg[0] = bn;
-        cfg[1] = ns;
-      }
-    }
-  }
-  return cfg[which];
-}
 
 }  // namespace
 
 bool gemm_nt_launch(const GemmArgs& g, hipStream_t s) {
   if (g.K % 8 || g.klen % FBK) return false;
   if (!operand_ok(g.a, true) || !operand_ok(g.b, false)) return false;
-  int bn = env_cfg(0), nst = env_cfg(1);
-  if (bn == 0) return false;
+  int bn = -1, nst = 2;
   const long long t128 = (long long)((g.M + BM - 1) / BM) * ((g.N + 127) / 128) * g.batch * g.split_k;
-  // measured (tools/nt_sweep.sh, tools/gemm_census.py with AVC_NT_CFG): more resident
+  // measured (tools/gemm_census.py, a tile / stage sweep in round 2): more resident
   // workgroups beat deeper stages on these shapes, so 2 stages; 128-wide tiles when there are
   // >= 4 of them per CU, or for long-K wide products (8192x1024x4096: 75 vs 98 us)
   if (bn != 64 && bn != 128) bn = (g.N > 64 && (t128 >= 1024 || (g.N >= 1024 && g.K >= 2048))) ? 128 : 64;

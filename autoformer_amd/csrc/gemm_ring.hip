@@ -163,44 +163,6 @@ __device__ __forceinline__ bool ring_arrive_last(unsigned* cnt, unsigned arrival
   return *flag != 0;
 }
 
-// Column-tile barrier of the fused BatchNorm apply: every row tile arrives on the column tile's
-// counter WITHOUT the last one resetting it; the last one runs the finalize (write-through stores),
-// drains them and only then resets the counter to 0 -- the release the others poll for (the counter
-// returns to 0 at no other time within the launch).  Needs every row tile of a column tile resident
-// at once: gemm_ring_launch allows it only for grids of at most one workgroup per CU.
-__device__ __forceinline__ bool ring_arrive_hold(unsigned* cnt, unsigned arrivals, unsigned mine, unsigned* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(cnt, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = old + mine == arrivals ? 1u : 0u;
-  }
-  __syncthreads();
-  return *flag != 0;
-}
-__device__ __forceinline__ void ring_release(unsigned* cnt) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the finalize's write-through stores are out
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-}
-constexpr unsigned RING_SPIN = 1u << 22;  // ~0.3 s of s_sleep 1 polls: a stalled grid, not contention
-__device__ __forceinline__ void ring_wait(unsigned* cnt, unsigned* fault, int nap) {
-  if (threadIdx.x == 0) {
-    unsigned n = 0;
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-      for (int k = 0; k < nap; ++k) __builtin_amdgcn_s_sleep(1);  // fewer polls on the one address
-      if ((n += nap) >= RING_SPIN) {
-        if (fault) atomicOr(fault, 2u);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-}
-
-// bf16 stores of a 2 x 4-wave-layout accumulator tile (the fused BN apply outputs; row-major, ld):
-// staged through each wave's LDS region like ring_store_tile's bf16 path, 16-B stores
 template <int BM_, int BN_>
 __device__ __forceinline__ void ring_store16(f32x4 (&v)[BM_ / 32][BN_ / 64], bf16* out, long long ld, int N, int m0,
                                              int n0, int mlim, char* smem_raw) {
@@ -503,10 +465,9 @@ __device__ __forceinline__ void ring_store_tile(const GemmArgs& g, f32x4 (&acc)[
 // under the K loop (a load-then-store loop in the epilogue had serialised four HBM round trips)
 constexpr int BNB_YQ = 128 * 16 / RNT;  // 16-B chunks per thread (128 rows x 16 chunks of 8 bf16)
 // LDS offset of the staged y tile (128 rows x 272 B + flag): below the C staging (ring_epi_lds),
-// above the partial sums, so the 2-stage conv ring's 98 KiB hold it; the fused BN-backward apply
-// (bnb_dy16), which re-reads y after the C stores, keeps it above them (launch_conv sizes the LDS)
-constexpr int BNB_YS_LO = 8 * 1024, BNB_YS_HI = 80 * 1024, BNB_YBYTES = 128 * (2 * 128 + 16) + 16;
-__device__ __forceinline__ int bnb_ys(const GemmArgs& g) { return g.bnb_dy16 ? BNB_YS_HI : BNB_YS_LO; }
+// above the partial sums, so the 2-stage conv ring's 98 KiB hold it
+constexpr int BNB_YS_LO = 8 * 1024;
+__device__ __forceinline__ int bnb_ys(const GemmArgs&) { return BNB_YS_LO; }
 __device__ __forceinline__ void ring_bnb_prefetch(const GemmArgs& g, int m0, int n0, u32x4 (&yv)[BNB_YQ]) {
   const bf16* yb = static_cast<const bf16*>(g.bnb_y);
   // unconditional loads at clamped addresses (N % 8 == 0 on this path), zeroed after: a load inside
@@ -597,52 +558,7 @@ __device__ __forceinline__ bool ring_bnb_epilogue(const GemmArgs& g, f32x4 (&acc
     }
   }
   const int nrb = (g.M + 127) / 128;
-  if (g.bnb_dy16) return ring_arrive_hold(g.bnb_cnt + n0 / BN_, (unsigned)nrb, 1u, flag);
   return ring_arrive_last(g.bnb_cnt + n0 / BN_, (unsigned)nrb, 1u, flag);
-}
-
-// The fused apply of the BatchNorm backward (avc_bnb_args.dy_bf16): after the column-tile barrier,
-// dy = k1*(dz - m1 - yc*rs*m2) from this tile's dL/da (the accumulators, rounded like the stored C),
-// y (still staged in LDS) and the constants -- the arithmetic of bn_bwd_apply_rows_kernel, so the
-// result is the apply pass's bit for bit
-__device__ __forceinline__ void ring_bnb_apply(const GemmArgs& g, f32x4 (&acc)[4][2], int m0, int n0, char* smem_raw) {
-  constexpr int NJ = 2, YP = 2 * 128 + 16;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
-  const int rbase = m0 + wm * 64 + 4 * (lane >> 4);
-  const int cbase = n0 + wn * 32 + (lane & 15);
-  const avcbn::BwdFin& f = g.bnb_fin;
-  const char* ys = smem_raw + bnb_ys(g);
-  const bool round16 = g.c == nullptr;
-  const int C = g.N;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int col = cbase + j * 16;
-    const bool cv = col < C;
-    const int cc = cv ? col : 0;
-    const float rs = f.rstd[cc], mu = f.mean[cc];
-    const float k1 = (f.gamma ? f.gamma[cc] : 1.f) * rs;
-    const float bt = f.beta ? f.beta[cc] : 0.f;
-    const float m1 = ld_sc1(f.coef + C + cc), m2 = ld_sc1(f.coef + 2 * C + cc);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = rbase + i * 16 + e;
-        float v = acc[i][j][e];
-        if (round16) v = (float)(bf16)v;
-        const float yf = (cv && row < g.M)
-                             ? __builtin_bit_cast(float, (unsigned)*reinterpret_cast<const unsigned short*>(
-                                                             ys + (row - m0) * YP + (col - n0) * 2)
-                                                             << 16)
-                             : 0.f;
-        const float yc = yf - mu;
-        const float dz = act_bwd_from_pre(v, yc * k1 + bt, g.bnb_act);
-        acc[i][j][e] = k1 * (dz - m1 - yc * rs * m2);
-      }
-  }
-  __syncthreads();  // every wave is done with the y tile before the staged stores reuse the LDS
-  ring_store16<128, 128>(acc, g.bnb_dy16, g.N, g.N, m0, n0, g.M, smem_raw);
 }
 
 // the last-arriving row tile of a column tile: the apply constants and parameter gradients of its
@@ -676,8 +592,7 @@ __device__ __forceinline__ void ring_bnb_finalize(const GemmArgs& g, int n0, cha
         a1 += red[(1 * FGR + k) * BN_ + cl];
         a2 += red[(2 * FGR + k) * BN_ + cl];
       }
-      if (g.bnb_dy16) avcbn::bwd_finalize_store<true>(c, a0, a1, a2, g.M, g.N, f);
-      else avcbn::bwd_finalize_store(c, a0, a1, a2, g.M, g.N, f);
+      avcbn::bwd_finalize_store(c, a0, a1, a2, g.M, g.N, f);
     }
   }
 }
@@ -734,12 +649,6 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
     if (bnb_last) {
       __syncthreads();  // the staged stores are done with the LDS
       ring_bnb_finalize(g, n0, smem_raw);
-    }
-    if (g.bnb_ws && g.bnb_dy16) {
-      unsigned* cnt = g.bnb_cnt + n0 / BN_;
-      if (bnb_last) ring_release(cnt);
-      else ring_wait(cnt, g.fault, g.nap);
-      ring_bnb_apply(g, acc, m0, n0, smem_raw);
     }
   }
   if (g.bn_partial) {
@@ -822,35 +731,7 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[BM
       const int ntile = (g.M + srows - 1) / srows;
       const int mine = min(NH, ntile - mt0);
       unsigned* cnt = g.bn_cnt + n0 / BN_;
-      if (!g.bn_apply16) {
-        if (ring_arrive_last(cnt, (unsigned)ntile, (unsigned)mine, flag)) bn_finalize_cols<BN_>(g, n0, red);
-      } else {
-        // fused apply (avc_bn_fin.apply_bf16): act(y*scale + shift) of this tile once the column tile's
-        // statistics are final -- y as stored (bf16-rounded when C is bf16 only), bn_apply_kernel's
-        // arithmetic
-        if (ring_arrive_hold(cnt, (unsigned)ntile, (unsigned)mine, flag)) {
-          bn_finalize_cols<BN_>(g, n0, red);
-          ring_release(cnt);
-        } else {
-          ring_wait(cnt, g.fault, g.nap);
-        }
-        const bool round16 = g.c == nullptr;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int col = cbase + j * 16;
-          const int cc = col < g.N ? col : 0;
-          const float sc = ld_sc1(g.bn_scale + cc), sh = ld_sc1(g.bn_shift + cc);
-#pragma unroll
-          for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              float v = acc[i][j][e];
-              if (round16) v = (float)(bf16)v;
-              acc[i][j][e] = act_fwd(v * sc + sh, g.bn_act);
-            }
-        }
-        ring_store16<BM_, BN_>(acc, g.bn_apply16, g.N, g.N, m0, n0, mlim, smem_raw);
-      }
+      if (ring_arrive_last(cnt, (unsigned)ntile, (unsigned)mine, flag)) bn_finalize_cols<BN_>(g, n0, red);
     }
   }
 }
@@ -970,196 +851,6 @@ __global__ void __launch_bounds__(RNT, 2) gemm_ring_kernel(GemmArgs g, int gm) {
   ring_epilogue<BM_, BN_>(g, acc, m0, n0, bz, ks, smem_raw);
 }
 
-// ---------------------------------------------------------------------------------------------
-// The same tile with 32-deep K slots of 64-B rows (K32): a slot of the 256 x 256 tile is 32 KB, so
-// four slots fit the LDS of the two-slot 64-deep form and THREE K-steps of fills are in flight
-// during a step's MFMAs instead of one (the K loop is bound by LDS-DMA latency: fills in flight /
-// latency = the per-CU operand rate, MI355X_MICROARCH.md "ldsdma-fill").  Row chunk swizzle:
-// logical 16-B chunk c of row r is stored at c ^ ((r >> 2) & 3), so the 16 rows of a fragment read
-// spread over all four chunk positions (64-B rows repeat the bank pattern every 4 rows).
-constexpr int R32 = 64;  // bytes per LDS row (32 bf16 of K)
-
-// R rows x 32 K per slot: R/128 glds per thread.  Instruction i of wave w covers slot rows
-// (8i + w)*16 .. +16; lane L writes row +(L>>2), 16-B position L&3, which holds global K chunk
-// (L&3) ^ ((L>>4)&3) for every i and w (the row's (r >> 2) & 3).
-template <int R, bool WIN>
-struct RingLoader32 {
-  static constexpr int NI = R / 128;
-  const bf16* base;
-  long long roff[NI];
-  int tt[NI];
-  bool rok[NI];
-  int kc;
-  int ld, pad, t_in, chans;
-
-  __device__ __forceinline__ void init(const OpDev& o, int row0, int bz) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    base = reinterpret_cast<const bf16*>(o.ptr) + (long long)bz * o.bstride;
-    kc = 8 * ((lane & 3) ^ ((lane >> 4) & 3));
-    ld = (int)o.ld;
-    pad = o.pad;
-    t_in = o.t_in;
-    chans = o.chans;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int r = row0 + (8 * i + w) * 16 + (lane >> 2);
-      rok[i] = r < o.rows;
-      const int rr = rok[i] ? r : 0;
-      if (WIN) {
-        const int b = (int)fdiv((uint32_t)rr, o.tdiv);
-        tt[i] = rr - b * o.t_out;
-        roff[i] = (long long)(b * o.t_in + tt[i]) * o.ld;
-      } else {
-        tt[i] = 0;
-        roff[i] = (long long)rr * o.ld;
-      }
-    }
-  }
-
-  __device__ __forceinline__ void issue(char* lds, int kbase, int kend, const FastDiv& cdv) {
-    const int w = threadIdx.x >> 6;
-    const int k = kbase + kc;
-    const bool kok = k < kend;
-    int tap = 0, cc = k;
-    if (WIN) {
-      tap = (int)fdiv((uint32_t)k, cdv);
-      cc = k - tap * chans;
-    }
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      bool ok = kok && rok[i];
-      long long off;
-      if (WIN) {
-        const int t2 = tt[i] + tap - pad;
-        ok = ok && t2 >= 0 && t2 < t_in;
-        off = roff[i] + (long long)(tap - pad) * ld + cc;
-      } else {
-        off = roff[i] + k;
-      }
-      glds16(ok ? (const void*)(base + off) : (const void*)g_zero16_rg, lds + (8 * i + w) * 16 * R32);
-    }
-  }
-};
-
-template <int BM_, int BN_, int NST, bool WIN>
-__global__ void __launch_bounds__(RNT, 2) gemm_ring32_kernel(GemmArgs g, int gm) {
-  constexpr int TWM = BM_ / 2, TWN = BN_ / 4, MI = TWM / 16, NJ = TWN / 16;
-  constexpr int A_BYTES = BM_ * R32, STAGE = (BM_ + BN_) * R32;
-  constexpr int LPT = BM_ / 128 + BN_ / 128;  // glds per thread per K-step
-  constexpr int P = NST - 1;                  // K-steps in flight
-  constexpr int KS = 32;
-  static_assert(NST >= 2 && NST <= 6 && BM_ % 128 == 0 && BN_ % 128 == 0, "ring32 shape");
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
-
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
-  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-  const int nN = (g.N + BN_ - 1) / BN_, nM = (g.M + BM_ - 1) / BM_;
-  const int z = lid / (nN * nM);
-  const int rem = lid - z * nN * nM;
-  const int grp = rem / (gm * nN);
-  const int fm = grp * gm;
-  const int gsz = min(nM - fm, gm);
-  const int wi = rem - grp * gm * nN;
-  const int mt = fm + wi % gsz, nt = wi / gsz;
-  const int m0 = mt * BM_, n0 = nt * BN_;
-  const int bz = z / g.split_k, ks = z - bz * g.split_k;
-  const int kbeg = ks * g.klen;
-  const int kend = min(g.K, kbeg + g.klen);
-  const int nkt = kend > kbeg ? (kend - kbeg + KS - 1) / KS : 0;
-
-  RingLoader32<BM_, WIN> la;
-  RingLoader32<BN_, false> lb;
-  la.init(g.a, m0, bz);
-  lb.init(g.b, n0, bz);
-  const FastDiv cdv = g.a.cdv;
-
-  f32x4 acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // fragment reads: row (lane&15) of each 16-row block, logical chunk lane>>4 stored at
-  // (lane>>4) ^ ((row>>2)&3) (block bases are multiples of 16 rows)
-  const int frow = lane & 15;
-  const int chk = ((lane >> 4) ^ ((frow >> 2) & 3)) << 4;
-  const int aoff = (wm * TWM + frow) * R32 + chk, boff = A_BYTES + (wn * TWN + frow) * R32 + chk;
-
-#pragma unroll
-  for (int p = 0; p < P; ++p)
-    if (p < nkt) {
-      char* st = smem_raw + p * STAGE;
-      la.issue(st, kbeg + p * KS, kend, cdv);
-      lb.issue(st + A_BYTES, kbeg + p * KS, kend, cdv);
-    }
-
-  constexpr int MH = MI / 2;
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int ahead = min(P - 1, nkt - 1 - kt);  // K-steps allowed to stay in flight
-    if constexpr (P >= 5) {
-      if (ahead >= 4) wait_vm<4 * LPT>();
-      else if (ahead == 3) wait_vm<3 * LPT>();
-      else if (ahead == 2) wait_vm<2 * LPT>();
-      else if (ahead == 1) wait_vm<LPT>();
-      else wait_vm<0>();
-    } else if constexpr (P >= 3) {
-      if (ahead >= 2) wait_vm<2 * LPT>();
-      else if (ahead == 1) wait_vm<LPT>();
-      else wait_vm<0>();
-    } else if constexpr (P == 2) {
-      if (ahead >= 1) wait_vm<LPT>();
-      else wait_vm<0>();
-    } else {
-      wait_vm<0>();
-    }
-    raw_barrier();
-    if (kt + P < nkt) {
-      char* st = smem_raw + ((kt + P) % NST) * STAGE;
-      la.issue(st, kbeg + (kt + P) * KS, kend, cdv);
-      lb.issue(st + A_BYTES, kbeg + (kt + P) * KS, kend, cdv);
-    }
-    // one 32-deep K-step: read B and the first half of A, MFMAs on it while the second half of A
-    // is read (inline-asm reads, counted lgkmcnt waits)
-    const unsigned st = lds_addr(smem_raw + (kt % NST) * STAGE);
-    const unsigned a0 = st + aoff, b0 = st + boff;
-    bf16x8 af[MI], bfr[NJ];
-    ds_read_n<NJ, 16 * R32>(bfr, b0);
-    ds_read_n<MH, 16 * R32>(af, a0);
-    ds_read_n<MH, 16 * R32, MH * 16 * R32>(af + MH, a0);
-    wait_lgkm<MH>();
-#pragma unroll
-    for (int i = 0; i < MH; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    wait_lgkm<0>();
-#pragma unroll
-    for (int i = MH; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-  }
-  __syncthreads();
-  ring_epilogue<BM_, BN_>(g, acc, m0, n0, bz, ks, smem_raw);
-}
-
-template <int BM_, int BN_, int NST, bool WIN>
-void launch32(const GemmArgs& g, int gm, hipStream_t s) {
-  const size_t lds = std::max((size_t)NST * (BM_ + BN_) * R32, ring_epi_lds<BM_, BN_>());
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ring32_kernel<BM_, BN_, NST, WIN>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
-  const int nb = ((g.M + BM_ - 1) / BM_) * ((g.N + BN_ - 1) / BN_) * g.batch * g.split_k;
-  gemm_ring32_kernel<BM_, BN_, NST, WIN><<<nb, RNT, lds, s>>>(g, gm);
-}
-
 template <int BM_, int BN_, int NST, bool WIN>
 void launch(const GemmArgs& g, int gm, hipStream_t s) {
   const size_t lds = std::max((size_t)NST * (BM_ + BN_) * RROW, ring_epi_lds<BM_, BN_>());
@@ -1190,7 +881,7 @@ void launch(const GemmArgs& g, int gm, hipStream_t s) {
 // (48 KiB) now fits on a CU beside it, so a backward conv no longer waits for those to drain from
 // its CUs: C2 5.78-5.80 -> 5.74-5.75 ms (profiles/r5_conv_ring_slope.txt).  The one-utterance tile
 // (CU_NST) and the warp-specialised diagnostic form (WS_NST) keep three.
-constexpr int CV_TM = 128, CV_TN = 128, CV_TAPS = 5, CV_CBK = 32, CV_NST = 2, CU_NST = 3, WS_NST = 3;
+constexpr int CV_TM = 128, CV_TN = 128, CV_TAPS = 5, CV_CBK = 32, CV_NST = 2, CU_NST = 3;
 constexpr int CV_AI = (CV_TM + CV_TAPS - 1 + 15) / 16;  // 9 halo instructions (16 rows of 64 B)
 constexpr int CV_BI = CV_TAPS * CV_TN / 16;             // 40 weight instructions
 constexpr int CV_TOT = CV_AI + CV_BI;                   // 49
@@ -1553,246 +1244,26 @@ __global__ void __launch_bounds__(RNT, 2) conv_utt_kernel(GemmArgs g, int gm) {
 void launch_conv_utt(const GemmArgs& g0, int gm, hipStream_t s) {
   GemmArgs g = g0;
   g.bn_rows = g.a.t_out;  // one statistics tile per utterance
-  // AVC_CU_NST = 2: two LDS stages (106 KiB, room for a side-stream workgroup beside it)
-  static const int nstu = [] {
-    const char* e = getenv("AVC_CU_NST");
-    return e && atoi(e) == 2 ? 2 : CU_NST;
-  }();
-  const size_t lds = std::max((size_t)nstu * CU_STAGE, ring_epi_lds<CU_TM, CV_TN>());
+  // three LDS stages (two: 106 KiB, room for a side-stream workgroup beside it -- measured no faster,
+  // profiles/r5_conv_ring_slope.txt)
+  const size_t lds = std::max((size_t)CU_NST * CU_STAGE, ring_epi_lds<CU_TM, CV_TN>());
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(nstu == 2 ? reinterpret_cast<const void*>(&conv_utt_kernel<2>)
-                                        : reinterpret_cast<const void*>(&conv_utt_kernel<3>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_utt_kernel<CU_NST>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int nb = (g.M / g.a.t_out) * ((g.N + CV_TN - 1) / CV_TN);
-  if (nstu == 2) conv_utt_kernel<2><<<nb, RNT, lds, s>>>(g, gm);
-  else conv_utt_kernel<3><<<nb, RNT, lds, s>>>(g, gm);
-}
-
-// ---------------------------------------------------------------------------------------------
-// The same conv tile, warp-specialised: waves 0-3 are MMA waves (2 x 2, 64 x 64 each: 8 fragment
-// reads per 16 MFMAs, half the LDS reads per FLOP of the 64 x 32 wave tile -- whose 6 reads per 8
-// MFMAs kept the LDS array ~75 % busy and the MFMA pipe at 0.28 with the loads removed,
-// profiles/r4_pmc_conv_ring.txt), waves 4-7 are loader waves that issue every LDS-DMA fill of the
-// ring (49 per stage: 13 / 12 / 12 / 12), so the MMA waves' instruction streams hold only fragment
-// reads and MFMAs.  One MMA wave and one loader wave per SIMD.  The stage protocol is the 8-wave
-// kernel's: loaders wait for their own fills of stage cs (counted vmcnt), one raw barrier per stage,
-// after which the slot of stage cs-1 is free (the MMA waves drained its reads before the barrier)
-// and receives stage cs+2.  After the K loop the MMA waves' 64 x 64 accumulators are redistributed
-// through LDS into the 2 x 4 layout of ring_epilogue, which all 8 waves then run unchanged.
-constexpr int CW_LI = (CV_TOT + 3) / 4;  // 13: fills per stage of loader wave 4 (12 for waves 5-7)
-
-template <bool ALIGNED>
-__global__ void __launch_bounds__(RNT, 2) conv_ring_ws_kernel(GemmArgs g, int gm) {
-  constexpr int P = WS_NST - 1;
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool loader = wid >= 4;
-
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
-  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-  const int nN = (g.N + CV_TN - 1) / CV_TN, nM = (g.M + CV_TM - 1) / CV_TM;
-  const int grp = lid / (gm * nN), fm = grp * gm, gsz = min(nM - fm, gm);
-  const int wi = lid - grp * gm * nN;
-  const int mt = fm + wi % gsz, nt = wi / gsz;
-  const int m0 = mt * CV_TM, n0 = nt * CV_TN;
-
-  const OpDev& A = g.a;
-  const OpDev& Bo = g.b;
-  const int pad = A.pad, T = A.t_out, chans = A.chans;
-  const int nst = chans / CV_CBK;
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if (loader) {
-    // ---- loader waves: fill qi = i*4 + lw writes stage bytes [qi KiB, +1 KiB), rows 16*qi + (lane>>2)
-    // of 64 B, 16-B slot lane&3 holding global chunk (lane&3) ^ ((row>>1)&3) (the 8-wave layout)
-    const int lw = wid - 4;
-    const bool full = lw < CV_TOT % 4;  // issues CW_LI fills per stage, else CW_LI - 1
-    const bf16* xa = reinterpret_cast<const bf16*>(A.ptr);
-    const bf16* wb = reinterpret_cast<const bf16*>(Bo.ptr);
-    const int b0 = (int)fdiv((uint32_t)m0, A.tdiv);
-    const bf16* zp = reinterpret_cast<const bf16*>(g_zero16_rg);
-    asm volatile("" : "+v"(zp));
-    const bf16* src[CW_LI];
-    int sst[CW_LI];
-#pragma unroll
-    for (int i = 0; i < CW_LI; ++i) {
-      const int qi = i * 4 + lw;
-      const int lrow = lane >> 2, slot = lane & 3;
-      src[i] = zp;
-      sst[i] = 0;
-      if (qi < CV_AI) {
-        const int hr = 16 * qi + lrow;
-        const int f = m0 - pad + hr;
-        bool ok = hr < CV_TM + CV_TAPS - 1 && f >= 0 && f < g.M;
-        if (ALIGNED && ok) ok = (int)fdiv((uint32_t)f, A.tdiv) == b0;
-        if (ok) {
-          src[i] = xa + (long long)f * A.ld + 8 * (slot ^ ((hr >> 1) & 3));
-          sst[i] = CV_CBK;
-        }
-      } else if (qi < CV_TOT) {
-        const int wr = 16 * (qi - CV_AI) + lrow;
-        const int tap = wr / CV_TN, n = n0 + (wr - tap * CV_TN);
-        if (n < g.N) {
-          src[i] = wb + (long long)n * Bo.ld + (long long)tap * chans + 8 * (slot ^ ((wr >> 1) & 3));
-          sst[i] = CV_CBK;
-        }
-      }
-    }
-    auto issue = [&](int stg, int cs) {
-      char* base = smem_raw + stg * CV_STAGE;
-#pragma unroll
-      for (int i = 0; i < CW_LI; ++i) {
-        const int qi = i * 4 + lw;
-        if (qi < CV_TOT) glds16(src[i] + (long long)cs * sst[i], base + qi * 1024);
-      }
-    };
-#pragma unroll
-    for (int p = 0; p < P; ++p)
-      if (p < nst) issue(p, p);
-    for (int cs = 0; cs < nst; ++cs) {
-      if (cs + 1 < nst) {
-        if (full) wait_vm<CW_LI>();
-        else wait_vm<CW_LI - 1>();
-      } else {
-        wait_vm<0>();
-      }
-      raw_barrier();
-      if (cs + P < nst) issue((cs + P) % WS_NST, cs + P);
-    }
-  } else {
-    // ---- MMA waves (wm, wn) = (wid >> 1, wid & 1): rows wm*64 .. +64, columns wn*64 .. +64
-    const int wm = wid >> 1, wn = wid & 1;
-    const int frow = lane & 15, kq = lane >> 4;
-    int aaddr[CV_TAPS];
-#pragma unroll
-    for (int k = 0; k < CV_TAPS; ++k) {
-      const int r = wm * 64 + frow + k;
-      aaddr[k] = r * 64 + 16 * (kq ^ ((r >> 1) & 3));
-    }
-    const int baddr = CV_ABYTES + (wn * 64 + frow) * 64 + 16 * (kq ^ ((frow >> 1) & 3));
-    unsigned vmask = 0xFFFFFFFFu;
-    if (!ALIGNED) {
-      vmask = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = min(m0 + wm * 64 + i * 16 + frow, g.M - 1);
-        const int b = (int)fdiv((uint32_t)m, A.tdiv);
-        const int t = m - b * T;
-#pragma unroll
-        for (int k = 0; k < CV_TAPS; ++k) {
-          const int t2 = t + k - pad;
-          if (t2 >= 0 && t2 < T) vmask |= 1u << (i * 8 + k);
-        }
-      }
-    }
-    for (int cs = 0; cs < nst; ++cs) {
-      raw_barrier();
-      const unsigned st = lds_addr(smem_raw + (cs % WS_NST) * CV_STAGE);
-      bf16x8 af[2][4], bfr[2][4];
-      auto read_tap = [&](auto kc, int slot) {
-        constexpr int k = decltype(kc)::value;
-        const unsigned a0 = st + aaddr[k], b0 = st + baddr;
-        af[slot][0] = ds_read16<0>(a0);
-        af[slot][1] = ds_read16<1024>(a0);
-        af[slot][2] = ds_read16<2048>(a0);
-        af[slot][3] = ds_read16<3072>(a0);
-        bfr[slot][0] = ds_read16<(k * CV_TN) * 64>(b0);
-        bfr[slot][1] = ds_read16<(k * CV_TN + 16) * 64>(b0);
-        bfr[slot][2] = ds_read16<(k * CV_TN + 32) * 64>(b0);
-        bfr[slot][3] = ds_read16<(k * CV_TN + 48) * 64>(b0);
-      };
-      auto mfma_tap = [&](auto kc, int slot) {
-        constexpr int k = decltype(kc)::value;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bf16x8 av = (ALIGNED || ((vmask >> (i * 8 + k)) & 1u)) ? af[slot][i] : bf16x8{};
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bfr[slot][j], acc[i][j], 0, 0, 0);
-        }
-      };
-      using I0 = std::integral_constant<int, 0>;
-      using I1 = std::integral_constant<int, 1>;
-      using I2 = std::integral_constant<int, 2>;
-      using I3 = std::integral_constant<int, 3>;
-      using I4 = std::integral_constant<int, 4>;
-      // tap k+1's eight reads in flight during tap k's sixteen MFMAs
-      read_tap(I0{}, 0);
-      read_tap(I1{}, 1);
-      wait_lgkm<8>();
-      mfma_tap(I0{}, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      read_tap(I2{}, 0);
-      wait_lgkm<8>();
-      mfma_tap(I1{}, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      read_tap(I3{}, 1);
-      wait_lgkm<8>();
-      mfma_tap(I2{}, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      read_tap(I4{}, 0);
-      wait_lgkm<8>();
-      mfma_tap(I3{}, 1);
-      wait_lgkm<0>();
-      mfma_tap(I4{}, 0);
-    }
-  }
-  // ---- redistribution into the 2 x 4 layout: MMA wave w's block (i, j) -> LDS [w][i][j][lane] (16 B)
-  __syncthreads();  // every wave is past the K loop (the stages are free)
-  f32x4* red = reinterpret_cast<f32x4*>(smem_raw);
-  if (!loader) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) red[((wid * 4 + i) * 4 + j) * 64 + lane] = acc[i][j];
-  }
-  __syncthreads();
-  // epilogue wave w' = (wm', wn') = (wid >> 2, wid & 3): rows wm'*64, columns wn'*32 = MMA wave
-  // (wm', wn' >> 1), its blocks j = 2 (wn' & 1) + j'
-  f32x4 acc2[4][2];
-  {
-    const int mw = (wid >> 2) * 2 + ((wid & 3) >> 1), jo = 2 * (wid & 1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc2[i][j] = red[((mw * 4 + i) * 4 + jo + j) * 64 + lane];
-  }
-  __syncthreads();  // the epilogue reuses the LDS
-  ring_epilogue<CV_TM, CV_TN>(g, acc2, m0, n0, 0, 0, smem_raw);
-}
-
-template <bool ALIGNED>
-void launch_conv_ws(const GemmArgs& g, int gm, hipStream_t s) {
-  const size_t lds = std::max((size_t)WS_NST * CV_STAGE, ring_epi_lds<CV_TM, CV_TN>());
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_ws_kernel<ALIGNED>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
-  const int nb = ((g.M + CV_TM - 1) / CV_TM) * ((g.N + CV_TN - 1) / CV_TN);
-  conv_ring_ws_kernel<ALIGNED><<<nb, RNT, lds, s>>>(g, gm);
+  conv_utt_kernel<CU_NST><<<nb, RNT, lds, s>>>(g, gm);
 }
 
 template <bool ALIGNED, int ABL = 0, bool BNB = false>
 void launch_conv(const GemmArgs& g, int gm, hipStream_t s) {
-  const size_t base = std::max((size_t)CV_NST * CV_STAGE, ring_epi_lds<CV_TM, CV_TN>());
-  const size_t hi = std::max(base, (size_t)BNB_YS_HI + BNB_YBYTES);  // the fused BN-backward apply's y tile
-  const size_t lds = (BNB && g.bnb_dy16) ? hi : base;
+  const size_t lds = std::max((size_t)CV_NST * CV_STAGE, ring_epi_lds<CV_TM, CV_TN>());
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<ALIGNED, ABL, BNB>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)hi);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int nb = ((g.M + CV_TM - 1) / CV_TM) * ((g.N + CV_TN - 1) / CV_TN);
@@ -1800,11 +1271,6 @@ void launch_conv(const GemmArgs& g, int gm, hipStream_t s) {
 }
 
 bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
-
-bool getenv_flag(const char* name, bool dflt) {
-  const char* e = getenv(name);
-  return e ? e[0] != '0' : dflt;
-}
 
 bool operand_ok(const OpDev& o, bool allow_win) {
   if (o.dtype != AVC_BF16 || !ok16(o.ptr) || o.ld % 8 || o.bstride % 8) return false;
@@ -1820,8 +1286,7 @@ struct RingCfg {
   int mode = -1;  // -1 auto, 0 off, 1 forced
   int bm = 0, bn = 0, nst = 0, gm = 8, win = 2;
   int abl = 0;  // timing ablations of the halo conv (win 3 / 4 through avc_gemm_set_ring)
-  int ws = 0;   // the warp-specialised halo conv (AVC_CONV_WS=1, or win 6 through avc_gemm_set_ring)
-  bool utt = true;  // one-utterance conv tiles for 128 < T <= 192 (AVC_CONV_UTT=0: gemm_conv.hip)
+  bool utt = true;  // one-utterance conv tiles for 128 < T <= 192 (win 10 through avc_gemm_set_ring: off)
 };
 RingCfg init_cfg() {
   RingCfg r;
@@ -1838,8 +1303,6 @@ RingCfg init_cfg() {
     if (n >= 4 && a3 > 0) r.gm = a3;
   }
   if (const char* e = getenv("AVC_RING_WIN")) r.win = atoi(e);
-  if (const char* e = getenv("AVC_CONV_WS")) r.ws = atoi(e);
-  r.utt = getenv_flag("AVC_CONV_UTT", true);
   return r;
 }
 RingCfg g_ring = init_cfg();
@@ -1855,9 +1318,6 @@ bool gemm_ring_launch(const GemmArgs& g, hipStream_t s) {
   return r;
 }
 
-thread_local bool g_ring_applied = false;
-bool gemm_ring_applied() { return g_ring_applied; }
-
 int ring_num_cus() {
   static int n = [] {
     int dev = 0;
@@ -1870,13 +1330,7 @@ int ring_num_cus() {
 
 bool gemm_ring_launch_(const GemmArgs& g_in, hipStream_t s) {
   const RingCfg& c = g_ring;
-  g_ring_applied = false;
-  // the fused BN apply outputs only on the halo convs below (one workgroup per CU, every row tile
-  // of a column tile resident for the barrier); every other launch gets them cleared
-  GemmArgs g = g_in;
-  const bool want_apply = (g.bn_apply16 && g.bn_cnt && g.bn_partial) || (g.bnb_dy16 && g.bnb_ws);
-  g.bn_apply16 = nullptr;
-  g.bnb_dy16 = nullptr;
+  const GemmArgs& g = g_in;
   if (c.mode == 0 || (g.a.win && !c.win)) return false;
   if (g.K % 8 || g.klen % RBK || g.atomic || g.cperm) return false;  // (no atomic / cperm stores)
   if (g.ctr && ((reinterpret_cast<uintptr_t>(g.c) & 15) || (reinterpret_cast<uintptr_t>(g.res) & 15) ||
@@ -1905,17 +1359,9 @@ bool gemm_ring_launch_(const GemmArgs& g_in, hipStream_t s) {
   const bool utt = win && c.win == 2 && c.mode != 1 && a.taps == CV_TAPS && a.t_in == T && 2 * a.pad == a.taps - 1 &&
                    g.K == a.taps * a.chans && a.chans % CV_CBK == 0 && g.batch == 1 && g.split_k == 1 && !g.b.win &&
                    T > CV_TM && T <= CU_TM && g.M % T == 0 && g.N >= 128 && !g.bnb_ws && !g.c16_act && !g.agrad &&
-                   !g.csum && !g.ctr && (!g.bn_partial || g.bn_cnt) && !c.abl && !c.ws && c.utt;
+                   !g.csum && !g.ctr && (!g.bn_partial || g.bn_cnt) && !c.abl && c.utt;
   if (utt) {
-    const int nb = (g.M / T) * ((g.N + CV_TN - 1) / CV_TN);
-    if (want_apply && g_in.bn_apply16 && nb <= ring_num_cus()) {
-      GemmArgs ga = g;
-      ga.bn_apply16 = g_in.bn_apply16;
-      launch_conv_utt(ga, c.gm, s);
-      g_ring_applied = true;
-    } else {
-      launch_conv_utt(g, c.gm, s);
-    }
+    launch_conv_utt(g, c.gm, s);
     g_ring_last = 3;
     return true;
   }
@@ -1927,27 +1373,11 @@ bool gemm_ring_launch_(const GemmArgs& g_in, hipStream_t s) {
     else if (c.abl == 5) launch_conv<true, 5>(g, c.gm, s);
     else if (c.abl == 6) launch_conv<true, 6>(g, c.gm, s);
     else if (g.bnb_ws) {  // the BN-backward reduction epilogue (8-wave tile only)
-      const int nb = ((g.M + CV_TM - 1) / CV_TM) * ((g.N + CV_TN - 1) / CV_TN);
-      GemmArgs ga = g;
-      if (want_apply && g_in.bnb_dy16 && nb <= ring_num_cus()) {
-        ga.bnb_dy16 = g_in.bnb_dy16;
-        g_ring_applied = true;
-      }
-      if (a.t_out % CV_TM == 0) launch_conv<true, 0, true>(ga, c.gm, s);
-      else launch_conv<false, 0, true>(ga, c.gm, s);
-    } else if (!c.ws && want_apply && g_in.bn_apply16 &&
-               ((g.M + CV_TM - 1) / CV_TM) * ((g.N + CV_TN - 1) / CV_TN) <= ring_num_cus()) {
-      GemmArgs ga = g;
-      ga.bn_apply16 = g_in.bn_apply16;
-      if (a.t_out % CV_TM == 0) launch_conv<true>(ga, c.gm, s);
-      else launch_conv<false>(ga, c.gm, s);
-      g_ring_applied = true;
-    } else if (c.ws) {
-      if (a.t_out % CV_TM == 0) launch_conv_ws<true>(g, c.gm, s);
-      else launch_conv_ws<false>(g, c.gm, s);
+      if (a.t_out % CV_TM == 0) launch_conv<true, 0, true>(g, c.gm, s);
+      else launch_conv<false, 0, true>(g, c.gm, s);
     } else if (a.t_out % CV_TM == 0) launch_conv<true>(g, c.gm, s);
     else launch_conv<false>(g, c.gm, s);
-    g_ring_last = c.ws && !g.bnb_ws && !c.abl ? 4 : 2;
+    g_ring_last = 2;
     return true;
   }
   int bm, bn, nst;
@@ -1972,13 +1402,7 @@ bool gemm_ring_launch_(const GemmArgs& g_in, hipStream_t s) {
       int bm, bn, nst, occ;
       double eff;
     };
-    // AVC_RING_NST128: ring slots of the 128 x 128 tile (4 = 128 KiB; 3 = 96 KiB leaves room for a
-    // side-stream workgroup beside it, as the 2-stage halo conv does)
-    static const int nst128 = [] {
-      const char* e = getenv("AVC_RING_NST128");
-      return e && atoi(e) == 3 ? 3 : 4;
-    }();
-    const Opt opts[4] = {{256, 256, 2, 1, 1.0}, {256, 128, 3, 1, 0.85}, {128, 128, nst128, 1, 0.75},
+    const Opt opts[4] = {{256, 256, 2, 1, 1.0}, {256, 128, 3, 1, 0.85}, {128, 128, 4, 1, 0.75},
                          {128, 128, 2, 2, g.agrad ? 0.38 : 0.47}};
     double best = 0;
     bm = 0;
@@ -2006,16 +1430,6 @@ bool gemm_ring_launch_(const GemmArgs& g_in, hipStream_t s) {
   RING_CASE(256, 256, 2) RING_CASE(256, 128, 3) RING_CASE(128, 128, 4) RING_CASE(128, 128, 3)
   RING_CASE(128, 256, 3) RING_CASE(256, 128, 2) RING_CASE(128, 128, 2)  // (128x128x2: 64 KB, two per CU)
 #undef RING_CASE
-  // 32-deep slots (nst = 10 + stages in the forced form)
-#define RING32_CASE(BMV, BNV, NSV)                        \
-  if (bm == BMV && bn == BNV && nst == 10 + NSV) {        \
-    if (win) launch32<BMV, BNV, NSV, true>(g, c.gm, s);   \
-    else launch32<BMV, BNV, NSV, false>(g, c.gm, s);      \
-    g_ring_last = 5;                                      \
-    return true;                                          \
-  }
-  RING32_CASE(256, 256, 4) RING32_CASE(256, 128, 5) RING32_CASE(128, 128, 6)
-#undef RING32_CASE
   return false;
 }
 
@@ -2033,11 +1447,8 @@ extern "C" int avc_gemm_set_ring(int mode, int bm, int bn, int nst, int gm, int 
   if (gm > 0) avcg::g_ring.gm = gm;
   avcg::g_ring.win = win >= 3 ? 2 : win;
   // 3: loads only, 4: reads + MFMAs only, 5: contiguous weight pieces, 7: MFMAs only, 8: reads only,
-  // 9: s_setprio around the MFMA groups (timing ablations); 6: the warp-specialised halo conv, 2: the
-  // 8-wave one
+  // 9: s_setprio around the MFMA groups (timing ablations of the halo conv)
   avcg::g_ring.abl = (win >= 3 && win <= 5) ? win - 2 : (win >= 7 && win <= 9) ? win - 3 : 0;
-  if (win == 6) avcg::g_ring.ws = 1;
-  else if (win == 2 || win == 10) avcg::g_ring.ws = 0;
   // 10: the halo convs without the one-utterance tile (T = 176 back on gemm_conv.hip); any other
   // value restores the default
   avcg::g_ring.utt = win != 10;

@@ -222,142 +222,6 @@ void launch(const GemmArgs& g, int nblocks, hipStream_t s) {
   gemm_tt_kernel<WINB><<<nblocks, 256, lds, s>>>(g);
 }
 
-// ------------------------------------------------------------------ pipelined TT kernel
-// BMT x 128 tile (BMT = 128: 4 waves as 2x2; 256: 8 waves as 4x2, each wave 64 x 64), BK = 64,
-// NST LDS stages with NST-1 K-tiles in flight: a counted `s_waitcnt vmcnt` + raw s_barrier per
-// K-tile, never vmcnt(0) inside the loop (cdna_hip_programming.md §5 "Pipelining across
-// barriers") -- the two-stage kernel above waits for the tile it just issued, one L2/HBM round
-// trip per 64 frames.  A is staged as BMT/128 column halves of the same 256-B-row image.
-template <int N>
-__device__ __forceinline__ void wait_vm_n(int ahead) {
-  // ahead = K-tiles allowed to stay in flight; N = glds per thread per K-tile
-  if (ahead >= 2) wait_vm<2 * N>();
-  else if (ahead == 1) wait_vm<N>();
-  else wait_vm<0>();
-}
-
-template <bool WINB, int BMT, int NST>
-__global__ void __launch_bounds__(BMT * 2, 1) gemm_tt2_kernel(GemmArgs g) {
-  constexpr int NW = BMT / 32, NT = NW * 64, NH = BMT / 128;
-  constexpr int A_BYTES = NH * TSTAGE_OP, STAGE = A_BYTES + TSTAGE_OP;
-  constexpr int LPT = (NH + 1) * (16 / NW);  // glds per thread per K-tile
-  constexpr int P = NST - 1;
-  static_assert(P <= 3, "at most 3 K-tiles in flight");
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
-  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-  const int nN = (g.N + 127) / 128, nM = (g.M + BMT - 1) / BMT;
-  const int z = lid / (nN * nM);
-  const int rem = lid - z * nN * nM;
-  const int mt = rem / nN, nt = rem - mt * nN;
-  const int m0 = mt * BMT, n0 = nt * 128;
-  const int bz = z / g.split_k, ks = z - bz * g.split_k;
-  const int kbeg = ks * g.klen;
-  const int kend = min(g.K, kbeg + g.klen);
-  const int nkt = kend > kbeg ? (kend - kbeg + FBK - 1) / FBK : 0;
-
-  TtLoader<false, NW> la[NH];
-#pragma unroll
-  for (int h = 0; h < NH; ++h) la[h].init(g.a, m0 + 128 * h, bz);
-  TtLoader<WINB, NW> lb;
-  lb.init(g.b, n0, bz);
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // wave (wm, wn): rows wm*64 .. +64 = half wm/2, column block (wm&1)*64 of that half
-  int ao0[4], ao1[4], bo0[4], bo1[4];
-  const int ahalf = (wm >> 1) * TSTAGE_OP;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) tr_offsets((wm & 1) * 8 + 2 * i, ao0[i], ao1[i]);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) tr_offsets(wn * 8 + 2 * j, bo0[j], bo1[j]);
-
-  auto issue = [&](int kt) {
-    char* st = smem_raw + (kt % NST) * STAGE;
-#pragma unroll
-    for (int h = 0; h < NH; ++h) la[h].issue(st + h * TSTAGE_OP, kbeg + kt * FBK, kend);
-    lb.issue(st + A_BYTES, kbeg + kt * FBK, kend);
-  };
-#pragma unroll
-  for (int p = 0; p < P; ++p)
-    if (p < nkt) issue(p);
-  for (int kt = 0; kt < nkt; ++kt) {
-    wait_vm_n<LPT>(min(P - 1, nkt - 1 - kt));
-    raw_barrier();
-    if (kt + P < nkt) issue(kt + P);
-    const char* As = smem_raw + (kt % NST) * STAGE + ahalf;
-    const char* Bs = smem_raw + (kt % NST) * STAGE + A_BYTES;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int ko = h * 32 * TROW;
-      bf16x8 af[4], bfr[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = tr_frag_asm(As + ko, ao0[i], ao1[i]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = tr_frag_asm(Bs + ko, bo0[j], bo1[j]);
-      tr_wait();
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-  }
-  // epilogue (weight gradients: plain store, accumulate, or split-K atomics)
-  const int rbase = m0 + wm * 64 + 4 * (lane >> 4), cbase = n0 + wn * 64 + (lane & 15);
-  float* C = g.c + (long long)bz * g.cbs;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = rbase + i * 16 + e;
-      if (row >= g.M) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = cbase + j * 16;
-        if (col >= g.N) continue;
-        float* cp = C + (long long)row * g.ldc + out_col(g, col);
-        const float v = acc[i][j][e];
-        if (g.atomic && !g.sk_ws) atomicAdd(cp, v);
-        else *cp = g.accumulate ? *cp + v : v;
-      }
-    }
-}
-
-template <bool WINB, int BMT, int NST>
-void launch2(const GemmArgs& g, hipStream_t s) {
-  const size_t lds = (size_t)NST * (BMT / 128 + 1) * TSTAGE_OP;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tt2_kernel<WINB, BMT, NST>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
-  const int nb = ((g.M + BMT - 1) / BMT) * ((g.N + 127) / 128) * g.batch * g.split_k;
-  gemm_tt2_kernel<WINB, BMT, NST><<<nb, BMT * 2, lds, s>>>(g);
-}
-
-// AVC_TT_CFG = "BMT,NST" selects the pipelined kernel (benchmarking); "0" keeps the two-stage one
-void tt_cfg(int& bmt, int& nst) {
-  static int cfg[2] = {-1, -1};
-  if (cfg[0] == -1) {
-    cfg[0] = 0;
-    cfg[1] = 0;
-    const char* e = getenv("AVC_TT_CFG");
-    if (e) sscanf(e, "%d,%d", &cfg[0], &cfg[1]);
-  }
-  bmt = cfg[0];
-  nst = cfg[1];
-}
-
 bool ok16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 // ------------------------------------------------------------------ halo form of the conv dW
@@ -591,9 +455,6 @@ float* gemm_splitk_ws(size_t bytes, hipStream_t s) {
 }
 
 bool gemm_tt_launch(const GemmArgs& g0, hipStream_t s) {
-  static const bool off = getenv("AVC_TT_DISABLE") != nullptr;
-  // AVC_TT_ABL=1 (timing diagnostic, wrong results): split-K partials stored instead of added
-  static const bool abl = getenv("AVC_TT_ABL") != nullptr;
   // AVC_TT_SPLITK=n: split-K reduced without atomics up to n splits (default 8); 0 = every split-K
   // product by atomics into the zeroed C (the pre-round-5 form)
   static const int fix_max = [] {
@@ -602,13 +463,12 @@ bool gemm_tt_launch(const GemmArgs& g0, hipStream_t s) {
   }();
   const bool fix_on = fix_max > 1;
   GemmArgs ga = g0;
-  if (abl) ga.atomic = false;
   const GemmArgs& g = ga;
   // the split-K reduction without atomics: `tiles` output tiles of `tile_bytes` each
   auto fixup = [&](int tiles, size_t tile_bytes) {
     // the last split's reduction takes ~one memory round trip per split: past SK_MAX splits the
     // atomics win (AVC_TT_SPLITK=n sets the bound; tools/tt_bench.py)
-    if (!fix_on || abl || g.split_k <= 1 || g.split_k > fix_max || g.batch != 1 || !g.c || g.bias || g.res ||
+    if (!fix_on || g.split_k <= 1 || g.split_k > fix_max || g.batch != 1 || !g.c || g.bias || g.res ||
         g.bn_partial || g.rbias)
       return;
     const size_t bytes = (size_t)tiles * g.split_k * tile_bytes;
@@ -620,36 +480,21 @@ bool gemm_tt_launch(const GemmArgs& g0, hipStream_t s) {
     ga.sk_cnt = c;
     ga.zero_c = 0;
   };
-  if (off || g.klen % FBK || g.M % 8 || g.N % 8) return false;
+  if (g.klen % FBK || g.M % 8 || g.N % 8) return false;
   for (const OpDev* o : {&g.a, &g.b})
     if (o->dtype != AVC_BF16 || !ok16(o->ptr) || o->ld % 8 || o->bstride % 8) return false;
   if (g.a.win) return false;
   if (g.b.win && g.b.chans % 8) return false;
-  // AVC_TT_HALO: 0 = off (window stream), 2 / 3 = LDS stages of the halo kernel
-  static const int halo = getenv("AVC_TT_HALO") ? atoi(getenv("AVC_TT_HALO")) : 2;
-  const bool halo_off = halo == 0;
   const OpDev& x = g.b;
-  if (!halo_off && x.win && x.taps == 5 && x.t_in == x.t_out && 2 * x.pad == x.taps - 1 && x.chans % 32 == 0 &&
+  if (x.win && x.taps == 5 && x.t_in == x.t_out && 2 * x.pad == x.taps - 1 && x.chans % 32 == 0 &&
       g.K % x.t_out == 0 && g.batch == 1 && g.N == x.taps * x.chans && !g.res && !g.c16 && !g.bias && !g.bn_partial) {
     fixup(((g.M + BM - 1) / BM) * (x.chans / 32), (size_t)BM * 32 * x.taps * 4);
     gemm_zero_c(ga, s);
-    if (halo == 2) launch_halo<2>(g, s);
-    else launch_halo<3>(g, s);
+    launch_halo<2>(g, s);  // two LDS stages (three measured no faster)
     return true;
   }
-  int bmt, nst;
-  tt_cfg(bmt, nst);
-  if (g.c16 || g.res || g.bias || g.bn_partial) bmt = 0;  // the pipelined kernel has the plain epilogue only
-  if (bmt == 0) fixup(((g.M + BM - 1) / BM) * ((g.N + 127) / 128), (size_t)BM * 128 * 4);
+  fixup(((g.M + BM - 1) / BM) * ((g.N + 127) / 128), (size_t)BM * 128 * 4);
   gemm_zero_c(ga, s);
-#define TT2_CASE(BMV, NSV)                               \
-  if (bmt == BMV && nst == NSV) {                        \
-    if (g.b.win) launch2<true, BMV, NSV>(g, s);          \
-    else launch2<false, BMV, NSV>(g, s);                 \
-    return true;                                         \
-  }
-  TT2_CASE(128, 2) TT2_CASE(128, 3) TT2_CASE(128, 4) TT2_CASE(256, 2) TT2_CASE(256, 3)
-#undef TT2_CASE
   const int nb = ((g.M + BM - 1) / BM) * ((g.N + 127) / 128) * g.batch * g.split_k;
   if (g.b.win) launch<true>(g, nb, s);
   else launch<false>(g, nb, s);

@@ -567,7 +567,6 @@ struct StepArgs {
   float* dg;           // bwd (B,T,dirs*4H)
   float* dcb;          // bwd [dirs][B][H]
   int B, T, H, dirs, s;
-  int dbg;  // diagnostic ablation bits (AVC_LSTM_DEBUG): 1 skip product, 2 skip stores
 };
 
 template <bool BF, int MT>
@@ -827,7 +826,7 @@ __global__ void __launch_bounds__(256) lstm_step_fwd_bf(StepArgs a) {
   f32x4 acc[MT][2];
 #pragma unroll
   for (int m = 0; m < MT; ++m) acc[m][0] = acc[m][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (a.s > 0 && !(a.dbg & 1)) {
+  if (a.s > 0) {
     const int r16 = lane & 15, ko = w * KW + 8 * (lane >> 4);
     const bf16* hp = reinterpret_cast<const bf16*>(a.hb) + ((long long)((a.s - 1) & 1) * a.dirs + d) * B * H;
     const bf16* W = reinterpret_cast<const bf16*>(a.w) + (long long)d * G * H;
@@ -861,7 +860,7 @@ __global__ void __launch_bounds__(256) lstm_step_fwd_bf(StepArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) red[w][m * 16 + 4 * (lane >> 4) + e][n * 16 + (lane & 15)] = acc[m][n][e];
   __syncthreads();
-  if (pv && !(a.dbg & 2)) {
+  if (pv) {
     float pre[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -997,7 +996,7 @@ struct PersistArgs {
   unsigned long long* trace;  // diagnostics (avc_lstm_trace), null in production
   unsigned* fault;            // process fault word (avc_set_fault_word), bit 0 on a spin timeout; nullable
   unsigned spin;              // spin bound per wait (PSPIN unless avc_lstm_set_spin / AVC_LSTM_SPIN)
-  int nap;                    // granule form: s_sleep(1)s between failed sweeps (AVC_LSTM_NAP)
+  int nap;                    // granule form: s_sleep(1)s between failed sweeps (0)
   int B, T, ng;
 };
 
@@ -1321,8 +1320,6 @@ struct PersistBwdArgs {
   unsigned spin;
   int nap;
   int B, T, ng;
-  int abl;  // diagnostic (AVC_LSTM_BWD_ABL=n): gather the group's payload 1 + n times per step -- the
-            // 128 KB per consumer a 16-utterance group would read
 };
 
 template <int H, bool GR>
@@ -1394,10 +1391,6 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
         __syncthreads();
         if (*quit) return;  // block-uniform exit after a spin timeout
         load_group<G, NCH, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
-        for (int k = 0; k < a.abl; ++k) {  // AVC_LSTM_BWD_ABL=n: n extra gathers (diagnostic)
-          __syncthreads();
-          load_group<G, NCH, PNT>(pay, ((s - 1) & 1) * B + b0, rows, As, AP);
-        }
         __syncthreads();
       }
       stamp(a.trace, T, s, 1);
@@ -1741,7 +1734,7 @@ struct Persist2BwdArgs {
   unsigned* fault;
   unsigned spin;
   int B, T, ng;
-  int opt;  // AVC_LSTM2_BWD_OPT bits (A/B): 1 = dG stores after a barrier behind the flag, 2 = no bf16 twin
+  int opt;  // bits: 1 = dG stores after a barrier behind the flag (the launch sets 1), 2 = no bf16 twin
 };
 
 constexpr int BKC = 1024, BNC = 4, BCP = BKC + 8, BNLW = 3;  // K-chunk, chunks, LDS pitch, W_hh0 frags in LDS
@@ -2027,23 +2020,8 @@ void set_bwd_lds_attr() {
 // payload is at most 16 KB -- the forward at H <= 512 (lstm1: 2.24 -> 1.74 us per step) --
 // and the flag form above that (H = 1024 forward 3.08 vs 3.26 us, backward 4.03 vs 4.43 us:
 // the doubled payload fetch costs more than the drain and the flag round trip it saves).
-// AVC_LSTM_GRAN overrides: bit 0 = forward, bit 1 = backward in the granule form.
-int gran_mask() {
-  static const int v = [] {
-    const char* e = getenv("AVC_LSTM_GRAN");
-    return e ? atoi(e) : -1;
-  }();
-  return v;
-}
-bool gran(bool bwd, int H) {
-  const int m = gran_mask();
-  if (m >= 0) return (m >> (bwd ? 1 : 0)) & 1;
-  return !bwd && (size_t)PRG * H * 4 <= 16384;
-}
-int nap() {
-  static const int v = getenv("AVC_LSTM_NAP") ? atoi(getenv("AVC_LSTM_NAP")) : 0;
-  return v;
-}
+bool gran(bool bwd, int H) { return !bwd && (size_t)PRG * H * 4 <= 16384; }
+int nap() { return 0; }  // s_sleep(1)s between the granule form's failed sweeps (none measured best)
 
 template <int H>
 const void* persist_fn(bool bwd) {
@@ -2240,24 +2218,16 @@ extern "C" int avc_lstm2_fwd(const float* xproj0, const void* w_hh0, const void*
   p.ng = ng;
   if (avc_zero_async(buf, px_ctl_bytes(ng), s)) return -1;
   // scheduling fence every 2 k-blocks of the product (without one the compiler hoists the A
-  // fragment reads and spills weight fragments).  AVC_LSTM2_CFG = LB*10 + OS (A/B): payload loads
-  // in LB batches (1 or 2); OS = 1 stores the previous tick's outputs under the payload loads
-  // instead of after the products
-  static const int cfg = getenv("AVC_LSTM2_CFG") ? atoi(getenv("AVC_LSTM2_CFG")) : 20;
+  // fragment reads and spills weight fragments); payload loads in 2 batches, the previous tick's
+  // outputs stored after the products (1 batch, or the stores under the payload loads: slower)
   const dim3 grid(ng * (H / QJU));
-  const size_t lds = persist2_lds<1024>();
-  switch (cfg) {
-    case 10: lstm2_persist_fwd<1024, 2, 1, false><<<grid, PNT, lds, s>>>(p); break;
-    case 11: lstm2_persist_fwd<1024, 2, 1, true><<<grid, PNT, lds, s>>>(p); break;
-    case 21: lstm2_persist_fwd<1024, 2, 2, true><<<grid, PNT, lds, s>>>(p); break;
-    default: lstm2_persist_fwd<1024, 2, 2, false><<<grid, PNT, lds, s>>>(p); break;
-  }
+  lstm2_persist_fwd<1024, 2, 2, false><<<grid, PNT, persist2_lds<1024>(), s>>>(p);
   return avc_check_launch("avc_lstm2_fwd");
 }
 
 // Two-layer wavefront backward (lstm2_persist_bwd): shape, compute mode and residency.
 bool persist2_bwd_path(int B, int H, bool bf) {
-  if (!bf || H != 1024 || no_persist_env() || getenv("AVC_LSTM2_OFF") || getenv("AVC_LSTM2_BWD_OFF")) return false;
+  if (!bf || H != 1024 || no_persist_env() || getenv("AVC_LSTM2_OFF")) return false;
   const int ng = (B + QRG - 1) / QRG, grid = ng * (H / QJU);
   if (grid > num_cus()) return false;
   static std::once_flag once[MAXDEV];
@@ -2312,8 +2282,8 @@ extern "C" int avc_lstm2_bwd(const float* dh1, const float* c0, const float* gat
   p.B = B;
   p.T = T;
   p.ng = ng;
-  static const int opt = getenv("AVC_LSTM2_BWD_OPT") ? atoi(getenv("AVC_LSTM2_BWD_OPT")) : 1;
-  p.opt = opt;
+  p.opt = 1;  // the dG stores behind a barrier after the flag (payload-as-output, bit 4: measured slower,
+              // profiles/r6_lstm2_bwd_payload_out.txt)
   if (avc_zero_async(buf, px_ctl_bytes(ng), s)) return -1;
   lstm2_persist_bwd<1024><<<dim3(ng * (H / QJU)), PNT, persist2_bwd_lds<1024>(), s>>>(p);
   return avc_check_launch("avc_lstm2_bwd");
@@ -2361,8 +2331,6 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
   AVC_CHECK_ARG(!bf || (wdtype == AVC_BF16 && hbuf), "avc_lstm_fwd: bf16 compute needs bf16 W_hh and hbuf");
   AVC_CHECK_ARG(bf || wdtype == AVC_F32, "avc_lstm_fwd: fp32 compute needs fp32 W_hh");
   StepArgs a = {};
-  static const int dbg = getenv("AVC_LSTM_DEBUG") ? atoi(getenv("AVC_LSTM_DEBUG")) : 0;
-  a.dbg = dbg;
   a.xproj = xproj;
   a.w = w_hh;
   a.hout = h;
@@ -2475,8 +2443,6 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
     p.B = B;
     p.T = T;
     p.ng = ng;
-    static const int abl = getenv("AVC_LSTM_BWD_ABL") ? atoi(getenv("AVC_LSTM_BWD_ABL")) : 0;
-    p.abl = abl;
     const bool gr = gran(true, H);
     if (avc_zero_async(gbuf, gr ? px_payload_off(ng) + (size_t)32 * B * H : px_ctl_bytes(ng), s)) return -1;
     // (persistent_path above set the dynamic-LDS attributes)

@@ -217,7 +217,8 @@ def tt_splitk_reduced(split_k):
     return 1 < split_k <= _TT_SPLITK_MAX
 
 
-_SPLIT_TARGET = int(os.environ.get("AVC_SPLIT_TARGET", "384") or 384)
+# workgroups a split-K product aims for (~1.5 per CU; re-measured with the in-kernel reduction in round 5)
+_SPLIT_TARGET = 384
 
 
 def auto_split_k(M, N, K, target=None, min_k=256, tiles=None):
@@ -1056,55 +1057,3 @@ def gelu_bwd_twin(g, x):
     d16 = _twin_buf(dx, None)
     L.call("avc_gelu_twin", g.data_ptr(), x.data_ptr(), dx.data_ptr(), _ptr(d16), x.numel(), 1, stream())
     return attach_twin(dx, d16)
-
-
-
-# ------------------------------------------------------------------------- segmented graph replay
-def capture_deps(stream_raw):
-    """Capture dependencies (graph node handles) of a capturing raw stream."""
-    import ctypes
-
-    arr = (ctypes.c_void_p * 256)()
-    n = L.lib().avc_capture_deps(ctypes.c_void_p(stream_raw), arr, 256)
-    if n < 0:
-        L.check(n, "avc_capture_deps")
-    return [arr[i] for i in range(n)]
-
-
-class GraphSplit:
-    """A captured step rebuilt as main-stream / side-stream graphs (graph.hip): the weight-gradient
-    branch replays beside the main chain instead of after it."""
-
-    FIELDS = ("main_nodes", "side_nodes", "cross_edges", "segments", "kernel_nodes", "memset_nodes",
-              "memcpy_nodes", "empty_nodes", "post_nodes", "record_nodes")
-
-    def __init__(self, raw_graph, main_tails, side_tails, max_segments=None, mode=None):
-        """mode 0 (default): up to max_segments main / side graph pairs ordered by events between
-        launches; mode 1: one main graph with event-record nodes, side segments behind waits on them
-        (profiles/r5_graph_modes.txt)."""
-        import ctypes
-
-        if max_segments is None:
-            max_segments = int(os.environ.get("AVC_GRAPH_SEGMENTS", "8"))
-        if mode is None:
-            mode = int(os.environ.get("AVC_GRAPH_MODE", "0"))
-        self.mode = mode
-        mt = (ctypes.c_void_p * len(main_tails))(*main_tails)
-        st = (ctypes.c_void_p * len(side_tails))(*side_tails)
-        h = ctypes.c_void_p()
-        counts = (ctypes.c_int * len(self.FIELDS))()
-        L.call("avc_graph_split", ctypes.c_void_p(raw_graph), mt, len(main_tails), st, len(side_tails),
-               int(max_segments), int(mode), ctypes.byref(h), counts)
-        self.handle = h
-        self.counts = dict(zip(self.FIELDS, tuple(counts)))
-
-    def launch(self, main_raw, side_raw):
-        L.call("avc_graph_launch2", self.handle, main_raw, side_raw)
-
-    def __del__(self):
-        if getattr(self, "handle", None):
-            try:
-                L.lib().avc_graph_split_destroy(self.handle)
-            except Exception:
-                pass
-            self.handle = None

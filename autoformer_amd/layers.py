@@ -21,17 +21,9 @@ from . import kernels as K
 from .kernels import operand
 
 _EPOCH = [0]
-_LAST_WGRAD_MAIN = os.environ.get("AVC_LAST_WGRAD_MAIN", "1") != "0"
-# diagnostics only (tools/ablate.sh): skip the side-stream weight-gradient GEMMs (wrong gradients)
+# diagnostics only (tools/contention_trace.py): skip the side-stream weight-gradient GEMMs (wrong
+# gradients; bench.py refuses it)
 _ABLATE_WGRAD = os.environ.get("AVC_ABLATE_WGRAD") == "1"
-# weight packs rebuilt by batched avc_pack_batch launches instead of one kernel per pack: fewer
-# launches, but measured +0.12 ms per C2 step (its few per-group events let the next forward
-# start later than the per-pack events do), so off unless asked for
-_PACK_BATCH = os.environ.get("AVC_PACK_BATCH", "0") == "1"
-_CONV_DW_DIRECT = os.environ.get("AVC_CONV_DW_DIRECT", "1") != "0"
-# conv dW split over the halo kernel's own 128 x 160 tiles (6 instead of 5 at 512 x 2560: 49.2 vs 50.7 us
-# isolated) -- in the C2 step no different (5.783 / 5.784 vs 5.782 / 5.762 ms, r5full4): off
-_HALO_SPLIT = os.environ.get("AVC_HALO_SPLIT", "0") != "0"
 
 # ---------------------------------------------------------------- gradient sink / side stream
 # In "sink" mode (set by TrainStep) parameter gradients are accumulated by the kernels
@@ -39,7 +31,7 @@ _HALO_SPLIT = os.environ.get("AVC_HALO_SPLIT", "0") != "0"
 # weight-gradient GEMMs (off the critical path of the backward) run on a side stream that
 # overlaps the latency-bound LSTM recurrences on the main stream.  The autograd functions
 # then return None for parameters.  join_side() must run before the gradients are read.
-_SINK = {"on": False, "side": None, "keep": []}
+_SINK = {"on": False, "side": None, "keep": [], "tail": False, "pend": {}}
 
 
 def set_grad_sink(on: bool) -> None:
@@ -48,7 +40,7 @@ def set_grad_sink(on: bool) -> None:
         _SINK["side"] = torch.cuda.Stream()
 
 
-# ---- cheap cross-stream ordering: raw HIP events on raw stream handles (graph.hip helpers) and
+# ---- cheap cross-stream ordering: raw HIP events on raw stream handles (events.hip) and
 # torch's current stream switched through its C bindings.  torch.cuda.Event() / .record() /
 # current_stream() / torch.cuda.stream() cost 10-15 us of Python each (measured ~1 ms per AutoVC
 # step at ~90 uses, tools/host_profile2.py); these cost a ctypes call.
@@ -171,70 +163,49 @@ class _Side:
         return False
 
 
-def main_wgrad_into(param, compute):
-    """The last layer's weight gradient, computed on the main stream (beside the side stream's
-    backlog) into a fresh tensor by compute(), then added into param.grad ON THE SIDE STREAM.  The
-    side stream may still be accumulating an earlier contribution into the same .grad -- the
-    encoder's first conv runs in the full pass and in the re-pass, and the re-pass's weight gradient
-    is a side-stream kernel -- and two read-modify-writes of one .grad on two streams lose updates
-    (round 6: the recorded C2 step's conv0 gradient 1.1e-3 off the eager one,
-    tests/test_gpu_replay.py).  The side stream is in order, so the add follows its own
-    accumulation; the step's join waits for it."""
-    tmp = compute()
-    with _Side() as sd:
-        sd.keep(tmp)
-        g = _grad_of(param)
-        K.add(g, tmp, out=g)
+def side_wrote(param) -> None:
+    """The side stream has just queued an accumulation into param.grad: remember where, so that a
+    later accumulation on the main stream (main_wgrad) waits for it."""
+    _SINK["pend"][id(param)] = ev_token(_SINK["side"].cuda_stream)
 
 
-# AVC_DEFER_LSTM2_WG (measured, off by default): the decoder lstm2 pair's four weight-gradient GEMMs
-# (4096 x 1024 x 8192 class) queued on the side stream only when the decoder lstm1 backward starts
-# ("1": beside that recurrence) or after it ("2": beside the encoder backward), instead of beside the
-# decoder conv stack's data-gradient convs that follow the lstm2 wavefront (those convs run 83-134 us
-# instead of ~40 beside them: profiles/r5_step_breakdown.txt, tools/timeline.py).  Both lose: C2
-# 5.89 / 6.10 vs 5.79-5.83 ms (the persistent lstm1 backward waits for CUs the GEMMs hold; mode 2
-# delays the decoder-slice Adam; profiles/r5_splitk_defer_ab.txt)
-_DEFER_MODE = os.environ.get("AVC_DEFER_LSTM2_WG", "0")
-_DEFER_LSTM2_WG = _DEFER_MODE != "0"
+def main_wgrad(param, last=False) -> bool:
+    """Whether this layer's weight gradient runs on the main stream, accumulating into param.grad
+    there: in the tail of the backward (set_tail: after the decoder's gradients, only the encoder's
+    full pass is left, and the main stream would otherwise wait for the side stream's backlog before
+    the optimizer step) when AVC_TAIL_WGRAD_MAIN is on.  The main stream first waits for the side
+    stream's last accumulation into the same .grad -- the encoder's convs run in the full pass and in
+    the re-pass, the re-pass's weight gradients are side-stream kernels, and two read-modify-writes of
+    one .grad on two unordered streams lose updates (round 6: a recorded C2 step's conv0 gradient had
+    been 1.1e-3 off the eager one, tests/test_gpu_replay.py).  That accumulation was queued long
+    before (the re-pass is the first part of the backward), so the wait costs nothing.  last: the
+    layer has no data gradient (the encoder's first conv, the last layer of every backward): on the
+    main stream in any case."""
+    if not (_SINK["on"] and (last or (_SINK["tail"] and _TAIL_WGRAD_MAIN))):
+        return False
+    tok = _SINK["pend"].pop(id(param), None)
+    if tok is not None:
+        wait_token(K.stream(), tok)
+    return True
 
 
-def defer_side(fn, *keep) -> None:
-    """Queue `fn` (weight-gradient launches) for the side stream at the next flush_deferred()."""
-    _SINK.setdefault("deferred", []).append((fn, keep))
+def set_tail(on: bool) -> None:
+    """From here to the next join_side() the backward is in its tail (see main_wgrad)."""
+    _SINK["tail"] = bool(on)
 
 
-def flush_deferred() -> None:
-    """Launch the deferred side-stream work now, after everything queued so far on this stream."""
-    pend = _SINK.get("deferred")
-    if not pend:
-        return
-    _SINK["deferred"] = []
-    with _Side() as sd:
-        for fn, keep in pend:
-            sd.keep(*keep)
-            fn()
+# the encoder's conv weight gradients in the tail of the backward on the main stream (round 6,
+# profiles/r6_tail_wgrad_main.txt); "0": on the side stream like every other weight gradient
+_TAIL_WGRAD_MAIN = os.environ.get("AVC_TAIL_WGRAD_MAIN", "1") != "0"
 
 
 def join_side() -> None:
-    flush_deferred()
+    _SINK["tail"] = False
+    _SINK["pend"].clear()
     side = _SINK["side"]
     if side is not None:
-        if _SINK.get("tails") == []:
-            # a capture that TrainStep splits into main / side graph segments (graph.hip): each
-            # stream's capture dependencies at the join
-            _SINK["tails"] = [K.capture_deps(K.stream()), K.capture_deps(side.cuda_stream)]
         stream_wait(K.stream(), ev_record(side.cuda_stream))
     _SINK["keep"].clear()
-
-
-def record_join_tails(on: bool):
-    """Arm (on) / take (off: returns [main tails, side tails] or None) the capture dependencies
-    that join_side() records while a graph capture is running."""
-    if on:
-        _SINK["tails"] = []
-        return None
-    t = _SINK.pop("tails", None)
-    return t if t else None
 
 
 def _grad_of(p):
@@ -346,7 +317,6 @@ _PACK_MAX_OPS = 128  # PACK_MAX_OPS of pack_batch_kernel (elem.hip)
 
 
 _BATCH = {}       # group index -> device op table of that group of packs
-_PACK_GROUP = 6   # caches per batched launch
 
 
 def _op_struct(o):
@@ -405,17 +375,17 @@ def _op_struct_type():
 
 
 def prefetch_packs() -> None:
-    """After the optimizer step: rebuild every weight pack of the plan on the side stream, in
-    the order the forward will ask for them.  The packs whose cache describes them (conv, LSTM,
-    linear: `PackCache.ops`) are rewritten IN PLACE by one batched launch (avc_pack_batch);
-    the others are rebuilt one by one (the encoder's first, so the forward's first wait is short)."""
+    """After the optimizer step: rebuild every weight pack of the plan on the side stream, one by one
+    in the order the forward will ask for them (the encoder's first, so the forward's first wait is
+    short), each behind its own event.  (Batched avc_pack_batch launches measured +0.12 ms per C2
+    step here: their few per-group events let the next forward start later; the recorded step
+    rewrites its frozen packs in place with them, repack_in_place.)"""
     side = _SINK["side"]
     if side is None or not _PLAN:
         return
     side_raw = side.cuda_stream
     stream_wait(side_raw, ev_record())
     with _OnStream(side), torch.no_grad():
-        batched = []
         for ref in list(_PLAN):
             c = ref()
             if c is None:
@@ -427,21 +397,8 @@ def prefetch_packs() -> None:
             key = _pack_key(c.params)
             if key == c.key:
                 continue
-            if _PACK_BATCH and c.ops is not None and c.val is not None and c.key is not None and c.key[1] == key[1]:
-                batched.append((c, key))
-                continue
             val = c.build()
             c.pending = (key, val, ev_token(side_raw))
-        # a few launches in first-use order, each with its own event: the next forward waits for
-        # the encoder's packs only, not for the whole batch
-        for gi in range(0, len(batched), _PACK_GROUP):
-            grp = batched[gi:gi + _PACK_GROUP]
-            plan = _batch_plan([c for c, _ in grp], gi)
-            K.L.call("avc_pack_batch", plan["ops"].data_ptr(), plan["prefix"].data_ptr(), plan["n"], plan["total"],
-                     K.stream())
-            ev = ev_token(side_raw)
-            for c, key in grp:
-                c.pending = (key, c.val, ev)
 
 
 def _need(t):
@@ -483,19 +440,12 @@ def conv_wgrad(dy, x, B, T_in, T_out, w, pad, into=None):
     M = B * T_out
     halo = Kw == 5 and 2 * pad == Kw - 1 and T_in == T_out and Ci % 32 == 0 and M % T_out == 0
     sk = K.auto_split_k(Co, Kw * Ci, M)
-    if halo and _HALO_SPLIT:
-        # the halo dW kernel's output tiles are 128 channels x (5 taps x 32 input channels): split over
-        # those when the partials are reduced in the kernel (512 x 2560: 64 tiles -> 6 splits, 49.2 vs
-        # 50.7 us at 5; tools/tt_bench.py)
-        sk_h = K.auto_split_k(Co, Kw * Ci, M, tiles=-(-Co // 128) * (Ci // 32))
-        if K.tt_splitk_reduced(sk_h):
-            sk = sk_h
     # the direct [Co][Ci][K] epilogue scatters its columns 4*Kw bytes apart: with split-K atomics
     # that is ~Kw x the atomic requests of the packed layout (measured +0.9 ms per C2 step), so
     # split products reduced by atomics go through the packed dWf and one unpack pass instead;
     # on the halo weight-gradient kernel (gemm_tt.hip: 5-tap 'same', Ci % 32 == 0) a product whose
     # partials the last split reduces (K.tt_splitk_reduced) stores the layout directly, 16-B runs
-    if not _CONV_DW_DIRECT or (sk > 1 and Kw > 1 and not (halo and K.tt_splitk_reduced(sk))):
+    if sk > 1 and Kw > 1 and not (halo and K.tt_splitk_reduced(sk)):
         dWf = torch.empty(Co, Kw * Ci, device=x.device)
         K.gemm(Co, Kw * Ci, M, operand(dy, Co, kstrided=True),
                operand(x, Ci, kstrided=True, window=(Kw, pad, T_out, T_in, Ci)), dWf, split_k=sk)
@@ -559,18 +509,13 @@ class ConvBNCore:
         a = None
         if bn.training:
             # batch statistics from the epilogue, finalized by the GEMM's last row tiles; the
-            # running statistics take stat_updates updates (the *_Adjust double pass).  A bf16-only
-            # activation without residual comes out of the same call (avc_bn_fin.apply_bf16: the halo
-            # conv applies BN + act in its epilogue behind a column-tile barrier)
+            # running statistics take stat_updates updates (the *_Adjust double pass)
             partial = K.bn_partial_buffer(M, Co, dev)
             nbt = bn.num_batches_tracked if bn.track_running_stats else None
             mom = bn.momentum if bn.momentum is not None else 0.1
-            fused = _BN_APPLY_FUSED and out_bf16 and bf and residual is None
-            a = torch.empty(M, Co, device=dev, dtype=torch.bfloat16) if fused else None
             stats = K.gemm(M, Co, Kdim, xop, wop, y, bias=conv.bias, bn_partial=partial,
                            bn_fin=(bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, mom, bn.eps,
-                                   self.stat_updates), row_bias=row_bias,
-                           **({"bn_apply": (a, self.act)} if fused else {}))
+                                   self.stat_updates), row_bias=row_bias)
         else:
             K.gemm(M, Co, Kdim, xop, wop, y, bias=conv.bias, row_bias=row_bias)
             stats = K.bn_eval(bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.eps)
@@ -645,17 +590,17 @@ class ConvBNCore:
                    **({"bnb_dy": prev_link.dy} if bnb is not None and prev_link.dy is not None else {}))
             if bnb is not None:
                 prev_link.dA_ptr = dx.data_ptr()
-        if sink and (n_dx or not _LAST_WGRAD_MAIN):
+        if sink and main_wgrad(conv.weight, last=not n_dx):
+            # the tail of the backward: on the main stream, right behind the data gradient
+            if not _ABLATE_WGRAD:
+                wgrad()
+            dW = dgamma = dbeta = dbias = None
+        elif sink:
             with _Side(ev) as sd:
                 sd.keep(dy, x)
                 if not _ABLATE_WGRAD:
                     wgrad()
-            dW = dgamma = dbeta = dbias = None
-        elif sink:
-            # no data gradient: this is the last layer of the backward (the encoder's first
-            # conv), after which the main stream would only wait for the side stream -- its
-            # weight gradient runs here, beside the side stream's remaining backlog
-            main_wgrad_into(conv.weight, lambda: conv_wgrad(dy, x, B, T_in, T_out, conv.weight, self.pad))
+                side_wrote(conv.weight)
             dW = dgamma = dbeta = dbias = None
         else:
             dW = wgrad()
@@ -692,7 +637,7 @@ class BnbLink:
             self.grads = (dg, db, dbi)
         self.coef = torch.empty(6 * C, device=dev)
         # the layer's dy (bf16) from the same GEMM (avc_bnb_args.dy_bf16; on the halo conv: its epilogue)
-        self.dy = torch.empty(M, C, device=dev, dtype=torch.bfloat16) if _BN_BWD_APPLY_FUSED else None
+        self.dy = None
         return (y, mean, rstd, bn.weight, bn.bias, core.act, self.coef, dg, db, dbi, int(sink))
 
 
@@ -715,14 +660,10 @@ def _links(ctx, x, core, a, saved, fuse_prev):
 # ring's ring_bnb_epilogue, aligned T only -- see _links): on since round 5 (C2 5.74 -> 5.67 ms,
 # profiles/r5_bnb_ab.txt); "0": the separate reduce / finalize passes
 _BNB_ON = os.environ.get("AVC_BNB", "1") != "0"
-# the BatchNorm apply passes in the same GEMM call (avc_bn_fin.apply_bf16 / avc_bnb_args.dy_bf16: on the
-# halo conv ring inside its epilogue behind a column-tile barrier, elsewhere a pass after the GEMM).
-# Measured slower in the C2 step (profiles/r5_bn_apply_fused_ab.txt: the barrier adds ~12 us per conv
-# against a 6 us apply pass; beside the side stream the waiting row tiles also hold their CUs), so off:
-# "1" both, "fwd" / "bwd" one side, "0" (default) the separate bn_apply / bn_bwd_apply calls
-_BN_APPLY_MODE = os.environ.get("AVC_BN_APPLY_FUSED", "0")
-_BN_APPLY_FUSED = _BN_APPLY_MODE in ("1", "fwd")
-_BN_BWD_APPLY_FUSED = _BN_APPLY_MODE in ("1", "bwd")
+# (round 5 also applied BN + act inside the halo conv's epilogue behind a column-tile barrier: slower in
+# the C2 step, ~12 us per conv against a 6 us apply pass, profiles/r5_bn_apply_fused_ab.txt; removed in
+# round 6.  avc_bn_fin.apply_bf16 / avc_bnb_args.dy_bf16 still ask one GEMM call for the apply outputs,
+# written by a pass after the GEMM.)
 
 
 class _ConvBNFn(torch.autograd.Function):
@@ -854,23 +795,26 @@ class _EncConv0FoldFn(torch.autograd.Function):
                    operand(emb, de, kstrided=True), dWe, ldc=Kw * de, batch=Kw, c_batch_stride=de)
             K.conv_grad_unpack_slice(dWe, Kw * de, de, gw, nm, de, accumulate=acc)
             return gw
-        if sink and (dmel is not None or demb is not None or not _LAST_WGRAD_MAIN):
+        if sink and main_wgrad(conv.weight, last=dmel is None and demb is None):
+            # the tail of the backward: on the main stream (see ConvBNCore.backward)
+            if not _ABLATE_WGRAD:
+                wgrad(_grad_of(conv.weight), True)
+            dW = dgamma = dbeta = dbias = None
+        elif sink:
             with _Side(ev) as sd:
                 sd.keep(dy, xm, Sdy, emb)
                 if not _ABLATE_WGRAD:
                     wgrad(_grad_of(conv.weight), True)
-            dW = dgamma = dbeta = dbias = None
-        elif sink:
-            # the last layer of the backward: on the main stream (see ConvBNCore.backward)
-            main_wgrad_into(conv.weight, lambda: wgrad(torch.empty_like(conv.weight), False))
+                side_wrote(conv.weight)
             dW = dgamma = dbeta = dbias = None
         else:
             dW = wgrad(torch.empty_like(conv.weight), False)
         return dmel, demb, None, None, None, None, dW, dbias, dgamma, dbeta
 
 
-# the speaker-half fold of the encoder's first conv (AVC_CONV0_FOLD=0: the concat form, A/B)
-_FOLD = os.environ.get("AVC_CONV0_FOLD", "1") == "1"
+# the speaker-half fold of the encoder's first conv (AVC_FOLD=0: the concat forms of conv0 and of the
+# decoder's lstm1 input, A/B and parity diagnostics)
+_FOLD = os.environ.get("AVC_FOLD", "1") != "0"
 
 
 def enc_conv0(core, mel2d, emb, B, T, out_bf16=False):
@@ -962,11 +906,10 @@ class LSTMLayerCore:
         h, c, g = K.lstm_fwd(xproj, whh, B, T, H, dirs, hbuf)
         return h, (c, g)
 
-    def backward(self, dh, x, h, saved, B, T, need_dx, dg=None, defer=False, dbp=None):
+    def backward(self, dh, x, h, saved, B, T, need_dx, dg=None, dbp=None):
         """dg: the gate gradients when a fused launch already produced them (the lstm2 wavefront:
         bf16 only when it also gave dbp, the (groups, 4H) partial sums of dg whose column sums are
-        the bias gradients).  defer: the weight gradients go to the side stream at the next
-        flush_deferred()."""
+        the bias gradients)."""
         c, g = saved
         H, dirs = self.H, self.dirs
         In = x.shape[1]
@@ -1013,10 +956,7 @@ class LSTMLayerCore:
         if need_dx:
             dx = torch.empty(M, In, device=x.device, dtype=x.dtype)  # bf16 for a bf16-stored input
             K.gemm(M, In, G, operand(dg, G), operand(wih_t, G), dx)
-        if sink and defer and not _ABLATE_WGRAD:
-            defer_side(wgrads, dg, x, h, dg_op, h_op, dbp)
-            grads = [None] * (4 * dirs)
-        elif sink:
+        if sink:
             with _Side(ev) as sd:
                 sd.keep(dg, x, h, dg_op, h_op, dbp)
                 if not _ABLATE_WGRAD:
@@ -1087,16 +1027,13 @@ class _LSTMPairFn(torch.autograd.Function):
             (cs0, gs0), (cs1, gs1) = ctx.saved
             wt0 = c0.packs()[3]
             _, _, _, wt1, wti1 = c1.packs()
-            if _PAIR_DB:  # bf16 dG only, the bias gradients from the kernel's per-group partials
-                dg0, dg1, dbp = K.lstm2_bwd(dh1.contiguous(), cs0, gs0, cs1, gs1, wt0, wti1, wt1, B, T, H,
-                                            fp32=False, db=True)
-                dbp0, dbp1 = dbp[0], dbp[1]
-            else:
-                dg0, dg1 = K.lstm2_bwd(dh1.contiguous(), cs0, gs0, cs1, gs1, wt0, wti1, wt1, B, T, H)
-                dbp0 = dbp1 = None
-            _, g1 = c1.backward(None, h0, h1, ctx.saved[1], B, T, False, dg=dg1, defer=_DEFER_LSTM2_WG, dbp=dbp1)
-            dx, g0 = c0.backward(None, x, h0, ctx.saved[0], B, T, ctx.needs_input_grad[0], dg=dg0,
-                                 defer=_DEFER_LSTM2_WG, dbp=dbp0)
+            # bf16 dG only (the GEMM operands), the bias gradients from the kernel's per-group partials
+            # (ABI 28; the fp32-dG form of the same kernel is held against it in test_gpu_lstm2_bwd.py)
+            dg0, dg1, dbp = K.lstm2_bwd(dh1.contiguous(), cs0, gs0, cs1, gs1, wt0, wti1, wt1, B, T, H,
+                                        fp32=False, db=True)
+            dbp0, dbp1 = dbp[0], dbp[1]
+            _, g1 = c1.backward(None, h0, h1, ctx.saved[1], B, T, False, dg=dg1, dbp=dbp1)
+            dx, g0 = c0.backward(None, x, h0, ctx.saved[0], B, T, ctx.needs_input_grad[0], dg=dg0, dbp=dbp0)
             return (dx, None, None, None, None, *g0, *g1)
         dh0, g1 = c1.backward(dh1.contiguous(), h0, h1, ctx.saved[1], B, T, True)
         dx, g0 = c0.backward(dh0, x, h0, ctx.saved[0], B, T, ctx.needs_input_grad[0])
@@ -1107,9 +1044,6 @@ _PAIR_OFF = bool(os.environ.get("AVC_LSTM2_OFF"))
 # the pair's backward as one wavefront launch (avc_lstm2_bwd; C2 5.83 -> 5.81 ms, isolated 1127 -> ~1050 us,
 # profiles/r5_lstm2_bwd_wavefront.txt); "0": two single-layer launches + the dX1 GEMM
 _PAIR_BWD = os.environ.get("AVC_LSTM2_BWD", "1") != "0"
-# the wavefront backward writes bf16 dG only (its GEMM operands) plus per-group bias-gradient partials,
-# instead of fp32 dG + bf16 twin and a column-sum pass over the fp32 dG (ABI 28); "0": the fp32 form
-_PAIR_DB = os.environ.get("AVC_LSTM2_DB", "1") != "0"
 
 
 def lstm(mod, cores, x, B, T):
@@ -1167,10 +1101,7 @@ class _LSTM1FoldFn(torch.autograd.Function):
         In = cd + de
         _, _, whh, whh_t, wih_t = core.packs()
         dev = h.device
-        if _DEFER_MODE != "2":
-            flush_deferred()  # the lstm2 weight gradients: beside this recurrence (AVC_DEFER_LSTM2_WG)
         dg = K.lstm_bwd(dh.contiguous(), h, c, g, whh if H <= 64 else None, whh_t, B, T, H, 1)
-        flush_deferred()  # mode 2: after it, beside the encoder backward
         M = B * T
         c2 = codes.reshape(B * nc, cd)
         s_code = K.segsum(dg, B * nc, T // nc, G, ld=G)  # (B*nc, G): dG summed over each code's frames

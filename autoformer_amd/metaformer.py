@@ -14,7 +14,6 @@ References:
 from __future__ import annotations
 
 import contextlib
-import os
 
 import torch
 
@@ -25,8 +24,7 @@ from .kernels import operand
 
 # gradient-sink mode: the mixer's weight-gradient products (both operands K-strided, compute-bound)
 # run on the side stream beside the memory-bound data-gradient chain (LayerNorm, GELU, transposes,
-# pads) instead of in line with it (AVC_MIX_SIDE=0: in line, A/B)
-_MIX_SIDE = os.environ.get("AVC_MIX_SIDE", "1") != "0"
+# pads) instead of in line with it (profiles/r3_metaconv_mixer_ab.txt)
 
 
 def _wside(on, *keep):
@@ -406,7 +404,7 @@ class _MLPMixerFn(torch.autograd.Function):
         # zero-padded products) and the function returns None for the parameters -- no autograd
         # accumulation pass per parameter
         sink = Lyr.sink_on()
-        side = sink and _MIX_SIDE and Lyr.side_stream() is not None
+        side = sink and Lyr.side_stream() is not None
         dout16 = K.twin(dout)
         with _wside(side, dout, dout16, Z2T, wp):
             if NPp != NP:

@@ -16,7 +16,6 @@ backward, Adam(lr = 1e-4, betas (0.9, 0.999), eps 1e-8).
 """
 from __future__ import annotations
 
-import contextlib
 import datetime
 import importlib
 import os
@@ -27,8 +26,9 @@ import torch
 from . import dist as D
 from . import kernels as K
 from .replay import collective
-from .layers import (ev_record, flush_deferred, freeze_packs, join_side, on_stream, plan_caches, prefetch_packs,
-                     record_join_tails, repack_in_place, set_grad_sink, side_stream, stream_wait, weights_changed)
+from .layers import (ev_record, freeze_packs, join_side, on_stream, plan_caches, prefetch_packs,
+                     repack_in_place, set_grad_sink, set_tail, side_stream, stream_wait,
+                     weights_changed)
 
 
 def _load_state(model, path, device):
@@ -226,15 +226,16 @@ class FusedAdam:
 
 # ------------------------------------------------------------------------- bench step
 # workgroup cap of the decoder-slice Adam that runs beside the encoder backward (0 = full grid;
-# 256 measured best: the full 4096-block grid slowed the latency-bound BiLSTM backward beside it)
-_SIDE_ADAM_BLOCKS = int(os.environ.get("AVC_SIDE_ADAM_BLOCKS", "256"))
+# 256 measured best: the full grid slowed the latency-bound BiLSTM backward beside it, 64 / 24 let
+# the step's tail wait for it, profiles/r5_replay_ab.txt)
+_SIDE_ADAM_BLOCKS = 256
 
 
 class TrainStep:
-    """One train.py step over the HIP model with flat buffers, optional DP and graph capture.
+    """One train.py step over the HIP model with flat buffers, optional DP and a recorded replay.
 
-    With world > 1 the gradients are averaged by RCCL between backward and Adam; the
-    whole step minus the collective is captured in hipGraphs once `capture()` is called."""
+    With world > 1 the gradients are averaged by RCCL between backward and Adam; after
+    `record()` every step replays the recorded native calls (replay.py), the collectives included."""
 
     def __init__(self, model, lr=1e-4, lambda_cd=1.0, extra=None, extra_modules=()):
         self.model = model
@@ -250,10 +251,6 @@ class TrainStep:
         D.broadcast_(self.flat)
         set_grad_sink(True)  # kernels accumulate straight into the flat gradient buffer
         self.opt = FusedAdam(self.flat, self.gflat, lr)
-        self.graph_fb = None
-        self.graph_f = None  # forward-only graph (capture(forward_only=True)); the backward stays eager
-        self.graph_split = None  # the captured step as main / side graph segments (capture(split=True))
-        self._graph_adam = False  # the optimizer step is inside the captured graph (world 1)
         self.world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
         self.loss = None
         # The decoder / postnet (/ discriminator) gradients are final once the backward reaches
@@ -270,9 +267,8 @@ class TrainStep:
             self.comm = torch.cuda.Stream()
         self._early = None
         self._early_adam = False
-        self._capturing = False
-        self._recording = False  # record(): the decoder slice's Adam stays on the comm stream (eager form)
-        self._pack_groups = None  # (encoder-slice caches, decoder-slice caches) of a captured step
+        self._recording = False  # inside record(): the decoder's weight packs are rewritten in place
+        self._pack_groups = None  # (encoder-slice caches, decoder-slice caches) of a recorded step
         # fault word (kernels.fault_word): read back asynchronously after every step into a
         # pinned word and checked at the next step, so a failed persistent recurrence raises
         # within one step without a host sync; check() is the synchronous form
@@ -281,7 +277,6 @@ class TrainStep:
         self._fault_ev = None
         self._one = torch.ones((), device=self.flat.device)
         self.recorded = None  # replay.StepRecord of record(): step() replays it
-        self._rstream = None
         # optional exposed all-reduce time: a list of (start, end) HIP event pairs recorded on
         # the main stream around its wait for the collective (bench.py's allreduce_ms)
         self.comm_timing = None
@@ -299,18 +294,7 @@ class TrainStep:
         K.raise_on_fault(self._fault.item())
 
     def _decoder_done(self):
-        flush_deferred()  # every decoder weight gradient is queued before its Adam slice waits for them
-        if self._capturing and not self._recording:
-            # captured step (world 1): the decoder-slice Adam and the in-place repack of the decoder's
-            # weight packs run on the weight-gradient stream, after the decoder's weight gradients
-            # queued there and beside the encoder backward
-            side = side_stream()
-            stream_wait(side.cuda_stream, ev_record())
-            with on_stream(side):
-                self.opt.step_slice(self.split, self.flat.numel(), advance=True, max_blocks=_SIDE_ADAM_BLOCKS)
-                repack_in_place(self._pack_groups[1], "graph_dec")
-            self._early_adam = True
-            return
+        set_tail(True)  # the rest of the backward is the encoder's full pass (layers.main_wgrad)
         comm = self.comm.cuda_stream
         stream_wait(comm, ev_record())
         side = side_stream()
@@ -350,7 +334,7 @@ class TrainStep:
         if timed:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        if not self._early_adam:  # no overlapped part (graph replay, or no hook fired)
+        if not self._early_adam:  # no overlapped part (no decoder hook fired)
             if self.world > 1:
                 D.allreduce_mean_(self.gflat)
             if timed:
@@ -383,54 +367,12 @@ class TrainStep:
                 self._rx.copy_(x)
             if emb is not self._re:
                 self._re.copy_(emb)
-            if self._rstream is not None:
-                rs = self._rstream.cuda_stream
-                stream_wait(rs, ev_record())
-                self.recorded.replay()
-                stream_wait(K.stream(), ev_record(rs))
-            else:
-                self.recorded.replay()
+            self.recorded.replay()
             self._probe_fault()
             return self.loss
-        if self.graph_split is not None:
-            # host-free step: the main chain and the weight-gradient branch replay as graph
-            # segments on their own streams (graph.hip); with world 1 the Adam step and the
-            # in-place weight repack are in the graph
-            self.graph_split.launch(K.stream(), side_stream().cuda_stream)
-            loss = self.loss
-            if not self._graph_adam:
-                self._finish()  # gradient average over ranks + Adam
-                repack_in_place(self._pack_groups[0] + self._pack_groups[1], "graph_all")
-            self._probe_fault()
-            return loss
-        if self.graph_fb is not None:
-            self.graph_fb.replay()
-            loss = self.loss
-        elif self.graph_f is not None:
-            # the captured forward replays into its static activations; the eager backward walks
-            # the autograd graph recorded at capture (retained) over those same tensors
-            # the forward reads the capture-time inputs: a new batch is copied into them through
-            # .data (the retained autograd graph saved them; a tracked in-place copy would bump their
-            # version and the backward would refuse them)
-            if x is not self._gx:
-                self._gx.data.copy_(x)
-            if emb is not self._ge:
-                self._ge.data.copy_(emb)
-            self.gflat.zero_()
-            # the replay does not ask PackCache.get for its packs (it rebuilds its own), so it would
-            # not wait for the previous step's side-stream prefetch: order it explicitly
-            side = side_stream()
-            if side is not None:
-                stream_wait(K.stream(), ev_record(side.cuda_stream))
-            self.graph_f.replay()
-            self.loss.backward(retain_graph=True)
-            join_side()
-            loss = self.loss
-        else:
-            loss = self._fwd_bwd(x, emb, overlap=self.split is not None)
+        loss = self._fwd_bwd(x, emb, overlap=self.split is not None)
         self._finish()
-        if self.graph_fb is None:
-            prefetch_packs()  # next step's weight packs (the backward's, with a forward graph), on the side stream
+        prefetch_packs()  # next step's weight packs, on the side stream
         self._probe_fault()
         return loss
 
@@ -450,22 +392,21 @@ class TrainStep:
             repack_in_place(caches, grp)  # eager: builds the op tables (and the current packs)
 
     def _recordable_tail(self):
-        """The optimizer step + in-place weight repack that end a captured / recorded step (with the
-        gradient average over ranks first when world > 1: recorded steps only)."""
-        if self._early_adam:
-            if self._recording:  # the decoder slice's average + Adam + repack ran on the comm stream
-                comm = self.comm.cuda_stream
-                if self.world > 1:
-                    box = self._comm_timing_mark(None)
-                    stream_wait(comm, ev_record())
-                    g = self.gflat[:self.split]
-                    with on_stream(self.comm):
-                        collective(lambda: D.finish_allreduce_(D.allreduce_mean_async_(g)))
-                    K.collective_enqueued("encoder-slice all-reduce")
-                stream_wait(K.stream(), ev_record(comm))
-                K.collective_joined()
-                if self.world > 1:
-                    self._comm_timing_mark(box)
+        """The optimizer step + in-place weight repack that end a recorded step (with the gradient
+        average over ranks first when world > 1)."""
+        if self._early_adam:  # the decoder slice's average + Adam + repack ran on the comm stream
+            comm = self.comm.cuda_stream
+            if self.world > 1:
+                box = self._comm_timing_mark(None)
+                stream_wait(comm, ev_record())
+                g = self.gflat[:self.split]
+                with on_stream(self.comm):
+                    collective(lambda: D.finish_allreduce_(D.allreduce_mean_async_(g)))
+                K.collective_enqueued("encoder-slice all-reduce")
+            stream_wait(K.stream(), ev_record(comm))
+            K.collective_joined()
+            if self.world > 1:
+                self._comm_timing_mark(box)
             self.opt.step_slice(0, self.split, advance=False)
             repack_in_place(self._pack_groups[0], "graph_enc")
         else:
@@ -518,107 +459,23 @@ class TrainStep:
         self._freeze_pack_groups()
         torch.cuda.synchronize()
         freeze_packs(True)
-        # AVC_REC_EARLY=0: no decoder-slice Adam beside the encoder backward (one Adam at the end)
-        self._capturing = self._recording = self.split is not None and os.environ.get("AVC_REC_EARLY", "1") != "0"
+        # the decoder slice's Adam beside the encoder backward (comm stream), as in the eager step
+        # (a high-priority stream for the recorded main chain and a single Adam after the backward
+        # measured no better: profiles/r5_replay_ab.txt)
+        self._recording = self.split is not None
         rec = R.StepRecord()
-        # AVC_REC_PRIO=1: the recorded main chain runs on a high-priority stream (the dispatcher hands
-        # freed CUs to its workgroups before the weight-gradient / optimizer streams')
-        self._rstream = torch.cuda.Stream(priority=-1) if os.environ.get("AVC_REC_PRIO", "0") != "0" else None
         try:
-            with R.recording(rec), contextlib.ExitStack() as es:
-                if self._rstream is not None:
-                    stream_wait(self._rstream.cuda_stream, ev_record())
-                    es.enter_context(on_stream(self._rstream))
-                self.loss = self._fwd_bwd(x, emb, overlap=self._capturing)
+            with R.recording(rec):
+                self.loss = self._fwd_bwd(x, emb, overlap=self._recording)
                 self._recordable_tail()
-            if self._rstream is not None:
-                stream_wait(K.stream(), ev_record(self._rstream.cuda_stream))
         finally:
-            self._capturing = self._recording = False
+            self._recording = False
             self._early_adam = False
             freeze_packs(False)
         weights_changed()
         self._probe_fault()
         self.recorded, self._rx, self._re = rec, x, emb
         return rec
-
-    def capture(self, x, emb, warmup=2, forward_only=False, split=None):
-        """Capture zero_grad + forward + re-pass + losses + backward into one hipGraph
-        (x, emb must stay the same tensors: the synthetic batch is resident in HBM).
-        split (default: on whenever the weight-gradient side stream exists): the captured graph is
-        rebuilt as main-stream / side-stream graph segments that replay concurrently (graph.hip,
-        avc_graph_split), so the weight-gradient branch overlaps the main chain as in the eager
-        step; with world 1 the Adam step is captured too (after the join), so a step is one
-        native call.
-        forward_only: capture the forward + re-pass + losses only and keep their autograd graph;
-        every step replays the forward (no host work for its ~half of the step's launches) and
-        runs the backward eagerly over the retained graph, so the weight-gradient side stream
-        still overlaps the data-gradient chain (one graph replays it serially)."""
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(warmup):
-                self._fwd_bwd(x, emb)
-                if self.world > 1:
-                    D.allreduce_mean_(self.gflat)
-                self.opt.step()
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        weights_changed()  # the captured forward must contain the weight repacks
-        # split=False keeps ONE graph: the runtime executes it in one queue, so the weight-gradient
-        # branch captured from the side stream runs after the main chain instead of beside it
-        g = torch.cuda.CUDAGraph()
-        if forward_only:
-            # the decoder hook (early decoder-slice Adam) is registered on the captured tensors and
-            # fires in every eager backward
-            self.model._decoder_bwd_done = self._decoder_done if self.split is not None else None
-            try:
-                with torch.cuda.graph(g):
-                    loss, _, x_psnt = self.loss_fn(self.model, x, emb, self.lambda_cd)
-                    if self.extra is not None:
-                        loss = loss + self.extra(x, emb, x_psnt)
-            finally:
-                self.model._decoder_bwd_done = None
-            self.loss = loss
-            self.graph_f = g
-            self._gx, self._ge = x, emb
-            return
-        if split is None:
-            split = side_stream() is not None and os.environ.get("AVC_GRAPH_SPLIT", "1") != "0"
-        if split:
-            # Weight packs: the captured forward reads the pack buffers as they are (freeze_packs) and
-            # the graph rewrites them in place after its Adam step (repack_in_place: the decoder's
-            # on the side stream right after the decoder-slice Adam, the encoder's after the join),
-            # so a replay runs no per-pack kernels on the main chain.  Bring them up to date first.
-            self._freeze_pack_groups()
-            torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph(keep_graph=True)
-            record_join_tails(True)
-            freeze_packs(True)
-            adam = self.world == 1
-            overlap = adam and self.split is not None
-            self._capturing = overlap
-            try:
-                with torch.cuda.graph(g):
-                    self.loss = self._fwd_bwd(x, emb, overlap=overlap)
-                    if adam:
-                        self._recordable_tail()
-            finally:
-                self._capturing = False
-                self._early_adam = False
-                freeze_packs(False)
-                tails = record_join_tails(False)
-            weights_changed()  # eager steps after this rebuild the packs that are not rewritten in place
-            if not tails or not all(tails):
-                raise RuntimeError("TrainStep.capture: the step recorded no main / side join to split at")
-            self._tails = tails  # (tools/graph_split_probe.py re-splits the same capture)
-            self.graph_split = K.GraphSplit(g.raw_cuda_graph(), tails[0], tails[1])
-            self._graph_adam = adam
-            self.graph_fb = g  # keeps the captured graph and its memory pool alive
-            return
-        with torch.cuda.graph(g):
-            self.loss = self._fwd_bwd(x, emb)
-        self.graph_fb = g  # capture only records: the next step() replays it
 
 
 # ------------------------------------------------------------------------- reference-shaped solvers

@@ -289,13 +289,6 @@ def main():
     ap.add_argument("--disc", action="store_true",
                     help="AutoVC + Discriminator two-model step (train_with_discriminator.py), T=176")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--graph", action="store_true",
-                    help="replay the captured step as main / side graph segments (graph.hip): the whole step "
-                         "(fwd + re-pass + losses + bwd + Adam + weight repack) without host work per kernel")
-    ap.add_argument("--graph-one", action="store_true",
-                    help="replay the fwd+bwd as ONE hipGraph (the runtime serialises the side-stream branch)")
-    ap.add_argument("--graph-fwd", action="store_true",
-                    help="replay the forward + losses as a hipGraph, backward eager over the retained autograd graph")
     ap.add_argument("--replay", action="store_true",
                     help="record one step's native calls and replay them (autoformer_amd/replay.py): the eager "
                          "step's kernels, streams and event edges without its Python -- the default")
@@ -307,7 +300,7 @@ def main():
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     # diagnostic ablations skip work inside the step: a number measured under them is not the metric
-    skipped = [k for k in ("AVC_ABLATE_WGRAD", "AVC_LSTM_DEBUG", "AVC_LSTM_BWD_ABL") if os.environ.get(k, "0") not in ("", "0")]
+    skipped = [k for k in ("AVC_ABLATE_WGRAD",) if os.environ.get(k, "0") not in ("", "0")]
     if skipped:
         raise SystemExit(f"bench.py: diagnostic ablation(s) {skipped} set; they skip work in the timed step")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -358,19 +351,15 @@ def main():
     else:
         trainer = TrainStep(model, lr=1e-4)
 
-    graph = args.graph or args.graph_fwd or args.graph_one
     # the recorded replay (replay.py) is the default step form of the AutoVC steps: the same kernels,
     # streams and event edges as the eager step, with no per-kernel Python, so a slow host does not
     # set the step time.  The MetaConv / MetaPool steps (~29 ms) are never host-bound and ran ~1 %
     # faster eager (29.13-29.23 vs 29.52-29.54 ms, profiles/r5_replay_ab.txt): eager unless --replay
     host_bound = args.model not in ("MetaConv", "MetaPool")
-    replay = not (args.eager or graph) and trainer.replayable() and (args.replay or host_bound)
+    replay = not args.eager and (args.replay or host_bound)
     for _ in range(args.warmup):
         trainer.step(x, e)
-    if graph:
-        trainer.capture(x, e, forward_only=args.graph_fwd, split=False if args.graph_one else None)
-        trainer.step(x, e)
-    elif replay:
+    if replay:
         trainer.record(x, e, warmup=0)
         trainer.step(x, e)
     torch.cuda.synchronize()
@@ -423,9 +412,7 @@ def main():
            "config": {"workload": f"{name} {step}, B={B}/GPU, T={T}, freq={freq}, dim_neck=44, dim_emb=256, "
                                   f"dim_pre=512",
                       "global_batch": B * world, "seq_len": T, "freq": freq, "parallelism": f"dp{world}",
-                      "graph": ("split" if args.graph else "one" if args.graph_one else
-                                "fwd" if args.graph_fwd else False),
-                      "launch": "replay" if replay else "graph" if graph else "eager"},
+                      "launch": "replay" if replay else "eager"},
            "step_mfma_frac": round(value * fpf / (world * peak * 1e12), 5) if fpf else None,
            "final_loss": loss_v}
     if world > 1:

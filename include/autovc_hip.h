@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 29
+#define AVC_ABI_VERSION 30
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -572,34 +572,14 @@ int avc_mg_wn_pack(const float* v, const float* g, const float* bias, int d0, in
 int avc_mg_conv_out(const float* x, int B, int L, int C, int taps, const float* w, const float* bias, float slope,
                     float* out, void* stream);
 
-/* Host-side event helpers (graph.hip): one reusable event (hipEventDisableTiming), recorded on a
- * raw stream handle, and a stream made to wait for the record current at the time of the call --
- * the step's cross-stream ordering (weight-gradient side stream, pack prefetch) without
- * torch.cuda.Event / current_stream() Python costs.  Work inside a stream capture as well. */
+/* Host-side event helpers (events.hip): one reusable event (no timing, no system-scope fence),
+ * recorded on a raw stream handle, and a stream made to wait for the record current at the time of
+ * the call -- the step's cross-stream ordering (weight-gradient side stream, comm stream, pack
+ * prefetch) without torch.cuda.Event / current_stream() Python costs.  (ABI 30: the hipGraph split
+ * entry points of ABI <= 29 are gone; the recorded replay replaced them.) */
 int avc_event_create(void** out);
 int avc_event_record(void* ev, void* stream);
 int avc_stream_wait_event(void* stream, void* ev);
-
-/* The captured training step (TrainStep.capture of train.py:82-99) replayed as main-stream and
- * side-stream graphs (graph.hip): the HIP runtime executes one graph in one queue, which serialises
- * the weight-gradient branch.
- * avc_capture_deps: the capture dependencies (graph node handles) of a capturing stream, at most
- *   max_out; returns their count (negative on error).
- * avc_graph_split: rebuilds `graph` (a hipGraph_t captured over the main stream with the side
- *   stream forked from it and joined at the end) from the two streams' tails at the join, plus one
- *   graph of the main-stream nodes captured after the join (the optimizer step).  mode 0: <=
- *   max_segments main / side graph pairs ordered by events between launches; mode 1: one main graph
- *   with event-record nodes, side segments behind host-side waits on them.  *handle for
- *   avc_graph_launch2.  counts[AVC_GRAPH_COUNTS] (optional): main nodes before the join, side
- *   nodes, main -> side edges, segments, kernel, memset (rebuilt as kernels), memcpy and empty
- *   nodes, main nodes after the join, event-record nodes.
- * avc_graph_launch2: one replay on (main, side); the main stream waits for the side at the end. */
-#define AVC_GRAPH_COUNTS 10
-int avc_capture_deps(void* stream, void** out, int max_out);
-int avc_graph_split(void* graph, void* const* main_tails, int n_main, void* const* side_tails, int n_side,
-                    int max_segments, int mode, void** handle, int* counts);
-int avc_graph_launch2(void* handle, void* main_stream, void* side_stream);
-int avc_graph_split_destroy(void* handle);
 
 
 #ifdef __cplusplus

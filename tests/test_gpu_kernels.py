@@ -894,62 +894,6 @@ def test_conv_chain_fused_bn_backward_matches_separate(T):
         assert relf(p, q) < 2e-3 or float((p - q).abs().max()) < 1e-4, relf(p, q)
 
 
-@pytest.mark.parametrize("B,T", [(64, 128), (64, 176), (8, 64)])
-def test_conv_chain_fused_bn_apply_matches_separate(B, T):
-    """The BatchNorm apply passes inside the conv GEMM calls (avc_bn_fin.apply_bf16 forward,
-    avc_bnb_args.dy_bf16 backward): on the halo conv ring (T = 128: 128-row tiles; T = 176: the
-    one-utterance tile) the epilogue applies BN + act / the BN backward behind a column-tile barrier,
-    at T = 64 (gemm_conv) the library runs the apply pass after the GEMM.  Outputs and every gradient
-    must equal the separate-apply run bit for bit (deterministic mode: no split-K atomics)."""
-    import autoformer_amd as A
-    from autoformer_amd import layers as Ly
-    from autoformer_amd import kernels as Kr
-
-    A.set_compute("bf16")
-    Ly.set_grad_sink(False)
-    Kr.set_deterministic(True)
-    C = 512
-    torch.manual_seed(11)
-    mods = []
-    for i in range(3):
-        conv = torch.nn.Conv1d(C if i else 80, C, 5, padding=2).to(DEV)
-        bn = torch.nn.BatchNorm1d(C).to(DEV).train()
-        with torch.no_grad():
-            bn.weight.uniform_(0.5, 1.5)
-            bn.bias.normal_(0, 0.1)
-        mods += [conv, bn]
-    acts = (Kr.ACT_RELU, Kr.ACT_RELU, Kr.ACT_TANH)
-    cores = [Ly.ConvBNCore(mods[2 * i], mods[2 * i + 1], acts[i]) for i in range(3)]
-    x0 = torch.randn(B * T, 80, device=DEV)
-    res = []
-    saved = Ly._BN_APPLY_FUSED, Ly._BN_BWD_APPLY_FUSED
-    try:
-        for fused in (True, False):
-            Ly._BN_APPLY_FUSED = Ly._BN_BWD_APPLY_FUSED = fused
-            for m in mods:
-                m.zero_grad(set_to_none=True)
-                if isinstance(m, torch.nn.BatchNorm1d):
-                    m.reset_running_stats()
-            x = x0.clone().requires_grad_(True)
-            h = Ly.conv_bn(cores[0], x, B, T, out_bf16=True)
-            h = Ly.conv_bn(cores[1], h, B, T, out_bf16=True, fuse_prev=True)
-            h = Ly.conv_bn(cores[2], h, B, T, out_bf16=True, fuse_prev=True)
-            (h.float() * torch.linspace(-1, 1, C, device=DEV)).sum().backward()
-            torch.cuda.synchronize()
-            res.append((h.detach().float().clone(), x.grad.clone(),
-                        [p.grad.clone() for m in mods for p in m.parameters()],
-                        [m.running_var.clone() for m in mods if isinstance(m, torch.nn.BatchNorm1d)]))
-        Kr.check_faults()
-    finally:
-        Ly._BN_APPLY_FUSED, Ly._BN_BWD_APPLY_FUSED = saved
-        Kr.set_deterministic(False)
-    (ha, dxa, ga, ra), (hb, dxb, gb, rb) = res
-    torch.testing.assert_close(ha, hb, rtol=0, atol=0)
-    torch.testing.assert_close(dxa, dxb, rtol=0, atol=0)
-    for p, q in zip(ga + ra, gb + rb):
-        torch.testing.assert_close(p, q, rtol=0, atol=0)
-
-
 @pytest.mark.parametrize("n1,n2,off", [(64 * 128 * 80, 64 * 8 * 88, 0), (1001, 37, 1), (5, 0, 0)])
 def test_vc_loss_block_matches_torch(n1, n2, off):
     """avc_vc_loss / avc_vc_loss_grad (the fused loss block of train.py:84-96) against

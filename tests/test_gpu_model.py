@@ -217,7 +217,7 @@ def test_encoder_list_api_and_eval_mode(golden):
 
 
 def test_trainstep_sink_graph_matches_plain_autograd(golden):
-    """TrainStep (flat buffers, gradient sink + side stream, fused Adam, hipGraph replay)
+    """TrainStep (flat buffers, gradient sink + side stream, fused Adam)
     reproduces the reference Solver's 3-step losses in fp32 compute."""
     from autoformer_amd.train import TrainStep
     from autoformer_amd.layers import set_grad_sink
@@ -253,13 +253,13 @@ def test_trainstep_sink_graph_matches_plain_autograd(golden):
         assert torch.allclose(p, p2, rtol=1e-4, atol=1e-6), n
 
 
-def test_trainstep_graph_replay_equals_eager():
-    """hipGraph replay of the step equals the eager step.  The bf16 step is not bit-reproducible
-    (split-K atomics reorder run to run, and Adam's first updates turn sign flips of tiny
-    gradients into whole-lr moves: two EAGER runs differ by up to 3 lr after 3 steps,
-    tools/replay_diff.py), so the parameters are held fixed (lr = 0) and the third step's
-    losses and per-tensor gradients are compared (rel-Frobenius 1e-2: bf16 run-to-run spread
-    1.3e-3 measured); a missing or stale kernel in the replay shows as an O(1) error."""
+def test_trainstep_recorded_replay_equals_eager_lr0():
+    """The recorded replay of the step (replay.py) equals the eager step.  The bf16 step is not
+    bit-reproducible (split-K atomics reorder run to run, and Adam's first updates turn sign flips of
+    tiny gradients into whole-lr moves: two EAGER runs differ by up to 3 lr after 3 steps), so the
+    parameters are held fixed (lr = 0) and the third step's losses and per-tensor gradients are
+    compared (rel-Frobenius 1e-2: bf16 run-to-run spread 1.3e-3 measured); a missing or stale
+    kernel in the replay shows as an O(1) error."""
     from autoformer_amd.detinit import det_inputs
     from autoformer_amd.layers import set_grad_sink
     from autoformer_amd.train import TrainStep
@@ -272,8 +272,7 @@ def test_trainstep_graph_replay_equals_eager():
         for _ in range(3):
             la = ta.step(x, e)
         tb.step(x, e)
-        tb.capture(x, e, warmup=0)  # records only
-        tb.step(x, e)               # replay = step 2
+        tb.record(x, e, warmup=0)   # = step 2, recorded
         lb = tb.step(x, e)          # replay = step 3
         torch.cuda.synchronize()
         assert abs(la.item() - lb.item()) <= 1e-4 * abs(la.item())

@@ -1,5 +1,5 @@
 # kernel-trace profile of the C2 bench -> gpurun_out/$1 (CSV), plus step breakdown / gaps;
-# further arguments go to bench.py (e.g. --graph)
+# further arguments go to bench.py (e.g. --eager)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/$1
