@@ -135,6 +135,66 @@ __global__ void conv_pack_kernel(const float* w, void* out, int dtype, int Co, i
   putd(out, o, w[i], dtype);
 }
 
+// LDS-staged conv weight permutations, coalesced on both sides (round 6: the per-element forms above
+// scatter 2-B stores Ci / K*Co elements apart -- ~64 B of memory traffic per stored bf16 -- and the
+// batched repack of the step's weights had run 225 us beside the encoder backward, 28 alone for the
+// encoder's seventh of it).  W[co][ci][k] fp32 ->
+//   mode 0, Wf[co][k][ci]:       unit = 4 output channels x 64 input channels (4 runs of 64*K floats in,
+//                                4*K runs of 64 out);
+//   mode 1, Wd[ci][K-1-k][co]:   unit = 32 output x 32 input channels (32 runs of 32*K floats in, 32*K
+//                                runs of 32 out).
+// K <= PK_KMAX; buf holds PK_BUF floats.  256 threads.
+constexpr int PK_KMAX = 8, PK_BUF = 32 * PK_KMAX * 33;
+__host__ __device__ constexpr long long conv_pack_units(int Co, int Ci, int mode) {
+  return mode == 0 ? (long long)((Co + 3) / 4) * ((Ci + 63) / 64) : (long long)((Co + 31) / 32) * ((Ci + 31) / 32);
+}
+__device__ void conv_pack_unit(const float* __restrict__ w, void* out, int dtype, int Co, int Ci, int K, int mode,
+                               long long u, float* buf) {
+  const int tid = threadIdx.x;
+  if (mode == 0) {
+    const int ncb = (Ci + 63) / 64;
+    const int co0 = (int)(u / ncb) * 4, ci0 = (int)(u % ncb) * 64;
+    const int n = 4 * 64 * K;
+    for (int e = tid; e < n; e += 256) {
+      const int r = e / (64 * K), rem = e - r * 64 * K;  // rem = ci_l * K + k
+      const int cil = rem / K, k = rem - cil * K;
+      const int co = co0 + r, ci = ci0 + cil;
+      buf[(r * K + k) * 65 + cil] = (co < Co && ci < Ci) ? w[((long long)co * Ci + ci0) * K + rem] : 0.f;
+    }
+    __syncthreads();
+    for (int e = tid; e < n; e += 256) {
+      const int r = e / (64 * K), rem = e - r * 64 * K;  // rem = k * 64 + ci_l
+      const int k = rem >> 6, cil = rem & 63;
+      const int co = co0 + r, ci = ci0 + cil;
+      if (co < Co && ci < Ci) putd(out, ((long long)co * K + k) * Ci + ci, buf[(r * K + k) * 65 + cil], dtype);
+    }
+  } else {
+    const int ncb = (Ci + 31) / 32;
+    const int co0 = (int)(u / ncb) * 32, ci0 = (int)(u % ncb) * 32;
+    const int n = 32 * 32 * K;
+    for (int e = tid; e < n; e += 256) {
+      const int r = e / (32 * K), rem = e - r * 32 * K;  // row r = co_l, rem = ci_l * K + k
+      const int co = co0 + r, ci = ci0 + rem / K;
+      buf[rem * 33 + r] = (co < Co && ci < Ci) ? w[((long long)co * Ci + ci0) * K + rem] : 0.f;
+    }
+    __syncthreads();
+    for (int e = tid; e < n; e += 256) {
+      const int q = e >> 5, col = e & 31;  // q = ci_l * K + k
+      const int cil = q / K, k = q - cil * K;
+      const int ci = ci0 + cil, co = co0 + col;
+      if (co < Co && ci < Ci) putd(out, ((long long)ci * K + (K - 1 - k)) * Co + co, buf[q * 33 + col], dtype);
+    }
+  }
+  __syncthreads();  // buf is reused by the caller's next unit
+}
+
+__global__ void __launch_bounds__(256) conv_pack_tiled_kernel(const float* w, void* out, int dtype, int Co, int Ci,
+                                                              int K, int mode) {
+  __shared__ float buf[PK_BUF];
+  const long long nu = conv_pack_units(Co, Ci, mode);
+  for (long long u = blockIdx.x; u < nu; u += gridDim.x) conv_pack_unit(w, out, dtype, Co, Ci, K, mode, u, buf);
+}
+
 __global__ void conv_grad_unpack_kernel(const float* dwf, float* dw, int Co, int Ci, int K, int acc) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   long long total = (long long)Co * Ci * K;
@@ -307,7 +367,8 @@ constexpr int PACK_MAX_OPS = 128;
 __global__ void __launch_bounds__(256) pack_batch_kernel(const avc_pack_op* __restrict__ ops,
                                                          const long long* __restrict__ prefix, int nops,
                                                          long long total) {
-  __shared__ float tile[32][33];
+  __shared__ float buf[PK_BUF];  // the conv units' staging; the transpose's 32 x 33 tile is its start
+  float (*tile)[33] = reinterpret_cast<float (*)[33]>(buf);
   __shared__ long long pre[PACK_MAX_OPS + 1];
   __shared__ avc_pack_op sops[PACK_MAX_OPS];
   const int tid = threadIdx.x;
@@ -340,6 +401,10 @@ __global__ void __launch_bounds__(256) pack_batch_kernel(const avc_pack_op* __re
         if (c < C && r < R) putd(op.dst, (long long)c * op.ld_out + r, tile[tx][y], op.out_dtype);
       }
       __syncthreads();  // the tile is reused by the next unit
+      continue;
+    }
+    if ((op.kind == AVC_PACK_CONV_F || op.kind == AVC_PACK_CONV_D) && op.d2 <= PK_KMAX) {
+      conv_pack_unit(op.src, op.dst, op.out_dtype, op.d0, op.d1, op.d2, op.kind == AVC_PACK_CONV_F ? 0 : 1, lu, buf);
       continue;
     }
     const long long n = (op.kind == AVC_PACK_CONV_F || op.kind == AVC_PACK_CONV_D) ? (long long)op.d0 * op.d1 * op.d2
@@ -523,7 +588,13 @@ extern "C" int avc_expand_codes(const float* pc, const float* pe, float* out, in
 extern "C" int avc_conv_pack(const float* w, void* out, int dtype, int Co, int Ci, int K, int mode, void* stream) {
   AVC_CHECK_ARG(w && out && (mode == 0 || mode == 1), "avc_conv_pack: bad args");
   long long n = (long long)Co * Ci * K;
-  conv_pack_kernel<<<GRID1(n)>>>(w, out, dtype, Co, Ci, K, mode);
+  if (K <= PK_KMAX) {
+    const long long nu = conv_pack_units(Co, Ci, mode);
+    conv_pack_tiled_kernel<<<(int)std::min<long long>(nu, 2048), 256, 0, as_stream(stream)>>>(w, out, dtype, Co, Ci, K,
+                                                                                               mode);
+  } else {
+    conv_pack_kernel<<<GRID1(n)>>>(w, out, dtype, Co, Ci, K, mode);
+  }
   return avc_check_launch("avc_conv_pack");
 }
 

@@ -335,11 +335,16 @@ def _op_struct(o):
 
 
 def _op_len(o):
-    """Units of an op in avc_pack_batch: 1024 elements, or a 32 x 32 transpose tile."""
+    """Units of an op in avc_pack_batch (elem.hip): a 32 x 32 transpose tile; for a conv pack with at most
+    8 taps an LDS-staged tile (Wf: 4 output x 64 input channels, Wd: 32 x 32); else 1024 elements."""
     from ._lib import PACK_CONV_D, PACK_CONV_F, PACK_TRANSPOSE
 
     d = o["dims"]
     if o["kind"] == PACK_TRANSPOSE:
+        return -(-d[0] // 32) * -(-d[1] // 32)
+    if o["kind"] == PACK_CONV_F and d[2] <= 8:
+        return -(-d[0] // 4) * -(-d[1] // 64)
+    if o["kind"] == PACK_CONV_D and d[2] <= 8:
         return -(-d[0] // 32) * -(-d[1] // 32)
     n = d[0] * d[1] * d[2] if o["kind"] in (PACK_CONV_F, PACK_CONV_D) else d[0]
     return -(-n // 1024)

@@ -690,6 +690,22 @@ def test_gemm_tt_time_shift_window():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("Co,Ci,Kw", [(512, 512, 5), (96, 40, 5), (80, 512, 5), (512, 80, 5), (33, 65, 3), (24, 44, 9)])
+def test_conv_pack_matches_permute(Co, Ci, Kw):
+    """avc_conv_pack (LDS-staged tiles for <= 8 taps, the per-element kernel above) against the torch
+    permutations it stands for: Wf[co][k][ci] and the flipped Wd[ci][K-1-k][co], bf16 and fp32."""
+    from autoformer_amd import kernels as Kr
+
+    w = torch.randn(Co, Ci, Kw, device=DEV)
+    for dt, tdt in ((Kr.BF16, torch.bfloat16), (Kr.F32, torch.float32)):
+        wf = Kr.conv_pack(w, 0, dt)
+        wd = Kr.conv_pack(w, 1, dt)
+        torch.cuda.synchronize()
+        assert torch.equal(wf.reshape(Co, Kw, Ci), w.permute(0, 2, 1).to(tdt))
+        assert torch.equal(wd.reshape(Ci, Kw, Co), w.flip(2).permute(1, 2, 0).to(tdt))
+
+
+@pytest.mark.gpu
 def test_pack_batch_matches_individual_packs():
     """avc_pack_batch (one launch for many packs) == the per-pack kernels it replaces."""
     import autoformer_amd as A

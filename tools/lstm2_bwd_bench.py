@@ -85,6 +85,23 @@ def main():
     period = np.diff(st[:, :, 0], axis=1)[:, 1:-1].mean()
     print(f"wavefront per tick: start -> products reduced {wait_prod:.2f} us, -> published {tail:.2f} us, "
           f"period {period:.2f} us")
+    # stamp 1 = the group's flags all seen (after the poll's barrier): the tick's wait vs its gather
+    wait = (st[:, ks, 1] - st[:, ks, 0]).mean()
+    gath = (st[:, ks, 2] - st[:, ks, 1]).mean()
+    print(f"  start -> flags seen {wait:.2f} us, flags seen -> products reduced {gath:.2f} us")
+    # producer skew: per group and tick, the members' publish stamps (flag raised just before stamp 3)
+    grp = np.arange(nwg) % ng
+    skew, hop = [], []
+    for g in range(ng):
+        m = grp == g
+        for k in range(1, T - 2):
+            pub = st[m, k, 3]
+            seen = st[m, k + 1, 1]
+            skew.append(pub.max() - np.median(pub))
+            hop.append(seen.min() - pub.max())
+    skew, hop = np.array(skew), np.array(hop)
+    print(f"  producer skew (last publish - median publish) mean {skew.mean():.2f} us, p90 {np.percentile(skew, 90):.2f}; "
+          f"last publish -> first consumer's flags seen {hop.mean():.2f} us")
 
 
 if __name__ == "__main__":
