@@ -368,7 +368,8 @@ __global__ void __launch_bounds__(256, 2) gemm_tt_halo_kernel(GemmArgs g) {
   // epilogue: row m0 + wm*64 + 16i + 4*(lane>>4) + e, column tap*chans + c0 + 16*wn + (lane & 15)
   const int rbase = m0 + wm * 64 + 4 * (lane >> 4);
   const int cl = c0 + 16 * wn + (lane & 15);
-  if (g.cperm == TAPS && (!g.atomic || g.sk_ws)) {
+  // (16-B vector path: C 16-B aligned and its rows a multiple of 4 floats apart; else per element)
+  if (g.cperm == TAPS && (!g.atomic || g.sk_ws) && (reinterpret_cast<uintptr_t>(g.c) & 15) == 0 && (g.ldc & 3) == 0) {
     // Straight into the Conv1d [Co][Ci][K] layout: the tile's (32 channels x 5 taps) of a row are
     // ONE contiguous 640-B run there, so each 64-row half is staged through LDS ([64][CPW] floats)
     // and stored as 16-B row chunks (per-element stores 20 B apart had cost more than the

@@ -29,6 +29,9 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "mel-frames/sec fwd+bwd, AutoVC 80×128 mel, batch=64, at 1/2/4/8 GPUs"
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3     # f32 MFMA
+# dense bf16 MFMA peak measured on the box: 16x16x32 chains on every CU, 2.05 GHz under that load
+# (tools/probes/mfma_peak.hip, profiles/r6_mfma_peak.txt)
+PEAK_BF16_MEASURED_TFLOPS = 2047.4
 # algorithmic work of one train step per mel frame (torch flop counter on the reference)
 FLOP_PER_FRAME = {("AutoVC", 128, 16): 191.55e6, ("AutoVC", 176, 22): 191.59e6, ("AutoVC+D", 176, 22): 191.87e6,
                   ("MetaConv", 176, 22): 1044.41e6, ("MetaPool", 176, 22): 981.86e6,
@@ -436,7 +439,11 @@ def main():
         gbs = kt["bytes"] / (step_us * 1e-6) / 1e9
         traffic, src = pmc_traffic(dominant)
         out["roofline"] = {"bound": "mfma", "achieved": round(tfs, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(tfs / PEAK_BF16_TFLOPS, 5), "traffic": traffic, "kernel": kt["kernel"],
+                           "frac": round(tfs / PEAK_BF16_TFLOPS, 5),
+                           "peak_measured": PEAK_BF16_MEASURED_TFLOPS,
+                           "frac_measured": round(tfs / PEAK_BF16_MEASURED_TFLOPS, 5),
+                           "peak_measured_source": "profiles/r6_mfma_peak.txt",
+                           "traffic": traffic, "kernel": kt["kernel"],
                            "avg_us": round(step_us, 3), "launches_timed": len(evs),
                            "avg_us_isolated": round(kt["avg_us"], 3), "flop_per_launch": kt["flops"],
                            "alg_bytes_per_launch": kt["bytes"], "hbm_achieved_gbs": round(gbs, 1),
