@@ -71,8 +71,7 @@ def kernel_timing_wave(model, B, T, reps=3):
     three recurrent products per step (W_hh1^T, W_ih1^T, W_hh0^T: 2 * B * 4H * H each) over T steps.
     Algorithmic bytes: the three transposed weights once (3 * 4H * H bf16) + per step
     dL/dh1 fp32 (B*H*4) + per layer c_t, c_{t-1} fp32 (2*B*H*4) + gates fp32 (B*4H*4) + dG out: bf16
-    (B*4H*2) in the step's form (layers._PAIR_DB: bf16 dG + per-group bias partials, ABI 28), fp32 and
-    bf16 (B*4H*6) otherwise; timed in the form the step runs."""
+    (B*4H*2) in the step's form (bf16 dG + per-group bias partials, ABI 28); timed in that form."""
     from autoformer_amd import kernels as K
     from autoformer_amd import layers as Ly
 
@@ -85,7 +84,7 @@ def kernel_timing_wave(model, B, T, reps=3):
     dh = torch.randn(B * T, H, device=dev, generator=g) * 0.1
     cs = [torch.randn(B * T, H, device=dev, generator=g) * 0.5 for _ in range(2)]
     gs = [torch.rand(B * T, 4 * H, device=dev, generator=g) for _ in range(2)]
-    db = Ly._PAIR_DB
+    db = True  # the step's form (layers._LSTMPairFn.backward)
     K.lstm2_bwd(dh, cs[0], gs[0], cs[1], gs[1], wt0, wti1, wt1, B, T, H, fp32=not db, db=db)  # warm
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
