@@ -135,18 +135,18 @@ __global__ void conv_pack_kernel(const float* w, void* out, int dtype, int Co, i
   putd(out, o, w[i], dtype);
 }
 
-// LDS-staged conv weight permutations, coalesced on both sides (round 6: the per-element forms above
-// scatter 2-B stores Ci / K*Co elements apart -- ~64 B of memory traffic per stored bf16 -- and the
-// batched repack of the step's weights had run 225 us beside the encoder backward, 28 alone for the
-// encoder's seventh of it).  W[co][ci][k] fp32 ->
-//   mode 0, Wf[co][k][ci]:       unit = 4 output channels x 64 input channels (4 runs of 64*K floats in,
-//                                4*K runs of 64 out);
-//   mode 1, Wd[ci][K-1-k][co]:   unit = 32 output x 32 input channels (32 runs of 32*K floats in, 32*K
-//                                runs of 32 out).
-// K <= PK_KMAX; buf holds PK_BUF floats.  256 threads.
-constexpr int PK_KMAX = 8, PK_BUF = 32 * PK_KMAX * 33;
+// Weight-pack units, LDS-staged where the layout changes, 256 threads (round 6: the per-element forms
+// scattered 2-B stores Ci or K*Co elements apart -- ~64 B of memory traffic per stored bf16 -- and the
+// batched repack ran at ~1 TB/s, 225 us beside the encoder backward for the decoder's weights).  Every
+// unit keeps 16 independent loads per thread in flight and needs at most PK_BUF floats of LDS (17 KiB,
+// so a pack workgroup still fits beside a conv ring workgroup).  W[co][ci][k] fp32 ->
+//   mode 0, Wf[co][k][ci]:     unit = 4 output x 64 input channels (K <= 16; 4 runs of 64*K floats in,
+//                              4*K runs of 64 out);
+//   mode 1, Wd[ci][K-1-k][co]: unit = 32 output x 16 input channels (K <= 8; 32 runs of 16*K floats in,
+//                              16*K runs of 32 out).
+constexpr int PK_KMAX_F = 16, PK_KMAX_D = 8, PK_BUF = 64 * 65;
 __host__ __device__ constexpr long long conv_pack_units(int Co, int Ci, int mode) {
-  return mode == 0 ? (long long)((Co + 3) / 4) * ((Ci + 63) / 64) : (long long)((Co + 31) / 32) * ((Ci + 31) / 32);
+  return mode == 0 ? (long long)((Co + 3) / 4) * ((Ci + 63) / 64) : (long long)((Co + 31) / 32) * ((Ci + 15) / 16);
 }
 __device__ void conv_pack_unit(const float* __restrict__ w, void* out, int dtype, int Co, int Ci, int K, int mode,
                                long long u, float* buf) {
@@ -169,11 +169,11 @@ __device__ void conv_pack_unit(const float* __restrict__ w, void* out, int dtype
       if (co < Co && ci < Ci) putd(out, ((long long)co * K + k) * Ci + ci, buf[(r * K + k) * 65 + cil], dtype);
     }
   } else {
-    const int ncb = (Ci + 31) / 32;
-    const int co0 = (int)(u / ncb) * 32, ci0 = (int)(u % ncb) * 32;
-    const int n = 32 * 32 * K;
+    const int ncb = (Ci + 15) / 16;
+    const int co0 = (int)(u / ncb) * 32, ci0 = (int)(u % ncb) * 16;
+    const int n = 32 * 16 * K;
     for (int e = tid; e < n; e += 256) {
-      const int r = e / (32 * K), rem = e - r * 32 * K;  // row r = co_l, rem = ci_l * K + k
+      const int r = e / (16 * K), rem = e - r * 16 * K;  // row r = co_l, rem = ci_l * K + k
       const int co = co0 + r, ci = ci0 + rem / K;
       buf[rem * 33 + r] = (co < Co && ci < Ci) ? w[((long long)co * Ci + ci0) * K + rem] : 0.f;
     }
@@ -364,11 +364,19 @@ __global__ void vc_loss_grad_kernel(const float* __restrict__ x, const float* __
 // search per unit (<= 128 ops).
 constexpr int PACK_MAX_OPS = 128;
 
+__device__ __forceinline__ void put4(void* dst, long long i, float4 v, int dtype) {
+  if (dtype == AVC_F32) {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(dst) + i) = v;
+  } else {
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(dst) + i) = bf16x4{(bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
+  }
+}
+__device__ __forceinline__ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 __global__ void __launch_bounds__(256) pack_batch_kernel(const avc_pack_op* __restrict__ ops,
                                                          const long long* __restrict__ prefix, int nops,
                                                          long long total) {
-  __shared__ float buf[PK_BUF];  // the conv units' staging; the transpose's 32 x 33 tile is its start
-  float (*tile)[33] = reinterpret_cast<float (*)[33]>(buf);
+  __shared__ float buf[PK_BUF];  // the units' staging (a transpose tile is [64][65])
   __shared__ long long pre[PACK_MAX_OPS + 1];
   __shared__ avc_pack_op sops[PACK_MAX_OPS];
   const int tid = threadIdx.x;
@@ -385,42 +393,98 @@ __global__ void __launch_bounds__(256) pack_batch_kernel(const avc_pack_op* __re
     }
     const avc_pack_op& op = sops[lo];
     const long long lu = u - pre[lo];
-    if (op.kind == AVC_PACK_TRANSPOSE) {  // dst[c*ld + r] = src[r*C + c], src [R][C]
-      const int R = op.d0, C = op.d1, tcn = (C + 31) / 32;
-      const int r0 = (int)(lu / tcn) * 32, c0 = (int)(lu % tcn) * 32;
-      const int tx = tid & 31, ty = tid >> 5;
+    if (op.kind == AVC_PACK_TRANSPOSE) {  // dst[c*ld + r] = src[r*C + c], src [R][C]; 64 x 64 tile
+      const int R = op.d0, C = op.d1, tcn = (C + 63) / 64;
+      const int r0 = (int)(lu / tcn) * 64, c0 = (int)(lu % tcn) * 64;
+      const bool v4 = (C & 3) == 0 && al16(op.src);
+      // load: 64 rows x 16 float4 = 4 per thread (row = q >> 4, col4 = q & 15), 16 B in flight each
+      float4 v[4];
 #pragma unroll
-      for (int y = ty; y < 32; y += 8) {
-        const int r = r0 + y, c = c0 + tx;
-        tile[y][tx] = (r < R && c < C) ? op.src[(long long)r * C + c] : 0.f;
+      for (int t = 0; t < 4; ++t) {
+        const int q = t * 256 + tid, r = r0 + (q >> 4), c = c0 + 4 * (q & 15);
+        if (v4 && r < R && c + 3 < C) {
+          v[t] = *reinterpret_cast<const float4*>(op.src + (long long)r * C + c);
+        } else {
+          float e[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) e[k] = (r < R && c + k < C) ? op.src[(long long)r * C + c + k] : 0.f;
+          v[t] = float4{e[0], e[1], e[2], e[3]};
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int q = t * 256 + tid, rl = q >> 4, cl = 4 * (q & 15);
+        buf[(cl + 0) * 65 + rl] = v[t].x;
+        buf[(cl + 1) * 65 + rl] = v[t].y;
+        buf[(cl + 2) * 65 + rl] = v[t].z;
+        buf[(cl + 3) * 65 + rl] = v[t].w;
       }
       __syncthreads();
+      // store: dst rows c0.. (64 of them), 64 consecutive r each: 4 x 4 elements per thread
+      const bool s4 = (op.ld_out & 3) == 0 && al16(op.dst);
 #pragma unroll
-      for (int y = ty; y < 32; y += 8) {
-        const int c = c0 + y, r = r0 + tx;
-        if (c < C && r < R) putd(op.dst, (long long)c * op.ld_out + r, tile[tx][y], op.out_dtype);
+      for (int t = 0; t < 4; ++t) {
+        const int q = t * 256 + tid, cl = q >> 4, rl = 4 * (q & 15);
+        const int c = c0 + cl, r = r0 + rl;
+        if (c >= C) continue;
+        // (65-float LDS rows are 4-B aligned only: four scalar reads)
+        const float e0 = buf[cl * 65 + rl], e1 = buf[cl * 65 + rl + 1], e2 = buf[cl * 65 + rl + 2],
+                    e3 = buf[cl * 65 + rl + 3];
+        const long long o = (long long)c * op.ld_out + r;
+        if (s4 && r + 3 < R) {
+          put4(op.dst, o, float4{e0, e1, e2, e3}, op.out_dtype);
+        } else {
+          const float e[4] = {e0, e1, e2, e3};
+          for (int k = 0; k < 4 && r + k < R; ++k) putd(op.dst, o + k, e[k], op.out_dtype);
+        }
       }
       __syncthreads();  // the tile is reused by the next unit
       continue;
     }
-    if ((op.kind == AVC_PACK_CONV_F || op.kind == AVC_PACK_CONV_D) && op.d2 <= PK_KMAX) {
-      conv_pack_unit(op.src, op.dst, op.out_dtype, op.d0, op.d1, op.d2, op.kind == AVC_PACK_CONV_F ? 0 : 1, lu, buf);
+    if (op.kind == AVC_PACK_CONV_F && op.d2 <= PK_KMAX_F) {
+      conv_pack_unit(op.src, op.dst, op.out_dtype, op.d0, op.d1, op.d2, 0, lu, buf);
       continue;
     }
-    const long long n = (op.kind == AVC_PACK_CONV_F || op.kind == AVC_PACK_CONV_D) ? (long long)op.d0 * op.d1 * op.d2
-                                                                                  : op.d0;
+    if (op.kind == AVC_PACK_CONV_D && op.d2 <= PK_KMAX_D) {
+      conv_pack_unit(op.src, op.dst, op.out_dtype, op.d0, op.d1, op.d2, 1, lu, buf);
+      continue;
+    }
+    const bool conv = op.kind == AVC_PACK_CONV_F || op.kind == AVC_PACK_CONV_D;
+    const long long n = conv ? (long long)op.d0 * op.d1 * op.d2 : op.d0;
+    if (!conv && al16(op.src) && al16(op.dst) && (op.kind != AVC_PACK_ADD || al16(op.src2))) {
+      // COPY / ADD: 4096 elements per unit, 4 float4 per thread (and 4 of src2)
+      float4 a[4], b[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const long long i = lu * 1024 + j * 256 + tid;
+      for (int t = 0; t < 4; ++t) {
+        const long long i = lu * 4096 + (t * 256 + tid) * 4;
+        a[t] = i + 3 < n ? *reinterpret_cast<const float4*>(op.src + i) : float4{0.f, 0.f, 0.f, 0.f};
+        b[t] = (op.kind == AVC_PACK_ADD && i + 3 < n) ? *reinterpret_cast<const float4*>(op.src2 + i)
+                                                      : float4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const long long i = lu * 4096 + (t * 256 + tid) * 4;
+        if (i + 3 < n) {
+          put4(op.dst, i, float4{a[t].x + b[t].x, a[t].y + b[t].y, a[t].z + b[t].z, a[t].w + b[t].w}, op.out_dtype);
+        } else {
+          for (long long k = i; k < n && k < i + 4; ++k)
+            putd(op.dst, k, op.src[k] + (op.kind == AVC_PACK_ADD ? op.src2[k] : 0.f), op.out_dtype);
+        }
+      }
+      continue;
+    }
+#pragma unroll 4
+    for (int j = 0; j < 16; ++j) {
+      const long long i = lu * 4096 + j * 256 + tid;
       if (i >= n) break;
       float v = op.src[i];
       long long o = i;
       if (op.kind == AVC_PACK_ADD) {
         v += op.src2[i];
-      } else if (op.kind == AVC_PACK_CONV_F || op.kind == AVC_PACK_CONV_D) {  // source W[co][ci][k]
-        const int K = op.d2, Ci = op.d1, Co = op.d0;
+      } else if (conv) {  // source W[co][ci][k]
+        const int K = op.d2, Ci = op.d1;
         const int ii = (int)i, k = ii % K, ci = (ii / K) % Ci, co = ii / (K * Ci);
-        o = op.kind == AVC_PACK_CONV_F ? ((long long)co * K + k) * Ci + ci : ((long long)ci * K + (K - 1 - k)) * Co + co;
+        o = op.kind == AVC_PACK_CONV_F ? ((long long)co * K + k) * Ci + ci : ((long long)ci * K + (K - 1 - k)) * op.d0 + co;
       }
       putd(op.dst, o, v, op.out_dtype);
     }
@@ -588,7 +652,7 @@ extern "C" int avc_expand_codes(const float* pc, const float* pe, float* out, in
 extern "C" int avc_conv_pack(const float* w, void* out, int dtype, int Co, int Ci, int K, int mode, void* stream) {
   AVC_CHECK_ARG(w && out && (mode == 0 || mode == 1), "avc_conv_pack: bad args");
   long long n = (long long)Co * Ci * K;
-  if (K <= PK_KMAX) {
+  if (K <= (mode == 0 ? PK_KMAX_F : PK_KMAX_D)) {
     const long long nu = conv_pack_units(Co, Ci, mode);
     conv_pack_tiled_kernel<<<(int)std::min<long long>(nu, 2048), 256, 0, as_stream(stream)>>>(w, out, dtype, Co, Ci, K,
                                                                                                mode);

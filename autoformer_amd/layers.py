@@ -335,19 +335,20 @@ def _op_struct(o):
 
 
 def _op_len(o):
-    """Units of an op in avc_pack_batch (elem.hip): a 32 x 32 transpose tile; for a conv pack with at most
-    8 taps an LDS-staged tile (Wf: 4 output x 64 input channels, Wd: 32 x 32); else 1024 elements."""
+    """Units of an op in avc_pack_batch (elem.hip pack_batch_kernel): a 64 x 64 transpose tile; an LDS-staged
+    conv tile (Wf: 4 output x 64 input channels for <= 16 taps, Wd: 32 x 16 for <= 8 taps); else 4096
+    elements."""
     from ._lib import PACK_CONV_D, PACK_CONV_F, PACK_TRANSPOSE
 
     d = o["dims"]
     if o["kind"] == PACK_TRANSPOSE:
-        return -(-d[0] // 32) * -(-d[1] // 32)
-    if o["kind"] == PACK_CONV_F and d[2] <= 8:
+        return -(-d[0] // 64) * -(-d[1] // 64)
+    if o["kind"] == PACK_CONV_F and d[2] <= 16:
         return -(-d[0] // 4) * -(-d[1] // 64)
     if o["kind"] == PACK_CONV_D and d[2] <= 8:
-        return -(-d[0] // 32) * -(-d[1] // 32)
+        return -(-d[0] // 32) * -(-d[1] // 16)
     n = d[0] * d[1] * d[2] if o["kind"] in (PACK_CONV_F, PACK_CONV_D) else d[0]
-    return -(-n // 1024)
+    return -(-n // 4096)
 
 
 def _batch_plan(caches, group=0):

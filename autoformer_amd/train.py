@@ -225,10 +225,11 @@ class FusedAdam:
 
 
 # ------------------------------------------------------------------------- bench step
-# workgroup cap of the decoder-slice Adam that runs beside the encoder backward (0 = full grid;
-# 256 measured best: the full grid slowed the latency-bound BiLSTM backward beside it, 64 / 24 let
-# the step's tail wait for it, profiles/r5_replay_ab.txt)
-_SIDE_ADAM_BLOCKS = 256
+# workgroup cap of the decoder-slice Adam that runs beside the encoder backward (0 = full grid: it slowed
+# the latency-bound BiLSTM backward beside it; 64 / 24 let the step's tail wait for it,
+# profiles/r5_replay_ab.txt).  Round 6, with the 16-B vector Adam: 512 (5.654 / 5.647 ms) vs 256 (5.683 /
+# 5.661), 128 (5.682 / 5.665), 1024 (5.667 / 5.693), profiles/r6_pack_ab.txt
+_SIDE_ADAM_BLOCKS = 512
 
 
 class TrainStep:

@@ -706,28 +706,31 @@ def test_conv_pack_matches_permute(Co, Ci, Kw):
 
 
 @pytest.mark.gpu
-def test_pack_batch_matches_individual_packs():
-    """avc_pack_batch (one launch for many packs) == the per-pack kernels it replaces."""
+@pytest.mark.parametrize("Co,Ci,G,In,H", [(96, 40, 176, 72, 44), (512, 512, 4096, 1024, 1024), (33, 70, 130, 67, 33)])
+def test_pack_batch_matches_individual_packs(Co, Ci, G, In, H):
+    """avc_pack_batch (one launch for many packs) == the per-pack kernels it replaces, on ragged shapes too
+    (tails of the 64 x 64 transpose tiles, the 4096-element copy units and the conv tiles; odd sizes take
+    the unaligned scalar forms)."""
     import autoformer_amd as A
     from autoformer_amd import kernels as Kr
     from autoformer_amd import layers as Lyr
 
     A.set_compute("bf16")
     dev = "cuda:0"
-    w = torch.randn(96, 40, 5, device=dev)
-    wih, whh = torch.randn(176, 72, device=dev), torch.randn(176, 44, device=dev)
-    bih, bhh = torch.randn(176, device=dev), torch.randn(176, device=dev)
+    w = torch.randn(Co, Ci, 5, device=dev)
+    wih, whh = torch.randn(G, In, device=dev), torch.randn(G, H, device=dev)
+    bih, bhh = torch.randn(G, device=dev), torch.randn(G, device=dev)
     ref = [Kr.conv_pack(w, 0, Kr.BF16), Kr.conv_pack(w, 1, Kr.BF16), Kr.convert(wih, Kr.BF16),
            Kr.transpose(whh, Kr.BF16), Kr.add(bih, bhh)]
     outs = [torch.empty_like(t) for t in ref]
     from autoformer_amd._lib import PACK_ADD, PACK_CONV_D, PACK_CONV_F, PACK_COPY, PACK_TRANSPOSE
-    ops = [{"src": w.data_ptr(), "dst": outs[0].data_ptr(), "kind": PACK_CONV_F, "dtype": Kr.BF16, "dims": (96, 40, 5)},
-           {"src": w.data_ptr(), "dst": outs[1].data_ptr(), "kind": PACK_CONV_D, "dtype": Kr.BF16, "dims": (96, 40, 5)},
-           {"src": wih.data_ptr(), "dst": outs[2].data_ptr(), "kind": PACK_COPY, "dtype": Kr.BF16, "dims": (176 * 72,)},
+    ops = [{"src": w.data_ptr(), "dst": outs[0].data_ptr(), "kind": PACK_CONV_F, "dtype": Kr.BF16, "dims": (Co, Ci, 5)},
+           {"src": w.data_ptr(), "dst": outs[1].data_ptr(), "kind": PACK_CONV_D, "dtype": Kr.BF16, "dims": (Co, Ci, 5)},
+           {"src": wih.data_ptr(), "dst": outs[2].data_ptr(), "kind": PACK_COPY, "dtype": Kr.BF16, "dims": (G * In,)},
            {"src": whh.data_ptr(), "dst": outs[3].data_ptr(), "kind": PACK_TRANSPOSE, "dtype": Kr.BF16,
-            "dims": (176, 44), "ld": 176},
+            "dims": (G, H), "ld": G},
            {"src": bih.data_ptr(), "src2": bhh.data_ptr(), "dst": outs[4].data_ptr(), "kind": PACK_ADD,
-            "dtype": Kr.F32, "dims": (176,)}]
+            "dtype": Kr.F32, "dims": (G,)}]
 
     class _C:  # the PackCache surface _batch_plan reads
         pass
