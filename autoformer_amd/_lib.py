@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AVC_LIB_PATH") or os.path.join(HERE, "libautovc_hip.so")
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["gemm_ring.hip", "gemm_conv.hip", "gemm_nt.hip", "gemm_tt.hip", "gemm.hip", "bn.hip", "lstm.hip", "elem.hip", "norm.hip", "variants.hip", "melgan.hip", "fold.hip", "disc.hip", "events.hip"]
-ABI_VERSION = 30
+ABI_VERSION = 31
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_LEAKY, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
@@ -68,6 +68,7 @@ _SIGS = {
     "avc_ring_reserve_test": (ctypes.c_uint, [ctypes.POINTER(ctypes.c_uint), ctypes.c_uint, ctypes.c_uint]),
     "avc_gemm": (c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "avc_expand_codes": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "avc_code_cat": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "avc_gemm_bn": (c_int, [ctypes.POINTER(GemmDesc), ctypes.POINTER(BnFin), c_void_p]),
     "avc_bn_finalize": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
                                 c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -90,6 +91,10 @@ _SIGS = {
                              c_void_p, c_void_p, c_int, c_void_p]),
     "avc_lstm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                              c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "avc_lstm_fwd_fold": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_void_p]),
+    "avc_lstm_bwd_fold": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "avc_lstm_bwd_scratch_bytes": (c_size, [c_int, c_int, c_int]),
     "avc_lstm2_persistent": (c_int, [c_int, c_int, c_int, c_int]),
     "avc_lstm2_scratch_bytes": (c_size, [c_int, c_int]),

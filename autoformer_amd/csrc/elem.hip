@@ -94,6 +94,18 @@ __global__ void expand_codes_kernel(const f32x4* __restrict__ pc, const f32x4* _
   out[i] = pc[((long long)b * nc + t / rep) * G4 + g] + pe[(long long)b * G4 + g];
 }
 
+// out[b*nc + j][k] = k < cd ? codes[b][j*cd + k] : emb[b][k - cd], bf16 (avc_code_cat)
+__global__ void code_cat_kernel(const float* __restrict__ codes, const float* __restrict__ emb, bf16* __restrict__ out,
+                                int nc, int cd, int de, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int C = cd + de;
+  const int k = (int)(i % C);
+  const long long r = i / C;  // b*nc + j
+  const long long b = r / nc;
+  out[i] = (bf16)(k < cd ? codes[r * cd + k] : emb[b * de + (k - cd)]);
+}
+
 __global__ void dec_concat_bwd_kernel(const float* dout, float* dcodes, int B, int T, int nc, int cd, int de) {
   const int C = cd + de;
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -647,6 +659,14 @@ extern "C" int avc_expand_codes(const float* pc, const float* pe, float* out, in
   expand_codes_kernel<<<GRID1(n4)>>>(reinterpret_cast<const f32x4*>(pc), reinterpret_cast<const f32x4*>(pe),
                                      reinterpret_cast<f32x4*>(out), T, nc, G / 4, n4);
   return avc_check_launch("avc_expand_codes");
+}
+
+extern "C" int avc_code_cat(const float* codes, const float* emb, void* out_bf16, int B, int nc, int cd, int de,
+                            void* stream) {
+  AVC_CHECK_ARG(codes && emb && out_bf16 && B > 0 && nc > 0 && cd > 0 && de > 0, "avc_code_cat: bad args");
+  const long long n = (long long)B * nc * (cd + de);
+  code_cat_kernel<<<GRID1(n)>>>(codes, emb, reinterpret_cast<bf16*>(out_bf16), nc, cd, de, n);
+  return avc_check_launch("avc_code_cat");
 }
 
 extern "C" int avc_conv_pack(const float* w, void* out, int dtype, int Co, int Ci, int K, int mode, void* stream) {

@@ -985,7 +985,7 @@ constexpr size_t px_ctl_bytes(int ng) { return 16 + (size_t)ng * PFL * 4; }
 constexpr size_t px_payload_off(int ng) { return (px_ctl_bytes(ng) + 255) & ~(size_t)255; }
 
 struct PersistArgs {
-  const float* xproj;
+  const float* xproj;  // (B, T/seg, 4H): row b*(T/seg) + t/seg is step t's input projection
   const bf16* w;
   float* hout;
   bf16* hout16;  // optional bf16 copy of h
@@ -998,6 +998,7 @@ struct PersistArgs {
   unsigned spin;              // spin bound per wait (PSPIN unless avc_lstm_set_spin / AVC_LSTM_SPIN)
   int nap;                    // granule form: s_sleep(1)s between failed sweeps (0)
   int B, T, ng;
+  int seg;                    // frames sharing one xproj row: 1, or T/nc for the lstm1 code fold
 };
 
 // Diagnostics: avc_lstm_trace(buf) makes the persistent kernels record the 100 MHz REALTIME
@@ -1205,7 +1206,7 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_fwd(PersistArgs a) {
     stamp(a.trace, T, s, 0);
     float px[4] = {0.f, 0.f, 0.f, 0.f};
     if (pv) {
-      const float* xp = a.xproj + ((long long)pb * T + t) * G + pj;
+      const float* xp = a.xproj + ((long long)pb * (T / a.seg) + t / a.seg) * G + pj;
 #pragma unroll
       for (int q = 0; q < 4; ++q) px[q] = xp[q * H];
     }
@@ -1313,6 +1314,8 @@ struct PersistBwdArgs {
   const bf16* wt;      // W_hh^T [H][4H]
   float* dg;           // (B,T,4H)
   bf16* dg16;          // (B,T,4H) or null
+  float* sc;           // (B, T/seg, 4H) dG summed over each seg-frame segment, or null
+  bf16* sc16;          // its bf16 twin, or null
   unsigned* ctl;       // scratch: ctl[0] timeout flag, flags from word 4
   bf16* pay;           // payload [2][B][4H]
   unsigned long long* trace;  // diagnostics (avc_lstm_trace), null in production
@@ -1320,6 +1323,7 @@ struct PersistBwdArgs {
   unsigned spin;
   int nap;
   int B, T, ng;
+  int seg;  // frames per sc row (the lstm1 code fold: T/nc)
 };
 
 template <int H, bool GR>
@@ -1356,6 +1360,7 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
   // MFMA A rows: 0..7 loaded utterances, 8..15 read the zero row
   const int arow = (lane & 15) < PRG ? (lane & 15) : PRG;
   float dc = 0.f;
+  float ssum[4] = {0.f, 0.f, 0.f, 0.f};  // waves 4..7: the cell's dG over the current segment
   __syncthreads();
 
   for (int s = 0; s < T; ++s) {
@@ -1465,11 +1470,26 @@ __global__ void __launch_bounds__(PNT, 1) lstm_persist_bwd(PersistBwdArgs a) {
       if (ob < B) {
         const float* o = outs + cell;
         const long long og = ((long long)ob * T + t) * G + oj;
+        if (a.dg) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) a.dg[og + q * H] = o[q * PRG * PJU];
+          for (int q = 0; q < 4; ++q) a.dg[og + q * H] = o[q * PRG * PJU];
+        }
         if (a.dg16) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) a.dg16[og + q * H] = (bf16)o[q * PRG * PJU];
+        }
+        if (a.sc) {  // segment sums (frames t .. t + seg - 1, taken in reverse) for the code fold
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ssum[q] += o[q * PRG * PJU];
+          if (t % a.seg == 0) {
+            const long long os = ((long long)ob * (T / a.seg) + t / a.seg) * G + oj;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              a.sc[os + q * H] = ssum[q];
+              if (a.sc16) a.sc16[os + q * H] = (bf16)ssum[q];
+              ssum[q] = 0.f;
+            }
+          }
         }
       }
     }
@@ -2091,6 +2111,73 @@ void launch_persist_bwd(dim3 grid, hipStream_t s, bool gr, const PersistBwdArgs&
   else lstm_persist_bwd<H, false><<<grid, PNT, persist_bwd_lds<H>(), s>>>(p);
 }
 
+// The one-launch persistent forward (persistent_path() true): hbuf = control words + flags +
+// the [2][B][H] payload (layout above); xproj row b*(T/seg) + t/seg feeds step t.
+int persist_fwd(const float* xproj, int seg, const void* w_hh, int B, int T, int H, float* h, void* h_bf16, float* c,
+                float* gates, void* hbuf, hipStream_t s, const char* what) {
+  const int ng = (B + PRG - 1) / PRG;
+  PersistArgs p;
+  p.xproj = xproj;
+  p.w = reinterpret_cast<const bf16*>(w_hh);
+  p.hout = h;
+  p.hout16 = reinterpret_cast<bf16*>(h_bf16);
+  p.call = c;
+  p.gall = gates;
+  p.ctl = reinterpret_cast<unsigned*>(hbuf);
+  p.pay = reinterpret_cast<bf16*>(reinterpret_cast<char*>(hbuf) + px_payload_off(ng));
+  p.trace = g_trace;
+  p.fault = fault_word();
+  p.spin = spin_bound();
+  p.nap = nap();
+  p.B = B;
+  p.T = T;
+  p.ng = ng;
+  p.seg = seg;
+  const bool gr = gran(false, H);
+  // flag form: only ctl + flags are polled; granule form: every tag of the payload too
+  if (avc_zero_async(hbuf, gr ? px_payload_off(ng) + (size_t)8 * B * H : px_ctl_bytes(ng), s)) return -1;
+  const dim3 grid(ng * (H / PJU));
+  if (H == 1024) gr ? lstm_persist_fwd<1024, true><<<grid, PNT, 0, s>>>(p) : lstm_persist_fwd<1024, false><<<grid, PNT, 0, s>>>(p);
+  else if (H == 768) gr ? lstm_persist_fwd<768, true><<<grid, PNT, 0, s>>>(p) : lstm_persist_fwd<768, false><<<grid, PNT, 0, s>>>(p);  // Adjust.py:30
+  else gr ? lstm_persist_fwd<512, true><<<grid, PNT, 0, s>>>(p) : lstm_persist_fwd<512, false><<<grid, PNT, 0, s>>>(p);
+  return avc_check_launch(what);
+}
+
+// The persistent backward (persistent_path() true); gbuf = control words + flags + the
+// [2][B][4H] payload.  dg (fp32) and dg16 nullable; sc / sc16 (nullable): dG summed over
+// each seg-frame segment.
+int persist_bwd(const float* dh_out, const float* c, const float* gates, const void* w_hh_t, int B, int T, int H,
+                float* dg, void* dg16, float* sc, void* sc16, int seg, void* gbuf, hipStream_t s, const char* what) {
+  const int ng = (B + PRG - 1) / PRG;
+  PersistBwdArgs p;
+  p.dhout = dh_out;
+  p.call = c;
+  p.gall = gates;
+  p.wt = reinterpret_cast<const bf16*>(w_hh_t);
+  p.dg = dg;
+  p.dg16 = reinterpret_cast<bf16*>(dg16);
+  p.sc = sc;
+  p.sc16 = reinterpret_cast<bf16*>(sc16);
+  p.ctl = reinterpret_cast<unsigned*>(gbuf);
+  p.pay = reinterpret_cast<bf16*>(reinterpret_cast<char*>(gbuf) + px_payload_off(ng));
+  p.trace = g_trace;
+  p.fault = fault_word();
+  p.spin = spin_bound();
+  p.nap = nap();
+  p.B = B;
+  p.T = T;
+  p.ng = ng;
+  p.seg = seg;
+  const bool gr = gran(true, H);
+  if (avc_zero_async(gbuf, gr ? px_payload_off(ng) + (size_t)32 * B * H : px_ctl_bytes(ng), s)) return -1;
+  // (persistent_path set the dynamic-LDS attributes)
+  const dim3 grid(ng * (H / PJU));
+  if (H == 1024) launch_persist_bwd<1024>(grid, s, gr, p);
+  else if (H == 768) launch_persist_bwd<768>(grid, s, gr, p);
+  else launch_persist_bwd<512>(grid, s, gr, p);
+  return avc_check_launch(what);
+}
+
 template <int HM>
 void launch_small_fwd(dim3 g, hipStream_t s, bool fast, const float* x, const float* w, int T, int H, int dirs,
                       float* h, bf16* h16, float* c, float* gt) {
@@ -2341,34 +2428,8 @@ extern "C" int avc_lstm_fwd(const float* xproj, const void* w_hh, int wdtype, in
   a.T = T;
   a.H = H;
   a.dirs = dirs;
-  const int ng = (B + PRG - 1) / PRG;
-  if (hbuf && persistent_path(B, H, dirs, bf, false)) {
-    // hbuf: control words + flags + the [2][B][H] bf16 payload in this mode (layout above)
-    PersistArgs p;
-    p.xproj = xproj;
-    p.w = reinterpret_cast<const bf16*>(w_hh);
-    p.hout = h;
-    p.hout16 = reinterpret_cast<bf16*>(h_bf16);
-    p.call = c;
-    p.gall = gates;
-    p.ctl = reinterpret_cast<unsigned*>(hbuf);
-    p.pay = reinterpret_cast<bf16*>(reinterpret_cast<char*>(hbuf) + px_payload_off(ng));
-    p.trace = g_trace;
-    p.fault = fault_word();
-    p.spin = spin_bound();
-    p.nap = nap();
-    p.B = B;
-    p.T = T;
-    p.ng = ng;
-    const bool gr = gran(false, H);
-    // flag form: only ctl + flags are polled; granule form: every tag of the payload too
-    if (avc_zero_async(hbuf, gr ? px_payload_off(ng) + (size_t)8 * B * H : px_ctl_bytes(ng), s)) return -1;
-    const dim3 grid(ng * (H / PJU));
-    if (H == 1024) gr ? lstm_persist_fwd<1024, true><<<grid, PNT, 0, s>>>(p) : lstm_persist_fwd<1024, false><<<grid, PNT, 0, s>>>(p);
-    else if (H == 768) gr ? lstm_persist_fwd<768, true><<<grid, PNT, 0, s>>>(p) : lstm_persist_fwd<768, false><<<grid, PNT, 0, s>>>(p);  // Adjust.py:30
-    else gr ? lstm_persist_fwd<512, true><<<grid, PNT, 0, s>>>(p) : lstm_persist_fwd<512, false><<<grid, PNT, 0, s>>>(p);
-    return avc_check_launch("avc_lstm_fwd(persistent)");
-  }
+  if (hbuf && persistent_path(B, H, dirs, bf, false))
+    return persist_fwd(xproj, 1, w_hh, B, T, H, h, h_bf16, c, gates, hbuf, s, "avc_lstm_fwd(persistent)");
   AVC_CHECK_ARG(h_bf16 == nullptr, "avc_lstm_fwd: the bf16 h copy is produced by the persistent path only");
   const int mt = (H >= 1024 && B > 16) ? 2 : 1;  // 256 workgroups at B = 64
   dim3 g(H / 8, cdiv(B, 16 * mt), dirs);
@@ -2424,34 +2485,9 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
   AVC_CHECK_ARG(w_hh_t && dcbuf, "avc_lstm_bwd: large-H path needs W_hh^T and dcbuf");
   const bool bf = compute == AVC_BF16;
   AVC_CHECK_ARG(!bf || (wdtype == AVC_BF16 && gbuf), "avc_lstm_bwd: bf16 compute needs bf16 W_hh^T and gbuf");
-  const int ng = (B + PRG - 1) / PRG;
-  if (persistent_path(B, H, dirs, bf, true)) {
-    // gbuf: control words + flags + the [2][B][4H] bf16 payload in this mode (layout above)
-    PersistBwdArgs p;
-    p.dhout = dh_out;
-    p.call = c;
-    p.gall = gates;
-    p.wt = reinterpret_cast<const bf16*>(w_hh_t);
-    p.dg = dgates;
-    p.dg16 = reinterpret_cast<bf16*>(dgates_bf16);
-    p.ctl = reinterpret_cast<unsigned*>(gbuf);
-    p.pay = reinterpret_cast<bf16*>(reinterpret_cast<char*>(gbuf) + px_payload_off(ng));
-    p.trace = g_trace;
-    p.fault = fault_word();
-    p.spin = spin_bound();
-    p.nap = nap();
-    p.B = B;
-    p.T = T;
-    p.ng = ng;
-    const bool gr = gran(true, H);
-    if (avc_zero_async(gbuf, gr ? px_payload_off(ng) + (size_t)32 * B * H : px_ctl_bytes(ng), s)) return -1;
-    // (persistent_path above set the dynamic-LDS attributes)
-    const dim3 grid(ng * (H / PJU));
-    if (H == 1024) launch_persist_bwd<1024>(grid, s, gr, p);
-    else if (H == 768) launch_persist_bwd<768>(grid, s, gr, p);
-    else launch_persist_bwd<512>(grid, s, gr, p);
-    return avc_check_launch("avc_lstm_bwd(persistent)");
-  }
+  if (persistent_path(B, H, dirs, bf, true))
+    return persist_bwd(dh_out, c, gates, w_hh_t, B, T, H, dgates, dgates_bf16, nullptr, nullptr, 1, gbuf, s,
+                       "avc_lstm_bwd(persistent)");
   AVC_CHECK_ARG(dgates_bf16 == nullptr, "avc_lstm_bwd: the bf16 dG twin is produced by the persistent path only");
   StepArgs a = {};
   a.w = w_hh_t;
@@ -2474,4 +2510,26 @@ extern "C" int avc_lstm_bwd(const float* dh_out, const float* h, const float* c,
     else lstm_step_bwd<false, 1><<<g, 256, 0, s>>>(a);
   }
   return avc_check_launch("avc_lstm_bwd");
+}
+
+extern "C" int avc_lstm_fwd_fold(const float* pcode, int nc, const void* w_hh, int B, int T, int H, float* h,
+                                 void* h_bf16, float* c, float* gates, void* hbuf, void* stream) {
+  AVC_CHECK_ARG(pcode && w_hh && h && h_bf16 && c && gates && hbuf && B > 0 && T > 0 && nc > 0 && T % nc == 0,
+                "avc_lstm_fwd_fold: bad args");
+  AVC_CHECK_ARG(persistent_path(B, H, 1, true, false), "avc_lstm_fwd_fold: B=%d H=%d is not on the persistent path",
+                B, H);
+  return persist_fwd(pcode, T / nc, w_hh, B, T, H, h, h_bf16, c, gates, hbuf, as_stream(stream),
+                     "avc_lstm_fwd_fold");
+}
+
+extern "C" int avc_lstm_bwd_fold(const float* dh_out, const float* c, const float* gates, const void* w_hh_t, int B,
+                                 int T, int H, int nc, float* dgates, void* dgates_bf16, float* s_code,
+                                 void* s_code_bf16, void* gbuf, void* stream) {
+  AVC_CHECK_ARG(dh_out && c && gates && w_hh_t && dgates_bf16 && s_code && gbuf && B > 0 && T > 0 && nc > 0 &&
+                    T % nc == 0,
+                "avc_lstm_bwd_fold: bad args");
+  AVC_CHECK_ARG(persistent_path(B, H, 1, true, true), "avc_lstm_bwd_fold: B=%d H=%d is not on the persistent path",
+                B, H);
+  return persist_bwd(dh_out, c, gates, w_hh_t, B, T, H, dgates, dgates_bf16, s_code, s_code_bf16, T / nc, gbuf,
+                     as_stream(stream), "avc_lstm_bwd_fold");
 }

@@ -659,6 +659,46 @@ def expand_codes(pc, pe, B, T, nc):
     return out
 
 
+def code_cat(codes, emb, B, nc, cd):
+    """(B*nc, cd+de) bf16 rows [code_j ; emb_b]: the folded lstm1's GEMM operand (avc_code_cat)."""
+    _dev(codes, emb)
+    de = emb.shape[1]
+    out = torch.empty(B * nc, cd + de, device=codes.device, dtype=torch.bfloat16)
+    L.call("avc_code_cat", codes.data_ptr(), emb.data_ptr(), out.data_ptr(), B, nc, cd, de, stream())
+    return out
+
+
+def lstm_fwd_fold(pcode, nc, w_hh, B, T, H, hbuf):
+    """Persistent lstm1 forward reading step t's input projection from pcode[b*nc + t // (T/nc)]
+    (avc_lstm_fwd_fold); returns h (bf16 twin attached), c, gates as lstm_fwd."""
+    _assert_no_collective("avc_lstm_fwd_fold")
+    dev = pcode.device
+    fault_word(dev)
+    h = torch.empty(B * T, H, device=dev)
+    h16 = torch.empty(B * T, H, device=dev, dtype=torch.bfloat16)
+    c = torch.empty(B * T, H, device=dev)
+    g = torch.empty(B * T, 4 * H, device=dev)
+    L.call("avc_lstm_fwd_fold", pcode.data_ptr(), nc, w_hh.data_ptr(), B, T, H, h.data_ptr(), h16.data_ptr(),
+           c.data_ptr(), g.data_ptr(), hbuf.data_ptr(), stream())
+    return attach_twin(h, h16), c, g
+
+
+def lstm_bwd_fold(dh, c, g, w_hh_t, B, T, H, nc, gbuf=None):
+    """Persistent lstm1 backward (avc_lstm_bwd_fold): dG as bf16 only, and s_code (B*nc, 4H) =
+    dG summed over each code's frames (fp32, bf16 twin attached)."""
+    _assert_no_collective("avc_lstm_bwd_fold")
+    dev = dh.device
+    fault_word(dev)
+    if gbuf is None:
+        gbuf = lstm_bwd_scratch(B, H, 1, dev)
+    dg16 = torch.empty(B * T, 4 * H, device=dev, dtype=torch.bfloat16)
+    sc = torch.empty(B * nc, 4 * H, device=dev)
+    sc16 = torch.empty(B * nc, 4 * H, device=dev, dtype=torch.bfloat16)
+    L.call("avc_lstm_bwd_fold", dh.data_ptr(), c.data_ptr(), g.data_ptr(), w_hh_t.data_ptr(), B, T, H, nc, None,
+           dg16.data_ptr(), sc.data_ptr(), sc16.data_ptr(), gbuf.data_ptr(), stream())
+    return dg16, attach_twin(sc, sc16)
+
+
 def dec_concat_bwd(dout, B, T, nc, cd, de):
     dcodes = torch.empty(B, nc * cd, device=dout.device)
     L.call("avc_dec_concat_bwd", dout.data_ptr(), dcodes.data_ptr(), B, T, nc, cd, de, stream())

@@ -1063,11 +1063,15 @@ def lstm(mod, cores, x, B, T):
 class _LSTM1FoldFn(torch.autograd.Function):
     """Decoder lstm1 on cat(code expansion, c_trg broadcast) (AutoVC.py:96,103,197-204) with the
     input projection folded per code and per utterance: W_ih . [code_j ; e] + b =
-    Wc . code_j + (We . e + b), computed once per code (B*nc rows) and once per utterance (B
-    rows) and expanded to the B*T frames, instead of a (B*T, cd+de) concat and its B*T x 4H x
-    (cd+de) GEMM.  The backward is folded the same way: the gate gradients dG are summed over
-    each code's frames (S_code) and each utterance (S_utt) first, then
-      dcodes = S_code . Wc,  dc_trg = S_utt . We,  dWc = S_code^T codes,  dWe = S_utt^T c_trg,
+    Wc . code_j + (We . e + b), computed once per code instead of a (B*T, cd+de) concat and its
+    B*T x 4H x (cd+de) GEMM.  On the persistent path (bf16) that is ONE GEMM over the (B*nc, cd+de)
+    rows [code_j ; e_b] (avc_code_cat) and the recurrence reads row b*nc + t/(T/nc) itself
+    (avc_lstm_fwd_fold); elsewhere a per-code and a per-utterance GEMM expanded to the B*T frames
+    (avc_expand_codes).  The backward is folded the same way: the gate gradients dG are summed over
+    each code's frames (S_code; inside the persistent recurrence, avc_lstm_bwd_fold) and each
+    utterance (S_utt) first, then
+      dcodes = S_code . Wc,  dc_trg = S_utt . We,  dWc = S_code^T codes,  dWe = S_utt^T c_trg
+      (= dW_ih = S_code^T [codes ; c_trg] over the code rows on the persistent path),
       db_ih = db_hh = colsum(S_code).
     `hook` (nullable) runs once every decoder / postnet gradient has been enqueued (the
     training step's overlapped decoder-slice all-reduce and Adam, train.py)."""
@@ -1080,16 +1084,26 @@ class _LSTM1FoldFn(torch.autograd.Function):
         In = cd + de
         wih, bsum, whh, _, _ = core.packs()
         dev = codes.device
-        c2 = codes.reshape(B * nc, cd)
-        pc = torch.empty(B * nc, G, device=dev)
-        K.gemm(B * nc, G, cd, operand(c2, cd), operand(wih, In), pc)
-        pe = torch.empty(B, G, device=dev)
-        K.gemm(B, G, de, operand(emb, de), operand(wih[:, cd:], In), pe, bias=bsum)
-        xproj = K.expand_codes(pc, pe, B, T, nc)
         hbuf = K.lstm_scratch(B, H, 1, dev) if H > 64 and K.compute() == K.BF16 else None
-        h, c, g = K.lstm_fwd(xproj, whh, B, T, H, 1, hbuf)
+        xcat = None
+        if hbuf is not None and T % nc == 0 and K.lstm_persistent_fwd(B, H, 1) and K.lstm_persistent_bwd(B, H, 1):
+            # one row per code, [code_j ; c_trg_b] in bf16: ONE GEMM gives every code's projection
+            # incl. the per-utterance half and the bias, and the recurrence reads row b*nc + t/(T/nc)
+            # itself (no (B*T, 4H) expansion)
+            xcat = K.code_cat(codes, emb, B, nc, cd)
+            pcode = torch.empty(B * nc, G, device=dev)
+            K.gemm(B * nc, G, In, operand(xcat, In), operand(wih, In), pcode, bias=bsum)
+            h, c, g = K.lstm_fwd_fold(pcode, nc, whh, B, T, H, hbuf)
+        else:
+            c2 = codes.reshape(B * nc, cd)
+            pc = torch.empty(B * nc, G, device=dev)
+            K.gemm(B * nc, G, cd, operand(c2, cd), operand(wih, In), pc)
+            pe = torch.empty(B, G, device=dev)
+            K.gemm(B, G, de, operand(emb, de), operand(wih[:, cd:], In), pe, bias=bsum)
+            xproj = K.expand_codes(pc, pe, B, T, nc)
+            h, c, g = K.lstm_fwd(xproj, whh, B, T, H, 1, hbuf)
         ctx.core, ctx.args, ctx.hook = core, (B, T, nc, cd), hook
-        ctx.saved = (c, g)
+        ctx.saved = (c, g, xcat)
         ctx.save_for_backward(codes, emb, h)
         ctx.h16 = getattr(h, "_bf16", None)
         return h
@@ -1100,18 +1114,24 @@ class _LSTM1FoldFn(torch.autograd.Function):
         K.attach_twin(h, ctx.h16)
         core = ctx.core
         B, T, nc, cd = ctx.args
-        c, g = ctx.saved
+        c, g, xcat = ctx.saved
         H = core.H
         G = 4 * H
         de = emb.shape[1]
         In = cd + de
         _, _, whh, whh_t, wih_t = core.packs()
         dev = h.device
-        dg = K.lstm_bwd(dh.contiguous(), h, c, g, whh if H <= 64 else None, whh_t, B, T, H, 1)
         M = B * T
         c2 = codes.reshape(B * nc, cd)
-        s_code = K.segsum(dg, B * nc, T // nc, G, ld=G)  # (B*nc, G): dG summed over each code's frames
-        s_utt = K.segsum(s_code, B, nc, G, ld=G)          # (B, G): ... and over each utterance
+        if xcat is not None:
+            # dG (bf16 only) and s_code = dG summed over each code's frames, both out of the recurrence
+            dg, s_code = K.lstm_bwd_fold(dh.contiguous(), c, g, whh_t, B, T, H, nc)
+        else:
+            dg = K.lstm_bwd(dh.contiguous(), h, c, g, whh if H <= 64 else None, whh_t, B, T, H, 1)
+            s_code = K.segsum(dg, B * nc, T // nc, G, ld=G)  # (B*nc, G): dG summed over each code's frames
+        s_utt = None
+        if xcat is None or ctx.needs_input_grad[1]:
+            s_utt = K.segsum(s_code, B, nc, G, ld=G)  # (B, G): ... and over each utterance
         dcodes = demb = None
         # few output tiles, K = 4H: split K (atomic fp32 accumulation into zeroed outputs).  More
         # than two atomic partials make the sum order-dependent, so the fp32 parity mode keeps
@@ -1133,10 +1153,14 @@ class _LSTM1FoldFn(torch.autograd.Function):
 
         def wgrads():
             dwih = _grad_of(w_ih) if sink else torch.zeros(G, In, device=dev)
-            K.gemm(G, cd, B * nc, operand(s_code, G, kstrided=True), operand(c2, cd, kstrided=True), dwih, ldc=In,
-                   accumulate=True, split_k=K.auto_split_k(G, cd, B * nc))
-            K.gemm(G, de, B, operand(s_utt, G, kstrided=True), operand(emb, de, kstrided=True), dwih[:, cd:],
-                   ldc=In, accumulate=True)
+            if xcat is not None:  # sum_j s_code[b,j] c_trg[b] = s_utt[b] c_trg[b]: one product over the code rows
+                K.gemm(G, In, B * nc, operand(s_code, G, kstrided=True), operand(xcat, In, kstrided=True), dwih,
+                       ldc=In, accumulate=True, split_k=K.auto_split_k(G, In, B * nc))
+            else:
+                K.gemm(G, cd, B * nc, operand(s_code, G, kstrided=True), operand(c2, cd, kstrided=True), dwih,
+                       ldc=In, accumulate=True, split_k=K.auto_split_k(G, cd, B * nc))
+                K.gemm(G, de, B, operand(s_utt, G, kstrided=True), operand(emb, de, kstrided=True), dwih[:, cd:],
+                       ldc=In, accumulate=True)
             dwhh = _grad_of(w_hh) if sink else torch.empty(G, H, device=dev)
             K.gemm(G, H, M, operand(dg, G, kstrided=True), operand(h_op, H, kstrided=True, window=(1, 1, T, T, H)),
                    dwhh, split_k=K.auto_split_k(G, H, M), accumulate=sink)
@@ -1148,7 +1172,7 @@ class _LSTM1FoldFn(torch.autograd.Function):
         ev = mark()
         if sink:
             with _Side(ev) as sd:
-                sd.keep(dg, h, h_op, s_code, s_utt, c2, emb)
+                sd.keep(dg, h, h_op, s_code, s_utt, c2, emb, xcat)
                 if not _ABLATE_WGRAD:
                     wgrads()
             grads = [None] * 4

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AVC_ABI_VERSION 30
+#define AVC_ABI_VERSION 31
 
 enum { AVC_F32 = 0, AVC_BF16 = 1 };
 enum { AVC_ACT_NONE = 0, AVC_ACT_RELU = 1, AVC_ACT_TANH = 2, AVC_ACT_LEAKY = 3, AVC_ACT_GELU = 4, AVC_ACT_SIGMOID = 5 };
@@ -255,6 +255,22 @@ int avc_lstm_bwd(const float* dh_out, const float* h, const float* c, const floa
                  const void* w_hh, const void* w_hh_t, int wdtype, int B, int T, int H, int dirs,
                  float* dgates, void* dgates_bf16, float* dcbuf, void* gbuf, int compute, void* stream);
 
+/* Decoder lstm1 with the input projection folded per code (ABI 31; AutoVC.py:96,103 on the concat
+ * of AutoVC.py:197-204): the persistent forward above reading step t's projection
+ * from row b*nc + t/(T/nc) of pcode (B*nc, 4H) fp32 = [code_j ; c_trg_b] . W_ih^T + b_ih + b_hh,
+ * without expanding it to B*T rows.  Persistent path only (bf16 compute, avc_lstm_persistent(B, H,
+ * 1, AVC_BF16, 0)), T % nc == 0; h_bf16 and hbuf as avc_lstm_fwd.  Replaces avc_expand_codes +
+ * avc_lstm_fwd there. */
+int avc_lstm_fwd_fold(const float* pcode, int nc, const void* w_hh, int B, int T, int H, float* h,
+                      void* h_bf16, float* c, float* gates, void* hbuf, void* stream);
+/* Its backward: the persistent backward writing dG's bf16 twin (dgates_bf16, required), dgates
+ * fp32 only when non-null, and s_code (B*nc, 4H) = dG summed over each code's T/nc frames (fp32,
+ * plus its bf16 twin s_code_bf16 when non-null) -- the fold's segment sum taken inside the
+ * recurrence instead of a pass over dG afterwards (avc_segsum).  gbuf as avc_lstm_bwd. */
+int avc_lstm_bwd_fold(const float* dh_out, const float* c, const float* gates, const void* w_hh_t,
+                      int B, int T, int H, int nc, float* dgates, void* dgates_bf16, float* s_code,
+                      void* s_code_bf16, void* gbuf, void* stream);
+
 /* Two stacked unidirectional layers of one nn.LSTM (decoder lstm2, AutoVC.py:96,110: 512 -> 1024,
  * num_layers=2) forward in ONE persistent launch, as a layer wavefront (tick k = layer 0 step k
  * beside layer 1 step k-1; layer 1's input projection inside the recurrence).  xproj0 (B,T,4H) =
@@ -356,6 +372,11 @@ int avc_dec_concat_bwd(const float* dout, float* dcodes, int B, int T, int n_cod
  * AutoVC.py:96,103 on the concat of AutoVC.py:197-204, without the concat or its (B*T x G x cd+de)
  * GEMM.  G % 4 == 0, 16-B aligned. */
 int avc_expand_codes(const float* pc, const float* pe, float* out, int B, int T, int nc, int G, void* stream);
+/* The folded lstm1's operand (ABI 31): out[b*nc + j] = [codes[b][j*cd : (j+1)*cd] ; emb[b]] in bf16,
+ * (B*nc, cd+de) -- one row per code, so ONE GEMM out . W_ih^T + b gives avc_lstm_fwd_fold's pcode and
+ * the weight gradient is s_code^T . out (the per-utterance half sums to s_utt^T . c_trg). */
+int avc_code_cat(const float* codes, const float* emb, void* out_bf16, int B, int nc, int cd, int de,
+                 void* stream);
 
 /* Weight repacks (and fp32 -> compute dtype).  conv: W[co][ci][k] ->
  *   mode 0: Wf[co][k][ci] (forward im2col order)

@@ -44,7 +44,7 @@ def test_python_binding_covers_header(lib):
 
 
 def test_abi_version_and_error_channel(lib):
-    assert lib.avc_abi_version() == 30
+    assert lib.avc_abi_version() == 31
     assert isinstance(lib.avc_last_error(), bytes)
 
 
