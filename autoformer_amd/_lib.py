@@ -56,10 +56,11 @@ class BnbArgs(ctypes.Structure):
 
 class PackOp(ctypes.Structure):
     _fields_ = [("src", c_void_p), ("src2", c_void_p), ("dst", c_void_p), ("kind", c_int), ("out_dtype", c_int),
-                ("d0", c_int), ("d1", c_int), ("d2", c_int), ("pad_", c_int), ("ld_out", c_ll)]
+                ("d0", c_int), ("d1", c_int), ("d2", c_int), ("pad_", c_int), ("ld_out", c_ll),
+                ("ci0", c_int), ("cn", c_int), ("cpad", c_int), ("mode", c_int)]
 
 
-PACK_COPY, PACK_TRANSPOSE, PACK_CONV_F, PACK_CONV_D, PACK_ADD = 0, 1, 2, 3, 4
+PACK_COPY, PACK_TRANSPOSE, PACK_CONV_F, PACK_CONV_D, PACK_ADD, PACK_CONV_SLICE = 0, 1, 2, 3, 4, 5
 
 
 _SIGS = {

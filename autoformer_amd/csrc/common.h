@@ -83,6 +83,35 @@ __device__ __forceinline__ float erf_nb(float x) {
   const float near = fmaf(t, r, t);
   return copysignf(t < 1.f ? near : far, x);
 }
+// Element i of a channel-slice pack of conv weight W [Co][Ci][K] (fp32) -- input channels
+// [ci0, ci0 + cn) of the conv0 fold, zero-padded to cpad (avc_conv_pack_slice, avc_pack_batch):
+//   mode 0: [Co][K][cpad]   mode 1: [cpad][K-1-k][Co]   mode 2: [K][Co][cpad]
+//   mode 3: [cn][K-1-k][cpad] with the OUTPUT channel axis padded to cpad
+__device__ __forceinline__ float slice_val(const float* w, int Co, int Ci, int K, int ci0, int cn, int cpad, int mode,
+                                           long long i) {
+  int co, ci, k;
+  if (mode == 3) {
+    co = (int)(i % cpad);
+    k = K - 1 - (int)((i / cpad) % K);
+    ci = (int)(i / ((long long)cpad * K));
+    return co < Co ? w[((long long)co * Ci + ci0 + ci) * K + k] : 0.f;
+  }
+  if (mode == 0) {
+    ci = (int)(i % cpad);
+    k = (int)((i / cpad) % K);
+    co = (int)(i / ((long long)cpad * K));
+  } else if (mode == 1) {
+    co = (int)(i % Co);
+    k = K - 1 - (int)((i / Co) % K);
+    ci = (int)(i / ((long long)Co * K));
+  } else {
+    ci = (int)(i % cpad);
+    co = (int)((i / cpad) % Co);
+    k = (int)(i / ((long long)cpad * Co));
+  }
+  return ci < cn ? w[((long long)co * Ci + ci0 + ci) * K + k] : 0.f;
+}
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 __device__ __forceinline__ float act_fwd(float x, int act) {

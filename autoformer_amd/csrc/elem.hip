@@ -369,11 +369,12 @@ __global__ void vc_loss_grad_kernel(const float* __restrict__ x, const float* __
   }
 }
 
-// Batched weight packing (avc_pack_batch).  The launch is cut into UNITS: 1024 elements of an
-// elementwise op (copy / add / conv re-layout, walked along the source, 4 per thread), or one
-// 32 x 32 tile of a transpose (staged through LDS so both the fp32 reads and the bf16 writes are
-// coalesced).  prefix[i] = first unit of op i; a block finds its op by one block-uniform binary
-// search per unit (<= 128 ops).
+// Batched weight packing (avc_pack_batch).  The launch is cut into UNITS: a 64 x 64 tile of a
+// transpose or a conv tile (staged through LDS so both the fp32 reads and the bf16 writes are
+// coalesced), or 4096 elements of anything else (copy / add: float4 along the source; a channel
+// slice of the conv0 fold or an oversized conv: scalar, along the destination / source).
+// prefix[i] = first unit of op i; a block finds its op by one block-uniform binary search per
+// unit (<= 128 ops).
 constexpr int PACK_MAX_OPS = 128;
 
 __device__ __forceinline__ void put4(void* dst, long long i, float4 v, int dtype) {
@@ -459,6 +460,17 @@ __global__ void __launch_bounds__(256) pack_batch_kernel(const avc_pack_op* __re
     }
     if (op.kind == AVC_PACK_CONV_D && op.d2 <= PK_KMAX_D) {
       conv_pack_unit(op.src, op.dst, op.out_dtype, op.d0, op.d1, op.d2, 1, lu, buf);
+      continue;
+    }
+    if (op.kind == AVC_PACK_CONV_SLICE) {  // avc_conv_pack_slice's layouts, one element per thread-step
+      const int Co = op.d0, Ci = op.d1, K = op.d2, cpad = op.cpad, cn = op.cn;
+      const long long n = (long long)(op.mode == 3 ? cn : Co) * cpad * K;
+#pragma unroll 4
+      for (int j = 0; j < 16; ++j) {
+        const long long i = lu * 4096 + j * 256 + tid;
+        if (i >= n) break;
+        putd(op.dst, i, slice_val(op.src, Co, Ci, K, op.ci0, cn, cpad, op.mode, i), op.out_dtype);
+      }
       continue;
     }
     const bool conv = op.kind == AVC_PACK_CONV_F || op.kind == AVC_PACK_CONV_D;

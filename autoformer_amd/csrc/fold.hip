@@ -28,29 +28,7 @@ __global__ void conv_pack_slice_kernel(const float* __restrict__ w, void* __rest
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long total = (long long)(mode == 3 ? cn : Co) * cpad * K;
   if (i >= total) return;
-  int co, ci, k;
-  if (mode == 3) {  // out[cn][k'][cpad], k' = K-1-k: the OUTPUT channel axis padded (data-gradient pack)
-    co = (int)(i % cpad);
-    k = K - 1 - (int)((i / cpad) % K);
-    ci = (int)(i / ((long long)cpad * K));
-    put(out, i, co < Co ? w[((long long)co * Ci + ci0 + ci) * K + k] : 0.f, dtype);
-    return;
-  }
-  if (mode == 0) {  // out[co][k][cpad]
-    ci = (int)(i % cpad);
-    k = (int)((i / cpad) % K);
-    co = (int)(i / ((long long)cpad * K));
-  } else if (mode == 1) {  // out[cpad][k'][co], k' = K-1-k
-    co = (int)(i % Co);
-    k = K - 1 - (int)((i / Co) % K);
-    ci = (int)(i / ((long long)Co * K));
-  } else {  // mode 2: out[k][co][cpad]
-    ci = (int)(i % cpad);
-    co = (int)((i / cpad) % Co);
-    k = (int)(i / ((long long)cpad * Co));
-  }
-  const float v = ci < cn ? w[((long long)co * Ci + ci0 + ci) * K + k] : 0.f;
-  put(out, i, v, dtype);
+  put(out, i, slice_val(w, Co, Ci, K, ci0, cn, cpad, mode, i), dtype);
 }
 
 // S[b][cls][co] = sum_{k valid for cls} E[b][k*Co + co]; cls = 0..pad-1 (t = cls), pad (interior),

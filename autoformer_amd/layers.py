@@ -331,16 +331,21 @@ def _op_struct(o):
     d = list(o["dims"]) + [0, 0, 0]
     st.d0, st.d1, st.d2 = d[0], d[1], d[2]
     st.ld_out = o.get("ld", 0)
+    if "slice" in o:  # CONV_SLICE: (ci0, cn, cpad, mode)
+        st.ci0, st.cn, st.cpad, st.mode = o["slice"]
     return st
 
 
 def _op_len(o):
     """Units of an op in avc_pack_batch (elem.hip pack_batch_kernel): a 64 x 64 transpose tile; an LDS-staged
     conv tile (Wf: 4 output x 64 input channels for <= 16 taps, Wd: 32 x 16 for <= 8 taps); else 4096
-    elements."""
-    from ._lib import PACK_CONV_D, PACK_CONV_F, PACK_TRANSPOSE
+    elements (of the destination for a conv0-fold channel slice)."""
+    from ._lib import PACK_CONV_D, PACK_CONV_F, PACK_CONV_SLICE, PACK_TRANSPOSE
 
     d = o["dims"]
+    if o["kind"] == PACK_CONV_SLICE:
+        _, cn, cpad, mode = o["slice"]
+        return -(-((cn if mode == 3 else d[0]) * cpad * d[2]) // 4096)
     if o["kind"] == PACK_TRANSPOSE:
         return -(-d[0] // 64) * -(-d[1] // 64)
     if o["kind"] == PACK_CONV_F and d[2] <= 16:
@@ -563,13 +568,20 @@ class ConvBNCore:
         if not hasattr(self, "fold_cache"):
             self.fold_cache = PackCache()
 
+        Co, Ci, Kw = w.shape
+        slices = ((0, nm, cp, 0), (0, nm, nm, 1), (nm, Ci - nm, Ci - nm, 2))
+
         def build():
             dt = K.compute()
-            Ci = w.shape[1]
             # (an fp32 speaker term on the generic fp32 kernel cost 51 us for this 64-row product)
-            return (K.conv_pack_slice(w, 0, nm, cp, 0, dt), K.conv_pack_slice(w, 0, nm, nm, 1, dt),
-                    K.conv_pack_slice(w, nm, Ci - nm, Ci - nm, 2, dt))
-        return self.fold_cache.get([w], build)
+            return tuple(K.conv_pack_slice(w, ci0, cn, cpad, mode, dt) for ci0, cn, cpad, mode in slices)
+
+        def ops(val):  # the same three slices inside the batched repack (avc_pack_batch CONV_SLICE)
+            from ._lib import PACK_CONV_SLICE
+
+            return [{"src": w.data_ptr(), "dst": t.data_ptr(), "kind": PACK_CONV_SLICE, "dtype": K._dt(t),
+                     "dims": (Co, Ci, Kw), "slice": sl} for t, sl in zip(val, slices)]
+        return self.fold_cache.get([w], build, ops=ops)
 
     def backward(self, dA, x, a, saved, B, T_in, n_dx, self_link=None, prev_link=None):
         """self_link: this layer's BnbLink (its BN backward statistics may already have been
@@ -753,12 +765,21 @@ class _EncConv0FoldFn(torch.autograd.Function):
         Wmf, _, We = core.fold_packs(nm, cp)
         dev = mel2d.device
         xm = K.pad_cols(mel2d, cp, dtype=K.compute())
-        # a fresh compute-dtype copy of emb, never attached to it: a caller may refill emb in
-        # place (a captured step fed through the same input tensors), a cached twin would go stale
-        e = K.convert(emb, K.BF16) if K.compute() == K.BF16 else emb
-        E = torch.empty(B, Kw * Co, device=dev)
-        K.gemm(B, Kw * Co, de, operand(e, de), operand(We, de), E)
-        S = K.conv_edge_table(E, B, Co, Kw, T, pad)
+        # the speaker term's edge table depends on emb and the weights only: the encoder re-pass on
+        # mel_postnet (same c_org, same weights) reuses the first pass's table (a recorded step replays
+        # the reuse; a refilled emb bumps its version, an Adam step the pack epoch)
+        key = (_pack_key([core.conv.weight]), emb._version, B, T)
+        hit = getattr(core, "_edge", None)
+        if hit is not None and hit[0]() is emb and hit[1] == key:
+            S = hit[2]
+        else:
+            # a fresh compute-dtype copy of emb, never attached to it: a caller may refill emb in
+            # place (a captured step fed through the same input tensors), a cached twin would go stale
+            e = K.convert(emb, K.BF16) if K.compute() == K.BF16 else emb
+            E = torch.empty(B, Kw * Co, device=dev)
+            K.gemm(B, Kw * Co, de, operand(e, de), operand(We, de), E)
+            S = K.conv_edge_table(E, B, Co, Kw, T, pad)
+            core._edge = (weakref.ref(emb), key, S)
         a, saved = core.conv_bn_act(operand(xm, cp, window=(Kw, pad, T, T, cp)), operand(Wmf, Kw * cp), Kw * cp,
                                     B * T, T, dev, None, out_bf16, row_bias=(S, T, pad))
         ctx.core, ctx.B, ctx.T, ctx.saved, ctx.dims = core, B, T, saved, (nm, de, cp)
@@ -1197,6 +1218,20 @@ def copy_pack_ops(w, val):
     return [{"src": w.data_ptr(), "dst": val.data_ptr(), "kind": PACK_COPY, "dtype": K._dt(val), "dims": (w.numel(),)}]
 
 
+def _linear_packs(cache, w):
+    """(w, w^T) in the compute dtype: the forward's and the data gradient's K-contiguous B operands."""
+    from ._lib import PACK_TRANSPOSE
+
+    def build():
+        return K.convert(w, K.compute()), K.transpose(w, K.compute())
+
+    def ops(val):
+        wc, wt = val
+        return copy_pack_ops(w, wc) + [{"src": w.data_ptr(), "dst": wt.data_ptr(), "kind": PACK_TRANSPOSE,
+                                        "dtype": K._dt(wt), "dims": tuple(w.shape), "ld": w.shape[0]}]
+    return cache.get([w], build, ops=ops)
+
+
 class _LinearFn(torch.autograd.Function):
     """LinearNorm (Norm.py:40-50) on frame-major rows."""
 
@@ -1204,7 +1239,7 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b, cache):
         M, In = x.shape
         Out = w.shape[0]
-        wc = cache.get([w], lambda: K.convert(w, K.compute()), ops=lambda val: copy_pack_ops(w, val))
+        wc, _ = _linear_packs(cache, w)
         y = torch.empty(M, Out, device=x.device)
         K.gemm(M, Out, In, operand(x, In), operand(wc, In), y, bias=b)
         ctx.cache = cache
@@ -1220,6 +1255,11 @@ class _LinearFn(torch.autograd.Function):
         Out = w.shape[0]
         sink = _SINK["on"]
         b = ctx.bias
+        if K.compute() == K.BF16 and getattr(dy, "_bf16", None) is None:
+            # a bf16 operand (the products round to bf16 either way) puts the data gradient on the
+            # LDS-staged NT kernels instead of the register-staged fp32-operand path (29 -> ~13 us
+            # for the decoder projection's 8192 x 1024 x 80), and the weight gradient on the TT kernel
+            K.attach_twin(dy, K.convert(dy, K.BF16))
 
         def wgrad():
             dw = _grad_of(w) if sink else torch.empty(Out, In, device=x.device)
@@ -1230,9 +1270,9 @@ class _LinearFn(torch.autograd.Function):
         ev = mark()
         dx = None
         if ctx.needs_input_grad[0]:
-            wc = ctx.cache.get([w], lambda: K.convert(w, K.compute()))
+            _, wt = _linear_packs(ctx.cache, w)
             dx = torch.empty(M, In, device=x.device)
-            K.gemm(M, In, Out, operand(dy, Out), operand(wc, In, kstrided=True), dx)
+            K.gemm(M, In, Out, operand(dy, Out), operand(wt, Out), dx)
         if sink:
             with _Side(ev) as sd:
                 sd.keep(dy, x)

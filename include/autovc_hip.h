@@ -500,13 +500,16 @@ int avc_transpose_batched2(const void* src, int src_dtype, float* dst, void* dst
                            int accumulate, void* stream);
 
 /* Batched weight packing: every bf16 / re-laid-out copy of the parameters the kernels read
- * (conv Wf / Wd, LSTM W_ih / W_hh / W_hh^T / W_ih^T, b_ih + b_hh, linear W) rebuilt after the
- * optimizer step in ONE launch instead of one small kernel per copy.  `ops` and `prefix`
- * (device memory, caller-owned): op i covers UNITS [prefix[i], prefix[i+1]) of the launch, a
- * unit being 1024 elements of a copy / add / conv re-layout (ceil(n / 1024) units) or one
- * 32 x 32 tile of a transpose (ceil(d0 / 32) * ceil(d1 / 32) units); total = prefix[nops];
- * nops <= 128. */
-enum { AVC_PACK_COPY = 0, AVC_PACK_TRANSPOSE = 1, AVC_PACK_CONV_F = 2, AVC_PACK_CONV_D = 3, AVC_PACK_ADD = 4 };
+ * (conv Wf / Wd, the conv0 fold's channel-slice packs, LSTM W_ih / W_hh / W_hh^T / W_ih^T,
+ * b_ih + b_hh, linear W and W^T) rebuilt after the optimizer step in ONE launch instead of one
+ * small kernel per copy.  `ops` and `prefix` (device memory, caller-owned): op i covers UNITS
+ * [prefix[i], prefix[i+1]) of the launch, a unit being one 64 x 64 tile of a transpose
+ * (ceil(d0 / 64) * ceil(d1 / 64) units), one LDS-staged conv tile (CONV_F with K <= 16: 4 output x
+ * 64 input channels, ceil(d0 / 4) * ceil(d1 / 64) units; CONV_D with K <= 8: 32 x 16,
+ * ceil(d0 / 32) * ceil(d1 / 16) units) or 4096 elements of anything else (ceil(n / 4096) units);
+ * total = prefix[nops]; nops <= 128. */
+enum { AVC_PACK_COPY = 0, AVC_PACK_TRANSPOSE = 1, AVC_PACK_CONV_F = 2, AVC_PACK_CONV_D = 3, AVC_PACK_ADD = 4,
+       AVC_PACK_CONV_SLICE = 5 };
 typedef struct {
   const float* src;   /* the fp32 parameter */
   const float* src2;  /* AVC_PACK_ADD: second addend (b_hh), else null */
@@ -515,9 +518,11 @@ typedef struct {
   int out_dtype;      /* AVC_F32 / AVC_BF16 */
   int d0, d1, d2;     /* COPY / ADD: n = d0.  TRANSPOSE: src [d0][d1] -> dst[c*ld_out + r].
                          CONV_F: W [d0=Co][d1=Ci][d2=K] -> dst[co][k*Ci + ci];
-                         CONV_D: -> dst[ci][(K-1-k)*Co + co] (flipped taps: the data-gradient operand) */
+                         CONV_D: -> dst[ci][(K-1-k)*Co + co] (flipped taps: the data-gradient operand);
+                         CONV_SLICE: W [d0=Co][d1=Ci][d2=K] -> avc_conv_pack_slice(ci0, cn, cpad, mode) */
   int pad_;
   long long ld_out;   /* TRANSPOSE: destination row stride (>= d0) */
+  int ci0, cn, cpad, mode;  /* CONV_SLICE only (ABI 31) */
 } avc_pack_op;
 int avc_pack_batch(const avc_pack_op* ops, const long long* prefix, int nops, long long total, void* stream);
 

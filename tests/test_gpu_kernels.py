@@ -710,7 +710,7 @@ def test_conv_pack_matches_permute(Co, Ci, Kw):
 def test_pack_batch_matches_individual_packs(Co, Ci, G, In, H):
     """avc_pack_batch (one launch for many packs) == the per-pack kernels it replaces, on ragged shapes too
     (tails of the 64 x 64 transpose tiles, the 4096-element copy units and the conv tiles; odd sizes take
-    the unaligned scalar forms)."""
+    the unaligned scalar forms), the conv0 fold's channel-slice packs in all four layouts included."""
     import autoformer_amd as A
     from autoformer_amd import kernels as Kr
     from autoformer_amd import layers as Lyr
@@ -720,10 +720,14 @@ def test_pack_batch_matches_individual_packs(Co, Ci, G, In, H):
     w = torch.randn(Co, Ci, 5, device=dev)
     wih, whh = torch.randn(G, In, device=dev), torch.randn(G, H, device=dev)
     bih, bhh = torch.randn(G, device=dev), torch.randn(G, device=dev)
+    # the conv0 fold's channel slices (avc_conv_pack_slice modes 0-3: padded, flipped, per tap, padded Co)
+    nm = Ci // 3 + 1
+    slices = [(0, nm, nm + 7, 0), (0, nm, nm, 1), (nm, Ci - nm, Ci - nm, 2), (1, Ci - 2, Co + 5, 3)]
     ref = [Kr.conv_pack(w, 0, Kr.BF16), Kr.conv_pack(w, 1, Kr.BF16), Kr.convert(wih, Kr.BF16),
            Kr.transpose(whh, Kr.BF16), Kr.add(bih, bhh)]
+    ref += [Kr.conv_pack_slice(w, *sl, Kr.BF16) for sl in slices]
     outs = [torch.empty_like(t) for t in ref]
-    from autoformer_amd._lib import PACK_ADD, PACK_CONV_D, PACK_CONV_F, PACK_COPY, PACK_TRANSPOSE
+    from autoformer_amd._lib import PACK_ADD, PACK_CONV_D, PACK_CONV_F, PACK_CONV_SLICE, PACK_COPY, PACK_TRANSPOSE
     ops = [{"src": w.data_ptr(), "dst": outs[0].data_ptr(), "kind": PACK_CONV_F, "dtype": Kr.BF16, "dims": (Co, Ci, 5)},
            {"src": w.data_ptr(), "dst": outs[1].data_ptr(), "kind": PACK_CONV_D, "dtype": Kr.BF16, "dims": (Co, Ci, 5)},
            {"src": wih.data_ptr(), "dst": outs[2].data_ptr(), "kind": PACK_COPY, "dtype": Kr.BF16, "dims": (G * In,)},
@@ -731,6 +735,8 @@ def test_pack_batch_matches_individual_packs(Co, Ci, G, In, H):
             "dims": (G, H), "ld": G},
            {"src": bih.data_ptr(), "src2": bhh.data_ptr(), "dst": outs[4].data_ptr(), "kind": PACK_ADD,
             "dtype": Kr.F32, "dims": (G,)}]
+    ops += [{"src": w.data_ptr(), "dst": o.data_ptr(), "kind": PACK_CONV_SLICE, "dtype": Kr.BF16, "dims": (Co, Ci, 5),
+             "slice": sl} for o, sl in zip(outs[5:], slices)]
 
     class _C:  # the PackCache surface _batch_plan reads
         pass
