@@ -2040,6 +2040,8 @@ void set_bwd_lds_attr() {
 // payload is at most 16 KB -- the forward at H <= 512 (lstm1: 2.24 -> 1.74 us per step) --
 // and the flag form above that (H = 1024 forward 3.08 vs 3.26 us, backward 4.03 vs 4.43 us:
 // the doubled payload fetch costs more than the drain and the flag round trip it saves).
+// (round 6: the granule form for the lstm1 backward too, H = 512, 64 KB granule payload per consumer: C2 5.53-5.55
+// vs 5.50 ms, profiles/r6_gran_bwd512_ab.txt)
 bool gran(bool bwd, int H) { return !bwd && (size_t)PRG * H * 4 <= 16384; }
 int nap() { return 0; }  // s_sleep(1)s between the granule form's failed sweeps (none measured best)
 

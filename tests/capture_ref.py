@@ -3,7 +3,7 @@
 `Capture` wraps the kernels-module entry points that carry the step's arithmetic -- every GEMM
 (conv windows, halo conv / halo dW, split-K weight gradients, the lstm1 fold products, fused
 bias / residual / BN-statistics / BN-finalize / bf16-twin / cperm epilogues), the persistent and
-wavefront LSTM recurrences, the small-H BiLSTM, the BN apply / backward passes, the code
+wavefront LSTM recurrences (the folded lstm1's included), the small-H BiLSTM, the BN apply / backward passes, the code
 expansion, the MetaFormer blocks (GroupNorm, LayerNorm, GELU twins, pooling mixer, patchify,
 batched transposes), the discriminator head, the loss block, BCE and the fused Adam.  For each call it synchronises, snapshots what the op accumulates into, runs the
 production kernel, and computes the same op in float64 from the very tensors the kernel read
@@ -321,6 +321,37 @@ class Capture:
                 r[:B] = ref.reshape(B, T, 4 * H)
                 res[f"db{layer}"] = _rel(out[2][layer], r.view(ng, 16 * T, 4 * H).sum(1))
         self.records.append(("lstm2_bwd", f"lstm2_bwd B{B} T{T} H{H}", res))
+        return out
+
+    def _lstm_fwd_fold(self, pcode, nc, w_hh, B, T, H, hbuf):
+        """The folded lstm1 forward: step t's projection is row b*nc + t/(T/nc) of pcode."""
+        torch.cuda.synchronize()
+        h, c, g = self._orig["lstm_fwd_fold"](pcode, nc, w_hh, B, T, H, hbuf)
+        torch.cuda.synchronize()
+        G = 4 * H
+        xproj = pcode.view(B, nc, 1, G).expand(B, nc, T // nc, G).reshape(B * T, G)
+        rh, rc, rg = lstm_fwd_ref(xproj, w_hh, B, T, H, 1)
+        res = {"h": _rel(h, rh), "c": _rel(c, rc), "gates": _rel(g, rg), "h_bf16": _rel(h._bf16, rh)}
+        self.records.append(("lstm_fwd_fold", f"lstm_fwd_fold B{B} T{T} H{H} nc{nc}", res))
+        return h, c, g
+
+    def _lstm_bwd_fold(self, dh, c, g, w_hh_t, B, T, H, nc, gbuf=None):
+        """The folded lstm1 backward: bf16 dG and the per-code sums S_code (fp32 + bf16 twin)."""
+        torch.cuda.synchronize()
+        dg16, sc = self._orig["lstm_bwd_fold"](dh, c, g, w_hh_t, B, T, H, nc, gbuf)
+        torch.cuda.synchronize()
+        ref = lstm_bwd_ref(dh, c, g, w_hh_t.t(), B, T, H, 1)
+        rs = ref.view(B * nc, T // nc, 4 * H).sum(1)
+        res = {"dG_bf16": _rel(dg16, ref), "s_code": _rel(sc, rs), "s_code_bf16": _rel(sc._bf16, rs)}
+        self.records.append(("lstm_bwd_fold", f"lstm_bwd_fold B{B} T{T} H{H} nc{nc}", res))
+        return dg16, sc
+
+    def _code_cat(self, codes, emb, B, nc, cd):
+        torch.cuda.synchronize()
+        out = self._orig["code_cat"](codes, emb, B, nc, cd)
+        torch.cuda.synchronize()
+        ref = torch.cat([codes.double().reshape(B * nc, cd), emb.double().repeat_interleave(nc, 0)], 1)
+        self.records.append(("code_cat", f"code_cat B{B} nc{nc}", {"out": _rel(out, ref)}))
         return out
 
     def _bn_apply(self, y, scale, shift, act, residual=None, out=None, twin16=None, out_bf16=False):
@@ -648,7 +679,8 @@ class Capture:
 
     # ---------------------------------------------------------------- context
     def __enter__(self):
-        for name in ("gemm", "lstm_fwd", "lstm2_fwd", "lstm_bwd", "lstm2_bwd", "bn_apply", "bn_bwd", "expand_codes",
+        for name in ("gemm", "lstm_fwd", "lstm2_fwd", "lstm_bwd", "lstm2_bwd", "lstm_fwd_fold", "lstm_bwd_fold", "code_cat",
+                     "bn_apply", "bn_bwd", "expand_codes",
                      "conv_edge_table", "conv_edge_colsum", "group_norm_fwd", "group_norm_bwd", "layer_norm_fwd",
                      "layer_norm_bwd", "gelu_fwd_operand", "gelu_bwd_twin", "pool3_mixer", "patchify",
                      "transpose_batched", "transpose_pad", "disc_dense_fwd", "disc_dense_bwd", "vc_loss", "vc_loss_grad", "bce_loss",

@@ -83,11 +83,11 @@ def _assert(cap, must):
 @pytest.mark.timeout(600)
 def test_c2_ops_vs_fp64():
     cap = _run("AutoVC", 16, 64, 128)
-    _assert(cap, ["gemm", "lstm_fwd", "lstm2_fwd", "lstm_bwd", "lstm2_bwd", "bn_apply", "bn_bwd", "expand_codes",
-                  "conv_edge_table", "conv_edge_colsum"] + STEP_OPS)
+    _assert(cap, ["gemm", "lstm_fwd", "lstm2_fwd", "lstm_bwd", "lstm2_bwd", "lstm_fwd_fold", "lstm_bwd_fold",
+                  "code_cat", "bn_apply", "bn_bwd", "conv_edge_table", "conv_edge_colsum"] + STEP_OPS)
     tags = " | ".join(t for _, t, _ in cap.records)
-    # the decoder lstm2 backward runs as the two-layer wavefront launch, lstm1's as the single-layer one
-    assert "lstm2_bwd B64 T128 H1024" in tags and "lstm_bwd B64 T128 H512" in tags
+    # the decoder lstm2 backward runs as the two-layer wavefront launch, lstm1's as the folded single-layer one
+    assert "lstm2_bwd B64 T128 H1024" in tags and "lstm_bwd_fold B64 T128 H512 nc8" in tags
     assert " sk" in tags and " win" in tags and " acc" in tags and " rowbias" in tags
 
 
