@@ -1241,7 +1241,11 @@ class _LinearFn(torch.autograd.Function):
         Out = w.shape[0]
         wc, _ = _linear_packs(cache, w)
         y = torch.empty(M, Out, device=x.device)
-        K.gemm(M, Out, In, operand(x, In), operand(wc, In), y, bias=b)
+        # the bf16 twin from the GEMM's epilogue: the next layer's operand (the decoder projection feeds the
+        # postnet's first conv) without a conversion pass
+        y16 = torch.empty(M, Out, device=x.device, dtype=torch.bfloat16) if K.compute() == K.BF16 else None
+        K.gemm(M, Out, In, operand(x, In), operand(wc, In), y, bias=b, c_bf16=y16)
+        K.attach_twin(y, y16)
         ctx.cache = cache
         ctx.bias = b
         ctx.save_for_backward(x, w)
