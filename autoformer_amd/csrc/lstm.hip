@@ -1859,6 +1859,7 @@ __global__ void __launch_bounds__(PNT, 1) lstm2_persist_bwd(Persist2BwdArgs a) {
       if (w == 0 && !poll_flags(flags, NR, (unsigned)k, a.ctl, a.fault, a.spin)) *quit = 1;
       __syncthreads();
       if (*quit) return;  // block-uniform exit after a spin timeout
+      if (k < T) stamp(a.trace, T, k, 1);
       const int slot = (k - 1) & 1;
       issue(0, slot);
       issue(1, slot);
