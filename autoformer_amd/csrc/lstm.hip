@@ -111,6 +111,20 @@ __device__ __forceinline__ float dot_lds(const float* __restrict__ v, const f32x
   return t[0] + t[1];
 }
 
+// dot_lds with the h slices already in registers (the forward issues its deferred LDS writes between the
+// reads and the FMAs)
+template <int HM>
+__device__ __forceinline__ float dot_regs(const f32x4 (&hv)[HM / 4], const f32x2 (&w)[HM / 2]) {
+  f32x2 a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+  for (int k = 0; k < HM / 4; ++k) {
+    a[(2 * k) & 3] = __builtin_elementwise_fma(f32x2{hv[k][0], hv[k][1]}, w[2 * k], a[(2 * k) & 3]);
+    a[(2 * k + 1) & 3] = __builtin_elementwise_fma(f32x2{hv[k][2], hv[k][3]}, w[2 * k + 1], a[(2 * k + 1) & 3]);
+  }
+  const f32x2 t = (a[0] + a[1]) + (a[2] + a[3]);
+  return t[0] + t[1];
+}
+
 // Forward.  T is padded to a multiple of SC with ghost steps that are never written out.
 template <int HM, bool FAST, bool TRACE>
 __global__ void __launch_bounds__(SNT) lstm_small_fwd(const float* __restrict__ xproj, const float* __restrict__ whh,
@@ -189,11 +203,15 @@ __global__ void __launch_bounds__(SNT) lstm_small_fwd(const float* __restrict__ 
   for (int r = 0; r < SD; ++r) ring[r] = xload(r);
   __syncthreads();
 
+  // the chunk-buffer writes of step s (gates, h, c for the flush wave) are issued during step s + 1, after
+  // that step's h reads: the barrier's LDS wait then covers the h_{s+1} write alone, and the deferred writes
+  // complete under the next step's FMAs.  The flush of chunk k - 1 moves one step later accordingly.
+  float pgv = 0.f, phv = 0.f, pcv = 0.f;
   for (int k = 0; k * SC < Tp; ++k) {
-    if (w == 4 && k > 0) flush(k - 1);
 #pragma unroll
     for (int i = 0; i < SC; ++i) {
       const int s = k * SC + i;
+      if (w == 4 && k > 0 && i == 1) flush(k - 1);
       // the ring advances in every wave (the flush wave's loads are harmless and unused): a ring
       // slot written only inside the role branch would need a copy at the branch join, and that
       // copy waits for the load just issued
@@ -201,7 +219,21 @@ __global__ void __launch_bounds__(SNT) lstm_small_fwd(const float* __restrict__ 
       ring[i % SD] = xload(s + SD);
       if (TRACE && w == 0) sstamp(tr, Tp, s, 0, 0.f);
       if (w < 4) {
-        const float pre = (act ? xv : 0.f) + dot_lds<HM>(hs[s & 1], wv);
+        f32x4 hv[HM / 4];
+        {
+          const f32x4* v4 = reinterpret_cast<const f32x4*>(hs[s & 1]);
+#pragma unroll
+          for (int kk = 0; kk < HM / 4; ++kk) hv[kk] = v4[kk];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (s > 0 && act) {  // step s - 1's chunk entries (buffer / row of that step)
+          const int pb = i > 0 ? (k & 1) : ((k - 1) & 1), pi = i > 0 ? i - 1 : SC - 1;
+          gst[pb][pi][row] = pgv;
+          if (q == 0) hst[pb][pi][j] = phv;
+          else if (q == 1) cst[pb][pi][j] = pcv;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const float pre = (act ? xv : 0.f) + dot_regs<HM>(hv, wv);
         if (TRACE && w == 0) sstamp(tr, Tp, s, 1, pre);
         float gv;
         if (FAST) {  // tanh(x) = 2 sig(2x) - 1: one exp + rcp for all four gate lanes
@@ -214,20 +246,21 @@ __global__ void __launch_bounds__(SNT) lstm_small_fwd(const float* __restrict__ 
         c = fg * c + ig * gg;
         const float h = og * act_tanh<FAST>(c);
         if (TRACE && w == 0) sstamp(tr, Tp, s, 2, h);
-        if (act) {
-          gst[k & 1][i][row] = gv;
-          if (q == 0) {
-            hs[(s + 1) & 1][j] = h;
-            hst[k & 1][i][j] = h;
-          } else if (q == 1) {
-            cst[k & 1][i][j] = c;
-          }
-        }
+        if (act && q == 0) hs[(s + 1) & 1][j] = h;
+        pgv = gv;
+        phv = h;
+        pcv = c;
       }
       if (TRACE && w < 4) sstamp(tr, Tp, s, w == 0 ? 3 : 4 + w, 0.f);
       __syncthreads();
     }
   }
+  if (w < 4 && act) {  // the last step's chunk entries
+    gst[(Tp / SC - 1) & 1][SC - 1][row] = pgv;
+    if (q == 0) hst[(Tp / SC - 1) & 1][SC - 1][j] = phv;
+    else if (q == 1) cst[(Tp / SC - 1) & 1][SC - 1][j] = pcv;
+  }
+  __syncthreads();
   if (w == 4) flush(Tp / SC - 1);
 }
 
