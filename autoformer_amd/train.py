@@ -285,6 +285,16 @@ class TrainStep:
     def _probe_fault(self):
         if self._fault_ev is not None and self._fault_ev.query():
             K.raise_on_fault(self._fault_host.item())
+        comm = getattr(self, "comm", None)
+        if comm is not None:
+            # the read-back copy and its event on the comm stream, behind the step's main-stream work: the
+            # main stream records one event instead of running the copy and a fenced event itself
+            stream_wait(comm.cuda_stream, ev_record())
+            with on_stream(comm):
+                self._fault_host.copy_(self._fault, non_blocking=True)
+                self._fault_ev = torch.cuda.Event()
+                self._fault_ev.record(comm)
+            return
         self._fault_host.copy_(self._fault, non_blocking=True)
         self._fault_ev = torch.cuda.Event()
         self._fault_ev.record()
